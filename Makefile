@@ -1,0 +1,36 @@
+# Top-level build: the product library (HIP, gfx950) and the oracle (gcc, test infrastructure).
+HIPCC ?= /opt/rocm/bin/hipcc
+ARCH ?= gfx950
+PKG := gnss_sim_receiver_amd
+CSRC := $(PKG)/csrc
+HIP_SRCS := $(wildcard $(CSRC)/*.hip)
+CPP_SRCS := $(wildcard $(CSRC)/*.cpp)
+HDRS := $(wildcard $(CSRC)/*.h) include/gnsship.h
+HIPFLAGS := --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 -Iinclude -I$(CSRC) -Wall -Wno-unused-result
+LIB := $(PKG)/libgnsship.so
+OBJDIR := build/obj
+
+OBJS := $(patsubst $(CSRC)/%.hip,$(OBJDIR)/%.o,$(HIP_SRCS)) $(patsubst $(CSRC)/%.cpp,$(OBJDIR)/%.cpp.o,$(CPP_SRCS))
+
+all: $(LIB) oracle
+
+$(OBJDIR)/%.o: $(CSRC)/%.hip $(HDRS)
+	@mkdir -p $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(OBJDIR)/%.cpp.o: $(CSRC)/%.cpp $(HDRS)
+	@mkdir -p $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) -x c++ -c $< -o $@
+
+$(LIB): $(OBJS)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS)
+
+oracle:
+	$(MAKE) -s -C oracle all
+	-@test -d /root/reference && $(MAKE) -s -C oracle ref || true
+
+clean:
+	rm -rf build $(LIB)
+	$(MAKE) -s -C oracle clean
+
+.PHONY: all oracle clean

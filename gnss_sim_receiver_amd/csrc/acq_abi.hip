@@ -1,0 +1,230 @@
+// acq_abi.hip — C-ABI of the PCPS acquisition engine (include/gnsship.h, gnsship_acq_*).
+#include <cmath>
+#include <cstring>
+#include <new>
+#include <vector>
+
+#include "acq_engine.h"
+#include "engine.h"
+
+namespace gnsship {
+int fail(gnsship_ctx* ctx, int code, const char* what);
+int hip_fail(gnsship_ctx* ctx, hipError_t e, const char* where);
+size_t fmt_bytes(int fmt);
+
+bool make_fft_plan(int n, FftPlan& plan)
+{
+    if (n < 2 || n > kMaxAcqN) return false;
+    plan.n = n;
+    plan.n_passes = 0;
+    int m = n;
+    const int radices[] = {8, 5, 4, 3, 2};
+    for (int r : radices) {
+        while (m % r == 0) {
+            if (plan.n_passes >= kMaxPasses) return false;
+            plan.radix[plan.n_passes++] = r;
+            m /= r;
+        }
+    }
+    return m == 1;
+}
+}  // namespace gnsship
+
+using namespace gnsship;
+
+#define HIP_TRY(ctx, expr)                                      \
+    do {                                                        \
+        hipError_t _e = (expr);                                 \
+        if (_e != hipSuccess) return hip_fail((ctx), _e, #expr); \
+    } while (0)
+
+struct gnsship_acq {
+    gnsship_ctx* ctx = nullptr;
+    gnsship_acq_conf conf{};
+    FftPlan plan{};
+    int n_bins = 0;
+    int dwell_count = 0;
+    float2* tw = nullptr;        // N twiddles exp(-2πi t/N)
+    float2* wipe = nullptr;      // n_bins × N Doppler wipeoffs
+    float2* codes_fft = nullptr; // max_prns × N  conj(FFT(code))
+    float2* X = nullptr;         // n_bins × N  FFT(in ⊙ w_b)
+    RowStat* rowstat = nullptr;  // max_prns × n_bins
+    gnsship_acq_result* res_dev = nullptr;
+    void* sig_dev = nullptr;     // staging for host input (N CF32)
+    float* grid_dev = nullptr;   // optional |Y|² grid (max_prns × n_bins × N)
+    size_t grid_bytes = 0;
+    std::vector<char> code_set;
+};
+
+static void acq_free_grid_buffers(gnsship_acq* a)
+{
+    if (a->wipe) (void)hipFree(a->wipe);
+    if (a->X) (void)hipFree(a->X);
+    if (a->rowstat) (void)hipFree(a->rowstat);
+    if (a->grid_dev) (void)hipFree(a->grid_dev);
+    a->wipe = nullptr;
+    a->X = nullptr;
+    a->rowstat = nullptr;
+    a->grid_dev = nullptr;
+    a->grid_bytes = 0;
+}
+
+extern "C" int gnsship_acq_destroy(gnsship_acq* a)
+{
+    if (!a) return GNSSHIP_E_INVAL;
+    (void)hipSetDevice(a->ctx->device);
+    (void)hipStreamSynchronize(a->ctx->stream);
+    acq_free_grid_buffers(a);
+    void* ptrs[] = {a->tw, a->codes_fft, a->res_dev, a->sig_dev};
+    for (void* p : ptrs)
+        if (p) (void)hipFree(p);
+    delete a;
+    return GNSSHIP_OK;
+}
+
+// update_grid_doppler_wipeoffs (pcps_acquisition.cc:295-302) with update_local_carrier (:232-245):
+// row i = volk_gnsssdr_s32f_sincos_32fc_generic(−2π·f_i/fs) — cosf/sinf of a float-accumulated
+// phase, computed here on the host with the same libm so the table is bit-identical.
+extern "C" int gnsship_acq_set_grid(gnsship_acq* a, int doppler_max, int doppler_step, int doppler_center)
+{
+    if (!a) return GNSSHIP_E_INVAL;
+    gnsship_ctx* ctx = a->ctx;
+    if (doppler_max < 0 || doppler_step <= 0) return fail(ctx, GNSSHIP_E_INVAL, "gnsship_acq_set_grid: doppler_max >= 0, doppler_step > 0");
+    const int nb = static_cast<int>(std::ceil(static_cast<double>(2 * doppler_max) / static_cast<double>(doppler_step)));  // :261
+    if (nb < 1) return fail(ctx, GNSSHIP_E_INVAL, "gnsship_acq_set_grid: empty Doppler grid");
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    const int N = a->conf.fft_size;
+    if (nb != a->n_bins || !a->wipe) {
+        acq_free_grid_buffers(a);
+        HIP_TRY(ctx, hipMalloc(&a->wipe, sizeof(float2) * static_cast<size_t>(nb) * N));
+        HIP_TRY(ctx, hipMalloc(&a->X, sizeof(float2) * static_cast<size_t>(nb) * N));
+        HIP_TRY(ctx, hipMalloc(&a->rowstat, sizeof(RowStat) * static_cast<size_t>(nb) * a->conf.max_prns));
+        a->n_bins = nb;
+    }
+    std::vector<float2> host(static_cast<size_t>(nb) * N);
+    const float two_pi = static_cast<float>(2.0 * M_PI);
+    for (int i = 0; i < nb; i++) {
+        const int32_t doppler = -doppler_max + doppler_center + doppler_step * i;
+        const float freq = static_cast<float>(doppler);  // + d_doppler_bias (0: CDMA signals)
+        const float step = -(two_pi * freq / static_cast<float>(a->conf.fs_in));
+        float ph = 0.0F;
+        float2* row = host.data() + static_cast<size_t>(i) * N;
+        for (int n = 0; n < N; n++) {
+            row[n] = make_float2(std::cos(ph), std::sin(ph));
+            ph += step;
+        }
+    }
+    HIP_TRY(ctx, hipMemcpy(a->wipe, host.data(), sizeof(float2) * host.size(), hipMemcpyHostToDevice));
+    a->conf.doppler_max = doppler_max;
+    a->conf.doppler_step = doppler_step;
+    a->conf.doppler_center = doppler_center;
+    a->dwell_count = 0;
+    return GNSSHIP_OK;
+}
+
+extern "C" int gnsship_acq_create(gnsship_ctx* ctx, const gnsship_acq_conf* conf, gnsship_acq** out)
+{
+    if (!ctx || !conf || !out) return GNSSHIP_E_INVAL;
+    *out = nullptr;
+    FftPlan plan;
+    if (!make_fft_plan(conf->fft_size, plan))
+        return fail(ctx, GNSSHIP_E_INVAL, "gnsship_acq_create: fft_size must be 2^a 3^b 5^c and <= 16384 for the LDS-resident FFT");
+    if (conf->fs_in <= 0 || conf->max_prns < 1 || conf->max_dwells < 1 || conf->samples_per_chip < 0 || conf->samples_per_code <= 0.0f)
+        return fail(ctx, GNSSHIP_E_INVAL, "gnsship_acq_create: bad configuration");
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    gnsship_acq* a = new (std::nothrow) gnsship_acq();
+    if (!a) return GNSSHIP_E_NOMEM;
+    a->ctx = ctx;
+    a->conf = *conf;
+    a->plan = plan;
+    a->code_set.assign(conf->max_prns, 0);
+    const int N = conf->fft_size;
+    std::vector<float2> tw(N);
+    for (int t = 0; t < N; t++) {
+        const double ang = -2.0 * M_PI * static_cast<double>(t) / static_cast<double>(N);
+        tw[t] = make_float2(static_cast<float>(std::cos(ang)), static_cast<float>(std::sin(ang)));
+    }
+    hipError_t e = hipMalloc(&a->tw, sizeof(float2) * N);
+    if (e == hipSuccess) e = hipMemcpy(a->tw, tw.data(), sizeof(float2) * N, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMalloc(&a->codes_fft, sizeof(float2) * static_cast<size_t>(N) * conf->max_prns);
+    if (e == hipSuccess) e = hipMalloc(&a->res_dev, sizeof(gnsship_acq_result) * conf->max_prns);
+    if (e == hipSuccess) e = hipMalloc(&a->sig_dev, sizeof(float2) * static_cast<size_t>(N));
+    if (e != hipSuccess) {
+        gnsship_acq_destroy(a);
+        return hip_fail(ctx, e, "gnsship_acq_create");
+    }
+    if (int rc = gnsship_acq_set_grid(a, conf->doppler_max, conf->doppler_step, conf->doppler_center)) {
+        gnsship_acq_destroy(a);
+        return rc;
+    }
+    *out = a;
+    return GNSSHIP_OK;
+}
+
+extern "C" int gnsship_acq_num_bins(gnsship_acq* a, int* n_bins)
+{
+    if (!a || !n_bins) return GNSSHIP_E_INVAL;
+    *n_bins = a->n_bins;
+    return GNSSHIP_OK;
+}
+
+// pcps_acquisition::set_local_code (:175-208), sampled_ms == ms_per_code, no bit-transition padding:
+// FFT of the code, then volk_32fc_conjugate_32fc.
+extern "C" int gnsship_acq_set_local_code(gnsship_acq* a, int prn_slot, const float* code)
+{
+    if (!a) return GNSSHIP_E_INVAL;
+    gnsship_ctx* ctx = a->ctx;
+    if (!code || prn_slot < 0 || prn_slot >= a->conf.max_prns) return fail(ctx, GNSSHIP_E_INVAL, "gnsship_acq_set_local_code: bad slot / code");
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    const int N = a->conf.fft_size;
+    HIP_TRY(ctx, hipMemcpyAsync(a->sig_dev, code, sizeof(float2) * N, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(ctx, launch_acq_fft_rows(a->sig_dev, GNSSHIP_FMT_CF32, nullptr, 1, a->plan, a->tw, a->codes_fft + static_cast<size_t>(prn_slot) * N,
+                     1, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    a->code_set[prn_slot] = 1;
+    return GNSSHIP_OK;
+}
+
+// acquisition_core (:600-871), step one, one dwell per call (dwells accumulate into the grid when
+// max_dwells > 1 and a grid is kept on the device; the statistic divides by the dwell count).
+extern "C" int gnsship_acq_run(gnsship_acq* a, const void* sig, int fmt, int sig_on_device, int n_prns, gnsship_acq_result* results,
+    float* grid)
+{
+    if (!a) return GNSSHIP_E_INVAL;
+    gnsship_ctx* ctx = a->ctx;
+    if (!sig || !results || n_prns < 1 || n_prns > a->conf.max_prns || fmt_bytes(fmt) == 0)
+        return fail(ctx, GNSSHIP_E_INVAL, "gnsship_acq_run: bad arguments");
+    for (int p = 0; p < n_prns; p++)
+        if (!a->code_set[p]) return fail(ctx, GNSSHIP_E_STATE, "gnsship_acq_run: set_local_code missing for a prn slot");
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    const int N = a->conf.fft_size;
+    const void* src = sig;
+    if (!sig_on_device) {
+        HIP_TRY(ctx, hipMemcpyAsync(a->sig_dev, sig, fmt_bytes(fmt) * N, hipMemcpyHostToDevice, ctx->stream));
+        src = a->sig_dev;
+    }
+    const bool keep_grid = (grid != nullptr) || a->conf.max_dwells > 1;
+    const size_t gbytes = sizeof(float) * static_cast<size_t>(a->conf.max_prns) * a->n_bins * N;
+    if (keep_grid && a->grid_bytes < gbytes) {
+        if (a->grid_dev) HIP_TRY(ctx, hipFree(a->grid_dev));
+        a->grid_dev = nullptr;
+        HIP_TRY(ctx, hipMalloc(&a->grid_dev, gbytes));
+        a->grid_bytes = gbytes;
+    }
+    // non-coherent dwells (:657-665): restart the accumulation after max_dwells
+    if (a->dwell_count >= a->conf.max_dwells) a->dwell_count = 0;
+    const int accumulate = (a->conf.max_dwells > 1 && a->dwell_count > 0) ? 1 : 0;
+    a->dwell_count++;
+    HIP_TRY(ctx, launch_acq_fft_rows(src, fmt, a->wipe, a->n_bins, a->plan, a->tw, a->X, 0, ctx->stream));
+    HIP_TRY(ctx, launch_acq_search(a->X, a->codes_fft, n_prns, a->n_bins, a->plan, a->tw, a->conf.samples_per_chip, accumulate, a->rowstat,
+                     keep_grid ? a->grid_dev : nullptr, ctx->stream));
+    HIP_TRY(ctx, launch_acq_decide(a->rowstat, n_prns, a->n_bins, N, a->conf.doppler_max, a->conf.doppler_step, a->conf.doppler_center,
+                     a->dwell_count, a->conf.use_cfar, a->conf.samples_per_code, a->res_dev, ctx->stream));
+    HIP_TRY(ctx, hipMemcpyAsync(results, a->res_dev, sizeof(gnsship_acq_result) * n_prns, hipMemcpyDeviceToHost, ctx->stream));
+    if (grid)
+        HIP_TRY(ctx, hipMemcpyAsync(grid, a->grid_dev, sizeof(float) * static_cast<size_t>(n_prns) * a->n_bins * N, hipMemcpyDeviceToHost,
+                         ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    return GNSSHIP_OK;
+}

@@ -1,0 +1,38 @@
+// acq_engine.h — internal types of the PCPS acquisition engine (not part of the C ABI).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+#include "gnsship.h"
+
+namespace gnsship {
+
+constexpr int kAcqThreads = 1024;   // one workgroup per transform: 16 wave64
+constexpr int kMaxAcqN = 16384;     // LDS-resident transform: 16384 complex64 = 128 KiB
+constexpr int kMaxPasses = 16;
+
+struct FftPlan {
+    int32_t n;
+    int32_t n_passes;
+    int32_t radix[kMaxPasses];
+};
+
+// Per (prn, bin) row statistics of the |IFFT|² grid.
+struct RowStat {
+    float max;     // first-index maximum value
+    int32_t argmax;
+    float sum;     // row sum (CFAR input power numerator)
+    float second;  // max outside the ±samples_per_chip window around argmax
+};
+
+// Factor n into radices {8,5,4,3,2} (largest first); false if n has another prime factor.
+bool make_fft_plan(int n, FftPlan& plan);
+
+hipError_t launch_acq_fft_rows(const void* sig, int fmt, const float2* mult, int n_rows, const FftPlan& plan, const float2* tw, float2* rows,
+    int conj_out, hipStream_t stream);
+hipError_t launch_acq_search(const float2* X, const float2* codes_fft, int n_prns, int n_bins, const FftPlan& plan, const float2* tw,
+    int samples_per_chip, int accumulate, RowStat* rowstat, float* grid, hipStream_t stream);
+hipError_t launch_acq_decide(const RowStat* rowstat, int n_prns, int n_bins, int N, int doppler_max, int doppler_step, int doppler_center,
+    int dwells, int use_cfar, float samples_per_code, gnsship_acq_result* out, hipStream_t stream);
+
+}  // namespace gnsship

@@ -1,0 +1,523 @@
+// gnsship_abi.hip — C-ABI implementation (include/gnsship.h): contexts, device buffers, the code
+// bank, the per-channel correlator handle and the batched correlator.  The acquisition entry
+// points live in acq_abi.hip.  No exception or exit() crosses the ABI: every entry point maps
+// failures to an int status and keeps the message in ctx->last_error.
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <new>
+
+#include "engine.h"
+
+using namespace gnsship;
+
+namespace gnsship {
+
+int fail(gnsship_ctx* ctx, int code, const char* what)
+{
+    if (ctx) ctx->last_error = what;
+    return code;
+}
+
+int hip_fail(gnsship_ctx* ctx, hipError_t e, const char* where)
+{
+    if (ctx) {
+        char buf[256];
+        std::snprintf(buf, sizeof(buf), "%s: %s", where, hipGetErrorString(e));
+        ctx->last_error = buf;
+    }
+    return (e == hipErrorOutOfMemory || e == hipErrorMemoryAllocation) ? GNSSHIP_E_NOMEM : GNSSHIP_E_DEVICE;
+}
+
+#define HIP_TRY(ctx, expr)                                      \
+    do {                                                        \
+        hipError_t _e = (expr);                                 \
+        if (_e != hipSuccess) return hip_fail((ctx), _e, #expr); \
+    } while (0)
+
+int set_device(gnsship_ctx* ctx)
+{
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    return GNSSHIP_OK;
+}
+
+// Upload the code bank table when codes changed (synchronous w.r.t. the ctx stream).
+int sync_code_table(gnsship_ctx* ctx)
+{
+    if (!ctx->codes_dirty) return GNSSHIP_OK;
+    const int n = static_cast<int>(ctx->codes_host.size());
+    if (n > ctx->codes_dev_cap) {
+        if (ctx->codes_dev) HIP_TRY(ctx, hipFree(ctx->codes_dev));
+        ctx->codes_dev = nullptr;
+        const int cap = n < 64 ? 64 : 2 * n;
+        HIP_TRY(ctx, hipMalloc(&ctx->codes_dev, sizeof(CodeDesc) * cap));
+        ctx->codes_dev_cap = cap;
+    }
+    HIP_TRY(ctx, hipMemcpyAsync(ctx->codes_dev, ctx->codes_host.data(), sizeof(CodeDesc) * n, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    ctx->codes_dirty = false;
+    return GNSSHIP_OK;
+}
+
+// Host-side derivation of the device job from one reference-style call (see engine.h DevJob).
+// The phasors are formed with the reference's float operations:
+//   phase_offset_as_complex = (cos(rem), -sin(rem))             cpu_multicorrelator_real_codes.cc:115
+//   phase_inc = std::exp(complex<float>(0, -phase_step_rad))     :123  (glibc cexpf → cosf/sinf)
+bool derive_job(const gnsship_corr_job& in, DevJob& out)
+{
+    if (in.n_samples < 0 || in.n_taps < 1 || in.n_taps > kMaxTaps || in.sample_offset < 0) return false;
+    if (in.flags & 1) return false;  // high-dynamics variants: not on the device path yet
+    const float p0r = std::cos(in.rem_carrier_phase_rad), p0i = -std::sin(in.rem_carrier_phase_rad);
+    const float incr = std::cos(-in.phase_step_rad), inci = std::sin(-in.phase_step_rad);
+    out.sample_offset = in.sample_offset;
+    out.n_samples = in.n_samples;
+    out.code_id = in.code_id;
+    out.n_taps = in.n_taps;
+    out.theta0 = std::atan2(static_cast<double>(p0i), static_cast<double>(p0r));
+    out.mag0 = static_cast<float>(std::hypot(static_cast<double>(p0r), static_cast<double>(p0i)));
+    out.dtheta = std::atan2(static_cast<double>(inci), static_cast<double>(incr));
+    out.log_mag_inc = static_cast<float>(std::log(std::hypot(static_cast<double>(incr), static_cast<double>(inci))));
+    out.rem_code = in.rem_code_phase_chips;
+    out.code_step = in.code_phase_step_chips;
+    for (int t = 0; t < kMaxTaps; t++) out.shifts[t] = (t < in.n_taps) ? in.shifts_chips[t] : 0.0f;
+    out.pad0 = 0;
+    return true;
+}
+
+// Split jobs into ≤kCorrChunk-sample chunks; returns number of chunks.
+int plan_chunks(std::vector<DevJob>& jobs, std::vector<ChunkDesc>& chunks, bool& any_multi)
+{
+    chunks.clear();
+    any_multi = false;
+    for (size_t j = 0; j < jobs.size(); j++) {
+        const int n = jobs[j].n_samples;
+        const int nc = n <= 0 ? 1 : (n + kCorrChunk - 1) / kCorrChunk;
+        jobs[j].n_chunks = nc;
+        jobs[j].first_chunk = static_cast<int32_t>(chunks.size());
+        if (nc > 1) any_multi = true;
+        for (int c = 0; c < nc; c++) {
+            ChunkDesc d;
+            d.job = static_cast<int32_t>(j);
+            d.start = c * kCorrChunk;
+            const int rem = n - d.start;
+            d.len = rem < kCorrChunk ? (rem > 0 ? rem : 0) : kCorrChunk;
+            d.pad = 0;
+            chunks.push_back(d);
+        }
+    }
+    return static_cast<int>(chunks.size());
+}
+
+size_t fmt_bytes(int fmt)
+{
+    switch (fmt) {
+    case GNSSHIP_FMT_CF32: return 8;
+    case GNSSHIP_FMT_CI16: return 4;
+    case GNSSHIP_FMT_CI8: return 2;
+    default: return 0;
+    }
+}
+
+}  // namespace gnsship
+
+// ============================================================================ context / buffers
+extern "C" int gnsship_abi_version(void) { return GNSSHIP_ABI_VERSION; }
+
+extern "C" int gnsship_device_count(int* n)
+{
+    if (!n) return GNSSHIP_E_INVAL;
+    int c = 0;
+    hipError_t e = hipGetDeviceCount(&c);
+    if (e != hipSuccess) {
+        *n = 0;
+        return GNSSHIP_E_DEVICE;
+    }
+    *n = c;
+    return GNSSHIP_OK;
+}
+
+extern "C" int gnsship_ctx_create(int device, gnsship_ctx** out)
+{
+    if (!out) return GNSSHIP_E_INVAL;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return GNSSHIP_E_DEVICE;
+    if (device < 0 || device >= n) return GNSSHIP_E_INVAL;
+    gnsship_ctx* ctx = new (std::nothrow) gnsship_ctx();
+    if (!ctx) return GNSSHIP_E_NOMEM;
+    ctx->device = device;
+    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete ctx;
+        return GNSSHIP_E_DEVICE;
+    }
+    for (auto& ev : ctx->events) {
+        if (hipEventCreate(&ev) != hipSuccess) {
+            delete ctx;
+            return GNSSHIP_E_DEVICE;
+        }
+    }
+    *out = ctx;
+    return GNSSHIP_OK;
+}
+
+extern "C" int gnsship_ctx_destroy(gnsship_ctx* ctx)
+{
+    if (!ctx) return GNSSHIP_E_INVAL;
+    (void)hipSetDevice(ctx->device);
+    (void)hipStreamSynchronize(ctx->stream);
+    for (auto& c : ctx->codes_host)
+        if (c.ptr) (void)hipFree(const_cast<float*>(c.ptr));
+    if (ctx->codes_dev) (void)hipFree(ctx->codes_dev);
+    for (auto& ev : ctx->events)
+        if (ev) (void)hipEventDestroy(ev);
+    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+    return GNSSHIP_OK;
+}
+
+extern "C" const char* gnsship_last_error(const gnsship_ctx* ctx) { return ctx ? ctx->last_error.c_str() : "null context"; }
+
+extern "C" int gnsship_ctx_sync(gnsship_ctx* ctx)
+{
+    if (!ctx) return GNSSHIP_E_INVAL;
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    return GNSSHIP_OK;
+}
+
+extern "C" int gnsship_ctx_stream(gnsship_ctx* ctx, void** stream)
+{
+    if (!ctx || !stream) return GNSSHIP_E_INVAL;
+    *stream = reinterpret_cast<void*>(ctx->stream);
+    return GNSSHIP_OK;
+}
+
+extern "C" int gnsship_ctx_event_record(gnsship_ctx* ctx, int slot)
+{
+    if (!ctx || slot < 0 || slot >= 16) return GNSSHIP_E_INVAL;
+    HIP_TRY(ctx, hipEventRecord(ctx->events[slot], ctx->stream));
+    return GNSSHIP_OK;
+}
+
+extern "C" int gnsship_ctx_event_elapsed_ms(gnsship_ctx* ctx, int a, int b, float* ms)
+{
+    if (!ctx || !ms || a < 0 || a >= 16 || b < 0 || b >= 16) return GNSSHIP_E_INVAL;
+    HIP_TRY(ctx, hipEventSynchronize(ctx->events[b]));
+    HIP_TRY(ctx, hipEventElapsedTime(ms, ctx->events[a], ctx->events[b]));
+    return GNSSHIP_OK;
+}
+
+extern "C" int gnsship_dev_alloc(gnsship_ctx* ctx, size_t bytes, void** p)
+{
+    if (!ctx || !p) return GNSSHIP_E_INVAL;
+    *p = nullptr;
+    if (int rc = set_device(ctx)) return rc;
+    HIP_TRY(ctx, hipMalloc(p, bytes ? bytes : 16));
+    return GNSSHIP_OK;
+}
+
+extern "C" int gnsship_dev_free(gnsship_ctx* ctx, void* p)
+{
+    if (!ctx) return GNSSHIP_E_INVAL;
+    if (!p) return GNSSHIP_OK;
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    HIP_TRY(ctx, hipFree(p));
+    return GNSSHIP_OK;
+}
+
+extern "C" int gnsship_dev_upload(gnsship_ctx* ctx, void* dst, const void* src, size_t bytes)
+{
+    if (!ctx || (!dst && bytes) || (!src && bytes)) return GNSSHIP_E_INVAL;
+    HIP_TRY(ctx, hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    return GNSSHIP_OK;
+}
+
+extern "C" int gnsship_dev_download(gnsship_ctx* ctx, void* dst, const void* src, size_t bytes)
+{
+    if (!ctx || (!dst && bytes) || (!src && bytes)) return GNSSHIP_E_INVAL;
+    HIP_TRY(ctx, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    return GNSSHIP_OK;
+}
+
+extern "C" int gnsship_code_set(gnsship_ctx* ctx, int code_id, const float* code, int len)
+{
+    if (!ctx || !code || code_id < 0 || code_id >= (1 << 20) || len < 1 || len > kMaxCodeLen)
+        return fail(ctx, GNSSHIP_E_INVAL, "gnsship_code_set: bad code id / length (1..16384)");
+    if (int rc = set_device(ctx)) return rc;
+    if (static_cast<int>(ctx->codes_host.size()) <= code_id) ctx->codes_host.resize(code_id + 1, CodeDesc{nullptr, 0, 0});
+    CodeDesc& d = ctx->codes_host[code_id];
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    if (d.ptr && d.len != len) {
+        HIP_TRY(ctx, hipFree(const_cast<float*>(d.ptr)));
+        d.ptr = nullptr;
+    }
+    if (!d.ptr) {
+        float* p = nullptr;
+        HIP_TRY(ctx, hipMalloc(&p, sizeof(float) * len));
+        d.ptr = p;
+    }
+    d.len = len;
+    HIP_TRY(ctx, hipMemcpy(const_cast<float*>(d.ptr), code, sizeof(float) * len, hipMemcpyHostToDevice));
+    ctx->codes_dirty = true;
+    return GNSSHIP_OK;
+}
+
+extern "C" int gnsship_code_count(gnsship_ctx* ctx, int* n)
+{
+    if (!ctx || !n) return GNSSHIP_E_INVAL;
+    *n = static_cast<int>(ctx->codes_host.size());
+    return GNSSHIP_OK;
+}
+
+// ============================================================================ batched correlator
+struct gnsship_batch {
+    gnsship_ctx* ctx = nullptr;
+    int max_jobs = 0;
+    int n_jobs = 0;
+    int n_chunks = 0;
+    int max_code_len = 1;
+    bool any_multi = false;
+    int chunk_cap = 0;
+    DevJob* jobs_dev = nullptr;
+    ChunkDesc* chunks_dev = nullptr;
+    float* partials_dev = nullptr;
+    float* out_dev = nullptr;
+    std::vector<DevJob> jobs_host;
+    std::vector<ChunkDesc> chunks_host;
+};
+
+extern "C" int gnsship_batch_create(gnsship_ctx* ctx, int max_jobs, gnsship_batch** out)
+{
+    if (!ctx || !out || max_jobs < 1) return fail(ctx, GNSSHIP_E_INVAL, "gnsship_batch_create: bad arguments");
+    *out = nullptr;
+    if (int rc = set_device(ctx)) return rc;
+    gnsship_batch* b = new (std::nothrow) gnsship_batch();
+    if (!b) return GNSSHIP_E_NOMEM;
+    b->ctx = ctx;
+    b->max_jobs = max_jobs;
+    hipError_t e = hipMalloc(&b->jobs_dev, sizeof(DevJob) * max_jobs);
+    if (e == hipSuccess) e = hipMalloc(&b->out_dev, sizeof(float) * 2 * kMaxTaps * max_jobs);
+    if (e != hipSuccess) {
+        if (b->jobs_dev) (void)hipFree(b->jobs_dev);
+        delete b;
+        return hip_fail(ctx, e, "gnsship_batch_create");
+    }
+    *out = b;
+    return GNSSHIP_OK;
+}
+
+extern "C" int gnsship_batch_set_jobs(gnsship_batch* b, const gnsship_corr_job* jobs, int n_jobs, int64_t n_buffer_samples)
+{
+    if (!b) return GNSSHIP_E_INVAL;
+    gnsship_ctx* ctx = b->ctx;
+    if ((!jobs && n_jobs) || n_jobs < 0 || n_jobs > b->max_jobs) return fail(ctx, GNSSHIP_E_INVAL, "gnsship_batch_set_jobs: n_jobs out of range");
+    if (int rc = set_device(ctx)) return rc;
+    if (int rc = sync_code_table(ctx)) return rc;
+    b->jobs_host.resize(n_jobs);
+    int max_len = 1;
+    for (int j = 0; j < n_jobs; j++) {
+        const gnsship_corr_job& in = jobs[j];
+        if (!derive_job(in, b->jobs_host[j])) return fail(ctx, GNSSHIP_E_INVAL, "gnsship_batch_set_jobs: invalid job (taps, length, offset or flags)");
+        if (in.code_id < 0 || in.code_id >= static_cast<int>(ctx->codes_host.size()) || !ctx->codes_host[in.code_id].ptr)
+            return fail(ctx, GNSSHIP_E_INVAL, "gnsship_batch_set_jobs: job refers to an unset code id");
+        if (in.sample_offset + in.n_samples > n_buffer_samples) return fail(ctx, GNSSHIP_E_INVAL, "gnsship_batch_set_jobs: job reads past the sample buffer");
+        if (ctx->codes_host[in.code_id].len > max_len) max_len = ctx->codes_host[in.code_id].len;
+    }
+    b->max_code_len = max_len;
+    b->n_chunks = plan_chunks(b->jobs_host, b->chunks_host, b->any_multi);
+    if (b->n_chunks > b->chunk_cap) {
+        if (b->chunks_dev) HIP_TRY(ctx, hipFree(b->chunks_dev));
+        if (b->partials_dev) HIP_TRY(ctx, hipFree(b->partials_dev));
+        b->chunks_dev = nullptr;
+        b->partials_dev = nullptr;
+        HIP_TRY(ctx, hipMalloc(&b->chunks_dev, sizeof(ChunkDesc) * b->n_chunks));
+        HIP_TRY(ctx, hipMalloc(&b->partials_dev, sizeof(float) * 2 * kMaxTaps * b->n_chunks));
+        b->chunk_cap = b->n_chunks;
+    }
+    b->n_jobs = n_jobs;
+    if (n_jobs) {
+        HIP_TRY(ctx, hipMemcpyAsync(b->jobs_dev, b->jobs_host.data(), sizeof(DevJob) * n_jobs, hipMemcpyHostToDevice, ctx->stream));
+        HIP_TRY(ctx, hipMemcpyAsync(b->chunks_dev, b->chunks_host.data(), sizeof(ChunkDesc) * b->n_chunks, hipMemcpyHostToDevice, ctx->stream));
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    }
+    return GNSSHIP_OK;
+}
+
+extern "C" int gnsship_batch_launch(gnsship_batch* b, const void* dev_samples, int fmt)
+{
+    if (!b) return GNSSHIP_E_INVAL;
+    gnsship_ctx* ctx = b->ctx;
+    if (fmt_bytes(fmt) == 0) return fail(ctx, GNSSHIP_E_INVAL, "gnsship_batch_launch: unknown sample format");
+    if (!dev_samples && b->n_jobs) return fail(ctx, GNSSHIP_E_INVAL, "gnsship_batch_launch: null sample buffer");
+    if (b->n_jobs == 0) return GNSSHIP_OK;
+    if (ctx->codes_dirty) return fail(ctx, GNSSHIP_E_STATE, "gnsship_batch_launch: code bank changed after set_jobs");
+    hipError_t e = launch_corr_batch(dev_samples, fmt, b->jobs_dev, b->n_jobs, b->chunks_dev, b->n_chunks, ctx->codes_dev, b->max_code_len,
+        b->any_multi, b->partials_dev, b->out_dev, ctx->stream);
+    if (e != hipSuccess) return hip_fail(ctx, e, "launch_corr_batch");
+    return GNSSHIP_OK;
+}
+
+extern "C" int gnsship_batch_results(gnsship_batch* b, float* out)
+{
+    if (!b || (!out && b->n_jobs)) return GNSSHIP_E_INVAL;
+    gnsship_ctx* ctx = b->ctx;
+    if (b->n_jobs == 0) return GNSSHIP_OK;
+    HIP_TRY(ctx, hipMemcpyAsync(out, b->out_dev, sizeof(float) * 2 * kMaxTaps * b->n_jobs, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    return GNSSHIP_OK;
+}
+
+extern "C" int gnsship_batch_results_device(gnsship_batch* b, void** dev_out)
+{
+    if (!b || !dev_out) return GNSSHIP_E_INVAL;
+    *dev_out = b->out_dev;
+    return GNSSHIP_OK;
+}
+
+extern "C" int gnsship_batch_destroy(gnsship_batch* b)
+{
+    if (!b) return GNSSHIP_E_INVAL;
+    gnsship_ctx* ctx = b->ctx;
+    (void)hipSetDevice(ctx->device);
+    (void)hipStreamSynchronize(ctx->stream);
+    if (b->jobs_dev) (void)hipFree(b->jobs_dev);
+    if (b->chunks_dev) (void)hipFree(b->chunks_dev);
+    if (b->partials_dev) (void)hipFree(b->partials_dev);
+    if (b->out_dev) (void)hipFree(b->out_dev);
+    delete b;
+    return GNSSHIP_OK;
+}
+
+// ============================================================================ per-channel correlator
+// Mirror of Cpu_Multicorrelator_Real_Codes: one handle = one channel's correlator bank.
+struct gnsship_corr {
+    gnsship_ctx* ctx = nullptr;
+    int max_samples = 0;
+    int n_taps = 0;
+    bool high_dyn = false;
+    bool code_set = false;
+    int code_len = 0;
+    float shifts[kMaxTaps] = {};
+    float* code_dev = nullptr;
+    CodeDesc* code_table_dev = nullptr;
+    void* sig_dev = nullptr;  // staging for host input (max_samples CF32)
+    DevJob* job_dev = nullptr;
+    ChunkDesc* chunks_dev = nullptr;
+    float* partials_dev = nullptr;
+    float* out_dev = nullptr;
+    int chunk_cap = 0;
+};
+
+extern "C" int gnsship_corr_create(gnsship_ctx* ctx, int max_signal_length_samples, int n_correlators, gnsship_corr** out)
+{
+    if (!ctx || !out || max_signal_length_samples < 1 || n_correlators < 1 || n_correlators > kMaxTaps)
+        return fail(ctx, GNSSHIP_E_INVAL, "gnsship_corr_create: bad arguments (1..8 correlators)");
+    *out = nullptr;
+    if (int rc = set_device(ctx)) return rc;
+    gnsship_corr* c = new (std::nothrow) gnsship_corr();
+    if (!c) return GNSSHIP_E_NOMEM;
+    c->ctx = ctx;
+    c->max_samples = max_signal_length_samples;
+    c->n_taps = n_correlators;
+    c->chunk_cap = (max_signal_length_samples + kCorrChunk - 1) / kCorrChunk;
+    hipError_t e = hipMalloc(&c->code_table_dev, sizeof(CodeDesc));
+    if (e == hipSuccess) e = hipMalloc(&c->sig_dev, 8 * static_cast<size_t>(max_signal_length_samples));
+    if (e == hipSuccess) e = hipMalloc(&c->job_dev, sizeof(DevJob));
+    if (e == hipSuccess) e = hipMalloc(&c->chunks_dev, sizeof(ChunkDesc) * c->chunk_cap);
+    if (e == hipSuccess) e = hipMalloc(&c->partials_dev, sizeof(float) * 2 * kMaxTaps * c->chunk_cap);
+    if (e == hipSuccess) e = hipMalloc(&c->out_dev, sizeof(float) * 2 * kMaxTaps);
+    if (e != hipSuccess) {
+        gnsship_corr_destroy(c);
+        return hip_fail(ctx, e, "gnsship_corr_create");
+    }
+    *out = c;
+    return GNSSHIP_OK;
+}
+
+extern "C" int gnsship_corr_set_local_code_and_taps(gnsship_corr* c, int code_length_chips, const float* code, const float* shifts)
+{
+    if (!c) return GNSSHIP_E_INVAL;
+    gnsship_ctx* ctx = c->ctx;
+    if (!code || !shifts || code_length_chips < 1 || code_length_chips > kMaxCodeLen)
+        return fail(ctx, GNSSHIP_E_INVAL, "gnsship_corr_set_local_code_and_taps: bad code / shifts");
+    if (int rc = set_device(ctx)) return rc;
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    if (c->code_dev && c->code_len != code_length_chips) {
+        HIP_TRY(ctx, hipFree(c->code_dev));
+        c->code_dev = nullptr;
+    }
+    if (!c->code_dev) HIP_TRY(ctx, hipMalloc(&c->code_dev, sizeof(float) * code_length_chips));
+    c->code_len = code_length_chips;
+    HIP_TRY(ctx, hipMemcpy(c->code_dev, code, sizeof(float) * code_length_chips, hipMemcpyHostToDevice));
+    CodeDesc d{c->code_dev, code_length_chips, 0};
+    HIP_TRY(ctx, hipMemcpy(c->code_table_dev, &d, sizeof(d), hipMemcpyHostToDevice));
+    for (int t = 0; t < c->n_taps; t++) c->shifts[t] = shifts[t];
+    c->code_set = true;
+    return GNSSHIP_OK;
+}
+
+extern "C" int gnsship_corr_set_high_dynamics_resampler(gnsship_corr* c, int enable)
+{
+    if (!c) return GNSSHIP_E_INVAL;
+    c->high_dyn = enable != 0;
+    return GNSSHIP_OK;
+}
+
+extern "C" int gnsship_corr_run(gnsship_corr* c, const void* sig, int fmt, int sig_on_device, float rem_carr, float phase_step,
+    float phase_rate_step, float rem_code, float code_step, float code_rate_step, int n, float* corr_out)
+{
+    if (!c) return GNSSHIP_E_INVAL;
+    gnsship_ctx* ctx = c->ctx;
+    if (!c->code_set) return fail(ctx, GNSSHIP_E_STATE, "gnsship_corr_run: set_local_code_and_taps not called");
+    if (!sig || !corr_out || n < 0 || n > c->max_samples || fmt_bytes(fmt) == 0)
+        return fail(ctx, GNSSHIP_E_INVAL, "gnsship_corr_run: bad arguments (length > max_signal_length_samples?)");
+    if (c->high_dyn && (phase_rate_step != 0.0f || code_rate_step != 0.0f))
+        return fail(ctx, GNSSHIP_E_INVAL, "gnsship_corr_run: high-dynamics resampler with nonzero rates is not supported on the device path");
+    if (int rc = set_device(ctx)) return rc;
+    gnsship_corr_job in{};
+    in.sample_offset = 0;
+    in.n_samples = n;
+    in.code_id = 0;
+    in.n_taps = c->n_taps;
+    in.flags = 0;
+    in.rem_carrier_phase_rad = rem_carr;
+    in.phase_step_rad = phase_step;
+    in.phase_rate_step_rad = phase_rate_step;
+    in.rem_code_phase_chips = rem_code;
+    in.code_phase_step_chips = code_step;
+    in.code_phase_rate_step_chips = code_rate_step;
+    for (int t = 0; t < kMaxTaps; t++) in.shifts_chips[t] = t < c->n_taps ? c->shifts[t] : 0.0f;
+    std::vector<DevJob> jobs(1);
+    if (!derive_job(in, jobs[0])) return fail(ctx, GNSSHIP_E_INVAL, "gnsship_corr_run: invalid job");
+    std::vector<ChunkDesc> chunks;
+    bool multi = false;
+    const int nch = plan_chunks(jobs, chunks, multi);
+    const void* src = sig;
+    if (!sig_on_device) {
+        HIP_TRY(ctx, hipMemcpyAsync(c->sig_dev, sig, fmt_bytes(fmt) * static_cast<size_t>(n), hipMemcpyHostToDevice, ctx->stream));
+        src = c->sig_dev;
+    }
+    HIP_TRY(ctx, hipMemcpyAsync(c->job_dev, jobs.data(), sizeof(DevJob), hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(ctx, hipMemcpyAsync(c->chunks_dev, chunks.data(), sizeof(ChunkDesc) * nch, hipMemcpyHostToDevice, ctx->stream));
+    hipError_t e = launch_corr_batch(src, fmt, c->job_dev, 1, c->chunks_dev, nch, c->code_table_dev, c->code_len, multi, c->partials_dev,
+        c->out_dev, ctx->stream);
+    if (e != hipSuccess) return hip_fail(ctx, e, "launch_corr_batch");
+    float tmp[2 * kMaxTaps];
+    HIP_TRY(ctx, hipMemcpyAsync(tmp, c->out_dev, sizeof(tmp), hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    std::memcpy(corr_out, tmp, sizeof(float) * 2 * c->n_taps);
+    return GNSSHIP_OK;
+}
+
+extern "C" int gnsship_corr_destroy(gnsship_corr* c)
+{
+    if (!c) return GNSSHIP_E_INVAL;
+    (void)hipSetDevice(c->ctx->device);
+    (void)hipStreamSynchronize(c->ctx->stream);
+    void* ptrs[] = {c->code_dev, c->code_table_dev, c->sig_dev, c->job_dev, c->chunks_dev, c->partials_dev, c->out_dev};
+    for (void* p : ptrs)
+        if (p) (void)hipFree(p);
+    delete c;
+    return GNSSHIP_OK;
+}

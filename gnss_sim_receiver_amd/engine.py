@@ -1,0 +1,312 @@
+"""Thin Python handles over the C ABI, used by the tests, the bench and the smoke entry point.
+
+The classes mirror the reference's engine objects one-to-one:
+
+* :class:`MultiCorrelatorRealCodes` — ``Cpu_Multicorrelator_Real_Codes``
+  (src/algorithms/tracking/libs/cpu_multicorrelator_real_codes.h:37-61): ``init``,
+  ``set_local_code_and_taps``, ``set_input_output_vectors``,
+  ``Carrier_wipeoff_multicorrelator_resampler``, ``free`` with the same argument meaning.
+* :class:`CorrelatorBatch` — many (channel, epoch) correlations in one device launch.
+* :class:`PcpsAcquisition` — ``pcps_acquisition::set_local_code`` / ``init`` / ``acquisition_core``.
+
+All compute runs in ``libgnsship.so`` (HIP, gfx950).  These wrappers only move arguments.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import abi
+from .abi import FMT_CF32, FMT_CI8, FMT_CI16, JOB_DTYPE, MAX_TAPS, check, fptr
+
+_FMT_OF_DTYPE = {np.dtype(np.complex64): FMT_CF32, np.dtype(np.int16): FMT_CI16, np.dtype(np.int8): FMT_CI8}
+_FMT_BYTES = {FMT_CF32: 8, FMT_CI16: 4, FMT_CI8: 2}
+
+
+def sample_format(x: np.ndarray) -> int:
+    """complex64 → CF32 (gr_complex); int16 [..., 2] interleaved → CI16; int8 interleaved → CI8."""
+    try:
+        return _FMT_OF_DTYPE[x.dtype]
+    except KeyError as e:
+        raise TypeError(f"unsupported IF sample dtype {x.dtype}") from e
+
+
+def device_count() -> int:
+    n = ctypes.c_int(0)
+    rc = abi.load().gnsship_device_count(ctypes.byref(n))
+    return n.value if rc == abi.OK else 0
+
+
+class Context:
+    """One HIP device, one stream, one code bank."""
+
+    def __init__(self, device: int = 0):
+        self.lib = abi.load()
+        h = ctypes.c_void_p()
+        check(self.lib.gnsship_ctx_create(device, ctypes.byref(h)), f"gnsship_ctx_create(device={device})")
+        self.h = h
+        self.device = device
+
+    def close(self):
+        if self.h:
+            self.lib.gnsship_ctx_destroy(self.h)
+            self.h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def sync(self):
+        check(self.lib.gnsship_ctx_sync(self.h), "gnsship_ctx_sync", self.h)
+
+    def stream(self) -> int:
+        s = ctypes.c_void_p()
+        check(self.lib.gnsship_ctx_stream(self.h, ctypes.byref(s)), "gnsship_ctx_stream", self.h)
+        return s.value or 0
+
+    def event_record(self, slot: int):
+        check(self.lib.gnsship_ctx_event_record(self.h, slot), "gnsship_ctx_event_record", self.h)
+
+    def event_elapsed_ms(self, a: int, b: int) -> float:
+        ms = ctypes.c_float()
+        check(self.lib.gnsship_ctx_event_elapsed_ms(self.h, a, b, ctypes.byref(ms)), "gnsship_ctx_event_elapsed_ms", self.h)
+        return ms.value
+
+    def set_code(self, code_id: int, code: np.ndarray):
+        code = np.ascontiguousarray(code, np.float32)
+        check(self.lib.gnsship_code_set(self.h, code_id, fptr(code), len(code)), "gnsship_code_set", self.h)
+
+    def upload(self, host: np.ndarray) -> "DeviceBuffer":
+        buf = DeviceBuffer(self, host.nbytes)
+        buf.upload(host)
+        return buf
+
+
+class DeviceBuffer:
+    """An HBM allocation owned by a context (the IF sample buffer lives in one)."""
+
+    def __init__(self, ctx: Context, nbytes: int):
+        self.ctx = ctx
+        p = ctypes.c_void_p()
+        check(ctx.lib.gnsship_dev_alloc(ctx.h, nbytes, ctypes.byref(p)), f"gnsship_dev_alloc({nbytes})", ctx.h)
+        self.ptr = p.value
+        self.nbytes = nbytes
+
+    def upload(self, host: np.ndarray, offset: int = 0):
+        host = np.ascontiguousarray(host)
+        assert offset + host.nbytes <= self.nbytes
+        check(self.ctx.lib.gnsship_dev_upload(self.ctx.h, self.ptr + offset, host.ctypes.data, host.nbytes), "gnsship_dev_upload",
+              self.ctx.h)
+
+    def download(self, out: np.ndarray, offset: int = 0):
+        assert offset + out.nbytes <= self.nbytes and out.flags.c_contiguous
+        check(self.ctx.lib.gnsship_dev_download(self.ctx.h, out.ctypes.data, self.ptr + offset, out.nbytes), "gnsship_dev_download",
+              self.ctx.h)
+        return out
+
+    def free(self):
+        if self.ptr:
+            self.ctx.lib.gnsship_dev_free(self.ctx.h, self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            if self.ptr and self.ctx.h:
+                self.free()
+        except Exception:
+            pass
+
+
+class MultiCorrelatorRealCodes:
+    """Mirror of Cpu_Multicorrelator_Real_Codes (cpu_multicorrelator_real_codes.h:37-61)."""
+
+    def __init__(self, ctx: Context):
+        self.ctx = ctx
+        self.h = None
+        self.n_correlators = 0
+        self._out = None
+        self._sig = None
+
+    def init(self, max_signal_length_samples: int, n_correlators: int) -> bool:
+        h = ctypes.c_void_p()
+        check(self.ctx.lib.gnsship_corr_create(self.ctx.h, max_signal_length_samples, n_correlators, ctypes.byref(h)),
+              "gnsship_corr_create", self.ctx.h)
+        self.h = h
+        self.n_correlators = n_correlators
+        return True
+
+    def set_high_dynamics_resampler(self, use: bool):
+        check(self.ctx.lib.gnsship_corr_set_high_dynamics_resampler(self.h, int(use)), "set_high_dynamics_resampler", self.ctx.h)
+
+    def set_local_code_and_taps(self, code_length_chips: int, local_code_in: np.ndarray, shifts_chips: np.ndarray) -> bool:
+        code = np.ascontiguousarray(local_code_in[:code_length_chips], np.float32)
+        shifts = np.ascontiguousarray(shifts_chips, np.float32)
+        if len(shifts) < self.n_correlators:
+            raise ValueError("need one shift per correlator")
+        check(self.ctx.lib.gnsship_corr_set_local_code_and_taps(self.h, code_length_chips, fptr(code), fptr(shifts)),
+              "gnsship_corr_set_local_code_and_taps", self.ctx.h)
+        return True
+
+    def set_input_output_vectors(self, corr_out: np.ndarray, sig_in: np.ndarray) -> bool:
+        self._out = corr_out
+        self._sig = sig_in
+        return True
+
+    def Carrier_wipeoff_multicorrelator_resampler(self, rem_carrier_phase_in_rad, phase_step_rad, phase_rate_step_rad,
+                                                  rem_code_phase_chips, code_phase_step_chips, code_phase_rate_step_chips,
+                                                  signal_length_samples) -> bool:
+        sig = np.ascontiguousarray(self._sig)
+        fmt = sample_format(sig)
+        tmp = np.zeros(2 * self.n_correlators, np.float32)
+        check(self.ctx.lib.gnsship_corr_run(self.h, sig.ctypes.data, fmt, 0, rem_carrier_phase_in_rad, phase_step_rad,
+                                            phase_rate_step_rad, rem_code_phase_chips, code_phase_step_chips,
+                                            code_phase_rate_step_chips, signal_length_samples, fptr(tmp)),
+              "gnsship_corr_run", self.ctx.h)
+        self._out[: self.n_correlators] = tmp.view(np.complex64)
+        return True
+
+    def free(self) -> bool:
+        if self.h:
+            self.ctx.lib.gnsship_corr_destroy(self.h)
+            self.h = None
+        return True
+
+    def __del__(self):
+        try:
+            if self.h and self.ctx.h:
+                self.free()
+        except Exception:
+            pass
+
+
+class CorrelatorBatch:
+    """Batched multicorrelator: every row of a JOB_DTYPE array is one channel-epoch."""
+
+    def __init__(self, ctx: Context, max_jobs: int):
+        self.ctx = ctx
+        h = ctypes.c_void_p()
+        check(ctx.lib.gnsship_batch_create(ctx.h, max_jobs, ctypes.byref(h)), "gnsship_batch_create", ctx.h)
+        self.h = h
+        self.n_jobs = 0
+
+    def set_jobs(self, jobs: np.ndarray, n_buffer_samples: int):
+        jobs = np.ascontiguousarray(jobs, JOB_DTYPE)
+        check(self.ctx.lib.gnsship_batch_set_jobs(self.h, jobs.ctypes.data, len(jobs), n_buffer_samples), "gnsship_batch_set_jobs",
+              self.ctx.h)
+        self.n_jobs = len(jobs)
+
+    def launch(self, samples: DeviceBuffer, fmt: int = FMT_CF32):
+        check(self.ctx.lib.gnsship_batch_launch(self.h, samples.ptr, fmt), "gnsship_batch_launch", self.ctx.h)
+
+    def launch_ptr(self, dev_ptr: int, fmt: int = FMT_CF32):
+        check(self.ctx.lib.gnsship_batch_launch(self.h, dev_ptr, fmt), "gnsship_batch_launch", self.ctx.h)
+
+    def results(self) -> np.ndarray:
+        out = np.zeros((self.n_jobs, 2 * MAX_TAPS), np.float32)
+        check(self.ctx.lib.gnsship_batch_results(self.h, fptr(out)), "gnsship_batch_results", self.ctx.h)
+        return out.view(np.complex64)
+
+    def close(self):
+        if self.h:
+            self.ctx.lib.gnsship_batch_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            if self.h and self.ctx.h:
+                self.close()
+        except Exception:
+            pass
+
+
+def correlate_host(ctx: Context, samples: np.ndarray, jobs: np.ndarray, codes: list) -> np.ndarray:
+    """Upload samples + codes, run one batch, return complex64[n_jobs, MAX_TAPS]."""
+    fmt = sample_format(samples)
+    for i, c in enumerate(codes):
+        ctx.set_code(i, c)
+    buf = ctx.upload(samples)
+    n_samples = samples.nbytes // _FMT_BYTES[fmt]
+    b = CorrelatorBatch(ctx, max(1, len(jobs)))
+    try:
+        b.set_jobs(jobs, n_samples)
+        b.launch(buf, fmt)
+        return b.results()
+    finally:
+        b.close()
+        buf.free()
+
+
+class PcpsAcquisition:
+    """pcps_acquisition (pcps_acquisition.cc) over up to ``max_prns`` local codes at once."""
+
+    def __init__(self, ctx: Context, fs_in: int, fft_size: int, doppler_max: int, doppler_step: int, doppler_center: int = 0,
+                 use_cfar: bool = True, samples_per_chip: int = None, samples_per_code: float = None, max_prns: int = 1,
+                 max_dwells: int = 1, chip_rate: float = 1023000.0, ms_per_code: int = 1):
+        self.ctx = ctx
+        conf = abi.AcqConf()
+        conf.fs_in = fs_in
+        conf.fft_size = fft_size
+        conf.doppler_max = doppler_max
+        conf.doppler_step = doppler_step
+        conf.doppler_center = doppler_center
+        conf.max_dwells = max_dwells
+        conf.use_cfar = int(use_cfar)
+        # Acq_Conf::SetDerivedParams (acq_conf.cc:113-118), float arithmetic as in the reference
+        spms = np.float32(np.float32(fs_in) * np.float32(0.001))
+        conf.samples_per_chip = int(np.ceil(np.float32(fs_in) / np.float32(chip_rate))) if samples_per_chip is None else samples_per_chip
+        conf.samples_per_code = float(np.float32(spms * np.float32(ms_per_code))) if samples_per_code is None else samples_per_code
+        conf.max_prns = max_prns
+        self.conf = conf
+        h = ctypes.c_void_p()
+        check(ctx.lib.gnsship_acq_create(ctx.h, ctypes.byref(conf), ctypes.byref(h)), "gnsship_acq_create", ctx.h)
+        self.h = h
+        nb = ctypes.c_int()
+        check(ctx.lib.gnsship_acq_num_bins(self.h, ctypes.byref(nb)), "gnsship_acq_num_bins", ctx.h)
+        self.n_bins = nb.value
+
+    def set_grid(self, doppler_max: int, doppler_step: int, doppler_center: int = 0):
+        check(self.ctx.lib.gnsship_acq_set_grid(self.h, doppler_max, doppler_step, doppler_center), "gnsship_acq_set_grid", self.ctx.h)
+        nb = ctypes.c_int()
+        check(self.ctx.lib.gnsship_acq_num_bins(self.h, ctypes.byref(nb)), "gnsship_acq_num_bins", self.ctx.h)
+        self.n_bins = nb.value
+
+    def set_local_code(self, code: np.ndarray, prn_slot: int = 0):
+        code = np.ascontiguousarray(code, np.complex64)
+        if len(code) != self.conf.fft_size:
+            raise ValueError("local code must have fft_size samples")
+        check(self.ctx.lib.gnsship_acq_set_local_code(self.h, prn_slot, fptr(code.view(np.float32))), "gnsship_acq_set_local_code",
+              self.ctx.h)
+
+    def run(self, sig, n_prns: int = 1, want_grid: bool = False, fmt: int = None):
+        """sig: host ndarray (CF32/CI16/CI8) or DeviceBuffer (then pass fmt)."""
+        res = (abi.AcqResult * n_prns)()
+        grid = np.zeros((n_prns, self.n_bins, self.conf.fft_size), np.float32) if want_grid else None
+        if isinstance(sig, DeviceBuffer):
+            ptr, on_dev, f = sig.ptr, 1, FMT_CF32 if fmt is None else fmt
+        else:
+            sig = np.ascontiguousarray(sig)
+            ptr, on_dev, f = sig.ctypes.data, 0, sample_format(sig)
+        check(self.ctx.lib.gnsship_acq_run(self.h, ptr, f, on_dev, n_prns, res, fptr(grid) if want_grid else None),
+              "gnsship_acq_run", self.ctx.h)
+        return list(res), grid
+
+    def close(self):
+        if self.h:
+            self.ctx.lib.gnsship_acq_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            if self.h and self.ctx.h:
+                self.close()
+        except Exception:
+            pass

@@ -1,0 +1,142 @@
+"""Synthetic GNSS IF generator and truth-aligned correlator job builder.
+
+    x[n] = Σ_k A_k · c_k(n) · d_k(n) · exp(j(2π(f_IF,k + fD_k)·n/fs + φ_k)) + w[n]
+
+* w: complex Gaussian, σ = 1 per component (as signal_generator_c.cc:540-546);
+* A_k = sqrt(2·10^(CN0_k/10) / fs), so that C/N0 = A² / (2σ²/fs);
+* c_k: the PRN code clocked at chip_rate·(1 + fD/f_carrier) (code Doppler), delayed by τ_k chips;
+* d_k: ±1 data bits (GPS 50 bps = 20 code periods per bit), off by default.
+
+Formats: gr_complex = complex64; ibyte = round(8·x) clipped to ±127, int8 interleaved I,Q.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import codes as C
+from .abi import JOB_DTYPE, MAX_TAPS
+
+SYSTEMS = {
+    # name: (chip_rate, code_len, carrier_hz, code generator)
+    "GPS": (C.GPS_L1_CA_CODE_RATE_CPS, C.GPS_L1_CA_CODE_LENGTH_CHIPS, C.GPS_L1_FREQ_HZ, C.gps_l1_ca_code_gen_float),
+    "BDS": (C.BEIDOU_B1I_CODE_RATE_CPS, C.BEIDOU_B1I_CODE_LENGTH_CHIPS, C.BEIDOU_B1I_FREQ_HZ, C.beidou_b1i_code_gen_float),
+}
+
+
+@dataclass
+class Satellite:
+    prn: int
+    doppler_hz: float
+    code_delay_chips: float
+    carrier_phase_rad: float = 0.0
+    cn0_dbhz: float = 45.0
+    system: str = "GPS"
+    data_bits: bool = False
+    bit_seed: int = 0
+    f_if_hz: float = 0.0
+    code: np.ndarray = field(default=None, repr=False)
+
+    def __post_init__(self):
+        if self.code is None:
+            self.code = SYSTEMS[self.system][3](self.prn)
+
+    @property
+    def chip_rate(self):
+        return SYSTEMS[self.system][0]
+
+    @property
+    def code_len(self):
+        return SYSTEMS[self.system][1]
+
+    def code_freq(self):
+        rate, _, fc, _ = SYSTEMS[self.system]
+        return rate * (1.0 + self.doppler_hz / fc)
+
+    def chip_phase(self, n: np.ndarray, fs: float) -> np.ndarray:
+        """Received code phase [chips] at sample n (unwrapped)."""
+        return n / fs * self.code_freq() - self.code_delay_chips
+
+    def carrier_phase(self, n: np.ndarray, fs: float) -> np.ndarray:
+        return 2.0 * np.pi * (self.f_if_hz + self.doppler_hz) * (n / fs) + self.carrier_phase_rad
+
+
+def generate_if(fs: float, n_samples: int, sats: list, seed: int = 0, noise: bool = True, start: int = 0,
+                block: int = 1 << 20) -> np.ndarray:
+    """complex64[n_samples] of synthetic IF starting at absolute sample `start`."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    out = np.empty(n_samples, np.complex64)
+    for b0 in range(0, n_samples, block):
+        b1 = min(n_samples, b0 + block)
+        n = np.arange(start + b0, start + b1, dtype=np.float64)
+        acc = np.zeros(b1 - b0, np.complex128)
+        for s in sats:
+            amp = np.sqrt(2.0 * 10.0 ** (s.cn0_dbhz / 10.0) / fs)
+            ph = s.chip_phase(n, fs)
+            chip = np.floor(ph).astype(np.int64)
+            c = s.code[np.mod(chip, s.code_len)].astype(np.float64)
+            if s.data_bits:
+                periods = np.floor_divide(chip, s.code_len)
+                bit_idx = np.floor_divide(periods, 20)
+                bits = np.where((np.bitwise_xor(bit_idx * 2654435761 + s.bit_seed, 0x5BD1E995) >> 7) & 1, -1.0, 1.0)
+                c = c * bits
+            acc += amp * c * np.exp(1j * s.carrier_phase(n, fs))
+        if noise:
+            acc += rng.standard_normal(b1 - b0) + 1j * rng.standard_normal(b1 - b0)
+        out[b0:b1] = acc.astype(np.complex64)
+    return out
+
+
+def to_ibyte(x: np.ndarray, scale: float = 8.0) -> np.ndarray:
+    """int8 interleaved I,Q: round(scale·x) clipped to ±127 (the C5 ibyte format)."""
+    iq = np.empty(2 * len(x), np.float32)
+    iq[0::2] = x.real
+    iq[1::2] = x.imag
+    return np.clip(np.rint(scale * iq), -127, 127).astype(np.int8)
+
+
+def to_ishort(x: np.ndarray, scale: float = 256.0) -> np.ndarray:
+    iq = np.empty(2 * len(x), np.float32)
+    iq[0::2] = x.real
+    iq[1::2] = x.imag
+    return np.clip(np.rint(scale * iq), -32767, 32767).astype(np.int16)
+
+
+def truth_jobs(sat: Satellite, fs: float, n_epochs: int, vector_length: int, shifts_chips, code_id: int,
+               samples_per_chip: int = 1, first_epoch: int = 1) -> np.ndarray:
+    """One correlator job per code period, NCO set from the synthetic truth (as a locked DLL/PLL
+    would): epoch e starts at the first sample at or after the start of code period e, with
+    rem_code = −(fractional chip at that sample) and rem_carr = carrier phase at that sample.
+    Argument meaning/units follow dll_pll_veml_tracking::do_correlation_step (:1037-1048)."""
+    jobs = np.zeros(n_epochs, JOB_DTYPE)
+    L = sat.code_len
+    fcode = sat.code_freq()
+    for i in range(n_epochs):
+        e = first_epoch + i
+        # sample where the received code phase crosses e*L chips
+        t_start = (e * L + sat.code_delay_chips) / fcode
+        s = int(np.ceil(t_start * fs))
+        chip = sat.chip_phase(np.float64(s), fs) - e * L
+        carr = np.mod(sat.carrier_phase(np.float64(s), fs), 2 * np.pi)
+        jobs[i]["sample_offset"] = s
+        jobs[i]["n_samples"] = vector_length
+        jobs[i]["code_id"] = code_id
+        jobs[i]["n_taps"] = len(shifts_chips)
+        jobs[i]["rem_carrier_phase_rad"] = np.float32(carr)
+        jobs[i]["phase_step_rad"] = np.float32(2 * np.pi * (sat.f_if_hz + sat.doppler_hz) / fs)
+        jobs[i]["rem_code_phase_chips"] = np.float32(-chip * samples_per_chip)
+        jobs[i]["code_phase_step_chips"] = np.float32(fcode / fs * samples_per_chip)
+        sh = np.zeros(MAX_TAPS, np.float32)
+        sh[: len(shifts_chips)] = np.asarray(shifts_chips, np.float32) * samples_per_chip
+        jobs[i]["shifts_chips"] = sh
+    return jobs
+
+
+def random_sky(n_sats: int, seed: int, system: str = "GPS", cn0: float = 45.0, prns=None, dmax: float = 5000.0):
+    """Satellites with fD ~ U[±dmax], τ ~ U[0, L), φ ~ U[0, 2π)."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    L = SYSTEMS[system][1]
+    prns = list(range(1, n_sats + 1)) if prns is None else list(prns)
+    return [Satellite(prn=p, doppler_hz=float(rng.uniform(-dmax, dmax)), code_delay_chips=float(rng.uniform(0, L)),
+                      carrier_phase_rad=float(rng.uniform(0, 2 * np.pi)), cn0_dbhz=cn0, system=system) for p in prns]

@@ -1,0 +1,192 @@
+/*
+ * gnsship.h — C ABI of the MI355X-native GNSS acquisition + tracking correlator engine.
+ *
+ * This is the drop-in boundary.  Everything behind it is HIP code for gfx950;
+ * everything in front of it is plain C: opaque handles, plain pointers and sizes, int status
+ * codes.  No exceptions, no exit(), no torch / STL types cross this boundary.
+ *
+ * What each group of entry points replaces in the reference (ShingoNishimoto/gnss_sim_receiver,
+ * a GNSS-SDR v0.0.19 fork; paths relative to its root):
+ *
+ *  gnsship_corr_*       Cpu_Multicorrelator_Real_Codes
+ *                         (src/algorithms/tracking/libs/cpu_multicorrelator_real_codes.h:37-61,
+ *                          .cc:36-167), i.e. volk_gnsssdr_32f_xn_resampler_32f_xn +
+ *                          volk_gnsssdr_32fc_32f_rotator_dot_prod_32fc_xn, as called from
+ *                          dll_pll_veml_tracking::do_correlation_step (dll_pll_veml_tracking.cc:1037-1062).
+ *  gnsship_batch_*      The same correlation for many (channel, epoch) jobs in one launch: what
+ *                         GNU Radio's thread-per-channel scheduling does across all channels.
+ *  gnsship_acq_*        pcps_acquisition::set_local_code (pcps_acquisition.cc:175-208),
+ *                         update_grid_doppler_wipeoffs (:295-302), acquisition_core (:600-871),
+ *                         max_to_input_power_statistic / first_vs_second_peak_statistic (:496-597).
+ *
+ * Threading: handles are not re-entrant; distinct handles may be used from distinct threads
+ * (each context owns one HIP stream).  All *_run calls are synchronous unless named *_launch.
+ */
+#ifndef GNSSHIP_H
+#define GNSSHIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GNSSHIP_ABI_VERSION 1
+
+/* ---- status codes (reference: bool-always-true + LOG/throw; here explicit) ---- */
+#define GNSSHIP_OK 0
+#define GNSSHIP_E_INVAL (-1)   /* bad argument / shape */
+#define GNSSHIP_E_NOMEM (-2)   /* device or host allocation failed */
+#define GNSSHIP_E_DEVICE (-3)  /* HIP runtime error (message in gnsship_last_error) */
+#define GNSSHIP_E_STATE (-4)   /* call order violated (e.g. run before set_local_code) */
+
+/* ---- IF sample formats (reference item types: gr_complex, cshort, ibyte/cbyte) ---- */
+#define GNSSHIP_FMT_CF32 0 /* interleaved float32 I,Q  (gr_complex)            */
+#define GNSSHIP_FMT_CI16 1 /* interleaved int16  I,Q  (lv_16sc_t / cshort)      */
+#define GNSSHIP_FMT_CI8 2  /* interleaved int8   I,Q  (ibyte/cbyte), no scaling  */
+
+#define GNSSHIP_MAX_TAPS 8
+
+typedef struct gnsship_ctx gnsship_ctx;
+typedef struct gnsship_corr gnsship_corr;
+typedef struct gnsship_batch gnsship_batch;
+typedef struct gnsship_acq gnsship_acq;
+
+/* ------------------------------------------------------------------------------------------ */
+/* Context: one HIP device + one stream + a code bank.                                        */
+/* ------------------------------------------------------------------------------------------ */
+int gnsship_abi_version(void);
+int gnsship_device_count(int* n_devices);
+int gnsship_ctx_create(int device, gnsship_ctx** out);
+int gnsship_ctx_destroy(gnsship_ctx* ctx);
+const char* gnsship_last_error(const gnsship_ctx* ctx);
+int gnsship_ctx_sync(gnsship_ctx* ctx);
+/* hipStream_t of the context, as void*, so a caller can order its own work against ours. */
+int gnsship_ctx_stream(gnsship_ctx* ctx, void** stream);
+/* HIP events recorded on the context stream (slots 0..15), for in-stream kernel timing. */
+int gnsship_ctx_event_record(gnsship_ctx* ctx, int slot);
+int gnsship_ctx_event_elapsed_ms(gnsship_ctx* ctx, int slot_begin, int slot_end, float* ms);
+
+/* Device buffers (HBM).  The IF sample stream lives in one of these. */
+int gnsship_dev_alloc(gnsship_ctx* ctx, size_t bytes, void** dev_ptr);
+int gnsship_dev_free(gnsship_ctx* ctx, void* dev_ptr);
+int gnsship_dev_upload(gnsship_ctx* ctx, void* dev_dst, const void* host_src, size_t bytes);
+int gnsship_dev_download(gnsship_ctx* ctx, void* host_dst, const void* dev_src, size_t bytes);
+
+/* Code bank: local code replicas (float, one value per code sample, e.g. 1023 for GPS C/A,
+ * 8184 for Galileo E1 sinBOC(1,1) at 2 samples/chip).  Jobs refer to a code by its id.
+ * Replaces the borrowed pointer of set_local_code_and_taps (cpu_multicorrelator_real_codes.cc:53-63):
+ * the code is COPIED to the device. */
+int gnsship_code_set(gnsship_ctx* ctx, int code_id, const float* code, int code_length);
+int gnsship_code_count(gnsship_ctx* ctx, int* n_codes);
+
+/* Local code replica generators (product side; reference src/algorithms/libs/ *_signal_replica.cc). */
+/* gps_l1_ca_code_gen_float (gps_sdr_signal_replica.cc:113): dest[1023] = ±1 */
+int gnsship_gps_l1_ca_code_gen_float(float* dest, int32_t prn, uint32_t chip_shift);
+/* gps_l1_ca_code_gen_complex_sampled (:145): dest = n complex (code in imag); returns n or <0 */
+int gnsship_gps_l1_ca_code_gen_complex_sampled(float* dest, uint32_t prn, int32_t sampling_freq, uint32_t chip_shift);
+/* beidou_b1i_code_gen_float (beidou_b1i_signal_replica.cc:113): dest[2046] = ±1 */
+int gnsship_beidou_b1i_code_gen_float(float* dest, int32_t prn, uint32_t chip_shift);
+/* beidou_b1i_code_gen_complex_sampled (:142): dest = n complex (code in real); returns n or <0 */
+int gnsship_beidou_b1i_code_gen_complex_sampled(float* dest, uint32_t prn, int32_t sampling_freq, uint32_t chip_shift);
+/* samples per code period: (int)(fs / (chip_rate / code_len)) as the generators compute it */
+int gnsship_code_samples_per_code(int32_t chip_rate, int32_t code_len, int32_t fs);
+
+/* ------------------------------------------------------------------------------------------ */
+/* Per-channel correlator: mirror of Cpu_Multicorrelator_Real_Codes.                          */
+/* ------------------------------------------------------------------------------------------ */
+/* init(max_signal_length_samples, n_correlators)  (cpu_multicorrelator_real_codes.cc:36-50) */
+int gnsship_corr_create(gnsship_ctx* ctx, int max_signal_length_samples, int n_correlators, gnsship_corr** out);
+/* set_local_code_and_taps(code_length_chips, local_code_in, shifts_chips)  (:53-63) */
+int gnsship_corr_set_local_code_and_taps(gnsship_corr* c, int code_length_chips, const float* local_code_in, const float* shifts_chips);
+/* set_high_dynamics_resampler (:163-167).  Default false, as Dll_Pll_Conf::high_dyn (dll_pll_conf.h:80). */
+int gnsship_corr_set_high_dynamics_resampler(gnsship_corr* c, int enable);
+/* Carrier_wipeoff_multicorrelator_resampler(...)  (:103-126).  `sig` is `fmt` samples; if
+ * sig_on_device != 0 it is a device pointer (e.g. into a gnsship_dev_alloc ring), else host.
+ * corr_out receives n_correlators complex<float> (2 floats each).  Synchronous. */
+int gnsship_corr_run(gnsship_corr* c, const void* sig, int fmt, int sig_on_device,
+    float rem_carrier_phase_in_rad, float phase_step_rad, float phase_rate_step_rad,
+    float rem_code_phase_chips, float code_phase_step_chips, float code_phase_rate_step_chips,
+    int signal_length_samples, float* corr_out);
+/* free()  (:147-160) */
+int gnsship_corr_destroy(gnsship_corr* c);
+
+/* ------------------------------------------------------------------------------------------ */
+/* Batched correlation: many (channel, epoch) jobs per launch.                                */
+/* ------------------------------------------------------------------------------------------ */
+/* One job = one call of Carrier_wipeoff_multicorrelator_resampler for one channel-epoch.
+ * NCO arguments carry the same meaning and float type as the reference call
+ * (dll_pll_veml_tracking.cc:1041-1048): code phases are in code SAMPLES (chips × samples/chip). */
+typedef struct gnsship_corr_job {
+    int64_t sample_offset;   /* first IF sample of this epoch in the device sample buffer      */
+    int32_t n_samples;       /* correlation length (vector_length)                            */
+    int32_t code_id;         /* code bank id                                                   */
+    int32_t n_taps;          /* 1..GNSSHIP_MAX_TAPS                                            */
+    int32_t flags;           /* bit0: high-dynamics resampler/rotator (unsupported: E_INVAL)   */
+    float rem_carrier_phase_rad;
+    float phase_step_rad;
+    float phase_rate_step_rad;
+    float rem_code_phase_chips;
+    float code_phase_step_chips;
+    float code_phase_rate_step_chips;
+    float shifts_chips[GNSSHIP_MAX_TAPS];
+} gnsship_corr_job; /* 80 bytes */
+
+int gnsship_batch_create(gnsship_ctx* ctx, int max_jobs, gnsship_batch** out);
+/* Copy job descriptors host→device (validated on the host: shapes, code ids, bounds). */
+int gnsship_batch_set_jobs(gnsship_batch* b, const gnsship_corr_job* jobs, int n_jobs, int64_t n_buffer_samples);
+/* Enqueue the correlation of all jobs on the context stream; results stay on the device.
+ * dev_samples: device IF buffer in `fmt`; n_buffer_samples bounds every job. Asynchronous. */
+int gnsship_batch_launch(gnsship_batch* b, const void* dev_samples, int fmt);
+/* Wait for the last launch and copy results: out[j*2*GNSSHIP_MAX_TAPS + 2*t + {0,1}] = tap t of job j. */
+int gnsship_batch_results(gnsship_batch* b, float* out);
+/* Device pointer of the result array (n_jobs × GNSSHIP_MAX_TAPS complex<float>). */
+int gnsship_batch_results_device(gnsship_batch* b, void** dev_out);
+int gnsship_batch_destroy(gnsship_batch* b);
+
+/* ------------------------------------------------------------------------------------------ */
+/* PCPS acquisition.                                                                          */
+/* ------------------------------------------------------------------------------------------ */
+/* Mirror of the Acq_Conf fields the core reads (acq_conf.h:33-81). */
+typedef struct gnsship_acq_conf {
+    int64_t fs_in;              /* sampling rate [Sps] (resampled_fs when no resampler)    */
+    int32_t fft_size;           /* d_fft_size = consumed samples (sampled_ms == ms_per_code) */
+    int32_t doppler_max;        /* [Hz]                                                       */
+    int32_t doppler_step;       /* [Hz]                                                       */
+    int32_t doppler_center;     /* [Hz]                                                       */
+    int32_t max_dwells;         /* non-coherent dwells accumulated into the grid              */
+    int32_t use_cfar;           /* 1: max_to_input_power_statistic, 0: first_vs_second_peak   */
+    int32_t samples_per_chip;   /* ceil(fs / chip_rate)                                       */
+    float samples_per_code;     /* samples_per_ms * ms_per_code                               */
+    int32_t max_prns;           /* number of local-code slots (PRNs searched per call)        */
+} gnsship_acq_conf;
+
+/* What acquisition_core leaves in Gnss_Synchro + block members (pcps_acquisition.cc:683-696). */
+typedef struct gnsship_acq_result {
+    uint32_t doppler_index;      /* winning Doppler bin                                       */
+    uint32_t code_index;         /* indext: winning FFT sample index                          */
+    int32_t doppler_hz;          /* Acq_doppler_hz                                            */
+    float peak;                  /* grid maximum (or first peak)                             */
+    float input_power;           /* d_input_power (CFAR) / second peak (first_vs_second)     */
+    float test_statistic;        /* d_test_statistics                                         */
+    double acq_delay_samples;    /* fmod(indext, samples_per_code)                            */
+} gnsship_acq_result;
+
+int gnsship_acq_create(gnsship_ctx* ctx, const gnsship_acq_conf* conf, gnsship_acq** out);
+/* Rebuild the Doppler wipeoff table (update_grid_doppler_wipeoffs): row i is exp(j*phi_n),
+ * phi accumulated in float32 exactly as volk_gnsssdr_s32f_sincos_32fc_generic. */
+int gnsship_acq_set_grid(gnsship_acq* a, int doppler_max, int doppler_step, int doppler_center);
+/* set_local_code: `code` is fft_size complex<float> (sampled, replicated); FFT + conj on device. */
+int gnsship_acq_set_local_code(gnsship_acq* a, int prn_slot, const float* code);
+/* acquisition_core over prn slots [0, n_prns): one dwell of fft_size samples, all bins.
+ * results[n_prns]; grid (optional, host, n_prns*n_bins*fft_size floats) receives |IFFT|^2. */
+int gnsship_acq_run(gnsship_acq* a, const void* sig, int fmt, int sig_on_device, int n_prns,
+    gnsship_acq_result* results, float* grid);
+int gnsship_acq_num_bins(gnsship_acq* a, int* n_bins);
+int gnsship_acq_destroy(gnsship_acq* a);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GNSSHIP_H */

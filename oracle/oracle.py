@@ -1,0 +1,258 @@
+"""CPU oracle for the GNSS hot path — TEST INFRASTRUCTURE ONLY.
+
+Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline`` leg may import this
+module, and only as the checker / the timed CPU baseline.  The product package
+``gnss_sim_receiver_amd`` never imports it (tests/test_product_isolation.py checks that).
+
+Two layers:
+
+* ``liboracle.so`` (``oracle/gnss_oracle.c``): C restatement of the reference's generic
+  volk_gnsssdr kernels, code generators and acquisition statistics, each function citing the
+  reference file:line it follows.
+* ``pcps_acquisition_core`` below: numpy restatement of ``pcps_acquisition::acquisition_core``
+  (src/algorithms/acquisition/gnuradio_blocks/pcps_acquisition.cc:600-871).  The FFT is a third-party
+  dependency of the reference (GNU Radio gr-fft → FFTW3f, version unpinned, absent here); its
+  published algorithm is the unnormalised DFT with forward kernel e^{-j2πkn/N}, which numpy's
+  pocketfft computes (``np.fft.fft`` / ``N·np.fft.ifft``).  Acquisition parity is therefore
+  defined on the peak (Doppler bin, code index), which is bit-exact whenever the peak is not a
+  near-tie; the fixtures record the tie margin.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+from dataclasses import dataclass
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+MAX_TAPS = 8
+
+_f32p = ctypes.POINTER(ctypes.c_float)
+_i32p = ctypes.POINTER(ctypes.c_int32)
+
+JOB_DTYPE = np.dtype(
+    [
+        ("sample_offset", "<i8"),
+        ("n_samples", "<i4"),
+        ("code_id", "<i4"),
+        ("n_taps", "<i4"),
+        ("flags", "<i4"),
+        ("rem_carrier_phase_rad", "<f4"),
+        ("phase_step_rad", "<f4"),
+        ("phase_rate_step_rad", "<f4"),
+        ("rem_code_phase_chips", "<f4"),
+        ("code_phase_step_chips", "<f4"),
+        ("code_phase_rate_step_chips", "<f4"),
+        ("shifts_chips", "<f4", (MAX_TAPS,)),
+    ]
+)
+assert JOB_DTYPE.itemsize == 80
+
+
+class AcqStat(ctypes.Structure):
+    _fields_ = [
+        ("doppler_index", ctypes.c_uint32),
+        ("code_index", ctypes.c_uint32),
+        ("doppler_hz", ctypes.c_int32),
+        ("peak", ctypes.c_float),
+        ("input_power", ctypes.c_float),
+        ("test_statistic", ctypes.c_float),
+        ("acq_delay_samples", ctypes.c_double),
+    ]
+
+
+def _ptr(a: np.ndarray, ctype=ctypes.c_float):
+    return a.ctypes.data_as(ctypes.POINTER(ctype))
+
+
+def build(fast: bool = True) -> None:
+    """Compile liboracle(.so, _fast.so) with oracle/Makefile (gcc only)."""
+    targets = ["all"]
+    subprocess.run(["make", "-s", "-C", HERE] + targets, check=True)
+
+
+_LIBS: dict = {}
+
+
+def lib(fast: bool = False) -> ctypes.CDLL:
+    name = "liboracle_fast.so" if fast else "liboracle.so"
+    if name in _LIBS:
+        return _LIBS[name]
+    path = os.path.join(HERE, name)
+    if not os.path.exists(path):
+        build()
+    L = ctypes.CDLL(path)
+    L.orc_gps_l1_ca_code_gen_float.argtypes = [_f32p, ctypes.c_int32, ctypes.c_uint32]
+    L.orc_gps_l1_ca_code_gen_complex_sampled.argtypes = [_f32p, ctypes.c_uint32, ctypes.c_int32, ctypes.c_uint32]
+    L.orc_beidou_b1i_code_gen_float.argtypes = [_f32p, ctypes.c_int32, ctypes.c_uint32]
+    L.orc_beidou_b1i_code_gen_complex_sampled.argtypes = [_f32p, ctypes.c_uint32, ctypes.c_int32, ctypes.c_uint32]
+    L.orc_resampler_generic.argtypes = [_f32p, _f32p, ctypes.c_float, ctypes.c_float, _f32p, ctypes.c_uint, ctypes.c_int, ctypes.c_uint]
+    L.orc_high_dynamics_resampler_generic.argtypes = [
+        _f32p, _f32p, ctypes.c_float, ctypes.c_float, ctypes.c_float, _f32p, ctypes.c_uint, ctypes.c_int, ctypes.c_uint]
+    L.orc_multicorrelator_real_codes.argtypes = [
+        _f32p, _f32p, _f32p, ctypes.c_int, _f32p, ctypes.c_int, ctypes.c_int,
+        ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float,
+        ctypes.c_int, _f32p]
+    L.orc_corr_batch.argtypes = [_f32p, ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(_f32p), _i32p, _f32p, ctypes.c_int]
+    L.orc_sincos_generic.argtypes = [_f32p, ctypes.c_float, _f32p, ctypes.c_uint]
+    L.orc_sincos_phases.argtypes = [_f32p, ctypes.c_float, ctypes.c_float, ctypes.c_uint]
+    L.orc_doppler_wipeoff_grid.argtypes = [_f32p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                           ctypes.c_int, ctypes.c_int64]
+    L.orc_index_max_generic.argtypes = [_f32p, ctypes.c_uint32]
+    L.orc_index_max_generic.restype = ctypes.c_uint32
+    L.orc_sum_serial_f32.argtypes = [_f32p, ctypes.c_uint32]
+    L.orc_sum_serial_f32.restype = ctypes.c_float
+    L.orc_max_to_input_power_statistic.argtypes = [
+        _f32p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32,
+        ctypes.c_float, ctypes.POINTER(AcqStat)]
+    L.orc_first_vs_second_peak_statistic.argtypes = [
+        _f32p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32,
+        ctypes.c_float, ctypes.POINTER(AcqStat)]
+    L.orc_cf32_multiply.argtypes = [_f32p, _f32p, _f32p, ctypes.c_uint32]
+    L.orc_cf32_magnitude_squared.argtypes = [_f32p, _f32p, ctypes.c_uint32]
+    _LIBS[name] = L
+    return L
+
+
+# ------------------------------------------------------------------------------------------ codes
+def gps_l1_ca_code(prn: int, chip_shift: int = 0) -> np.ndarray:
+    """gps_l1_ca_code_gen_float (gps_sdr_signal_replica.cc:113-124): 1023 float ±1."""
+    out = np.zeros(1023, np.float32)
+    if lib().orc_gps_l1_ca_code_gen_float(_ptr(out), prn, chip_shift):
+        raise ValueError(f"bad GPS PRN {prn}")
+    return out
+
+
+def gps_l1_ca_code_sampled(prn: int, fs: int, chip_shift: int = 0) -> np.ndarray:
+    """gps_l1_ca_code_gen_complex_sampled (:145-185): complex64, code in the imaginary part."""
+    n = int(float(fs) / (1023000.0 / 1023.0))
+    out = np.zeros(2 * n, np.float32)
+    lib().orc_gps_l1_ca_code_gen_complex_sampled(_ptr(out), prn, fs, chip_shift)
+    return out.view(np.complex64)
+
+
+def beidou_b1i_code(prn: int, chip_shift: int = 0) -> np.ndarray:
+    out = np.zeros(2046, np.float32)
+    if lib().orc_beidou_b1i_code_gen_float(_ptr(out), prn, chip_shift):
+        raise ValueError(f"bad BeiDou PRN {prn}")
+    return out
+
+
+def beidou_b1i_code_sampled(prn: int, fs: int, chip_shift: int = 0) -> np.ndarray:
+    n = int(float(fs) / (2046000.0 / 2046.0))
+    out = np.zeros(2 * n, np.float32)
+    lib().orc_beidou_b1i_code_gen_complex_sampled(_ptr(out), prn, fs, chip_shift)
+    return out.view(np.complex64)
+
+
+# ------------------------------------------------------------------------------------ correlator
+def resampler(code, rem, step, shifts, n, high_dyn_rate=None):
+    code = np.ascontiguousarray(code, np.float32)
+    shifts = np.ascontiguousarray(shifts, np.float32)
+    out = np.zeros((len(shifts), n), np.float32)
+    if high_dyn_rate is None:
+        lib().orc_resampler_generic(_ptr(out), _ptr(code), rem, step, _ptr(shifts), len(code), len(shifts), n)
+    else:
+        lib().orc_high_dynamics_resampler_generic(_ptr(out), _ptr(code), rem, step, high_dyn_rate, _ptr(shifts),
+                                                  len(code), len(shifts), n)
+    return out
+
+
+def multicorrelator(sig, code, shifts, rem_carr, carr_step, rem_code, code_step, n=None,
+                    carr_rate=0.0, code_rate=0.0, high_dyn=False, fast=False):
+    """Cpu_Multicorrelator_Real_Codes::Carrier_wipeoff_multicorrelator_resampler
+    (cpu_multicorrelator_real_codes.cc:103-126): returns complex64[n_taps]."""
+    sig = np.ascontiguousarray(sig, np.complex64)
+    code = np.ascontiguousarray(code, np.float32)
+    shifts = np.ascontiguousarray(shifts, np.float32)
+    n = len(sig) if n is None else n
+    out = np.zeros(2 * len(shifts), np.float32)
+    rc = lib(fast).orc_multicorrelator_real_codes(
+        _ptr(out), _ptr(sig.view(np.float32)), _ptr(code), len(code), _ptr(shifts), len(shifts), int(high_dyn),
+        rem_carr, carr_step, carr_rate, rem_code, code_step, code_rate, n, None)
+    if rc:
+        raise ValueError("oracle multicorrelator rejected arguments")
+    return out.view(np.complex64)
+
+
+def corr_batch(samples: np.ndarray, jobs: np.ndarray, codes: list, n_threads: int = 1, fast: bool = False) -> np.ndarray:
+    """Run every job (JOB_DTYPE) on host CF32 samples; returns complex64[n_jobs, MAX_TAPS]."""
+    samples = np.ascontiguousarray(samples, np.complex64)
+    jobs = np.ascontiguousarray(jobs, JOB_DTYPE)
+    codes = [np.ascontiguousarray(c, np.float32) for c in codes]
+    arr = (_f32p * len(codes))(*[_ptr(c) for c in codes])
+    lens = np.array([len(c) for c in codes], np.int32)
+    out = np.zeros((len(jobs), 2 * MAX_TAPS), np.float32)
+    lib(fast).orc_corr_batch(_ptr(samples.view(np.float32)), jobs.ctypes.data, len(jobs), arr, _ptr(lens, ctypes.c_int32),
+                             _ptr(out), n_threads)
+    return out.view(np.complex64)
+
+
+# ----------------------------------------------------------------------------------- acquisition
+def doppler_wipeoff_grid(n_bins, fft_size, doppler_max, doppler_step, doppler_center, fs, doppler_bias=0):
+    """update_grid_doppler_wipeoffs (pcps_acquisition.cc:295-302) → complex64[n_bins, fft_size]."""
+    t = np.zeros((n_bins, 2 * fft_size), np.float32)
+    lib().orc_doppler_wipeoff_grid(_ptr(t), n_bins, fft_size, doppler_max, doppler_step, doppler_center, doppler_bias, fs)
+    return t.view(np.complex64)
+
+
+def num_doppler_bins(doppler_max: int, doppler_step: int) -> int:
+    """pcps_acquisition::init (pcps_acquisition.cc:261)."""
+    return int(np.ceil(float(2 * doppler_max) / float(doppler_step)))
+
+
+@dataclass
+class AcqResult:
+    doppler_index: int
+    code_index: int
+    doppler_hz: int
+    peak: float
+    input_power: float
+    test_statistic: float
+    acq_delay_samples: float
+
+
+def acquisition_grid(sig, code_sampled, wipeoffs, fft_dtype=np.complex128):
+    """The Doppler loop of acquisition_core (pcps_acquisition.cc:640-672) for one dwell:
+    grid[i] = |IFFT(FFT(in ⊙ wipe_i) ⊙ conj(FFT(code)))|²  (unnormalised FFTW conventions)."""
+    n = wipeoffs.shape[1]
+    sig = np.ascontiguousarray(sig[:n], np.complex64)
+    code = np.ascontiguousarray(code_sampled[:n], np.complex64)
+    code_fft_conj = np.conj(np.fft.fft(code.astype(fft_dtype)))
+    wiped = (sig[None, :] * wipeoffs).astype(np.complex64)  # volk_32fc_x2_multiply_32fc (float)
+    X = np.fft.fft(wiped.astype(fft_dtype), axis=1)
+    Y = np.fft.ifft(X * code_fft_conj[None, :], axis=1) * n  # FFTW backward is unnormalised
+    return (Y.real ** 2 + Y.imag ** 2).astype(np.float32)
+
+
+def acquisition_statistic(grid, doppler_max, doppler_step, doppler_center, use_cfar, samples_per_chip,
+                          samples_per_code, dwells=1) -> AcqResult:
+    grid = np.ascontiguousarray(grid, np.float32)
+    nb, n = grid.shape
+    st = AcqStat()
+    if use_cfar:
+        lib().orc_max_to_input_power_statistic(_ptr(grid), nb, n, doppler_max, doppler_step, doppler_center, dwells,
+                                               samples_per_code, ctypes.byref(st))
+    else:
+        lib().orc_first_vs_second_peak_statistic(_ptr(grid), nb, n, doppler_max, doppler_step, doppler_center,
+                                                 samples_per_chip, samples_per_code, ctypes.byref(st))
+    return AcqResult(st.doppler_index, st.code_index, st.doppler_hz, st.peak, st.input_power, st.test_statistic,
+                     st.acq_delay_samples)
+
+
+def pcps_acquisition_core(sig, code_sampled, fs, doppler_max, doppler_step, doppler_center=0, use_cfar=True,
+                          samples_per_chip=None, samples_per_code=None, fft_dtype=np.complex128):
+    """acquisition_core (pcps_acquisition.cc:600-871), one dwell, step one, no resampler."""
+    n = len(code_sampled)
+    nb = num_doppler_bins(doppler_max, doppler_step)
+    w = doppler_wipeoff_grid(nb, n, doppler_max, doppler_step, doppler_center, fs)
+    grid = acquisition_grid(sig, code_sampled, w, fft_dtype)
+    if samples_per_chip is None:
+        samples_per_chip = int(np.ceil(np.float32(fs) / np.float32(1023000.0)))
+    if samples_per_code is None:
+        samples_per_code = float(np.float32(np.float32(fs) * np.float32(0.001)))
+    res = acquisition_statistic(grid, doppler_max, doppler_step, doppler_center, use_cfar, samples_per_chip,
+                                samples_per_code)
+    return res, grid

@@ -1,0 +1,31 @@
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (runs through libgnsship.so on cuda:0)")
+
+
+@pytest.fixture(scope="session")
+def built():
+    """Make sure libgnsship.so and the oracle exist (gcc/hipcc cross-compile, no GPU needed)."""
+    import subprocess
+    lib = os.path.join(ROOT, "gnss_sim_receiver_amd", "libgnsship.so")
+    orc = os.path.join(ROOT, "oracle", "liboracle.so")
+    if not (os.path.exists(lib) and os.path.exists(orc)):
+        subprocess.run(["make", "-s", "-C", ROOT, "all"], check=True)
+    return True
+
+
+@pytest.fixture(scope="session")
+def ctx(built):
+    from gnss_sim_receiver_amd import engine
+    c = engine.Context(0)
+    yield c
+    c.close()
