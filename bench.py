@@ -1,0 +1,260 @@
+#!/usr/bin/env python3
+"""Benchmark: IF Msamples/s processed & tracked channels sustained (BASELINE.json `metric`).
+
+Workload (N=1: BASELINE.json configs[1], "GPS L1 C/A, 12 channels, 4 Msps synthetic IF, HIP
+multicorrelator on 1 MI355X"):
+  * a 1-second synthetic IF block (4 Msps gr_complex, 32 MB) resident in HBM; 32 GPS satellites
+    present (SURVEY.md §8d model, CN0 45 dB-Hz, seed 0x6E550002);
+  * each rank runs one 12-channel receiver: channel c tracks satellite c mod 32;
+  * one step = the multicorrelator hot path over that block: every channel-epoch of the second
+    (12 × 1000 epochs, N = vector_length = 4000 samples, E/P/L taps at ±0.25 chip) as one
+    batched launch (rotator-anchor replay + correlation).  The NCO of every epoch comes from the
+    synthetic truth, i.e. what a locked DLL/PLL would command (the loop filters are §8f row f1).
+Multi-GPU (torchrun, one process per GPU): rank 0 broadcasts the IF block over RCCL every step
+(the reference fans one conditioner output out to every channel); every rank correlates its own 12
+channels (weak scaling).  value = Σ_ranks IF samples processed ÷ max-over-ranks wall time.
+
+Also reported: the dominant kernel's HBM roofline (HIP events on the engine stream), a CPU baseline
+(the oracle port at -O3 -march=native, threaded, on a bounded sample of the same workload, rank 0
+at N=1), and the PCPS acquisition sweep rate (32 PRNs × 40 Doppler bins, N = 4000).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+FS = 4_000_000
+VL = 4000               # vector_length = round(fs / (chip_rate / code_length))  (gps_l1_ca_dll_pll_tracking.cc:47)
+N_CH = 12               # channels per receiver (configs[1])
+N_SATS = 32
+SHIFTS = [-0.25, 0.0, 0.25]   # Dll_Pll_Conf early_late_space_chips = 0.25 (dll_pll_conf.h:50)
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
+SEED = 0x6E550002
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--seconds", type=float, default=1.0, help="IF block length per step [s]")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline time budget (0 = skip)")
+    ap.add_argument("--no-acq", action="store_true")
+    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_corr.json"),
+                    help="rocprofv3 PMC summary giving HBM bytes per launch (optional)")
+    return ap.parse_args()
+
+
+def build_block(seconds: float):
+    from gnss_sim_receiver_amd import signals
+    sats = signals.random_sky(N_SATS, seed=SEED)
+    n = int(round(FS * seconds)) + 2 * VL
+    return sats, signals.generate_if(FS, n, sats, seed=SEED), n
+
+
+def receiver_jobs(sats, rank: int, seconds: float):
+    from gnss_sim_receiver_amd import signals
+    n_ep = int(round(seconds * 1000))
+    jobs, code_ids = [], {}
+    for c in range(rank * N_CH, (rank + 1) * N_CH):
+        s = sats[c % N_SATS]
+        cid = code_ids.setdefault(s.prn, len(code_ids))
+        jobs.append(signals.truth_jobs(s, FS, n_ep, VL, SHIFTS, cid))
+    # epoch-major: the channels of one epoch read the same samples back to back (L2 reuse)
+    jobs = np.stack(jobs, axis=1).reshape(-1)
+    codes = [None] * len(code_ids)
+    for prn, cid in code_ids.items():
+        codes[cid] = next(s.code for s in sats if s.prn == prn)
+    return jobs, codes
+
+
+def cpu_baseline(block, jobs, codes, budget_s):
+    """Oracle port (generic semantics, -O3 -march=native, pthreads) on the same block and jobs,
+    repeated until the time budget is spent (bounded sample)."""
+    from oracle import oracle as O
+    O.build()
+    threads = min(16, len(os.sched_getaffinity(0)))
+    O.corr_batch(block, jobs[: N_CH * 10], codes, n_threads=threads, fast=True)  # warm
+    reps, t0 = 0, time.perf_counter()
+    per = max(N_CH, (len(jobs) // N_CH // 10) * N_CH)  # 1/10 of the block per call
+    done_jobs = 0
+    while time.perf_counter() - t0 < budget_s:
+        lo = (reps * per) % len(jobs)
+        sl = jobs[lo: lo + per]
+        O.corr_batch(block, sl, codes, n_threads=threads, fast=True)
+        done_jobs += len(sl)
+        reps += 1
+    dt = time.perf_counter() - t0
+    epochs = done_jobs / N_CH
+    msps = epochs * VL / dt / 1e6
+    return {"value": round(msps, 2), "unit": "Msamples/s", "cores": threads, "kind": "port",
+            "sample": f"{done_jobs} channel-epochs ({epochs:.0f} epochs × {N_CH} ch, N={VL}, 3 taps) of the same block in {dt:.1f} s, "
+                      f"oracle/gnss_oracle.c generic semantics at -O3 -march=native, {threads} pthreads",
+            "channel_msps": round(done_jobs * VL / dt / 1e6, 2)}
+
+
+def acq_bench(ctx, block, sats):
+    """32-PRN all-sky PCPS sweep at 4 Msps: 40 bins (±5 kHz / 250 Hz) × 4000-sample FFTs."""
+    from gnss_sim_receiver_amd import codes as C, engine
+    acq = engine.PcpsAcquisition(ctx, FS, VL, 5000, 250, 0, True, max_prns=32)
+    for k in range(32):
+        acq.set_local_code(C.gps_l1_ca_code_gen_complex_sampled(k + 1, FS), k)
+    dev = ctx.upload(np.ascontiguousarray(block[:VL]))
+    for _ in range(3):
+        acq.run(dev, n_prns=32)
+    reps = 20
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        res, _ = acq.run(dev, n_prns=32)
+    dt = (time.perf_counter() - t0) / reps
+    found = sum(1 for r in res if r.test_statistic > 40)
+    cells = 32 * acq.n_bins
+    out = {"config": "32 PRN x 40 bins, fft 4000, 4 Msps (C3 sweep shape at 4 Msps)", "sweep_ms": round(dt * 1e3, 3),
+           "sweeps_per_s": round(1 / dt, 1), "cells_per_s": round(cells / dt, 0), "prns_detected": found,
+           "algorithmic_GBps": round(cells * 20 * VL / dt / 1e9, 1)}
+    acq.close()
+    dev.free()
+    return out
+
+
+def main():
+    args = parse()
+    from gnss_sim_receiver_amd import abi, engine, sharding
+
+    rank, world, local_rank = sharding.dist_env()
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            raise SystemExit("--gpus N>1 must be launched with torch.distributed.run (one process per GPU)")
+    torch = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl")
+
+    ctx = engine.Context(local_rank)
+    sats = None
+    if rank == 0:
+        sats, block, n_samples = build_block(args.seconds)
+    else:
+        from gnss_sim_receiver_amd import signals
+        sats = signals.random_sky(N_SATS, seed=SEED)  # same satellites (codes, truth) on every rank
+        n_samples = int(round(FS * args.seconds)) + 2 * VL
+        block = None
+
+    # IF block resident in HBM
+    if torch is not None:
+        dev_t = torch.empty(n_samples, dtype=torch.complex64, device=f"cuda:{local_rank}")
+        if rank == 0:
+            dev_t.copy_(torch.from_numpy(block))
+        sharding.broadcast_block(dev_t, src=0)
+        torch.cuda.synchronize()
+        dev_ptr = dev_t.data_ptr()
+    else:
+        dev_buf = ctx.upload(block)
+        dev_ptr = dev_buf.ptr
+
+    jobs, codes = receiver_jobs(sats, rank, args.seconds)
+    for cid, c in enumerate(codes):
+        ctx.set_code(cid, c)
+    batch = engine.CorrelatorBatch(ctx, len(jobs))
+    batch.set_jobs(jobs, n_samples)
+
+    def step():
+        if torch is not None:
+            sharding.broadcast_block(dev_t, src=0)   # RCCL fan-out of the IF block (exchange step)
+            torch.cuda.current_stream().synchronize()
+        batch.launch_ptr(dev_ptr, abi.FMT_CF32)
+
+    for _ in range(args.warmup):
+        step()
+    ctx.sync()
+
+    def barrier():
+        if torch is not None:
+            torch.distributed.barrier()
+            torch.cuda.synchronize()
+        ctx.sync()
+
+    barrier()
+    t0 = time.perf_counter()
+    ctx.event_record(0)
+    for _ in range(args.steps):
+        step()
+    ctx.event_record(1)
+    barrier()
+    wall = time.perf_counter() - t0
+    wall = sharding.max_over_ranks(wall)
+    launch_ms = ctx.event_elapsed_ms(0, 1) / args.steps
+
+    # per-kernel split on the same stream: anchors-only and correlate-only launches
+    def timed(stages, reps=max(5, args.steps)):
+        ctx.event_record(2)
+        for _ in range(reps):
+            batch.launch_ptr(dev_ptr, abi.FMT_CF32, stages)
+        ctx.event_record(3)
+        return ctx.event_elapsed_ms(2, 3) / reps
+
+    anchor_ms = timed(abi.STAGE_ANCHORS)
+    corr_ms = timed(abi.STAGE_CORRELATE)
+
+    epochs = int(round(args.seconds * 1000))
+    samples_per_step = epochs * VL                # IF samples each 12-channel receiver consumes
+    chan_samples = len(jobs) * VL                 # channel-samples correlated per rank per step
+    value = world * samples_per_step * args.steps / wall / 1e6
+    bytes_per_launch = chan_samples * 8 + len(jobs) * 3 * 8   # s·N + 8·T_out per channel-epoch
+    achieved = bytes_per_launch / (corr_ms * 1e-3) / 1e9
+    traffic = None
+    if os.path.exists(args.pmc):
+        try:
+            traffic = json.load(open(args.pmc)).get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    result = {
+        "metric": "IF Msamples/sec processed & tracked-channels sustained @1/2/4/8 GPU",
+        "value": round(value, 1),
+        "unit": "Msamples/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(wall / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic",
+        "config": {"workload": "GPS L1 C/A, 12 channels, 4 Msps synthetic IF (gr_complex), HIP multicorrelator (configs[1])",
+                   "channels_per_gpu": N_CH, "fs_sps": FS, "vector_length": VL, "taps": 3, "block_s": args.seconds,
+                   "channel_epochs_per_step_per_gpu": int(len(jobs)), "nco": "synthetic truth (locked-loop NCO), loop filters = §8f f1",
+                   "parallelism": f"channels sharded, IF block RCCL-broadcast, {world} rank(s)"},
+        "tracked_channels_sustained": int(world * chan_samples * args.steps / wall / FS),
+        "channel_msamples_per_s": round(world * chan_samples * args.steps / wall / 1e6, 1),
+        "kernel_ms": {"launch_total": round(launch_ms, 4), "corr_anchor_kernel": round(anchor_ms, 4),
+                      "corr_batch_kernel+reduce": round(corr_ms, 4)},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic},
+    }
+    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+        result["cpu_baseline"] = cpu_baseline(block, jobs, codes, args.cpu_seconds)
+    if rank == 0 and not args.no_acq:
+        result["acquisition"] = acq_bench(ctx, block, sats)
+    batch.close()
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if torch is not None:
+        torch.distributed.barrier()
+        torch.distributed.destroy_process_group()
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()

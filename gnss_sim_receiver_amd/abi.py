@@ -19,6 +19,7 @@ HEADER_PATH = os.path.join(REPO_DIR, "include", "gnsship.h")
 
 OK, E_INVAL, E_NOMEM, E_DEVICE, E_STATE = 0, -1, -2, -3, -4
 FMT_CF32, FMT_CI16, FMT_CI8 = 0, 1, 2
+STAGE_ANCHORS, STAGE_CORRELATE = 1, 2
 MAX_TAPS = 8
 _ERRNAMES = {E_INVAL: "E_INVAL", E_NOMEM: "E_NOMEM", E_DEVICE: "E_DEVICE", E_STATE: "E_STATE"}
 
@@ -111,6 +112,7 @@ _SIGNATURES = {
     "gnsship_batch_create": ([_vp, _i, _vpp], _i),
     "gnsship_batch_set_jobs": ([_vp, _vp, _i, ctypes.c_int64], _i),
     "gnsship_batch_launch": ([_vp, _vp, _i], _i),
+    "gnsship_batch_launch_stages": ([_vp, _vp, _i, _i], _i),
     "gnsship_batch_results": ([_vp, _f32p], _i),
     "gnsship_batch_results_device": ([_vp, _vpp], _i),
     "gnsship_batch_destroy": ([_vp], _i),

@@ -22,10 +22,12 @@ struct CodeDesc {
     int32_t pad;
 };
 
-// Device-side job, derived on the host from gnsship_corr_job: every float argument that the
-// reference turns into a phasor is pre-evaluated ONCE per job on the host with the reference's
-// own float operations (cosf/sinf of float, as std::cos / std::exp(complex<float>) do in
-// cpu_multicorrelator_real_codes.cc:115,123), then its exact angle / magnitude taken in double.
+constexpr int kRenorm = 256;             // the generic rotator renormalises |phase| every 256 samples
+
+// Device-side job, derived on the host from gnsship_corr_job.  The two phasors the reference
+// forms per call are evaluated on the host with the reference's own float operations
+// (cpu_multicorrelator_real_codes.cc:115,123: (cos rem, −sin rem) and std::exp(complex<float>(0,−step))
+// = glibc cexpf → (cosf(−step), sinf(−step))); the device then reproduces the rotator recursion.
 struct DevJob {
     int64_t sample_offset;
     int32_t n_samples;
@@ -33,14 +35,21 @@ struct DevJob {
     int32_t n_taps;
     int32_t n_chunks;       // workgroups covering this job
     int32_t first_chunk;    // index of its first chunk (partials row)
-    int32_t pad0;
-    double theta0;          // arg(phase_offset_as_complex)
-    double dtheta;          // arg(phase_inc) = arg(exp(-j*phase_step_rad)) in float, exactly
-    float mag0;             // |phase_offset_as_complex|
-    float log_mag_inc;      // log|phase_inc| (per-sample magnitude growth between renormalisations)
+    int32_t anchor_offset;  // first of ceil(n/256) anchors of this job
+    float p0_re, p0_im;     // phase_offset_as_complex
+    float inc_re, inc_im;   // phase_inc
+    double dtheta;          // arg(phase_inc) in double (exact angle of the float phasor)
+    float log_mag_inc;      // log|phase_inc| (magnitude growth between renormalisations)
     float rem_code;         // rem_code_phase_chips  (float, as passed by the reference)
     float code_step;        // code_phase_step_chips
+    float pad1;
     float shifts[kMaxTaps];
+};
+
+// Rotator anchor of one 256-sample block k of a job: `a` = the phasor the reference multiplies
+// sample 256k by (before renormalising), `q` = a/|a| (the renormalised phasor it then rotates).
+struct Anchor {
+    float a_re, a_im, q_re, q_im;
 };
 
 struct ChunkDesc {
@@ -51,8 +60,10 @@ struct ChunkDesc {
 };
 
 // Launch the batched correlator: partials[chunk][2*kMaxTaps] then per-job reduction into out.
+// anchors: scratch of Σ ceil(n_j/256) Anchor entries, recomputed by every launch.
 hipError_t launch_corr_batch(const void* samples, int fmt, const DevJob* jobs, int n_jobs, const ChunkDesc* chunks, int n_chunks,
-    const CodeDesc* codes, int max_code_len, bool any_multi_chunk, float* partials, float* out, hipStream_t stream);
+    const CodeDesc* codes, int max_code_len, bool any_multi_chunk, Anchor* anchors, float* partials, float* out, hipStream_t stream,
+    int stages = GNSSHIP_STAGE_ANCHORS | GNSSHIP_STAGE_CORRELATE);
 
 }  // namespace gnsship
 

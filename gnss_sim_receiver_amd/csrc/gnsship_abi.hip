@@ -73,24 +73,30 @@ bool derive_job(const gnsship_corr_job& in, DevJob& out)
     out.n_samples = in.n_samples;
     out.code_id = in.code_id;
     out.n_taps = in.n_taps;
-    out.theta0 = std::atan2(static_cast<double>(p0i), static_cast<double>(p0r));
-    out.mag0 = static_cast<float>(std::hypot(static_cast<double>(p0r), static_cast<double>(p0i)));
+    out.p0_re = p0r;
+    out.p0_im = p0i;
+    out.inc_re = incr;
+    out.inc_im = inci;
     out.dtheta = std::atan2(static_cast<double>(inci), static_cast<double>(incr));
     out.log_mag_inc = static_cast<float>(std::log(std::hypot(static_cast<double>(incr), static_cast<double>(inci))));
     out.rem_code = in.rem_code_phase_chips;
     out.code_step = in.code_phase_step_chips;
+    out.pad1 = 0.0f;
     for (int t = 0; t < kMaxTaps; t++) out.shifts[t] = (t < in.n_taps) ? in.shifts_chips[t] : 0.0f;
-    out.pad0 = 0;
     return true;
 }
 
-// Split jobs into ≤kCorrChunk-sample chunks; returns number of chunks.
-int plan_chunks(std::vector<DevJob>& jobs, std::vector<ChunkDesc>& chunks, bool& any_multi)
+// Split jobs into ≤kCorrChunk-sample chunks and lay out their rotator anchors; returns the
+// number of chunks, total anchors in *n_anchors.
+int plan_chunks(std::vector<DevJob>& jobs, std::vector<ChunkDesc>& chunks, bool& any_multi, int64_t* n_anchors)
 {
     chunks.clear();
     any_multi = false;
+    int64_t anchors = 0;
     for (size_t j = 0; j < jobs.size(); j++) {
         const int n = jobs[j].n_samples;
+        jobs[j].anchor_offset = static_cast<int32_t>(anchors);
+        anchors += (n + kRenorm - 1) / kRenorm;
         const int nc = n <= 0 ? 1 : (n + kCorrChunk - 1) / kCorrChunk;
         jobs[j].n_chunks = nc;
         jobs[j].first_chunk = static_cast<int32_t>(chunks.size());
@@ -105,6 +111,7 @@ int plan_chunks(std::vector<DevJob>& jobs, std::vector<ChunkDesc>& chunks, bool&
             chunks.push_back(d);
         }
     }
+    *n_anchors = anchors > 0 ? anchors : 1;
     return static_cast<int>(chunks.size());
 }
 
@@ -283,6 +290,8 @@ struct gnsship_batch {
     ChunkDesc* chunks_dev = nullptr;
     float* partials_dev = nullptr;
     float* out_dev = nullptr;
+    Anchor* anchors_dev = nullptr;
+    int64_t anchor_cap = 0;
     std::vector<DevJob> jobs_host;
     std::vector<ChunkDesc> chunks_host;
 };
@@ -325,7 +334,14 @@ extern "C" int gnsship_batch_set_jobs(gnsship_batch* b, const gnsship_corr_job* 
         if (ctx->codes_host[in.code_id].len > max_len) max_len = ctx->codes_host[in.code_id].len;
     }
     b->max_code_len = max_len;
-    b->n_chunks = plan_chunks(b->jobs_host, b->chunks_host, b->any_multi);
+    int64_t n_anchors = 0;
+    b->n_chunks = plan_chunks(b->jobs_host, b->chunks_host, b->any_multi, &n_anchors);
+    if (n_anchors > b->anchor_cap) {
+        if (b->anchors_dev) HIP_TRY(ctx, hipFree(b->anchors_dev));
+        b->anchors_dev = nullptr;
+        HIP_TRY(ctx, hipMalloc(&b->anchors_dev, sizeof(Anchor) * n_anchors));
+        b->anchor_cap = n_anchors;
+    }
     if (b->n_chunks > b->chunk_cap) {
         if (b->chunks_dev) HIP_TRY(ctx, hipFree(b->chunks_dev));
         if (b->partials_dev) HIP_TRY(ctx, hipFree(b->partials_dev));
@@ -346,14 +362,19 @@ extern "C" int gnsship_batch_set_jobs(gnsship_batch* b, const gnsship_corr_job* 
 
 extern "C" int gnsship_batch_launch(gnsship_batch* b, const void* dev_samples, int fmt)
 {
-    if (!b) return GNSSHIP_E_INVAL;
+    return gnsship_batch_launch_stages(b, dev_samples, fmt, GNSSHIP_STAGE_ANCHORS | GNSSHIP_STAGE_CORRELATE);
+}
+
+extern "C" int gnsship_batch_launch_stages(gnsship_batch* b, const void* dev_samples, int fmt, int stages)
+{
+    if (!b || stages < 1 || stages > 3) return GNSSHIP_E_INVAL;
     gnsship_ctx* ctx = b->ctx;
     if (fmt_bytes(fmt) == 0) return fail(ctx, GNSSHIP_E_INVAL, "gnsship_batch_launch: unknown sample format");
     if (!dev_samples && b->n_jobs) return fail(ctx, GNSSHIP_E_INVAL, "gnsship_batch_launch: null sample buffer");
     if (b->n_jobs == 0) return GNSSHIP_OK;
     if (ctx->codes_dirty) return fail(ctx, GNSSHIP_E_STATE, "gnsship_batch_launch: code bank changed after set_jobs");
     hipError_t e = launch_corr_batch(dev_samples, fmt, b->jobs_dev, b->n_jobs, b->chunks_dev, b->n_chunks, ctx->codes_dev, b->max_code_len,
-        b->any_multi, b->partials_dev, b->out_dev, ctx->stream);
+        b->any_multi, b->anchors_dev, b->partials_dev, b->out_dev, ctx->stream, stages);
     if (e != hipSuccess) return hip_fail(ctx, e, "launch_corr_batch");
     return GNSSHIP_OK;
 }
@@ -385,6 +406,7 @@ extern "C" int gnsship_batch_destroy(gnsship_batch* b)
     if (b->chunks_dev) (void)hipFree(b->chunks_dev);
     if (b->partials_dev) (void)hipFree(b->partials_dev);
     if (b->out_dev) (void)hipFree(b->out_dev);
+    if (b->anchors_dev) (void)hipFree(b->anchors_dev);
     delete b;
     return GNSSHIP_OK;
 }
@@ -406,6 +428,7 @@ struct gnsship_corr {
     ChunkDesc* chunks_dev = nullptr;
     float* partials_dev = nullptr;
     float* out_dev = nullptr;
+    Anchor* anchors_dev = nullptr;
     int chunk_cap = 0;
 };
 
@@ -427,6 +450,7 @@ extern "C" int gnsship_corr_create(gnsship_ctx* ctx, int max_signal_length_sampl
     if (e == hipSuccess) e = hipMalloc(&c->chunks_dev, sizeof(ChunkDesc) * c->chunk_cap);
     if (e == hipSuccess) e = hipMalloc(&c->partials_dev, sizeof(float) * 2 * kMaxTaps * c->chunk_cap);
     if (e == hipSuccess) e = hipMalloc(&c->out_dev, sizeof(float) * 2 * kMaxTaps);
+    if (e == hipSuccess) e = hipMalloc(&c->anchors_dev, sizeof(Anchor) * ((max_signal_length_samples + kRenorm - 1) / kRenorm + 1));
     if (e != hipSuccess) {
         gnsship_corr_destroy(c);
         return hip_fail(ctx, e, "gnsship_corr_create");
@@ -492,7 +516,8 @@ extern "C" int gnsship_corr_run(gnsship_corr* c, const void* sig, int fmt, int s
     if (!derive_job(in, jobs[0])) return fail(ctx, GNSSHIP_E_INVAL, "gnsship_corr_run: invalid job");
     std::vector<ChunkDesc> chunks;
     bool multi = false;
-    const int nch = plan_chunks(jobs, chunks, multi);
+    int64_t n_anchors = 0;
+    const int nch = plan_chunks(jobs, chunks, multi, &n_anchors);
     const void* src = sig;
     if (!sig_on_device) {
         HIP_TRY(ctx, hipMemcpyAsync(c->sig_dev, sig, fmt_bytes(fmt) * static_cast<size_t>(n), hipMemcpyHostToDevice, ctx->stream));
@@ -500,8 +525,8 @@ extern "C" int gnsship_corr_run(gnsship_corr* c, const void* sig, int fmt, int s
     }
     HIP_TRY(ctx, hipMemcpyAsync(c->job_dev, jobs.data(), sizeof(DevJob), hipMemcpyHostToDevice, ctx->stream));
     HIP_TRY(ctx, hipMemcpyAsync(c->chunks_dev, chunks.data(), sizeof(ChunkDesc) * nch, hipMemcpyHostToDevice, ctx->stream));
-    hipError_t e = launch_corr_batch(src, fmt, c->job_dev, 1, c->chunks_dev, nch, c->code_table_dev, c->code_len, multi, c->partials_dev,
-        c->out_dev, ctx->stream);
+    hipError_t e = launch_corr_batch(src, fmt, c->job_dev, 1, c->chunks_dev, nch, c->code_table_dev, c->code_len, multi, c->anchors_dev,
+        c->partials_dev, c->out_dev, ctx->stream);
     if (e != hipSuccess) return hip_fail(ctx, e, "launch_corr_batch");
     float tmp[2 * kMaxTaps];
     HIP_TRY(ctx, hipMemcpyAsync(tmp, c->out_dev, sizeof(tmp), hipMemcpyDeviceToHost, ctx->stream));
@@ -515,7 +540,7 @@ extern "C" int gnsship_corr_destroy(gnsship_corr* c)
     if (!c) return GNSSHIP_E_INVAL;
     (void)hipSetDevice(c->ctx->device);
     (void)hipStreamSynchronize(c->ctx->stream);
-    void* ptrs[] = {c->code_dev, c->code_table_dev, c->sig_dev, c->job_dev, c->chunks_dev, c->partials_dev, c->out_dev};
+    void* ptrs[] = {c->code_dev, c->code_table_dev, c->sig_dev, c->job_dev, c->chunks_dev, c->partials_dev, c->out_dev, c->anchors_dev};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     delete c;

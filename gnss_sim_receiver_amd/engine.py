@@ -207,8 +207,8 @@ class CorrelatorBatch:
     def launch(self, samples: DeviceBuffer, fmt: int = FMT_CF32):
         check(self.ctx.lib.gnsship_batch_launch(self.h, samples.ptr, fmt), "gnsship_batch_launch", self.ctx.h)
 
-    def launch_ptr(self, dev_ptr: int, fmt: int = FMT_CF32):
-        check(self.ctx.lib.gnsship_batch_launch(self.h, dev_ptr, fmt), "gnsship_batch_launch", self.ctx.h)
+    def launch_ptr(self, dev_ptr: int, fmt: int = FMT_CF32, stages: int = 3):
+        check(self.ctx.lib.gnsship_batch_launch_stages(self.h, dev_ptr, fmt, stages), "gnsship_batch_launch_stages", self.ctx.h)
 
     def results(self) -> np.ndarray:
         out = np.zeros((self.n_jobs, 2 * MAX_TAPS), np.float32)

@@ -139,6 +139,11 @@ int gnsship_batch_set_jobs(gnsship_batch* b, const gnsship_corr_job* jobs, int n
 /* Enqueue the correlation of all jobs on the context stream; results stay on the device.
  * dev_samples: device IF buffer in `fmt`; n_buffer_samples bounds every job. Asynchronous. */
 int gnsship_batch_launch(gnsship_batch* b, const void* dev_samples, int fmt);
+/* Profiling split of gnsship_batch_launch: stages bit0 = rotator-anchor replay (NCO arguments
+ * only), bit1 = correlation (+ chunk reduction).  3 == gnsship_batch_launch. */
+#define GNSSHIP_STAGE_ANCHORS 1
+#define GNSSHIP_STAGE_CORRELATE 2
+int gnsship_batch_launch_stages(gnsship_batch* b, const void* dev_samples, int fmt, int stages);
 /* Wait for the last launch and copy results: out[j*2*GNSSHIP_MAX_TAPS + 2*t + {0,1}] = tap t of job j. */
 int gnsship_batch_results(gnsship_batch* b, float* out);
 /* Device pointer of the result array (n_jobs × GNSSHIP_MAX_TAPS complex<float>). */

@@ -67,10 +67,10 @@ def test_multi_prn_sweep_present_and_absent(ctx):
         if flat[-1] / flat[-2] > 1.0 + 1e-4:  # peak not a near-tie: must be exact
             assert (res[k].doppler_index, res[k].code_index) == (ref.doppler_index, ref.code_index), p
         np.testing.assert_allclose(res[k].test_statistic, ref.test_statistic, rtol=2e-3)
-    for k in range(4):
-        assert res[k].test_statistic > 20
-    for k in range(4, 8):
-        assert res[k].test_statistic < 20
+    # noise-only CFAR statistic ≈ 2·ln(cells) ≈ 25 for 80 × 4000 cells; present PRNs far above
+    absent_max = max(res[k].test_statistic for k in range(4, 8))
+    assert absent_max < 40
+    assert min(res[k].test_statistic for k in range(4)) > 2 * absent_max
     acq.close()
 
 

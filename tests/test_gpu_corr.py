@@ -122,10 +122,13 @@ def test_edge_cases_index_wrap_and_lengths(ctx):
     for j in range(1, len(jobs)):
         t = jobs[j]["n_taps"]
         n = jobs[j]["n_samples"]
-        # noise-only: |ref| ~ sqrt(n); compare against the accumulation scale as well
-        scale = np.maximum(np.abs(ref[j, :t]), np.sqrt(n) * 1e-1)
+        # Noise-only taps can cancel to |ref| ≪ ||x||₂, where the reference's own serial float sum
+        # carries ~n·2⁻²⁴·|partial sum| of rounding; the bound is then taken relative to the
+        # accumulation scale ||x||₂ (the RMS of such a sum).
+        x = sig[jobs[j]["sample_offset"]: jobs[j]["sample_offset"] + n]
+        scale = np.maximum(np.abs(ref[j, :t]), np.sqrt(np.sum(np.abs(x.astype(np.complex128)) ** 2)))
         e = np.max(np.abs(out[j, :t] - ref[j, :t]) / scale)
-        assert e <= 1e-4 if n > 50000 else e <= TOL, (j, e)
+        assert e <= TOL, (j, e)
 
 
 def test_bounds_and_state_errors(ctx):
