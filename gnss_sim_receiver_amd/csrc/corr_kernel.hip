@@ -30,6 +30,10 @@
 //    deviation from the reference is its own ≤255-step rounding walk (≈1e-6 rad).
 #include "engine.h"
 
+// Every product/sum on the parity path is rounded on its own, like the reference's generic C;
+// the few fused multiply-adds wanted are written explicitly (__fmaf_rn).
+#pragma clang fp contract(off)
+
 namespace gnsship {
 
 __device__ __forceinline__ float2 cmul_rn(float ar, float ai, float br, float bi)
@@ -51,21 +55,29 @@ __global__ void corr_anchor_kernel(const DevJob* __restrict__ jobs, int n_jobs, 
     const DevJob job = jobs[j];
     const int nblk = (job.n_samples + kRenorm - 1) / kRenorm;
     Anchor* out = anchors + job.anchor_offset;
+    typedef float f2v __attribute__((ext_vector_type(2)));
     float pr = job.p0_re, pi = job.p0_im;
-    const float ir = job.inc_re, ii = job.inc_im;
+    // phase·inc = (pr·ir − pi·ii, pr·ii + pi·ir) as two packed products + one packed add, each
+    // rounded separately like the reference's written-out complex product (no FMA).  The sign
+    // sits in the constant: fl(pi·(−ii)) = −fl(pi·ii) and x + (−y) ≡ x − y, bit for bit.
+    const f2v inc_a = {job.inc_re, job.inc_im};   // × pr
+    const f2v inc_b = {-job.inc_im, job.inc_re};  // × pi
     for (int k = 0; k < nblk; k++) {
         // sample 256k uses `a = phase`; then phase /= |phase|; then 256 rotations reach 256(k+1)
         const float m = hypotf_glibc(pr, pi);
         const float qr = __fdiv_rn(pr, m), qi = __fdiv_rn(pi, m);
         out[k] = Anchor{pr, pi, qr, qi};
-        pr = qr;
-        pi = qi;
-        const int steps = (k == nblk - 1) ? 0 : kRenorm;
-        for (int s = 0; s < steps; s++) {
-            const float2 p = cmul_rn(pr, pi, ir, ii);
-            pr = p.x;
-            pi = p.y;
+        f2v p = {qr, qi};
+        if (k != nblk - 1) {
+#pragma unroll 16
+            for (int s = 0; s < kRenorm; s++) {
+                const f2v m1 = f2v{p.x, p.x} * inc_a;
+                const f2v m2 = f2v{p.y, p.y} * inc_b;
+                p = m1 + m2;
+            }
         }
+        pr = p.x;
+        pi = p.y;
     }
 }
 
@@ -90,62 +102,113 @@ __device__ __forceinline__ float wave_sum(float v)
     return v;
 }
 
-template <int FMT, int NT>
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+// (a·b) for phasor products off the parity-critical path (contraction allowed: one packed
+// multiply + one packed FMA).  bsw = (−b.im, b.re).
+__device__ __forceinline__ f2 cmul_pk(f2 a, f2 b, f2 bsw)
+{
+    return __builtin_elementwise_fma(f2{a.y, a.y}, bsw, f2{a.x, a.x} * b);
+}
+
+// Positive modulo of the reference's wrap (volk_gnsssdr_32f_xn_resampler_32f_xn.h:75-77).
+__device__ __forceinline__ int wrap_index(int idx, int L)
+{
+    idx = idx < 0 ? idx + L : idx;
+    idx = idx >= L ? idx - L : idx;
+    if (static_cast<unsigned>(idx) >= static_cast<unsigned>(L)) {  // more than one period away
+        idx %= L;
+        if (idx < 0) idx += L;
+    }
+    return idx;
+}
+
+// One chunk of one job.  `code` points at chip 0 of the padded LDS replica (valid indices
+// [−kCodeMargin, L + kCodeMargin)).  IN_MARGIN: the host proved every index of the job lies in the
+// padded range, so the chip index is used directly (no modulo).
+template <int FMT, int NT, bool IN_MARGIN>
 __device__ __forceinline__ void corr_chunk(const void* __restrict__ samples, const DevJob& job, const ChunkDesc& ch,
-    const Anchor* __restrict__ anchors, const float* __restrict__ lds_code, int L, float* __restrict__ dst)
+    const Anchor* __restrict__ anchors, const float* __restrict__ code, int L, float* __restrict__ dst)
 {
     __shared__ float red[kCorrThreads / 64][2 * kMaxTaps];
 
-    float acc[2 * NT];
+    f2 acc[NT];
 #pragma unroll
-    for (int v = 0; v < 2 * NT; v++) acc[v] = 0.0f;
-
+    for (int t = 0; t < NT; t++) acc[t] = f2{0.0f, 0.0f};
     float shifts[NT];
 #pragma unroll
     for (int t = 0; t < NT; t++) shifts[t] = (t < job.n_taps) ? job.shifts[t] : 0.0f;
 
     const int tid = threadIdx.x;  // == offset j inside every 256-sample block this lane visits
+    const int64_t base = job.sample_offset + ch.start;
     // E_j = |inc|^j · e^{i j Δ}: rotation from the renormalised anchor to sample 256k + j
-    float er, ei;
+    // (angle formed and range-reduced in double, then an accurate float sincos)
+    f2 e, esw;
     {
-        double s, c;
-        sincos(static_cast<double>(tid) * job.dtheta, &s, &c);
-        const double mag = 1.0 + static_cast<double>(tid) * static_cast<double>(job.log_mag_inc);
-        er = static_cast<float>(mag * c);
-        ei = static_cast<float>(mag * s);
+        constexpr double kTwoPi = 6.283185307179586476925286766559;
+        constexpr double kInvTwoPi = 0.15915494309189533576888376337251;
+        double th = static_cast<double>(tid) * job.dtheta;
+        th = fma(-kTwoPi, rint(th * kInvTwoPi), th);
+        float s, c;
+        sincosf(static_cast<float>(th), &s, &c);
+        const float mag = __fmaf_rn(static_cast<float>(tid), job.log_mag_inc, 1.0f);
+        e = f2{mag * c, mag * s};
+        esw = f2{-e.y, e.x};
     }
-    const int64_t base = job.sample_offset;
     const Anchor* anc = anchors + job.anchor_offset + (ch.start >> 8);
-#pragma unroll 4
-    for (int m = 0; m < kCorrSamplesPerThread; m++) {
-        const int r = tid + m * kCorrThreads;
-        if (r >= ch.len) break;
-        const int n = ch.start + r;  // sample index relative to the job (the reference's loop counter)
-        const float2 x = load_sample<FMT>(samples, base + n);
-        const Anchor a = anc[m];  // wave-uniform address
-        const float2 p = (tid == 0) ? make_float2(a.a_re, a.a_im) : cmul_rn(a.q_re, a.q_im, er, ei);
-        const float2 tt = cmul_rn(x.x, x.y, p.x, p.y);  // in_common[n] * phase
+    const int last_blk = (ch.len - 1) >> 8;  // last 256-sample block of the chunk (chunk-uniform)
 
-        // code resampler, generic association order: ((step*n) + shift) - rem
-        const float sn = __fmul_rn(job.code_step, static_cast<float>(n));
+    // Software pipeline over groups of kGroup samples per lane: the loads of group g+1 are in
+    // flight while group g is correlated.  Lanes past the chunk end read sample 0 of the chunk and
+    // contribute zero.
+    constexpr int kGroup = 4;
+    constexpr int kGroups = kCorrSamplesPerThread / kGroup;
+    auto load_group = [&](int g, f2 (&dstx)[kGroup]) {
 #pragma unroll
-        for (int t = 0; t < NT; t++) {
-            int idx = static_cast<int>(floorf(__fsub_rn(__fadd_rn(sn, shifts[t]), job.rem_code)));
-            if (static_cast<unsigned>(idx) >= static_cast<unsigned>(L)) {
-                idx %= L;
-                if (idx < 0) idx += L;
-            }
-            const float cv = lds_code[idx];
-            acc[2 * t] = __fmaf_rn(tt.x, cv, acc[2 * t]);
-            acc[2 * t + 1] = __fmaf_rn(tt.y, cv, acc[2 * t + 1]);
+        for (int u = 0; u < kGroup; u++) {
+            const int r = tid + (g * kGroup + u) * kCorrThreads;
+            const float2 v = load_sample<FMT>(samples, base + (r < ch.len ? r : 0));
+            dstx[u] = (r < ch.len) ? f2{v.x, v.y} : f2{0.0f, 0.0f};
         }
+    };
+    f2 xs[kGroup], xn[kGroup];
+    load_group(0, xs);
+#pragma unroll 1
+    for (int g = 0; g < kGroups; g++) {
+        if (g * kGroup * kCorrThreads >= ch.len) break;  // chunk-uniform: no lane has samples left
+        if (g + 1 < kGroups && (g + 1) * kGroup * kCorrThreads < ch.len) load_group(g + 1, xn);
+#pragma unroll
+        for (int u = 0; u < kGroup; u++) {
+            const int m = g * kGroup + u;
+            const int r = tid + m * kCorrThreads;
+            const int n = ch.start + (r < ch.len ? r : 0);  // the reference's loop counter (clamped tail)
+            const int mm = m < last_blk ? m : last_blk;     // chunk-uniform → scalar anchor load
+            const Anchor a = anc[mm];
+            // phasor at sample n: the anchor itself at j = 0, else q_k · E_j
+            const f2 p = (tid == 0) ? f2{a.a_re, a.a_im} : cmul_pk(f2{a.q_re, a.q_im}, e, esw);
+            const f2 tt = cmul_pk(xs[u], p, f2{-p.y, p.x});  // in_common[n] * phase
+            // code resampler, generic association order: ((step*n) + shift) - rem, each rounded
+            const float sn = __fmul_rn(job.code_step, static_cast<float>(n));
+#pragma unroll
+            for (int t = 0; t < NT; t++) {
+                int idx = static_cast<int>(floorf(__fsub_rn(__fadd_rn(sn, shifts[t]), job.rem_code)));
+                if constexpr (!IN_MARGIN) idx = wrap_index(idx, L);
+                const float cv = code[idx];
+                acc[t] = __builtin_elementwise_fma(tt, f2{cv, cv}, acc[t]);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < kGroup; u++) xs[u] = xn[u];
     }
 
     const int lane = tid & 63, wave = tid >> 6;
 #pragma unroll
-    for (int v = 0; v < 2 * NT; v++) {
-        const float w = wave_sum(acc[v]);
-        if (lane == 0) red[wave][v] = w;
+    for (int t = 0; t < NT; t++) {
+        const float wr = wave_sum(acc[t].x), wi = wave_sum(acc[t].y);
+        if (lane == 0) {
+            red[wave][2 * t] = wr;
+            red[wave][2 * t + 1] = wi;
+        }
     }
     __syncthreads();
     if (tid < 2 * kMaxTaps) {
@@ -158,28 +221,39 @@ __device__ __forceinline__ void corr_chunk(const void* __restrict__ samples, con
     }
 }
 
-template <int FMT>
-__global__ __launch_bounds__(kCorrThreads) void corr_batch_kernel(const void* __restrict__ samples, const DevJob* __restrict__ jobs,
-    const ChunkDesc* __restrict__ chunks, int n_chunks, const CodeDesc* __restrict__ codes, const Anchor* __restrict__ anchors,
-    float* __restrict__ partials, float* __restrict__ out)
+// One launch per chunk class (tap-count template × in-margin flag), so each kernel is compiled
+// for exactly its path and the register allocation is not the worst case over all variants.
+template <int FMT, int NT, bool IN_MARGIN>
+__global__ __launch_bounds__(kCorrThreads, kCorrWavesPerSimd) void corr_batch_kernel(const void* __restrict__ samples, const DevJob* __restrict__ jobs,
+    const ChunkDesc* __restrict__ chunks, int n_chunks, int chunk_base, const CodeDesc* __restrict__ codes,
+    const Anchor* __restrict__ anchors, float* __restrict__ partials, float* __restrict__ out)
 {
     extern __shared__ __attribute__((aligned(16))) float lds_code[];
-    const int ci = blockIdx.x;
+    // XCD-aware chunk order: workgroups are dealt round-robin over the 8 XCDs (b and b+8 share
+    // one), so give each XCD a CONTIGUOUS range of chunks.  Jobs arrive epoch-major, so the
+    // channels that read the same IF samples then share one XCD's L2 (bijective for any grid).
+    const int nb = static_cast<int>(gridDim.x);
+    const int b = blockIdx.x;
+    const int q = nb >> 3, rmd = nb & 7, x = b & 7;
+    const int ci = x * q + (x < rmd ? x : rmd) + (b >> 3);
     if (ci >= n_chunks) return;
     const ChunkDesc ch = chunks[ci];
     const DevJob job = jobs[ch.job];
     const CodeDesc cd = codes[job.code_id];
     const int L = cd.len;
-    for (int i = threadIdx.x; i < L; i += kCorrThreads) lds_code[i] = cd.ptr[i];
-    __syncthreads();
-    float* dst = (job.n_chunks == 1) ? out + static_cast<int64_t>(ch.job) * 2 * kMaxTaps
-                                     : partials + static_cast<int64_t>(ci) * 2 * kMaxTaps;
-    switch (job.n_taps) {
-    case 1: corr_chunk<FMT, 1>(samples, job, ch, anchors, lds_code, L, dst); break;
-    case 3: corr_chunk<FMT, 3>(samples, job, ch, anchors, lds_code, L, dst); break;
-    case 5: corr_chunk<FMT, 5>(samples, job, ch, anchors, lds_code, L, dst); break;
-    default: corr_chunk<FMT, kMaxTaps>(samples, job, ch, anchors, lds_code, L, dst); break;
+    // padded replica in LDS: lds[kCodeMargin + i] = code[i mod L] for i in [−kCodeMargin, L + kCodeMargin)
+    const int total = L + 2 * kCodeMargin;
+    for (int i = threadIdx.x; i < total; i += kCorrThreads) {
+        int src = i - kCodeMargin;
+        src = src < 0 ? src + L * ((-src + L - 1) / L) : src;
+        src = src % L;
+        lds_code[i] = cd.ptr[src];
     }
+    __syncthreads();
+    const float* code = lds_code + kCodeMargin;
+    float* dst = (job.n_chunks == 1) ? out + static_cast<int64_t>(ch.job) * 2 * kMaxTaps
+                                     : partials + static_cast<int64_t>(chunk_base + ci) * 2 * kMaxTaps;
+    corr_chunk<FMT, NT, IN_MARGIN>(samples, job, ch, anchors, code, L, dst);
 }
 
 // Sum the chunk partials of multi-chunk jobs, in chunk order.
@@ -196,8 +270,8 @@ __global__ void corr_reduce_kernel(const DevJob* __restrict__ jobs, int n_jobs, 
 }
 
 hipError_t launch_corr_batch(const void* samples, int fmt, const DevJob* jobs, int n_jobs, const ChunkDesc* chunks, int n_chunks,
-    const CodeDesc* codes, int max_code_len, bool any_multi_chunk, Anchor* anchors, float* partials, float* out, hipStream_t stream,
-    int stages)
+    const ChunkClass* classes, const CodeDesc* codes, int max_code_len, bool any_multi_chunk, Anchor* anchors, float* partials, float* out,
+    hipStream_t stream, int stages)
 {
     if (n_chunks <= 0) return hipSuccess;
     if (max_code_len < 1 || max_code_len > kMaxCodeLen) return hipErrorInvalidValue;
@@ -208,19 +282,36 @@ hipError_t launch_corr_batch(const void* samples, int fmt, const DevJob* jobs, i
         if (e != hipSuccess) return e;
     }
     if (!(stages & GNSSHIP_STAGE_CORRELATE)) return hipSuccess;
-    const size_t lds = (static_cast<size_t>(max_code_len) * sizeof(float) + 15) & ~static_cast<size_t>(15);
-    dim3 grid(n_chunks), block(kCorrThreads);
-    switch (fmt) {
-    case GNSSHIP_FMT_CF32:
-        hipLaunchKernelGGL(corr_batch_kernel<GNSSHIP_FMT_CF32>, grid, block, lds, stream, samples, jobs, chunks, n_chunks, codes, anchors, partials, out);
-        break;
-    case GNSSHIP_FMT_CI16:
-        hipLaunchKernelGGL(corr_batch_kernel<GNSSHIP_FMT_CI16>, grid, block, lds, stream, samples, jobs, chunks, n_chunks, codes, anchors, partials, out);
-        break;
-    case GNSSHIP_FMT_CI8:
-        hipLaunchKernelGGL(corr_batch_kernel<GNSSHIP_FMT_CI8>, grid, block, lds, stream, samples, jobs, chunks, n_chunks, codes, anchors, partials, out);
-        break;
-    default: return hipErrorInvalidValue;
+    const size_t lds = (static_cast<size_t>(max_code_len + 2 * kCodeMargin) * sizeof(float) + 15) & ~static_cast<size_t>(15);
+    for (int c = 0; c < kChunkClasses; c++) {
+        const int cnt = classes[c].count;
+        if (cnt <= 0) continue;
+        const ChunkDesc* cc = chunks + classes[c].start;
+        const int cb = classes[c].start;
+        dim3 grid(cnt), block(kCorrThreads);
+#define GNSSHIP_LAUNCH_CORR(F, NTV, MV) \
+    hipLaunchKernelGGL((corr_batch_kernel<F, NTV, MV>), grid, block, lds, stream, samples, jobs, cc, cnt, cb, codes, anchors, partials, out)
+#define GNSSHIP_LAUNCH_NT(F)                                                     \
+    switch (c) {                                                                 \
+    case 0: GNSSHIP_LAUNCH_CORR(F, 1, false); break;                             \
+    case 1: GNSSHIP_LAUNCH_CORR(F, 1, true); break;                              \
+    case 2: GNSSHIP_LAUNCH_CORR(F, 3, false); break;                             \
+    case 3: GNSSHIP_LAUNCH_CORR(F, 3, true); break;                              \
+    case 4: GNSSHIP_LAUNCH_CORR(F, 5, false); break;                             \
+    case 5: GNSSHIP_LAUNCH_CORR(F, 5, true); break;                              \
+    case 6: GNSSHIP_LAUNCH_CORR(F, kMaxTaps, false); break;                      \
+    default: GNSSHIP_LAUNCH_CORR(F, kMaxTaps, true); break;                      \
+    }
+        switch (fmt) {
+        case GNSSHIP_FMT_CF32: GNSSHIP_LAUNCH_NT(GNSSHIP_FMT_CF32); break;
+        case GNSSHIP_FMT_CI16: GNSSHIP_LAUNCH_NT(GNSSHIP_FMT_CI16); break;
+        case GNSSHIP_FMT_CI8: GNSSHIP_LAUNCH_NT(GNSSHIP_FMT_CI8); break;
+        default: return hipErrorInvalidValue;
+        }
+#undef GNSSHIP_LAUNCH_NT
+#undef GNSSHIP_LAUNCH_CORR
+        e = hipGetLastError();
+        if (e != hipSuccess) return e;
     }
     e = hipGetLastError();
     if (e != hipSuccess || !any_multi_chunk) return e;

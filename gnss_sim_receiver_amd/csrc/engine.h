@@ -13,7 +13,8 @@ constexpr int kMaxTaps = GNSSHIP_MAX_TAPS;
 constexpr int kCorrThreads = 256;        // one workgroup = 4 wave64
 constexpr int kCorrSamplesPerThread = 16;
 constexpr int kCorrChunk = kCorrThreads * kCorrSamplesPerThread;  // 4096 samples per workgroup
-constexpr int kMaxCodeLen = 16384;       // LDS budget for the local code replica (64 KiB)
+constexpr int kCorrWavesPerSimd = 4;     // ≥4 resident workgroups per CU (≤128 VGPRs)
+constexpr int kMaxCodeLen = 16384;       // LDS budget for the local code replica (64 KiB + margins)
 
 // A local code replica resident in HBM.
 struct CodeDesc {
@@ -42,9 +43,14 @@ struct DevJob {
     float log_mag_inc;      // log|phase_inc| (magnitude growth between renormalisations)
     float rem_code;         // rem_code_phase_chips  (float, as passed by the reference)
     float code_step;        // code_phase_step_chips
-    float pad1;
+    int32_t in_margin;      // 1: every chip index of the job lies in [−kCodeMargin, L + kCodeMargin)
     float shifts[kMaxTaps];
 };
+
+// The LDS copy of a code replica is padded with kCodeMargin wrapped chips on both sides, so chip
+// indices a few chips outside [0, L) — the usual case at epoch edges with early/late taps — need
+// no modulo.  Jobs that can leave the margin (checked on the host) take the general wrap path.
+constexpr int kCodeMargin = 32;
 
 // Rotator anchor of one 256-sample block k of a job: `a` = the phasor the reference multiplies
 // sample 256k by (before renormalising), `q` = a/|a| (the renormalised phasor it then rotates).
@@ -60,10 +66,23 @@ struct ChunkDesc {
 };
 
 // Launch the batched correlator: partials[chunk][2*kMaxTaps] then per-job reduction into out.
+// Chunks are grouped by class = 2·tap_class + in_margin, tap_class: 0 → 1 tap, 1 → ≤3, 2 → ≤5, 3 → ≤8;
+// each class is one kernel launch over chunks[start, start + count).
+constexpr int kChunkClasses = 8;
+struct ChunkClass {
+    int32_t start;
+    int32_t count;
+};
+inline int chunk_class(int n_taps, int in_margin)
+{
+    const int tc = n_taps <= 1 ? 0 : n_taps <= 3 ? 1 : n_taps <= 5 ? 2 : 3;
+    return 2 * tc + (in_margin ? 1 : 0);
+}
+
 // anchors: scratch of Σ ceil(n_j/256) Anchor entries, recomputed by every launch.
 hipError_t launch_corr_batch(const void* samples, int fmt, const DevJob* jobs, int n_jobs, const ChunkDesc* chunks, int n_chunks,
-    const CodeDesc* codes, int max_code_len, bool any_multi_chunk, Anchor* anchors, float* partials, float* out, hipStream_t stream,
-    int stages = GNSSHIP_STAGE_ANCHORS | GNSSHIP_STAGE_CORRELATE);
+    const ChunkClass* classes, const CodeDesc* codes, int max_code_len, bool any_multi_chunk, Anchor* anchors, float* partials, float* out,
+    hipStream_t stream, int stages = GNSSHIP_STAGE_ANCHORS | GNSSHIP_STAGE_CORRELATE);
 
 }  // namespace gnsship
 

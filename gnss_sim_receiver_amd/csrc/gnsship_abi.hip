@@ -63,7 +63,7 @@ int sync_code_table(gnsship_ctx* ctx)
 // The phasors are formed with the reference's float operations:
 //   phase_offset_as_complex = (cos(rem), -sin(rem))             cpu_multicorrelator_real_codes.cc:115
 //   phase_inc = std::exp(complex<float>(0, -phase_step_rad))     :123  (glibc cexpf → cosf/sinf)
-bool derive_job(const gnsship_corr_job& in, DevJob& out)
+bool derive_job(const gnsship_corr_job& in, int code_len, DevJob& out)
 {
     if (in.n_samples < 0 || in.n_taps < 1 || in.n_taps > kMaxTaps || in.sample_offset < 0) return false;
     if (in.flags & 1) return false;  // high-dynamics variants: not on the device path yet
@@ -81,14 +81,25 @@ bool derive_job(const gnsship_corr_job& in, DevJob& out)
     out.log_mag_inc = static_cast<float>(std::log(std::hypot(static_cast<double>(incr), static_cast<double>(inci))));
     out.rem_code = in.rem_code_phase_chips;
     out.code_step = in.code_phase_step_chips;
-    out.pad1 = 0.0f;
     for (int t = 0; t < kMaxTaps; t++) out.shifts[t] = (t < in.n_taps) ? in.shifts_chips[t] : 0.0f;
+    // Range of floor(step·n + shift − rem) over the job, bounded in double with 2 chips of slack
+    // (each float rounding moves a value < 2^15 by far less than one chip): inside the padded
+    // LDS replica the kernel skips the modulo.
+    double smin = in.shifts_chips[0], smax = in.shifts_chips[0];
+    for (int t = 1; t < in.n_taps; t++) {
+        smin = std::min(smin, static_cast<double>(in.shifts_chips[t]));
+        smax = std::max(smax, static_cast<double>(in.shifts_chips[t]));
+    }
+    const double span = static_cast<double>(in.code_phase_step_chips) * static_cast<double>(in.n_samples > 0 ? in.n_samples - 1 : 0);
+    const double lo = std::min(0.0, span) + smin - in.rem_code_phase_chips - 2.0;
+    const double hi = std::max(0.0, span) + smax - in.rem_code_phase_chips + 2.0;
+    out.in_margin = (std::isfinite(lo) && std::isfinite(hi) && lo >= -kCodeMargin && hi < static_cast<double>(code_len + kCodeMargin)) ? 1 : 0;
     return true;
 }
 
 // Split jobs into ≤kCorrChunk-sample chunks and lay out their rotator anchors; returns the
 // number of chunks, total anchors in *n_anchors.
-int plan_chunks(std::vector<DevJob>& jobs, std::vector<ChunkDesc>& chunks, bool& any_multi, int64_t* n_anchors)
+int plan_chunks(std::vector<DevJob>& jobs, std::vector<ChunkDesc>& chunks, bool& any_multi, int64_t* n_anchors, ChunkClass* classes)
 {
     chunks.clear();
     any_multi = false;
@@ -97,19 +108,27 @@ int plan_chunks(std::vector<DevJob>& jobs, std::vector<ChunkDesc>& chunks, bool&
         const int n = jobs[j].n_samples;
         jobs[j].anchor_offset = static_cast<int32_t>(anchors);
         anchors += (n + kRenorm - 1) / kRenorm;
-        const int nc = n <= 0 ? 1 : (n + kCorrChunk - 1) / kCorrChunk;
-        jobs[j].n_chunks = nc;
-        jobs[j].first_chunk = static_cast<int32_t>(chunks.size());
-        if (nc > 1) any_multi = true;
-        for (int c = 0; c < nc; c++) {
-            ChunkDesc d;
-            d.job = static_cast<int32_t>(j);
-            d.start = c * kCorrChunk;
-            const int rem = n - d.start;
-            d.len = rem < kCorrChunk ? (rem > 0 ? rem : 0) : kCorrChunk;
-            d.pad = 0;
-            chunks.push_back(d);
+        jobs[j].n_chunks = n <= 0 ? 1 : (n + kCorrChunk - 1) / kCorrChunk;
+        if (jobs[j].n_chunks > 1) any_multi = true;
+    }
+    // chunks grouped by class (one launch each), job order kept inside a class
+    for (int c = 0; c < kChunkClasses; c++) {
+        classes[c].start = static_cast<int32_t>(chunks.size());
+        for (size_t j = 0; j < jobs.size(); j++) {
+            if (chunk_class(jobs[j].n_taps, jobs[j].in_margin) != c) continue;
+            const int n = jobs[j].n_samples;
+            jobs[j].first_chunk = static_cast<int32_t>(chunks.size());
+            for (int k = 0; k < jobs[j].n_chunks; k++) {
+                ChunkDesc d;
+                d.job = static_cast<int32_t>(j);
+                d.start = k * kCorrChunk;
+                const int rem = n - d.start;
+                d.len = rem < kCorrChunk ? (rem > 0 ? rem : 0) : kCorrChunk;
+                d.pad = 0;
+                chunks.push_back(d);
+            }
         }
+        classes[c].count = static_cast<int32_t>(chunks.size()) - classes[c].start;
     }
     *n_anchors = anchors > 0 ? anchors : 1;
     return static_cast<int>(chunks.size());
@@ -285,6 +304,7 @@ struct gnsship_batch {
     int n_chunks = 0;
     int max_code_len = 1;
     bool any_multi = false;
+    ChunkClass classes[kChunkClasses] = {};
     int chunk_cap = 0;
     DevJob* jobs_dev = nullptr;
     ChunkDesc* chunks_dev = nullptr;
@@ -327,15 +347,16 @@ extern "C" int gnsship_batch_set_jobs(gnsship_batch* b, const gnsship_corr_job* 
     int max_len = 1;
     for (int j = 0; j < n_jobs; j++) {
         const gnsship_corr_job& in = jobs[j];
-        if (!derive_job(in, b->jobs_host[j])) return fail(ctx, GNSSHIP_E_INVAL, "gnsship_batch_set_jobs: invalid job (taps, length, offset or flags)");
         if (in.code_id < 0 || in.code_id >= static_cast<int>(ctx->codes_host.size()) || !ctx->codes_host[in.code_id].ptr)
             return fail(ctx, GNSSHIP_E_INVAL, "gnsship_batch_set_jobs: job refers to an unset code id");
+        if (!derive_job(in, ctx->codes_host[in.code_id].len, b->jobs_host[j]))
+            return fail(ctx, GNSSHIP_E_INVAL, "gnsship_batch_set_jobs: invalid job (taps, length, offset or flags)");
         if (in.sample_offset + in.n_samples > n_buffer_samples) return fail(ctx, GNSSHIP_E_INVAL, "gnsship_batch_set_jobs: job reads past the sample buffer");
         if (ctx->codes_host[in.code_id].len > max_len) max_len = ctx->codes_host[in.code_id].len;
     }
     b->max_code_len = max_len;
     int64_t n_anchors = 0;
-    b->n_chunks = plan_chunks(b->jobs_host, b->chunks_host, b->any_multi, &n_anchors);
+    b->n_chunks = plan_chunks(b->jobs_host, b->chunks_host, b->any_multi, &n_anchors, b->classes);
     if (n_anchors > b->anchor_cap) {
         if (b->anchors_dev) HIP_TRY(ctx, hipFree(b->anchors_dev));
         b->anchors_dev = nullptr;
@@ -373,7 +394,7 @@ extern "C" int gnsship_batch_launch_stages(gnsship_batch* b, const void* dev_sam
     if (!dev_samples && b->n_jobs) return fail(ctx, GNSSHIP_E_INVAL, "gnsship_batch_launch: null sample buffer");
     if (b->n_jobs == 0) return GNSSHIP_OK;
     if (ctx->codes_dirty) return fail(ctx, GNSSHIP_E_STATE, "gnsship_batch_launch: code bank changed after set_jobs");
-    hipError_t e = launch_corr_batch(dev_samples, fmt, b->jobs_dev, b->n_jobs, b->chunks_dev, b->n_chunks, ctx->codes_dev, b->max_code_len,
+    hipError_t e = launch_corr_batch(dev_samples, fmt, b->jobs_dev, b->n_jobs, b->chunks_dev, b->n_chunks, b->classes, ctx->codes_dev, b->max_code_len,
         b->any_multi, b->anchors_dev, b->partials_dev, b->out_dev, ctx->stream, stages);
     if (e != hipSuccess) return hip_fail(ctx, e, "launch_corr_batch");
     return GNSSHIP_OK;
@@ -513,11 +534,12 @@ extern "C" int gnsship_corr_run(gnsship_corr* c, const void* sig, int fmt, int s
     in.code_phase_rate_step_chips = code_rate_step;
     for (int t = 0; t < kMaxTaps; t++) in.shifts_chips[t] = t < c->n_taps ? c->shifts[t] : 0.0f;
     std::vector<DevJob> jobs(1);
-    if (!derive_job(in, jobs[0])) return fail(ctx, GNSSHIP_E_INVAL, "gnsship_corr_run: invalid job");
+    if (!derive_job(in, c->code_len, jobs[0])) return fail(ctx, GNSSHIP_E_INVAL, "gnsship_corr_run: invalid job");
     std::vector<ChunkDesc> chunks;
     bool multi = false;
     int64_t n_anchors = 0;
-    const int nch = plan_chunks(jobs, chunks, multi, &n_anchors);
+    ChunkClass classes[kChunkClasses];
+    const int nch = plan_chunks(jobs, chunks, multi, &n_anchors, classes);
     const void* src = sig;
     if (!sig_on_device) {
         HIP_TRY(ctx, hipMemcpyAsync(c->sig_dev, sig, fmt_bytes(fmt) * static_cast<size_t>(n), hipMemcpyHostToDevice, ctx->stream));
@@ -525,7 +547,7 @@ extern "C" int gnsship_corr_run(gnsship_corr* c, const void* sig, int fmt, int s
     }
     HIP_TRY(ctx, hipMemcpyAsync(c->job_dev, jobs.data(), sizeof(DevJob), hipMemcpyHostToDevice, ctx->stream));
     HIP_TRY(ctx, hipMemcpyAsync(c->chunks_dev, chunks.data(), sizeof(ChunkDesc) * nch, hipMemcpyHostToDevice, ctx->stream));
-    hipError_t e = launch_corr_batch(src, fmt, c->job_dev, 1, c->chunks_dev, nch, c->code_table_dev, c->code_len, multi, c->anchors_dev,
+    hipError_t e = launch_corr_batch(src, fmt, c->job_dev, 1, c->chunks_dev, nch, classes, c->code_table_dev, c->code_len, multi, c->anchors_dev,
         c->partials_dev, c->out_dev, ctx->stream);
     if (e != hipSuccess) return hip_fail(ctx, e, "launch_corr_batch");
     float tmp[2 * kMaxTaps];
