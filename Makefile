@@ -34,3 +34,10 @@ clean:
 	$(MAKE) -s -C oracle clean
 
 .PHONY: all oracle clean
+
+# C++ mirror-class test (links the product library and, as the checker, the oracle source)
+MIRROR_TEST := tests/cpp/mirror_test
+$(MIRROR_TEST): tests/cpp/mirror_test.cpp include/gnsship_cpp.hpp include/gnsship.h oracle/gnss_oracle.c $(LIB)
+	gcc -O2 -fPIC -ffp-contract=off -std=gnu11 -c oracle/gnss_oracle.c -o build/gnss_oracle_test.o
+	g++ -O2 -std=c++17 -Iinclude tests/cpp/mirror_test.cpp build/gnss_oracle_test.o -o $@ -L$(PKG) -lgnsship -Wl,-rpath,'$$ORIGIN/../../$(PKG)' -lpthread -lm
+all: $(MIRROR_TEST)

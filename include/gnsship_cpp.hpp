@@ -1,0 +1,299 @@
+// gnsship_cpp.hpp — header-only C++ mirror of the reference's engine classes, on top of the C ABI
+// (include/gnsship.h).  A GNSS-SDR adapter swaps
+//   Cpu_Multicorrelator_Real_Codes  → gnsship::Hip_Multicorrelator_Real_Codes
+//   pcps_acquisition's FFT core     → gnsship::Pcps_Acquisition_Hip
+// keeping method names, argument meaning and the reference's error behaviour (bool returns;
+// configuration errors throw std::invalid_argument like Acq_Conf::SetFromConfiguration,
+// acq_conf.cc:28-31).  Only the C ABI crosses the shared-library boundary.
+#ifndef GNSSHIP_CPP_HPP
+#define GNSSHIP_CPP_HPP
+
+#include <cmath>
+#include <complex>
+#include <cstdint>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "gnsship.h"
+
+namespace gnsship {
+
+// One context (device + stream + code bank) per device, shared by every channel of a process.
+class Device {
+public:
+    static std::shared_ptr<Device> get(int device = 0)
+    {
+        static std::mutex mu;
+        static std::map<int, std::weak_ptr<Device>> live;
+        std::lock_guard<std::mutex> lk(mu);
+        auto sp = live[device].lock();
+        if (!sp) {
+            sp = std::shared_ptr<Device>(new Device(device));
+            live[device] = sp;
+        }
+        return sp;
+    }
+    ~Device()
+    {
+        if (ctx_) gnsship_ctx_destroy(ctx_);
+    }
+    gnsship_ctx* ctx() const { return ctx_; }
+    std::mutex& mutex() { return mu_; }  // serialises calls that share the context stream
+
+private:
+    explicit Device(int device)
+    {
+        if (gnsship_ctx_create(device, &ctx_) != GNSSHIP_OK) throw std::runtime_error("gnsship: no HIP device " + std::to_string(device));
+    }
+    gnsship_ctx* ctx_ = nullptr;
+    std::mutex mu_;
+};
+
+// Mirror of Cpu_Multicorrelator_Real_Codes (src/algorithms/tracking/libs/cpu_multicorrelator_real_codes.h:37-61).
+class Hip_Multicorrelator_Real_Codes {
+public:
+    explicit Hip_Multicorrelator_Real_Codes(int device = 0) : dev_(Device::get(device)) {}
+    ~Hip_Multicorrelator_Real_Codes() { free(); }
+    Hip_Multicorrelator_Real_Codes(const Hip_Multicorrelator_Real_Codes&) = delete;
+    Hip_Multicorrelator_Real_Codes& operator=(const Hip_Multicorrelator_Real_Codes&) = delete;
+
+    void set_high_dynamics_resampler(bool use_high_dynamics_resampler)
+    {
+        high_dyn_ = use_high_dynamics_resampler;
+        if (h_) gnsship_corr_set_high_dynamics_resampler(h_, high_dyn_ ? 1 : 0);
+    }
+    bool init(int max_signal_length_samples, int n_correlators)
+    {
+        std::lock_guard<std::mutex> lk(dev_->mutex());
+        free_locked();
+        n_ = n_correlators;
+        if (gnsship_corr_create(dev_->ctx(), max_signal_length_samples, n_correlators, &h_) != GNSSHIP_OK) return false;
+        gnsship_corr_set_high_dynamics_resampler(h_, high_dyn_ ? 1 : 0);
+        return true;
+    }
+    // The reference borrows the pointers (:53-63); the device engine copies the code at this call.
+    bool set_local_code_and_taps(int code_length_chips, const float* local_code_in, float* shifts_chips)
+    {
+        if (!h_) return false;
+        std::lock_guard<std::mutex> lk(dev_->mutex());
+        return gnsship_corr_set_local_code_and_taps(h_, code_length_chips, local_code_in, shifts_chips) == GNSSHIP_OK;
+    }
+    bool set_input_output_vectors(std::complex<float>* corr_out, const std::complex<float>* sig_in)
+    {
+        out_ = corr_out;
+        in_ = sig_in;
+        return true;
+    }
+    bool Carrier_wipeoff_multicorrelator_resampler(float rem_carrier_phase_in_rad, float phase_step_rad, float phase_rate_step_rad,
+        float rem_code_phase_chips, float code_phase_step_chips, float code_phase_rate_step_chips, int signal_length_samples)
+    {
+        if (!h_ || !out_ || !in_) return false;
+        std::vector<float> tmp(2 * static_cast<size_t>(n_));
+        int rc;
+        {
+            std::lock_guard<std::mutex> lk(dev_->mutex());
+            rc = gnsship_corr_run(h_, in_, GNSSHIP_FMT_CF32, 0, rem_carrier_phase_in_rad, phase_step_rad, phase_rate_step_rad, rem_code_phase_chips,
+                code_phase_step_chips, code_phase_rate_step_chips, signal_length_samples, tmp.data());
+        }
+        if (rc != GNSSHIP_OK) return false;
+        for (int t = 0; t < n_; t++) out_[t] = std::complex<float>(tmp[2 * t], tmp[2 * t + 1]);
+        return true;
+    }
+    bool Carrier_wipeoff_multicorrelator_resampler(float rem_carrier_phase_in_rad, float phase_step_rad, float rem_code_phase_chips,
+        float code_phase_step_chips, float code_phase_rate_step_chips, int signal_length_samples)
+    {
+        return Carrier_wipeoff_multicorrelator_resampler(rem_carrier_phase_in_rad, phase_step_rad, 0.0F, rem_code_phase_chips,
+            code_phase_step_chips, code_phase_rate_step_chips, signal_length_samples);
+    }
+    bool free()
+    {
+        std::lock_guard<std::mutex> lk(dev_->mutex());
+        free_locked();
+        return true;
+    }
+    const char* last_error() const { return gnsship_last_error(dev_->ctx()); }
+
+private:
+    void free_locked()
+    {
+        if (h_) gnsship_corr_destroy(h_);
+        h_ = nullptr;
+    }
+    std::shared_ptr<Device> dev_;
+    gnsship_corr* h_ = nullptr;
+    int n_ = 0;
+    bool high_dyn_ = false;  // Dll_Pll_Conf::high_dyn default (dll_pll_conf.h:80)
+    std::complex<float>* out_ = nullptr;
+    const std::complex<float>* in_ = nullptr;
+};
+
+// Mirror of the Acq_Conf fields the PCPS core reads (src/algorithms/acquisition/libs/acq_conf.h:33-81)
+// with SetDerivedParams (acq_conf.cc:113-118).
+struct Acq_Conf {
+    int64_t fs_in{4000000LL};
+    float doppler_step{250.0};
+    float pfa{0.0};
+    uint32_t sampled_ms{1U};
+    uint32_t ms_per_code{1U};
+    uint32_t chips_per_second{1023000U};
+    uint32_t max_dwells{1U};
+    int32_t doppler_max{5000};
+    bool bit_transition_flag{false};
+    bool use_CFAR_algorithm_flag{true};
+    // derived
+    float samples_per_ms{0.0};
+    float samples_per_code{0.0};
+    uint32_t samples_per_chip{2U};
+    void SetDerivedParams()
+    {
+        if (pfa < 0.0F || pfa > 1.0F) pfa = 0.0F;       // acq_conf.cc:63-67
+        if (pfa <= 0.0F) use_CFAR_algorithm_flag = false;  // :75-79
+        if (bit_transition_flag) throw std::invalid_argument("gnsship: bit_transition_flag is not supported by the HIP PCPS core yet");
+        samples_per_ms = static_cast<float>(fs_in) * 0.001F;
+        samples_per_chip = static_cast<unsigned int>(std::ceil(static_cast<float>(fs_in) / static_cast<float>(chips_per_second)));
+        samples_per_code = samples_per_ms * static_cast<float>(ms_per_code);
+    }
+};
+
+// What acquisition_core writes into Gnss_Synchro (gnss_synchro.h:52-55; pcps_acquisition.cc:683-696).
+struct Acq_Outcome {
+    double Acq_delay_samples{0.0};
+    double Acq_doppler_hz{0.0};
+    uint64_t Acq_samplestamp_samples{0};
+    uint32_t Acq_doppler_step{0};
+    float test_statistics{0.0F};
+    float input_power{0.0F};
+    float peak{0.0F};
+    bool positive{false};
+};
+
+// Regularised lower incomplete gamma P(a, x) for integer a ≥ 1 and its inverse (Newton), the
+// boost::math::gamma_p_inv call of pcps_acquisition::calculate_threshold (pcps_acquisition.cc:884-899).
+inline double gamma_p_int(int a, double x)
+{
+    double term = 1.0, sum = 1.0;
+    for (int k = 1; k < a; k++) {
+        term *= x / k;
+        sum += term;
+    }
+    return 1.0 - std::exp(-x) * sum;
+}
+inline double gamma_p_inv_int(int a, double p)
+{
+    if (p <= 0.0) return 0.0;
+    if (p >= 1.0) return INFINITY;
+    // Q = 1 - p is tiny for CFAR thresholds; iterate on log Q for accuracy.
+    const double logq = std::log1p(-p);
+    double x = std::max(1.0, a - logq);
+    for (int it = 0; it < 100; it++) {
+        double term = 1.0, sum = 1.0;
+        for (int k = 1; k < a; k++) {
+            term *= x / k;
+            sum += term;
+        }
+        const double lq = -x + std::log(sum);  // log Q(a, x)
+        double lterm = 1.0;
+        for (int k = 1; k < a; k++) lterm *= x / k;  // x^{a-1}/(a-1)!
+        const double dlq = -lterm / sum;  // d log Q / dx
+        const double step = (lq - logq) / dlq;
+        x -= step;
+        if (x <= 0.0) x = 1e-12;
+        if (std::fabs(step) < 1e-13 * std::max(1.0, x)) break;
+    }
+    return x;
+}
+
+// Mirror of the engine part of pcps_acquisition (pcps_acquisition.cc): set_local_code, init (Doppler
+// grid), set_doppler_*, set_threshold, calculate_threshold, acquisition_core over one buffer.
+class Pcps_Acquisition_Hip {
+public:
+    explicit Pcps_Acquisition_Hip(const Acq_Conf& conf, int device = 0) : conf_(conf), dev_(Device::get(device))
+    {
+        conf_.SetDerivedParams();
+        fft_size_ = static_cast<int>(conf_.sampled_ms * static_cast<uint32_t>(conf_.samples_per_ms));  // :71, :84-91
+        gnsship_acq_conf c{};
+        c.fs_in = conf_.fs_in;
+        c.fft_size = fft_size_;
+        c.doppler_max = conf_.doppler_max;
+        c.doppler_step = static_cast<int32_t>(conf_.doppler_step);
+        c.doppler_center = 0;
+        c.max_dwells = static_cast<int32_t>(conf_.max_dwells);
+        c.use_cfar = conf_.use_CFAR_algorithm_flag ? 1 : 0;
+        c.samples_per_chip = static_cast<int32_t>(conf_.samples_per_chip);
+        c.samples_per_code = conf_.samples_per_code;
+        c.max_prns = 1;
+        std::lock_guard<std::mutex> lk(dev_->mutex());
+        if (gnsship_acq_create(dev_->ctx(), &c, &h_) != GNSSHIP_OK)
+            throw std::invalid_argument(std::string("gnsship_acq_create: ") + gnsship_last_error(dev_->ctx()));
+    }
+    ~Pcps_Acquisition_Hip()
+    {
+        if (h_) gnsship_acq_destroy(h_);
+    }
+    int fft_size() const { return fft_size_; }
+    void set_threshold(float threshold) { threshold_ = threshold; }
+    void set_doppler_max(uint32_t doppler_max) { conf_.doppler_max = static_cast<int32_t>(doppler_max); }
+    void set_doppler_step(uint32_t doppler_step) { doppler_step_ = doppler_step; }
+    void set_doppler_center(int32_t doppler_center) { doppler_center_ = doppler_center; }
+    // set_local_code (:175-208): FFT of the sampled code + conjugate, on the device
+    bool set_local_code(const std::complex<float>* code)
+    {
+        std::lock_guard<std::mutex> lk(dev_->mutex());
+        return gnsship_acq_set_local_code(h_, 0, reinterpret_cast<const float*>(code)) == GNSSHIP_OK;
+    }
+    // init (:248-292): rebuild the Doppler wipeoff grid for the current max/step/center
+    bool init()
+    {
+        std::lock_guard<std::mutex> lk(dev_->mutex());
+        const int step = doppler_step_ ? static_cast<int>(doppler_step_) : static_cast<int>(conf_.doppler_step);
+        if (gnsship_acq_set_grid(h_, conf_.doppler_max, step, doppler_center_) != GNSSHIP_OK) return false;
+        calculate_threshold();
+        return true;
+    }
+    // calculate_threshold (:884-899)
+    void calculate_threshold()
+    {
+        if (conf_.pfa <= 0.0F) return;
+        int nb = 0;
+        gnsship_acq_num_bins(h_, &nb);
+        const int num_bins = fft_size_ * nb;
+        threshold_ = static_cast<float>(2.0 * gamma_p_inv_int(2 * static_cast<int>(conf_.max_dwells),
+                                                  std::pow(1.0 - conf_.pfa, 1.0 / static_cast<float>(num_bins))));
+    }
+    float threshold() const { return threshold_; }
+    // acquisition_core (:600-871) over fft_size gr_complex samples (one dwell)
+    bool acquisition_core(const std::complex<float>* in, uint64_t samp_count, Acq_Outcome& out)
+    {
+        gnsship_acq_result r{};
+        {
+            std::lock_guard<std::mutex> lk(dev_->mutex());
+            if (gnsship_acq_run(h_, in, GNSSHIP_FMT_CF32, 0, 1, &r, nullptr) != GNSSHIP_OK) return false;
+        }
+        out.Acq_delay_samples = r.acq_delay_samples;
+        out.Acq_doppler_hz = static_cast<double>(r.doppler_hz);
+        out.Acq_samplestamp_samples = samp_count;
+        out.test_statistics = r.test_statistic;
+        out.input_power = r.input_power;
+        out.peak = r.peak;
+        out.positive = r.test_statistic > threshold_;  // :765-816 (step one, no bit-transition)
+        return true;
+    }
+    const char* last_error() const { return gnsship_last_error(dev_->ctx()); }
+
+private:
+    Acq_Conf conf_;
+    std::shared_ptr<Device> dev_;
+    gnsship_acq* h_ = nullptr;
+    int fft_size_ = 0;
+    float threshold_ = 0.0F;
+    uint32_t doppler_step_ = 0;
+    int32_t doppler_center_ = 0;
+};
+
+}  // namespace gnsship
+
+#endif  // GNSSHIP_CPP_HPP

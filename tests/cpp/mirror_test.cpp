@@ -1,0 +1,156 @@
+// tests/cpp/mirror_test.cpp — C++ parity test of the header-only mirror classes
+// (include/gnsship_cpp.hpp) against the CPU oracle (oracle/gnss_oracle.c, linked in: test code only).
+// Structured like the reference's tracking-lib tests
+// (src/tests/unit-tests/signal-processing-blocks/tracking/cpu_multicorrelator_real_codes_test.cc:54-160):
+// random uniform input, N in {2048, 4096, 8192}, 1..12 concurrent threads each owning a correlator,
+// but with the outputs CHECKED (the reference's test only times them).
+//   mirror_test corr   — correlator parity (exit 0 on pass)
+//   mirror_test acq    — PCPS acquisition peak parity vs a direct-DFT oracle
+//   mirror_test gamma  — prints calculate_threshold's gamma_p_inv for the CPU test (no GPU)
+#include <cmath>
+#include <complex>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <random>
+#include <thread>
+#include <vector>
+
+#include "gnsship_cpp.hpp"
+
+extern "C" {
+int orc_gps_l1_ca_code_gen_float(float* dest, int32_t prn, uint32_t chip_shift);
+int orc_gps_l1_ca_code_gen_complex_sampled(float* dest, uint32_t prn, int32_t sampling_freq, uint32_t chip_shift);
+int orc_multicorrelator_real_codes(float* corr_out, const float* sig_in, const float* local_code, int code_length_chips,
+    const float* shifts_chips, int n_correlators, int high_dyn, float rem_carrier_phase_in_rad, float phase_step_rad,
+    float phase_rate_step_rad, float rem_code_phase_chips, float code_phase_step_chips, float code_phase_rate_step_chips,
+    int signal_length_samples, float* scratch);
+void orc_doppler_wipeoff_grid(float* table, int n_bins, int fft_size, int doppler_max, int doppler_step, int doppler_center,
+    int doppler_bias, int64_t fs);
+}
+
+static int corr_test()
+{
+    const int sizes[] = {2048, 4096, 8192};
+    const int max_threads = 12;
+    float code[1023];
+    orc_gps_l1_ca_code_gen_float(code, 1, 0);
+    int failures = 0;
+    for (int n : sizes) {
+        for (int nt = 1; nt <= max_threads; nt += 11) {
+            std::vector<std::thread> th;
+            std::vector<double> worst(nt, 0.0);
+            for (int t = 0; t < nt; t++) {
+                th.emplace_back([&, t]() {
+                    std::mt19937 gen(1000 + 17 * t + n);
+                    std::uniform_real_distribution<float> u(-1.0F, 1.0F);
+                    std::vector<std::complex<float>> in(n);
+                    for (auto& v : in) v = std::complex<float>(u(gen), u(gen));
+                    float shifts[3] = {-0.5F, 0.0F, 0.5F};
+                    gnsship::Hip_Multicorrelator_Real_Codes mc;
+                    mc.init(n, 3);
+                    mc.set_local_code_and_taps(1023, code, shifts);
+                    std::complex<float> out[3];
+                    mc.set_input_output_vectors(out, in.data());
+                    for (int it = 0; it < 4; it++) {
+                        const float rem_carr = u(gen) * 3.14F, step = 0.01F * u(gen), rem_code = u(gen), code_step = 0.25575F + 0.0001F * u(gen);
+                        if (!mc.Carrier_wipeoff_multicorrelator_resampler(rem_carr, step, 0.0F, rem_code, code_step, 0.0F, n)) {
+                            worst[t] = 1e9;
+                            return;
+                        }
+                        float ref[6];
+                        orc_multicorrelator_real_codes(ref, reinterpret_cast<const float*>(in.data()), code, 1023, shifts, 3, 0, rem_carr, step, 0.0F,
+                            rem_code, code_step, 0.0F, n, nullptr);
+                        // noise-only input: relative to the accumulation scale ||x||_2
+                        double scale = 0.0;
+                        for (auto& v : in) scale += std::norm(std::complex<double>(v));
+                        scale = std::sqrt(scale);
+                        for (int k = 0; k < 3; k++) {
+                            const double e = std::abs(std::complex<double>(out[k]) - std::complex<double>(ref[2 * k], ref[2 * k + 1]));
+                            const double r = e / std::max(scale, std::abs(std::complex<double>(ref[2 * k], ref[2 * k + 1])));
+                            if (r > worst[t]) worst[t] = r;
+                        }
+                    }
+                    mc.free();
+                });
+            }
+            for (auto& x : th) x.join();
+            double w = 0;
+            for (double v : worst) w = std::max(w, v);
+            std::printf("corr N=%d threads=%d worst_rel_err=%.3e %s\n", n, nt, w, w <= 1e-5 ? "ok" : "FAIL");
+            if (!(w <= 1e-5)) failures++;
+        }
+    }
+    return failures;
+}
+
+static int acq_test()
+{
+    // fs = 2.048 Msps → fft_size 2048; PRN 12 at fD = -777 Hz, delay 1000 samples, 48 dB-Hz
+    gnsship::Acq_Conf conf;
+    conf.fs_in = 2048000;
+    conf.doppler_max = 5000;
+    conf.doppler_step = 500.0F;
+    conf.pfa = 0.01F;
+    gnsship::Pcps_Acquisition_Hip acq(conf);
+    const int n = acq.fft_size();
+    std::vector<float> code(2 * n);
+    orc_gps_l1_ca_code_gen_complex_sampled(code.data(), 12, 2048000, 0);
+    acq.set_local_code(reinterpret_cast<const std::complex<float>*>(code.data()));
+    acq.init();
+    std::mt19937 gen(7);
+    std::normal_distribution<double> g(0.0, 1.0);
+    std::vector<std::complex<float>> sig(n);
+    const double amp = std::sqrt(2 * std::pow(10.0, 4.8) / 2048000.0);
+    float chips[1023];
+    orc_gps_l1_ca_code_gen_float(chips, 12, 0);
+    for (int i = 0; i < n; i++) {
+        const double t = i / 2048000.0;
+        const long c = static_cast<long>(std::floor((i - 1000) / 2048000.0 * 1023000.0 * (1 - 777.0 / 1575.42e6)));
+        const double cv = chips[((c % 1023) + 1023) % 1023];
+        sig[i] = std::complex<float>(amp * cv * std::cos(2 * M_PI * -777.0 * t) + g(gen), amp * cv * std::sin(2 * M_PI * -777.0 * t) + g(gen));
+    }
+    gnsship::Acq_Outcome out;
+    if (!acq.acquisition_core(sig.data(), 123456, out)) return 1;
+    // direct-DFT oracle of the |IFFT(FFT(x w) conj(FFT(c)))|² grid = circular cross-correlation
+    const int nb = 20;
+    std::vector<float> w(2 * static_cast<size_t>(nb) * n);
+    orc_doppler_wipeoff_grid(w.data(), nb, n, 5000, 500, 0, 0, 2048000);
+    double best = -1;
+    int bb = 0, bi = 0;
+    for (int b = 0; b < nb; b++) {
+        std::vector<std::complex<double>> x(n);
+        for (int i = 0; i < n; i++) {
+            const std::complex<float> wf(w[2 * (static_cast<size_t>(b) * n + i)], w[2 * (static_cast<size_t>(b) * n + i) + 1]);
+            x[i] = std::complex<double>(sig[i] * wf);
+        }
+        for (int tau = 0; tau < n; tau++) {
+            std::complex<double> acc = 0;
+            for (int i = 0; i < n; i++) acc += x[(i + tau) % n] * std::complex<double>(code[2 * i], -code[2 * i + 1]);
+            const double v = std::norm(acc);
+            if (v > best) {
+                best = v;
+                bb = b;
+                bi = tau;
+            }
+        }
+    }
+    const double fd = -5000 + 500 * bb;
+    std::printf("acq gpu: delay %.1f doppler %.1f stat %.2f thr %.2f positive %d | oracle: delay %d doppler %.1f\n", out.Acq_delay_samples,
+        out.Acq_doppler_hz, out.test_statistics, acq.threshold(), out.positive ? 1 : 0, bi, fd);
+    return (static_cast<int>(out.Acq_delay_samples) == bi && out.Acq_doppler_hz == fd && out.positive && out.Acq_samplestamp_samples == 123456) ? 0 : 1;
+}
+
+int main(int argc, char** argv)
+{
+    const char* mode = argc > 1 ? argv[1] : "corr";
+    if (!std::strcmp(mode, "gamma")) {
+        const int as[] = {2, 4, 6};
+        const double ps[] = {0.5, 0.9, 0.999, 1.0 - 1e-6, 1.0 - 3.125e-8};
+        for (int a : as)
+            for (double p : ps) std::printf("%d %.17g %.17g\n", a, p, gnsship::gamma_p_inv_int(a, p));
+        return 0;
+    }
+    if (!std::strcmp(mode, "acq")) return acq_test();
+    return corr_test();
+}
