@@ -6,7 +6,10 @@ CSRC := $(PKG)/csrc
 HIP_SRCS := $(wildcard $(CSRC)/*.hip)
 CPP_SRCS := $(wildcard $(CSRC)/*.cpp)
 HDRS := $(wildcard $(CSRC)/*.h) include/gnsship.h
-HIPFLAGS := --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 -Iinclude -I$(CSRC) -Wall -Wno-unused-result
+# -ffp-contract=off: no implicit fusion anywhere (the HIP header intrinsics __fmul_rn/__fadd_rn
+# carry contract flags and were fused into v_fma_f32 otherwise, breaking the bit-exact chip index);
+# fused multiply-adds are written explicitly where wanted.
+HIPFLAGS := --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 -ffp-contract=off -Iinclude -I$(CSRC) -Wall -Wno-unused-result
 LIB := $(PKG)/libgnsship.so
 OBJDIR := build/obj
 

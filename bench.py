@@ -134,13 +134,18 @@ def main():
         if world == 1 and args.gpus > 1:
             raise SystemExit("--gpus N>1 must be launched with torch.distributed.run (one process per GPU)")
     torch = None
+    device = local_rank
     if world > 1:
         import torch
         import torch.distributed as dist
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl")
+        # GNSSHIP_DIST_BACKEND=gloo + several ranks per GPU rehearses the multi-rank flow on a
+        # one-GPU box (RCCL refuses two ranks on one device); the production path is nccl (RCCL).
+        backend = os.environ.get("GNSSHIP_DIST_BACKEND", "nccl")
+        device = local_rank % max(1, torch.cuda.device_count()) if backend != "nccl" else local_rank
+        torch.cuda.set_device(device)
+        dist.init_process_group(backend)
 
-    ctx = engine.Context(local_rank)
+    ctx = engine.Context(device)
     sats = None
     if rank == 0:
         sats, block, n_samples = build_block(args.seconds)
@@ -150,29 +155,57 @@ def main():
         n_samples = int(round(FS * args.seconds)) + 2 * VL
         block = None
 
-    # IF block resident in HBM
+    # IF block resident in HBM.  Multi-GPU: two device buffers, so that the RCCL broadcast of block
+    # k+1 (on the communicator's stream) overlaps the correlation of block k (engine stream).
     if torch is not None:
-        dev_t = torch.empty(n_samples, dtype=torch.complex64, device=f"cuda:{local_rank}")
+        dev_ts = [torch.empty(n_samples, dtype=torch.complex64, device=f"cuda:{device}") for _ in range(2)]
         if rank == 0:
-            dev_t.copy_(torch.from_numpy(block))
-        sharding.broadcast_block(dev_t, src=0)
+            for t in dev_ts:
+                t.copy_(torch.from_numpy(block))
+        for t in dev_ts:
+            sharding.broadcast_block(t, src=0)
         torch.cuda.synchronize()
-        dev_ptr = dev_t.data_ptr()
+        dev_ptrs = [t.data_ptr() for t in dev_ts]
     else:
         dev_buf = ctx.upload(block)
-        dev_ptr = dev_buf.ptr
+        dev_ptrs = [dev_buf.ptr, dev_buf.ptr]
+    dev_ptr = dev_ptrs[0]
 
-    jobs, codes = receiver_jobs(sats, rank, args.seconds)
-    for cid, c in enumerate(codes):
+    # Two 12-channel receivers per rank (channel sets 24r..24r+11 and 24r+12..24r+23, channel c
+    # tracking satellite c mod 32), stepped alternately: each step is one full receiver-second, and
+    # the NCO-only anchor replay of the next receiver's batch overlaps the current correlation.
+    receivers, all_codes = [], {}
+    for k in range(2):
+        jk, ck = receiver_jobs(sats, 2 * rank + k, args.seconds)
+        jk["code_id"] += 32 * k  # receiver k's code-bank entries live at 32·k + id
+        for cid, c in enumerate(ck):
+            all_codes[32 * k + cid] = c
+        receivers.append((jk, ck))
+    jobs, codes = receivers[0]  # receiver 0 (code ids unshifted): CPU baseline + roofline split
+    for cid, c in sorted(all_codes.items()):
         ctx.set_code(cid, c)
-    batch = engine.CorrelatorBatch(ctx, len(jobs))
-    batch.set_jobs(jobs, n_samples)
+    batches = []
+    for jk, _ in receivers:
+        b = engine.CorrelatorBatch(ctx, len(jk))
+        b.set_jobs(jk, n_samples)
+        batches.append(b)
+    batch = batches[0]
+
+    step_no = [0]
 
     def step():
-        if torch is not None:
-            sharding.broadcast_block(dev_t, src=0)   # RCCL fan-out of the IF block (exchange step)
-            torch.cuda.current_stream().synchronize()
-        batch.launch_ptr(dev_ptr, abi.FMT_CF32)
+        cur = step_no[0] & 1
+        step_no[0] += 1
+        b = batches[cur]
+        if torch is None:
+            b.launch_ptr(dev_ptrs[0], abi.FMT_CF32)
+            return
+        # exchange step: fan the NEXT block out to every rank while this one is correlated
+        work = sharding.broadcast_block(dev_ts[cur ^ 1], src=0, async_op=True)
+        b.launch_ptr(dev_ptrs[cur], abi.FMT_CF32)
+        ctx.sync()
+        work.wait()
+        torch.cuda.current_stream().synchronize()
 
     for _ in range(args.warmup):
         step()
@@ -247,7 +280,8 @@ def main():
         result["cpu_baseline"] = cpu_baseline(block, jobs, codes, args.cpu_seconds)
     if rank == 0 and not args.no_acq:
         result["acquisition"] = acq_bench(ctx, block, sats)
-    batch.close()
+    for b in batches:
+        b.close()
     if rank == 0:
         print(json.dumps(result), flush=True)
     if torch is not None:

@@ -111,6 +111,15 @@ __device__ __forceinline__ f2 cmul_pk(f2 a, f2 b, f2 bsw)
     return __builtin_elementwise_fma(f2{a.y, a.y}, bsw, f2{a.x, a.x} * b);
 }
 
+// (int)floor(x) in one instruction (V_CVT_FLR_I32_F32), as the resampler's (int)floor(...) for
+// in-range values.
+__device__ __forceinline__ int cvt_floor_i32(float x)
+{
+    int r;
+    asm("v_cvt_flr_i32_f32 %0, %1" : "=v"(r) : "v"(x));
+    return r;
+}
+
 // Positive modulo of the reference's wrap (volk_gnsssdr_32f_xn_resampler_32f_xn.h:75-77).
 __device__ __forceinline__ int wrap_index(int idx, int L)
 {
@@ -131,6 +140,10 @@ __device__ __forceinline__ void corr_chunk(const void* __restrict__ samples, con
     const Anchor* __restrict__ anchors, const float* __restrict__ code, int L, float* __restrict__ dst)
 {
     __shared__ float red[kCorrThreads / 64][2 * kMaxTaps];
+    if (ch.len <= 0) {  // zero-length job (workgroup-uniform): nothing to read, outputs are zero
+        if (threadIdx.x < 2 * kMaxTaps) dst[threadIdx.x] = 0.0f;
+        return;
+    }
 
     f2 acc[NT];
 #pragma unroll
@@ -157,48 +170,71 @@ __device__ __forceinline__ void corr_chunk(const void* __restrict__ samples, con
     }
     const Anchor* anc = anchors + job.anchor_offset + (ch.start >> 8);
     const int last_blk = (ch.len - 1) >> 8;  // last 256-sample block of the chunk (chunk-uniform)
+    const bool lane_j0 = (tid == 0);
 
-    // Software pipeline over groups of kGroup samples per lane: the loads of group g+1 are in
-    // flight while group g is correlated.  Lanes past the chunk end read sample 0 of the chunk and
-    // contribute zero.
+    // Software pipeline over groups of kGroup samples per lane, ping-pong register buffers: the
+    // loads of group g+1 are in flight while group g is correlated.  Whole groups inside the chunk
+    // run without any tail test; in the (at most one) partial group, lanes past the chunk end read
+    // the chunk's last sample and contribute zero.
     constexpr int kGroup = 4;
     constexpr int kGroups = kCorrSamplesPerThread / kGroup;
+    constexpr int kGroupSpan = kGroup * kCorrThreads;
+    static_assert(kGroups % 2 == 0, "ping-pong over pairs of groups");
     auto load_group = [&](int g, f2 (&dstx)[kGroup]) {
+        if ((g + 1) * kGroupSpan <= ch.len) {
 #pragma unroll
-        for (int u = 0; u < kGroup; u++) {
-            const int r = tid + (g * kGroup + u) * kCorrThreads;
-            const float2 v = load_sample<FMT>(samples, base + (r < ch.len ? r : 0));
-            dstx[u] = (r < ch.len) ? f2{v.x, v.y} : f2{0.0f, 0.0f};
+            for (int u = 0; u < kGroup; u++) {
+                const float2 v = load_sample<FMT>(samples, base + tid + (g * kGroup + u) * kCorrThreads);
+                dstx[u] = f2{v.x, v.y};
+            }
+        } else {
+#pragma unroll
+            for (int u = 0; u < kGroup; u++) {
+                const int r = tid + (g * kGroup + u) * kCorrThreads;
+                const float2 v = load_sample<FMT>(samples, base + (r < ch.len ? r : ch.len - 1));
+                dstx[u] = (r < ch.len) ? f2{v.x, v.y} : f2{0.0f, 0.0f};
+            }
         }
     };
-    f2 xs[kGroup], xn[kGroup];
-    load_group(0, xs);
-#pragma unroll 1
-    for (int g = 0; g < kGroups; g++) {
-        if (g * kGroup * kCorrThreads >= ch.len) break;  // chunk-uniform: no lane has samples left
-        if (g + 1 < kGroups && (g + 1) * kGroup * kCorrThreads < ch.len) load_group(g + 1, xn);
+    auto correlate_group = [&](int g, const f2 (&xg)[kGroup]) {
+        // anchors of this group's 256-sample blocks: chunk-uniform addresses → scalar loads
+        Anchor ag[kGroup];
 #pragma unroll
         for (int u = 0; u < kGroup; u++) {
             const int m = g * kGroup + u;
-            const int r = tid + m * kCorrThreads;
-            const int n = ch.start + (r < ch.len ? r : 0);  // the reference's loop counter (clamped tail)
-            const int mm = m < last_blk ? m : last_blk;     // chunk-uniform → scalar anchor load
-            const Anchor a = anc[mm];
-            // phasor at sample n: the anchor itself at j = 0, else q_k · E_j
-            const f2 p = (tid == 0) ? f2{a.a_re, a.a_im} : cmul_pk(f2{a.q_re, a.q_im}, e, esw);
-            const f2 tt = cmul_pk(xs[u], p, f2{-p.y, p.x});  // in_common[n] * phase
+            ag[u] = anc[m < last_blk ? m : last_blk];
+        }
+        const bool full = (g + 1) * kGroupSpan <= ch.len;  // group-uniform
+#pragma unroll
+        for (int u = 0; u < kGroup; u++) {
+            const int r = tid + (g * kGroup + u) * kCorrThreads;
+            const int n = ch.start + (full ? r : (r < ch.len ? r : ch.len - 1));  // reference loop counter
+            // phasor at sample n: the anchor itself at j = 0, else q_k · E_j (select, no branch)
+            const f2 pq = cmul_pk(f2{ag[u].q_re, ag[u].q_im}, e, esw);
+            const f2 p = lane_j0 ? f2{ag[u].a_re, ag[u].a_im} : pq;
+            const f2 tt = cmul_pk(xg[u], p, f2{-p.y, p.x});  // in_common[n] * phase
             // code resampler, generic association order: ((step*n) + shift) - rem, each rounded
-            const float sn = __fmul_rn(job.code_step, static_cast<float>(n));
+            // on its own (the file is built with -ffp-contract=off)
+            const float sn = job.code_step * static_cast<float>(n);
 #pragma unroll
             for (int t = 0; t < NT; t++) {
-                int idx = static_cast<int>(floorf(__fsub_rn(__fadd_rn(sn, shifts[t]), job.rem_code)));
+                int idx = cvt_floor_i32((sn + shifts[t]) - job.rem_code);
                 if constexpr (!IN_MARGIN) idx = wrap_index(idx, L);
                 const float cv = code[idx];
                 acc[t] = __builtin_elementwise_fma(tt, f2{cv, cv}, acc[t]);
             }
         }
+    };
+    f2 xa[kGroup], xb[kGroup];
+    load_group(0, xa);
 #pragma unroll
-        for (int u = 0; u < kGroup; u++) xs[u] = xn[u];
+    for (int g = 0; g < kGroups; g += 2) {
+        if (g * kGroupSpan >= ch.len) break;  // chunk-uniform
+        if ((g + 1) * kGroupSpan < ch.len) load_group(g + 1, xb);
+        correlate_group(g, xa);
+        if ((g + 1) * kGroupSpan >= ch.len) break;
+        if (g + 2 < kGroups && (g + 2) * kGroupSpan < ch.len) load_group(g + 2, xa);
+        correlate_group(g + 1, xb);
     }
 
     const int lane = tid & 63, wave = tid >> 6;

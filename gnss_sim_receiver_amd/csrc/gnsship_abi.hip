@@ -314,7 +314,24 @@ struct gnsship_batch {
     int64_t anchor_cap = 0;
     std::vector<DevJob> jobs_host;
     std::vector<ChunkDesc> chunks_host;
+    // The anchor replay (NCO arguments only, latency-bound, few waves) runs on the batch's own
+    // stream; the correlation on the context stream waits for it.  With two batches in flight the
+    // replay of one overlaps the correlation of the other.
+    hipStream_t aux = nullptr;
+    hipEvent_t anchors_ready = nullptr;  // aux → ctx: anchors written
+    hipEvent_t corr_done = nullptr;      // ctx → aux: correlation finished reading the anchors
 };
+
+static void batch_release(gnsship_batch* b)
+{
+    void* ptrs[] = {b->jobs_dev, b->chunks_dev, b->partials_dev, b->out_dev, b->anchors_dev};
+    for (void* p : ptrs)
+        if (p) (void)hipFree(p);
+    if (b->anchors_ready) (void)hipEventDestroy(b->anchors_ready);
+    if (b->corr_done) (void)hipEventDestroy(b->corr_done);
+    if (b->aux) (void)hipStreamDestroy(b->aux);
+    delete b;
+}
 
 extern "C" int gnsship_batch_create(gnsship_ctx* ctx, int max_jobs, gnsship_batch** out)
 {
@@ -327,9 +344,12 @@ extern "C" int gnsship_batch_create(gnsship_ctx* ctx, int max_jobs, gnsship_batc
     b->max_jobs = max_jobs;
     hipError_t e = hipMalloc(&b->jobs_dev, sizeof(DevJob) * max_jobs);
     if (e == hipSuccess) e = hipMalloc(&b->out_dev, sizeof(float) * 2 * kMaxTaps * max_jobs);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&b->aux, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&b->anchors_ready, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&b->corr_done, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventRecord(b->corr_done, ctx->stream);
     if (e != hipSuccess) {
-        if (b->jobs_dev) (void)hipFree(b->jobs_dev);
-        delete b;
+        batch_release(b);
         return hip_fail(ctx, e, "gnsship_batch_create");
     }
     *out = b;
@@ -394,9 +414,21 @@ extern "C" int gnsship_batch_launch_stages(gnsship_batch* b, const void* dev_sam
     if (!dev_samples && b->n_jobs) return fail(ctx, GNSSHIP_E_INVAL, "gnsship_batch_launch: null sample buffer");
     if (b->n_jobs == 0) return GNSSHIP_OK;
     if (ctx->codes_dirty) return fail(ctx, GNSSHIP_E_STATE, "gnsship_batch_launch: code bank changed after set_jobs");
-    hipError_t e = launch_corr_batch(dev_samples, fmt, b->jobs_dev, b->n_jobs, b->chunks_dev, b->n_chunks, b->classes, ctx->codes_dev, b->max_code_len,
-        b->any_multi, b->anchors_dev, b->partials_dev, b->out_dev, ctx->stream, stages);
-    if (e != hipSuccess) return hip_fail(ctx, e, "launch_corr_batch");
+    if (stages & GNSSHIP_STAGE_ANCHORS) {
+        // WAR: the previous correlation of this batch must have consumed the anchors
+        HIP_TRY(ctx, hipStreamWaitEvent(b->aux, b->corr_done, 0));
+        hipError_t e = launch_corr_batch(dev_samples, fmt, b->jobs_dev, b->n_jobs, b->chunks_dev, b->n_chunks, b->classes, ctx->codes_dev,
+            b->max_code_len, b->any_multi, b->anchors_dev, b->partials_dev, b->out_dev, b->aux, GNSSHIP_STAGE_ANCHORS);
+        if (e != hipSuccess) return hip_fail(ctx, e, "launch_corr_batch(anchors)");
+        HIP_TRY(ctx, hipEventRecord(b->anchors_ready, b->aux));
+        HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, b->anchors_ready, 0));  // RAW: correlation (or caller) after replay
+    }
+    if (stages & GNSSHIP_STAGE_CORRELATE) {
+        hipError_t e = launch_corr_batch(dev_samples, fmt, b->jobs_dev, b->n_jobs, b->chunks_dev, b->n_chunks, b->classes, ctx->codes_dev,
+            b->max_code_len, b->any_multi, b->anchors_dev, b->partials_dev, b->out_dev, ctx->stream, GNSSHIP_STAGE_CORRELATE);
+        if (e != hipSuccess) return hip_fail(ctx, e, "launch_corr_batch(correlate)");
+        HIP_TRY(ctx, hipEventRecord(b->corr_done, ctx->stream));
+    }
     return GNSSHIP_OK;
 }
 
@@ -423,12 +455,8 @@ extern "C" int gnsship_batch_destroy(gnsship_batch* b)
     gnsship_ctx* ctx = b->ctx;
     (void)hipSetDevice(ctx->device);
     (void)hipStreamSynchronize(ctx->stream);
-    if (b->jobs_dev) (void)hipFree(b->jobs_dev);
-    if (b->chunks_dev) (void)hipFree(b->chunks_dev);
-    if (b->partials_dev) (void)hipFree(b->partials_dev);
-    if (b->out_dev) (void)hipFree(b->out_dev);
-    if (b->anchors_dev) (void)hipFree(b->anchors_dev);
-    delete b;
+    if (b->aux) (void)hipStreamSynchronize(b->aux);
+    batch_release(b);
     return GNSSHIP_OK;
 }
 
