@@ -1,5 +1,6 @@
 // acq_abi.hip — C-ABI of the PCPS acquisition engine (include/gnsship.h, gnsship_acq_*).
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <vector>
@@ -28,6 +29,26 @@ bool make_fft_plan(int n, FftPlan& plan)
     }
     return m == 1;
 }
+
+// Transform layout for size n: the single-pass LDS transform when it fits, else the four-step
+// N = P·M (smallest supported P with M = N/P ≤ 1024 and M {2,3,5}-smooth).  force_big selects the
+// four-step at sizes the LDS transform also covers (test knob GNSSHIP_ACQ_FORCE_BIG=1).
+bool choose_acq_layout(int n, bool force_big, FftPlan& plan, int& P)
+{
+    P = 0;
+    if (!force_big && make_fft_plan(n, plan)) return true;
+    if (n < 2 || n > kMaxAcqBigN) return false;
+    for (int p = 16; p <= 32; p++) {
+        if (!big_p_supported(p) || n % p != 0) continue;
+        const int m = n / p;
+        if (m > kAcqThreads || m < 2) continue;
+        if (make_fft_plan(m, plan)) {
+            P = p;
+            return true;
+        }
+    }
+    return false;
+}
 }  // namespace gnsship
 
 using namespace gnsship;
@@ -41,7 +62,8 @@ using namespace gnsship;
 struct gnsship_acq {
     gnsship_ctx* ctx = nullptr;
     gnsship_acq_conf conf{};
-    FftPlan plan{};
+    FftPlan plan{};              // whole transform (P == 0) or the M-point row transform (P > 0)
+    int P = 0;                   // four-step register points; spectra are then stored transposed
     int n_bins = 0;
     int dwell_count = 0;
     float2* tw = nullptr;        // N twiddles exp(-2πi t/N)
@@ -128,8 +150,11 @@ extern "C" int gnsship_acq_create(gnsship_ctx* ctx, const gnsship_acq_conf* conf
     if (!ctx || !conf || !out) return GNSSHIP_E_INVAL;
     *out = nullptr;
     FftPlan plan;
-    if (!make_fft_plan(conf->fft_size, plan))
-        return fail(ctx, GNSSHIP_E_INVAL, "gnsship_acq_create: fft_size must be 2^a 3^b 5^c and <= 16384 for the LDS-resident FFT");
+    int P = 0;
+    const char* fb = std::getenv("GNSSHIP_ACQ_FORCE_BIG");
+    if (!choose_acq_layout(conf->fft_size, fb && fb[0] == '1', plan, P))
+        return fail(ctx, GNSSHIP_E_INVAL,
+            "gnsship_acq_create: fft_size must be 2^a 3^b 5^c, and either <= 16384 or P*M with P in {16..32}, M <= 1024 (max 32768)");
     if (conf->fs_in <= 0 || conf->max_prns < 1 || conf->max_dwells < 1 || conf->samples_per_chip < 0 || conf->samples_per_code <= 0.0f)
         return fail(ctx, GNSSHIP_E_INVAL, "gnsship_acq_create: bad configuration");
     HIP_TRY(ctx, hipSetDevice(ctx->device));
@@ -138,6 +163,7 @@ extern "C" int gnsship_acq_create(gnsship_ctx* ctx, const gnsship_acq_conf* conf
     a->ctx = ctx;
     a->conf = *conf;
     a->plan = plan;
+    a->P = P;
     a->code_set.assign(conf->max_prns, 0);
     const int N = conf->fft_size;
     std::vector<float2> tw(N);
@@ -179,8 +205,11 @@ extern "C" int gnsship_acq_set_local_code(gnsship_acq* a, int prn_slot, const fl
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     const int N = a->conf.fft_size;
     HIP_TRY(ctx, hipMemcpyAsync(a->sig_dev, code, sizeof(float2) * N, hipMemcpyHostToDevice, ctx->stream));
-    HIP_TRY(ctx, launch_acq_fft_rows(a->sig_dev, GNSSHIP_FMT_CF32, nullptr, 1, a->plan, a->tw, a->codes_fft + static_cast<size_t>(prn_slot) * N,
-                     1, ctx->stream));
+    float2* dst = a->codes_fft + static_cast<size_t>(prn_slot) * N;
+    if (a->P)
+        HIP_TRY(ctx, launch_acq_fft_big(a->sig_dev, GNSSHIP_FMT_CF32, nullptr, 1, a->P, a->plan, a->tw, dst, 1, ctx->stream));
+    else
+        HIP_TRY(ctx, launch_acq_fft_rows(a->sig_dev, GNSSHIP_FMT_CF32, nullptr, 1, a->plan, a->tw, dst, 1, ctx->stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     a->code_set[prn_slot] = 1;
     return GNSSHIP_OK;
@@ -216,9 +245,15 @@ extern "C" int gnsship_acq_run(gnsship_acq* a, const void* sig, int fmt, int sig
     if (a->dwell_count >= a->conf.max_dwells) a->dwell_count = 0;
     const int accumulate = (a->conf.max_dwells > 1 && a->dwell_count > 0) ? 1 : 0;
     a->dwell_count++;
-    HIP_TRY(ctx, launch_acq_fft_rows(src, fmt, a->wipe, a->n_bins, a->plan, a->tw, a->X, 0, ctx->stream));
-    HIP_TRY(ctx, launch_acq_search(a->X, a->codes_fft, n_prns, a->n_bins, a->plan, a->tw, a->conf.samples_per_chip, accumulate, a->rowstat,
-                     keep_grid ? a->grid_dev : nullptr, ctx->stream));
+    if (a->P) {
+        HIP_TRY(ctx, launch_acq_fft_big(src, fmt, a->wipe, a->n_bins, a->P, a->plan, a->tw, a->X, 0, ctx->stream));
+        HIP_TRY(ctx, launch_acq_search_big(a->X, a->codes_fft, n_prns, a->n_bins, a->P, a->plan, a->tw, a->conf.samples_per_chip, accumulate,
+                         a->rowstat, keep_grid ? a->grid_dev : nullptr, ctx->stream));
+    } else {
+        HIP_TRY(ctx, launch_acq_fft_rows(src, fmt, a->wipe, a->n_bins, a->plan, a->tw, a->X, 0, ctx->stream));
+        HIP_TRY(ctx, launch_acq_search(a->X, a->codes_fft, n_prns, a->n_bins, a->plan, a->tw, a->conf.samples_per_chip, accumulate,
+                         a->rowstat, keep_grid ? a->grid_dev : nullptr, ctx->stream));
+    }
     HIP_TRY(ctx, launch_acq_decide(a->rowstat, n_prns, a->n_bins, N, a->conf.doppler_max, a->conf.doppler_step, a->conf.doppler_center,
                      a->dwell_count, a->conf.use_cfar, a->conf.samples_per_code, a->res_dev, ctx->stream));
     HIP_TRY(ctx, hipMemcpyAsync(results, a->res_dev, sizeof(gnsship_acq_result) * n_prns, hipMemcpyDeviceToHost, ctx->stream));

@@ -10,6 +10,7 @@ namespace gnsship {
 constexpr int kAcqThreads = 1024;   // one workgroup per transform: 16 wave64
 constexpr int kMaxAcqN = 16384;     // LDS-resident transform: 16384 complex64 = 128 KiB
 constexpr int kMaxPasses = 16;
+constexpr int kMaxAcqBigN = 32768;  // four-step limit: 32 register points × 1024 LDS rows
 
 struct FftPlan {
     int32_t n;
@@ -32,6 +33,12 @@ hipError_t launch_acq_fft_rows(const void* sig, int fmt, const float2* mult, int
     int conj_out, hipStream_t stream);
 hipError_t launch_acq_search(const float2* X, const float2* codes_fft, int n_prns, int n_bins, const FftPlan& plan, const float2* tw,
     int samples_per_chip, int accumulate, RowStat* rowstat, float* grid, hipStream_t stream);
+// Large transforms (N > kMaxAcqN): N = P·M, P ∈ {16,18,20,24,25,27,30,32} in registers, M ≤ 1024 in LDS.
+bool big_p_supported(int P);
+hipError_t launch_acq_fft_big(const void* sig, int fmt, const float2* mult, int n_rows, int P, const FftPlan& row_plan, const float2* tw,
+    float2* rowsT, int conj_out, hipStream_t stream);
+hipError_t launch_acq_search_big(const float2* XT, const float2* codesT, int n_prns, int n_bins, int P, const FftPlan& row_plan,
+    const float2* tw, int samples_per_chip, int accumulate, RowStat* rowstat, float* grid, hipStream_t stream);
 hipError_t launch_acq_decide(const RowStat* rowstat, int n_prns, int n_bins, int N, int doppler_max, int doppler_step, int doppler_center,
     int dwells, int use_cfar, float samples_per_code, gnsship_acq_result* out, hipStream_t stream);
 

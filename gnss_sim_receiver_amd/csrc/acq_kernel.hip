@@ -182,6 +182,186 @@ __global__ __launch_bounds__(kAcqThreads) void acq_fft_rows_kernel(const void* _
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Large transforms (kMaxAcqN < N ≤ 32768, e.g. the 25000-point transform of a 1 ms GPS code at
+// 25 Msps): four-step with one workgroup per transform, N = P·M, M ≤ 1024 rows of the LDS stage and
+// P ≤ 32 points per thread in registers.  Thread t owns column t: x[t + M·q], q < P.
+//   forward:  X[kq + P·k] = Σ_t W_M^{t·k} · W_N^{t·kq} · Σ_q x[t + M·q] W_P^{q·kq}
+//             (register P-point DFT, twiddle, then M-point row DFTs in LDS, 16 rows per round);
+//             stored row-major TRANSPOSED: XT[kq·M + k] = X[kq + P·k].
+//   inverse:  y[t + M·q] = Σ_kq W_P^{−q·kq} · W_N^{−t·kq} · Σ_k Z[kq + P·k] W_M^{−t·k}
+//             reads Z in the same transposed layout (rows first, registers last) and so returns
+//             natural order.  Point-wise products between two transposed spectra need no reorder.
+// Pass twiddles come from the N-entry table: exp(−2πi m/M) = tw[m·P].
+// ---------------------------------------------------------------------------------------------
+constexpr int kBigRows = 8;  // rows per LDS round: two ping-pong buffers of 8 × M ≤ 8192 complex (2 × 64 KiB)
+
+// Out-of-place Stockham pass over `rows` rows of length M: src → dst, one barrier.  Out of place so
+// a butterfly's R values are the only registers it needs (the P register points of the four-step
+// stay live across the row passes; 1024 threads leave 128 VGPRs per lane).
+template <int R, int SIGN>
+__device__ __forceinline__ void stockham_pass_rows(const float2* __restrict__ src, float2* __restrict__ dst, int M, int rows, int Ns,
+    const float2* __restrict__ tw, int tw_stride)
+{
+    const int nb = M / R;
+    const int total = rows * nb;
+    const int tstep = (M / (Ns * R)) * tw_stride;
+    for (int j = threadIdx.x; j < total; j += kAcqThreads) {
+        const int row = j / nb;
+        const int jl = j - row * nb;
+        const int k = jl % Ns;
+        const float2* in = src + row * M + jl;
+        float2 v[R];
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+            float2 x = in[r * nb];
+            if (r > 0 && k > 0) {
+                float2 w = tw[k * r * tstep];
+                if (SIGN > 0) w.y = -w.y;
+                x = cmulf(x, w);
+            }
+            v[r] = x;
+        }
+        dft_small<R, SIGN>(v);
+        float2* out = dst + row * M + (jl / Ns) * Ns * R + k;
+#pragma unroll
+        for (int r = 0; r < R; r++) out[r * Ns] = v[r];
+    }
+    __syncthreads();
+}
+
+// Row FFTs from buffer a; returns the buffer (a or b) holding the result.
+template <int SIGN>
+__device__ __forceinline__ float2* fft_rows_lds(float2* __restrict__ a, float2* __restrict__ b, const FftPlan& plan, int rows,
+    const float2* __restrict__ tw, int tw_stride)
+{
+    int Ns = 1;
+    for (int p = 0; p < plan.n_passes; p++) {
+        const int R = plan.radix[p];
+        switch (R) {
+        case 2: stockham_pass_rows<2, SIGN>(a, b, plan.n, rows, Ns, tw, tw_stride); break;
+        case 3: stockham_pass_rows<3, SIGN>(a, b, plan.n, rows, Ns, tw, tw_stride); break;
+        case 4: stockham_pass_rows<4, SIGN>(a, b, plan.n, rows, Ns, tw, tw_stride); break;
+        case 5: stockham_pass_rows<5, SIGN>(a, b, plan.n, rows, Ns, tw, tw_stride); break;
+        default: stockham_pass_rows<8, SIGN>(a, b, plan.n, rows, Ns, tw, tw_stride); break;
+        }
+        float2* t = a;
+        a = b;
+        b = t;
+        Ns *= R;
+    }
+    return a;
+}
+
+constexpr int first_radix(int m)
+{
+    return (m % 8 == 0) ? 8 : (m % 5 == 0) ? 5 : (m % 4 == 0) ? 4 : (m % 3 == 0) ? 3 : 2;
+}
+
+// cos/sin of 2π·m/L in double by Taylor series, for compile-time register-DFT twiddles (L ≤ 32).
+constexpr double ct_sin_red(double x)
+{
+    double term = x, sum = x;
+    for (int i = 1; i < 30; i++) {
+        term *= -x * x / ((2.0 * i) * (2.0 * i + 1.0));
+        sum += term;
+    }
+    return sum;
+}
+constexpr double ct_cos_red(double x)
+{
+    double term = 1.0, sum = 1.0;
+    for (int i = 1; i < 30; i++) {
+        term *= -x * x / ((2.0 * i - 1.0) * (2.0 * i));
+        sum += term;
+    }
+    return sum;
+}
+constexpr double kPi = 3.14159265358979323846;
+constexpr double ct_angle(int m, int L)
+{
+    // reduce 2π·m/L into (−π, π]
+    const int mm = m % L;
+    const int ms = (2 * mm > L) ? mm - L : mm;
+    return 2.0 * kPi * static_cast<double>(ms) / static_cast<double>(L);
+}
+
+// In-register Stockham DFT of length P (compile-time, fully unrolled).  Pass twiddles
+// exp(SIGN·2πi·m/(Ns·R)) are literal constants.
+template <int P, int Ns, int SIGN>
+__device__ __forceinline__ void dft_reg(float2* x, const float2* __restrict__ tw, int N)
+{
+    if constexpr (Ns < P) {
+        constexpr int R = first_radix(P / Ns);
+        constexpr int nb = P / R;
+        float2 y[P];
+#pragma unroll
+        for (int j = 0; j < nb; j++) {
+            const int k = j % Ns;
+            float2 v[R];
+#pragma unroll
+            for (int r = 0; r < R; r++) {
+                float2 a = x[j + r * nb];
+                if (r > 0 && k > 0) {
+                    const double ang = ct_angle(k * r, Ns * R);
+                    const float2 w = make_float2(static_cast<float>(ct_cos_red(ang)), static_cast<float>(SIGN * ct_sin_red(ang)));
+                    a = cmulf(a, w);
+                }
+                v[r] = a;
+            }
+            dft_small<R, SIGN>(v);
+#pragma unroll
+            for (int r = 0; r < R; r++) y[(j / Ns) * Ns * R + k + r * Ns] = v[r];
+        }
+#pragma unroll
+        for (int i = 0; i < P; i++) x[i] = y[i];
+        dft_reg<P, Ns * R, SIGN>(x, tw, N);
+    }
+}
+
+// rowsT[b] = transposed FFT(sig ⊙ mult[b]); conj_out for the code spectrum.
+template <int FMT, int P>
+__global__ __launch_bounds__(kAcqThreads) void acq_fft_big_kernel(const void* __restrict__ sig, const float2* __restrict__ mult,
+    FftPlan row_plan, const float2* __restrict__ tw, float2* __restrict__ rowsT, int conj_out)
+{
+    extern __shared__ __attribute__((aligned(16))) float2 lds[];
+    const int M = row_plan.n;
+    const int N = P * M;
+    const int t = threadIdx.x;
+    const int b = blockIdx.x;
+    const float2* m = mult ? mult + static_cast<int64_t>(b) * N : nullptr;
+    float2 v[P];
+    if (t < M) {
+#pragma unroll
+        for (int q = 0; q < P; q++) {
+            float2 x = load_if<FMT>(sig, t + M * q);
+            if (m) x = cmulf(x, m[t + M * q]);  // volk_32fc_x2_multiply_32fc(in, wipeoff)
+            v[q] = x;
+        }
+        dft_reg<P, 1, -1>(v, tw, N);
+    }
+    float2* out = rowsT + static_cast<int64_t>(b) * N;
+#pragma unroll
+    for (int r0 = 0; r0 < P; r0 += kBigRows) {
+        const int nrows = (P - r0) < kBigRows ? (P - r0) : kBigRows;
+        if (t < M) {
+#pragma unroll
+            for (int kk = 0; kk < kBigRows; kk++) {
+                const int kq = r0 + kk;
+                if (kq < P) lds[kk * M + t] = kq ? cmulf(v[kq], tw[t * kq]) : v[kq];  // W_N^{t·kq}, t·kq < N
+            }
+        }
+        __syncthreads();
+        const float2* res = fft_rows_lds<-1>(lds, lds + kBigRows * M, row_plan, nrows, tw, P);
+        for (int i = t; i < nrows * M; i += kAcqThreads) {
+            float2 y = res[i];
+            if (conj_out) y.y = -y.y;
+            out[r0 * M + i] = y;
+        }
+        __syncthreads();
+    }
+}
+
 struct MaxIdx {
     float v;
     int i;
@@ -277,6 +457,88 @@ __global__ __launch_bounds__(kAcqThreads) void acq_search_kernel(const float2* _
     }
 }
 
+// Large-N search: Y = IFFT(XT_b ⊙ CT_p) by the transposed four-step (rows in LDS, then the
+// register P-point stage), |Y|² and the same row statistics as acq_search_kernel.  Thread t holds
+// y[t + M·q] for q < P, i.e. the natural index n = t + M·q.
+template <int P>
+__global__ __launch_bounds__(kAcqThreads) void acq_search_big_kernel(const float2* __restrict__ XT, const float2* __restrict__ codesT,
+    FftPlan row_plan, const float2* __restrict__ tw, int n_bins, int samples_per_chip, int accumulate, RowStat* __restrict__ rowstat,
+    float* __restrict__ grid_out)
+{
+    extern __shared__ __attribute__((aligned(16))) float2 lds[];
+    __shared__ MaxIdx red_m[kAcqThreads / 64];
+    __shared__ float red_s[kAcqThreads / 64];
+    const int b = blockIdx.x, p = blockIdx.y;
+    const int M = row_plan.n;
+    const int N = P * M;
+    const int t = threadIdx.x;
+    const float2* x = XT + static_cast<int64_t>(b) * N;
+    const float2* c = codesT + static_cast<int64_t>(p) * N;
+    float2 v[P];
+#pragma unroll
+    for (int r0 = 0; r0 < P; r0 += kBigRows) {
+        const int nrows = (P - r0) < kBigRows ? (P - r0) : kBigRows;
+        for (int i = t; i < nrows * M; i += kAcqThreads) lds[i] = cmulf(x[r0 * M + i], c[r0 * M + i]);  // ×conj(code FFT)
+        __syncthreads();
+        const float2* res = fft_rows_lds<+1>(lds, lds + kBigRows * M, row_plan, nrows, tw, P);
+        if (t < M) {
+#pragma unroll
+            for (int kk = 0; kk < kBigRows; kk++) {
+                const int kq = r0 + kk;
+                if (kq < P) {
+                    float2 w = tw[t * kq];  // W_N^{−t·kq}
+                    w.y = -w.y;
+                    v[kq] = kq ? cmulf(res[kk * M + t], w) : res[kk * M + t];
+                }
+            }
+        }
+        __syncthreads();
+    }
+    // |Y|² is parked in LDS (N floats ≤ the 2·kBigRows·M complex of the row buffers) for the
+    // second-peak scan; all row-pass reads of LDS finished at the last round's barrier.
+    float* mag = reinterpret_cast<float*>(lds);
+    MaxIdx m{-1.0f, 0x7fffffff};
+    float s = 0.0f;
+    if (t < M) {
+        dft_reg<P, 1, +1>(v, tw, N);
+        float* row = grid_out ? grid_out + (static_cast<int64_t>(p) * n_bins + b) * N : nullptr;
+#pragma unroll
+        for (int q = 0; q < P; q++) {
+            const int n = t + M * q;
+            float g = __fadd_rn(__fmul_rn(v[q].x, v[q].x), __fmul_rn(v[q].y, v[q].y));  // volk_32fc_magnitude_squared_32f
+            if (row) {
+                if (accumulate) g = __fadd_rn(row[n], g);  // volk_32f_x2_add_32f
+                row[n] = g;
+            }
+            mag[n] = g;
+            m = better(m, MaxIdx{g, n});
+            s += g;
+        }
+    }
+    const MaxIdx best = block_argmax(m, red_m);
+    const float sum = block_sum(s, red_s);
+    int e1 = best.i - samples_per_chip, e2 = best.i + samples_per_chip;
+    if (e1 < 0) e1 += N; else if (e2 >= N) e2 -= N;
+    MaxIdx m2{0.0f, 0x7fffffff};
+    if (t < M) {
+#pragma unroll
+        for (int q = 0; q < P; q++) {
+            const int n = t + M * q;
+            const bool in_win = (e1 < e2) ? (n >= e1 && n < e2) : (n >= e1 || n < e2);
+            m2 = better(m2, MaxIdx{in_win ? 0.0f : mag[n], n});
+        }
+    }
+    const MaxIdx second = block_argmax(m2, red_m);
+    if (t == 0) {
+        RowStat r;
+        r.max = best.v;
+        r.argmax = best.i;
+        r.sum = sum;
+        r.second = second.v;
+        rowstat[static_cast<int64_t>(p) * n_bins + b] = r;
+    }
+}
+
 // One thread per PRN: the reference's row scan (strict >, ascending bin) and decision values.
 __global__ void acq_decide_kernel(const RowStat* __restrict__ rowstat, int n_prns, int n_bins, int N, int doppler_max, int doppler_step,
     int doppler_center, int dwells, int use_cfar, float samples_per_code, gnsship_acq_result* __restrict__ out)
@@ -337,6 +599,61 @@ hipError_t launch_acq_search(const float2* X, const float2* codes_fft, int n_prn
     const size_t lds = sizeof(float2) * static_cast<size_t>(plan.n);
     hipLaunchKernelGGL(acq_search_kernel, dim3(n_bins, n_prns), dim3(kAcqThreads), lds, stream, X, codes_fft, plan, tw, n_bins,
         samples_per_chip, accumulate, rowstat, grid);
+    return hipGetLastError();
+}
+
+#define GNSSHIP_BIG_P_LIST(X) X(16) X(18) X(20) X(24) X(25) X(27) X(30) X(32)
+
+bool big_p_supported(int P)
+{
+#define GNSSHIP_P_CASE(p) \
+    case p: return true;
+    switch (P) { GNSSHIP_BIG_P_LIST(GNSSHIP_P_CASE) default: return false; }
+#undef GNSSHIP_P_CASE
+}
+
+hipError_t launch_acq_fft_big(const void* sig, int fmt, const float2* mult, int n_rows, int P, const FftPlan& row_plan, const float2* tw,
+    float2* rowsT, int conj_out, hipStream_t stream)
+{
+    const size_t lds = 2 * sizeof(float2) * static_cast<size_t>(kBigRows) * row_plan.n;
+    if (row_plan.n > kAcqThreads) return hipErrorInvalidValue;
+#define GNSSHIP_P_CASE(p)                                                                                                            \
+    case p:                                                                                                                          \
+        if (fmt == GNSSHIP_FMT_CF32)                                                                                                 \
+            hipLaunchKernelGGL((acq_fft_big_kernel<GNSSHIP_FMT_CF32, p>), dim3(n_rows), dim3(kAcqThreads), lds, stream, sig, mult,   \
+                row_plan, tw, rowsT, conj_out);                                                                                      \
+        else if (fmt == GNSSHIP_FMT_CI16)                                                                                            \
+            hipLaunchKernelGGL((acq_fft_big_kernel<GNSSHIP_FMT_CI16, p>), dim3(n_rows), dim3(kAcqThreads), lds, stream, sig, mult,   \
+                row_plan, tw, rowsT, conj_out);                                                                                      \
+        else if (fmt == GNSSHIP_FMT_CI8)                                                                                             \
+            hipLaunchKernelGGL((acq_fft_big_kernel<GNSSHIP_FMT_CI8, p>), dim3(n_rows), dim3(kAcqThreads), lds, stream, sig, mult,    \
+                row_plan, tw, rowsT, conj_out);                                                                                      \
+        else                                                                                                                         \
+            return hipErrorInvalidValue;                                                                                             \
+        break;
+    switch (P) {
+        GNSSHIP_BIG_P_LIST(GNSSHIP_P_CASE)
+    default: return hipErrorInvalidValue;
+    }
+#undef GNSSHIP_P_CASE
+    return hipGetLastError();
+}
+
+hipError_t launch_acq_search_big(const float2* XT, const float2* codesT, int n_prns, int n_bins, int P, const FftPlan& row_plan,
+    const float2* tw, int samples_per_chip, int accumulate, RowStat* rowstat, float* grid, hipStream_t stream)
+{
+    const size_t lds = 2 * sizeof(float2) * static_cast<size_t>(kBigRows) * row_plan.n;
+    if (row_plan.n > kAcqThreads) return hipErrorInvalidValue;
+#define GNSSHIP_P_CASE(p)                                                                                                            \
+    case p:                                                                                                                          \
+        hipLaunchKernelGGL((acq_search_big_kernel<p>), dim3(n_bins, n_prns), dim3(kAcqThreads), lds, stream, XT, codesT, row_plan, tw, \
+            n_bins, samples_per_chip, accumulate, rowstat, grid);                                                                    \
+        break;
+    switch (P) {
+        GNSSHIP_BIG_P_LIST(GNSSHIP_P_CASE)
+    default: return hipErrorInvalidValue;
+    }
+#undef GNSSHIP_P_CASE
     return hipGetLastError();
 }
 

@@ -114,3 +114,75 @@ def test_bad_configuration_rejected(ctx):
     with pytest.raises(abi.GnssHipError):
         acq.run(np.zeros(4000, np.complex64))  # no local code yet
     acq.close()
+
+
+# ---- large transforms (four-step, N = P·M > 16384): SURVEY §8 C3, 25 Msps, 1 ms GPS code ----
+
+def _acq_big_case(ctx, fs, n, prns, present, dmax, step, cfar, seed, want_grid=False):
+    sig = signals.generate_if(fs, n, present, seed=seed)
+    acq = engine.PcpsAcquisition(ctx, fs, n, dmax, step, 0, cfar, max_prns=len(prns))
+    for k, p in enumerate(prns):
+        acq.set_local_code(codes.gps_l1_ca_code_gen_complex_sampled(p, fs), k)
+    res, grid = acq.run(sig, n_prns=len(prns), want_grid=want_grid)
+    acq.close()
+    return sig, res, grid
+
+
+def test_c3_25msps_four_step_matches_oracle(ctx):
+    fs, n, dmax, step = 25000000, 25000, 5000, 250
+    present = [signals.Satellite(prn=p, doppler_hz=d, code_delay_chips=c, cn0_dbhz=46.0)
+               for p, d, c in [(4, 1750.0, 211.3), (17, -3900.0, 999.9)]]
+    prns = [4, 17, 30]
+    sig, res, grid = _acq_big_case(ctx, fs, n, prns, present, dmax, step, True, seed=21, want_grid=True)
+    for k, p in enumerate(prns):
+        ref, rgrid = O.pcps_acquisition_core(sig, codes.gps_l1_ca_code_gen_complex_sampled(p, fs), fs, dmax, step, 0, True)
+        # fp32 four-step vs complex128: grid within 1e-5 of the grid maximum
+        assert np.max(np.abs(grid[k] - rgrid)) / rgrid.max() < 1e-5, p
+        flat = np.sort(rgrid.ravel())
+        if flat[-1] / flat[-2] > 1.0 + 1e-4:
+            assert (res[k].doppler_index, res[k].code_index) == (ref.doppler_index, ref.code_index), p
+            assert res[k].acq_delay_samples == ref.acq_delay_samples
+        np.testing.assert_allclose(res[k].test_statistic, ref.test_statistic, rtol=2e-3)
+    assert res[0].test_statistic > 2 * res[2].test_statistic  # noise-only CFAR ≈ 2·ln(10⁶ cells) ≈ 28
+
+
+def test_four_step_forced_at_small_size_first_vs_second(ctx, monkeypatch):
+    """The four-step path at N = 4000 (P = 16, M = 250) against the oracle, second-peak statistic."""
+    monkeypatch.setenv("GNSSHIP_ACQ_FORCE_BIG", "1")
+    fs, n = 4000000, 4000
+    sat = signals.Satellite(prn=22, doppler_hz=-620.0, code_delay_chips=432.1, cn0_dbhz=47.0)
+    sig, (r,), grid = _acq_big_case(ctx, fs, n, [22], [sat], 5000, 250, False, seed=5, want_grid=True)
+    ref, rgrid = O.pcps_acquisition_core(sig, codes.gps_l1_ca_code_gen_complex_sampled(22, fs), fs, 5000, 250, 0, False)
+    assert np.max(np.abs(grid[0] - rgrid)) / rgrid.max() < 1e-5
+    assert (r.doppler_index, r.code_index) == (ref.doppler_index, ref.code_index)
+    np.testing.assert_allclose([r.peak, r.input_power, r.test_statistic], [ref.peak, ref.input_power, ref.test_statistic],
+                               rtol=2e-4)
+
+
+@pytest.mark.parametrize("fmt", ["ci16", "ci8"])
+def test_four_step_integer_formats(ctx, fmt):
+    fs, n = 25000000, 25000
+    sat = signals.Satellite(prn=9, doppler_hz=2250.0, code_delay_chips=600.2, cn0_dbhz=52.0)
+    x = signals.generate_if(fs, n, [sat], seed=31)
+    raw = signals.to_ishort(x) if fmt == "ci16" else signals.to_ibyte(x)
+    code = codes.gps_l1_ca_code_gen_complex_sampled(9, fs)
+    acq = engine.PcpsAcquisition(ctx, fs, n, 5000, 500, 0, True)
+    acq.set_local_code(code)
+    (r,), _ = acq.run(raw)
+    ref, _ = O.pcps_acquisition_core(raw.astype(np.float32).view(np.complex64), code, fs, 5000, 500, 0, True)
+    assert (r.doppler_index, r.code_index) == (ref.doppler_index, ref.code_index)
+    np.testing.assert_allclose(r.test_statistic, ref.test_statistic, rtol=2e-3)
+    acq.close()
+
+
+def test_four_step_max_size_and_limit(ctx):
+    from gnss_sim_receiver_amd import abi
+    # 32768 = 32 × 1024: the largest four-step transform; a 1 ms code at 32.768 Msps
+    fs, n = 32768000, 32768
+    sat = signals.Satellite(prn=2, doppler_hz=-1000.0, code_delay_chips=55.5, cn0_dbhz=50.0)
+    sig, (r,), grid = _acq_big_case(ctx, fs, n, [2], [sat], 2000, 500, True, seed=3, want_grid=True)
+    ref, rgrid = O.pcps_acquisition_core(sig, codes.gps_l1_ca_code_gen_complex_sampled(2, fs), fs, 2000, 500, 0, True)
+    assert np.max(np.abs(grid[0] - rgrid)) / rgrid.max() < 1e-5
+    assert (r.doppler_index, r.code_index) == (ref.doppler_index, ref.code_index)
+    with pytest.raises(abi.GnssHipError):
+        engine.PcpsAcquisition(ctx, 40000000, 40000, 5000, 250)  # > 32768
