@@ -125,6 +125,47 @@ def acq_bench(ctx, fs, n, sig, label):
     return out
 
 
+def e1_bench(ctx, seconds=0.2, reps=10):
+    """C4 per-GPU share: 8 Galileo E1 channels at 25 Msps, 4 ms epochs (N = 100000),
+    5-tap VEML on the E1-C pilot + 1-tap prompt on the E1-B data replica per channel-epoch."""
+    from gnss_sim_receiver_amd import abi, engine, signals as S
+    fs, vl, nch = 25e6, 100000, 8
+    sats = S.random_sky(nch, seed=SEED + 4, system="GAL", prns=[1, 5, 12, 19, 24, 30, 33, 36])
+    n_ep = int(round(seconds * 250))
+    sig = S.generate_if(fs, vl * (n_ep + 2), sats, seed=SEED + 4)
+    jobs, codes = [], []
+    for k, s in enumerate(sats):
+        pj = S.truth_jobs(s, fs, n_ep, vl, [-1.0, -0.5, 0.0, 0.5, 1.0], 100 + 2 * k)
+        dj = pj.copy()
+        dj["code_id"] = 100 + 2 * k + 1
+        dj["n_taps"] = 1
+        dj["shifts_chips"] = 0.0
+        jobs += [pj, dj]
+        ctx.set_code(100 + 2 * k, s.code)
+        ctx.set_code(100 + 2 * k + 1, s.code_data)
+    jobs = np.concatenate(jobs)
+    dev = ctx.upload(sig)
+    b = engine.CorrelatorBatch(ctx, len(jobs))
+    b.set_jobs(jobs, len(sig))
+    for _ in range(2):
+        b.launch_ptr(dev.ptr, abi.FMT_CF32)
+    ctx.sync()
+    ctx.event_record(4)
+    for _ in range(reps):
+        b.launch_ptr(dev.ptr, abi.FMT_CF32)
+    ctx.event_record(5)
+    ctx.sync()
+    ms = ctx.event_elapsed_ms(4, 5) / reps
+    b.close()
+    dev.free()
+    if_msps = n_ep * vl / (ms * 1e-3) / 1e6
+    return {"config": "C4 per-GPU share: Galileo E1, 8 ch, 25 Msps, N=100000, 5 pilot taps + 1 data tap, gr_complex",
+            "ms_per_signal_second": round(ms / seconds, 4), "if_msamples_per_s": round(if_msps, 1),
+            "realtime_factor": round(if_msps * 1e6 / fs, 1),
+            "channels_sustained_realtime": int(nch * if_msps * 1e6 / fs),
+            "algorithmic_GBps": round(2 * nch * n_ep * vl * 8 / (ms * 1e-3) / 1e9, 1)}
+
+
 def main():
     args = parse()
     from gnss_sim_receiver_amd import abi, engine, sharding
@@ -284,6 +325,8 @@ def main():
         sig25 = S.generate_if(25000000, 25000, sats, seed=2)
         result["acquisition_c3"] = acq_bench(ctx, 25000000, 25000, sig25,
                                              "C3: 32 PRN x 40 bins, fft 25000 (four-step), 25 Msps")
+    if rank == 0 and not args.no_acq:
+        result["tracking_c4_e1"] = e1_bench(ctx)
     for b in batches:
         b.close()
     if rank == 0:

@@ -22,7 +22,13 @@ SYSTEMS = {
     # name: (chip_rate, code_len, carrier_hz, code generator)
     "GPS": (C.GPS_L1_CA_CODE_RATE_CPS, C.GPS_L1_CA_CODE_LENGTH_CHIPS, C.GPS_L1_FREQ_HZ, C.gps_l1_ca_code_gen_float),
     "BDS": (C.BEIDOU_B1I_CODE_RATE_CPS, C.BEIDOU_B1I_CODE_LENGTH_CHIPS, C.BEIDOU_B1I_FREQ_HZ, C.beidou_b1i_code_gen_float),
+    # Galileo E1 in units of the sinBOC(1,1) replica (2 samples per chip, 8184 per 4 ms code):
+    # the tracking code is the E1-C pilot (track_pilot = true), the data code E1-B
+    # (dll_pll_veml_tracking.cc:684-697 with galileo_e1_code_gen_sinboc11_float).
+    "GAL": (2.0 * C.GALILEO_E1_CODE_CHIP_RATE_CPS, 2 * C.GALILEO_E1_B_CODE_LENGTH_CHIPS, C.GALILEO_E1_FREQ_HZ,
+            lambda prn: C.galileo_e1_code_gen_sinboc11_float("1C", prn)),
 }
+DATA_CODES = {"GAL": lambda prn: C.galileo_e1_code_gen_sinboc11_float("1B", prn)}
 
 
 @dataclass
@@ -37,10 +43,13 @@ class Satellite:
     bit_seed: int = 0
     f_if_hz: float = 0.0
     code: np.ndarray = field(default=None, repr=False)
+    code_data: np.ndarray = field(default=None, repr=False)  # E1-B data component (Galileo)
 
     def __post_init__(self):
         if self.code is None:
             self.code = SYSTEMS[self.system][3](self.prn)
+        if self.code_data is None and self.system in DATA_CODES:
+            self.code_data = DATA_CODES[self.system](self.prn)
 
     @property
     def chip_rate(self):
@@ -76,6 +85,8 @@ def generate_if(fs: float, n_samples: int, sats: list, seed: int = 0, noise: boo
             ph = s.chip_phase(n, fs)
             chip = np.floor(ph).astype(np.int64)
             c = s.code[np.mod(chip, s.code_len)].astype(np.float64)
+            if s.code_data is not None:  # Galileo E1 OS: (E1B − E1C)/√2 with sinBOC(1,1) subcarriers
+                c = (s.code_data[np.mod(chip, s.code_len)].astype(np.float64) - c) / np.sqrt(2.0)
             if s.data_bits:
                 periods = np.floor_divide(chip, s.code_len)
                 bit_idx = np.floor_divide(periods, 20)

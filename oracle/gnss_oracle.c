@@ -243,6 +243,39 @@ void orc_rotator_dot_prod_generic(float* result, const float* in_common, float i
     phase[1] = pi;
 }
 
+/* Test-only variant of orc_rotator_dot_prod_generic: the SAME float products (x·phase in float,
+ * same phasor recursion and renormalisation), accumulated in double.  Separates the reference's
+ * serial-float-sum rounding (≈ √N half-ulps of the accumulator, ~1e-5 relative at N ≥ 1e5) from
+ * everything else when judging a parallel reduction at long integrations. */
+static void orc_rotator_dot_prod_acc64(float* result, const float* in_common, float inc_re, float inc_im, float* phase,
+    const float* in_a, int num_a_vectors, unsigned int num_points)
+{
+    float pr = phase[0], pi = phase[1];
+    double acc[2 * ORC_MAX_TAPS];
+    for (int t = 0; t < 2 * num_a_vectors; t++) acc[t] = 0.0;
+    for (unsigned int n = 0; n < num_points; n++) {
+        float tr, ti;
+        cmul(in_common[2 * n], in_common[2 * n + 1], pr, pi, &tr, &ti);
+        if (n % 256 == 0) {
+            const float m = hypotf(pr, pi);
+            pr /= m;
+            pi /= m;
+        }
+        float nr, ni;
+        cmul(pr, pi, inc_re, inc_im, &nr, &ni);
+        pr = nr;
+        pi = ni;
+        for (int t = 0; t < num_a_vectors; t++) {
+            const float c = in_a[(size_t)t * num_points + n];
+            acc[2 * t] += (double)(tr * c);
+            acc[2 * t + 1] += (double)(ti * c);
+        }
+    }
+    for (int t = 0; t < 2 * num_a_vectors; t++) result[t] = (float)acc[t];
+    phase[0] = pr;
+    phase[1] = pi;
+}
+
 /* volk_gnsssdr_32fc_32f_high_dynamic_rotator_dot_prod_32fc_xn_generic —
  *   volk_gnsssdr_32fc_32f_high_dynamic_rotator_dot_prod_32fc_xn.h:68-110 (non-Windows branch,
  *   cpowf; note (n*n) is unsigned int and wraps for n >= 65536, as in the reference). */
@@ -286,11 +319,27 @@ void orc_high_dynamic_rotator_dot_prod_generic(float* result, const float* in_co
  *   src/algorithms/tracking/libs/cpu_multicorrelator_real_codes.cc:103-126 (+update_local_code :75-100).
  * phase_offset = (cos rem, −sin rem); phase_inc = exp(−j·step) (std::exp of complex<float>, i.e.
  * glibc cexpf → (cosf(−step), sinf(−step))).  scratch: n_taps*signal_length floats or NULL. */
+static int orc_multicorrelator_impl(float* corr_out, const float* sig_in, const float* local_code, int code_length_chips,
+    const float* shifts_chips, int n_correlators, int high_dyn, float rem_carrier_phase_in_rad, float phase_step_rad,
+    float phase_rate_step_rad, float rem_code_phase_chips, float code_phase_step_chips, float code_phase_rate_step_chips,
+    int signal_length_samples, float* scratch, int accum_f64);
+
 int orc_multicorrelator_real_codes(float* corr_out, const float* sig_in, const float* local_code, int code_length_chips,
     const float* shifts_chips, int n_correlators, int high_dyn, float rem_carrier_phase_in_rad, float phase_step_rad,
     float phase_rate_step_rad, float rem_code_phase_chips, float code_phase_step_chips, float code_phase_rate_step_chips,
     int signal_length_samples, float* scratch)
 {
+    return orc_multicorrelator_impl(corr_out, sig_in, local_code, code_length_chips, shifts_chips, n_correlators, high_dyn,
+        rem_carrier_phase_in_rad, phase_step_rad, phase_rate_step_rad, rem_code_phase_chips, code_phase_step_chips,
+        code_phase_rate_step_chips, signal_length_samples, scratch, 0);
+}
+
+static int orc_multicorrelator_impl(float* corr_out, const float* sig_in, const float* local_code, int code_length_chips,
+    const float* shifts_chips, int n_correlators, int high_dyn, float rem_carrier_phase_in_rad, float phase_step_rad,
+    float phase_rate_step_rad, float rem_code_phase_chips, float code_phase_step_chips, float code_phase_rate_step_chips,
+    int signal_length_samples, float* scratch, int accum_f64)
+{
+    if (accum_f64 && high_dyn) return -1;
     if (n_correlators < 1 || n_correlators > ORC_MAX_TAPS || signal_length_samples < 0) return -1;
     float* codes = scratch;
     int own = 0;
@@ -311,6 +360,8 @@ int orc_multicorrelator_real_codes(float* corr_out, const float* sig_in, const f
         const float rr = cosf(-phase_rate_step_rad), ri = sinf(-phase_rate_step_rad);
         orc_high_dynamic_rotator_dot_prod_generic(corr_out, sig_in, inc_re, inc_im, rr, ri, phase, codes, n_correlators,
             (unsigned)signal_length_samples);
+    } else if (accum_f64) {
+        orc_rotator_dot_prod_acc64(corr_out, sig_in, inc_re, inc_im, phase, codes, n_correlators, (unsigned)signal_length_samples);
     } else {
         orc_rotator_dot_prod_generic(corr_out, sig_in, inc_re, inc_im, phase, codes, n_correlators, (unsigned)signal_length_samples);
     }
@@ -338,6 +389,7 @@ typedef struct {
     float* out;
     int j0, j1;
     int max_n;
+    int accum_f64;
 } orc_batch_arg;
 
 static void* orc_batch_worker(void* p)
@@ -346,10 +398,10 @@ static void* orc_batch_worker(void* p)
     float* scratch = (float*)malloc((size_t)ORC_MAX_TAPS * (size_t)(a->max_n > 0 ? a->max_n : 1) * sizeof(float));
     for (int j = a->j0; j < a->j1; j++) {
         const orc_job* jb = &a->jobs[j];
-        orc_multicorrelator_real_codes(a->out + (size_t)j * 2 * ORC_MAX_TAPS, a->samples + 2 * jb->sample_offset, a->codes[jb->code_id],
+        orc_multicorrelator_impl(a->out + (size_t)j * 2 * ORC_MAX_TAPS, a->samples + 2 * jb->sample_offset, a->codes[jb->code_id],
             a->code_lengths[jb->code_id], jb->shifts_chips, jb->n_taps, jb->flags & 1, jb->rem_carrier_phase_rad, jb->phase_step_rad,
             jb->phase_rate_step_rad, jb->rem_code_phase_chips, jb->code_phase_step_chips, jb->code_phase_rate_step_chips, jb->n_samples,
-            scratch);
+            scratch, a->accum_f64);
     }
     free(scratch);
     return NULL;
@@ -357,8 +409,18 @@ static void* orc_batch_worker(void* p)
 
 /* Run n_jobs correlations over host CF32 samples with n_threads pthreads (GNU Radio runs one
  * thread per channel block; here jobs are split in contiguous ranges).  out: n_jobs × 8 taps. */
+int orc_corr_batch_ex(const float* samples, const orc_job* jobs, int n_jobs, const float* const* codes, const int* code_lengths,
+    float* out, int n_threads, int accum_f64);
+
 int orc_corr_batch(const float* samples, const orc_job* jobs, int n_jobs, const float* const* codes, const int* code_lengths,
     float* out, int n_threads)
+{
+    return orc_corr_batch_ex(samples, jobs, n_jobs, codes, code_lengths, out, n_threads, 0);
+}
+
+/* accum_f64 = 1: the test-only double-accumulation variant (orc_rotator_dot_prod_acc64). */
+int orc_corr_batch_ex(const float* samples, const orc_job* jobs, int n_jobs, const float* const* codes, const int* code_lengths,
+    float* out, int n_threads, int accum_f64)
 {
     if (n_threads < 1) n_threads = 1;
     if (n_threads > 256) n_threads = 256;
@@ -378,6 +440,7 @@ int orc_corr_batch(const float* samples, const orc_job* jobs, int n_jobs, const 
         args[t].j0 = (int)((int64_t)n_jobs * t / n_threads);
         args[t].j1 = (int)((int64_t)n_jobs * (t + 1) / n_threads);
         args[t].max_n = max_n;
+        args[t].accum_f64 = accum_f64;
         if (n_threads == 1) {
             orc_batch_worker(&args[t]);
         } else if (pthread_create(&th[t], NULL, orc_batch_worker, &args[t]) == 0) {

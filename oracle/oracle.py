@@ -96,6 +96,7 @@ def lib(fast: bool = False) -> ctypes.CDLL:
         ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float,
         ctypes.c_int, _f32p]
     L.orc_corr_batch.argtypes = [_f32p, ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(_f32p), _i32p, _f32p, ctypes.c_int]
+    L.orc_corr_batch_ex.argtypes = [_f32p, ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(_f32p), _i32p, _f32p, ctypes.c_int, ctypes.c_int]
     L.orc_sincos_generic.argtypes = [_f32p, ctypes.c_float, _f32p, ctypes.c_uint]
     L.orc_sincos_phases.argtypes = [_f32p, ctypes.c_float, ctypes.c_float, ctypes.c_uint]
     L.orc_doppler_wipeoff_grid.argtypes = [_f32p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
@@ -177,16 +178,18 @@ def multicorrelator(sig, code, shifts, rem_carr, carr_step, rem_code, code_step,
     return out.view(np.complex64)
 
 
-def corr_batch(samples: np.ndarray, jobs: np.ndarray, codes: list, n_threads: int = 1, fast: bool = False) -> np.ndarray:
-    """Run every job (JOB_DTYPE) on host CF32 samples; returns complex64[n_jobs, MAX_TAPS]."""
+def corr_batch(samples: np.ndarray, jobs: np.ndarray, codes: list, n_threads: int = 1, fast: bool = False,
+               accum_f64: bool = False) -> np.ndarray:
+    """Run every job (JOB_DTYPE) on host CF32 samples; returns complex64[n_jobs, MAX_TAPS].
+    accum_f64: same float products, double accumulation (isolates the serial-sum rounding)."""
     samples = np.ascontiguousarray(samples, np.complex64)
     jobs = np.ascontiguousarray(jobs, JOB_DTYPE)
     codes = [np.ascontiguousarray(c, np.float32) for c in codes]
     arr = (_f32p * len(codes))(*[_ptr(c) for c in codes])
     lens = np.array([len(c) for c in codes], np.int32)
     out = np.zeros((len(jobs), 2 * MAX_TAPS), np.float32)
-    lib(fast).orc_corr_batch(_ptr(samples.view(np.float32)), jobs.ctypes.data, len(jobs), arr, _ptr(lens, ctypes.c_int32),
-                             _ptr(out), n_threads)
+    lib(fast).orc_corr_batch_ex(_ptr(samples.view(np.float32)), jobs.ctypes.data, len(jobs), arr, _ptr(lens, ctypes.c_int32),
+                                _ptr(out), n_threads, int(accum_f64))
     return out.view(np.complex64)
 
 

@@ -1,0 +1,82 @@
+"""Galileo E1 tracking correlations on the GPU (SURVEY §8d C4 / C5 shapes) vs the oracle.
+
+dll_pll_veml_tracking with track_pilot = true runs, per channel-epoch, a 5-tap VEML correlator
+on the E1-C pilot replica (shifts ±vel, ±el, 0 in replica samples, 2 per chip; :472-513) and a
+1-tap prompt correlator on the E1-B data replica with the same NCO (:526-532).  Both are jobs of
+one batch here.  N = 100000 (4 ms at 25 Msps) and 200000 (50 Msps ibyte).
+Tolerance: at N ≥ 1e5 the reference's serial float accumulation is itself ~1e-5 away from the exact
+sum of its own float products (a √N random walk of half-ulps of the accumulator; measured up to
+1.4e-5 here).  So the 1e-5 per-tap contract is applied against the oracle with the same float
+products accumulated in double (oracle corr_batch(accum_f64=True)), and against the serial
+oracle the bound is 1e-5 plus that oracle's own distance to the exact accumulation.  Errors are
+relative to max(|ref|, ‖x‖₂) (‖x‖₂ only matters for a tap at the noise floor).
+"""
+import numpy as np
+import pytest
+
+from gnss_sim_receiver_amd import engine, signals
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-5
+VEML = [-0.5, -0.25, 0.0, 0.25, 0.5]  # Dll_Pll_Conf defaults (very_early_late 0.5, early_late 0.25 chips)
+
+
+def e1_jobs(sats, fs, n_ep, vl):
+    jobs, cl = [], []
+    for k, s in enumerate(sats):
+        cl += [s.code, s.code_data]
+        pj = signals.truth_jobs(s, fs, n_ep, vl, [2 * x for x in VEML], 2 * k)  # pilot, shifts in replica samples
+        dj = pj.copy()
+        dj["code_id"] = 2 * k + 1
+        dj["n_taps"] = 1
+        dj["shifts_chips"] = 0.0
+        jobs += [pj, dj]
+    return np.concatenate(jobs), cl
+
+
+def check(out, sig, jobs, codes):
+    r32 = O.corr_batch(sig, jobs, codes, n_threads=8)
+    r64 = O.corr_batch(sig, jobs, codes, n_threads=8, accum_f64=True)
+    worst = 0.0
+    for j in range(len(jobs)):
+        t = jobs[j]["n_taps"]
+        o, n = jobs[j]["sample_offset"], jobs[j]["n_samples"]
+        scale = np.maximum(np.abs(r64[j, :t]), float(np.linalg.norm(sig[o:o + n].astype(np.complex128))))
+        e64 = np.abs(out[j, :t] - r64[j, :t]) / scale
+        serial = np.abs(r32[j, :t] - r64[j, :t]) / scale
+        e32 = np.abs(out[j, :t] - r32[j, :t]) / scale
+        assert np.all(e64 <= TOL), (j, e64)
+        assert np.all(e32 <= TOL + serial), (j, e32, serial)
+        assert np.all(out[j, t:] == 0)
+        worst = max(worst, float(e64.max()))
+    return worst
+
+
+def test_c4_e1_pilot_veml_and_data_prompt(ctx):
+    fs, vl, n_ep = 25e6, 100000, 2
+    sats = signals.random_sky(8, seed=404, system="GAL", cn0=45.0, prns=[1, 5, 12, 19, 24, 30, 33, 36])
+    sig = signals.generate_if(fs, vl * (n_ep + 2), sats, seed=44)
+    jobs, cl = e1_jobs(sats, fs, n_ep, vl)
+    rng = np.random.default_rng(1)
+    jobs["rem_carrier_phase_rad"] += rng.uniform(-0.2, 0.2, len(jobs)).astype(np.float32)
+    out = engine.correlate_host(ctx, sig, jobs, cl)
+    check(out, sig, jobs, cl)
+    # locked truth NCO: prompt pilot and data prompt carry the signal, sinBOC VE/VL taps are the
+    # negative side peaks of the BOC(1,1) correlation (ACF(±0.5 chip) = −0.5)
+    pil = out[jobs["n_taps"] == 5]
+    assert np.all(np.abs(pil[:, 2]) > 3 * np.abs(pil[:, 1]))
+    assert np.all(np.real(pil[:, 0] * np.conj(pil[:, 2])) < 0)
+
+
+def test_c5_e1_ibyte_50msps(ctx):
+    fs, vl = 50e6, 200000
+    sats = signals.random_sky(3, seed=505, system="GAL", cn0=48.0, prns=[2, 9, 21])
+    for s in sats:
+        s.f_if_hz = 7.161e6  # C5: IF centred at 1568.259 MHz
+    x = signals.generate_if(fs, vl * 3, sats, seed=55)
+    raw = signals.to_ibyte(x)
+    as_float = raw.astype(np.float32).view(np.complex64)
+    jobs, cl = e1_jobs(sats, fs, 1, vl)
+    out = engine.correlate_host(ctx, raw, jobs, cl)
+    check(out, as_float, jobs, cl)
