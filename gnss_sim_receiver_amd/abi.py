@@ -71,6 +71,55 @@ class AcqResult(ctypes.Structure):
     ]
 
 
+SYS_GPS_L1CA, SYS_GAL_E1, SYS_BDS_B1I = 0, 1, 2
+
+
+class TrkConf(ctypes.Structure):
+    """gnsship_trk_conf — Dll_Pll_Conf (dll_pll_conf.h:33-80), same names/units; defaults as there
+    with the gnss_sdr_flags defaults for cn0_samples/cn0_min/max_*lock_fail/carrier_lock_th."""
+    _fields_ = [
+        ("fs_in", ctypes.c_double), ("carrier_lock_th", ctypes.c_double),
+        ("pll_bw_hz", ctypes.c_float), ("dll_bw_hz", ctypes.c_float), ("fll_bw_hz", ctypes.c_float),
+        ("early_late_space_chips", ctypes.c_float), ("very_early_late_space_chips", ctypes.c_float),
+        ("slope", ctypes.c_float), ("spc", ctypes.c_float), ("y_intercept", ctypes.c_float),
+        ("cn0_smoother_alpha", ctypes.c_float), ("carrier_lock_test_smoother_alpha", ctypes.c_float),
+        ("pull_in_time_s", ctypes.c_uint32), ("bit_synchronization_time_limit_s", ctypes.c_uint32),
+        ("vector_length", ctypes.c_uint32),
+        ("pll_filter_order", ctypes.c_int32), ("dll_filter_order", ctypes.c_int32),
+        ("cn0_samples", ctypes.c_int32), ("cn0_smoother_samples", ctypes.c_int32),
+        ("carrier_lock_test_smoother_samples", ctypes.c_int32), ("cn0_min", ctypes.c_int32),
+        ("max_code_lock_fail", ctypes.c_int32), ("max_carrier_lock_fail", ctypes.c_int32),
+        ("carrier_aiding", ctypes.c_int32), ("track_pilot", ctypes.c_int32), ("system", ctypes.c_int32),
+    ]
+
+    @classmethod
+    def defaults(cls, system: int, fs_in: float, vector_length: int, **kw) -> "TrkConf":
+        c = cls(fs_in=fs_in, carrier_lock_th=0.7, pll_bw_hz=35.0, dll_bw_hz=2.0, fll_bw_hz=35.0,
+                early_late_space_chips=0.25, very_early_late_space_chips=0.5, slope=1.0, spc=0.5, y_intercept=1.0,
+                cn0_smoother_alpha=0.002, carrier_lock_test_smoother_alpha=0.002, pull_in_time_s=10,
+                bit_synchronization_time_limit_s=20, vector_length=vector_length, pll_filter_order=3, dll_filter_order=2,
+                cn0_samples=20, cn0_smoother_samples=200, carrier_lock_test_smoother_samples=25, cn0_min=25,
+                max_code_lock_fail=50, max_carrier_lock_fail=5000, carrier_aiding=1, track_pilot=1, system=system)
+        for k, v in kw.items():
+            setattr(c, k, v)
+        return c
+
+
+class TrkStartArgs(ctypes.Structure):
+    """gnsship_trk_start_args — the Gnss_Synchro fields start_tracking reads (:647-649)."""
+    _fields_ = [("code_id", ctypes.c_int32), ("data_code_id", ctypes.c_int32), ("acq_delay_samples", ctypes.c_double),
+                ("acq_doppler_hz", ctypes.c_double), ("acq_samplestamp_samples", ctypes.c_uint64), ("first_sample", ctypes.c_uint64)]
+
+
+TRK_EPOCH_DTYPE = np.dtype([
+    ("sample_counter", "<u8"), ("prompt_i", "<f8"), ("prompt_q", "<f8"), ("code_phase_samples", "<f8"),
+    ("carrier_phase_rads", "<f8"), ("carrier_doppler_hz", "<f8"), ("cn0_db_hz", "<f8"), ("carrier_lock_test", "<f4"),
+    ("state", "<i4"), ("flags", "<i4"), ("pad", "<i4"), ("code_freq_chips", "<f8"), ("rem_code_phase_chips", "<f8"),
+    ("rem_carr_phase_rad", "<f4"), ("prn_length_samples", "<i4"),
+])
+assert TRK_EPOCH_DTYPE.itemsize == 96
+
+
 class GnssHipError(RuntimeError):
     def __init__(self, code: int, what: str):
         super().__init__(f"{what} failed: {_ERRNAMES.get(code, code)}")
@@ -122,6 +171,12 @@ _SIGNATURES = {
     "gnsship_acq_run": ([_vp, _vp, _i, _i, _i, ctypes.POINTER(AcqResult), _f32p], _i),
     "gnsship_acq_num_bins": ([_vp, ctypes.POINTER(_i)], _i),
     "gnsship_acq_destroy": ([_vp], _i),
+    "gnsship_trk_create": ([_vp, ctypes.POINTER(TrkConf), _i, _vpp], _i),
+    "gnsship_trk_start": ([_vp, _i, ctypes.POINTER(TrkStartArgs)], _i),
+    "gnsship_trk_stop": ([_vp, _i], _i),
+    "gnsship_trk_run": ([_vp, _vp, _i, _i, ctypes.c_uint64, ctypes.c_int64, _i, _vp, ctypes.POINTER(_i)], _i),
+    "gnsship_trk_channel_state": ([_vp, _i, ctypes.POINTER(_i), ctypes.POINTER(ctypes.c_uint64)], _i),
+    "gnsship_trk_destroy": ([_vp], _i),
 }
 
 

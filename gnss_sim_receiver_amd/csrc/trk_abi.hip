@@ -1,0 +1,438 @@
+// trk_abi.hip — C-ABI of the device-resident tracking loop (include/gnsship.h, gnsship_trk_*).
+//
+// Host side of dll_pll_veml_tracking: the constructor's per-signal constants (:142-330), the
+// loop-filter / smoother set-up (:462-466, :540-553, Tracking_loop_filter::update_coefficients
+// tracking_loop_filter.cc:100-200, Tracking_FLL_PLL_filter::set_params :23-55), and
+// start_tracking + the state-1 pull-in (:643-883, :1757-1788).  The per-epoch loop runs on the
+// device (trk_kernel.hip) between fixed-plan correlator launches.
+#include <cmath>
+#include <cstddef>
+#include <cstring>
+#include <new>
+#include <vector>
+
+#include "engine.h"
+#include "trk_engine.h"
+
+namespace gnsship {
+int fail(gnsship_ctx* ctx, int code, const char* what);
+int hip_fail(gnsship_ctx* ctx, hipError_t e, const char* where);
+int set_device(gnsship_ctx* ctx);
+int sync_code_table(gnsship_ctx* ctx);
+size_t fmt_bytes(int fmt);
+int plan_chunks(std::vector<DevJob>& jobs, std::vector<ChunkDesc>& chunks, bool& any_multi, int64_t* n_anchors, ChunkClass* classes);
+}  // namespace gnsship
+
+using namespace gnsship;
+static_assert(sizeof(gnsship_trk_epoch) == 96, "gnsship_trk_epoch layout");
+
+#define HIP_TRY(ctx, expr)                                       \
+    do {                                                         \
+        hipError_t _e = (expr);                                  \
+        if (_e != hipSuccess) return hip_fail((ctx), _e, #expr); \
+    } while (0)
+
+struct gnsship_trk {
+    gnsship_ctx* ctx = nullptr;
+    TrkParams params{};
+    int max_channels = 0;
+    int n_jobs = 0, n_chunks = 0;
+    bool any_multi = false;
+    ChunkClass classes[kChunkClasses]{};
+    std::vector<TrkChannel> host_chans;
+    TrkParams* params_dev = nullptr;
+    TrkChannel* chans_dev = nullptr;
+    DevJob* jobs_dev = nullptr;
+    ChunkDesc* chunks_dev = nullptr;
+    Anchor* anchors_dev = nullptr;
+    float* partials_dev = nullptr;
+    float* out_dev = nullptr;
+    gnsship_trk_epoch* rec_dev = nullptr;
+    size_t rec_cap = 0;
+    int* ran_dev = nullptr;
+    size_t ran_cap = 0;
+    void* stage_dev = nullptr;
+    size_t stage_cap = 0;
+};
+
+namespace {
+
+void set_bits(uint32_t* bits, const char* s)
+{
+    for (int i = 0; s[i]; i++)
+        if (s[i] == '1') bits[i >> 5] |= 1u << (i & 31);
+}
+
+// GPS L1 C/A preamble 10001011 at 20 symbols per bit (GPS_L1_CA.h:73, IS-GPS-200 TLM word)
+void gps_preamble_symbols(char* out)
+{
+    const char bits[] = "10001011";
+    int n = 0;
+    for (int b = 0; b < 8; b++)
+        for (int r = 0; r < 20; r++) out[n++] = bits[b];
+    out[n] = '\0';
+}
+
+// Tracking_loop_filter::update_coefficients (tracking_loop_filter.cc:100-200), no last integrator
+// (the tracking block constructs it with include_last_integrator = false, :465).
+void loop_filter_coefficients(float T, float bw, int order, TrkParams& p)
+{
+    const float zeta = 1.0F / std::sqrt(2.0F);
+    float g1, g2, g3, wn;
+    switch (order) {
+    case 1:
+        wn = bw * 4.0F;
+        g1 = wn;
+        p.lf_n_in = 1;
+        p.lf_in[0] = g1;
+        p.lf_n_out = 0;
+        break;
+    case 2:
+        wn = bw * (8.0F * zeta) / (4.0F * zeta * zeta + 1.0F);
+        g1 = wn * wn;
+        g2 = wn * 2.0F * zeta;
+        p.lf_n_in = 2;
+        p.lf_in[0] = static_cast<float>(g1 * T / 2.0 + g2);
+        p.lf_in[1] = static_cast<float>(g1 * T / 2.0 - g2);
+        p.lf_n_out = 1;
+        p.lf_out[0] = 1.0F;
+        break;
+    default: {
+        wn = bw / 0.7845F;
+        const float a3 = 1.1F, b3 = 2.4F;
+        g1 = wn * wn * wn;
+        g2 = a3 * wn * wn;
+        g3 = b3 * wn;
+        p.lf_n_in = 3;
+        p.lf_in[0] = static_cast<float>(g3 + T / 2.0 * (g2 + T / 2.0 * g1));
+        p.lf_in[1] = static_cast<float>(g1 * T * T / 2.0 - 2.0 * g3);
+        p.lf_in[2] = static_cast<float>(g3 + T / 2.0 * (-g2 + T / 2.0 * g1));
+        p.lf_n_out = 2;
+        p.lf_out[0] = 2.0F;
+        p.lf_out[1] = -1.0F;
+    } break;
+    }
+}
+
+bool build_params(const gnsship_trk_conf& c, TrkParams& p)
+{
+    std::memset(&p, 0, sizeof(p));
+    p.conf = c;
+    char sec[kTrkMaxSecondary + 1] = {0};
+    switch (c.system) {
+    case GNSSHIP_SYS_GPS_L1CA:  // :142-200 (1C), start_tracking :662-668 forces track_pilot = false
+        p.code_chip_rate = 1.023e6;
+        p.carrier_freq = 1575.42e6;
+        p.code_period = 0.001;
+        p.code_length_chips = 1023;
+        p.code_samples_per_chip = 1;
+        p.symbols_per_bit = 20;
+        p.veml = 0;
+        p.track_pilot = 0;
+        p.secondary = 0;
+        gps_preamble_symbols(sec);
+        p.secondary_len = 160;
+        set_bits(p.secondary_bits, sec);
+        break;
+    case GNSSHIP_SYS_GAL_E1:  // :262-291 (1B); Galileo_E1.h:35-52
+        p.code_chip_rate = 1.023e6;
+        p.carrier_freq = 1575.42e6;
+        p.code_period = 0.004;
+        p.code_length_chips = 4092;
+        p.code_samples_per_chip = 2;
+        p.symbols_per_bit = 1;
+        p.veml = 1;
+        p.track_pilot = c.track_pilot ? 1 : 0;
+        if (p.track_pilot) {
+            p.secondary = 1;
+            p.secondary_len = 25;
+            set_bits(p.secondary_bits, "0011100000001010110110010");  // CS25 (GALILEO_E1_C_SECONDARY_CODE)
+        }
+        break;
+    case GNSSHIP_SYS_BDS_B1I:  // :762-797 (MEO/IGSO branch); Beidou_B1I.h:35-48
+        p.code_chip_rate = 2.046e6;
+        p.carrier_freq = 1561.098e6;
+        p.code_period = 0.001;
+        p.code_length_chips = 2046;
+        p.code_samples_per_chip = 1;
+        p.symbols_per_bit = 20;
+        p.veml = 0;
+        p.track_pilot = 0;
+        p.secondary = 1;
+        p.secondary_len = 20;
+        set_bits(p.secondary_bits, "00000100110101001110");  // NH code (BEIDOU_B1I_SECONDARY_CODE_STR)
+        p.data_secondary_len = 20;
+        set_bits(p.data_secondary_bits, "00000100110101001110");
+        break;
+    default: return false;
+    }
+    p.n_taps = p.veml ? 5 : 3;
+    const float spcf = static_cast<float>(p.code_samples_per_chip);
+    if (p.veml) {
+        p.shifts[0] = -c.very_early_late_space_chips * spcf;
+        p.shifts[1] = -c.early_late_space_chips * spcf;
+        p.shifts[2] = 0.0F;
+        p.shifts[3] = c.early_late_space_chips * spcf;
+        p.shifts[4] = c.very_early_late_space_chips * spcf;
+    } else {
+        p.shifts[0] = -c.early_late_space_chips * spcf;
+        p.shifts[1] = 0.0F;
+        p.shifts[2] = c.early_late_space_chips * spcf;
+    }
+    loop_filter_coefficients(static_cast<float>(p.code_period), c.dll_bw_hz, c.dll_filter_order, p);
+    // Tracking_FLL_PLL_filter::set_params (tracking_FLL_PLL_filter.cc:23-55)
+    p.fp_order = c.pll_filter_order;
+    if (p.fp_order == 3) {
+        p.fp_b3 = 2.400F;
+        p.fp_a3 = 1.100F;
+        p.fp_a2 = 1.414F;
+        p.fp_w0p = c.pll_bw_hz / 0.7845F;
+        p.fp_w0p2 = p.fp_w0p * p.fp_w0p;
+        p.fp_w0p3 = p.fp_w0p2 * p.fp_w0p;
+        p.fp_w0f = c.fll_bw_hz / 0.53F;
+        p.fp_w0f2 = p.fp_w0f * p.fp_w0f;
+    } else {
+        p.fp_a2 = 1.414F;
+        p.fp_w0p = c.pll_bw_hz / 0.53F;
+        p.fp_w0p2 = p.fp_w0p * p.fp_w0p;
+        p.fp_w0f = c.fll_bw_hz / 0.25F;
+    }
+    // Exponential_Smoother settings (:540-553, exponential_smoother.cc:29-73)
+    auto clamp01 = [](float a) { return a < 0.0F ? 0.0F : (a > 1.0F ? 1.0F : a); };
+    p.cn0_alpha = clamp01(c.cn0_smoother_alpha);
+    p.cn0_one_minus_alpha = 1.0F - p.cn0_alpha;
+    p.cn0_min_value = 25.0F;
+    p.cn0_offset = 12.0F;
+    int ns = c.cn0_smoother_samples / static_cast<int>(p.code_period * 1000.0);
+    p.cn0_init_samples = ns <= 0 ? 1 : ns;
+    p.lock_alpha = clamp01(c.carrier_lock_test_smoother_alpha);
+    p.lock_one_minus_alpha = 1.0F - p.lock_alpha;
+    p.lock_min_value = -1.0F;
+    p.lock_offset = 0.0F;
+    p.lock_init_samples = c.carrier_lock_test_smoother_samples <= 0 ? 1 : c.carrier_lock_test_smoother_samples;
+    p.jobs_per_channel = p.track_pilot ? 2 : 1;
+    p.chunks_per_job = (static_cast<int>(c.vector_length) + kCorrChunk - 1) / kCorrChunk;
+    return true;
+}
+
+void release(gnsship_trk* t)
+{
+    void* ptrs[] = {t->params_dev, t->chans_dev, t->jobs_dev, t->chunks_dev, t->anchors_dev, t->partials_dev, t->out_dev, t->rec_dev, t->ran_dev,
+        t->stage_dev};
+    for (void* p : ptrs)
+        if (p) (void)hipFree(p);
+}
+
+}  // namespace
+
+extern "C" int gnsship_trk_destroy(gnsship_trk* t)
+{
+    if (!t) return GNSSHIP_E_INVAL;
+    (void)hipSetDevice(t->ctx->device);
+    (void)hipStreamSynchronize(t->ctx->stream);
+    release(t);
+    delete t;
+    return GNSSHIP_OK;
+}
+
+extern "C" int gnsship_trk_create(gnsship_ctx* ctx, const gnsship_trk_conf* conf, int max_channels, gnsship_trk** out)
+{
+    if (!ctx || !conf || !out) return GNSSHIP_E_INVAL;
+    *out = nullptr;
+    if (max_channels < 1 || conf->fs_in <= 0.0 || conf->vector_length < 1 || conf->cn0_samples < 1 || conf->cn0_samples > kTrkMaxCn0Samples ||
+        conf->pll_filter_order < 2 || conf->pll_filter_order > 3 || conf->dll_filter_order < 1 || conf->dll_filter_order > 3)
+        return fail(ctx, GNSSHIP_E_INVAL, "gnsship_trk_create: bad configuration (cn0_samples 1..64, pll order 2..3, dll order 1..3)");
+    gnsship_trk* t = new (std::nothrow) gnsship_trk();
+    if (!t) return GNSSHIP_E_NOMEM;
+    t->ctx = ctx;
+    if (!build_params(*conf, t->params)) {
+        delete t;
+        return fail(ctx, GNSSHIP_E_INVAL, "gnsship_trk_create: unknown system");
+    }
+    if (int rc = set_device(ctx)) {
+        delete t;
+        return rc;
+    }
+    t->max_channels = max_channels;
+    const TrkParams& p = t->params;
+    t->n_jobs = max_channels * p.jobs_per_channel;
+    std::vector<DevJob> jobs(t->n_jobs);
+    for (int i = 0; i < t->n_jobs; i++) {
+        std::memset(&jobs[i], 0, sizeof(DevJob));
+        jobs[i].n_samples = static_cast<int32_t>(conf->vector_length);
+        jobs[i].n_taps = (p.jobs_per_channel == 2 && (i % 2) == 1) ? 1 : p.n_taps;
+        jobs[i].in_margin = 0;
+    }
+    std::vector<ChunkDesc> chunks;
+    int64_t n_anchors = 0;
+    t->n_chunks = plan_chunks(jobs, chunks, t->any_multi, &n_anchors, t->classes);
+    for (auto& j : jobs) j.n_samples = 0;  // idle until a channel starts
+    for (auto& c : chunks) c.len = 0;
+    t->host_chans.assign(max_channels, TrkChannel{});
+    for (auto& c : t->host_chans) std::memset(&c, 0, sizeof(TrkChannel));
+    hipError_t e = hipMalloc(&t->params_dev, sizeof(TrkParams));
+    if (e == hipSuccess) e = hipMemcpy(t->params_dev, &t->params, sizeof(TrkParams), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMalloc(&t->chans_dev, sizeof(TrkChannel) * max_channels);
+    if (e == hipSuccess) e = hipMemcpy(t->chans_dev, t->host_chans.data(), sizeof(TrkChannel) * max_channels, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMalloc(&t->jobs_dev, sizeof(DevJob) * t->n_jobs);
+    if (e == hipSuccess) e = hipMemcpy(t->jobs_dev, jobs.data(), sizeof(DevJob) * t->n_jobs, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMalloc(&t->chunks_dev, sizeof(ChunkDesc) * t->n_chunks);
+    if (e == hipSuccess) e = hipMemcpy(t->chunks_dev, chunks.data(), sizeof(ChunkDesc) * t->n_chunks, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMalloc(&t->anchors_dev, sizeof(Anchor) * static_cast<size_t>(n_anchors));
+    if (e == hipSuccess) e = hipMalloc(&t->partials_dev, sizeof(float) * 2 * kMaxTaps * static_cast<size_t>(t->n_chunks));
+    if (e == hipSuccess) e = hipMalloc(&t->out_dev, sizeof(float) * 2 * kMaxTaps * static_cast<size_t>(t->n_jobs));
+    if (e != hipSuccess) {
+        release(t);
+        delete t;
+        return hip_fail(ctx, e, "gnsship_trk_create");
+    }
+    *out = t;
+    return GNSSHIP_OK;
+}
+
+// start_tracking (:643-883) and the state-1 pull-in (:1757-1788) at nitems_read = first_sample.
+extern "C" int gnsship_trk_start(gnsship_trk* t, int channel, const gnsship_trk_start_args* a)
+{
+    if (!t) return GNSSHIP_E_INVAL;
+    gnsship_ctx* ctx = t->ctx;
+    if (!a || channel < 0 || channel >= t->max_channels) return fail(ctx, GNSSHIP_E_INVAL, "gnsship_trk_start: bad channel / arguments");
+    if (a->code_id < 0 || a->code_id >= static_cast<int>(ctx->codes_host.size()) || !ctx->codes_host[a->code_id].ptr)
+        return fail(ctx, GNSSHIP_E_STATE, "gnsship_trk_start: tracking code not in the code bank");
+    const TrkParams& p = t->params;
+    if (p.track_pilot && (a->data_code_id < 0 || a->data_code_id >= static_cast<int>(ctx->codes_host.size()) || !ctx->codes_host[a->data_code_id].ptr))
+        return fail(ctx, GNSSHIP_E_STATE, "gnsship_trk_start: data code not in the code bank");
+    if (a->first_sample < a->acq_samplestamp_samples) return fail(ctx, GNSSHIP_E_INVAL, "gnsship_trk_start: first_sample before the acquisition stamp");
+    TrkChannel c;
+    std::memset(&c, 0, sizeof(c));
+    const gnsship_trk_conf& k = p.conf;
+    c.code_id = a->code_id;
+    c.data_code_id = p.track_pilot ? a->data_code_id : a->code_id;
+    c.acq_sample_stamp = a->acq_samplestamp_samples;
+    c.carrier_doppler_hz = a->acq_doppler_hz;
+    c.carrier_phase_step_rad = 2.0 * M_PI * c.carrier_doppler_hz / k.fs_in;
+    c.carrier_lock_test = 1.0F;
+    c.cn0_db_hz = 0.0F;
+    c.spc = k.spc;
+    // carrier filter initialize(acq doppler); code filter initialize(0) (tracking_loop_filter.cc:50-56)
+    if (p.fp_order == 3) {
+        c.fp_x = 2.0F * static_cast<float>(a->acq_doppler_hz);
+        c.fp_w = 0.0F;
+    } else {
+        c.fp_w = static_cast<float>(a->acq_doppler_hz);
+        c.fp_x = 0.0F;
+    }
+    c.lf_idx = 3;
+    c.cn0_sm.initializing = 1;
+    c.lock_sm.initializing = 1;
+    c.cloop = 1;
+    c.pull_in = 1;
+    // state 1
+    const int64_t diff = static_cast<int64_t>(a->first_sample) - static_cast<int64_t>(c.acq_sample_stamp);
+    const double delta = static_cast<double>(diff) - a->acq_delay_samples;
+    c.code_freq_chips = p.code_chip_rate;
+    c.code_phase_step_chips = c.code_freq_chips / k.fs_in;
+    const double T_chip = 1.0 / c.code_freq_chips;
+    const double T_prn = T_chip * static_cast<double>(p.code_length_chips);
+    const double T_prn_samples = T_prn * k.fs_in;
+    const double acq_code_phase_samples = T_prn_samples - std::fmod(delta, T_prn_samples);
+    c.current_prn_length_samples = static_cast<int32_t>(std::round(T_prn_samples));
+    const int32_t samples_offset = static_cast<int32_t>(std::round(acq_code_phase_samples));
+    c.acc_carrier_phase_rad -= c.carrier_phase_step_rad * static_cast<double>(samples_offset);
+    c.state = 2;
+    c.nitems_read = a->first_sample + static_cast<uint64_t>(samples_offset);
+    if (int rc = set_device(ctx)) return rc;
+    HIP_TRY(ctx, hipMemcpyAsync(t->chans_dev + channel, &c, sizeof(TrkChannel), hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    return GNSSHIP_OK;
+}
+
+extern "C" int gnsship_trk_stop(gnsship_trk* t, int channel)
+{
+    if (!t) return GNSSHIP_E_INVAL;
+    gnsship_ctx* ctx = t->ctx;
+    if (channel < 0 || channel >= t->max_channels) return fail(ctx, GNSSHIP_E_INVAL, "gnsship_trk_stop: bad channel");
+    if (int rc = set_device(ctx)) return rc;
+    const int32_t zero = 0;
+    HIP_TRY(ctx, hipMemcpyAsync(reinterpret_cast<char*>(t->chans_dev + channel) + offsetof(TrkChannel, state), &zero, sizeof(zero),
+                     hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    return GNSSHIP_OK;
+}
+
+extern "C" int gnsship_trk_channel_state(gnsship_trk* t, int channel, int* state, uint64_t* next_sample)
+{
+    if (!t) return GNSSHIP_E_INVAL;
+    gnsship_ctx* ctx = t->ctx;
+    if (channel < 0 || channel >= t->max_channels) return fail(ctx, GNSSHIP_E_INVAL, "gnsship_trk_channel_state: bad channel");
+    if (int rc = set_device(ctx)) return rc;
+    TrkChannel c;
+    HIP_TRY(ctx, hipMemcpyAsync(&c, t->chans_dev + channel, sizeof(TrkChannel), hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    if (state) *state = c.state;
+    if (next_sample) *next_sample = c.nitems_read;
+    return GNSSHIP_OK;
+}
+
+extern "C" int gnsship_trk_run(gnsship_trk* t, const void* sig, int fmt, int sig_on_device, uint64_t buffer_first_sample, int64_t n_buffer_samples,
+    int max_rounds, gnsship_trk_epoch* out, int* rounds_done)
+{
+    if (!t) return GNSSHIP_E_INVAL;
+    gnsship_ctx* ctx = t->ctx;
+    if (!sig || n_buffer_samples < 0 || max_rounds < 0 || fmt_bytes(fmt) == 0) return fail(ctx, GNSSHIP_E_INVAL, "gnsship_trk_run: bad arguments");
+    if (rounds_done) *rounds_done = 0;
+    if (max_rounds == 0) return GNSSHIP_OK;
+    if (int rc = set_device(ctx)) return rc;
+    if (int rc = sync_code_table(ctx)) return rc;
+    int max_len = 1;
+    for (const auto& cd : ctx->codes_host)
+        if (cd.ptr && cd.len > max_len) max_len = cd.len;
+    const void* src = sig;
+    if (!sig_on_device) {
+        const size_t bytes = fmt_bytes(fmt) * static_cast<size_t>(n_buffer_samples);
+        if (t->stage_cap < bytes) {
+            if (t->stage_dev) HIP_TRY(ctx, hipFree(t->stage_dev));
+            t->stage_dev = nullptr;
+            HIP_TRY(ctx, hipMalloc(&t->stage_dev, bytes));
+            t->stage_cap = bytes;
+        }
+        HIP_TRY(ctx, hipMemcpyAsync(t->stage_dev, sig, bytes, hipMemcpyHostToDevice, ctx->stream));
+        src = t->stage_dev;
+    }
+    const size_t nrec = static_cast<size_t>(max_rounds) * t->max_channels;
+    if (out && t->rec_cap < nrec) {
+        if (t->rec_dev) HIP_TRY(ctx, hipFree(t->rec_dev));
+        t->rec_dev = nullptr;
+        HIP_TRY(ctx, hipMalloc(&t->rec_dev, sizeof(gnsship_trk_epoch) * nrec));
+        t->rec_cap = nrec;
+    }
+    if (t->ran_cap < static_cast<size_t>(max_rounds) + 1) {
+        if (t->ran_dev) HIP_TRY(ctx, hipFree(t->ran_dev));
+        t->ran_dev = nullptr;
+        HIP_TRY(ctx, hipMalloc(&t->ran_dev, sizeof(int) * (max_rounds + 1)));
+        t->ran_cap = static_cast<size_t>(max_rounds) + 1;
+    }
+    HIP_TRY(ctx, hipMemsetAsync(t->ran_dev, 0, sizeof(int) * (max_rounds + 1), ctx->stream));
+    const int nc = t->max_channels;
+    for (int r = 0; r <= max_rounds; r++) {
+        const int consume = r > 0 ? 1 : 0, emit = r < max_rounds ? 1 : 0;
+        gnsship_trk_epoch* rec = (out && r > 0) ? t->rec_dev + static_cast<size_t>(r - 1) * nc : nullptr;
+        hipError_t e = launch_trk_step(t->params_dev, t->chans_dev, nc, t->jobs_dev, t->chunks_dev, t->out_dev, buffer_first_sample, n_buffer_samples,
+            consume, emit, rec, t->ran_dev + r, ctx->stream);
+        if (e != hipSuccess) return hip_fail(ctx, e, "launch_trk_step");
+        if (!emit) break;
+        e = launch_corr_batch(src, fmt, t->jobs_dev, t->n_jobs, t->chunks_dev, t->n_chunks, t->classes, ctx->codes_dev, max_len, t->any_multi,
+            t->anchors_dev, t->partials_dev, t->out_dev, ctx->stream);
+        if (e != hipSuccess) return hip_fail(ctx, e, "launch_corr_batch(tracking)");
+    }
+    std::vector<int> ran(max_rounds + 1);
+    HIP_TRY(ctx, hipMemcpyAsync(ran.data(), t->ran_dev, sizeof(int) * (max_rounds + 1), hipMemcpyDeviceToHost, ctx->stream));
+    if (out) HIP_TRY(ctx, hipMemcpyAsync(out, t->rec_dev, sizeof(gnsship_trk_epoch) * nrec, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    if (rounds_done) {
+        int n = 0;
+        for (int r = 0; r < max_rounds; r++)
+            if (ran[r] > 0) n = r + 1;
+        *rounds_done = n;
+    }
+    return GNSSHIP_OK;
+}

@@ -1,0 +1,78 @@
+// trk_engine.h — internal types of the device-resident tracking loop (not part of the C ABI).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+#include "engine.h"
+#include "gnsship.h"
+
+namespace gnsship {
+
+constexpr int kTrkMaxSecondary = 256;  // longest sign pattern searched (GPS preamble: 160 symbols)
+constexpr int kTrkMaxCn0Samples = 64;  // prompt buffer of the CN0 / carrier-lock estimators
+
+// Signal constants the reference selects per system/signal (dll_pll_veml_tracking.cc:142-330,
+// start_tracking :662-826) plus the loop-filter coefficients derived from Dll_Pll_Conf once.
+struct TrkParams {
+    gnsship_trk_conf conf;
+    double code_chip_rate, carrier_freq, code_period;
+    int32_t code_length_chips, code_samples_per_chip, symbols_per_bit, veml, track_pilot;
+    int32_t secondary, secondary_len, data_secondary_len, n_taps;
+    uint32_t secondary_bits[kTrkMaxSecondary / 32];       // bit i = character i == '1'
+    uint32_t data_secondary_bits[kTrkMaxSecondary / 32];
+    float shifts[5];                                        // d_local_code_shift_chips (× samples per chip)
+    // Tracking_loop_filter (code) coefficients
+    float lf_in[4], lf_out[3];
+    int32_t lf_n_in, lf_n_out;
+    // Tracking_FLL_PLL_filter constants
+    float fp_w0p3, fp_w0f2, fp_a2, fp_w0f, fp_a3, fp_w0p2, fp_b3, fp_w0p;
+    int32_t fp_order;
+    // Exponential_Smoother settings
+    float cn0_alpha, cn0_one_minus_alpha, cn0_min_value, cn0_offset;
+    int32_t cn0_init_samples;
+    float lock_alpha, lock_one_minus_alpha, lock_min_value, lock_offset;
+    int32_t lock_init_samples;
+    // job layout
+    int32_t jobs_per_channel;  // 1, or 2 with the E1 data prompt
+    int32_t chunks_per_job;
+};
+
+struct Smoother {
+    float old_value, init_sum;
+    int32_t initializing, counter;
+};
+
+// One channel: the dll_pll_veml_tracking members the per-epoch path reads or writes.
+struct TrkChannel {
+    int32_t state;  // 0 idle / lost, 2 wide tracking, 4 narrow tracking
+    int32_t cloop, pull_in, pll_180, ran, acc_phase_init;
+    int32_t code_id, data_code_id;
+    uint64_t acq_sample_stamp;
+    uint64_t nitems_read;      // absolute index of the next input sample
+    uint64_t epoch_start;      // nitems_read of the epoch whose correlation is in flight
+    double carrier_doppler_hz, carrier_phase_step_rad, code_freq_chips, code_phase_step_chips;
+    double rem_code_phase_chips, rem_code_phase_samples, acc_carrier_phase_rad;
+    double carr_phase_error_hz, carr_error_filt_hz, code_error_chips, code_error_filt_chips, K_blk_samples;
+    float rem_carr_phase_rad;
+    int32_t current_prn_length_samples;
+    float spc;
+    float ve[2], e[2], p[2], l[2], vl[2], p_data[2];
+    int32_t cn0_counter, carrier_fail, code_fail, current_symbol, current_data_symbol;
+    float cn0_db_hz, carrier_lock_test;
+    float prompt_buf[2 * kTrkMaxCn0Samples];
+    uint32_t sign_bits[kTrkMaxSecondary / 32];  // d_Prompt_circular_buffer (real < 0), oldest first
+    int32_t sign_count;
+    // Tracking_loop_filter state
+    float lf_inputs[4], lf_outputs[4];
+    int32_t lf_idx;
+    // Tracking_FLL_PLL_filter state
+    float fp_w, fp_x;
+    Smoother cn0_sm, lock_sm;
+};
+
+// One round: consume the previous epoch's correlations (when `consume`), then lay down the next
+// epoch's jobs / chunk lengths for every channel whose window is in the buffer (when `emit`).
+hipError_t launch_trk_step(const TrkParams* params, TrkChannel* chans, int n_chans, DevJob* jobs, ChunkDesc* chunks, const float* corr_out,
+    uint64_t buf_first, int64_t buf_len, int consume, int emit, gnsship_trk_epoch* rec, int* ran_count, hipStream_t stream);
+
+}  // namespace gnsship

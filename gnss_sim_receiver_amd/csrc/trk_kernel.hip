@@ -1,0 +1,461 @@
+// trk_kernel.hip — device-resident DLL/PLL tracking loop, one lane per channel.
+//
+// Per round the host enqueues, without synchronising:
+//   trk_step_kernel(consume, emit) → corr_anchor_kernel → corr_batch_kernel(s) → corr_reduce_kernel
+// The step kernel consumes the correlations of the epoch that just ran (state machine of
+// dll_pll_veml_tracking::general_work states 2 and 4) and writes the next epoch's correlator
+// jobs in place (the job/chunk plan is fixed: every epoch correlates vector_length samples,
+// :1049), so the same launch sequence repeats with no host round trip.
+//
+// Reference functions restated here (types as in the reference):
+//   Tracking_loop_filter::apply           tracking_loop_filter.cc:58-84
+//   Tracking_FLL_PLL_filter::get_carrier_error   tracking_FLL_PLL_filter.cc:72-110
+//   pll_cloop_two_quadrant_atan / pll_four_quadrant_atan / dll_nc_e_minus_l_normalized /
+//   dll_nc_vemlp_normalized               tracking_discriminators.cc:99-160
+//   cn0_m2m4_estimator / carrier_lock_detector   lock_detectors.cc:90-147
+//   Exponential_Smoother::smooth(float)   exponential_smoother.cc:76-105
+//   cn0_and_tracking_lock_status :972-1029, run_dll_pll :1065-1152, update_tracking_vars
+//   :1189-1260, save_correlation_results :1262-1350, acquire_secondary :925-970,
+//   general_work states 2 (:1789-1932) and 4 (:1971-2028).
+// The job derivation repeats derive_job (gnsship_abi.hip) with the device libm: the phasors
+// (cosf/sinf) may differ from glibc's in the last ulp, i.e. ~1e-7 in the correlations.
+#include <cmath>
+
+#include "trk_engine.h"
+
+namespace gnsship {
+
+namespace {
+
+constexpr double kTwoPi = 6.283185307179586476925286766559;
+
+__device__ float smooth(Smoother& s, float raw, float alpha, float one_minus_alpha, float min_value, float offset, int init_samples)
+{
+    float v;
+    if (s.initializing) {
+        s.counter++;
+        v = raw;
+        s.init_sum = __fadd_rn(s.init_sum, v);
+        if (s.counter == init_samples) {
+            s.old_value = __fdiv_rn(s.init_sum, static_cast<float>(s.counter));
+            if (s.old_value < __fadd_rn(min_value, offset)) {
+                s.counter = 0;
+                s.init_sum = 0.0f;
+            } else {
+                s.initializing = 0;
+            }
+        }
+    } else {
+        v = __fadd_rn(__fmul_rn(alpha, raw), __fmul_rn(one_minus_alpha, s.old_value));
+        s.old_value = v;
+    }
+    return v;
+}
+
+__device__ float cn0_m2m4(const float* prompt, int length, float coh_integration_time_s)
+{
+    float psig = 0.0f, m_2 = 0.0f, m_4 = 0.0f, aux;
+    const float n = static_cast<float>(length);
+    for (int i = 0; i < length; i++) {
+        psig = __fadd_rn(psig, fabsf(prompt[2 * i]));
+        aux = __fadd_rn(__fmul_rn(prompt[2 * i + 1], prompt[2 * i + 1]), __fmul_rn(prompt[2 * i], prompt[2 * i]));
+        m_2 = __fadd_rn(m_2, aux);
+        m_4 = __fadd_rn(m_4, __fmul_rn(aux, aux));
+    }
+    psig = __fdiv_rn(psig, n);
+    psig = __fmul_rn(psig, psig);
+    m_2 = __fdiv_rn(m_2, n);
+    m_4 = __fdiv_rn(m_4, n);
+    aux = sqrtf(__fsub_rn(__fmul_rn(__fmul_rn(2.0f, m_2), m_2), m_4));
+    const float snr = isnan(aux) ? __fdiv_rn(psig, __fsub_rn(m_2, psig)) : __fdiv_rn(aux, __fsub_rn(m_2, aux));
+    return __fsub_rn(__fmul_rn(10.0f, log10f(snr)), __fmul_rn(10.0f, log10f(coh_integration_time_s)));
+}
+
+__device__ float carrier_lock_detector(const float* prompt)  // called with length 1 (:989)
+{
+    const float si = prompt[0], sq = prompt[1];
+    const float nbp = __fadd_rn(__fmul_rn(si, si), __fmul_rn(sq, sq));
+    const float nbd = __fsub_rn(__fmul_rn(si, si), __fmul_rn(sq, sq));
+    return __fdiv_rn(nbd, nbp);
+}
+
+__device__ bool lock_status(const TrkParams& k, TrkChannel& c, double coh_integration_time_s)
+{
+    const int ns = k.conf.cn0_samples;
+    if (c.cn0_counter < ns) {
+        c.prompt_buf[2 * c.cn0_counter] = c.p[0];
+        c.prompt_buf[2 * c.cn0_counter + 1] = c.p[1];
+        c.cn0_counter++;
+        return true;
+    }
+    const int slot = c.cn0_counter % ns;
+    c.prompt_buf[2 * slot] = c.p[0];
+    c.prompt_buf[2 * slot + 1] = c.p[1];
+    c.cn0_counter++;
+    const float raw = cn0_m2m4(c.prompt_buf, ns, static_cast<float>(coh_integration_time_s));
+    c.cn0_db_hz = smooth(c.cn0_sm, raw, k.cn0_alpha, k.cn0_one_minus_alpha, k.cn0_min_value, k.cn0_offset, k.cn0_init_samples);
+    c.carrier_lock_test = smooth(c.lock_sm, carrier_lock_detector(c.prompt_buf), k.lock_alpha, k.lock_one_minus_alpha, k.lock_min_value,
+        k.lock_offset, k.lock_init_samples);
+    if (!c.pull_in) {
+        if (static_cast<double>(c.carrier_lock_test) < k.conf.carrier_lock_th)
+            c.carrier_fail++;
+        else if (c.carrier_fail > 0)
+            c.carrier_fail--;
+        if (c.cn0_db_hz < static_cast<float>(k.conf.cn0_min))
+            c.code_fail++;
+        else if (c.code_fail > 0)
+            c.code_fail--;
+    }
+    if (c.carrier_fail > k.conf.max_carrier_lock_fail || c.code_fail > k.conf.max_code_lock_fail) {
+        c.carrier_fail = 0;
+        c.code_fail = 0;
+        return false;
+    }
+    return true;
+}
+
+__device__ float loop_filter_apply(const TrkParams& k, TrkChannel& c, float x)
+{
+    float result = 0.0f;
+    for (int ii = 0; ii < k.lf_n_out; ii++) result = __fadd_rn(result, __fmul_rn(k.lf_out[ii], c.lf_outputs[(c.lf_idx + ii) % 4]));
+    c.lf_idx--;
+    if (c.lf_idx < 0) c.lf_idx += 4;
+    c.lf_inputs[c.lf_idx] = x;
+    for (int ii = 0; ii < k.lf_n_in; ii++) result = __fadd_rn(result, __fmul_rn(k.lf_in[ii], c.lf_inputs[(c.lf_idx + ii) % 4]));
+    c.lf_outputs[c.lf_idx] = result;
+    return result;
+}
+
+__device__ float carrier_filter(const TrkParams& k, TrkChannel& c, float fll, float pll, float T)
+{
+    if (k.fp_order == 3) {
+        c.fp_w = __fadd_rn(c.fp_w, __fmul_rn(T, __fadd_rn(__fmul_rn(k.fp_w0p3, pll), __fmul_rn(k.fp_w0f2, fll))));
+        const float inner = __fadd_rn(__fadd_rn(__fmul_rn(0.5f, c.fp_w), __fmul_rn(__fmul_rn(k.fp_a2, k.fp_w0f), fll)),
+            __fmul_rn(__fmul_rn(k.fp_a3, k.fp_w0p2), pll));
+        c.fp_x = __fadd_rn(c.fp_x, __fmul_rn(T, inner));
+        return __fadd_rn(__fmul_rn(0.5f, c.fp_x), __fmul_rn(__fmul_rn(k.fp_b3, k.fp_w0p), pll));
+    }
+    const float w_new = __fadd_rn(__fadd_rn(c.fp_w, __fmul_rn(__fmul_rn(pll, k.fp_w0p2), T)), __fmul_rn(__fmul_rn(fll, k.fp_w0f), T));
+    const float e = __fadd_rn(__fmul_rn(0.5f, __fadd_rn(w_new, c.fp_w)), __fmul_rn(__fmul_rn(k.fp_a2, k.fp_w0p), pll));
+    c.fp_w = w_new;
+    return e;
+}
+
+__device__ void run_dll_pll(const TrkParams& k, TrkChannel& c)
+{
+    double disc;
+    if (c.cloop)
+        disc = (c.p[0] != 0.0f) ? static_cast<double>(atanf(__fdiv_rn(c.p[1], c.p[0]))) : 0.0;
+    else
+        disc = static_cast<double>(atan2f(c.p[1], c.p[0]));  // gr::fast_atan2f restated as atan2f
+    c.carr_phase_error_hz = disc / kTwoPi;
+    c.carr_error_filt_hz = carrier_filter(k, c, 0.0f, static_cast<float>(c.carr_phase_error_hz), static_cast<float>(k.code_period));
+    c.carrier_doppler_hz = c.carr_error_filt_hz;
+    if (k.veml) {
+        const double early = static_cast<double>(sqrtf(__fadd_rn(__fadd_rn(__fadd_rn(__fmul_rn(c.ve[0], c.ve[0]), __fmul_rn(c.ve[1], c.ve[1])),
+                                                                          __fmul_rn(c.e[0], c.e[0])),
+            __fmul_rn(c.e[1], c.e[1]))));
+        const double late = static_cast<double>(sqrtf(__fadd_rn(__fadd_rn(__fadd_rn(__fmul_rn(c.l[0], c.l[0]), __fmul_rn(c.l[1], c.l[1])),
+                                                                         __fmul_rn(c.vl[0], c.vl[0])),
+            __fmul_rn(c.vl[1], c.vl[1]))));
+        const double s = early + late;
+        c.code_error_chips = (s == 0.0) ? 0.0 : (early - late) / s;
+    } else {
+        const double pe = static_cast<double>(hypotf(c.e[0], c.e[1]));
+        const double pl = static_cast<double>(hypotf(c.l[0], c.l[1]));
+        const double s = pe + pl;
+        const float slope = k.conf.slope;
+        const float norm = __fdiv_rn(__fsub_rn(k.conf.y_intercept, __fmul_rn(slope, c.spc)), slope);
+        c.code_error_chips = (s == 0.0) ? 0.0 : static_cast<double>(norm) * (pe - pl) / s;
+    }
+    c.code_error_filt_chips = loop_filter_apply(k, c, static_cast<float>(c.code_error_chips));
+    c.code_freq_chips = k.code_chip_rate - c.code_error_filt_chips;
+    if (k.conf.carrier_aiding) c.code_freq_chips += c.carrier_doppler_hz * k.code_chip_rate / k.carrier_freq;
+}
+
+__device__ void update_tracking_vars(const TrkParams& k, TrkChannel& c)
+{
+    const double fs = k.conf.fs_in;
+    const double T_chip = 1.0 / c.code_freq_chips;
+    const double T_prn = T_chip * static_cast<double>(k.code_length_chips);
+    const double T_prn_samples = T_prn * fs;
+    c.K_blk_samples = T_prn_samples + c.rem_code_phase_samples;
+    c.current_prn_length_samples = static_cast<int32_t>(floor(c.K_blk_samples));
+    c.carrier_phase_step_rad = kTwoPi * c.carrier_doppler_hz / fs;
+    const double n = static_cast<double>(c.current_prn_length_samples);
+    const double adv = c.carrier_phase_step_rad * n + 0.5 * 0.0 * n * n;
+    c.rem_carr_phase_rad = __fadd_rn(c.rem_carr_phase_rad, static_cast<float>(adv));
+    c.rem_carr_phase_rad = static_cast<float>(fmod(static_cast<double>(c.rem_carr_phase_rad), kTwoPi));
+    c.acc_carrier_phase_rad -= adv;
+    c.code_phase_step_chips = c.code_freq_chips / fs;
+    c.rem_code_phase_samples = c.K_blk_samples - n;
+    c.rem_code_phase_chips = c.code_freq_chips * c.rem_code_phase_samples / fs;
+}
+
+__device__ __forceinline__ int bit_at(const uint32_t* bits, int i) { return (bits[i >> 5] >> (i & 31)) & 1; }
+
+__device__ void push_sign(const TrkParams& k, TrkChannel& c, float prompt_re)
+{
+    const int cap = k.secondary_len;
+    const uint32_t neg = prompt_re < 0.0f ? 1u : 0u;
+    if (c.sign_count == cap) {  // boost::circular_buffer::push_back on a full buffer drops the oldest
+        for (int w = 0; w < kTrkMaxSecondary / 32; w++) {
+            const uint32_t carry = (w + 1 < kTrkMaxSecondary / 32) ? (c.sign_bits[w + 1] & 1u) : 0u;
+            c.sign_bits[w] = (c.sign_bits[w] >> 1) | (carry << 31);
+        }
+        const int i = cap - 1;
+        c.sign_bits[i >> 5] = (c.sign_bits[i >> 5] & ~(1u << (i & 31))) | (neg << (i & 31));
+    } else {
+        const int i = c.sign_count++;
+        c.sign_bits[i >> 5] = (c.sign_bits[i >> 5] & ~(1u << (i & 31))) | (neg << (i & 31));
+    }
+}
+
+__device__ bool acquire_secondary(const TrkParams& k, TrkChannel& c)
+{
+    int corr = 0;
+    for (int i = 0; i < k.secondary_len; i++) {
+        const int neg = bit_at(c.sign_bits, i);
+        const int one = bit_at(k.secondary_bits, i);
+        corr += (neg ^ one) ? 1 : -1;  // +1 for (real < 0, '0') and (real ≥ 0, '1')
+    }
+    if (abs(corr) == k.secondary_len) {
+        c.pll_180 = corr < 0 ? 1 : 0;
+        return true;
+    }
+    return false;
+}
+
+__device__ void clear_tracking_vars(TrkChannel& c)
+{
+    c.p_data[0] = c.p_data[1] = 0.0f;
+    c.carr_phase_error_hz = 0.0;
+    c.carr_error_filt_hz = 0.0;
+    c.code_error_chips = 0.0;
+    c.code_error_filt_chips = 0.0;
+    c.current_symbol = 0;
+    c.current_data_symbol = 0;
+    c.sign_count = 0;
+}
+
+__device__ __forceinline__ void cadd(float* acc, const float* v, float sgn)
+{
+    acc[0] = __fadd_rn(acc[0], __fmul_rn(sgn, v[0]));
+    acc[1] = __fadd_rn(acc[1], __fmul_rn(sgn, v[1]));
+}
+
+__device__ void zero_accu(TrkChannel& c)
+{
+    c.ve[0] = c.ve[1] = c.e[0] = c.e[1] = c.p[0] = c.p[1] = 0.0f;
+    c.l[0] = c.l[1] = c.vl[0] = c.vl[1] = 0.0f;
+}
+
+// One general_work call for the epoch that started at c.epoch_start; returns false when the
+// channel stops (loss of lock).
+__device__ bool epoch_update(const TrkParams& k, TrkChannel& c, const float* taps, const float* pdata, gnsship_trk_epoch& rec)
+{
+    const uint64_t nir = c.epoch_start;
+    const uint64_t fs_int = static_cast<uint64_t>(static_cast<int>(k.conf.fs_in));
+    rec.sample_counter = nir;
+    if (c.pull_in && static_cast<uint64_t>(k.conf.pull_in_time_s) < (nir - c.acq_sample_stamp) / fs_int) {
+        c.pull_in = 0;
+        c.carrier_fail = 0;
+        c.code_fail = 0;
+    }
+    const int eo = k.veml ? 2 : 0;
+    const int st = c.state;
+    bool loss = false;
+    if (st == 2) {
+        if (k.veml) {
+            c.ve[0] = taps[0];
+            c.ve[1] = taps[1];
+            c.vl[0] = taps[8];
+            c.vl[1] = taps[9];
+        }
+        c.e[0] = taps[eo];
+        c.e[1] = taps[eo + 1];
+        c.p[0] = taps[eo + 2];
+        c.p[1] = taps[eo + 3];
+        c.l[0] = taps[eo + 4];
+        c.l[1] = taps[eo + 5];
+        c.spc = k.conf.early_late_space_chips;
+        rec.prompt_i = static_cast<double>(c.p[0]);  // diagnostic: the epoch's prompt (no symbol flag in state 2)
+        rec.prompt_q = static_cast<double>(c.p[1]);
+        if (static_cast<uint64_t>(k.conf.bit_synchronization_time_limit_s) < (nir - c.acq_sample_stamp) / fs_int) c.carrier_fail = 300000;
+        if (!lock_status(k, c, k.code_period)) {
+            clear_tracking_vars(c);
+            c.state = 0;
+            loss = true;
+        } else {
+            bool next_state = false;
+            run_dll_pll(k, c);
+            update_tracking_vars(k, c);
+            if (!c.pull_in) {
+                if (k.secondary || k.symbols_per_bit > 1) {
+                    push_sign(k, c, taps[eo + 2]);
+                    if (c.sign_count == k.secondary_len) next_state = acquire_secondary(k, c);
+                } else {
+                    next_state = true;
+                }
+            }
+            if (next_state) {
+                zero_accu(c);
+                c.p_data[0] = c.p_data[1] = 0.0f;
+                c.sign_count = 0;
+                c.current_symbol = 0;
+                c.current_data_symbol = 0;
+                c.state = 4;
+            }
+        }
+    } else {
+        // save_correlation_results
+        float sgn = 1.0f;
+        if (k.secondary) {
+            sgn = bit_at(k.secondary_bits, c.current_symbol) ? -1.0f : 1.0f;
+            c.current_symbol = (c.current_symbol + 1) % k.secondary_len;
+        }
+        if (k.veml) {
+            cadd(c.ve, taps, sgn);
+            cadd(c.vl, taps + 8, sgn);
+        }
+        cadd(c.e, taps + eo, sgn);
+        cadd(c.p, taps + eo + 2, sgn);
+        cadd(c.l, taps + eo + 4, sgn);
+        const float* src = k.track_pilot ? pdata : taps + eo + 2;
+        if (k.symbols_per_bit > 1) {
+            if (k.data_secondary_len > 0) {
+                cadd(c.p_data, src, bit_at(k.data_secondary_bits, c.current_data_symbol) ? -1.0f : 1.0f);
+                c.current_data_symbol = (c.current_data_symbol + 1) % k.data_secondary_len;
+            } else {
+                cadd(c.p_data, src, 1.0f);
+                c.current_data_symbol = (c.current_data_symbol + 1) % k.symbols_per_bit;
+            }
+        } else {
+            c.p_data[0] = src[0];
+            c.p_data[1] = src[1];
+        }
+        c.cloop = k.track_pilot ? 0 : 1;
+        if (!lock_status(k, c, k.code_period)) {
+            clear_tracking_vars(c);
+            c.state = 0;
+            loss = true;
+        } else {
+            run_dll_pll(k, c);
+            update_tracking_vars(k, c);
+            if (!c.acc_phase_init) {
+                c.acc_carrier_phase_rad = -static_cast<double>(c.rem_carr_phase_rad);
+                c.acc_phase_init = 1;
+            }
+            if (c.current_data_symbol == 0) {
+                rec.prompt_i = static_cast<double>(c.p_data[0]);
+                rec.prompt_q = static_cast<double>(c.p_data[1]);
+                rec.flags |= 1;
+                c.p_data[0] = c.p_data[1] = 0.0f;
+            }
+            zero_accu(c);
+        }
+    }
+    rec.state = st;
+    if (loss) rec.flags |= 2;
+    if (c.pll_180) rec.flags |= 4;
+    rec.code_phase_samples = c.rem_code_phase_samples;
+    rec.carrier_phase_rads = c.acc_carrier_phase_rad;
+    rec.carrier_doppler_hz = c.carrier_doppler_hz;
+    rec.cn0_db_hz = static_cast<double>(c.cn0_db_hz);
+    rec.carrier_lock_test = c.carrier_lock_test;
+    rec.code_freq_chips = c.code_freq_chips;
+    rec.rem_code_phase_chips = c.rem_code_phase_chips;
+    rec.rem_carr_phase_rad = c.rem_carr_phase_rad;
+    rec.prn_length_samples = c.current_prn_length_samples;
+    if (loss) return false;
+    c.nitems_read = nir + static_cast<uint64_t>(c.current_prn_length_samples);  // consume_each (:2061)
+    return true;
+}
+
+// derive_job (gnsship_abi.hip) for a tracking epoch; the plan fields of `j` are kept.
+__device__ void fill_job(DevJob& j, const TrkParams& k, const TrkChannel& c, int64_t offset, int code_id, int n_taps, const float* shifts)
+{
+    const float spcf = static_cast<float>(k.code_samples_per_chip);
+    const float rem_carr = c.rem_carr_phase_rad;
+    const float step = static_cast<float>(c.carrier_phase_step_rad);
+    const float p0r = cosf(rem_carr), p0i = -sinf(rem_carr);
+    const float incr = cosf(-step), inci = sinf(-step);
+    j.sample_offset = offset;
+    j.n_samples = static_cast<int32_t>(k.conf.vector_length);
+    j.code_id = code_id;
+    j.n_taps = n_taps;
+    j.p0_re = p0r;
+    j.p0_im = p0i;
+    j.inc_re = incr;
+    j.inc_im = inci;
+    j.dtheta = atan2(static_cast<double>(inci), static_cast<double>(incr));
+    j.log_mag_inc = static_cast<float>(log(hypot(static_cast<double>(incr), static_cast<double>(inci))));
+    j.rem_code = __fmul_rn(static_cast<float>(c.rem_code_phase_chips), spcf);
+    j.code_step = __fmul_rn(static_cast<float>(c.code_phase_step_chips), spcf);
+    j.in_margin = 0;  // the tracking plan launches the general (wrapping) chip-index path
+    for (int t = 0; t < kMaxTaps; t++) j.shifts[t] = t < n_taps ? shifts[t] : 0.0f;
+}
+
+__global__ void trk_step_kernel(const TrkParams* __restrict__ pk, TrkChannel* __restrict__ chans, int n_chans, DevJob* __restrict__ jobs,
+    ChunkDesc* __restrict__ chunks, const float* __restrict__ corr_out, uint64_t buf_first, int64_t buf_len, int consume, int emit,
+    gnsship_trk_epoch* __restrict__ rec, int* __restrict__ ran_count)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n_chans) return;
+    const TrkParams& k = *pk;
+    TrkChannel c = chans[i];
+    const int jb = i * k.jobs_per_channel;
+    if (consume && c.ran) {
+        gnsship_trk_epoch r = {};
+        r.flags = 8;
+        const float* taps = corr_out + static_cast<int64_t>(jb) * 2 * kMaxTaps;
+        const float* pdata = k.jobs_per_channel > 1 ? corr_out + static_cast<int64_t>(jb + 1) * 2 * kMaxTaps : taps;
+        epoch_update(k, c, taps, pdata, r);
+        if (rec) rec[i] = r;
+    } else if (consume && rec) {
+        gnsship_trk_epoch r = {};
+        rec[i] = r;
+    }
+    c.ran = 0;
+    if (emit) {
+        const uint64_t vl = k.conf.vector_length;
+        const bool runnable = (c.state == 2 || c.state == 4) && c.nitems_read >= buf_first &&
+                              c.nitems_read + vl <= buf_first + static_cast<uint64_t>(buf_len);
+        for (int q = 0; q < k.jobs_per_channel; q++) {
+            DevJob& j = jobs[jb + q];
+            if (runnable) {
+                if (q == 0) {
+                    fill_job(j, k, c, static_cast<int64_t>(c.nitems_read - buf_first), c.code_id, k.n_taps, k.shifts);
+                } else {
+                    const float zero[1] = {0.0f};
+                    fill_job(j, k, c, static_cast<int64_t>(c.nitems_read - buf_first), c.data_code_id, 1, zero);
+                }
+            } else {
+                j.n_samples = 0;
+            }
+            for (int m = 0; m < k.chunks_per_job; m++) {
+                const int start = m * kCorrChunk;
+                const int rem = static_cast<int>(vl) - start;
+                chunks[j.first_chunk + m].len = runnable ? (rem < kCorrChunk ? rem : kCorrChunk) : 0;
+            }
+        }
+        if (runnable) {
+            c.ran = 1;
+            c.epoch_start = c.nitems_read;
+            atomicAdd(ran_count, 1);
+        }
+    }
+    chans[i] = c;
+}
+
+}  // namespace
+
+hipError_t launch_trk_step(const TrkParams* params, TrkChannel* chans, int n_chans, DevJob* jobs, ChunkDesc* chunks, const float* corr_out,
+    uint64_t buf_first, int64_t buf_len, int consume, int emit, gnsship_trk_epoch* rec, int* ran_count, hipStream_t stream)
+{
+    hipLaunchKernelGGL(trk_step_kernel, dim3((n_chans + 63) / 64), dim3(64), 0, stream, params, chans, n_chans, jobs, chunks, corr_out, buf_first,
+        buf_len, consume, emit, rec, ran_count);
+    return hipGetLastError();
+}
+
+}  // namespace gnsship

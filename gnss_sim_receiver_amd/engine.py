@@ -310,3 +310,61 @@ class PcpsAcquisition:
                 self.close()
         except Exception:
             pass
+
+
+class DllPllVemlTracking:
+    """dll_pll_veml_tracking (dll_pll_veml_tracking.cc) for up to ``max_channels`` channels, the
+    per-epoch loop resident on the device: ``start_tracking`` → :meth:`start`, ``general_work``
+    over an IF buffer → :meth:`run` (one record per channel-epoch, TRK_EPOCH_DTYPE)."""
+
+    def __init__(self, ctx: Context, conf: "abi.TrkConf", max_channels: int):
+        self.ctx = ctx
+        self.conf = conf
+        self.max_channels = max_channels
+        h = ctypes.c_void_p()
+        check(ctx.lib.gnsship_trk_create(ctx.h, ctypes.byref(conf), max_channels, ctypes.byref(h)), "gnsship_trk_create", ctx.h)
+        self.h = h
+
+    def start(self, channel: int, code_id: int, acq_delay_samples: float, acq_doppler_hz: float, acq_samplestamp: int,
+              first_sample: int, data_code_id: int = -1):
+        a = abi.TrkStartArgs(code_id=code_id, data_code_id=data_code_id, acq_delay_samples=acq_delay_samples,
+                             acq_doppler_hz=acq_doppler_hz, acq_samplestamp_samples=acq_samplestamp, first_sample=first_sample)
+        check(self.ctx.lib.gnsship_trk_start(self.h, channel, ctypes.byref(a)), "gnsship_trk_start", self.ctx.h)
+
+    def stop(self, channel: int):
+        check(self.ctx.lib.gnsship_trk_stop(self.h, channel), "gnsship_trk_stop", self.ctx.h)
+
+    def channel_state(self, channel: int):
+        st, nx = ctypes.c_int(), ctypes.c_uint64()
+        check(self.ctx.lib.gnsship_trk_channel_state(self.h, channel, ctypes.byref(st), ctypes.byref(nx)), "gnsship_trk_channel_state",
+              self.ctx.h)
+        return st.value, nx.value
+
+    def run(self, sig, buffer_first_sample: int, max_rounds: int, fmt: int = None, n_buffer_samples: int = None,
+            records: bool = True):
+        """sig: host ndarray or DeviceBuffer (pass fmt and n_buffer_samples).  Returns (records
+        [max_rounds, max_channels] or None, rounds_done)."""
+        out = np.zeros((max_rounds, self.max_channels), abi.TRK_EPOCH_DTYPE) if records else None
+        if isinstance(sig, DeviceBuffer):
+            ptr, on_dev, f = sig.ptr, 1, FMT_CF32 if fmt is None else fmt
+            n = n_buffer_samples if n_buffer_samples is not None else sig.nbytes // _FMT_BYTES[f]
+        else:
+            sig = np.ascontiguousarray(sig)
+            ptr, on_dev, f = sig.ctypes.data, 0, sample_format(sig)
+            n = sig.nbytes // _FMT_BYTES[f]
+        done = ctypes.c_int()
+        check(self.ctx.lib.gnsship_trk_run(self.h, ptr, f, on_dev, buffer_first_sample, n, max_rounds,
+                                           out.ctypes.data if records else None, ctypes.byref(done)), "gnsship_trk_run", self.ctx.h)
+        return out, done.value
+
+    def close(self):
+        if self.h:
+            self.ctx.lib.gnsship_trk_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            if self.h and self.ctx.h:
+                self.close()
+        except Exception:
+            pass

@@ -44,6 +44,12 @@ class Satellite:
     f_if_hz: float = 0.0
     code: np.ndarray = field(default=None, repr=False)
     code_data: np.ndarray = field(default=None, repr=False)  # E1-B data component (Galileo)
+    # cyclic navigation-bit pattern ('0' → +1, '1' → −1): GPS / BDS one bit per 20 code periods,
+    # Galileo one E1-B symbol per code period (250 sps)
+    bits: str = None
+    # cyclic secondary code, one chip per code period: E1-C CS25 on the Galileo pilot, the B1I NH
+    # code on the BeiDou signal
+    secondary: str = None
 
     def __post_init__(self):
         if self.code is None:
@@ -85,8 +91,19 @@ def generate_if(fs: float, n_samples: int, sats: list, seed: int = 0, noise: boo
             ph = s.chip_phase(n, fs)
             chip = np.floor(ph).astype(np.int64)
             c = s.code[np.mod(chip, s.code_len)].astype(np.float64)
+            period = np.floor_divide(chip, s.code_len)
+            if s.secondary:
+                sec = np.array([1.0 if b == "0" else -1.0 for b in s.secondary])
+                c = c * sec[np.mod(period, len(sec))]
+            data_sign = 1.0
+            if s.bits:
+                pat = np.array([1.0 if b == "0" else -1.0 for b in s.bits])
+                per_bit = 1 if s.code_data is not None else 20
+                data_sign = pat[np.mod(np.floor_divide(period, per_bit), len(pat))]
             if s.code_data is not None:  # Galileo E1 OS: (E1B − E1C)/√2 with sinBOC(1,1) subcarriers
-                c = (s.code_data[np.mod(chip, s.code_len)].astype(np.float64) - c) / np.sqrt(2.0)
+                c = (data_sign * s.code_data[np.mod(chip, s.code_len)].astype(np.float64) - c) / np.sqrt(2.0)
+            else:
+                c = c * data_sign
             if s.data_bits:
                 periods = np.floor_divide(chip, s.code_len)
                 bit_idx = np.floor_divide(periods, 20)

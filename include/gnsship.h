@@ -191,6 +191,91 @@ int gnsship_acq_run(gnsship_acq* a, const void* sig, int fmt, int sig_on_device,
 int gnsship_acq_num_bins(gnsship_acq* a, int* n_bins);
 int gnsship_acq_destroy(gnsship_acq* a);
 
+/* ---------------------------------------------------------------------------------------------
+ * Closed-loop tracking engine: the per-epoch DLL/PLL of dll_pll_veml_tracking
+ * resident on the device.  Replaces, for N channels at once, the general_work loop of
+ * src/algorithms/tracking/gnuradio_blocks/dll_pll_veml_tracking.cc:1728-2094 around
+ * do_correlation_step (:1037-1062): cn0_and_tracking_lock_status (:972-1029), run_dll_pll
+ * (:1065-1152), update_tracking_vars (:1189-1260), save_correlation_results and the bit /
+ * secondary-code synchronisation of states 2 and 4.  start_tracking (:643-883) and the state-1
+ * pull-in (:1757-1788) run on the host in gnsship_trk_start.  Not covered: extended coherent
+ * integration (state 3; extend_correlation_symbols = 1 is the default), high_dyn rate smoothing,
+ * the FLL branches (enable_fll_* default false) and BeiDou GEO satellites.
+ * ------------------------------------------------------------------------------------------- */
+#define GNSSHIP_SYS_GPS_L1CA 0 /* GPS L1 C/A: 3 taps, bit sync on the 160-symbol preamble */
+#define GNSSHIP_SYS_GAL_E1 1   /* Galileo E1 B/C: VEML 5 taps on the pilot + data prompt, CS25 secondary */
+#define GNSSHIP_SYS_BDS_B1I 2  /* BeiDou B1I MEO/IGSO (PRN 6-58): 3 taps, 20-chip NH secondary code */
+
+typedef struct gnsship_trk_conf { /* Dll_Pll_Conf (dll_pll_conf.h:33-80), same names and units */
+    double fs_in;
+    double carrier_lock_th;
+    float pll_bw_hz;
+    float dll_bw_hz;
+    float fll_bw_hz;
+    float early_late_space_chips;
+    float very_early_late_space_chips;
+    float slope;
+    float spc;
+    float y_intercept;
+    float cn0_smoother_alpha;
+    float carrier_lock_test_smoother_alpha;
+    uint32_t pull_in_time_s;
+    uint32_t bit_synchronization_time_limit_s;
+    uint32_t vector_length;
+    int32_t pll_filter_order;
+    int32_t dll_filter_order;
+    int32_t cn0_samples;
+    int32_t cn0_smoother_samples;
+    int32_t carrier_lock_test_smoother_samples;
+    int32_t cn0_min;
+    int32_t max_code_lock_fail;
+    int32_t max_carrier_lock_fail;
+    int32_t carrier_aiding;
+    int32_t track_pilot;
+    int32_t system; /* GNSSHIP_SYS_*: the signal constants the adapter selects */
+} gnsship_trk_conf;
+
+typedef struct gnsship_trk_start_args { /* Gnss_Synchro fields start_tracking reads (:647-649) */
+    int32_t code_id;      /* code-bank entry of the tracking replica (pilot for E1) */
+    int32_t data_code_id; /* E1 with track_pilot: data replica; otherwise ignored */
+    double acq_delay_samples;
+    double acq_doppler_hz;
+    uint64_t acq_samplestamp_samples;
+    uint64_t first_sample; /* nitems_read when the block first runs after start (state-1 pull-in) */
+} gnsship_trk_start_args;
+
+typedef struct gnsship_trk_epoch { /* one general_work call of one channel (Gnss_Synchro subset) */
+    uint64_t sample_counter;       /* nitems_read at the epoch start */
+    double prompt_i, prompt_q;     /* valid when flags & 1 (state 4 symbol output) */
+    double code_phase_samples;     /* d_rem_code_phase_samples */
+    double carrier_phase_rads;     /* d_acc_carrier_phase_rad */
+    double carrier_doppler_hz;
+    double cn0_db_hz;
+    float carrier_lock_test;
+    int32_t state;                 /* state the epoch ran in (2 or 4) */
+    int32_t flags;                 /* 1 valid symbol, 2 loss of lock, 4 PLL 180°, 8 epoch ran */
+    int32_t pad;
+    double code_freq_chips;
+    double rem_code_phase_chips;
+    float rem_carr_phase_rad;
+    int32_t prn_length_samples;    /* d_current_prn_length_samples after the update */
+} gnsship_trk_epoch; /* 96 bytes */
+
+typedef struct gnsship_trk gnsship_trk;
+int gnsship_trk_create(gnsship_ctx* ctx, const gnsship_trk_conf* conf, int max_channels, gnsship_trk** out);
+int gnsship_trk_start(gnsship_trk* t, int channel, const gnsship_trk_start_args* args);
+int gnsship_trk_stop(gnsship_trk* t, int channel);
+/* Runs up to max_rounds epochs of every tracking channel over the IF buffer holding absolute
+ * samples [buffer_first_sample, +n_buffer_samples) (device pointer when sig_on_device, else host
+ * memory staged to the device).  Per round each channel whose next vector_length window lies in
+ * the buffer runs one epoch; no host round trip between rounds.  out (optional): max_rounds ×
+ * max_channels records, flags & 8 marking the epochs that ran.  *rounds_done: rounds in which at
+ * least one channel ran. */
+int gnsship_trk_run(gnsship_trk* t, const void* sig, int fmt, int sig_on_device, uint64_t buffer_first_sample, int64_t n_buffer_samples,
+    int max_rounds, gnsship_trk_epoch* out, int* rounds_done);
+int gnsship_trk_channel_state(gnsship_trk* t, int channel, int* state, uint64_t* next_sample);
+int gnsship_trk_destroy(gnsship_trk* t);
+
 #ifdef __cplusplus
 }
 #endif
