@@ -102,7 +102,8 @@ def _L():
     L.orc_carrier_lock_detector.argtypes = [_f32p, ctypes.c_int]
     L.orc_carrier_lock_detector.restype = ctypes.c_float
     L.orc_trk_start.argtypes = [ctypes.POINTER(OrcTrkConf), vp, ctypes.c_double, ctypes.c_double, ctypes.c_uint64, ctypes.c_uint64]
-    L.orc_trk_run.argtypes = [ctypes.POINTER(OrcTrkConf), vp, _f32p, ctypes.c_int64, _f32p, ctypes.c_int, _f32p, ctypes.c_int, vp]
+    L.orc_trk_run.argtypes = [ctypes.POINTER(OrcTrkConf), vp, _f32p, ctypes.c_uint64, ctypes.c_int64, _f32p, ctypes.c_int, _f32p, ctypes.c_int,
+                              vp]
     L.orc_trk_nitems_read.argtypes = [vp]
     L.orc_trk_nitems_read.restype = ctypes.c_uint64
     L.orc_trk_state.argtypes = [vp]
@@ -169,17 +170,39 @@ def carrier_lock_detector(prompt: np.ndarray) -> float:
     return _L().orc_carrier_lock_detector(_ptr(p.view(np.float32)), len(p))
 
 
+class Channel:
+    """One oracle channel: start_tracking, then run() over successive buffers."""
+
+    def __init__(self, k: OrcTrkConf, code: np.ndarray, acq_delay_samples: float, acq_doppler_hz: float, acq_samplestamp: int,
+                 first_sample: int, data_code: np.ndarray = None):
+        L = _L()
+        self.k = k
+        self.buf = ctypes.create_string_buffer(L.orc_trk_sizeof_channel())
+        self.code = np.ascontiguousarray(code, np.float32)
+        self.data_code = np.ascontiguousarray(data_code, np.float32) if data_code is not None else None
+        L.orc_trk_start(ctypes.byref(k), self.buf, acq_delay_samples, acq_doppler_hz, acq_samplestamp, first_sample)
+
+    def run(self, samples: np.ndarray, buffer_first: int, max_epochs: int) -> np.ndarray:
+        L = _L()
+        x = np.ascontiguousarray(samples, np.complex64)
+        out = np.zeros(max_epochs, EPOCH_DTYPE)
+        dc = self.data_code
+        n = L.orc_trk_run(ctypes.byref(self.k), self.buf, _ptr(x.view(np.float32)), buffer_first, len(x), _ptr(self.code), len(self.code),
+                          _ptr(dc) if dc is not None else None, max_epochs, out.ctypes.data)
+        return out[:n]
+
+    @property
+    def state(self) -> int:
+        return _L().orc_trk_state(self.buf)
+
+    @property
+    def next_sample(self) -> int:
+        return _L().orc_trk_nitems_read(self.buf)
+
+
 def track(k: OrcTrkConf, samples: np.ndarray, code: np.ndarray, acq_delay_samples: float, acq_doppler_hz: float, acq_samplestamp: int,
-          first_sample: int, max_epochs: int, data_code: np.ndarray = None) -> np.ndarray:
-    """start_tracking + general_work until max_epochs / loss of lock / end of `samples` (absolute
-    sample 0 = samples[0]).  Returns EPOCH_DTYPE records of the epochs run."""
-    L = _L()
-    ch = ctypes.create_string_buffer(L.orc_trk_sizeof_channel())
-    L.orc_trk_start(ctypes.byref(k), ch, acq_delay_samples, acq_doppler_hz, acq_samplestamp, first_sample)
-    x = np.ascontiguousarray(samples, np.complex64)
-    code = np.ascontiguousarray(code, np.float32)
-    dc = np.ascontiguousarray(data_code, np.float32) if data_code is not None else None
-    out = np.zeros(max_epochs, EPOCH_DTYPE)
-    n = L.orc_trk_run(ctypes.byref(k), ch, _ptr(x.view(np.float32)), len(x), _ptr(code), len(code),
-                      _ptr(dc) if dc is not None else None, max_epochs, out.ctypes.data)
-    return out[:n]
+          first_sample: int, max_epochs: int, data_code: np.ndarray = None, buffer_first: int = 0) -> np.ndarray:
+    """start_tracking + general_work until max_epochs / loss of lock / end of `samples`
+    (samples[i] = absolute sample buffer_first + i).  Returns EPOCH_DTYPE records."""
+    ch = Channel(k, code, acq_delay_samples, acq_doppler_hz, acq_samplestamp, first_sample, data_code)
+    return ch.run(samples, buffer_first, max_epochs)

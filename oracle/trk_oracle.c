@@ -690,23 +690,23 @@ int orc_multicorrelator_real_codes(float* corr_out, const float* sig_in, const f
     float phase_rate_step_rad, float rem_code_phase_chips, float code_phase_step_chips, float code_phase_rate_step_chips,
     int signal_length_samples, float* scratch);
 
-/* Closed loop over host CF32 samples [0, n_samples) for one channel: for each epoch, correlate
+/* Closed loop over host CF32 samples (samples[i] = absolute sample buffer_first + i) for one channel: for each epoch, correlate
  * vector_length samples at nitems_read with the oracle multicorrelator (the tracking code and,
  * when track_pilot, the data code with one prompt tap), then update.  Stops after max_epochs,
  * when the channel goes idle, or when the next window leaves the buffer.  Returns epochs run. */
-int orc_trk_run(const orc_trk_conf* k, orc_trk_channel* c, const float* samples, int64_t n_samples, const float* code, int code_len,
-    const float* data_code, int max_epochs, orc_trk_epoch* out)
+int orc_trk_run(const orc_trk_conf* k, orc_trk_channel* c, const float* samples, uint64_t buffer_first, int64_t n_samples, const float* code,
+    int code_len, const float* data_code, int max_epochs, orc_trk_epoch* out)
 {
     const int vl = (int)k->vector_length;
     float* scratch = (float*)malloc((size_t)5 * (size_t)vl * sizeof(float));
     int e = 0;
     for (; e < max_epochs; e++) {
         if (c->state != 2 && c->state != 4) break;
-        if ((int64_t)c->nitems_read + vl > n_samples) break;
+        if (c->nitems_read < buffer_first || (int64_t)(c->nitems_read - buffer_first) + vl > n_samples) break;
         float args[6];
         orc_trk_correlation_args(k, c, args);
         float taps[10] = {0}, pdata[2] = {0};
-        const float* x = samples + 2 * c->nitems_read;
+        const float* x = samples + 2 * (c->nitems_read - buffer_first);
         orc_multicorrelator_real_codes(taps, x, code, code_len, c->shifts, c->n_taps, 0, args[0], args[1], args[2], args[3], args[4], args[5], vl,
             scratch);
         if (k->track_pilot && data_code) {

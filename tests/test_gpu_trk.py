@@ -1,0 +1,138 @@
+"""Device-resident tracking loop (gnsship_trk, HIP) vs the oracle loop (oracle/trk_oracle.c).
+
+Same IF, same start_tracking arguments, every epoch compared.  The loop is a contracting
+feedback system, so the device/oracle differences stay at the size of their per-epoch inputs'
+differences (correlations ≲1e-6 relative, device vs glibc libm ulps):
+  exact      sample_counter (every consume_each), state, flags, prn_length_samples
+  ≤ 2e-3 Hz  carrier Doppler; ≤ 2e-3 chips/s code frequency; ≤ 1e-5 chips remnant code phase
+  ≤ 5e-3 dB  CN0; prompt ≤ 1e-4·|P| (+1e-3); ≤ 1e-2 rad accumulated carrier phase.
+"""
+import numpy as np
+import pytest
+
+from gnss_sim_receiver_amd import abi, engine, signals
+from oracle import trk as T
+
+import trk_scenarios as S
+
+pytestmark = pytest.mark.gpu
+SYS = {"GPS": abi.SYS_GPS_L1CA, "GAL": abi.SYS_GAL_E1, "BDS": abi.SYS_BDS_B1I}
+SHARED = ["fs_in", "carrier_lock_th", "pll_bw_hz", "dll_bw_hz", "fll_bw_hz", "early_late_space_chips", "very_early_late_space_chips",
+          "slope", "spc", "y_intercept", "cn0_smoother_alpha", "carrier_lock_test_smoother_alpha", "pull_in_time_s",
+          "bit_synchronization_time_limit_s", "vector_length", "pll_filter_order", "dll_filter_order", "cn0_samples",
+          "cn0_smoother_samples", "carrier_lock_test_smoother_samples", "cn0_min", "max_code_lock_fail", "max_carrier_lock_fail",
+          "carrier_aiding", "track_pilot"]
+
+
+def dev_conf(k, system):
+    c = abi.TrkConf.defaults(SYS[system], k.fs_in, k.vector_length)
+    for f in SHARED:
+        setattr(c, f, getattr(k, f))
+    if system == "GAL":
+        c.track_pilot = k.track_pilot
+    return c
+
+
+def compare(dev, ref, label=""):
+    d = dev[(dev["flags"] & 8) == 8]
+    assert len(d) == len(ref), (label, len(d), len(ref))
+    for f in ("sample_counter", "state", "prn_length_samples"):
+        assert np.array_equal(d[f], ref[f]), (label, f, np.nonzero(d[f] != ref[f])[0][:5])
+    assert np.array_equal(d["flags"] & 7, ref["flags"] & 7), label
+    np.testing.assert_allclose(d["carrier_doppler_hz"], ref["carrier_doppler_hz"], rtol=0, atol=2e-3, err_msg=label)
+    np.testing.assert_allclose(d["code_freq_chips"], ref["code_freq_chips"], rtol=0, atol=2e-3, err_msg=label)
+    np.testing.assert_allclose(d["rem_code_phase_chips"], ref["rem_code_phase_chips"], rtol=0, atol=1e-5, err_msg=label)
+    np.testing.assert_allclose(d["cn0_db_hz"], ref["cn0_db_hz"], rtol=0, atol=5e-3, err_msg=label)
+    np.testing.assert_allclose(d["carrier_phase_rads"], ref["carrier_phase_rads"], rtol=0, atol=1e-2, err_msg=label)
+    pd = d["prompt_i"] + 1j * d["prompt_q"]
+    pr = ref["prompt_i"] + 1j * ref["prompt_q"]
+    assert np.all(np.abs(pd - pr) <= 1e-4 * np.abs(pr) + 1e-3), label
+
+
+def test_gps_pull_in_eight_channels(ctx):
+    fs, epochs = 4e6, 300
+    rng = np.random.default_rng(17)
+    sats = [signals.Satellite(prn=p, doppler_hz=float(rng.uniform(-4000, 4000)), code_delay_chips=float(rng.uniform(0, 1023)),
+                              cn0_dbhz=47.0, carrier_phase_rad=float(rng.uniform(0, 6.28))) for p in range(1, 9)]
+    k = T.conf("GPS", fs, 4000)
+    x = signals.generate_if(fs, 4000 * (epochs + 3), sats, seed=3)
+    trk = engine.DllPllVemlTracking(ctx, dev_conf(k, "GPS"), len(sats))
+    starts = []
+    for ch, s in enumerate(sats):
+        delay = (s.code_delay_chips / s.code_freq()) * fs + float(rng.uniform(-0.4, 0.4))
+        dop = s.doppler_hz + float(rng.uniform(-30, 30))
+        ctx.set_code(ch, s.code)
+        trk.start(ch, ch, delay, dop, 0, 0)
+        starts.append((delay, dop))
+    rec, rounds = trk.run(x, 0, epochs)
+    assert rounds == epochs
+    for ch, s in enumerate(sats):
+        ref = T.track(k, x, s.code, starts[ch][0], starts[ch][1], 0, 0, epochs)
+        compare(rec[:, ch], ref, f"ch{ch}")
+    trk.close()
+
+
+@pytest.mark.parametrize("system,fs,epochs", [("GPS", 4e6, 700), ("GAL", 25e6 / 4, 90), ("BDS", 4.092e6, 300)])
+def test_sync_to_state_4_matches_oracle(ctx, system, fs, epochs):
+    sat, k, x, stamp, first, delay, dop = S.sync(system, fs, epochs)
+    trk = engine.DllPllVemlTracking(ctx, dev_conf(k, system), 2)
+    ctx.set_code(20, sat.code)
+    if sat.code_data is not None:
+        ctx.set_code(21, sat.code_data)
+    trk.start(1, 20, delay, dop, stamp, first, data_code_id=21)  # channel 0 left idle
+    rec, rounds = trk.run(x, first, epochs)
+    ref = T.track(k, x, sat.code, delay, dop, stamp, first, epochs, data_code=sat.code_data, buffer_first=first)
+    assert ref["state"][-1] == 4
+    compare(rec[:, 1], ref, system)
+    assert not np.any(rec[:, 0]["flags"])
+    trk.close()
+
+
+def test_buffers_in_pieces_and_channel_state(ctx):
+    sat, k, x, stamp, first, delay, dop = S.pull_in("GPS", 4e6, 45.0, 2100.0, 50.5, -20.0, 0.3, 120)
+    ctx.set_code(3, sat.code)
+    trk = engine.DllPllVemlTracking(ctx, dev_conf(k, "GPS"), 1)
+    trk.start(0, 3, delay, dop, stamp, first)
+    a, ra = trk.run(x[:150000], 0, 120)
+    st, nx = trk.channel_state(0)
+    assert st == 2 and 0 < ra < 120
+    b, rb = trk.run(x[nx:], nx, 120)
+    got = np.concatenate([a[:ra, 0], b[:, 0]])
+    ref = T.track(k, x, sat.code, delay, dop, stamp, first, 120)
+    compare(got[(got["flags"] & 8) == 8][:len(ref)], ref, "pieces")
+    trk.close()
+
+
+def test_loss_of_lock_matches_oracle(ctx):
+    """Signal for 0.3 s then noise only (whose m2m4 estimate sits near 29 dB-Hz, hence cn0_min = 35):
+    CN0 decays through the smoother below cn0_min and the
+    code-lock fail counter passes max_code_lock_fail → state 0, flags & 2, no further epochs."""
+    fs = 4e6
+    sat, k, x, stamp, first, delay, dop = S.sync("GPS", fs, 1200, cn0=45.0, cn0_smoother_alpha=0.02, cn0_min=35)
+    cut = int(0.3 * fs)
+    noise = signals.generate_if(fs, len(x) - cut, [], seed=99, start=first + cut)
+    x = np.concatenate([x[:cut], noise])
+    ctx.set_code(5, sat.code)
+    trk = engine.DllPllVemlTracking(ctx, dev_conf(k, "GPS"), 1)
+    trk.start(0, 5, delay, dop, stamp, first)
+    rec, rounds = trk.run(x, first, 1200)
+    ref = T.track(k, x, sat.code, delay, dop, stamp, first, 1200, buffer_first=first)
+    assert ref["flags"][-1] & 2 and len(ref) < 1200
+    compare(rec[:, 0], ref, "loss")
+    assert rounds == len(ref)
+    assert trk.channel_state(0)[0] == 0
+    trk.close()
+
+
+def test_bad_configuration_and_arguments(ctx):
+    k = T.conf("GPS", 4e6, 4000)
+    bad = dev_conf(k, "GPS")
+    bad.cn0_samples = 100
+    with pytest.raises(abi.GnssHipError):
+        engine.DllPllVemlTracking(ctx, bad, 1)
+    trk = engine.DllPllVemlTracking(ctx, dev_conf(k, "GPS"), 2)
+    with pytest.raises(abi.GnssHipError):
+        trk.start(2, 0, 0.0, 0.0, 0, 0)  # channel out of range
+    with pytest.raises(abi.GnssHipError):
+        trk.start(0, 999, 0.0, 0.0, 0, 0)  # code not in the bank
+    trk.close()
