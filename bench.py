@@ -166,6 +166,35 @@ def e1_bench(ctx, seconds=0.2, reps=10):
             "algorithmic_GBps": round(2 * nch * n_ep * vl * 8 / (ms * 1e-3) / 1e9, 1)}
 
 
+def trk_bench(ctx, block, sats, n_ch, rounds):
+    """Closed-loop tracking (gnsship_trk, §8f f1): n_ch GPS L1 C/A channels (channel c tracks
+    satellite c mod 32, started from truth acquisition at sample 0) stepped `rounds` epochs over the
+    HBM-resident block, loop state and correlator jobs on the device, no host round trip."""
+    from gnss_sim_receiver_amd import abi, engine
+    conf = abi.TrkConf.defaults(abi.SYS_GPS_L1CA, FS, VL)
+    trk = engine.DllPllVemlTracking(ctx, conf, n_ch)
+    for i, s in enumerate(sats):
+        ctx.set_code(300 + i, s.code)
+    for ch in range(n_ch):
+        i = ch % len(sats)
+        s = sats[i]
+        trk.start(ch, 300 + i, (s.code_delay_chips / s.code_freq()) * FS, s.doppler_hz, 0, 0)
+    dev = ctx.upload(block)
+    n = len(block)
+    trk.run(dev, 0, 3, n_buffer_samples=n, records=False)  # warm-up (first epochs of every channel)
+    t0 = time.perf_counter()
+    _, done = trk.run(dev, 0, rounds, n_buffer_samples=n, records=False)
+    dt = time.perf_counter() - t0
+    tracking = sum(1 for ch in range(n_ch) if trk.channel_state(ch)[0] in (2, 4))
+    trk.close()
+    dev.free()
+    sig_s = done * 1e-3
+    return {"config": f"{n_ch} GPS L1 C/A channels, 4 Msps, closed DLL/PLL loop on the device, {done} epochs",
+            "ms_per_signal_second": round(dt / sig_s * 1e3, 3), "realtime_factor": round(sig_s / dt, 1),
+            "us_per_epoch_round": round(dt / done * 1e6, 2), "channel_epochs_per_s": round(n_ch * done / dt, 0),
+            "channels_still_tracking": tracking}
+
+
 def main():
     args = parse()
     from gnss_sim_receiver_amd import abi, engine, sharding
@@ -327,6 +356,10 @@ def main():
                                              "C3: 32 PRN x 40 bins, fft 25000 (four-step), 25 Msps")
     if rank == 0 and not args.no_acq:
         result["tracking_c4_e1"] = e1_bench(ctx)
+        if block is not None:
+            rounds = int(round(args.seconds * 1000)) - 8
+            result["closed_loop_c2"] = trk_bench(ctx, block, sats, N_CH, rounds)
+            result["closed_loop_1024ch"] = trk_bench(ctx, block, sats, 1024, min(rounds, 250))
     for b in batches:
         b.close()
     if rank == 0:
