@@ -11,6 +11,7 @@
 #include <cmath>
 #include <complex>
 #include <cstdint>
+#include <atomic>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -292,6 +293,122 @@ private:
     float threshold_ = 0.0F;
     uint32_t doppler_step_ = 0;
     int32_t doppler_center_ = 0;
+};
+
+// Mirror of Dll_Pll_Conf (src/algorithms/tracking/libs/dll_pll_conf.h:33-80): same field names and
+// defaults (FLAGS_* defaults from gnss_sdr_flags.cc:48-57 for the lock-detector fields).
+struct Dll_Pll_Conf {
+    double fs_in{2000000.0};
+    double carrier_lock_th{0.7};
+    float pll_bw_hz{35.0F}, dll_bw_hz{2.0F}, fll_bw_hz{35.0F};
+    float early_late_space_chips{0.25F}, very_early_late_space_chips{0.5F};
+    float slope{1.0F}, spc{0.5F}, y_intercept{1.0F};
+    float cn0_smoother_alpha{0.002F}, carrier_lock_test_smoother_alpha{0.002F};
+    uint32_t pull_in_time_s{10U}, bit_synchronization_time_limit_s{20U}, vector_length{0U};
+    int32_t pll_filter_order{3}, dll_filter_order{2};
+    int32_t cn0_samples{20}, cn0_smoother_samples{200}, carrier_lock_test_smoother_samples{25}, cn0_min{25};
+    int32_t max_code_lock_fail{50}, max_carrier_lock_fail{5000};
+    bool carrier_aiding{true}, track_pilot{true};
+    char system{'G'};    // 'G' GPS L1 C/A, 'E' Galileo E1, 'C' BeiDou B1I
+    char signal[3]{"1C"};
+};
+
+// Mirror of dll_pll_veml_tracking (gnuradio_blocks/dll_pll_veml_tracking.cc) for many channels on one
+// device: start_tracking(:643-883) per channel, general_work over an IF buffer for all of them (the
+// per-epoch loop runs on the device; one record per channel-epoch).
+class Dll_Pll_Veml_Tracking_Hip {
+public:
+    Dll_Pll_Veml_Tracking_Hip(const Dll_Pll_Conf& conf, int max_channels, int device = 0) : dev_(Device::get(device)), channels_(max_channels)
+    {
+        gnsship_trk_conf c{};
+        c.fs_in = conf.fs_in;
+        c.carrier_lock_th = conf.carrier_lock_th;
+        c.pll_bw_hz = conf.pll_bw_hz;
+        c.dll_bw_hz = conf.dll_bw_hz;
+        c.fll_bw_hz = conf.fll_bw_hz;
+        c.early_late_space_chips = conf.early_late_space_chips;
+        c.very_early_late_space_chips = conf.very_early_late_space_chips;
+        c.slope = conf.slope;
+        c.spc = conf.spc;
+        c.y_intercept = conf.y_intercept;
+        c.cn0_smoother_alpha = conf.cn0_smoother_alpha;
+        c.carrier_lock_test_smoother_alpha = conf.carrier_lock_test_smoother_alpha;
+        c.pull_in_time_s = conf.pull_in_time_s;
+        c.bit_synchronization_time_limit_s = conf.bit_synchronization_time_limit_s;
+        c.vector_length = conf.vector_length;
+        c.pll_filter_order = conf.pll_filter_order;
+        c.dll_filter_order = conf.dll_filter_order;
+        c.cn0_samples = conf.cn0_samples;
+        c.cn0_smoother_samples = conf.cn0_smoother_samples;
+        c.carrier_lock_test_smoother_samples = conf.carrier_lock_test_smoother_samples;
+        c.cn0_min = conf.cn0_min;
+        c.max_code_lock_fail = conf.max_code_lock_fail;
+        c.max_carrier_lock_fail = conf.max_carrier_lock_fail;
+        c.carrier_aiding = conf.carrier_aiding ? 1 : 0;
+        c.track_pilot = conf.track_pilot ? 1 : 0;
+        c.system = conf.system == 'E' ? GNSSHIP_SYS_GAL_E1 : conf.system == 'C' ? GNSSHIP_SYS_BDS_B1I : GNSSHIP_SYS_GPS_L1CA;
+        code_base_ = 1024 + 2 * max_channels * next_engine_id();
+        std::lock_guard<std::mutex> lk(dev_->mutex());
+        if (gnsship_trk_create(dev_->ctx(), &c, max_channels, &h_) != GNSSHIP_OK)
+            throw std::invalid_argument(std::string("gnsship_trk_create: ") + gnsship_last_error(dev_->ctx()));
+    }
+    ~Dll_Pll_Veml_Tracking_Hip()
+    {
+        if (h_) gnsship_trk_destroy(h_);
+    }
+    // start_tracking for one channel: the local code(s) as the block generates them (d_tracking_code,
+    // d_data_code; code_len = samples per chip × chips) and the acquisition's Gnss_Synchro fields.
+    bool start_tracking(int channel, const float* tracking_code, const float* data_code, int code_len, double acq_delay_samples,
+        double acq_doppler_hz, uint64_t acq_samplestamp_samples, uint64_t first_sample)
+    {
+        if (channel < 0 || channel >= channels_) return false;
+        std::lock_guard<std::mutex> lk(dev_->mutex());
+        const int cid = code_base_ + 2 * channel;
+        if (gnsship_code_set(dev_->ctx(), cid, tracking_code, code_len) != GNSSHIP_OK) return false;
+        if (data_code && gnsship_code_set(dev_->ctx(), cid + 1, data_code, code_len) != GNSSHIP_OK) return false;
+        gnsship_trk_start_args a{};
+        a.code_id = cid;
+        a.data_code_id = data_code ? cid + 1 : -1;
+        a.acq_delay_samples = acq_delay_samples;
+        a.acq_doppler_hz = acq_doppler_hz;
+        a.acq_samplestamp_samples = acq_samplestamp_samples;
+        a.first_sample = first_sample;
+        return gnsship_trk_start(h_, channel, &a) == GNSSHIP_OK;
+    }
+    bool stop_tracking(int channel)
+    {
+        std::lock_guard<std::mutex> lk(dev_->mutex());
+        return gnsship_trk_stop(h_, channel) == GNSSHIP_OK;
+    }
+    // general_work for every channel over gr_complex samples [first_sample, first_sample + n): up to
+    // max_epochs epochs per channel; records (max_epochs × max_channels, optional) as gnsship_trk_epoch.
+    int work(const std::complex<float>* in, uint64_t first_sample, int64_t n, int max_epochs, gnsship_trk_epoch* records = nullptr,
+        bool in_on_device = false)
+    {
+        int done = 0;
+        std::lock_guard<std::mutex> lk(dev_->mutex());
+        if (gnsship_trk_run(h_, in, GNSSHIP_FMT_CF32, in_on_device ? 1 : 0, first_sample, n, max_epochs, records, &done) != GNSSHIP_OK) return -1;
+        return done;
+    }
+    int state(int channel, uint64_t* next_sample = nullptr)
+    {
+        int st = -1;
+        std::lock_guard<std::mutex> lk(dev_->mutex());
+        gnsship_trk_channel_state(h_, channel, &st, next_sample);
+        return st;
+    }
+    const char* last_error() const { return gnsship_last_error(dev_->ctx()); }
+
+private:
+    static int next_engine_id()
+    {
+        static std::atomic<int> n{0};
+        return n++;
+    }
+    std::shared_ptr<Device> dev_;
+    gnsship_trk* h_ = nullptr;
+    int channels_ = 0;
+    int code_base_ = 0;
 };
 
 }  // namespace gnsship

@@ -141,6 +141,54 @@ static int acq_test()
     return (static_cast<int>(out.Acq_delay_samples) == bi && out.Acq_doppler_hz == fd && out.positive && out.Acq_samplestamp_samples == 123456) ? 0 : 1;
 }
 
+// Closed-loop tracking through Dll_Pll_Veml_Tracking_Hip: a synthetic GPS L1 C/A signal (PRN 3,
+// 48 dB-Hz, 1500 Hz Doppler) acquired with a 25 Hz / 0.3-sample error; after 300 epochs the
+// carrier Doppler must sit within 5 Hz of the truth and every epoch must advance ~4000 samples.
+static int trk_test()
+{
+    const double fs = 4e6, fd = 1500.0, delay_chips = 200.5;
+    const double fcode = 1.023e6 * (1.0 + fd / 1575.42e6);
+    const int epochs = 300, n = 4000 * (epochs + 3);
+    float code[1023];
+    orc_gps_l1_ca_code_gen_float(code, 3, 0);
+    std::vector<std::complex<float>> x(n);
+    std::mt19937 rng(7);
+    std::normal_distribution<float> g(0.0F, 1.0F);
+    const double amp = std::sqrt(2.0 * std::pow(10.0, 4.8) / fs);
+    for (int i = 0; i < n; i++) {
+        const double ph = i / fs * fcode - delay_chips;
+        const int chip = static_cast<int>(((static_cast<long long>(std::floor(ph)) % 1023) + 1023) % 1023);
+        const double car = 2.0 * M_PI * fd * i / fs + 0.3;
+        x[i] = std::complex<float>(static_cast<float>(amp * code[chip] * std::cos(car) + g(rng)),
+            static_cast<float>(amp * code[chip] * std::sin(car) + g(rng)));
+    }
+    gnsship::Dll_Pll_Conf conf;
+    conf.fs_in = fs;
+    conf.vector_length = 4000;
+    conf.system = 'G';
+    gnsship::Dll_Pll_Veml_Tracking_Hip trk(conf, 2);
+    const double delay_samples = delay_chips / fcode * fs + 0.3;
+    if (!trk.start_tracking(1, code, nullptr, 1023, delay_samples, fd + 25.0, 0, 0)) {
+        std::printf("start_tracking failed: %s\n", trk.last_error());
+        return 1;
+    }
+    std::vector<gnsship_trk_epoch> rec(static_cast<size_t>(epochs) * 2);
+    const int done = trk.work(x.data(), 0, n, epochs, rec.data());
+    if (done != epochs) {
+        std::printf("epochs %d != %d: %s\n", done, epochs, trk.last_error());
+        return 1;
+    }
+    int bad = 0;
+    for (int e = 1; e < epochs; e++) {
+        const gnsship_trk_epoch& r = rec[static_cast<size_t>(e) * 2 + 1];
+        const uint64_t adv = r.sample_counter - rec[static_cast<size_t>(e - 1) * 2 + 1].sample_counter;
+        if (!(r.flags & 8) || adv < 3995 || adv > 4005 || rec[static_cast<size_t>(e) * 2].flags) bad++;
+    }
+    const double dop = rec[static_cast<size_t>(epochs - 1) * 2 + 1].carrier_doppler_hz;
+    std::printf("trk: last Doppler %.3f Hz (truth %.1f), state %d, bad epochs %d\n", dop, fd, trk.state(1), bad);
+    return (bad == 0 && std::fabs(dop - fd) < 5.0 && trk.state(1) == 2) ? 0 : 1;
+}
+
 int main(int argc, char** argv)
 {
     const char* mode = argc > 1 ? argv[1] : "corr";
@@ -152,5 +200,6 @@ int main(int argc, char** argv)
         return 0;
     }
     if (!std::strcmp(mode, "acq")) return acq_test();
+    if (!std::strcmp(mode, "trk")) return trk_test();
     return corr_test();
 }

@@ -1,5 +1,5 @@
 """C++ mirror classes (include/gnsship_cpp.hpp): calculate_threshold's gamma_p_inv on the CPU; the
-correlator / acquisition mirrors on the GPU through tests/cpp/mirror_test (built by `make`)."""
+correlator / acquisition / tracking mirrors on the GPU through tests/cpp/mirror_test (built by `make`)."""
 import os
 import subprocess
 
@@ -36,5 +36,12 @@ def test_hip_multicorrelator_mirror_threads(mirror_bin):
 @pytest.mark.gpu
 def test_pcps_acquisition_mirror(mirror_bin):
     r = subprocess.run([mirror_bin, "acq"], capture_output=True, text=True, timeout=300)
+    print(r.stdout)
+    assert r.returncode == 0, r.stdout + r.stderr
+
+
+@pytest.mark.gpu
+def test_dll_pll_veml_tracking_mirror(mirror_bin):
+    r = subprocess.run([mirror_bin, "trk"], capture_output=True, text=True, timeout=300)
     print(r.stdout)
     assert r.returncode == 0, r.stdout + r.stderr
