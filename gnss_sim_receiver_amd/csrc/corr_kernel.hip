@@ -275,8 +275,20 @@ __global__ __launch_bounds__(kCorrThreads, kCorrWavesPerSimd) void corr_batch_ke
     if (ci >= n_chunks) return;
     const ChunkDesc ch = chunks[ci];
     const DevJob job = jobs[ch.job];
+    float* dst = (job.n_chunks == 1) ? out + static_cast<int64_t>(ch.job) * 2 * kMaxTaps
+                                     : partials + static_cast<int64_t>(chunk_base + ci) * 2 * kMaxTaps;
+    // Idle chunk (tracking channels without a window this round, zero-length jobs): touch neither
+    // the code bank (the job's code slot may be empty) nor the samples.  Workgroup-uniform.
+    if (ch.len <= 0) {
+        if (threadIdx.x < 2 * kMaxTaps) dst[threadIdx.x] = 0.0f;
+        return;
+    }
     const CodeDesc cd = codes[job.code_id];
     const int L = cd.len;
+    if (L <= 0 || cd.ptr == nullptr) {
+        if (threadIdx.x < 2 * kMaxTaps) dst[threadIdx.x] = 0.0f;
+        return;
+    }
     // padded replica in LDS: lds[kCodeMargin + i] = code[i mod L] for i in [−kCodeMargin, L + kCodeMargin)
     const int total = L + 2 * kCodeMargin;
     for (int i = threadIdx.x; i < total; i += kCorrThreads) {
@@ -287,8 +299,6 @@ __global__ __launch_bounds__(kCorrThreads, kCorrWavesPerSimd) void corr_batch_ke
     }
     __syncthreads();
     const float* code = lds_code + kCodeMargin;
-    float* dst = (job.n_chunks == 1) ? out + static_cast<int64_t>(ch.job) * 2 * kMaxTaps
-                                     : partials + static_cast<int64_t>(chunk_base + ci) * 2 * kMaxTaps;
     corr_chunk<FMT, NT, IN_MARGIN>(samples, job, ch, anchors, code, L, dst);
 }
 

@@ -136,3 +136,18 @@ def test_bad_configuration_and_arguments(ctx):
     with pytest.raises(abi.GnssHipError):
         trk.start(0, 999, 0.0, 0.0, 0, 0)  # code not in the bank
     trk.close()
+
+
+def test_idle_channel_with_empty_code_slot():
+    """Regression: a never-started channel's job points at code slot 0; in a fresh context that slot
+    is empty.  Idle chunks must not touch the code bank (illegal address before the fix)."""
+    with engine.Context(0) as fresh:
+        sat, k, x, stamp, first, delay, dop = S.pull_in("GPS", 4e6, 48.0, 900.0, 20.0, 5.0, 0.1, 30)
+        fresh.set_code(77, sat.code)
+        trk = engine.DllPllVemlTracking(fresh, dev_conf(k, "GPS"), 3)
+        trk.start(2, 77, delay, dop, stamp, first)
+        rec, rounds = trk.run(x, 0, 30)
+        assert rounds == 30
+        assert not np.any(rec[:, 0]["flags"]) and not np.any(rec[:, 1]["flags"])
+        compare(rec[:, 2], T.track(k, x, sat.code, delay, dop, stamp, first, 30), "idle")
+        trk.close()
