@@ -48,11 +48,9 @@ __device__ __forceinline__ float hypotf_glibc(float x, float y)
     return static_cast<float>(__dsqrt_rn(__dadd_rn(__dmul_rn(dx, dx), __dmul_rn(dy, dy))));
 }
 
-__global__ void corr_anchor_kernel(const DevJob* __restrict__ jobs, int n_jobs, Anchor* __restrict__ anchors)
+// The reference rotator recursion of one job, stored at every renormalisation point.
+__device__ __forceinline__ void replay_anchors(const DevJob& job, Anchor* __restrict__ anchors)
 {
-    const int j = blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= n_jobs) return;
-    const DevJob job = jobs[j];
     const int nblk = (job.n_samples + kRenorm - 1) / kRenorm;
     Anchor* out = anchors + job.anchor_offset;
     typedef float f2v __attribute__((ext_vector_type(2)));
@@ -79,6 +77,14 @@ __global__ void corr_anchor_kernel(const DevJob* __restrict__ jobs, int n_jobs, 
         pr = p.x;
         pi = p.y;
     }
+}
+
+__global__ void corr_anchor_kernel(const DevJob* __restrict__ jobs, int n_jobs, Anchor* __restrict__ anchors)
+{
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n_jobs) return;
+    const DevJob job = jobs[j];
+    replay_anchors(job, anchors);
 }
 
 template <int FMT>
@@ -262,14 +268,26 @@ __device__ __forceinline__ void corr_chunk(const void* __restrict__ samples, con
 template <int FMT, int NT, bool IN_MARGIN>
 __global__ __launch_bounds__(kCorrThreads, kCorrWavesPerSimd) void corr_batch_kernel(const void* __restrict__ samples, const DevJob* __restrict__ jobs,
     const ChunkDesc* __restrict__ chunks, int n_chunks, int chunk_base, const CodeDesc* __restrict__ codes,
-    const Anchor* __restrict__ anchors, float* __restrict__ partials, float* __restrict__ out)
+    const Anchor* __restrict__ anchors, float* __restrict__ partials, float* __restrict__ out, AnchorPrefetch pf)
 {
     extern __shared__ __attribute__((aligned(16))) float lds_code[];
+    // Leading workgroups replay the rotator anchors of ANOTHER batch (the next one of a
+    // double-buffered pair): one lane per job, latency-bound chains that run beside the
+    // correlation instead of in a separate stream behind a cross-queue event.
+    if (static_cast<int>(blockIdx.x) < pf.n_blocks) {
+        const int j = blockIdx.x * kCorrThreads + threadIdx.x;
+        if (j < pf.n_jobs) {
+            const DevJob pj = pf.jobs[j];
+            replay_anchors(pj, pf.anchors);
+        }
+        return;
+    }
     // XCD-aware chunk order: workgroups are dealt round-robin over the 8 XCDs (b and b+8 share
     // one), so give each XCD a CONTIGUOUS range of chunks.  Jobs arrive epoch-major, so the
     // channels that read the same IF samples then share one XCD's L2 (bijective for any grid).
-    const int nb = static_cast<int>(gridDim.x);
-    const int b = blockIdx.x;
+    // pf.n_blocks is a multiple of 8, so b keeps the hardware's b mod 8 placement.
+    const int nb = static_cast<int>(gridDim.x) - pf.n_blocks;
+    const int b = blockIdx.x - pf.n_blocks;
     const int q = nb >> 3, rmd = nb & 7, x = b & 7;
     const int ci = x * q + (x < rmd ? x : rmd) + (b >> 3);
     if (ci >= n_chunks) return;
@@ -317,9 +335,20 @@ __global__ void corr_reduce_kernel(const DevJob* __restrict__ jobs, int n_jobs, 
 
 hipError_t launch_corr_batch(const void* samples, int fmt, const DevJob* jobs, int n_jobs, const ChunkDesc* chunks, int n_chunks,
     const ChunkClass* classes, const CodeDesc* codes, int max_code_len, bool any_multi_chunk, Anchor* anchors, float* partials, float* out,
-    hipStream_t stream, int stages)
+    hipStream_t stream, int stages, const AnchorPrefetch* prefetch)
 {
-    if (n_chunks <= 0) return hipSuccess;
+    AnchorPrefetch pf{nullptr, 0, nullptr, 0};
+    if (prefetch && prefetch->n_jobs > 0 && (stages & GNSSHIP_STAGE_CORRELATE)) {
+        pf = *prefetch;
+        pf.n_blocks = ((pf.n_jobs + kCorrThreads - 1) / kCorrThreads + 7) & ~7;
+    }
+    if (n_chunks <= 0) {
+        if (pf.n_jobs > 0) {
+            hipLaunchKernelGGL(corr_anchor_kernel, dim3((pf.n_jobs + 63) / 64), dim3(64), 0, stream, pf.jobs, pf.n_jobs, pf.anchors);
+            return hipGetLastError();
+        }
+        return hipSuccess;
+    }
     if (max_code_len < 1 || max_code_len > kMaxCodeLen) return hipErrorInvalidValue;
     hipError_t e = hipSuccess;
     if (stages & GNSSHIP_STAGE_ANCHORS) {
@@ -334,9 +363,9 @@ hipError_t launch_corr_batch(const void* samples, int fmt, const DevJob* jobs, i
         if (cnt <= 0) continue;
         const ChunkDesc* cc = chunks + classes[c].start;
         const int cb = classes[c].start;
-        dim3 grid(cnt), block(kCorrThreads);
+        dim3 grid(cnt + pf.n_blocks), block(kCorrThreads);
 #define GNSSHIP_LAUNCH_CORR(F, NTV, MV) \
-    hipLaunchKernelGGL((corr_batch_kernel<F, NTV, MV>), grid, block, lds, stream, samples, jobs, cc, cnt, cb, codes, anchors, partials, out)
+    hipLaunchKernelGGL((corr_batch_kernel<F, NTV, MV>), grid, block, lds, stream, samples, jobs, cc, cnt, cb, codes, anchors, partials, out, pf)
 #define GNSSHIP_LAUNCH_NT(F)                                                     \
     switch (c) {                                                                 \
     case 0: GNSSHIP_LAUNCH_CORR(F, 1, false); break;                             \
@@ -358,6 +387,7 @@ hipError_t launch_corr_batch(const void* samples, int fmt, const DevJob* jobs, i
 #undef GNSSHIP_LAUNCH_CORR
         e = hipGetLastError();
         if (e != hipSuccess) return e;
+        pf = AnchorPrefetch{nullptr, 0, nullptr, 0};  // only the first class launch carries the prefetch
     }
     e = hipGetLastError();
     if (e != hipSuccess || !any_multi_chunk) return e;

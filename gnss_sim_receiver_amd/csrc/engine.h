@@ -79,10 +79,19 @@ inline int chunk_class(int n_taps, int in_margin)
     return 2 * tc + (in_margin ? 1 : 0);
 }
 
-// anchors: scratch of Σ ceil(n_j/256) Anchor entries, recomputed by every launch.
+// Anchor replay of another job set carried by a correlation launch (leading workgroups).
+struct AnchorPrefetch {
+    const DevJob* jobs;
+    int32_t n_jobs;
+    Anchor* anchors;
+    int32_t n_blocks;  // set by launch_corr_batch
+};
+
+// anchors: scratch of Σ ceil(n_j/256) Anchor entries, recomputed by every launch.  prefetch
+// (optional, with the CORRELATE stage): replay `prefetch->jobs`' anchors in the same launch.
 hipError_t launch_corr_batch(const void* samples, int fmt, const DevJob* jobs, int n_jobs, const ChunkDesc* chunks, int n_chunks,
     const ChunkClass* classes, const CodeDesc* codes, int max_code_len, bool any_multi_chunk, Anchor* anchors, float* partials, float* out,
-    hipStream_t stream, int stages = GNSSHIP_STAGE_ANCHORS | GNSSHIP_STAGE_CORRELATE);
+    hipStream_t stream, int stages = GNSSHIP_STAGE_ANCHORS | GNSSHIP_STAGE_CORRELATE, const AnchorPrefetch* prefetch = nullptr);
 
 }  // namespace gnsship
 

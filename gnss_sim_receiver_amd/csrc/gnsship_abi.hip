@@ -320,6 +320,9 @@ struct gnsship_batch {
     hipStream_t aux = nullptr;
     hipEvent_t anchors_ready = nullptr;  // aux → ctx: anchors written
     hipEvent_t corr_done = nullptr;      // ctx → aux: correlation finished reading the anchors
+    // gnsship_batch_launch_pipelined: anchors of the current job set already written on the context
+    // stream (by a launch that carried this batch as `next`); cleared by set_jobs.
+    bool anchors_valid = false;
 };
 
 static void batch_release(gnsship_batch* b)
@@ -362,6 +365,7 @@ extern "C" int gnsship_batch_set_jobs(gnsship_batch* b, const gnsship_corr_job* 
     gnsship_ctx* ctx = b->ctx;
     if ((!jobs && n_jobs) || n_jobs < 0 || n_jobs > b->max_jobs) return fail(ctx, GNSSHIP_E_INVAL, "gnsship_batch_set_jobs: n_jobs out of range");
     if (int rc = set_device(ctx)) return rc;
+    b->anchors_valid = false;
     if (int rc = sync_code_table(ctx)) return rc;
     b->jobs_host.resize(n_jobs);
     int max_len = 1;
@@ -429,6 +433,40 @@ extern "C" int gnsship_batch_launch_stages(gnsship_batch* b, const void* dev_sam
         if (e != hipSuccess) return hip_fail(ctx, e, "launch_corr_batch(correlate)");
         HIP_TRY(ctx, hipEventRecord(b->corr_done, ctx->stream));
     }
+    return GNSSHIP_OK;
+}
+
+// Correlate `b` and, in the same launch, replay the rotator anchors of `next` (leading workgroups
+// of the correlation grid; see corr_batch_kernel).  Everything on the context stream, so a
+// double-buffered pair A, B, A, B, ... needs no cross-stream event: each launch finds its anchors
+// written by the previous one, and same-stream order keeps the next replay from overwriting
+// anchors a correlation still reads.  `b`'s anchors are computed first when no earlier launch
+// prefetched them (first call, or after set_jobs).
+extern "C" int gnsship_batch_launch_pipelined(gnsship_batch* b, const void* dev_samples, int fmt, gnsship_batch* next)
+{
+    if (!b) return GNSSHIP_E_INVAL;
+    gnsship_ctx* ctx = b->ctx;
+    if (fmt_bytes(fmt) == 0) return fail(ctx, GNSSHIP_E_INVAL, "gnsship_batch_launch_pipelined: unknown sample format");
+    if (next == b || (next && next->ctx != ctx)) return fail(ctx, GNSSHIP_E_INVAL, "gnsship_batch_launch_pipelined: next must be another batch of the same context");
+    if (!dev_samples && b->n_jobs) return fail(ctx, GNSSHIP_E_INVAL, "gnsship_batch_launch_pipelined: null sample buffer");
+    if (ctx->codes_dirty) return fail(ctx, GNSSHIP_E_STATE, "gnsship_batch_launch_pipelined: code bank changed after set_jobs");
+    if (int rc = set_device(ctx)) return rc;
+    AnchorPrefetch pf{nullptr, 0, nullptr, 0};
+    const bool prefetch = next && next->n_jobs > 0;
+    if (prefetch) pf = AnchorPrefetch{next->jobs_dev, next->n_jobs, next->anchors_dev, 0};
+    if (b->n_jobs > 0 && !b->anchors_valid) {
+        hipError_t e = launch_corr_batch(dev_samples, fmt, b->jobs_dev, b->n_jobs, b->chunks_dev, b->n_chunks, b->classes, ctx->codes_dev,
+            b->max_code_len, b->any_multi, b->anchors_dev, b->partials_dev, b->out_dev, ctx->stream, GNSSHIP_STAGE_ANCHORS);
+        if (e != hipSuccess) return hip_fail(ctx, e, "launch_corr_batch(anchors)");
+    }
+    if (b->n_jobs > 0 || prefetch) {
+        hipError_t e = launch_corr_batch(dev_samples, fmt, b->jobs_dev, b->n_jobs, b->chunks_dev, b->n_jobs > 0 ? b->n_chunks : 0, b->classes,
+            ctx->codes_dev, b->max_code_len, b->any_multi, b->anchors_dev, b->partials_dev, b->out_dev, ctx->stream, GNSSHIP_STAGE_CORRELATE,
+            prefetch ? &pf : nullptr);
+        if (e != hipSuccess) return hip_fail(ctx, e, "launch_corr_batch(pipelined)");
+    }
+    b->anchors_valid = b->n_jobs > 0;
+    if (prefetch) next->anchors_valid = true;
     return GNSSHIP_OK;
 }
 

@@ -210,6 +210,12 @@ class CorrelatorBatch:
     def launch_ptr(self, dev_ptr: int, fmt: int = FMT_CF32, stages: int = 3):
         check(self.ctx.lib.gnsship_batch_launch_stages(self.h, dev_ptr, fmt, stages), "gnsship_batch_launch_stages", self.ctx.h)
 
+    def launch_pipelined(self, dev_ptr: int, fmt: int = FMT_CF32, next_batch: "CorrelatorBatch" = None):
+        """Correlate this batch and replay `next_batch`'s anchors in the same launch
+        (gnsship_batch_launch_pipelined): alternate two batches A, B, A, B, ... on the context stream."""
+        nh = next_batch.h if next_batch is not None else None
+        check(self.ctx.lib.gnsship_batch_launch_pipelined(self.h, dev_ptr, fmt, nh), "gnsship_batch_launch_pipelined", self.ctx.h)
+
     def results(self) -> np.ndarray:
         out = np.zeros((self.n_jobs, 2 * MAX_TAPS), np.float32)
         check(self.ctx.lib.gnsship_batch_results(self.h, fptr(out)), "gnsship_batch_results", self.ctx.h)

@@ -145,6 +145,12 @@ int gnsship_batch_launch(gnsship_batch* b, const void* dev_samples, int fmt);
 #define GNSSHIP_STAGE_CORRELATE 2
 int gnsship_batch_launch_stages(gnsship_batch* b, const void* dev_samples, int fmt, int stages);
 /* Wait for the last launch and copy results: out[j*2*GNSSHIP_MAX_TAPS + 2*t + {0,1}] = tap t of job j. */
+/* Correlate b and, inside the same launch, replay the rotator anchors of `next` (another batch of the
+ * same context; NULL for none) — the double-buffered form of batch_launch for a pair of batches
+ * alternated on the context stream, with no cross-stream event per launch.  b's own anchors come
+ * from the previous launch that named it as `next` (or are computed first).  Do not mix with
+ * gnsship_batch_launch_stages on the same batches. */
+int gnsship_batch_launch_pipelined(gnsship_batch* b, const void* dev_samples, int fmt, gnsship_batch* next);
 int gnsship_batch_results(gnsship_batch* b, float* out);
 /* Device pointer of the result array (n_jobs × GNSSHIP_MAX_TAPS complex<float>). */
 int gnsship_batch_results_device(gnsship_batch* b, void** dev_out);

@@ -176,3 +176,44 @@ def test_device_resident_buffer_large_batch_properties(ctx):
     ref = O.corr_batch(sig, jobs[pick], cl, n_threads=8)
     for r, j in enumerate(pick):
         assert rel_err(out[j, :3], ref[r, :3]) <= TOL
+
+
+def test_pipelined_pair_matches_plain_launches(ctx):
+    """gnsship_batch_launch_pipelined: A, B, A, B with each launch replaying the other batch's
+    anchors gives exactly the plain launch results (same kernels, same anchors), including after
+    set_jobs invalidates a batch's prefetched anchors."""
+    fs = 4e6
+    sats = signals.random_sky(6, seed=41)
+    sig = signals.generate_if(fs, 4000 * 40, sats, seed=42)
+    dev = ctx.upload(sig)
+    ja = np.concatenate([signals.truth_jobs(s, fs, 12, 4000, [-0.25, 0.0, 0.25], k) for k, s in enumerate(sats[:3])])
+    jb = np.concatenate([signals.truth_jobs(s, fs, 9, 4000, [-0.5, -0.25, 0.0, 0.25, 0.5], k + 3, first_epoch=20)
+                         for k, s in enumerate(sats[3:])])
+    for k, s in enumerate(sats):
+        ctx.set_code(k, s.code)
+    A, B = engine.CorrelatorBatch(ctx, len(ja)), engine.CorrelatorBatch(ctx, len(jb))
+    A.set_jobs(ja, len(sig))
+    B.set_jobs(jb, len(sig))
+    A.launch_ptr(dev.ptr)
+    ref_a = A.results()
+    B.launch_ptr(dev.ptr)
+    ref_b = B.results()
+    for rnd in range(3):
+        A.launch_pipelined(dev.ptr, next_batch=B)
+        assert np.array_equal(A.results(), ref_a), rnd
+        B.launch_pipelined(dev.ptr, next_batch=A)
+        assert np.array_equal(B.results(), ref_b), rnd
+    # new jobs for A: its prefetched anchors are stale and must be recomputed
+    ja2 = ja.copy()
+    ja2["rem_carrier_phase_rad"] += np.float32(0.7)
+    A.set_jobs(ja2, len(sig))
+    A.launch_pipelined(dev.ptr, next_batch=B)
+    got = A.results()
+    ref = O.corr_batch(sig, ja2, [s.code for s in sats], n_threads=8)
+    for j in range(len(ja2)):
+        assert rel_err(got[j, :3], ref[j, :3]) <= TOL
+    with pytest.raises(abi.GnssHipError):
+        A.launch_pipelined(dev.ptr, next_batch=A)
+    A.close()
+    B.close()
+    dev.free()
