@@ -44,3 +44,17 @@ $(MIRROR_TEST): tests/cpp/mirror_test.cpp include/gnsship_cpp.hpp include/gnsshi
 	gcc -O2 -fPIC -ffp-contract=off -std=gnu11 -c oracle/gnss_oracle.c -o build/gnss_oracle_test.o
 	g++ -O2 -std=c++17 -Iinclude tests/cpp/mirror_test.cpp build/gnss_oracle_test.o -o $@ -L$(PKG) -lgnsship -Wl,-rpath,'$$ORIGIN/../../$(PKG)' -lpthread -lm
 all: $(MIRROR_TEST)
+
+# Profiling variant (workgroup phase timestamps in corr_batch_kernel; scripts/corr_wg_profile.py)
+PROF_LIB := scripts/libgnsship_prof.so
+PROF_OBJS := $(patsubst $(CSRC)/%.hip,build/prof_obj/%.o,$(HIP_SRCS)) $(patsubst $(CSRC)/%.cpp,build/prof_obj/%.cpp.o,$(CPP_SRCS))
+build/prof_obj/%.o: $(CSRC)/%.hip $(HDRS)
+	@mkdir -p build/prof_obj
+	$(HIPCC) $(HIPFLAGS) -DGNSSHIP_CORR_PROFILE -c $< -o $@
+build/prof_obj/%.cpp.o: $(CSRC)/%.cpp $(HDRS)
+	@mkdir -p build/prof_obj
+	$(HIPCC) $(HIPFLAGS) -x c++ -c $< -o $@
+$(PROF_LIB): $(PROF_OBJS)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(PROF_OBJS)
+prof: $(PROF_LIB)
+.PHONY: prof

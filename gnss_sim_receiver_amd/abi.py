@@ -196,10 +196,12 @@ def load() -> ctypes.CDLL:
     global _LIB
     if _LIB is not None:
         return _LIB
-    if not os.path.exists(LIB_PATH):
-        raise RuntimeError(f"{LIB_PATH} is missing: build it with `make` or __graft_entry__.build(); "
+    # GNSSHIP_LIB_PATH: tooling only (scripts/corr_wg_profile.py loads the instrumented build)
+    path = os.environ.get("GNSSHIP_LIB_PATH", LIB_PATH)
+    if not os.path.exists(path):
+        raise RuntimeError(f"{path} is missing: build it with `make` or __graft_entry__.build(); "
                            "the GNSS engine has no CPU fallback")
-    lib = ctypes.CDLL(LIB_PATH)
+    lib = ctypes.CDLL(path)
     for name, (argtypes, restype) in _SIGNATURES.items():
         fn = getattr(lib, name)  # AttributeError if the symbol is not exported
         fn.argtypes = argtypes

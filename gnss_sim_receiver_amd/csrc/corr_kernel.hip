@@ -36,6 +36,20 @@
 
 namespace gnsship {
 
+// Workgroup phase timestamps for the profiling build only (make prof → libgnsship_prof.so,
+// scripts/corr_wg_profile.py): slot [8·blockIdx + k] = wall_clock64() at phase k, thread 0.
+#ifdef GNSSHIP_CORR_PROFILE
+__device__ unsigned long long* g_corr_prof = nullptr;
+#define GNSSHIP_PROF_STAMP(k)                                                                                                        \
+    do {                                                                                                                             \
+        if (threadIdx.x == 0 && g_corr_prof) g_corr_prof[static_cast<size_t>(blockIdx.x) * 8 + (k)] = wall_clock64();               \
+    } while (0)
+#else
+#define GNSSHIP_PROF_STAMP(k) \
+    do {                      \
+    } while (0)
+#endif
+
 __device__ __forceinline__ float2 cmul_rn(float ar, float ai, float br, float bi)
 {
     return make_float2(__fsub_rn(__fmul_rn(ar, br), __fmul_rn(ai, bi)), __fadd_rn(__fmul_rn(ar, bi), __fmul_rn(ai, br)));
@@ -64,7 +78,7 @@ __device__ __forceinline__ void replay_anchors(const DevJob& job, Anchor* __rest
         // sample 256k uses `a = phase`; then phase /= |phase|; then 256 rotations reach 256(k+1)
         const float m = hypotf_glibc(pr, pi);
         const float qr = __fdiv_rn(pr, m), qi = __fdiv_rn(pi, m);
-        out[k] = Anchor{pr, pi, qr, qi};
+        out[k] = Anchor{qr, qi};
         f2v p = {qr, qi};
         if (k != nblk - 1) {
 #pragma unroll 16
@@ -117,6 +131,16 @@ __device__ __forceinline__ f2 cmul_pk(f2 a, f2 b, f2 bsw)
     return __builtin_elementwise_fma(f2{a.y, a.y}, bsw, f2{a.x, a.x} * b);
 }
 
+// x·p for packed complex values in two VOP3P instructions, the operand swizzles in op_sel /
+// neg modifiers (no moves):  t = (x.re·p.re, x.re·p.im);  x·p = (x.im·(−p.im) + t.re, x.im·p.re + t.im)
+__device__ __forceinline__ f2 cmul_pk2(f2 x, f2 p)
+{
+    f2 t, r;
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]" : "=v"(t) : "v"(x), "v"(p));
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[0,1,0]" : "=v"(r) : "v"(x), "v"(p), "v"(t));
+    return r;
+}
+
 // (int)floor(x) in one instruction (V_CVT_FLR_I32_F32), as the resampler's (int)floor(...) for
 // in-range values.
 __device__ __forceinline__ int cvt_floor_i32(float x)
@@ -138,139 +162,118 @@ __device__ __forceinline__ int wrap_index(int idx, int L)
     return idx;
 }
 
-// One chunk of one job.  `code` points at chip 0 of the padded LDS replica (valid indices
-// [−kCodeMargin, L + kCodeMargin)).  IN_MARGIN: the host proved every index of the job lies in the
-// padded range, so the chip index is used directly (no modulo).
-template <int FMT, int NT, bool IN_MARGIN>
-__device__ __forceinline__ void corr_chunk(const void* __restrict__ samples, const DevJob& job, const ChunkDesc& ch,
-    const Anchor* __restrict__ anchors, const float* __restrict__ code, int L, float* __restrict__ dst)
+#ifndef GNSSHIP_CORR_GROUP
+#define GNSSHIP_CORR_GROUP 4
+#endif
+constexpr int kGroup = GNSSHIP_CORR_GROUP;  // samples per lane per pipeline stage
+constexpr int kGroups = kCorrSamplesPerThread / kGroup;
+constexpr int kGroupSpan = kGroup * kCorrThreads;
+static_assert(kGroups % 2 == 0, "ping-pong over pairs of groups");
+
+// Samples of pipeline group g for this lane.  Whole groups inside the chunk load without any tail
+// test; in the (at most one) partial group, lanes past the chunk end read the chunk's last sample
+// and contribute zero.
+template <int FMT>
+__device__ __forceinline__ void load_group(const void* __restrict__ samples, int64_t base, int len, int g, f2 (&dstx)[kGroup])
 {
-    __shared__ float red[kCorrThreads / 64][2 * kMaxTaps];
-    if (ch.len <= 0) {  // zero-length job (workgroup-uniform): nothing to read, outputs are zero
-        if (threadIdx.x < 2 * kMaxTaps) dst[threadIdx.x] = 0.0f;
-        return;
-    }
-
-    f2 acc[NT];
-#pragma unroll
-    for (int t = 0; t < NT; t++) acc[t] = f2{0.0f, 0.0f};
-    float shifts[NT];
-#pragma unroll
-    for (int t = 0; t < NT; t++) shifts[t] = (t < job.n_taps) ? job.shifts[t] : 0.0f;
-
-    const int tid = threadIdx.x;  // == offset j inside every 256-sample block this lane visits
-    const int64_t base = job.sample_offset + ch.start;
-    // E_j = |inc|^j · e^{i j Δ}: rotation from the renormalised anchor to sample 256k + j
-    // (angle formed and range-reduced in double, then an accurate float sincos)
-    f2 e, esw;
-    {
-        constexpr double kTwoPi = 6.283185307179586476925286766559;
-        constexpr double kInvTwoPi = 0.15915494309189533576888376337251;
-        double th = static_cast<double>(tid) * job.dtheta;
-        th = fma(-kTwoPi, rint(th * kInvTwoPi), th);
-        float s, c;
-        sincosf(static_cast<float>(th), &s, &c);
-        const float mag = __fmaf_rn(static_cast<float>(tid), job.log_mag_inc, 1.0f);
-        e = f2{mag * c, mag * s};
-        esw = f2{-e.y, e.x};
-    }
-    const Anchor* anc = anchors + job.anchor_offset + (ch.start >> 8);
-    const int last_blk = (ch.len - 1) >> 8;  // last 256-sample block of the chunk (chunk-uniform)
-    const bool lane_j0 = (tid == 0);
-
-    // Software pipeline over groups of kGroup samples per lane, ping-pong register buffers: the
-    // loads of group g+1 are in flight while group g is correlated.  Whole groups inside the chunk
-    // run without any tail test; in the (at most one) partial group, lanes past the chunk end read
-    // the chunk's last sample and contribute zero.
-    constexpr int kGroup = 4;
-    constexpr int kGroups = kCorrSamplesPerThread / kGroup;
-    constexpr int kGroupSpan = kGroup * kCorrThreads;
-    static_assert(kGroups % 2 == 0, "ping-pong over pairs of groups");
-    auto load_group = [&](int g, f2 (&dstx)[kGroup]) {
-        if ((g + 1) * kGroupSpan <= ch.len) {
-#pragma unroll
-            for (int u = 0; u < kGroup; u++) {
-                const float2 v = load_sample<FMT>(samples, base + tid + (g * kGroup + u) * kCorrThreads);
-                dstx[u] = f2{v.x, v.y};
-            }
-        } else {
-#pragma unroll
-            for (int u = 0; u < kGroup; u++) {
-                const int r = tid + (g * kGroup + u) * kCorrThreads;
-                const float2 v = load_sample<FMT>(samples, base + (r < ch.len ? r : ch.len - 1));
-                dstx[u] = (r < ch.len) ? f2{v.x, v.y} : f2{0.0f, 0.0f};
-            }
-        }
-    };
-    auto correlate_group = [&](int g, const f2 (&xg)[kGroup]) {
-        // anchors of this group's 256-sample blocks: chunk-uniform addresses → scalar loads
-        Anchor ag[kGroup];
+    const int tid = threadIdx.x;
+    if ((g + 1) * kGroupSpan <= len) {
 #pragma unroll
         for (int u = 0; u < kGroup; u++) {
-            const int m = g * kGroup + u;
-            ag[u] = anc[m < last_blk ? m : last_blk];
+            const float2 v = load_sample<FMT>(samples, base + tid + (g * kGroup + u) * kCorrThreads);
+            dstx[u] = f2{v.x, v.y};
         }
-        const bool full = (g + 1) * kGroupSpan <= ch.len;  // group-uniform
+    } else {
 #pragma unroll
         for (int u = 0; u < kGroup; u++) {
             const int r = tid + (g * kGroup + u) * kCorrThreads;
-            const int n = ch.start + (full ? r : (r < ch.len ? r : ch.len - 1));  // reference loop counter
-            // phasor at sample n: the anchor itself at j = 0, else q_k · E_j (select, no branch)
-            const f2 pq = cmul_pk(f2{ag[u].q_re, ag[u].q_im}, e, esw);
-            const f2 p = lane_j0 ? f2{ag[u].a_re, ag[u].a_im} : pq;
-            const f2 tt = cmul_pk(xg[u], p, f2{-p.y, p.x});  // in_common[n] * phase
-            // code resampler, generic association order: ((step*n) + shift) - rem, each rounded
-            // on its own (the file is built with -ffp-contract=off)
-            const float sn = job.code_step * static_cast<float>(n);
-#pragma unroll
-            for (int t = 0; t < NT; t++) {
-                int idx = cvt_floor_i32((sn + shifts[t]) - job.rem_code);
-                if constexpr (!IN_MARGIN) idx = wrap_index(idx, L);
-                const float cv = code[idx];
-                acc[t] = __builtin_elementwise_fma(tt, f2{cv, cv}, acc[t]);
-            }
+            const float2 v = load_sample<FMT>(samples, base + (r < len ? r : len - 1));
+            dstx[u] = (r < len) ? f2{v.x, v.y} : f2{0.0f, 0.0f};
         }
-    };
-    f2 xa[kGroup], xb[kGroup];
-    load_group(0, xa);
-#pragma unroll
-    for (int g = 0; g < kGroups; g += 2) {
-        if (g * kGroupSpan >= ch.len) break;  // chunk-uniform
-        if ((g + 1) * kGroupSpan < ch.len) load_group(g + 1, xb);
-        correlate_group(g, xa);
-        if ((g + 1) * kGroupSpan >= ch.len) break;
-        if (g + 2 < kGroups && (g + 2) * kGroupSpan < ch.len) load_group(g + 2, xa);
-        correlate_group(g + 1, xb);
     }
+}
 
-    const int lane = tid & 63, wave = tid >> 6;
+// E_j = |inc|^j · e^{i j Δ}: rotation from a renormalised anchor to sample 256k + j, for this
+// lane's j = threadIdx.x (angle formed and range-reduced in double, then an accurate float sincos).
+__device__ __forceinline__ f2 anchor_to_lane_rotation(const DevJob& job)
+{
+    constexpr double kTwoPi = 6.283185307179586476925286766559;
+    constexpr double kInvTwoPi = 0.15915494309189533576888376337251;
+    const int tid = threadIdx.x;
+    double th = static_cast<double>(tid) * job.dtheta;
+    th = fma(-kTwoPi, rint(th * kInvTwoPi), th);
+    float s, c;
+    sincosf(static_cast<float>(th), &s, &c);
+    const float mag = __fmaf_rn(static_cast<float>(tid), job.log_mag_inc, 1.0f);
+    return f2{mag * c, mag * s};
+}
+
+// Correlation of one pipeline group (kGroup samples per lane) of one chunk into acc.
+// `code` points at chip 0 of the padded LDS replica (valid indices [−kCodeMargin, L + kCodeMargin)).
+// IN_MARGIN: the host proved every chip index of the job lies in the padded range (no modulo).
+// FULL: the whole group lies inside the chunk (group-uniform; only a chunk's last group can be
+// partial) — no tail clamps in the fast path.
+template <int NT, bool IN_MARGIN, bool FULL>
+__device__ __forceinline__ void correlate_group(const DevJob& job, const ChunkDesc& ch, const Anchor (&qk)[kBlocksPerChunk], f2 e,
+    f2 esw, const float (&shifts)[NT], const float* __restrict__ code, int L, int g, const f2 (&xg)[kGroup], f2 (&acc)[NT])
+{
+    const int tid = threadIdx.x;  // == offset j inside every 256-sample block this lane visits
+    // phase 1: every chip index of the group and its LDS read, all in flight together (the code
+    // resampler, generic association order ((step*n) + shift) - rem, each rounded on its own; the
+    // file is built with -ffp-contract=off)
+    float cv[kGroup][NT];
 #pragma unroll
-    for (int t = 0; t < NT; t++) {
-        const float wr = wave_sum(acc[t].x), wi = wave_sum(acc[t].y);
-        if (lane == 0) {
-            red[wave][2 * t] = wr;
-            red[wave][2 * t + 1] = wi;
+    for (int u = 0; u < kGroup; u++) {
+        const int r = tid + (g * kGroup + u) * kCorrThreads;
+        const int n = ch.start + (FULL ? r : (r < ch.len ? r : ch.len - 1));  // reference loop counter
+        const float sn = job.code_step * static_cast<float>(n);
+#pragma unroll
+        for (int t = 0; t < NT; t++) {
+            int idx = cvt_floor_i32((sn + shifts[t]) - job.rem_code);
+            if constexpr (!IN_MARGIN) idx = wrap_index(idx, L);
+            cv[u][t] = code[idx];
         }
     }
-    __syncthreads();
-    if (tid < 2 * kMaxTaps) {
-        float s = 0.0f;
-        if (tid < 2 * NT && tid < 2 * job.n_taps) {
+    // phase 2: phasor at sample n = 256k + j: q_k · E_j, with E_0 = 1 — lane 0 uses the
+    // renormalised anchor q_k where the reference uses a_k = |a_k|·q_k (|a_k| − 1 ≲ 1.5e-5 on one
+    // sample in 256: ≲ 6e-8 of a tap sum); then in_common[n]·phase and the tap sums
 #pragma unroll
-            for (int w = 0; w < kCorrThreads / 64; w++) s += red[w][tid];
-        }
-        dst[tid] = s;
+    for (int u = 0; u < kGroup; u++) {
+        const Anchor& a = qk[g * kGroup + u];  // block of sample u: chunk-uniform (SGPRs)
+        const f2 p = cmul_pk(f2{a.q_re, a.q_im}, e, esw);
+        const f2 tt = cmul_pk2(xg[u], p);
+#pragma unroll
+        for (int t = 0; t < NT; t++) acc[t] = __builtin_elementwise_fma(tt, f2{cv[u][t], cv[u][t]}, acc[t]);
     }
+}
+
+// Waves per SIMD the register allocation must allow: the 1- and 3-tap classes (GPS/B1I E-P-L, E1
+// data prompt) are held to 64 VGPRs for full occupancy — the kernel is latency-bound, residency is
+// its throughput; wider tap classes keep the general bound.
+#ifndef GNSSHIP_CORR_WAVES_EPL
+#define GNSSHIP_CORR_WAVES_EPL 6
+#endif
+template <int NT, bool IN_MARGIN>
+constexpr int corr_waves_per_simd()
+{
+    return (NT <= 3 && IN_MARGIN) ? GNSSHIP_CORR_WAVES_EPL : kCorrWavesPerSimd;
 }
 
 // One launch per chunk class (tap-count template × in-margin flag), so each kernel is compiled
 // for exactly its path and the register allocation is not the worst case over all variants.
+// One workgroup per WORK ITEM: up to kMaxChunksPerItem chunks sharing one code replica
+// (consecutive chunks of one long job, or same-code jobs such as consecutive epochs of one
+// channel).  Per workgroup the replica is staged in LDS once, the sample pipeline runs on across
+// chunk boundaries (the next chunk's first group loads while this chunk's last group is
+// correlated), per-chunk wave sums park in LDS, and one barrier closes the item.
 template <int FMT, int NT, bool IN_MARGIN>
-__global__ __launch_bounds__(kCorrThreads, kCorrWavesPerSimd) void corr_batch_kernel(const void* __restrict__ samples, const DevJob* __restrict__ jobs,
-    const ChunkDesc* __restrict__ chunks, int n_chunks, int chunk_base, const CodeDesc* __restrict__ codes,
+__global__ __launch_bounds__(kCorrThreads, (corr_waves_per_simd<NT, IN_MARGIN>())) void corr_batch_kernel(const void* __restrict__ samples,
+    const DevJob* __restrict__ jobs, const ChunkDesc* __restrict__ chunks, const WorkItem* __restrict__ items, int n_items,
     const Anchor* __restrict__ anchors, float* __restrict__ partials, float* __restrict__ out, AnchorPrefetch pf)
 {
     extern __shared__ __attribute__((aligned(16))) float lds_code[];
+    __shared__ float red[kMaxChunksPerItem][kCorrThreads / 64][2 * NT];
+    GNSSHIP_PROF_STAMP(0);
     // Leading workgroups replay the rotator anchors of ANOTHER batch (the next one of a
     // double-buffered pair): one lane per job, latency-bound chains that run beside the
     // correlation instead of in a separate stream behind a cross-queue event.
@@ -280,47 +283,148 @@ __global__ __launch_bounds__(kCorrThreads, kCorrWavesPerSimd) void corr_batch_ke
             const DevJob pj = pf.jobs[j];
             replay_anchors(pj, pf.anchors);
         }
+        GNSSHIP_PROF_STAMP(5);
         return;
     }
-    // XCD-aware chunk order: workgroups are dealt round-robin over the 8 XCDs (b and b+8 share
-    // one), so give each XCD a CONTIGUOUS range of chunks.  Jobs arrive epoch-major, so the
-    // channels that read the same IF samples then share one XCD's L2 (bijective for any grid).
-    // pf.n_blocks is a multiple of 8, so b keeps the hardware's b mod 8 placement.
+    // XCD-aware item order: workgroups are dealt round-robin over the 8 XCDs (b and b+8 share one),
+    // so give each XCD a CONTIGUOUS range of items.  Jobs arrive epoch-major, so the channels that
+    // read the same IF samples then share one XCD's L2 (bijective for any grid).  pf.n_blocks is a
+    // multiple of 8, so b keeps the hardware's b mod 8 placement.
     const int nb = static_cast<int>(gridDim.x) - pf.n_blocks;
     const int b = blockIdx.x - pf.n_blocks;
     const int q = nb >> 3, rmd = nb & 7, x = b & 7;
-    const int ci = x * q + (x < rmd ? x : rmd) + (b >> 3);
-    if (ci >= n_chunks) return;
-    const ChunkDesc ch = chunks[ci];
-    const DevJob job = jobs[ch.job];
-    float* dst = (job.n_chunks == 1) ? out + static_cast<int64_t>(ch.job) * 2 * kMaxTaps
-                                     : partials + static_cast<int64_t>(chunk_base + ci) * 2 * kMaxTaps;
-    // Idle chunk (tracking channels without a window this round, zero-length jobs): touch neither
-    // the code bank (the job's code slot may be empty) nor the samples.  Workgroup-uniform.
-    if (ch.len <= 0) {
-        if (threadIdx.x < 2 * kMaxTaps) dst[threadIdx.x] = 0.0f;
+    const int ii = x * q + (x < rmd ? x : rmd) + (b >> 3);
+    if (ii >= n_items) return;
+    const WorkItem it = items[ii];
+    const ChunkDesc c0 = chunks[it.first];
+    const int L = c0.code_len;  // one replica for the whole item
+    if (L <= 0 || c0.code == nullptr) {  // no code (never happens for a valid plan): outputs zero
+        for (int c = 0; c < it.count; c++) {
+            const ChunkDesc cz = chunks[it.first + c];
+            const DevJob& jz = jobs[cz.job];
+            float* dz = (jz.n_chunks == 1) ? out + static_cast<int64_t>(cz.job) * 2 * kMaxTaps : partials + static_cast<int64_t>(it.first + c) * 2 * kMaxTaps;
+            if (threadIdx.x < 2 * kMaxTaps) dz[threadIdx.x] = 0.0f;
+        }
         return;
     }
-    const CodeDesc cd = codes[job.code_id];
-    const int L = cd.len;
-    if (L <= 0 || cd.ptr == nullptr) {
-        if (threadIdx.x < 2 * kMaxTaps) dst[threadIdx.x] = 0.0f;
-        return;
-    }
-    // padded replica in LDS: lds[kCodeMargin + i] = code[i mod L] for i in [−kCodeMargin, L + kCodeMargin)
+    // Latency order: the code replica's loads first (its pointer is in the chunk descriptor, not
+    // behind the job), then this lane's first sample group, then the LDS stores of the replica —
+    // the in-order vmcnt wait for the code leaves the sample loads in flight across the barrier.
+    // Padded replica: lds[kCodeMargin + i] = code[i mod L] for i in [−kCodeMargin, L + kCodeMargin).
+    constexpr int kFillRegs = 9;  // ≤ 2304 padded chips from registers (GPS 1087, B1I 2110)
     const int total = L + 2 * kCodeMargin;
-    for (int i = threadIdx.x; i < total; i += kCorrThreads) {
+    float cr[kFillRegs];
+#pragma unroll
+    for (int k = 0; k < kFillRegs; k++) {
+        const int i = threadIdx.x + k * kCorrThreads;
         int src = i - kCodeMargin;
         src = src < 0 ? src + L * ((-src + L - 1) / L) : src;
         src = src % L;
-        lds_code[i] = cd.ptr[src];
+        cr[k] = (i < total) ? c0.code[src] : 0.0f;
+    }
+    f2 xa[kGroup], xb[kGroup];
+    f2 e;
+    {
+        const DevJob& j0 = jobs[c0.job];
+        if (c0.len > 0) load_group<FMT>(samples, j0.sample_offset + c0.start, c0.len, 0, xa);
+        e = anchor_to_lane_rotation(j0);  // ALU work while the loads are in flight
+    }
+#pragma unroll
+    for (int k = 0; k < kFillRegs; k++) {
+        const int i = threadIdx.x + k * kCorrThreads;
+        if (i < total) lds_code[i] = cr[k];
+    }
+    for (int i = threadIdx.x + kFillRegs * kCorrThreads; i < total; i += kCorrThreads) {  // long replicas (E1: 8248)
+        lds_code[i] = c0.code[(i - kCodeMargin) % L];
     }
     __syncthreads();
+    GNSSHIP_PROF_STAMP(1);
     const float* code = lds_code + kCodeMargin;
-    corr_chunk<FMT, NT, IN_MARGIN>(samples, job, ch, anchors, code, L, dst);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    int prev_job = c0.job;
+
+    for (int c = 0; c < it.count; c++) {
+        const ChunkDesc ch = chunks[it.first + c];
+        const DevJob job = jobs[ch.job];
+        if (c > 0 && ch.job != prev_job) e = anchor_to_lane_rotation(job);  // same job: same E_j
+        prev_job = ch.job;
+        // only what the next chunk's first sample group needs is carried across the chunk
+        const bool has_next = c + 1 < it.count;
+        int nstart = 0, nlen = 0;
+        int64_t noff = 0;
+        if (has_next) {
+            const ChunkDesc chn = chunks[it.first + c + 1];
+            nstart = chn.start;
+            nlen = chn.len;
+            noff = jobs[chn.job].sample_offset;
+        }
+        const f2 esw = f2{-e.y, e.x};
+        float shifts[NT];
+#pragma unroll
+        for (int t = 0; t < NT; t++) shifts[t] = (t < job.n_taps) ? job.shifts[t] : 0.0f;
+        // the chunk's 16 anchors as one contiguous uniform block (scalar loads, one wait before the
+        // loop: in the loop only in-order LDS reads use lgkmcnt).  Blocks past the chunk end (the
+        // job's tail, padded buffer end) are finite values multiplied by zero samples.
+        const Anchor* anc = anchors + job.anchor_offset + (ch.start >> 8);
+        Anchor qk[kBlocksPerChunk];
+#pragma unroll
+        for (int m = 0; m < kBlocksPerChunk; m++) qk[m] = anc[m];
+        const int64_t base = job.sample_offset + ch.start;
+        const int ng = (ch.len + kGroupSpan - 1) / kGroupSpan;  // groups in this chunk (0..kGroups)
+        GNSSHIP_PROF_STAMP(2);
+        f2 acc[NT];
+#pragma unroll
+        for (int t = 0; t < NT; t++) acc[t] = f2{0.0f, 0.0f};
+        // ping-pong over groups: group g in xa (g even) / xb (g odd); the load issued with group g
+        // is group g+1 of this chunk, or — after the last group — group 0 of the next chunk.
+#pragma unroll
+        for (int g = 0; g < kGroups; g++) {
+            if (g < ng) {  // chunk-uniform
+                f2(&cur)[kGroup] = (g & 1) ? xb : xa;
+                f2(&nxt)[kGroup] = (g & 1) ? xa : xb;
+                if (g + 1 < ng)
+                    load_group<FMT>(samples, base, ch.len, g + 1, nxt);
+                else if (has_next && nlen > 0)
+                    load_group<FMT>(samples, noff + nstart, nlen, 0, nxt);
+                if ((g + 1) * kGroupSpan <= ch.len)
+                    correlate_group<NT, IN_MARGIN, true>(job, ch, qk, e, esw, shifts, code, L, g, cur, acc);
+                else
+                    correlate_group<NT, IN_MARGIN, false>(job, ch, qk, e, esw, shifts, code, L, g, cur, acc);
+            }
+        }
+        // next chunk's group 0 sits in buffer ng & 1 → move it to xa (an empty chunk issued none)
+        if (ng == 0 && has_next && nlen > 0) load_group<FMT>(samples, noff + nstart, nlen, 0, xa);
+        if (ng & 1) {
+#pragma unroll
+            for (int u = 0; u < kGroup; u++) xa[u] = xb[u];
+        }
+        GNSSHIP_PROF_STAMP(3);
+#pragma unroll
+        for (int t = 0; t < NT; t++) {
+            const float wr = wave_sum(acc[t].x), wi = wave_sum(acc[t].y);
+            if (lane == 0) {
+                red[c][wave][2 * t] = wr;
+                red[c][wave][2 * t + 1] = wi;
+            }
+        }
+    }
+    __syncthreads();
+    // per-chunk outputs: thread (c, v) sums the 4 wave partials of value v of chunk c, in wave order
+    for (int k = threadIdx.x; k < it.count * 2 * kMaxTaps; k += kCorrThreads) {
+        const int c = k / (2 * kMaxTaps), v = k % (2 * kMaxTaps);
+        const ChunkDesc cc = chunks[it.first + c];
+        const DevJob& jc = jobs[cc.job];
+        float* dst = (jc.n_chunks == 1) ? out + static_cast<int64_t>(cc.job) * 2 * kMaxTaps : partials + static_cast<int64_t>(it.first + c) * 2 * kMaxTaps;
+        float s = 0.0f;
+        if (v < 2 * NT && v < 2 * jc.n_taps && cc.len > 0) {
+#pragma unroll
+            for (int w = 0; w < kCorrThreads / 64; w++) s += red[c][w][v];
+        }
+        dst[v] = s;
+    }
+    GNSSHIP_PROF_STAMP(4);
 }
 
-// Sum the chunk partials of multi-chunk jobs, in chunk order.
 __global__ void corr_reduce_kernel(const DevJob* __restrict__ jobs, int n_jobs, const float* __restrict__ partials, float* __restrict__ out)
 {
     const int gid = blockIdx.x * blockDim.x + threadIdx.x;
@@ -333,10 +437,20 @@ __global__ void corr_reduce_kernel(const DevJob* __restrict__ jobs, int n_jobs, 
     out[static_cast<int64_t>(j) * 2 * kMaxTaps + v] = s;
 }
 
-hipError_t launch_corr_batch(const void* samples, int fmt, const DevJob* jobs, int n_jobs, const ChunkDesc* chunks, int n_chunks,
-    const ChunkClass* classes, const CodeDesc* codes, int max_code_len, bool any_multi_chunk, Anchor* anchors, float* partials, float* out,
+#ifdef GNSSHIP_CORR_PROFILE
+}  // namespace gnsship
+extern "C" int gnsship_debug_corr_profile(void* dev_buf)
+{
+    return hipMemcpyToSymbol(HIP_SYMBOL(gnsship::g_corr_prof), &dev_buf, sizeof(void*)) == hipSuccess ? 0 : -3;
+}
+namespace gnsship {
+#endif
+
+hipError_t launch_corr_batch(const void* samples, int fmt, const DevJob* jobs, int n_jobs, const ChunkDesc* chunks, const WorkItem* items,
+    int n_items, const ChunkClass* classes, int max_code_len, bool any_multi_chunk, Anchor* anchors, float* partials, float* out,
     hipStream_t stream, int stages, const AnchorPrefetch* prefetch)
 {
+    const int n_chunks = n_items;  // work items to launch (0: nothing to correlate)
     AnchorPrefetch pf{nullptr, 0, nullptr, 0};
     if (prefetch && prefetch->n_jobs > 0 && (stages & GNSSHIP_STAGE_CORRELATE)) {
         pf = *prefetch;
@@ -361,11 +475,10 @@ hipError_t launch_corr_batch(const void* samples, int fmt, const DevJob* jobs, i
     for (int c = 0; c < kChunkClasses; c++) {
         const int cnt = classes[c].count;
         if (cnt <= 0) continue;
-        const ChunkDesc* cc = chunks + classes[c].start;
-        const int cb = classes[c].start;
+        const WorkItem* ic = items + classes[c].start;
         dim3 grid(cnt + pf.n_blocks), block(kCorrThreads);
 #define GNSSHIP_LAUNCH_CORR(F, NTV, MV) \
-    hipLaunchKernelGGL((corr_batch_kernel<F, NTV, MV>), grid, block, lds, stream, samples, jobs, cc, cnt, cb, codes, anchors, partials, out, pf)
+    hipLaunchKernelGGL((corr_batch_kernel<F, NTV, MV>), grid, block, lds, stream, samples, jobs, chunks, ic, cnt, anchors, partials, out, pf)
 #define GNSSHIP_LAUNCH_NT(F)                                                     \
     switch (c) {                                                                 \
     case 0: GNSSHIP_LAUNCH_CORR(F, 1, false); break;                             \

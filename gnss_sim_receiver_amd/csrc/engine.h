@@ -52,22 +52,37 @@ struct DevJob {
 // no modulo.  Jobs that can leave the margin (checked on the host) take the general wrap path.
 constexpr int kCodeMargin = 32;
 
-// Rotator anchor of one 256-sample block k of a job: `a` = the phasor the reference multiplies
-// sample 256k by (before renormalising), `q` = a/|a| (the renormalised phasor it then rotates).
+// Rotator anchor of one 256-sample block k of a job: the renormalised phasor q = a/|a| the
+// reference rotates from sample 256k on (a = the phasor it multiplies sample 256k by; the
+// correlation uses q·E_j for every lane, including j = 0 — see corr_kernel.hip).
 struct Anchor {
-    float a_re, a_im, q_re, q_im;
+    float q_re, q_im;
 };
+// Anchor buffers carry kAnchorPad zero entries past the last job: a chunk reads its 16 anchors as
+// one contiguous scalar block even when its job ends early.
+constexpr int kBlocksPerChunk = kCorrChunk / 256;  // renormalisation blocks per chunk (16)
+constexpr int kAnchorPad = kBlocksPerChunk;
 
 struct ChunkDesc {
     int32_t job;
-    int32_t start;  // first sample (relative to the job)
+    int32_t start;     // first sample (relative to the job)
     int32_t len;
-    int32_t pad;
+    int32_t code_len;  // the job's code replica, carried here so that a workgroup fetches it
+    const float* code; // without waiting for the job descriptor (attach_codes)
+};
+
+// A workgroup's work: chunks [first, first + count) of the (reordered) chunk array, all sharing
+// one code replica (corr_batch_kernel stages it in LDS once per item).
+constexpr int kMaxChunksPerItem = 8;
+constexpr int kChunksPerItemDefault = 2;
+struct WorkItem {
+    int32_t first;
+    int32_t count;
 };
 
 // Launch the batched correlator: partials[chunk][2*kMaxTaps] then per-job reduction into out.
 // Chunks are grouped by class = 2·tap_class + in_margin, tap_class: 0 → 1 tap, 1 → ≤3, 2 → ≤5, 3 → ≤8;
-// each class is one kernel launch over chunks[start, start + count).
+// each class is one kernel launch over work items [start, start + count).
 constexpr int kChunkClasses = 8;
 struct ChunkClass {
     int32_t start;
@@ -87,11 +102,20 @@ struct AnchorPrefetch {
     int32_t n_blocks;  // set by launch_corr_batch
 };
 
+// Fill ChunkDesc::code / code_len from a code table indexed by the chunks' jobs' code ids.
+void attach_codes(std::vector<ChunkDesc>& chunks, const std::vector<struct DevJob>& jobs, const std::vector<CodeDesc>& table);
+
 // anchors: scratch of Σ ceil(n_j/256) Anchor entries, recomputed by every launch.  prefetch
 // (optional, with the CORRELATE stage): replay `prefetch->jobs`' anchors in the same launch.
-hipError_t launch_corr_batch(const void* samples, int fmt, const DevJob* jobs, int n_jobs, const ChunkDesc* chunks, int n_chunks,
-    const ChunkClass* classes, const CodeDesc* codes, int max_code_len, bool any_multi_chunk, Anchor* anchors, float* partials, float* out,
+hipError_t launch_corr_batch(const void* samples, int fmt, const DevJob* jobs, int n_jobs, const ChunkDesc* chunks, const WorkItem* items,
+    int n_items, const ChunkClass* classes, int max_code_len, bool any_multi_chunk, Anchor* anchors, float* partials, float* out,
     hipStream_t stream, int stages = GNSSHIP_STAGE_ANCHORS | GNSSHIP_STAGE_CORRELATE, const AnchorPrefetch* prefetch = nullptr);
+
+// Plan chunks (≤ kCorrChunk samples), rotator anchors and work items for a job list: chunks of one
+// job stay contiguous and in order; single-chunk jobs with equal code id (pair_by_code) share items
+// of up to chunks_per_item chunks in job order.  Returns the chunk count.
+int plan_chunks(std::vector<DevJob>& jobs, std::vector<ChunkDesc>& chunks, std::vector<WorkItem>& items, bool& any_multi, int64_t* n_anchors,
+    ChunkClass* classes, int chunks_per_item, bool pair_by_code);
 
 }  // namespace gnsship
 
@@ -105,4 +129,5 @@ struct gnsship_ctx {
     gnsship::CodeDesc* codes_dev = nullptr;
     int codes_dev_cap = 0;
     bool codes_dirty = false;
+    uint64_t codes_version = 0;  // bumped by every gnsship_code_set (holders of code pointers re-attach)
 };

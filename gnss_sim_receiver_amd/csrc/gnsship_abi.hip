@@ -4,7 +4,9 @@
 // failures to an int status and keeps the message in ctx->last_error.
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <map>
 #include <new>
 
 #include "engine.h"
@@ -97,12 +99,15 @@ bool derive_job(const gnsship_corr_job& in, int code_len, DevJob& out)
     return true;
 }
 
-// Split jobs into ≤kCorrChunk-sample chunks and lay out their rotator anchors; returns the
-// number of chunks, total anchors in *n_anchors.
-int plan_chunks(std::vector<DevJob>& jobs, std::vector<ChunkDesc>& chunks, bool& any_multi, int64_t* n_anchors, ChunkClass* classes)
+// Split jobs into ≤kCorrChunk-sample chunks, lay out their rotator anchors and group the chunks of
+// each class into work items (see engine.h).  Returns the number of chunks.
+int plan_chunks(std::vector<DevJob>& jobs, std::vector<ChunkDesc>& chunks, std::vector<WorkItem>& items, bool& any_multi, int64_t* n_anchors,
+    ChunkClass* classes, int chunks_per_item, bool pair_by_code)
 {
     chunks.clear();
+    items.clear();
     any_multi = false;
+    chunks_per_item = chunks_per_item < 1 ? 1 : (chunks_per_item > kMaxChunksPerItem ? kMaxChunksPerItem : chunks_per_item);
     int64_t anchors = 0;
     for (size_t j = 0; j < jobs.size(); j++) {
         const int n = jobs[j].n_samples;
@@ -111,27 +116,69 @@ int plan_chunks(std::vector<DevJob>& jobs, std::vector<ChunkDesc>& chunks, bool&
         jobs[j].n_chunks = n <= 0 ? 1 : (n + kCorrChunk - 1) / kCorrChunk;
         if (jobs[j].n_chunks > 1) any_multi = true;
     }
+    auto job_chunk = [&](int j, int k) {
+        ChunkDesc d;
+        d.job = j;
+        d.start = k * kCorrChunk;
+        const int rem = jobs[j].n_samples - d.start;
+        d.len = rem < kCorrChunk ? (rem > 0 ? rem : 0) : kCorrChunk;
+        d.code_len = 0;
+        d.code = nullptr;
+        return d;
+    };
     // chunks grouped by class (one launch each), job order kept inside a class
     for (int c = 0; c < kChunkClasses; c++) {
-        classes[c].start = static_cast<int32_t>(chunks.size());
+        classes[c].start = static_cast<int32_t>(items.size());
+        std::map<int, std::vector<int>> open;  // code id → pending single-chunk jobs
+        auto emit_jobs = [&](std::vector<int>& js) {
+            WorkItem it{static_cast<int32_t>(chunks.size()), static_cast<int32_t>(js.size())};
+            for (int j : js) {
+                jobs[j].first_chunk = static_cast<int32_t>(chunks.size());
+                chunks.push_back(job_chunk(j, 0));
+            }
+            items.push_back(it);
+            js.clear();
+        };
         for (size_t j = 0; j < jobs.size(); j++) {
             if (chunk_class(jobs[j].n_taps, jobs[j].in_margin) != c) continue;
-            const int n = jobs[j].n_samples;
+            const int nch = jobs[j].n_chunks;
+            if (nch == 1 && pair_by_code && chunks_per_item > 1) {
+                std::vector<int>& pend = open[jobs[j].code_id];
+                pend.push_back(static_cast<int>(j));
+                if (static_cast<int>(pend.size()) == chunks_per_item) emit_jobs(pend);
+                continue;
+            }
+            // a long job: its chunks contiguous and in order, cut into items
             jobs[j].first_chunk = static_cast<int32_t>(chunks.size());
-            for (int k = 0; k < jobs[j].n_chunks; k++) {
-                ChunkDesc d;
-                d.job = static_cast<int32_t>(j);
-                d.start = k * kCorrChunk;
-                const int rem = n - d.start;
-                d.len = rem < kCorrChunk ? (rem > 0 ? rem : 0) : kCorrChunk;
-                d.pad = 0;
-                chunks.push_back(d);
+            for (int k = 0; k < nch; k += chunks_per_item) {
+                const int cnt = std::min(chunks_per_item, nch - k);
+                items.push_back(WorkItem{static_cast<int32_t>(chunks.size()), cnt});
+                for (int m = 0; m < cnt; m++) chunks.push_back(job_chunk(static_cast<int>(j), k + m));
             }
         }
-        classes[c].count = static_cast<int32_t>(chunks.size()) - classes[c].start;
+        for (auto& kv : open)
+            if (!kv.second.empty()) emit_jobs(kv.second);
+        classes[c].count = static_cast<int32_t>(items.size()) - classes[c].start;
     }
     *n_anchors = anchors > 0 ? anchors : 1;
     return static_cast<int>(chunks.size());
+}
+
+int chunks_per_item_setting()
+{
+    const char* e = std::getenv("GNSSHIP_CHUNKS_PER_ITEM");  // tuning knob
+    const int v = e ? std::atoi(e) : kChunksPerItemDefault;
+    return v < 1 ? 1 : (v > kMaxChunksPerItem ? kMaxChunksPerItem : v);
+}
+
+void attach_codes(std::vector<ChunkDesc>& chunks, const std::vector<DevJob>& jobs, const std::vector<CodeDesc>& table)
+{
+    for (auto& c : chunks) {
+        const int id = jobs[c.job].code_id;
+        const bool ok = id >= 0 && id < static_cast<int>(table.size());
+        c.code = ok ? table[id].ptr : nullptr;
+        c.code_len = ok ? table[id].len : 0;
+    }
 }
 
 size_t fmt_bytes(int fmt)
@@ -286,6 +333,7 @@ extern "C" int gnsship_code_set(gnsship_ctx* ctx, int code_id, const float* code
     d.len = len;
     HIP_TRY(ctx, hipMemcpy(const_cast<float*>(d.ptr), code, sizeof(float) * len, hipMemcpyHostToDevice));
     ctx->codes_dirty = true;
+    ctx->codes_version++;
     return GNSSHIP_OK;
 }
 
@@ -306,14 +354,18 @@ struct gnsship_batch {
     bool any_multi = false;
     ChunkClass classes[kChunkClasses] = {};
     int chunk_cap = 0;
+    int n_items = 0;
+    int item_cap = 0;
     DevJob* jobs_dev = nullptr;
     ChunkDesc* chunks_dev = nullptr;
+    WorkItem* items_dev = nullptr;
     float* partials_dev = nullptr;
     float* out_dev = nullptr;
     Anchor* anchors_dev = nullptr;
     int64_t anchor_cap = 0;
     std::vector<DevJob> jobs_host;
     std::vector<ChunkDesc> chunks_host;
+    std::vector<WorkItem> items_host;
     // The anchor replay (NCO arguments only, latency-bound, few waves) runs on the batch's own
     // stream; the correlation on the context stream waits for it.  With two batches in flight the
     // replay of one overlaps the correlation of the other.
@@ -327,7 +379,7 @@ struct gnsship_batch {
 
 static void batch_release(gnsship_batch* b)
 {
-    void* ptrs[] = {b->jobs_dev, b->chunks_dev, b->partials_dev, b->out_dev, b->anchors_dev};
+    void* ptrs[] = {b->jobs_dev, b->chunks_dev, b->items_dev, b->partials_dev, b->out_dev, b->anchors_dev};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     if (b->anchors_ready) (void)hipEventDestroy(b->anchors_ready);
@@ -380,11 +432,21 @@ extern "C" int gnsship_batch_set_jobs(gnsship_batch* b, const gnsship_corr_job* 
     }
     b->max_code_len = max_len;
     int64_t n_anchors = 0;
-    b->n_chunks = plan_chunks(b->jobs_host, b->chunks_host, b->any_multi, &n_anchors, b->classes);
+    b->n_chunks = plan_chunks(b->jobs_host, b->chunks_host, b->items_host, b->any_multi, &n_anchors, b->classes, chunks_per_item_setting(), true);
+    b->n_items = static_cast<int>(b->items_host.size());
+    attach_codes(b->chunks_host, b->jobs_host, ctx->codes_host);
+    if (b->n_items > b->item_cap) {
+        if (b->items_dev) HIP_TRY(ctx, hipFree(b->items_dev));
+        b->items_dev = nullptr;
+        HIP_TRY(ctx, hipMalloc(&b->items_dev, sizeof(WorkItem) * b->n_items));
+        b->item_cap = b->n_items;
+    }
+    if (b->n_items) HIP_TRY(ctx, hipMemcpy(b->items_dev, b->items_host.data(), sizeof(WorkItem) * b->n_items, hipMemcpyHostToDevice));
     if (n_anchors > b->anchor_cap) {
         if (b->anchors_dev) HIP_TRY(ctx, hipFree(b->anchors_dev));
         b->anchors_dev = nullptr;
-        HIP_TRY(ctx, hipMalloc(&b->anchors_dev, sizeof(Anchor) * n_anchors));
+        HIP_TRY(ctx, hipMalloc(&b->anchors_dev, sizeof(Anchor) * (n_anchors + kAnchorPad)));
+        HIP_TRY(ctx, hipMemset(b->anchors_dev, 0, sizeof(Anchor) * (n_anchors + kAnchorPad)));
         b->anchor_cap = n_anchors;
     }
     if (b->n_chunks > b->chunk_cap) {
@@ -421,14 +483,14 @@ extern "C" int gnsship_batch_launch_stages(gnsship_batch* b, const void* dev_sam
     if (stages & GNSSHIP_STAGE_ANCHORS) {
         // WAR: the previous correlation of this batch must have consumed the anchors
         HIP_TRY(ctx, hipStreamWaitEvent(b->aux, b->corr_done, 0));
-        hipError_t e = launch_corr_batch(dev_samples, fmt, b->jobs_dev, b->n_jobs, b->chunks_dev, b->n_chunks, b->classes, ctx->codes_dev,
+        hipError_t e = launch_corr_batch(dev_samples, fmt, b->jobs_dev, b->n_jobs, b->chunks_dev, b->items_dev, b->n_items, b->classes,
             b->max_code_len, b->any_multi, b->anchors_dev, b->partials_dev, b->out_dev, b->aux, GNSSHIP_STAGE_ANCHORS);
         if (e != hipSuccess) return hip_fail(ctx, e, "launch_corr_batch(anchors)");
         HIP_TRY(ctx, hipEventRecord(b->anchors_ready, b->aux));
         HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, b->anchors_ready, 0));  // RAW: correlation (or caller) after replay
     }
     if (stages & GNSSHIP_STAGE_CORRELATE) {
-        hipError_t e = launch_corr_batch(dev_samples, fmt, b->jobs_dev, b->n_jobs, b->chunks_dev, b->n_chunks, b->classes, ctx->codes_dev,
+        hipError_t e = launch_corr_batch(dev_samples, fmt, b->jobs_dev, b->n_jobs, b->chunks_dev, b->items_dev, b->n_items, b->classes,
             b->max_code_len, b->any_multi, b->anchors_dev, b->partials_dev, b->out_dev, ctx->stream, GNSSHIP_STAGE_CORRELATE);
         if (e != hipSuccess) return hip_fail(ctx, e, "launch_corr_batch(correlate)");
         HIP_TRY(ctx, hipEventRecord(b->corr_done, ctx->stream));
@@ -455,13 +517,13 @@ extern "C" int gnsship_batch_launch_pipelined(gnsship_batch* b, const void* dev_
     const bool prefetch = next && next->n_jobs > 0;
     if (prefetch) pf = AnchorPrefetch{next->jobs_dev, next->n_jobs, next->anchors_dev, 0};
     if (b->n_jobs > 0 && !b->anchors_valid) {
-        hipError_t e = launch_corr_batch(dev_samples, fmt, b->jobs_dev, b->n_jobs, b->chunks_dev, b->n_chunks, b->classes, ctx->codes_dev,
+        hipError_t e = launch_corr_batch(dev_samples, fmt, b->jobs_dev, b->n_jobs, b->chunks_dev, b->items_dev, b->n_items, b->classes,
             b->max_code_len, b->any_multi, b->anchors_dev, b->partials_dev, b->out_dev, ctx->stream, GNSSHIP_STAGE_ANCHORS);
         if (e != hipSuccess) return hip_fail(ctx, e, "launch_corr_batch(anchors)");
     }
     if (b->n_jobs > 0 || prefetch) {
-        hipError_t e = launch_corr_batch(dev_samples, fmt, b->jobs_dev, b->n_jobs, b->chunks_dev, b->n_jobs > 0 ? b->n_chunks : 0, b->classes,
-            ctx->codes_dev, b->max_code_len, b->any_multi, b->anchors_dev, b->partials_dev, b->out_dev, ctx->stream, GNSSHIP_STAGE_CORRELATE,
+        hipError_t e = launch_corr_batch(dev_samples, fmt, b->jobs_dev, b->n_jobs, b->chunks_dev, b->items_dev, b->n_jobs > 0 ? b->n_items : 0,
+            b->classes, b->max_code_len, b->any_multi, b->anchors_dev, b->partials_dev, b->out_dev, ctx->stream, GNSSHIP_STAGE_CORRELATE,
             prefetch ? &pf : nullptr);
         if (e != hipSuccess) return hip_fail(ctx, e, "launch_corr_batch(pipelined)");
     }
@@ -513,6 +575,7 @@ struct gnsship_corr {
     void* sig_dev = nullptr;  // staging for host input (max_samples CF32)
     DevJob* job_dev = nullptr;
     ChunkDesc* chunks_dev = nullptr;
+    WorkItem* items_dev = nullptr;
     float* partials_dev = nullptr;
     float* out_dev = nullptr;
     Anchor* anchors_dev = nullptr;
@@ -535,9 +598,12 @@ extern "C" int gnsship_corr_create(gnsship_ctx* ctx, int max_signal_length_sampl
     if (e == hipSuccess) e = hipMalloc(&c->sig_dev, 8 * static_cast<size_t>(max_signal_length_samples));
     if (e == hipSuccess) e = hipMalloc(&c->job_dev, sizeof(DevJob));
     if (e == hipSuccess) e = hipMalloc(&c->chunks_dev, sizeof(ChunkDesc) * c->chunk_cap);
+    if (e == hipSuccess) e = hipMalloc(&c->items_dev, sizeof(WorkItem) * c->chunk_cap);
     if (e == hipSuccess) e = hipMalloc(&c->partials_dev, sizeof(float) * 2 * kMaxTaps * c->chunk_cap);
     if (e == hipSuccess) e = hipMalloc(&c->out_dev, sizeof(float) * 2 * kMaxTaps);
-    if (e == hipSuccess) e = hipMalloc(&c->anchors_dev, sizeof(Anchor) * ((max_signal_length_samples + kRenorm - 1) / kRenorm + 1));
+    const size_t n_anc = (max_signal_length_samples + kRenorm - 1) / kRenorm + 1 + kAnchorPad;
+    if (e == hipSuccess) e = hipMalloc(&c->anchors_dev, sizeof(Anchor) * n_anc);
+    if (e == hipSuccess) e = hipMemset(c->anchors_dev, 0, sizeof(Anchor) * n_anc);
     if (e != hipSuccess) {
         gnsship_corr_destroy(c);
         return hip_fail(ctx, e, "gnsship_corr_create");
@@ -602,10 +668,12 @@ extern "C" int gnsship_corr_run(gnsship_corr* c, const void* sig, int fmt, int s
     std::vector<DevJob> jobs(1);
     if (!derive_job(in, c->code_len, jobs[0])) return fail(ctx, GNSSHIP_E_INVAL, "gnsship_corr_run: invalid job");
     std::vector<ChunkDesc> chunks;
+    std::vector<WorkItem> items;
     bool multi = false;
     int64_t n_anchors = 0;
     ChunkClass classes[kChunkClasses];
-    const int nch = plan_chunks(jobs, chunks, multi, &n_anchors, classes);
+    const int nch = plan_chunks(jobs, chunks, items, multi, &n_anchors, classes, chunks_per_item_setting(), false);
+    attach_codes(chunks, jobs, std::vector<CodeDesc>{CodeDesc{c->code_dev, c->code_len, 0}});
     const void* src = sig;
     if (!sig_on_device) {
         HIP_TRY(ctx, hipMemcpyAsync(c->sig_dev, sig, fmt_bytes(fmt) * static_cast<size_t>(n), hipMemcpyHostToDevice, ctx->stream));
@@ -613,8 +681,9 @@ extern "C" int gnsship_corr_run(gnsship_corr* c, const void* sig, int fmt, int s
     }
     HIP_TRY(ctx, hipMemcpyAsync(c->job_dev, jobs.data(), sizeof(DevJob), hipMemcpyHostToDevice, ctx->stream));
     HIP_TRY(ctx, hipMemcpyAsync(c->chunks_dev, chunks.data(), sizeof(ChunkDesc) * nch, hipMemcpyHostToDevice, ctx->stream));
-    hipError_t e = launch_corr_batch(src, fmt, c->job_dev, 1, c->chunks_dev, nch, classes, c->code_table_dev, c->code_len, multi, c->anchors_dev,
-        c->partials_dev, c->out_dev, ctx->stream);
+    HIP_TRY(ctx, hipMemcpyAsync(c->items_dev, items.data(), sizeof(WorkItem) * items.size(), hipMemcpyHostToDevice, ctx->stream));
+    hipError_t e = launch_corr_batch(src, fmt, c->job_dev, 1, c->chunks_dev, c->items_dev, static_cast<int>(items.size()), classes, c->code_len, multi,
+        c->anchors_dev, c->partials_dev, c->out_dev, ctx->stream);
     if (e != hipSuccess) return hip_fail(ctx, e, "launch_corr_batch");
     float tmp[2 * kMaxTaps];
     HIP_TRY(ctx, hipMemcpyAsync(tmp, c->out_dev, sizeof(tmp), hipMemcpyDeviceToHost, ctx->stream));
@@ -628,7 +697,7 @@ extern "C" int gnsship_corr_destroy(gnsship_corr* c)
     if (!c) return GNSSHIP_E_INVAL;
     (void)hipSetDevice(c->ctx->device);
     (void)hipStreamSynchronize(c->ctx->stream);
-    void* ptrs[] = {c->code_dev, c->code_table_dev, c->sig_dev, c->job_dev, c->chunks_dev, c->partials_dev, c->out_dev, c->anchors_dev};
+    void* ptrs[] = {c->code_dev, c->code_table_dev, c->sig_dev, c->job_dev, c->chunks_dev, c->items_dev, c->partials_dev, c->out_dev, c->anchors_dev};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     delete c;

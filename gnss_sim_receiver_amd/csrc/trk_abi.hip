@@ -20,7 +20,7 @@ int hip_fail(gnsship_ctx* ctx, hipError_t e, const char* where);
 int set_device(gnsship_ctx* ctx);
 int sync_code_table(gnsship_ctx* ctx);
 size_t fmt_bytes(int fmt);
-int plan_chunks(std::vector<DevJob>& jobs, std::vector<ChunkDesc>& chunks, bool& any_multi, int64_t* n_anchors, ChunkClass* classes);
+int chunks_per_item_setting();
 }  // namespace gnsship
 
 using namespace gnsship;
@@ -40,10 +40,16 @@ struct gnsship_trk {
     bool any_multi = false;
     ChunkClass classes[kChunkClasses]{};
     std::vector<TrkChannel> host_chans;
+    std::vector<ChunkDesc> chunks_host;   // plan (lengths are rewritten on the device each round)
+    std::vector<int32_t> jobs_first_chunk;
+    std::vector<int32_t> job_code;        // code-bank id per job (−1: channel never started)
+    uint64_t attached_version = 0;        // ctx->codes_version the chunk code pointers reflect
     TrkParams* params_dev = nullptr;
     TrkChannel* chans_dev = nullptr;
     DevJob* jobs_dev = nullptr;
     ChunkDesc* chunks_dev = nullptr;
+    WorkItem* items_dev = nullptr;
+    int n_items = 0;
     Anchor* anchors_dev = nullptr;
     float* partials_dev = nullptr;
     float* out_dev = nullptr;
@@ -217,8 +223,8 @@ bool build_params(const gnsship_trk_conf& c, TrkParams& p)
 
 void release(gnsship_trk* t)
 {
-    void* ptrs[] = {t->params_dev, t->chans_dev, t->jobs_dev, t->chunks_dev, t->anchors_dev, t->partials_dev, t->out_dev, t->rec_dev, t->ran_dev,
-        t->stage_dev};
+    void* ptrs[] = {t->params_dev, t->chans_dev, t->jobs_dev, t->chunks_dev, t->items_dev, t->anchors_dev, t->partials_dev, t->out_dev, t->rec_dev,
+        t->ran_dev, t->stage_dev};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
 }
@@ -264,10 +270,18 @@ extern "C" int gnsship_trk_create(gnsship_ctx* ctx, const gnsship_trk_conf* conf
         jobs[i].in_margin = 0;
     }
     std::vector<ChunkDesc> chunks;
+    std::vector<WorkItem> items;
     int64_t n_anchors = 0;
-    t->n_chunks = plan_chunks(jobs, chunks, t->any_multi, &n_anchors, t->classes);
+    // codes are bound when channels start: items only group the chunks of one job
+    t->n_chunks = plan_chunks(jobs, chunks, items, t->any_multi, &n_anchors, t->classes, chunks_per_item_setting(), false);
+    t->n_items = static_cast<int>(items.size());
     for (auto& j : jobs) j.n_samples = 0;  // idle until a channel starts
-    for (auto& c : chunks) c.len = 0;
+    for (auto& c : chunks) c.len = 0;      // (code pointers are attached when a channel starts)
+    t->chunks_host = chunks;
+    t->jobs_first_chunk.resize(t->n_jobs);
+    for (int i = 0; i < t->n_jobs; i++) t->jobs_first_chunk[i] = jobs[i].first_chunk;
+    t->job_code.assign(t->n_jobs, -1);
+    t->attached_version = ctx->codes_version;
     t->host_chans.assign(max_channels, TrkChannel{});
     for (auto& c : t->host_chans) std::memset(&c, 0, sizeof(TrkChannel));
     hipError_t e = hipMalloc(&t->params_dev, sizeof(TrkParams));
@@ -278,7 +292,10 @@ extern "C" int gnsship_trk_create(gnsship_ctx* ctx, const gnsship_trk_conf* conf
     if (e == hipSuccess) e = hipMemcpy(t->jobs_dev, jobs.data(), sizeof(DevJob) * t->n_jobs, hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMalloc(&t->chunks_dev, sizeof(ChunkDesc) * t->n_chunks);
     if (e == hipSuccess) e = hipMemcpy(t->chunks_dev, chunks.data(), sizeof(ChunkDesc) * t->n_chunks, hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = hipMalloc(&t->anchors_dev, sizeof(Anchor) * static_cast<size_t>(n_anchors));
+    if (e == hipSuccess) e = hipMalloc(&t->items_dev, sizeof(WorkItem) * t->n_items);
+    if (e == hipSuccess) e = hipMemcpy(t->items_dev, items.data(), sizeof(WorkItem) * t->n_items, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMalloc(&t->anchors_dev, sizeof(Anchor) * static_cast<size_t>(n_anchors + kAnchorPad));
+    if (e == hipSuccess) e = hipMemset(t->anchors_dev, 0, sizeof(Anchor) * static_cast<size_t>(n_anchors + kAnchorPad));
     if (e == hipSuccess) e = hipMalloc(&t->partials_dev, sizeof(float) * 2 * kMaxTaps * static_cast<size_t>(t->n_chunks));
     if (e == hipSuccess) e = hipMalloc(&t->out_dev, sizeof(float) * 2 * kMaxTaps * static_cast<size_t>(t->n_jobs));
     if (e != hipSuccess) {
@@ -341,6 +358,21 @@ extern "C" int gnsship_trk_start(gnsship_trk* t, int channel, const gnsship_trk_
     c.state = 2;
     c.nitems_read = a->first_sample + static_cast<uint64_t>(samples_offset);
     if (int rc = set_device(ctx)) return rc;
+    // the channel's chunks carry its code replica(s): only the code fields are rewritten (the
+    // device owns the lengths)
+    for (int q = 0; q < p.jobs_per_channel; q++) {
+        const int job = channel * p.jobs_per_channel + q;
+        t->job_code[job] = q == 0 ? c.code_id : c.data_code_id;
+        const CodeDesc& cd = ctx->codes_host[t->job_code[job]];
+        for (int m = 0; m < p.chunks_per_job; m++) {
+            const int ci = t->jobs_first_chunk[job] + m;
+            ChunkDesc& d = t->chunks_host[ci];
+            d.code = cd.ptr;
+            d.code_len = cd.len;
+            HIP_TRY(ctx, hipMemcpyAsync(reinterpret_cast<char*>(t->chunks_dev + ci) + offsetof(ChunkDesc, code_len), &d.code_len,
+                             sizeof(ChunkDesc) - offsetof(ChunkDesc, code_len), hipMemcpyHostToDevice, ctx->stream));
+        }
+    }
     HIP_TRY(ctx, hipMemcpyAsync(t->chans_dev + channel, &c, sizeof(TrkChannel), hipMemcpyHostToDevice, ctx->stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     return GNSSHIP_OK;
@@ -386,6 +418,20 @@ extern "C" int gnsship_trk_run(gnsship_trk* t, const void* sig, int fmt, int sig
     int max_len = 1;
     for (const auto& cd : ctx->codes_host)
         if (cd.ptr && cd.len > max_len) max_len = cd.len;
+    if (t->attached_version != ctx->codes_version) {  // code bank changed: refresh every chunk's code pointer
+        for (int job = 0; job < t->n_jobs; job++) {
+            const int id = t->job_code[job];
+            const bool ok = id >= 0 && id < static_cast<int>(ctx->codes_host.size());
+            for (int m = 0; m < t->params.chunks_per_job; m++) {
+                ChunkDesc& d = t->chunks_host[t->jobs_first_chunk[job] + m];
+                d.code = ok ? ctx->codes_host[id].ptr : nullptr;
+                d.code_len = ok ? ctx->codes_host[id].len : 0;
+                d.len = 0;  // rewritten by the first step kernel of this run before any correlation
+            }
+        }
+        HIP_TRY(ctx, hipMemcpyAsync(t->chunks_dev, t->chunks_host.data(), sizeof(ChunkDesc) * t->n_chunks, hipMemcpyHostToDevice, ctx->stream));
+        t->attached_version = ctx->codes_version;
+    }
     const void* src = sig;
     if (!sig_on_device) {
         const size_t bytes = fmt_bytes(fmt) * static_cast<size_t>(n_buffer_samples);
@@ -420,7 +466,7 @@ extern "C" int gnsship_trk_run(gnsship_trk* t, const void* sig, int fmt, int sig
             consume, emit, rec, t->ran_dev + r, ctx->stream);
         if (e != hipSuccess) return hip_fail(ctx, e, "launch_trk_step");
         if (!emit) break;
-        e = launch_corr_batch(src, fmt, t->jobs_dev, t->n_jobs, t->chunks_dev, t->n_chunks, t->classes, ctx->codes_dev, max_len, t->any_multi,
+        e = launch_corr_batch(src, fmt, t->jobs_dev, t->n_jobs, t->chunks_dev, t->items_dev, t->n_items, t->classes, max_len, t->any_multi,
             t->anchors_dev, t->partials_dev, t->out_dev, ctx->stream);
         if (e != hipSuccess) return hip_fail(ctx, e, "launch_corr_batch(tracking)");
     }
