@@ -101,24 +101,57 @@ __global__ void corr_anchor_kernel(const DevJob* __restrict__ jobs, int n_jobs, 
     replay_anchors(job, anchors);
 }
 
+typedef float f2v_t __attribute__((ext_vector_type(2)));
+
+// IF samples are read through raw buffer loads: a chunk's samples get their own buffer resource
+// (base = its first sample, num_records = its length in bytes), so lanes past the chunk end read
+// zeros from the hardware range check — no clamps, selects or exec masks on the tail — and the
+// per-load offsets are SGPR constants (soffset) over one per-lane VGPR offset.
+typedef int i4v __attribute__((ext_vector_type(4)));
+extern "C" __device__ f2v_t gnsship_raw_buffer_load_f32x2(i4v rsrc, int voffset, int soffset, int aux) __asm("llvm.amdgcn.raw.buffer.load.v2f32");
+extern "C" __device__ int gnsship_raw_buffer_load_i32(i4v rsrc, int voffset, int soffset, int aux) __asm("llvm.amdgcn.raw.buffer.load.i32");
+extern "C" __device__ short gnsship_raw_buffer_load_i16(i4v rsrc, int voffset, int soffset, int aux) __asm("llvm.amdgcn.raw.buffer.load.i16");
+
 template <int FMT>
-__device__ __forceinline__ float2 load_sample(const void* __restrict__ base, int64_t i)
+constexpr int sample_bytes() { return FMT == GNSSHIP_FMT_CF32 ? 8 : (FMT == GNSSHIP_FMT_CI16 ? 4 : 2); }
+
+// Buffer resource over samples [first, first + len) (gfx9 raw buffer: stride 0, dword3 0x00020000).
+template <int FMT>
+__device__ __forceinline__ i4v sample_span(const void* samples, int64_t first, int len)
+{
+    const uint64_t p = reinterpret_cast<uint64_t>(samples) + static_cast<uint64_t>(first) * sample_bytes<FMT>();
+    return i4v{static_cast<int>(p & 0xffffffffu), static_cast<int>((p >> 32) & 0xffffu), (len > 0 ? len : 0) * sample_bytes<FMT>(), 0x00020000};
+}
+
+template <int FMT>
+__device__ __forceinline__ f2v_t load_sample(i4v span, int voffset, int soffset)
 {
     if constexpr (FMT == GNSSHIP_FMT_CF32) {
-        return reinterpret_cast<const float2*>(base)[i];
+        return gnsship_raw_buffer_load_f32x2(span, voffset, soffset, 0);
     } else if constexpr (FMT == GNSSHIP_FMT_CI16) {
-        const short2 s = reinterpret_cast<const short2*>(base)[i];
-        return make_float2(static_cast<float>(s.x), static_cast<float>(s.y));
+        const int v = gnsship_raw_buffer_load_i32(span, voffset, soffset, 0);
+        return f2v_t{static_cast<float>(static_cast<short>(v & 0xffff)), static_cast<float>(static_cast<short>(v >> 16))};
     } else {
-        const char2 s = reinterpret_cast<const char2*>(base)[i];
-        return make_float2(static_cast<float>(s.x), static_cast<float>(s.y));
+        const int v = gnsship_raw_buffer_load_i16(span, voffset, soffset, 0);
+        return f2v_t{static_cast<float>(static_cast<signed char>(v & 0xff)), static_cast<float>(static_cast<signed char>((v >> 8) & 0xff))};
     }
 }
 
-__device__ __forceinline__ float wave_sum(float v)
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float v)
 {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
+
+// Sum over each 16-lane row of the wave, valid in every lane of the row: a DPP butterfly (no LDS
+// round trip) — xor 1, xor 2 (quad_perm), then the 8- and 16-lane mirrors, each pairing two
+// already-summed halves.  The four row sums of a wave are combined with the other waves' in LDS.
+__device__ __forceinline__ float row_sum(float v)
+{
+    v += dpp_mov<0xB1>(v);   // quad_perm [1,0,3,2]
+    v += dpp_mov<0x4E>(v);   // quad_perm [2,3,0,1]
+    v += dpp_mov<0x141>(v);  // row_half_mirror
+    v += dpp_mov<0x140>(v);  // row_mirror
     return v;
 }
 
@@ -170,28 +203,19 @@ constexpr int kGroups = kCorrSamplesPerThread / kGroup;
 constexpr int kGroupSpan = kGroup * kCorrThreads;
 static_assert(kGroups % 2 == 0, "ping-pong over pairs of groups");
 
-// Samples of pipeline group g for this lane.  Whole groups inside the chunk load without any tail
-// test; in the (at most one) partial group, lanes past the chunk end read the chunk's last sample
-// and contribute zero.
+// Samples of pipeline group g of a chunk for this lane (zeros past the chunk end).
 template <int FMT>
-__device__ __forceinline__ void load_group(const void* __restrict__ samples, int64_t base, int len, int g, f2 (&dstx)[kGroup])
+__device__ __forceinline__ void load_group(i4v span, int g, f2 (&dstx)[kGroup])
 {
-    const int tid = threadIdx.x;
-    if ((g + 1) * kGroupSpan <= len) {
+    const int voff = static_cast<int>(threadIdx.x) * sample_bytes<FMT>();
 #pragma unroll
-        for (int u = 0; u < kGroup; u++) {
-            const float2 v = load_sample<FMT>(samples, base + tid + (g * kGroup + u) * kCorrThreads);
-            dstx[u] = f2{v.x, v.y};
-        }
-    } else {
-#pragma unroll
-        for (int u = 0; u < kGroup; u++) {
-            const int r = tid + (g * kGroup + u) * kCorrThreads;
-            const float2 v = load_sample<FMT>(samples, base + (r < len ? r : len - 1));
-            dstx[u] = (r < len) ? f2{v.x, v.y} : f2{0.0f, 0.0f};
-        }
-    }
+    for (int u = 0; u < kGroup; u++) dstx[u] = load_sample<FMT>(span, voff, (g * kGroup + u) * kCorrThreads * sample_bytes<FMT>());
 }
+
+// s_waitcnt immediates (gfx9 encoding: vmcnt [3:0]+[15:14], expcnt [6:4], lgkmcnt [11:8]) that
+// wait on the vector-memory counter only.
+constexpr int waitcnt_vm(int n) { return (n & 0xF) | ((n >> 4) << 14) | (0x7 << 4) | (0xF << 8); }
+constexpr int kWaitVmcntGroup = waitcnt_vm(kGroup);
 
 // E_j = |inc|^j · e^{i j Δ}: rotation from a renormalised anchor to sample 256k + j, for this
 // lane's j = threadIdx.x (angle formed and range-reduced in double, then an accurate float sincos).
@@ -222,11 +246,14 @@ __device__ __forceinline__ void correlate_group(const DevJob& job, const ChunkDe
     // resampler, generic association order ((step*n) + shift) - rem, each rounded on its own; the
     // file is built with -ffp-contract=off)
     float cv[kGroup][NT];
+    // (float)n for the group's first sample; the later ones are exact float increments of 256
+    // (n + 256u is representable whenever (float)n's ulp divides 256, i.e. for every int32 n)
+    const float fn0 = static_cast<float>(ch.start + tid + g * kGroupSpan);
 #pragma unroll
     for (int u = 0; u < kGroup; u++) {
         const int r = tid + (g * kGroup + u) * kCorrThreads;
-        const int n = ch.start + (FULL ? r : (r < ch.len ? r : ch.len - 1));  // reference loop counter
-        const float sn = job.code_step * static_cast<float>(n);
+        const float fn = FULL ? fn0 + static_cast<float>(u * kCorrThreads) : static_cast<float>(ch.start + (r < ch.len ? r : ch.len - 1));
+        const float sn = job.code_step * fn;  // reference loop counter n, as float
 #pragma unroll
         for (int t = 0; t < NT; t++) {
             int idx = cvt_floor_i32((sn + shifts[t]) - job.rem_code);
@@ -241,7 +268,8 @@ __device__ __forceinline__ void correlate_group(const DevJob& job, const ChunkDe
     for (int u = 0; u < kGroup; u++) {
         const Anchor& a = qk[g * kGroup + u];  // block of sample u: chunk-uniform (SGPRs)
         const f2 p = cmul_pk(f2{a.q_re, a.q_im}, e, esw);
-        const f2 tt = cmul_pk2(xg[u], p);
+        const f2 x = xg[u];  // zero past the chunk end (buffer range check)
+        const f2 tt = cmul_pk2(x, p);
 #pragma unroll
         for (int t = 0; t < NT; t++) acc[t] = __builtin_elementwise_fma(tt, f2{cv[u][t], cv[u][t]}, acc[t]);
     }
@@ -272,7 +300,7 @@ __global__ __launch_bounds__(kCorrThreads, (corr_waves_per_simd<NT, IN_MARGIN>()
     const Anchor* __restrict__ anchors, float* __restrict__ partials, float* __restrict__ out, AnchorPrefetch pf)
 {
     extern __shared__ __attribute__((aligned(16))) float lds_code[];
-    __shared__ float red[kMaxChunksPerItem][kCorrThreads / 64][2 * NT];
+    __shared__ float red[kMaxChunksPerItem][kCorrThreads / 16][2 * NT];  // per chunk: 16 row sums per value
     GNSSHIP_PROF_STAMP(0);
     // Leading workgroups replay the rotator anchors of ANOTHER batch (the next one of a
     // double-buffered pair): one lane per job, latency-bound chains that run beside the
@@ -307,40 +335,34 @@ __global__ __launch_bounds__(kCorrThreads, (corr_waves_per_simd<NT, IN_MARGIN>()
         }
         return;
     }
-    // Latency order: the code replica's loads first (its pointer is in the chunk descriptor, not
-    // behind the job), then this lane's first sample group, then the LDS stores of the replica —
-    // the in-order vmcnt wait for the code leaves the sample loads in flight across the barrier.
-    // Padded replica: lds[kCodeMargin + i] = code[i mod L] for i in [−kCodeMargin, L + kCodeMargin).
-    constexpr int kFillRegs = 9;  // ≤ 2304 padded chips from registers (GPS 1087, B1I 2110)
-    const int total = L + 2 * kCodeMargin;
-    float cr[kFillRegs];
-#pragma unroll
-    for (int k = 0; k < kFillRegs; k++) {
-        const int i = threadIdx.x + k * kCorrThreads;
-        int src = i - kCodeMargin;
-        src = src < 0 ? src + L * ((-src + L - 1) / L) : src;
-        src = src % L;
-        cr[k] = (i < total) ? c0.code[src] : 0.0f;
+    // Latency order: the code replica first, loaded straight into LDS (global_load_lds_dwordx4: no
+    // VGPRs, nothing to spill, in flight across the sample prefetch), then this lane's first sample
+    // group, then E_j while both are in flight.  The replica is pre-wrapped in HBM (engine.h:
+    // padded_code_quads): lds[kCodeMargin + i] = code[i mod L], i in [−kCodeMargin, L + kCodeMargin).
+    {
+        typedef __attribute__((address_space(1))) const void* gptr;
+        typedef __attribute__((address_space(3))) void* lptr;
+        const int nq = padded_code_quads(L);
+        const float4* src4 = reinterpret_cast<const float4*>(c0.code - kCodeMargin);
+        float4* lds4 = reinterpret_cast<float4*>(lds_code);
+        const int wave_base = threadIdx.x & ~63;
+        for (int q0 = 0; q0 < nq; q0 += kCorrThreads) {  // GPS 2 passes, B1I 3, E1 9
+            if (q0 + static_cast<int>(threadIdx.x) < nq)
+                __builtin_amdgcn_global_load_lds((gptr)(src4 + q0 + threadIdx.x), (lptr)(lds4 + q0 + wave_base), 16, 0, 0);
+        }
     }
     f2 xa[kGroup], xb[kGroup];
     f2 e;
     {
         const DevJob& j0 = jobs[c0.job];
-        if (c0.len > 0) load_group<FMT>(samples, j0.sample_offset + c0.start, c0.len, 0, xa);
+        load_group<FMT>(sample_span<FMT>(samples, j0.sample_offset + c0.start, c0.len), 0, xa);
         e = anchor_to_lane_rotation(j0);  // ALU work while the loads are in flight
-    }
-#pragma unroll
-    for (int k = 0; k < kFillRegs; k++) {
-        const int i = threadIdx.x + k * kCorrThreads;
-        if (i < total) lds_code[i] = cr[k];
-    }
-    for (int i = threadIdx.x + kFillRegs * kCorrThreads; i < total; i += kCorrThreads) {  // long replicas (E1: 8248)
-        lds_code[i] = c0.code[(i - kCodeMargin) % L];
+        // the replica's loads were issued before the kGroup sample loads (vmcnt retires in order)
+        __builtin_amdgcn_s_waitcnt(kWaitVmcntGroup);
     }
     __syncthreads();
     GNSSHIP_PROF_STAMP(1);
     const float* code = lds_code + kCodeMargin;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     int prev_job = c0.job;
 
     for (int c = 0; c < it.count; c++) {
@@ -350,13 +372,10 @@ __global__ __launch_bounds__(kCorrThreads, (corr_waves_per_simd<NT, IN_MARGIN>()
         prev_job = ch.job;
         // only what the next chunk's first sample group needs is carried across the chunk
         const bool has_next = c + 1 < it.count;
-        int nstart = 0, nlen = 0;
-        int64_t noff = 0;
+        i4v next_span = i4v{0, 0, 0, 0x00020000};
         if (has_next) {
             const ChunkDesc chn = chunks[it.first + c + 1];
-            nstart = chn.start;
-            nlen = chn.len;
-            noff = jobs[chn.job].sample_offset;
+            next_span = sample_span<FMT>(samples, jobs[chn.job].sample_offset + chn.start, chn.len);
         }
         const f2 esw = f2{-e.y, e.x};
         float shifts[NT];
@@ -369,9 +388,9 @@ __global__ __launch_bounds__(kCorrThreads, (corr_waves_per_simd<NT, IN_MARGIN>()
         Anchor qk[kBlocksPerChunk];
 #pragma unroll
         for (int m = 0; m < kBlocksPerChunk; m++) qk[m] = anc[m];
-        const int64_t base = job.sample_offset + ch.start;
+        const i4v span = sample_span<FMT>(samples, job.sample_offset + ch.start, ch.len);
         const int ng = (ch.len + kGroupSpan - 1) / kGroupSpan;  // groups in this chunk (0..kGroups)
-        GNSSHIP_PROF_STAMP(2);
+        GNSSHIP_PROF_STAMP(c == 0 ? 2 : 6);
         f2 acc[NT];
 #pragma unroll
         for (int t = 0; t < NT; t++) acc[t] = f2{0.0f, 0.0f};
@@ -383,9 +402,9 @@ __global__ __launch_bounds__(kCorrThreads, (corr_waves_per_simd<NT, IN_MARGIN>()
                 f2(&cur)[kGroup] = (g & 1) ? xb : xa;
                 f2(&nxt)[kGroup] = (g & 1) ? xa : xb;
                 if (g + 1 < ng)
-                    load_group<FMT>(samples, base, ch.len, g + 1, nxt);
-                else if (has_next && nlen > 0)
-                    load_group<FMT>(samples, noff + nstart, nlen, 0, nxt);
+                    load_group<FMT>(span, g + 1, nxt);
+                else if (has_next)
+                    load_group<FMT>(next_span, 0, nxt);
                 if ((g + 1) * kGroupSpan <= ch.len)
                     correlate_group<NT, IN_MARGIN, true>(job, ch, qk, e, esw, shifts, code, L, g, cur, acc);
                 else
@@ -393,23 +412,23 @@ __global__ __launch_bounds__(kCorrThreads, (corr_waves_per_simd<NT, IN_MARGIN>()
             }
         }
         // next chunk's group 0 sits in buffer ng & 1 → move it to xa (an empty chunk issued none)
-        if (ng == 0 && has_next && nlen > 0) load_group<FMT>(samples, noff + nstart, nlen, 0, xa);
+        if (ng == 0 && has_next) load_group<FMT>(next_span, 0, xa);
         if (ng & 1) {
 #pragma unroll
             for (int u = 0; u < kGroup; u++) xa[u] = xb[u];
         }
-        GNSSHIP_PROF_STAMP(3);
+        GNSSHIP_PROF_STAMP(c == 0 ? 3 : 7);
 #pragma unroll
         for (int t = 0; t < NT; t++) {
-            const float wr = wave_sum(acc[t].x), wi = wave_sum(acc[t].y);
-            if (lane == 0) {
-                red[c][wave][2 * t] = wr;
-                red[c][wave][2 * t + 1] = wi;
+            const float wr = row_sum(acc[t].x), wi = row_sum(acc[t].y);
+            if ((threadIdx.x & 15) == 0) {
+                red[c][threadIdx.x >> 4][2 * t] = wr;
+                red[c][threadIdx.x >> 4][2 * t + 1] = wi;
             }
         }
     }
     __syncthreads();
-    // per-chunk outputs: thread (c, v) sums the 4 wave partials of value v of chunk c, in wave order
+    // per-chunk outputs: thread (c, v) sums the 16 row partials of value v of chunk c, in lane order
     for (int k = threadIdx.x; k < it.count * 2 * kMaxTaps; k += kCorrThreads) {
         const int c = k / (2 * kMaxTaps), v = k % (2 * kMaxTaps);
         const ChunkDesc cc = chunks[it.first + c];
@@ -418,7 +437,7 @@ __global__ __launch_bounds__(kCorrThreads, (corr_waves_per_simd<NT, IN_MARGIN>()
         float s = 0.0f;
         if (v < 2 * NT && v < 2 * jc.n_taps && cc.len > 0) {
 #pragma unroll
-            for (int w = 0; w < kCorrThreads / 64; w++) s += red[c][w][v];
+            for (int w = 0; w < kCorrThreads / 16; w++) s += red[c][w][v];
         }
         dst[v] = s;
     }

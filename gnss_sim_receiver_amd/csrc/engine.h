@@ -51,6 +51,13 @@ struct DevJob {
 // indices a few chips outside [0, L) — the usual case at epoch edges with early/late taps — need
 // no modulo.  Jobs that can leave the margin (checked on the host) take the general wrap path.
 constexpr int kCodeMargin = 32;
+// Device code replicas are stored pre-wrapped in HBM, [code[L−M..L−1] | code[0..L−1] | code[0..M−1]]
+// (M = kCodeMargin) rounded up to whole 16-byte quads; the pointer handed around (CodeDesc::ptr,
+// ChunkDesc::code) is chip 0.  The correlator copies the padded span into LDS with aligned 16-byte
+// loads and no index arithmetic.
+constexpr int padded_code_quads(int len) { return (len + 2 * kCodeMargin + 3) / 4; }
+hipError_t upload_padded_code(const float* code, int len, float** chip0);  // allocates; *chip0 = chip 0
+hipError_t free_padded_code(const float* chip0);
 
 // Rotator anchor of one 256-sample block k of a job: the renormalised phasor q = a/|a| the
 // reference rotates from sample 256k on (a = the phasor it multiplies sample 256k by; the
@@ -73,7 +80,7 @@ struct ChunkDesc {
 
 // A workgroup's work: chunks [first, first + count) of the (reordered) chunk array, all sharing
 // one code replica (corr_batch_kernel stages it in LDS once per item).
-constexpr int kMaxChunksPerItem = 8;
+constexpr int kMaxChunksPerItem = 4;
 constexpr int kChunksPerItemDefault = 2;
 struct WorkItem {
     int32_t first;

@@ -164,6 +164,27 @@ int plan_chunks(std::vector<DevJob>& jobs, std::vector<ChunkDesc>& chunks, std::
     return static_cast<int>(chunks.size());
 }
 
+hipError_t upload_padded_code(const float* code, int len, float** chip0)
+{
+    std::vector<float> pad(static_cast<size_t>(padded_code_quads(len)) * 4, 0.0f);
+    for (int i = -kCodeMargin; i < len + kCodeMargin; i++) pad[i + kCodeMargin] = code[((i % len) + len) % len];
+    float* base = nullptr;
+    hipError_t e = hipMalloc(&base, sizeof(float) * pad.size());
+    if (e != hipSuccess) return e;
+    e = hipMemcpy(base, pad.data(), sizeof(float) * pad.size(), hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        (void)hipFree(base);
+        return e;
+    }
+    *chip0 = base + kCodeMargin;
+    return hipSuccess;
+}
+
+hipError_t free_padded_code(const float* chip0)
+{
+    return chip0 ? hipFree(const_cast<float*>(chip0 - kCodeMargin)) : hipSuccess;
+}
+
 int chunks_per_item_setting()
 {
     const char* e = std::getenv("GNSSHIP_CHUNKS_PER_ITEM");  // tuning knob
@@ -239,7 +260,7 @@ extern "C" int gnsship_ctx_destroy(gnsship_ctx* ctx)
     (void)hipSetDevice(ctx->device);
     (void)hipStreamSynchronize(ctx->stream);
     for (auto& c : ctx->codes_host)
-        if (c.ptr) (void)hipFree(const_cast<float*>(c.ptr));
+        if (c.ptr) (void)free_padded_code(c.ptr);
     if (ctx->codes_dev) (void)hipFree(ctx->codes_dev);
     for (auto& ev : ctx->events)
         if (ev) (void)hipEventDestroy(ev);
@@ -321,17 +342,15 @@ extern "C" int gnsship_code_set(gnsship_ctx* ctx, int code_id, const float* code
     if (static_cast<int>(ctx->codes_host.size()) <= code_id) ctx->codes_host.resize(code_id + 1, CodeDesc{nullptr, 0, 0});
     CodeDesc& d = ctx->codes_host[code_id];
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-    if (d.ptr && d.len != len) {
-        HIP_TRY(ctx, hipFree(const_cast<float*>(d.ptr)));
+    if (d.ptr) {
+        HIP_TRY(ctx, free_padded_code(d.ptr));
         d.ptr = nullptr;
+        d.len = 0;
     }
-    if (!d.ptr) {
-        float* p = nullptr;
-        HIP_TRY(ctx, hipMalloc(&p, sizeof(float) * len));
-        d.ptr = p;
-    }
+    float* p = nullptr;
+    HIP_TRY(ctx, upload_padded_code(code, len, &p));
+    d.ptr = p;
     d.len = len;
-    HIP_TRY(ctx, hipMemcpy(const_cast<float*>(d.ptr), code, sizeof(float) * len, hipMemcpyHostToDevice));
     ctx->codes_dirty = true;
     ctx->codes_version++;
     return GNSSHIP_OK;
@@ -620,13 +639,13 @@ extern "C" int gnsship_corr_set_local_code_and_taps(gnsship_corr* c, int code_le
         return fail(ctx, GNSSHIP_E_INVAL, "gnsship_corr_set_local_code_and_taps: bad code / shifts");
     if (int rc = set_device(ctx)) return rc;
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-    if (c->code_dev && c->code_len != code_length_chips) {
-        HIP_TRY(ctx, hipFree(c->code_dev));
+    if (c->code_dev) {
+        HIP_TRY(ctx, free_padded_code(c->code_dev));
         c->code_dev = nullptr;
+        c->code_set = false;
     }
-    if (!c->code_dev) HIP_TRY(ctx, hipMalloc(&c->code_dev, sizeof(float) * code_length_chips));
+    HIP_TRY(ctx, upload_padded_code(code, code_length_chips, &c->code_dev));
     c->code_len = code_length_chips;
-    HIP_TRY(ctx, hipMemcpy(c->code_dev, code, sizeof(float) * code_length_chips, hipMemcpyHostToDevice));
     CodeDesc d{c->code_dev, code_length_chips, 0};
     HIP_TRY(ctx, hipMemcpy(c->code_table_dev, &d, sizeof(d), hipMemcpyHostToDevice));
     for (int t = 0; t < c->n_taps; t++) c->shifts[t] = shifts[t];
@@ -697,7 +716,8 @@ extern "C" int gnsship_corr_destroy(gnsship_corr* c)
     if (!c) return GNSSHIP_E_INVAL;
     (void)hipSetDevice(c->ctx->device);
     (void)hipStreamSynchronize(c->ctx->stream);
-    void* ptrs[] = {c->code_dev, c->code_table_dev, c->sig_dev, c->job_dev, c->chunks_dev, c->items_dev, c->partials_dev, c->out_dev, c->anchors_dev};
+    (void)free_padded_code(c->code_dev);
+    void* ptrs[] = {c->code_table_dev, c->sig_dev, c->job_dev, c->chunks_dev, c->items_dev, c->partials_dev, c->out_dev, c->anchors_dev};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     delete c;

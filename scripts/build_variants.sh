@@ -7,7 +7,7 @@ OBJS=$(ls build/obj/*.o | grep -v corr_kernel)
 for spec in "$@"; do
   tag=${spec%%:*}; flags=${spec#*:}
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -ffp-contract=off -Iinclude -Ignss_sim_receiver_amd/csrc $flags \
-    -c gnss_sim_receiver_amd/csrc/corr_kernel.hip -o build/corr_$tag.o
+    -c ${CORR_SRC:-gnss_sim_receiver_amd/csrc/corr_kernel.hip} -o build/corr_$tag.o
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o scripts/libgnsship_$tag.so $OBJS build/corr_$tag.o
   echo "built scripts/libgnsship_$tag.so"
 done

@@ -2,8 +2,10 @@
 
     make prof && GNSSHIP_LIB_PATH=scripts/libgnsship_prof.so python scripts/corr_wg_profile.py
 
-Stamps (wall_clock64, 100 MHz) per workgroup: 0 entry, 1 code in LDS, 2 E_j ready, 3 main loop
-done, 4 end (5: end of an anchor-prefetch workgroup).  Prints phase-duration percentiles, the
+Stamps (wall_clock64, 100 MHz) per workgroup: 0 entry, 1 code in LDS, 2/6 chunk 0/1 set up,
+3/7 chunk 0/1 main loop done, 4 end (5: end of an anchor-prefetch workgroup).  Each stamp waits
+for the wave's outstanding scalar and LDS operations (lgkmcnt), so a phase boundary lands after
+the loads issued before it.  Prints phase-duration percentiles, the
 workgroup lifetime, and how many workgroups were resident over the kernel."""
 import ctypes
 import os
@@ -53,10 +55,16 @@ def main():
     t0 = corr[:, 0].min()
     us = lambda v: v / 100.0  # noqa: E731  (100 MHz → µs)
     print(f"mode {mode}: {len(corr)} correlation WGs, {len(anc)} anchor WGs; kernel span {us(corr[:, 4].max() - t0):.1f} us")
-    names = ["code->LDS", "E_j setup", "main loop", "reduce+store"]
-    for k in range(4):
-        d = us(corr[:, k + 1] - corr[:, k])
-        print(f"  {names[k]:13s} p10 {np.percentile(d, 10):6.2f}  p50 {np.percentile(d, 50):6.2f}  p90 {np.percentile(d, 90):6.2f} us")
+    two = corr[corr[:, 6] > 0]  # items of two or more chunks: chunk 1 start (6) / main-loop end (7)
+    one = corr[corr[:, 6] == 0]
+    phases = [("code->LDS", corr, 0, 1), ("chunk0 start", corr, 1, 2), ("chunk0 loop", corr, 2, 3)]
+    if len(two):
+        phases += [("wave sums+c1 start", two, 3, 6), ("chunk1 loop", two, 6, 7), ("reduce+store", two, 7, 4)]
+    if len(one):
+        phases += [("reduce+store(1)", one, 3, 4)]
+    for name, rows, a, b in phases:
+        d = us(rows[:, b] - rows[:, a])
+        print(f"  {name:19s} n {len(rows):5d} p10 {np.percentile(d, 10):6.2f}  p50 {np.percentile(d, 50):6.2f}  p90 {np.percentile(d, 90):6.2f} us")
     life = us(corr[:, 4] - corr[:, 0])
     print(f"  WG lifetime   p10 {np.percentile(life, 10):6.2f}  p50 {np.percentile(life, 50):6.2f}  p90 {np.percentile(life, 90):6.2f} us")
     if len(anc):
