@@ -60,6 +60,9 @@ def build_block(seconds: float):
     return sats, signals.generate_if(FS, n, sats, seed=SEED), n
 
 
+N_RING = 3  # receivers per rank, stepped in a ring (pipelined anchor replay, see step())
+
+
 def receiver_jobs(sats, rank: int, seconds: float):
     from gnss_sim_receiver_amd import signals
     n_ep = int(round(seconds * 1000))
@@ -241,13 +244,13 @@ def main():
         dev_ptrs = [dev_buf.ptr, dev_buf.ptr]
     dev_ptr = dev_ptrs[0]
 
-    # Two 12-channel receivers per rank (channel sets 24r..24r+11 and 24r+12..24r+23, channel c
-    # tracking satellite c mod 32), stepped alternately: each step is one full receiver-second, and
-    # the NCO-only anchor replay of the next receiver's batch runs inside the current correlation
-    # launch (gnsship_batch_launch_pipelined).
+    # Three 12-channel receivers per rank (channel sets 36r+12k .. 36r+12k+11, channel c tracking
+    # satellite c mod 32), stepped in a ring: each step is one full receiver-second, and the
+    # NCO-only anchor replay of the next two receivers' batches rides inside the current
+    # correlation launch, half a replay chain each (gnsship_batch_launch_pipelined2).
     receivers, all_codes = [], {}
-    for k in range(2):
-        jk, ck = receiver_jobs(sats, 2 * rank + k, args.seconds)
+    for k in range(N_RING):
+        jk, ck = receiver_jobs(sats, N_RING * rank + k, args.seconds)
         jk["code_id"] += 32 * k  # receiver k's code-bank entries live at 32·k + id
         for cid, c in enumerate(ck):
             all_codes[32 * k + cid] = c
@@ -265,17 +268,19 @@ def main():
     step_no = [0]
 
     def step():
-        cur = step_no[0] & 1
+        i = step_no[0]
         step_no[0] += 1
-        b = batches[cur]
-        # each launch correlates this receiver and replays the other receiver's rotator anchors
-        # (gnsship_batch_launch_pipelined): one launch per step, one stream, no cross-stream event
+        cur = i & 1  # IF block double buffer
+        b, nb, nb2 = (batches[(i + m) % N_RING] for m in range(3))
+        # each launch correlates this receiver, finishes the next one's rotator-anchor replay and
+        # starts the one after's (gnsship_batch_launch_pipelined2): one launch per step, one
+        # stream, no cross-stream event
         if torch is None:
-            b.launch_pipelined(dev_ptrs[0], abi.FMT_CF32, batches[cur ^ 1])
+            b.launch_pipelined(dev_ptrs[0], abi.FMT_CF32, nb, nb2)
             return
         # exchange step: fan the NEXT block out to every rank while this one is correlated
         work = sharding.broadcast_block(dev_ts[cur ^ 1], src=0, async_op=True)
-        b.launch_pipelined(dev_ptrs[cur], abi.FMT_CF32, batches[cur ^ 1])
+        b.launch_pipelined(dev_ptrs[cur], abi.FMT_CF32, nb, nb2)
         ctx.sync()
         work.wait()
         torch.cuda.current_stream().synchronize()

@@ -165,6 +165,7 @@ _SIGNATURES = {
     "gnsship_batch_results": ([_vp, _f32p], _i),
     "gnsship_batch_results_device": ([_vp, _vpp], _i),
     "gnsship_batch_launch_pipelined": ([_vp, _vp, _i, _vp], _i),
+    "gnsship_batch_launch_pipelined2": ([_vp, _vp, _i, _vp, _vp], _i),
     "gnsship_batch_destroy": ([_vp], _i),
     "gnsship_acq_create": ([_vp, ctypes.POINTER(AcqConf), _vpp], _i),
     "gnsship_acq_set_grid": ([_vp, _i, _i, _i], _i),

@@ -62,25 +62,43 @@ __device__ __forceinline__ float hypotf_glibc(float x, float y)
     return static_cast<float>(__dsqrt_rn(__dadd_rn(__dmul_rn(dx, dx), __dmul_rn(dy, dy))));
 }
 
-// The reference rotator recursion of one job, stored at every renormalisation point.
-__device__ __forceinline__ void replay_anchors(const DevJob& job, Anchor* __restrict__ anchors)
+// First renormalisation block of replay segment seg of a job with nblk blocks (segments split at
+// the middle block; kAnchorSegments == 2).
+__device__ __forceinline__ int segment_block(int seg, int nblk)
+{
+    return seg <= 0 ? 0 : (seg >= kAnchorSegments ? nblk : (nblk + 1) / 2);
+}
+
+// The reference rotator recursion of one job, stored at every renormalisation point — blocks of
+// segments [seg_lo, seg_hi).  A later segment resumes from the stored anchor of the block before
+// it: the chain after a renormalisation depends only on the renormalised phasor q.
+__device__ __forceinline__ void replay_anchors(const DevJob& job, Anchor* __restrict__ anchors, int seg_lo, int seg_hi)
 {
     const int nblk = (job.n_samples + kRenorm - 1) / kRenorm;
+    const int kb = segment_block(seg_lo, nblk), ke = segment_block(seg_hi, nblk);
+    if (kb >= ke) return;
     Anchor* out = anchors + job.anchor_offset;
     typedef float f2v __attribute__((ext_vector_type(2)));
-    float pr = job.p0_re, pi = job.p0_im;
     // phase·inc = (pr·ir − pi·ii, pr·ii + pi·ir) as two packed products + one packed add, each
     // rounded separately like the reference's written-out complex product (no FMA).  The sign
     // sits in the constant: fl(pi·(−ii)) = −fl(pi·ii) and x + (−y) ≡ x − y, bit for bit.
     const f2v inc_a = {job.inc_re, job.inc_im};   // × pr
     const f2v inc_b = {-job.inc_im, job.inc_re};  // × pi
-    for (int k = 0; k < nblk; k++) {
+    f2v p;
+    if (kb == 0) {
+        p = f2v{job.p0_re, job.p0_im};
+    } else {
+        p = f2v{out[kb - 1].q_re, out[kb - 1].q_im};
+#pragma unroll 16
+        for (int s = 0; s < kRenorm; s++) p = f2v{p.x, p.x} * inc_a + f2v{p.y, p.y} * inc_b;
+    }
+    for (int k = kb; k < ke; k++) {
         // sample 256k uses `a = phase`; then phase /= |phase|; then 256 rotations reach 256(k+1)
-        const float m = hypotf_glibc(pr, pi);
-        const float qr = __fdiv_rn(pr, m), qi = __fdiv_rn(pi, m);
+        const float m = hypotf_glibc(p.x, p.y);
+        const float qr = __fdiv_rn(p.x, m), qi = __fdiv_rn(p.y, m);
         out[k] = Anchor{qr, qi};
-        f2v p = {qr, qi};
-        if (k != nblk - 1) {
+        p = f2v{qr, qi};
+        if (k != ke - 1) {
 #pragma unroll 16
             for (int s = 0; s < kRenorm; s++) {
                 const f2v m1 = f2v{p.x, p.x} * inc_a;
@@ -88,17 +106,15 @@ __device__ __forceinline__ void replay_anchors(const DevJob& job, Anchor* __rest
                 p = m1 + m2;
             }
         }
-        pr = p.x;
-        pi = p.y;
     }
 }
 
-__global__ void corr_anchor_kernel(const DevJob* __restrict__ jobs, int n_jobs, Anchor* __restrict__ anchors)
+__global__ void corr_anchor_kernel(const DevJob* __restrict__ jobs, int n_jobs, Anchor* __restrict__ anchors, int seg_lo, int seg_hi)
 {
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= n_jobs) return;
     const DevJob job = jobs[j];
-    replay_anchors(job, anchors);
+    replay_anchors(job, anchors, seg_lo, seg_hi);
 }
 
 typedef float f2v_t __attribute__((ext_vector_type(2)));
@@ -224,10 +240,20 @@ __device__ __forceinline__ f2 anchor_to_lane_rotation(const DevJob& job)
     constexpr double kTwoPi = 6.283185307179586476925286766559;
     constexpr double kInvTwoPi = 0.15915494309189533576888376337251;
     const int tid = threadIdx.x;
+#ifndef GNSSHIP_EJ_LIBM
+    // angle in revolutions, range-reduced in double; the hardware sin/cos (V_SIN/V_COS_F32) take
+    // revolutions — E_j to a few 1e-7, against the 1e-5 correlation tolerance (the libm sincosf
+    // form, GNSSHIP_EJ_LIBM, costs ~50 more VALU per chunk)
+    const double rev = static_cast<double>(tid) * (job.dtheta * kInvTwoPi);
+    const float rf = static_cast<float>(rev - rint(rev));
+    const float s = __builtin_amdgcn_sinf(rf), c = __builtin_amdgcn_cosf(rf);
+    (void)kTwoPi;
+#else
     double th = static_cast<double>(tid) * job.dtheta;
     th = fma(-kTwoPi, rint(th * kInvTwoPi), th);
     float s, c;
     sincosf(static_cast<float>(th), &s, &c);
+#endif
     const float mag = __fmaf_rn(static_cast<float>(tid), job.log_mag_inc, 1.0f);
     return f2{mag * c, mag * s};
 }
@@ -275,11 +301,12 @@ __device__ __forceinline__ void correlate_group(const DevJob& job, const ChunkDe
     }
 }
 
-// Waves per SIMD the register allocation must allow: the 1- and 3-tap classes (GPS/B1I E-P-L, E1
-// data prompt) are held to 64 VGPRs for full occupancy — the kernel is latency-bound, residency is
-// its throughput; wider tap classes keep the general bound.
+// Waves per SIMD the register allocation must allow: the 1- and 3-tap in-margin classes (GPS/B1I
+// E-P-L, E1 data prompt) are held to 7 waves (≤ 72 VGPRs, spill-free): residency hides the sample
+// and LDS latency of a kernel whose issue is otherwise VALU-bound; wider tap classes keep the
+// general bound.  (Measured: 6 → 7 waves +1%, 8 slower.)
 #ifndef GNSSHIP_CORR_WAVES_EPL
-#define GNSSHIP_CORR_WAVES_EPL 6
+#define GNSSHIP_CORR_WAVES_EPL 7
 #endif
 template <int NT, bool IN_MARGIN>
 constexpr int corr_waves_per_simd()
@@ -306,10 +333,15 @@ __global__ __launch_bounds__(kCorrThreads, (corr_waves_per_simd<NT, IN_MARGIN>()
     // double-buffered pair): one lane per job, latency-bound chains that run beside the
     // correlation instead of in a separate stream behind a cross-queue event.
     if (static_cast<int>(blockIdx.x) < pf.n_blocks) {
-        const int j = blockIdx.x * kCorrThreads + threadIdx.x;
-        if (j < pf.n_jobs) {
-            const DevJob pj = pf.jobs[j];
-            replay_anchors(pj, pf.anchors);
+#ifndef GNSSHIP_NO_REPLAY_PRIO
+        __builtin_amdgcn_s_setprio(3);  // a latency-bound serial chain: first pick of its SIMD's issue slots
+#endif
+        const bool t1 = static_cast<int>(blockIdx.x) >= pf.task[0].n_blocks;
+        const ReplayTask& t = pf.task[t1 ? 1 : 0];
+        const int j = (blockIdx.x - (t1 ? pf.task[0].n_blocks : 0)) * kCorrThreads + threadIdx.x;
+        if (j < t.n_jobs) {
+            const DevJob pj = t.jobs[j];
+            replay_anchors(pj, t.anchors, t.seg_lo, t.seg_hi);
         }
         GNSSHIP_PROF_STAMP(5);
         return;
@@ -470,22 +502,29 @@ hipError_t launch_corr_batch(const void* samples, int fmt, const DevJob* jobs, i
     hipStream_t stream, int stages, const AnchorPrefetch* prefetch)
 {
     const int n_chunks = n_items;  // work items to launch (0: nothing to correlate)
-    AnchorPrefetch pf{nullptr, 0, nullptr, 0};
-    if (prefetch && prefetch->n_jobs > 0 && (stages & GNSSHIP_STAGE_CORRELATE)) {
+    AnchorPrefetch pf{};
+    if (prefetch && (stages & GNSSHIP_STAGE_CORRELATE)) {
         pf = *prefetch;
-        pf.n_blocks = ((pf.n_jobs + kCorrThreads - 1) / kCorrThreads + 7) & ~7;
+        int nb = 0;
+        for (auto& t : pf.task) {
+            t.n_blocks = (t.n_jobs > 0 && t.seg_lo < t.seg_hi) ? (t.n_jobs + kCorrThreads - 1) / kCorrThreads : 0;
+            nb += t.n_blocks;
+        }
+        pf.n_blocks = (nb + 7) & ~7;
     }
     if (n_chunks <= 0) {
-        if (pf.n_jobs > 0) {
-            hipLaunchKernelGGL(corr_anchor_kernel, dim3((pf.n_jobs + 63) / 64), dim3(64), 0, stream, pf.jobs, pf.n_jobs, pf.anchors);
-            return hipGetLastError();
+        for (const auto& t : pf.task) {
+            if (t.n_blocks == 0) continue;
+            hipLaunchKernelGGL(corr_anchor_kernel, dim3((t.n_jobs + 63) / 64), dim3(64), 0, stream, t.jobs, t.n_jobs, t.anchors, t.seg_lo, t.seg_hi);
+            hipError_t e = hipGetLastError();
+            if (e != hipSuccess) return e;
         }
         return hipSuccess;
     }
     if (max_code_len < 1 || max_code_len > kMaxCodeLen) return hipErrorInvalidValue;
     hipError_t e = hipSuccess;
     if (stages & GNSSHIP_STAGE_ANCHORS) {
-        hipLaunchKernelGGL(corr_anchor_kernel, dim3((n_jobs + 63) / 64), dim3(64), 0, stream, jobs, n_jobs, anchors);
+        hipLaunchKernelGGL(corr_anchor_kernel, dim3((n_jobs + 63) / 64), dim3(64), 0, stream, jobs, n_jobs, anchors, 0, kAnchorSegments);
         e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
@@ -519,7 +558,7 @@ hipError_t launch_corr_batch(const void* samples, int fmt, const DevJob* jobs, i
 #undef GNSSHIP_LAUNCH_CORR
         e = hipGetLastError();
         if (e != hipSuccess) return e;
-        pf = AnchorPrefetch{nullptr, 0, nullptr, 0};  // only the first class launch carries the prefetch
+        pf = AnchorPrefetch{};  // only the first class launch carries the prefetch
     }
     e = hipGetLastError();
     if (e != hipSuccess || !any_multi_chunk) return e;

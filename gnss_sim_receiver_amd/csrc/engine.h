@@ -102,11 +102,21 @@ inline int chunk_class(int n_taps, int in_margin)
 }
 
 // Anchor replay of another job set carried by a correlation launch (leading workgroups).
-struct AnchorPrefetch {
+// Anchor replay carried by the leading workgroups of a correlation launch (see corr_batch_kernel).
+// A job's replay chain is split at its middle renormalisation block into kAnchorSegments
+// segments; segment s > 0 resumes from the anchor segment s − 1 stored (gnsship_batch_launch_pipelined2
+// spreads one batch's replay over two consecutive launches).
+constexpr int kAnchorSegments = 2;
+struct ReplayTask {
     const DevJob* jobs;
-    int32_t n_jobs;
     Anchor* anchors;
-    int32_t n_blocks;  // set by launch_corr_batch
+    int32_t n_jobs;
+    int32_t seg_lo, seg_hi;  // segments [seg_lo, seg_hi)
+    int32_t n_blocks;        // workgroups (set by launch_corr_batch)
+};
+struct AnchorPrefetch {
+    ReplayTask task[2];
+    int32_t n_blocks;        // all leading workgroups, a multiple of 8 (set by launch_corr_batch)
 };
 
 // Fill ChunkDesc::code / code_len from a code table indexed by the chunks' jobs' code ids.

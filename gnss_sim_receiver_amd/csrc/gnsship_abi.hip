@@ -391,9 +391,10 @@ struct gnsship_batch {
     hipStream_t aux = nullptr;
     hipEvent_t anchors_ready = nullptr;  // aux → ctx: anchors written
     hipEvent_t corr_done = nullptr;      // ctx → aux: correlation finished reading the anchors
-    // gnsship_batch_launch_pipelined: anchors of the current job set already written on the context
-    // stream (by a launch that carried this batch as `next`); cleared by set_jobs.
-    bool anchors_valid = false;
+    // gnsship_batch_launch_pipelined(2): replay segments of the current job set already written on
+    // the context stream by launches that carried this batch as `next` / `next2` (0..kAnchorSegments);
+    // cleared by set_jobs.
+    int anchor_segs = 0;
 };
 
 static void batch_release(gnsship_batch* b)
@@ -436,7 +437,7 @@ extern "C" int gnsship_batch_set_jobs(gnsship_batch* b, const gnsship_corr_job* 
     gnsship_ctx* ctx = b->ctx;
     if ((!jobs && n_jobs) || n_jobs < 0 || n_jobs > b->max_jobs) return fail(ctx, GNSSHIP_E_INVAL, "gnsship_batch_set_jobs: n_jobs out of range");
     if (int rc = set_device(ctx)) return rc;
-    b->anchors_valid = false;
+    b->anchor_segs = 0;
     if (int rc = sync_code_table(ctx)) return rc;
     b->jobs_host.resize(n_jobs);
     int max_len = 1;
@@ -517,38 +518,49 @@ extern "C" int gnsship_batch_launch_stages(gnsship_batch* b, const void* dev_sam
     return GNSSHIP_OK;
 }
 
-// Correlate `b` and, in the same launch, replay the rotator anchors of `next` (leading workgroups
-// of the correlation grid; see corr_batch_kernel).  Everything on the context stream, so a
-// double-buffered pair A, B, A, B, ... needs no cross-stream event: each launch finds its anchors
-// written by the previous one, and same-stream order keeps the next replay from overwriting
-// anchors a correlation still reads.  `b`'s anchors are computed first when no earlier launch
-// prefetched them (first call, or after set_jobs).
-extern "C" int gnsship_batch_launch_pipelined(gnsship_batch* b, const void* dev_samples, int fmt, gnsship_batch* next)
+// Correlate `b` and, in the same launch, replay rotator anchors of the batches that follow it
+// (leading workgroups of the correlation grid; see corr_batch_kernel): all remaining segments of
+// `next`, so that it is complete for the next launch, and the first segment of `next2`.
+// Everything on the context stream, so a ring of batches A, B, C, A, ... (or a pair A, B, A, ...
+// without next2) needs no cross-stream event: each launch finds its anchors written by earlier
+// ones, and same-stream order keeps a replay from overwriting anchors a correlation still reads.
+// The replay work is always done for the named batches (a batch named as `next` is replayed even
+// when its anchors are still complete).  `b`'s anchors are computed first when no earlier launch
+// completed them (first call, or after set_jobs).
+extern "C" int gnsship_batch_launch_pipelined2(gnsship_batch* b, const void* dev_samples, int fmt, gnsship_batch* next, gnsship_batch* next2)
 {
     if (!b) return GNSSHIP_E_INVAL;
     gnsship_ctx* ctx = b->ctx;
     if (fmt_bytes(fmt) == 0) return fail(ctx, GNSSHIP_E_INVAL, "gnsship_batch_launch_pipelined: unknown sample format");
-    if (next == b || (next && next->ctx != ctx)) return fail(ctx, GNSSHIP_E_INVAL, "gnsship_batch_launch_pipelined: next must be another batch of the same context");
+    if (next == b || next2 == b || (next2 && next2 == next) || (next && next->ctx != ctx) || (next2 && next2->ctx != ctx))
+        return fail(ctx, GNSSHIP_E_INVAL, "gnsship_batch_launch_pipelined: next / next2 must be distinct other batches of the same context");
     if (!dev_samples && b->n_jobs) return fail(ctx, GNSSHIP_E_INVAL, "gnsship_batch_launch_pipelined: null sample buffer");
     if (ctx->codes_dirty) return fail(ctx, GNSSHIP_E_STATE, "gnsship_batch_launch_pipelined: code bank changed after set_jobs");
     if (int rc = set_device(ctx)) return rc;
-    AnchorPrefetch pf{nullptr, 0, nullptr, 0};
-    const bool prefetch = next && next->n_jobs > 0;
-    if (prefetch) pf = AnchorPrefetch{next->jobs_dev, next->n_jobs, next->anchors_dev, 0};
-    if (b->n_jobs > 0 && !b->anchors_valid) {
+    AnchorPrefetch pf{};
+    const bool p1 = next && next->n_jobs > 0, p2 = next2 && next2->n_jobs > 0;
+    if (p1) pf.task[0] = ReplayTask{next->jobs_dev, next->anchors_dev, next->n_jobs, next->anchor_segs == 1 ? 1 : 0, kAnchorSegments, 0};
+    if (p2) pf.task[1] = ReplayTask{next2->jobs_dev, next2->anchors_dev, next2->n_jobs, 0, 1, 0};
+    if (b->n_jobs > 0 && b->anchor_segs < kAnchorSegments) {
         hipError_t e = launch_corr_batch(dev_samples, fmt, b->jobs_dev, b->n_jobs, b->chunks_dev, b->items_dev, b->n_items, b->classes,
             b->max_code_len, b->any_multi, b->anchors_dev, b->partials_dev, b->out_dev, ctx->stream, GNSSHIP_STAGE_ANCHORS);
         if (e != hipSuccess) return hip_fail(ctx, e, "launch_corr_batch(anchors)");
     }
-    if (b->n_jobs > 0 || prefetch) {
+    if (b->n_jobs > 0 || p1 || p2) {
         hipError_t e = launch_corr_batch(dev_samples, fmt, b->jobs_dev, b->n_jobs, b->chunks_dev, b->items_dev, b->n_jobs > 0 ? b->n_items : 0,
             b->classes, b->max_code_len, b->any_multi, b->anchors_dev, b->partials_dev, b->out_dev, ctx->stream, GNSSHIP_STAGE_CORRELATE,
-            prefetch ? &pf : nullptr);
+            (p1 || p2) ? &pf : nullptr);
         if (e != hipSuccess) return hip_fail(ctx, e, "launch_corr_batch(pipelined)");
     }
-    b->anchors_valid = b->n_jobs > 0;
-    if (prefetch) next->anchors_valid = true;
+    b->anchor_segs = b->n_jobs > 0 ? kAnchorSegments : 0;
+    if (p1) next->anchor_segs = kAnchorSegments;
+    if (p2) next2->anchor_segs = 1;
     return GNSSHIP_OK;
+}
+
+extern "C" int gnsship_batch_launch_pipelined(gnsship_batch* b, const void* dev_samples, int fmt, gnsship_batch* next)
+{
+    return gnsship_batch_launch_pipelined2(b, dev_samples, fmt, next, nullptr);
 }
 
 extern "C" int gnsship_batch_results(gnsship_batch* b, float* out)

@@ -210,11 +210,15 @@ class CorrelatorBatch:
     def launch_ptr(self, dev_ptr: int, fmt: int = FMT_CF32, stages: int = 3):
         check(self.ctx.lib.gnsship_batch_launch_stages(self.h, dev_ptr, fmt, stages), "gnsship_batch_launch_stages", self.ctx.h)
 
-    def launch_pipelined(self, dev_ptr: int, fmt: int = FMT_CF32, next_batch: "CorrelatorBatch" = None):
-        """Correlate this batch and replay `next_batch`'s anchors in the same launch
-        (gnsship_batch_launch_pipelined): alternate two batches A, B, A, B, ... on the context stream."""
+    def launch_pipelined(self, dev_ptr: int, fmt: int = FMT_CF32, next_batch: "CorrelatorBatch" = None,
+                         next2: "CorrelatorBatch" = None):
+        """Correlate this batch and, in the same launch, replay anchors of the batches after it
+        (gnsship_batch_launch_pipelined2): all of `next_batch`'s remaining replay and the first half
+        of `next2`'s.  Pairs alternate A, B, A, ...; rings of three A, B, C, A, ... (with next2)
+        carry half a replay chain per batch per launch."""
         nh = next_batch.h if next_batch is not None else None
-        check(self.ctx.lib.gnsship_batch_launch_pipelined(self.h, dev_ptr, fmt, nh), "gnsship_batch_launch_pipelined", self.ctx.h)
+        n2 = next2.h if next2 is not None else None
+        check(self.ctx.lib.gnsship_batch_launch_pipelined2(self.h, dev_ptr, fmt, nh, n2), "gnsship_batch_launch_pipelined2", self.ctx.h)
 
     def results(self) -> np.ndarray:
         out = np.zeros((self.n_jobs, 2 * MAX_TAPS), np.float32)

@@ -151,6 +151,11 @@ int gnsship_batch_launch_stages(gnsship_batch* b, const void* dev_samples, int f
  * from the previous launch that named it as `next` (or are computed first).  Do not mix with
  * gnsship_batch_launch_stages on the same batches. */
 int gnsship_batch_launch_pipelined(gnsship_batch* b, const void* dev_samples, int fmt, gnsship_batch* next);
+/* Three-batch ring form (A, B, C, A, ...): correlate b, finish the anchor replay of `next` and run
+ * the first half of `next2`'s (each job's replay chain split at its middle renormalisation block),
+ * so every launch carries half a replay chain per batch instead of a whole one.  next / next2 may
+ * be NULL; next2 == NULL is gnsship_batch_launch_pipelined. */
+int gnsship_batch_launch_pipelined2(gnsship_batch* b, const void* dev_samples, int fmt, gnsship_batch* next, gnsship_batch* next2);
 int gnsship_batch_results(gnsship_batch* b, float* out);
 /* Device pointer of the result array (n_jobs × GNSSHIP_MAX_TAPS complex<float>). */
 int gnsship_batch_results_device(gnsship_batch* b, void** dev_out);

@@ -217,3 +217,49 @@ def test_pipelined_pair_matches_plain_launches(ctx):
     A.close()
     B.close()
     dev.free()
+
+
+def test_pipelined_ring_of_three_split_replay(ctx):
+    """gnsship_batch_launch_pipelined2 over a ring A, B, C: each launch finishes the replay of the
+    next batch and runs the first half (up to each job's middle renormalisation block) of the one
+    after; the resumed second halves give bit-identical anchors, hence exactly the plain launch
+    results.  Covers odd block counts (3001-sample jobs: 12 blocks; 1 and 2 blocks), a set_jobs
+    between the two halves (full replay again) and invalid rings."""
+    fs = 4e6
+    sats = signals.random_sky(6, seed=51)
+    sig = signals.generate_if(fs, 4000 * 30, sats, seed=52)
+    dev = ctx.upload(sig)
+    for k, s in enumerate(sats):
+        ctx.set_code(k, s.code)
+    ja = np.concatenate([signals.truth_jobs(s, fs, 10, 4000, [-0.25, 0.0, 0.25], k) for k, s in enumerate(sats[:2])])
+    jb = np.concatenate([signals.truth_jobs(s, fs, 8, 3001, [-0.5, 0.0, 0.5], k + 2, first_epoch=5) for k, s in enumerate(sats[2:4])])
+    jc = np.concatenate([signals.truth_jobs(s, fs, 6, 4000, [0.0], k + 4, first_epoch=3) for k, s in enumerate(sats[4:])])
+    jc["n_samples"][::3] = 200   # one block
+    jc["n_samples"][1::3] = 300  # two blocks
+    sets = [ja, jb, jc]
+    batches = [engine.CorrelatorBatch(ctx, len(j)) for j in sets]
+    refs = []
+    for b, j in zip(batches, sets):
+        b.set_jobs(j, len(sig))
+        b.launch_ptr(dev.ptr)
+        refs.append(b.results())
+    for rnd in range(7):
+        k = rnd % 3
+        batches[k].launch_pipelined(dev.ptr, next_batch=batches[(k + 1) % 3], next2=batches[(k + 2) % 3])
+        assert np.array_equal(batches[k].results(), refs[k]), rnd
+    # C got its first half in the last launch (k = 0); new jobs for C discard it
+    jc2 = jc.copy()
+    jc2["rem_carrier_phase_rad"] += np.float32(0.4)
+    batches[2].set_jobs(jc2, len(sig))
+    batches[1].launch_pipelined(dev.ptr, next_batch=batches[2], next2=batches[0])
+    batches[2].launch_pipelined(dev.ptr, next_batch=batches[0], next2=batches[1])
+    ref = O.corr_batch(sig, jc2, [s.code for s in sats], n_threads=8)
+    got = batches[2].results()
+    for j in range(2, len(jc2), 3):  # the full-length jobs (the 1- and 2-block ones are checked bit-exactly above)
+        assert rel_err(got[j, :1], ref[j, :1]) <= TOL
+    for nb, n2 in ((batches[1], batches[1]), (batches[0], batches[1]), (batches[1], batches[0])):
+        with pytest.raises(abi.GnssHipError):
+            batches[0].launch_pipelined(dev.ptr, next_batch=nb, next2=n2)
+    for b in batches:
+        b.close()
+    dev.free()
