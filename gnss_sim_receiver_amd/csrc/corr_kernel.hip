@@ -29,6 +29,7 @@
 //  * phasor: exact at every renormalisation point (anchor replay); inside a block the only
 //    deviation from the reference is its own ≤255-step rounding walk (≈1e-6 rad).
 #include "engine.h"
+#include "nco_math.h"
 
 // Every product/sum on the parity path is rounded on its own, like the reference's generic C;
 // the few fused multiply-adds wanted are written explicitly (__fmaf_rn).
@@ -49,18 +50,6 @@ __device__ unsigned long long* g_corr_prof = nullptr;
     do {                      \
     } while (0)
 #endif
-
-__device__ __forceinline__ float2 cmul_rn(float ar, float ai, float br, float bi)
-{
-    return make_float2(__fsub_rn(__fmul_rn(ar, br), __fmul_rn(ai, bi)), __fadd_rn(__fmul_rn(ar, bi), __fmul_rn(ai, br)));
-}
-
-// std::abs(std::complex<float>) → glibc hypotf, which evaluates sqrt(x²+y²) in double and rounds once.
-__device__ __forceinline__ float hypotf_glibc(float x, float y)
-{
-    const double dx = x, dy = y;
-    return static_cast<float>(__dsqrt_rn(__dadd_rn(__dmul_rn(dx, dx), __dmul_rn(dy, dy))));
-}
 
 // First renormalisation block of replay segment seg of a job with nblk blocks (segments split at
 // the middle block; kAnchorSegments == 2).

@@ -134,6 +134,53 @@ hipError_t launch_corr_batch(const void* samples, int fmt, const DevJob* jobs, i
 int plan_chunks(std::vector<DevJob>& jobs, std::vector<ChunkDesc>& chunks, std::vector<WorkItem>& items, bool& any_multi, int64_t* n_anchors,
     ChunkClass* classes, int chunks_per_item, bool pair_by_code);
 
+// ---- High-dynamics correlator (Dll_Pll_Conf::high_dyn; corr_hd_kernel.hip) -------------------
+// Replaces volk_gnsssdr_32f_xn_high_dynamics_resampler_32f_xn_generic + volk_gnsssdr_32fc_32f_
+// high_dynamic_rotator_dot_prod_32fc_xn_generic, the pair Cpu_Multicorrelator_Real_Codes runs when
+// set_high_dynamics_resampler(true) (cpu_multicorrelator_real_codes.cc:75-100,116-119).
+struct HdJob {
+    int64_t sample_offset;
+    int32_t n_samples;
+    int32_t n_taps;
+    int32_t out_index;      // row of the output array
+    int32_t anchor_offset;  // ceil(n/256) Doppler-chain anchors
+    int32_t first_chunk, n_chunks;
+    float p0_re, p0_im;     // phase_offset_as_complex: the unnormalised start of the Doppler chain
+    float inc_re, inc_im;   // phase_inc
+    double dtheta;          // arg(phase_inc) in double
+    float log_mag_inc;      // log|phase_inc|
+    float rate_arg;         // Im clogf(phase_inc_rate) = atan2f(im, re): glibc cpowf's angle per n²
+    float rem_code, code_step, code_rate, shift0;
+    uint32_t shift_samples[kMaxTaps];  // tap t = tap 0 circularly shifted by this many samples
+    const float* code;
+    int32_t code_len;
+    int32_t pad;
+};
+struct HdChunk {
+    int32_t job, start, len, pad;
+};
+// Host-side plan of the high-dynamics jobs of a batch (or of one gnsship_corr_run).
+struct HdPlan {
+    std::vector<HdJob> jobs;
+    std::vector<HdChunk> chunks;
+    int64_t n_anchors = 0;
+    int max_code_len = 1;
+    HdJob* jobs_dev = nullptr;
+    HdChunk* chunks_dev = nullptr;
+    Anchor* anchors_dev = nullptr;
+    float* partials_dev = nullptr;
+    int job_cap = 0, chunk_cap = 0;
+    int64_t anchor_cap = 0;
+};
+// Derive one HdJob from a reference-style call; false when the arguments are outside what the
+// reference itself can run (taps, shifts that would make its memcpy lengths negative).
+bool derive_hd_job(const gnsship_corr_job& in, const float* code_dev, int code_len, int out_index, HdJob& out);
+// Chunks + anchor layout for plan.jobs; (re)allocates and uploads the device copies.
+hipError_t hd_plan_upload(HdPlan& plan, hipStream_t stream);
+void hd_plan_free(HdPlan& plan);
+// Doppler-chain anchors, per-chunk correlation, per-job reduction into out[out_index].
+hipError_t launch_corr_hd(const void* samples, int fmt, const HdPlan& plan, float* out, hipStream_t stream);
+
 }  // namespace gnsship
 
 struct gnsship_ctx {

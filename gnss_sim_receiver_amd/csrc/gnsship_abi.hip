@@ -395,10 +395,14 @@ struct gnsship_batch {
     // the context stream by launches that carried this batch as `next` / `next2` (0..kAnchorSegments);
     // cleared by set_jobs.
     int anchor_segs = 0;
+    // high-dynamics jobs (flags bit 0): correlated by corr_hd_kernel.hip after the main classes; their
+    // slots in the main plan are empty jobs
+    HdPlan hd;
 };
 
 static void batch_release(gnsship_batch* b)
 {
+    hd_plan_free(b->hd);
     void* ptrs[] = {b->jobs_dev, b->chunks_dev, b->items_dev, b->partials_dev, b->out_dev, b->anchors_dev};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
@@ -440,11 +444,25 @@ extern "C" int gnsship_batch_set_jobs(gnsship_batch* b, const gnsship_corr_job* 
     b->anchor_segs = 0;
     if (int rc = sync_code_table(ctx)) return rc;
     b->jobs_host.resize(n_jobs);
+    b->hd.jobs.clear();
     int max_len = 1;
     for (int j = 0; j < n_jobs; j++) {
         const gnsship_corr_job& in = jobs[j];
         if (in.code_id < 0 || in.code_id >= static_cast<int>(ctx->codes_host.size()) || !ctx->codes_host[in.code_id].ptr)
             return fail(ctx, GNSSHIP_E_INVAL, "gnsship_batch_set_jobs: job refers to an unset code id");
+        if (in.flags & ~1) return fail(ctx, GNSSHIP_E_INVAL, "gnsship_batch_set_jobs: unknown job flags");
+        if (in.flags & 1) {  // high-dynamics resampler/rotator: its own plan, an empty slot here
+            HdJob h;
+            if (!derive_hd_job(in, ctx->codes_host[in.code_id].ptr, ctx->codes_host[in.code_id].len, j, h))
+                return fail(ctx, GNSSHIP_E_INVAL, "gnsship_batch_set_jobs: invalid high-dynamics job (taps, length, offset or tap shifts)");
+            b->hd.jobs.push_back(h);
+            gnsship_corr_job empty = in;
+            empty.flags = 0;
+            empty.n_samples = 0;
+            derive_job(empty, ctx->codes_host[in.code_id].len, b->jobs_host[j]);
+            if (in.sample_offset + in.n_samples > n_buffer_samples) return fail(ctx, GNSSHIP_E_INVAL, "gnsship_batch_set_jobs: job reads past the sample buffer");
+            continue;
+        }
         if (!derive_job(in, ctx->codes_host[in.code_id].len, b->jobs_host[j]))
             return fail(ctx, GNSSHIP_E_INVAL, "gnsship_batch_set_jobs: invalid job (taps, length, offset or flags)");
         if (in.sample_offset + in.n_samples > n_buffer_samples) return fail(ctx, GNSSHIP_E_INVAL, "gnsship_batch_set_jobs: job reads past the sample buffer");
@@ -479,6 +497,7 @@ extern "C" int gnsship_batch_set_jobs(gnsship_batch* b, const gnsship_corr_job* 
         b->chunk_cap = b->n_chunks;
     }
     b->n_jobs = n_jobs;
+    HIP_TRY(ctx, hd_plan_upload(b->hd, ctx->stream));
     if (n_jobs) {
         HIP_TRY(ctx, hipMemcpyAsync(b->jobs_dev, b->jobs_host.data(), sizeof(DevJob) * n_jobs, hipMemcpyHostToDevice, ctx->stream));
         HIP_TRY(ctx, hipMemcpyAsync(b->chunks_dev, b->chunks_host.data(), sizeof(ChunkDesc) * b->n_chunks, hipMemcpyHostToDevice, ctx->stream));
@@ -513,6 +532,8 @@ extern "C" int gnsship_batch_launch_stages(gnsship_batch* b, const void* dev_sam
         hipError_t e = launch_corr_batch(dev_samples, fmt, b->jobs_dev, b->n_jobs, b->chunks_dev, b->items_dev, b->n_items, b->classes,
             b->max_code_len, b->any_multi, b->anchors_dev, b->partials_dev, b->out_dev, ctx->stream, GNSSHIP_STAGE_CORRELATE);
         if (e != hipSuccess) return hip_fail(ctx, e, "launch_corr_batch(correlate)");
+        e = launch_corr_hd(dev_samples, fmt, b->hd, b->out_dev, ctx->stream);
+        if (e != hipSuccess) return hip_fail(ctx, e, "launch_corr_hd");
         HIP_TRY(ctx, hipEventRecord(b->corr_done, ctx->stream));
     }
     return GNSSHIP_OK;
@@ -551,6 +572,10 @@ extern "C" int gnsship_batch_launch_pipelined2(gnsship_batch* b, const void* dev
             b->classes, b->max_code_len, b->any_multi, b->anchors_dev, b->partials_dev, b->out_dev, ctx->stream, GNSSHIP_STAGE_CORRELATE,
             (p1 || p2) ? &pf : nullptr);
         if (e != hipSuccess) return hip_fail(ctx, e, "launch_corr_batch(pipelined)");
+    }
+    if (b->n_jobs > 0) {
+        hipError_t e = launch_corr_hd(dev_samples, fmt, b->hd, b->out_dev, ctx->stream);
+        if (e != hipSuccess) return hip_fail(ctx, e, "launch_corr_hd");
     }
     b->anchor_segs = b->n_jobs > 0 ? kAnchorSegments : 0;
     if (p1) next->anchor_segs = kAnchorSegments;
@@ -611,6 +636,7 @@ struct gnsship_corr {
     float* out_dev = nullptr;
     Anchor* anchors_dev = nullptr;
     int chunk_cap = 0;
+    HdPlan hd;  // set_high_dynamics_resampler(true): the high-dynamics kernels
 };
 
 extern "C" int gnsship_corr_create(gnsship_ctx* ctx, int max_signal_length_samples, int n_correlators, gnsship_corr** out)
@@ -680,8 +706,6 @@ extern "C" int gnsship_corr_run(gnsship_corr* c, const void* sig, int fmt, int s
     if (!c->code_set) return fail(ctx, GNSSHIP_E_STATE, "gnsship_corr_run: set_local_code_and_taps not called");
     if (!sig || !corr_out || n < 0 || n > c->max_samples || fmt_bytes(fmt) == 0)
         return fail(ctx, GNSSHIP_E_INVAL, "gnsship_corr_run: bad arguments (length > max_signal_length_samples?)");
-    if (c->high_dyn && (phase_rate_step != 0.0f || code_rate_step != 0.0f))
-        return fail(ctx, GNSSHIP_E_INVAL, "gnsship_corr_run: high-dynamics resampler with nonzero rates is not supported on the device path");
     if (int rc = set_device(ctx)) return rc;
     gnsship_corr_job in{};
     in.sample_offset = 0;
@@ -696,6 +720,24 @@ extern "C" int gnsship_corr_run(gnsship_corr* c, const void* sig, int fmt, int s
     in.code_phase_step_chips = code_step;
     in.code_phase_rate_step_chips = code_rate_step;
     for (int t = 0; t < kMaxTaps; t++) in.shifts_chips[t] = t < c->n_taps ? c->shifts[t] : 0.0f;
+    const void* src = sig;
+    if (!sig_on_device) {
+        HIP_TRY(ctx, hipMemcpyAsync(c->sig_dev, sig, fmt_bytes(fmt) * static_cast<size_t>(n), hipMemcpyHostToDevice, ctx->stream));
+        src = c->sig_dev;
+    }
+    if (c->high_dyn) {  // cpu_multicorrelator_real_codes.cc:80-90,116-119
+        c->hd.jobs.resize(1);
+        if (!derive_hd_job(in, c->code_dev, c->code_len, 0, c->hd.jobs[0]))
+            return fail(ctx, GNSSHIP_E_INVAL, "gnsship_corr_run: invalid high-dynamics job (tap shifts beyond the signal length?)");
+        HIP_TRY(ctx, hd_plan_upload(c->hd, ctx->stream));
+        hipError_t e = launch_corr_hd(src, fmt, c->hd, c->out_dev, ctx->stream);
+        if (e != hipSuccess) return hip_fail(ctx, e, "launch_corr_hd");
+        float tmp[2 * kMaxTaps];
+        HIP_TRY(ctx, hipMemcpyAsync(tmp, c->out_dev, sizeof(tmp), hipMemcpyDeviceToHost, ctx->stream));
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+        std::memcpy(corr_out, tmp, sizeof(float) * 2 * c->n_taps);
+        return GNSSHIP_OK;
+    }
     std::vector<DevJob> jobs(1);
     if (!derive_job(in, c->code_len, jobs[0])) return fail(ctx, GNSSHIP_E_INVAL, "gnsship_corr_run: invalid job");
     std::vector<ChunkDesc> chunks;
@@ -705,11 +747,6 @@ extern "C" int gnsship_corr_run(gnsship_corr* c, const void* sig, int fmt, int s
     ChunkClass classes[kChunkClasses];
     const int nch = plan_chunks(jobs, chunks, items, multi, &n_anchors, classes, chunks_per_item_setting(), false);
     attach_codes(chunks, jobs, std::vector<CodeDesc>{CodeDesc{c->code_dev, c->code_len, 0}});
-    const void* src = sig;
-    if (!sig_on_device) {
-        HIP_TRY(ctx, hipMemcpyAsync(c->sig_dev, sig, fmt_bytes(fmt) * static_cast<size_t>(n), hipMemcpyHostToDevice, ctx->stream));
-        src = c->sig_dev;
-    }
     HIP_TRY(ctx, hipMemcpyAsync(c->job_dev, jobs.data(), sizeof(DevJob), hipMemcpyHostToDevice, ctx->stream));
     HIP_TRY(ctx, hipMemcpyAsync(c->chunks_dev, chunks.data(), sizeof(ChunkDesc) * nch, hipMemcpyHostToDevice, ctx->stream));
     HIP_TRY(ctx, hipMemcpyAsync(c->items_dev, items.data(), sizeof(WorkItem) * items.size(), hipMemcpyHostToDevice, ctx->stream));
@@ -729,6 +766,7 @@ extern "C" int gnsship_corr_destroy(gnsship_corr* c)
     (void)hipSetDevice(c->ctx->device);
     (void)hipStreamSynchronize(c->ctx->stream);
     (void)free_padded_code(c->code_dev);
+    hd_plan_free(c->hd);
     void* ptrs[] = {c->code_table_dev, c->sig_dev, c->job_dev, c->chunks_dev, c->items_dev, c->partials_dev, c->out_dev, c->anchors_dev};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);

@@ -279,9 +279,22 @@ static void orc_rotator_dot_prod_acc64(float* result, const float* in_common, fl
 /* volk_gnsssdr_32fc_32f_high_dynamic_rotator_dot_prod_32fc_xn_generic —
  *   volk_gnsssdr_32fc_32f_high_dynamic_rotator_dot_prod_32fc_xn.h:68-110 (non-Windows branch,
  *   cpowf; note (n*n) is unsigned int and wraps for n >= 65536, as in the reference). */
+static void orc_high_dynamic_rotator_dot_prod_impl(float* result, const float* in_common, float inc_re, float inc_im,
+    float rate_re, float rate_im, float* phase, const float* in_a, int num_a_vectors, unsigned int num_points, int accum_f64);
+
 void orc_high_dynamic_rotator_dot_prod_generic(float* result, const float* in_common, float inc_re, float inc_im,
     float rate_re, float rate_im, float* phase, const float* in_a, int num_a_vectors, unsigned int num_points)
 {
+    orc_high_dynamic_rotator_dot_prod_impl(result, in_common, inc_re, inc_im, rate_re, rate_im, phase, in_a, num_a_vectors, num_points, 0);
+}
+
+/* accum_f64 = 1: test-only variant, the same float products summed in double (as
+ * orc_rotator_dot_prod_acc64). */
+static void orc_high_dynamic_rotator_dot_prod_impl(float* result, const float* in_common, float inc_re, float inc_im,
+    float rate_re, float rate_im, float* phase, const float* in_a, int num_a_vectors, unsigned int num_points, int accum_f64)
+{
+    double acc64[2 * ORC_MAX_TAPS];
+    for (int t = 0; t < 2 * num_a_vectors; t++) acc64[t] = 0.0;
     float complex ph = phase[0] + phase[1] * I;
     float complex ph_doppler = ph;
     const float complex inc = inc_re + inc_im * I;
@@ -306,11 +319,16 @@ void orc_high_dynamic_rotator_dot_prod_generic(float* result, const float* in_co
         ph = qr + qi * I;
         for (int t = 0; t < num_a_vectors; t++) {
             const float c = in_a[(size_t)t * num_points + n];
-            acc[2 * t] += tr * c;
-            acc[2 * t + 1] += ti * c;
+            if (accum_f64) {
+                acc64[2 * t] += (double)(tr * c);
+                acc64[2 * t + 1] += (double)(ti * c);
+            } else {
+                acc[2 * t] += tr * c;
+                acc[2 * t + 1] += ti * c;
+            }
         }
     }
-    for (int t = 0; t < 2 * num_a_vectors; t++) result[t] = acc[t];
+    for (int t = 0; t < 2 * num_a_vectors; t++) result[t] = accum_f64 ? (float)acc64[t] : acc[t];
     phase[0] = crealf(ph);
     phase[1] = cimagf(ph);
 }
@@ -339,8 +357,14 @@ static int orc_multicorrelator_impl(float* corr_out, const float* sig_in, const 
     float phase_rate_step_rad, float rem_code_phase_chips, float code_phase_step_chips, float code_phase_rate_step_chips,
     int signal_length_samples, float* scratch, int accum_f64)
 {
-    if (accum_f64 && high_dyn) return -1;
     if (n_correlators < 1 || n_correlators > ORC_MAX_TAPS || signal_length_samples < 0) return -1;
+    if (high_dyn) { /* the reference's memcpy lengths go negative outside [0, N]: refused, not run */
+        unsigned int s = 0;
+        for (int t = 1; t < n_correlators; t++) {
+            s += (int)round((shifts_chips[t] - shifts_chips[t - 1]) / code_phase_step_chips);
+            if (s > (unsigned int)signal_length_samples) return -1;
+        }
+    }
     float* codes = scratch;
     int own = 0;
     if (!codes) {
@@ -358,8 +382,8 @@ static int orc_multicorrelator_impl(float* corr_out, const float* sig_in, const 
     const float inc_re = cosf(-phase_step_rad), inc_im = sinf(-phase_step_rad);
     if (high_dyn) {
         const float rr = cosf(-phase_rate_step_rad), ri = sinf(-phase_rate_step_rad);
-        orc_high_dynamic_rotator_dot_prod_generic(corr_out, sig_in, inc_re, inc_im, rr, ri, phase, codes, n_correlators,
-            (unsigned)signal_length_samples);
+        orc_high_dynamic_rotator_dot_prod_impl(corr_out, sig_in, inc_re, inc_im, rr, ri, phase, codes, n_correlators,
+            (unsigned)signal_length_samples, accum_f64);
     } else if (accum_f64) {
         orc_rotator_dot_prod_acc64(corr_out, sig_in, inc_re, inc_im, phase, codes, n_correlators, (unsigned)signal_length_samples);
     } else {

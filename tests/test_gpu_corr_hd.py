@@ -1,0 +1,139 @@
+"""High-dynamics multicorrelator parity on the GPU (corr_hd_kernel.hip) vs the oracle.
+
+The path Cpu_Multicorrelator_Real_Codes takes after set_high_dynamics_resampler(true)
+(cpu_multicorrelator_real_codes.cc:75-100,116-119): the high-dynamics resampler (tap 0 with the
+code-rate term, taps 1.. circular shifts of tap 0 — …_high_dynamics_resampler_32f_xn.h:67-91) and the
+high-dynamics rotator (Doppler chain × cpowf rate phasor — …_high_dynamic_rotator_dot_prod_32fc_xn.h:
+68-110).  The oracle's resampler is pinned bit-for-bit to the reference's own header compiled into
+oracle/_ref (tests/test_oracle.py); the rotator header needs the Mako-generated volk_gnsssdr.h, so its
+restatement (oracle/gnss_oracle.c, glibc cpowf) is pinned by the source only.
+
+Contract: per tap |out − ref| / |ref| ≤ 1e-5, as the standard path.  At N ≥ 65536 (n·n wraps, as in the
+reference) the reference's serial float sum itself drifts ~1e-5, so those jobs are held to 1e-5
+against the oracle's double-accumulation variant (same float products), as tests/test_gpu_e1.py.
+"""
+import numpy as np
+import pytest
+
+from gnss_sim_receiver_amd import abi, engine, signals
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-5
+
+
+def rel_err(out, ref):
+    return np.max(np.abs(out - ref) / np.maximum(np.abs(ref), 1e-30))
+
+
+def hd_jobs(sats, fs, n_ep, vl, shifts, carr_rate, code_rate, seed):
+    rng = np.random.default_rng(seed)
+    jobs = np.concatenate([signals.truth_jobs(s, fs, n_ep, vl, shifts, k) for k, s in enumerate(sats)])
+    jobs["flags"] = 1
+    jobs["phase_rate_step_rad"] = (carr_rate * rng.uniform(-1, 1, len(jobs))).astype(np.float32)
+    jobs["code_phase_rate_step_chips"] = (code_rate * rng.uniform(-1, 1, len(jobs))).astype(np.float32)
+    jobs["rem_carrier_phase_rad"] += rng.uniform(-0.3, 0.3, len(jobs)).astype(np.float32)
+    return jobs
+
+
+@pytest.mark.parametrize("fs,ntaps,system,fmt", [(4e6, 3, "GPS", "cf32"), (25e6, 5, "GPS", "cf32"), (4e6, 1, "GPS", "cf32"),
+                                                 (50e6, 3, "BDS", "ci8"), (4e6, 3, "GPS", "ci16")])
+def test_hd_batch_vs_oracle(ctx, fs, ntaps, system, fmt):
+    sats = signals.random_sky(4, seed=int(fs) % 7919 + ntaps, system=system)
+    vl = int(round(fs / 1000))
+    n_ep = 2
+    sig = signals.generate_if(fs, vl * (n_ep + 3), sats, seed=ntaps + 1)
+    shifts = {1: [0.0], 3: [-0.25, 0.0, 0.25], 5: [-0.5, -0.25, 0.0, 0.25, 0.5]}[ntaps]
+    # carrier rate up to ~1e-9 rad/sample² (θ up to ~0.6 rad over the epoch), code rate to 1e-10
+    jobs = hd_jobs(sats, fs, n_ep, vl, shifts, 4e-9 * (4e6 / fs) ** 2 * 10, 1e-10, int(fs) + ntaps)
+    cl = [s.code for s in sats]
+    raw = sig if fmt == "cf32" else (signals.to_ibyte(sig) if fmt == "ci8" else signals.to_ishort(sig))
+    as_float = sig if fmt == "cf32" else raw.astype(np.float32).view(np.complex64)
+    out = engine.correlate_host(ctx, raw, jobs, cl)
+    ref = O.corr_batch(as_float, jobs, cl, n_threads=8)
+    for j in range(len(jobs)):
+        t = jobs[j]["n_taps"]
+        e = rel_err(out[j, :t], ref[j, :t])
+        assert e <= TOL, (j, e, out[j, :t], ref[j, :t])
+        assert np.all(out[j, t:] == 0)
+
+
+def test_hd_mixed_with_standard_jobs(ctx):
+    """High-dynamics and standard jobs in one batch: each follows its own reference kernel pair."""
+    fs, vl = 4e6, 4000
+    sats = signals.random_sky(6, seed=77)
+    sig = signals.generate_if(fs, vl * 6, sats, seed=78)
+    jobs = np.concatenate([signals.truth_jobs(s, fs, 3, vl, [-0.25, 0.0, 0.25], k) for k, s in enumerate(sats)])
+    jobs["flags"][::2] = 1
+    jobs["phase_rate_step_rad"][::2] = np.float32(3e-10)
+    jobs["code_phase_rate_step_chips"][1::4] = np.float32(2e-11)  # ignored by the standard resampler
+    cl = [s.code for s in sats]
+    out = engine.correlate_host(ctx, sig, jobs, cl)
+    ref = O.corr_batch(sig, jobs, cl, n_threads=8)
+    assert rel_err(out[:, :3], ref[:, :3]) <= TOL
+    # the two kernel pairs differ on the same NCO (taps 1.. are whole-sample shifts of tap 0)
+    std = jobs.copy()
+    std["flags"] = 0
+    ref_std = O.corr_batch(sig, std, cl)
+    assert np.max(np.abs(ref_std[::2, 0] - ref[::2, 0])) > 0 or np.max(np.abs(ref_std[::2, 2] - ref[::2, 2])) > 0
+
+
+def test_hd_channel_handle_zero_rates(ctx):
+    """Per-channel mirror: set_high_dynamics_resampler(true) switches kernels even at zero rates."""
+    fs, vl = 4e6, 4000
+    s = signals.random_sky(1, seed=5)[0]
+    sig = signals.generate_if(fs, 3 * vl, [s], seed=6)
+    job = signals.truth_jobs(s, fs, 1, vl, [-0.25, 0.0, 0.25], 0)[0]
+    x = sig[job["sample_offset"]: job["sample_offset"] + vl]
+    sh = np.array([-0.25, 0.0, 0.25], np.float32)
+    args = (float(job["rem_carrier_phase_rad"]), float(job["phase_step_rad"]), float(job["rem_code_phase_chips"]),
+            float(job["code_phase_step_chips"]))
+    for rates in [(0.0, 0.0), (2e-10, 5e-11)]:
+        mc = engine.MultiCorrelatorRealCodes(ctx)
+        mc.init(vl, 3)
+        mc.set_high_dynamics_resampler(True)
+        mc.set_local_code_and_taps(1023, s.code, sh)
+        out = np.zeros(3, np.complex64)
+        mc.set_input_output_vectors(out, x)
+        mc.Carrier_wipeoff_multicorrelator_resampler(args[0], args[1], rates[0], args[2], args[3], rates[1], vl)
+        mc.free()
+        ref = O.multicorrelator(x, s.code, sh, args[0], args[1], args[2], args[3], n=vl, carr_rate=rates[0], code_rate=rates[1],
+                                high_dyn=True)
+        assert rel_err(out, ref) <= TOL, rates
+
+
+def test_hd_long_integration_index_wrap(ctx):
+    """N = 70000 > 65536: the reference's (float)(n*n) wraps in 32-bit unsigned, in the resampler and
+    in the rotator alike; the device wraps the same way."""
+    fs, n = 25e6, 70000
+    sats = signals.random_sky(2, seed=31)
+    sig = signals.generate_if(fs, n + 60000, sats, seed=32)
+    jobs = np.concatenate([signals.truth_jobs(s, fs, 1, n, [-0.5, 0.0, 0.5], k) for k, s in enumerate(sats)])
+    jobs["flags"] = 1
+    jobs["phase_rate_step_rad"] = np.float32(1e-6)      # cosf → 1.0f: |rate| = 1 to 5e-13, finite cpowf
+    jobs["code_phase_rate_step_chips"] = np.float32(3e-13)
+    cl = [s.code for s in sats]
+    out = engine.correlate_host(ctx, sig, jobs, cl)
+    ref64 = O.corr_batch(sig, jobs, cl, accum_f64=True)
+    assert np.all(np.isfinite(ref64[:, :3]))
+    xn = np.linalg.norm(sig[:n].astype(np.complex128))
+    e = np.max(np.abs(out[:, :3] - ref64[:, :3]) / np.maximum(np.abs(ref64[:, :3]), xn * 1e-3))
+    assert e <= TOL, e
+
+
+def test_hd_invalid_tap_shifts_rejected(ctx):
+    """Decreasing shifts make the reference's memcpy lengths negative: refused with E_INVAL."""
+    code = np.ones(1023, np.float32)
+    ctx.set_code(0, code)
+    j = np.zeros(1, abi.JOB_DTYPE)
+    j["n_samples"], j["n_taps"], j["flags"] = 4000, 3, 1
+    j["code_phase_step_chips"] = 0.25575
+    j["shifts_chips"][0, :3] = [0.25, 0.0, -0.25]
+    b = engine.CorrelatorBatch(ctx, 1)
+    with pytest.raises(abi.GnssHipError):
+        b.set_jobs(j, 8000)
+    j["shifts_chips"][0, :3] = [-0.25, 0.0, 0.25]
+    j["flags"] = 2
+    with pytest.raises(abi.GnssHipError):
+        b.set_jobs(j, 8000)
+    b.close()

@@ -112,6 +112,28 @@ def test_oracle_vs_reference_build_random(built):
         assert (o == O.resampler(code, rem, step, sh, n)).all(), trial
 
 
+@pytest.mark.skipif(not os.path.exists(REF_SO), reason="oracle/_ref not built (needs /root/reference)")
+def test_oracle_hd_resampler_vs_reference_build_random(built):
+    """High-dynamics resampler (…_high_dynamics_resampler_32f_xn.h:67-91): rate term with the
+    32-bit unsigned n·n (lengths past 65536 included), taps 1.. as circular shifts of tap 0."""
+    R = ctypes.CDLL(REF_SO)
+    R.ref_high_dynamics_resampler_generic.argtypes = [f32p, f32p, ctypes.c_float, ctypes.c_float, ctypes.c_float, f32p, ctypes.c_uint,
+                                                      ctypes.c_int, ctypes.c_uint]
+    rng = np.random.default_rng(6)
+    for trial in range(30):
+        L = [1023, 2046, 8184][trial % 3]
+        code = np.where(rng.random(L) > 0.5, 1.0, -1.0).astype(np.float32)
+        n = int(rng.integers(1000, 80000))
+        step = np.float32(rng.uniform(0.05, 1.5))
+        sh = np.sort(rng.uniform(-2, 2, int(rng.integers(1, 6)))).astype(np.float32)
+        rem = np.float32(rng.uniform(-3 * L, 3 * L))
+        rate = np.float32(rng.uniform(-1e-9, 1e-9))
+        o = np.zeros((len(sh), n), np.float32)
+        R.ref_high_dynamics_resampler_generic(o.ctypes.data_as(f32p), code.ctypes.data_as(f32p), rem, step, rate,
+                                              sh.ctypes.data_as(f32p), L, len(sh), n)
+        assert (o == O.resampler(code, rem, step, sh, n, high_dyn_rate=rate)).all(), trial
+
+
 def test_oracle_f64_accumulation_variant():
     """accum_f64 keeps the reference's float products and only changes the sum: equal to the
     serial generic sum within float rounding at N = 4000, and the serial sum's drift at 1e5 stays
