@@ -2,6 +2,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <algorithm>
 #include <new>
 #include <vector>
 
@@ -33,17 +34,32 @@ bool make_fft_plan(int n, FftPlan& plan)
 // Transform layout for size n: the single-pass LDS transform when it fits, else the four-step
 // N = P·M (smallest supported P with M = N/P ≤ 1024 and M {2,3,5}-smooth).  force_big selects the
 // four-step at sizes the LDS transform also covers (test knob GNSSHIP_ACQ_FORCE_BIG=1).
-bool choose_acq_layout(int n, bool force_big, FftPlan& plan, int& P)
+// Beyond that (or when no such P exists) the huge layout: N = P·M with P ∈ {4,…,32} register
+// points and M ≤ 16384 LDS rows, as separate kernels (smallest P first: the longest LDS rows).
+// force: 1 = four-step, 2 = huge, at sizes a smaller layout also covers (test knobs
+// GNSSHIP_ACQ_FORCE_BIG=1 / GNSSHIP_ACQ_FORCE_HUGE=1).
+bool choose_acq_layout(int n, int force, FftPlan& plan, int& P, bool& huge)
 {
     P = 0;
-    if (!force_big && make_fft_plan(n, plan)) return true;
-    if (n < 2 || n > kMaxAcqBigN) return false;
-    for (int p = 16; p <= 32; p++) {
-        if (!big_p_supported(p) || n % p != 0) continue;
-        const int m = n / p;
-        if (m > kAcqThreads || m < 2) continue;
-        if (make_fft_plan(m, plan)) {
+    huge = false;
+    if (force == 0 && make_fft_plan(n, plan)) return true;
+    if (force != 2 && n >= 2 && n <= kMaxAcqBigN) {
+        for (int p = 16; p <= 32; p++) {
+            if (!big_p_supported(p) || n % p != 0) continue;
+            const int m = n / p;
+            if (m > kAcqThreads || m < 2) continue;
+            if (make_fft_plan(m, plan)) {
+                P = p;
+                return true;
+            }
+        }
+    }
+    if (n < 8 || n > kMaxAcqHugeN) return false;
+    for (int p = 4; p <= 32; p++) {
+        if (!huge_p_supported(p) || n % p != 0) continue;
+        if (make_fft_plan(n / p, plan)) {
             P = p;
+            huge = true;
             return true;
         }
     }
@@ -63,7 +79,14 @@ struct gnsship_acq {
     gnsship_ctx* ctx = nullptr;
     gnsship_acq_conf conf{};
     FftPlan plan{};              // whole transform (P == 0) or the M-point row transform (P > 0)
-    int P = 0;                   // four-step register points; spectra are then stored transposed
+    int P = 0;                   // four-step / huge register points; spectra are then stored transposed
+    bool huge = false;           // huge layout (separate column and row kernels)
+    float2* twM = nullptr;       // huge: M twiddles exp(-2πi t/M) of the row transform
+    float2* T = nullptr;         // huge: forward column-stage scratch, n_bins × N
+    float2* U = nullptr;         // huge: inverse row-stage scratch, prn_batch × n_bins × N
+    float* grid_scratch = nullptr; // huge without a kept grid: prn_batch × n_bins × N
+    TileStat* tiles = nullptr;   // huge: prn_batch × n_bins × huge_tiles(M)
+    int prn_batch = 0;
     int n_bins = 0;
     int dwell_count = 0;
     float2* tw = nullptr;        // N twiddles exp(-2πi t/N)
@@ -80,6 +103,14 @@ struct gnsship_acq {
 
 static void acq_free_grid_buffers(gnsship_acq* a)
 {
+    void* hp[] = {a->T, a->U, a->grid_scratch, a->tiles};
+    for (void* p : hp)
+        if (p) (void)hipFree(p);
+    a->T = nullptr;
+    a->U = nullptr;
+    a->grid_scratch = nullptr;
+    a->tiles = nullptr;
+    a->prn_batch = 0;
     if (a->wipe) (void)hipFree(a->wipe);
     if (a->X) (void)hipFree(a->X);
     if (a->rowstat) (void)hipFree(a->rowstat);
@@ -97,7 +128,7 @@ extern "C" int gnsship_acq_destroy(gnsship_acq* a)
     (void)hipSetDevice(a->ctx->device);
     (void)hipStreamSynchronize(a->ctx->stream);
     acq_free_grid_buffers(a);
-    void* ptrs[] = {a->tw, a->codes_fft, a->res_dev, a->sig_dev};
+    void* ptrs[] = {a->tw, a->twM, a->codes_fft, a->res_dev, a->sig_dev};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     delete a;
@@ -123,6 +154,17 @@ extern "C" int gnsship_acq_set_grid(gnsship_acq* a, int doppler_max, int doppler
         HIP_TRY(ctx, hipMalloc(&a->X, sizeof(float2) * static_cast<size_t>(nb) * N));
         HIP_TRY(ctx, hipMalloc(&a->rowstat, sizeof(RowStat) * static_cast<size_t>(nb) * a->conf.max_prns));
         a->n_bins = nb;
+        if (a->huge) {
+            // PRNs searched per round: the inverse row-stage scratch held to ~256 MiB
+            const size_t cell = static_cast<size_t>(nb) * N * sizeof(float2);
+            int pb = static_cast<int>((size_t(256) << 20) / cell);
+            a->prn_batch = pb < 1 ? 1 : (pb > a->conf.max_prns ? a->conf.max_prns : pb);
+            const size_t tiles = static_cast<size_t>(a->prn_batch) * nb * huge_tiles(a->plan.n);
+            HIP_TRY(ctx, hipMalloc(&a->T, sizeof(float2) * static_cast<size_t>(nb) * N));
+            HIP_TRY(ctx, hipMalloc(&a->U, cell * a->prn_batch));
+            HIP_TRY(ctx, hipMalloc(&a->grid_scratch, sizeof(float) * static_cast<size_t>(nb) * N * a->prn_batch));
+            HIP_TRY(ctx, hipMalloc(&a->tiles, sizeof(TileStat) * tiles));
+        }
     }
     std::vector<float2> host(static_cast<size_t>(nb) * N);
     const float two_pi = static_cast<float>(2.0 * M_PI);
@@ -151,10 +193,13 @@ extern "C" int gnsship_acq_create(gnsship_ctx* ctx, const gnsship_acq_conf* conf
     *out = nullptr;
     FftPlan plan;
     int P = 0;
+    bool huge = false;
     const char* fb = std::getenv("GNSSHIP_ACQ_FORCE_BIG");
-    if (!choose_acq_layout(conf->fft_size, fb && fb[0] == '1', plan, P))
+    const char* fh = std::getenv("GNSSHIP_ACQ_FORCE_HUGE");
+    const int force = (fh && fh[0] == '1') ? 2 : ((fb && fb[0] == '1') ? 1 : 0);
+    if (!choose_acq_layout(conf->fft_size, force, plan, P, huge))
         return fail(ctx, GNSSHIP_E_INVAL,
-            "gnsship_acq_create: fft_size must be 2^a 3^b 5^c, and either <= 16384 or P*M with P in {16..32}, M <= 1024 (max 32768)");
+            "gnsship_acq_create: fft_size must be 2^a 3^b 5^c: <= 16384, or P*M (P in {16..32}, M <= 1024), or P*M (P in {4..32}, M <= 16384), max 524288");
     if (conf->fs_in <= 0 || conf->max_prns < 1 || conf->max_dwells < 1 || conf->samples_per_chip < 0 || conf->samples_per_code <= 0.0f)
         return fail(ctx, GNSSHIP_E_INVAL, "gnsship_acq_create: bad configuration");
     HIP_TRY(ctx, hipSetDevice(ctx->device));
@@ -164,6 +209,7 @@ extern "C" int gnsship_acq_create(gnsship_ctx* ctx, const gnsship_acq_conf* conf
     a->conf = *conf;
     a->plan = plan;
     a->P = P;
+    a->huge = huge;
     a->code_set.assign(conf->max_prns, 0);
     const int N = conf->fft_size;
     std::vector<float2> tw(N);
@@ -174,6 +220,16 @@ extern "C" int gnsship_acq_create(gnsship_ctx* ctx, const gnsship_acq_conf* conf
     hipError_t e = hipMalloc(&a->tw, sizeof(float2) * N);
     if (e == hipSuccess) e = hipMemcpy(a->tw, tw.data(), sizeof(float2) * N, hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMalloc(&a->codes_fft, sizeof(float2) * static_cast<size_t>(N) * conf->max_prns);
+    if (e == hipSuccess && huge) {
+        const int M = plan.n;
+        std::vector<float2> twm(M);
+        for (int t = 0; t < M; t++) {
+            const double ang = -2.0 * M_PI * static_cast<double>(t) / static_cast<double>(M);
+            twm[t] = make_float2(static_cast<float>(std::cos(ang)), static_cast<float>(std::sin(ang)));
+        }
+        e = hipMalloc(&a->twM, sizeof(float2) * M);
+        if (e == hipSuccess) e = hipMemcpy(a->twM, twm.data(), sizeof(float2) * M, hipMemcpyHostToDevice);
+    }
     if (e == hipSuccess) e = hipMalloc(&a->res_dev, sizeof(gnsship_acq_result) * conf->max_prns);
     if (e == hipSuccess) e = hipMalloc(&a->sig_dev, sizeof(float2) * static_cast<size_t>(N));
     if (e != hipSuccess) {
@@ -206,7 +262,9 @@ extern "C" int gnsship_acq_set_local_code(gnsship_acq* a, int prn_slot, const fl
     const int N = a->conf.fft_size;
     HIP_TRY(ctx, hipMemcpyAsync(a->sig_dev, code, sizeof(float2) * N, hipMemcpyHostToDevice, ctx->stream));
     float2* dst = a->codes_fft + static_cast<size_t>(prn_slot) * N;
-    if (a->P)
+    if (a->huge)
+        HIP_TRY(ctx, launch_acq_fft_huge(a->sig_dev, GNSSHIP_FMT_CF32, nullptr, 1, a->P, a->plan, a->tw, a->twM, a->T, dst, 1, ctx->stream));
+    else if (a->P)
         HIP_TRY(ctx, launch_acq_fft_big(a->sig_dev, GNSSHIP_FMT_CF32, nullptr, 1, a->P, a->plan, a->tw, dst, 1, ctx->stream));
     else
         HIP_TRY(ctx, launch_acq_fft_rows(a->sig_dev, GNSSHIP_FMT_CF32, nullptr, 1, a->plan, a->tw, dst, 1, ctx->stream));
@@ -245,7 +303,15 @@ extern "C" int gnsship_acq_run(gnsship_acq* a, const void* sig, int fmt, int sig
     if (a->dwell_count >= a->conf.max_dwells) a->dwell_count = 0;
     const int accumulate = (a->conf.max_dwells > 1 && a->dwell_count > 0) ? 1 : 0;
     a->dwell_count++;
-    if (a->P) {
+    if (a->huge) {
+        HIP_TRY(ctx, launch_acq_fft_huge(src, fmt, a->wipe, a->n_bins, a->P, a->plan, a->tw, a->twM, a->T, a->X, 0, ctx->stream));
+        for (int p0 = 0; p0 < n_prns; p0 += a->prn_batch) {
+            const int np = std::min(a->prn_batch, n_prns - p0);
+            float* g = keep_grid ? a->grid_dev + static_cast<size_t>(p0) * a->n_bins * N : a->grid_scratch;
+            HIP_TRY(ctx, launch_acq_search_huge(a->X, a->codes_fft, p0, np, a->n_bins, a->P, a->plan, a->tw, a->twM, a->U, g,
+                             keep_grid ? accumulate : 0, a->tiles, a->conf.samples_per_chip, a->rowstat, ctx->stream));
+        }
+    } else if (a->P) {
         HIP_TRY(ctx, launch_acq_fft_big(src, fmt, a->wipe, a->n_bins, a->P, a->plan, a->tw, a->X, 0, ctx->stream));
         HIP_TRY(ctx, launch_acq_search_big(a->X, a->codes_fft, n_prns, a->n_bins, a->P, a->plan, a->tw, a->conf.samples_per_chip, accumulate,
                          a->rowstat, keep_grid ? a->grid_dev : nullptr, ctx->stream));

@@ -39,6 +39,25 @@ hipError_t launch_acq_fft_big(const void* sig, int fmt, const float2* mult, int 
     float2* rowsT, int conj_out, hipStream_t stream);
 hipError_t launch_acq_search_big(const float2* XT, const float2* codesT, int n_prns, int n_bins, int P, const FftPlan& row_plan,
     const float2* tw, int samples_per_chip, int accumulate, RowStat* rowstat, float* grid, hipStream_t stream);
+// Huge transforms (N > kMaxAcqBigN): N = P·M, P ∈ {4,5,8,10,16,20,25,32} register points per
+// column, M ≤ kMaxAcqN LDS rows, column and row stages as separate kernels through HBM.
+constexpr int kMaxAcqHugeN = 32 * kMaxAcqN;
+struct TileStat {  // one column tile of one |IFFT|² row
+    float max;
+    int32_t argmax;
+    float sum;
+    int32_t pad;
+};
+bool huge_p_supported(int P);
+constexpr int huge_tiles(int M) { return (M + 255) / 256; }
+// rowsT[b] = transposed FFT(sig ⊙ mult[b]) for b < n_rows; scratch: n_rows × N complex.
+hipError_t launch_acq_fft_huge(const void* sig, int fmt, const float2* mult, int n_rows, int P, const FftPlan& row_plan, const float2* twN,
+    const float2* twM, float2* scratch, float2* rowsT, int conj_out, hipStream_t stream);
+// PRN slots [prn_offset, prn_offset + n_prns): U scratch n_prns × n_bins × N complex, grid rows
+// (n_prns × n_bins × N floats, relative to prn_offset), tiles n_prns × n_bins × huge_tiles(M).
+hipError_t launch_acq_search_huge(const float2* XT, const float2* codesT, int prn_offset, int n_prns, int n_bins, int P, const FftPlan& row_plan,
+    const float2* twN, const float2* twM, float2* U, float* grid, int accumulate, TileStat* tiles, int samples_per_chip, RowStat* rowstat,
+    hipStream_t stream);
 hipError_t launch_acq_decide(const RowStat* rowstat, int n_prns, int n_bins, int N, int doppler_max, int doppler_step, int doppler_center,
     int dwells, int use_cfar, float samples_per_code, gnsship_acq_result* out, hipStream_t stream);
 

@@ -574,6 +574,213 @@ __global__ void acq_decide_kernel(const RowStat* __restrict__ rowstat, int n_prn
     out[p] = r;
 }
 
+// ---------------------------------------------------------------------------------------------
+// Huge transforms (N > 32768: Galileo E1 at 25 Msps, N = 100000; 1 ms GPS/B1I at 50 Msps,
+// N = 50000; E1 at 50 Msps, N = 200000): N = P·M with the M-point rows LDS-resident
+// (M ≤ 16384) and P ≤ 32 register points per column, the two stages as separate kernels through
+// HBM (the spectrum of one bin is 8N bytes, far beyond one workgroup's LDS):
+//   forward:  huge_cols_fwd  T[kq·M + m] = W_N^{m·kq} Σ_q x[m + M·q] W_P^{q·kq}     (registers)
+//             huge_rows      XT[kq·M + k] = Σ_m T[kq·M + m] W_M^{m·k}                 (LDS rows)
+//             → the same TRANSPOSED layout as the four-step above: XT[kq·M + k] = X[kq + P·k]
+//   inverse:  huge_rows      U[kq·M + m] = Σ_k (XT ⊙ CT)[kq·M + k] W_M^{−m·k}          (LDS rows)
+//             huge_cols_inv  y[m + M·q] = Σ_kq W_P^{−q·kq} W_N^{−m·kq} U[kq·M + m]   (registers)
+//             |y|² into the grid row + per-tile max/argmax/sum, then huge_finalize per row:
+//             the reference's first-index maximum, the row sum and the second peak outside
+//             ±samples_per_chip (pcps_acquisition.cc:496-597).
+// ---------------------------------------------------------------------------------------------
+constexpr int kHugeColThreads = 256;
+
+template <int FMT, int P>
+__global__ __launch_bounds__(kHugeColThreads) void acq_huge_cols_fwd_kernel(const void* __restrict__ sig, const float2* __restrict__ mult,
+    int M, const float2* __restrict__ twN, float2* __restrict__ T)
+{
+    const int m = blockIdx.x * kHugeColThreads + threadIdx.x;
+    const int b = blockIdx.y;
+    const int N = P * M;
+    if (m >= M) return;
+    const float2* w = mult ? mult + static_cast<int64_t>(b) * N : nullptr;
+    float2 v[P];
+#pragma unroll
+    for (int q = 0; q < P; q++) {
+        float2 x = load_if<FMT>(sig, m + M * q);
+        if (w) x = cmulf(x, w[m + M * q]);  // volk_32fc_x2_multiply_32fc(in, wipeoff)
+        v[q] = x;
+    }
+    dft_reg<P, 1, -1>(v, twN, N);
+    float2* out = T + static_cast<int64_t>(b) * N + m;
+#pragma unroll
+    for (int kq = 0; kq < P; kq++) out[kq * M] = kq ? cmulf(v[kq], twN[m * kq]) : v[kq];  // W_N^{m·kq}, m·kq < N
+}
+
+// One LDS-resident M-point transform per block: row blockIdx.x of cell (blockIdx.y, blockIdx.z).
+// src row = A + y·a_sy + z·a_sz + x·M (times B + z·b_sz + y·b_sy + x·M when B is given);
+// dst row = D + y·d_sy + z·d_sz + x·M.  conj_out stores the conjugate (the code spectrum).
+template <int SIGN>
+__global__ __launch_bounds__(kAcqThreads) void acq_huge_rows_kernel(const float2* __restrict__ A, int64_t a_sy, int64_t a_sz,
+    const float2* __restrict__ B, int64_t b_sy, int64_t b_sz, float2* __restrict__ D, int64_t d_sy, int64_t d_sz, FftPlan plan,
+    const float2* __restrict__ twM, int conj_out)
+{
+    extern __shared__ __attribute__((aligned(16))) float2 lds[];
+    const int M = plan.n;
+    const int64_t row = static_cast<int64_t>(blockIdx.x) * M;
+    const float2* a = A + blockIdx.y * a_sy + blockIdx.z * a_sz + row;
+    const float2* bb = B ? B + blockIdx.y * b_sy + blockIdx.z * b_sz + row : nullptr;
+    for (int i = threadIdx.x; i < M; i += kAcqThreads) lds[i] = bb ? cmulf(a[i], bb[i]) : a[i];  // ×conj(code FFT)
+    __syncthreads();
+    fft_lds<SIGN>(lds, plan, twM);
+    float2* d = D + blockIdx.y * d_sy + blockIdx.z * d_sz + row;
+    for (int i = threadIdx.x; i < M; i += kAcqThreads) {
+        float2 y = lds[i];
+        if (conj_out) y.y = -y.y;
+        d[i] = y;
+    }
+}
+
+// Inverse column stage + |y|² for cell (prn blockIdx.z, bin blockIdx.y): grid row
+// g = grid + (z·n_bins + y)·N (accumulated over dwells when `accumulate`), tile statistics.
+template <int P>
+__global__ __launch_bounds__(kHugeColThreads) void acq_huge_cols_inv_kernel(const float2* __restrict__ U, int M, int n_bins,
+    const float2* __restrict__ twN, float* __restrict__ grid, int accumulate, TileStat* __restrict__ tiles)
+{
+    __shared__ MaxIdx red_m[kHugeColThreads / 64];
+    __shared__ float red_s[kHugeColThreads / 64];
+    const int m = blockIdx.x * kHugeColThreads + threadIdx.x;
+    const int N = P * M;
+    const int64_t cell = static_cast<int64_t>(blockIdx.z) * n_bins + blockIdx.y;
+    MaxIdx best{-1.0f, 0x7fffffff};
+    float s = 0.0f;
+    if (m < M) {
+        const float2* u = U + cell * N + m;
+        float2 v[P];
+#pragma unroll
+        for (int kq = 0; kq < P; kq++) {
+            float2 x = u[kq * M];
+            if (kq) {
+                float2 w = twN[m * kq];  // W_N^{−m·kq}
+                w.y = -w.y;
+                x = cmulf(x, w);
+            }
+            v[kq] = x;
+        }
+        dft_reg<P, 1, +1>(v, twN, N);
+        float* g = grid + cell * N;
+#pragma unroll
+        for (int q = 0; q < P; q++) {
+            const int n = m + M * q;
+            float mag = __fadd_rn(__fmul_rn(v[q].x, v[q].x), __fmul_rn(v[q].y, v[q].y));  // volk_32fc_magnitude_squared_32f
+            if (accumulate) mag = __fadd_rn(g[n], mag);                                      // volk_32f_x2_add_32f
+            g[n] = mag;
+            best = better(best, MaxIdx{mag, n});
+            s += mag;
+        }
+    }
+    const MaxIdx bm = block_argmax(best, red_m);
+    const float bs = block_sum(s, red_s);
+    if (threadIdx.x == 0) tiles[cell * gridDim.x + blockIdx.x] = TileStat{bm.v, bm.i, bs, 0};
+}
+
+// Row statistics of cell (prn blockIdx.y, bin blockIdx.x) from its tiles and grid row.
+__global__ __launch_bounds__(kAcqThreads) void acq_huge_finalize_kernel(const float* __restrict__ grid, const TileStat* __restrict__ tiles,
+    int n_tiles, int N, int n_bins, int prn_offset, int samples_per_chip, RowStat* __restrict__ rowstat)
+{
+    __shared__ MaxIdx red_m[kAcqThreads / 64];
+    __shared__ float red_s[kAcqThreads / 64];
+    const int64_t cell = static_cast<int64_t>(blockIdx.y) * n_bins + blockIdx.x;
+    const TileStat* ts = tiles + cell * n_tiles;
+    MaxIdx m{-1.0f, 0x7fffffff};
+    float s = 0.0f;
+    for (int i = threadIdx.x; i < n_tiles; i += kAcqThreads) {
+        m = better(m, MaxIdx{ts[i].max, ts[i].argmax});
+        s += ts[i].sum;
+    }
+    const MaxIdx best = block_argmax(m, red_m);
+    const float sum = block_sum(s, red_s);
+    int e1 = best.i - samples_per_chip, e2 = best.i + samples_per_chip;
+    if (e1 < 0) e1 += N; else if (e2 >= N) e2 -= N;
+    const float* g = grid + cell * N;
+    MaxIdx m2{0.0f, 0x7fffffff};
+    for (int i = threadIdx.x; i < N; i += kAcqThreads) {
+        const bool in_win = (e1 < e2) ? (i >= e1 && i < e2) : (i >= e1 || i < e2);
+        m2 = better(m2, MaxIdx{in_win ? 0.0f : g[i], i});
+    }
+    const MaxIdx second = block_argmax(m2, red_m);
+    if (threadIdx.x == 0) rowstat[(static_cast<int64_t>(prn_offset) + blockIdx.y) * n_bins + blockIdx.x] = RowStat{best.v, best.i, sum, second.v};
+}
+
+#define GNSSHIP_HUGE_P_LIST(X) X(4) X(5) X(8) X(10) X(16) X(20) X(25) X(32)
+
+bool huge_p_supported(int P)
+{
+#define GNSSHIP_P_CASE(p) \
+    case p: return true;
+    switch (P) { GNSSHIP_HUGE_P_LIST(GNSSHIP_P_CASE) default: return false; }
+#undef GNSSHIP_P_CASE
+}
+
+hipError_t launch_acq_fft_huge(const void* sig, int fmt, const float2* mult, int n_rows, int P, const FftPlan& row_plan, const float2* twN,
+    const float2* twM, float2* scratch, float2* rowsT, int conj_out, hipStream_t stream)
+{
+    const int M = row_plan.n;
+    const int64_t N = static_cast<int64_t>(P) * M;
+    const dim3 cgrid((M + kHugeColThreads - 1) / kHugeColThreads, n_rows);
+#define GNSSHIP_P_CASE(p)                                                                                                                 \
+    case p:                                                                                                                               \
+        if (fmt == GNSSHIP_FMT_CF32)                                                                                                      \
+            hipLaunchKernelGGL((acq_huge_cols_fwd_kernel<GNSSHIP_FMT_CF32, p>), cgrid, dim3(kHugeColThreads), 0, stream, sig, mult, M, twN, \
+                scratch);                                                                                                                 \
+        else if (fmt == GNSSHIP_FMT_CI16)                                                                                                 \
+            hipLaunchKernelGGL((acq_huge_cols_fwd_kernel<GNSSHIP_FMT_CI16, p>), cgrid, dim3(kHugeColThreads), 0, stream, sig, mult, M, twN, \
+                scratch);                                                                                                                 \
+        else if (fmt == GNSSHIP_FMT_CI8)                                                                                                  \
+            hipLaunchKernelGGL((acq_huge_cols_fwd_kernel<GNSSHIP_FMT_CI8, p>), cgrid, dim3(kHugeColThreads), 0, stream, sig, mult, M, twN,  \
+                scratch);                                                                                                                 \
+        else                                                                                                                              \
+            return hipErrorInvalidValue;                                                                                                  \
+        break;
+    switch (P) {
+        GNSSHIP_HUGE_P_LIST(GNSSHIP_P_CASE)
+    default: return hipErrorInvalidValue;
+    }
+#undef GNSSHIP_P_CASE
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    const size_t lds = sizeof(float2) * static_cast<size_t>(M);
+    hipLaunchKernelGGL(acq_huge_rows_kernel<-1>, dim3(P, n_rows, 1), dim3(kAcqThreads), lds, stream, scratch, N, int64_t(0),
+        static_cast<const float2*>(nullptr), int64_t(0), int64_t(0), rowsT, N, int64_t(0), row_plan, twM, conj_out);
+    return hipGetLastError();
+}
+
+hipError_t launch_acq_search_huge(const float2* XT, const float2* codesT, int prn_offset, int n_prns, int n_bins, int P, const FftPlan& row_plan,
+    const float2* twN, const float2* twM, float2* U, float* grid, int accumulate, TileStat* tiles, int samples_per_chip, RowStat* rowstat,
+    hipStream_t stream)
+{
+    const int M = row_plan.n;
+    const int64_t N = static_cast<int64_t>(P) * M;
+    const size_t lds = sizeof(float2) * static_cast<size_t>(M);
+    // rows: blockIdx.y = bin (XT row set), blockIdx.z = prn (code spectrum), U cell = z·n_bins + y
+    hipLaunchKernelGGL(acq_huge_rows_kernel<+1>, dim3(P, n_bins, n_prns), dim3(kAcqThreads), lds, stream, XT, N, int64_t(0),
+        codesT + static_cast<int64_t>(prn_offset) * N, int64_t(0), N, U, N, N * n_bins, row_plan, twM, 0);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    const int n_tiles = (M + kHugeColThreads - 1) / kHugeColThreads;
+    const dim3 cgrid(n_tiles, n_bins, n_prns);
+#define GNSSHIP_P_CASE(p)                                                                                                              \
+    case p:                                                                                                                            \
+        hipLaunchKernelGGL((acq_huge_cols_inv_kernel<p>), cgrid, dim3(kHugeColThreads), 0, stream, U, M, n_bins, twN, grid, accumulate, \
+            tiles);                                                                                                                    \
+        break;
+    switch (P) {
+        GNSSHIP_HUGE_P_LIST(GNSSHIP_P_CASE)
+    default: return hipErrorInvalidValue;
+    }
+#undef GNSSHIP_P_CASE
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(acq_huge_finalize_kernel, dim3(n_bins, n_prns), dim3(kAcqThreads), 0, stream, grid, tiles, n_tiles, static_cast<int>(N), n_bins,
+        prn_offset, samples_per_chip, rowstat);
+    return hipGetLastError();
+}
+
 hipError_t launch_acq_fft_rows(const void* sig, int fmt, const float2* mult, int n_rows, const FftPlan& plan, const float2* tw, float2* rows,
     int conj_out, hipStream_t stream)
 {

@@ -162,6 +162,63 @@ int orc_beidou_b1i_code_gen_complex_sampled(float* dest, uint32_t prn, int32_t s
     return samples_per_code;
 }
 
+/* resampler(span<const float>, span<float>, fs_in, fs_out) — src/algorithms/libs/gnss_signal_replica.cc:257-272
+ * with AUX_CEIL2(x) = (int32)(int64)(x + 1) (:25). */
+void orc_code_resampler(float* dest, uint32_t dest_size, const float* from, uint32_t from_size, float fs_in, float fs_out)
+{
+    const float t_out = 1.0F / fs_out;
+    for (uint32_t i = 0; i + 1 < dest_size; i++) {
+        const float aux = (t_out * ((float)i + 1.0F)) * fs_in;
+        const uint32_t idx = (uint32_t)((int32_t)(int64_t)(aux + 1) - 1);
+        dest[i] = from[idx];
+    }
+    dest[dest_size - 1] = from[from_size - 1];
+}
+
+/* galileo_e1_code_gen_float_sampled without the secondary code — galileo_e1_signal_replica.cc:143-204,
+ * from the 4092 primary chips (galileo_e1_code_gen_int output).  kind: 1 = "1B", 2 = "1C".
+ * Returns samples per code, or -1 on bad arguments. */
+int orc_galileo_e1_code_gen_float_sampled(float* dest, const int32_t* chips, int kind, int cboc, int32_t sampling_freq, uint32_t chip_shift)
+{
+    const int32_t code_freq_basis = 1023000;
+    const int32_t spc = cboc ? 12 : 2;
+    const uint32_t code_length = (uint32_t)spc * 4092U;
+    uint32_t spcode = (uint32_t)((double)sampling_freq / ((double)code_freq_basis / 4092));
+    const uint32_t delay = ((uint32_t)((int32_t)4092 - (int32_t)chip_shift) % (uint32_t)4092) * spcode / 4092U;
+    if (spcode < 1) return -1;
+    float* sig = (float*)malloc(sizeof(float) * code_length);
+    if (!sig) return -1;
+    const float alpha = sqrtf(10.0F / 11.0F), beta = sqrtf(1.0F / 11.0F);
+    for (uint32_t i = 0; i < 4092U; i++) {
+        for (int32_t j = 0; j < spc; j++) {
+            const int32_t s11 = (j < spc / 2) ? chips[i] : -chips[i];
+            if (cboc) {
+                const int32_t s61 = (j % 2 == 0) ? chips[i] : -chips[i];
+                sig[i * spc + j] = (kind == 1) ? alpha * (float)s11 + beta * (float)s61 : alpha * (float)s11 - beta * (float)s61;
+            } else {
+                sig[i * spc + j] = (float)s11;
+            }
+        }
+    }
+    float* src = sig;
+    float* res = NULL;
+    uint32_t n = code_length;
+    if (sampling_freq != spc * code_freq_basis) {
+        res = (float*)malloc(sizeof(float) * spcode);
+        if (!res) {
+            free(sig);
+            return -1;
+        }
+        orc_code_resampler(res, spcode, sig, code_length, (float)(spc * code_freq_basis), (float)sampling_freq);
+        src = res;
+        n = spcode;
+    }
+    for (uint32_t i = 0; i < spcode && i < n; i++) dest[(i + delay) % spcode] = src[i];
+    free(sig);
+    free(res);
+    return (int)spcode;
+}
+
 /* ------------------------------------------------------------------------------------------ */
 /* Tracking correlator                                                                        */
 /* ------------------------------------------------------------------------------------------ */

@@ -7,6 +7,7 @@ includes GNU Radio's fxpt_nco.h), so the tables are pinned by their hex heads be
 digits of E1-B PRN 1 ("F5D7…") and E1-C PRN 1 ("B393…") — and by code properties.
 """
 import numpy as np
+import pytest
 
 from gnss_sim_receiver_amd import codes as C
 
@@ -44,3 +45,34 @@ def test_e1_sinboc_and_edges():
     assert not C.galileo_e1_code_gen_int("5X", 3).any()
     sec = C.galileo_e1_c_secondary_code()
     assert len(sec) == 25 and np.array_equal(sec[:5], [1, 1, -1, -1, -1])  # "00111…" (Galileo_E1.h:52)
+
+
+@pytest.mark.parametrize("sig_id,cboc,prn,fs,shift", [("1B", False, 11, 25000000, 0), ("1C", False, 3, 4000000, 0),
+                                                      ("1B", True, 7, 25000000, 0), ("1C", True, 50, 12276000, 0),
+                                                      ("1B", False, 1, 2046000, 0), ("1C", False, 20, 50000000, 1000),
+                                                      ("1B", True, 36, 20000000, 4091)])
+def test_e1_sampled_code_matches_oracle(built, sig_id, cboc, prn, fs, shift):
+    """galileo_e1_code_gen_float_sampled (galileo_e1_signal_replica.cc:143-204): the product's
+    generator (codes.py) against the oracle's C restatement, from the same pinned ICD chips."""
+    import ctypes
+    from oracle import oracle as O
+    chips = np.ascontiguousarray(C.galileo_e1_code_gen_int(sig_id, prn), np.int32)
+    n = int(fs / 250)
+    out = np.zeros(n, np.float32)
+    got = O.lib().orc_galileo_e1_code_gen_float_sampled(out.ctypes.data_as(ctypes.POINTER(ctypes.c_float)),
+                                                          chips.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+                                                          1 if sig_id == "1B" else 2, int(cboc), fs, shift)
+    assert got == n
+    mine = C.galileo_e1_code_gen_float_sampled(sig_id, cboc, prn, fs, shift)
+    assert mine.dtype == np.float32 and len(mine) == n
+    assert np.array_equal(mine, out)
+    if not cboc and fs == 2046000:  # at 2 samples per chip the sampled code IS the tracking replica
+        assert np.array_equal(mine, C.galileo_e1_code_gen_sinboc11_float(sig_id, prn))
+
+
+def test_e1_secondary_sampled_code():
+    c = C.galileo_e1_code_gen_float_sampled("1C", False, 3, 2046000, 0, secondary_flag=True)
+    base = C.galileo_e1_code_gen_sinboc11_float("1C", 3)
+    sec = C.galileo_e1_c_secondary_code()
+    assert len(c) == 25 * 8184
+    assert np.array_equal(c.reshape(25, 8184), sec[:, None] * base[None, :])

@@ -185,4 +185,73 @@ def test_four_step_max_size_and_limit(ctx):
     assert np.max(np.abs(grid[0] - rgrid)) / rgrid.max() < 1e-5
     assert (r.doppler_index, r.code_index) == (ref.doppler_index, ref.code_index)
     with pytest.raises(abi.GnssHipError):
-        engine.PcpsAcquisition(ctx, 40000000, 40000, 5000, 250)  # > 32768
+        engine.PcpsAcquisition(ctx, 40001000, 40001, 5000, 250)  # 13·17·181: no layout
+
+
+# ---- huge transforms (N = P·M > 32768, column and row stages as separate kernels) ----------
+
+def test_huge_forced_at_small_size_matches_oracle(ctx, monkeypatch):
+    """The huge layout at N = 4000 (P = 4, M = 1000) against the oracle, both statistics."""
+    monkeypatch.setenv("GNSSHIP_ACQ_FORCE_HUGE", "1")
+    fs, n = 4000000, 4000
+    sat = signals.Satellite(prn=14, doppler_hz=1380.0, code_delay_chips=702.6, cn0_dbhz=47.0)
+    for cfar in (False, True):
+        sig, (r,), grid = _acq_big_case(ctx, fs, n, [14], [sat], 5000, 250, cfar, seed=15, want_grid=True)
+        ref, rgrid = O.pcps_acquisition_core(sig, codes.gps_l1_ca_code_gen_complex_sampled(14, fs), fs, 5000, 250, 0, cfar)
+        assert np.max(np.abs(grid[0] - rgrid)) / rgrid.max() < 1e-5
+        assert (r.doppler_index, r.code_index) == (ref.doppler_index, ref.code_index)
+        np.testing.assert_allclose([r.peak, r.input_power, r.test_statistic], [ref.peak, ref.input_power, ref.test_statistic],
+                                   rtol=2e-4)
+
+
+def test_huge_gps_50msps_multi_prn(ctx):
+    """1 ms GPS L1 C/A at 50 Msps (SURVEY §8d C5 rate): N = 50000 = 4 × 12500."""
+    fs, n, dmax, step = 50000000, 50000, 2000, 500
+    present = [signals.Satellite(prn=p, doppler_hz=d, code_delay_chips=c, cn0_dbhz=47.0) for p, d, c in [(6, 1200.0, 333.3), (21, -800.0, 40.9)]]
+    prns = [6, 21, 2]
+    sig, res, grid = _acq_big_case(ctx, fs, n, prns, present, dmax, step, True, seed=61, want_grid=True)
+    for k, p in enumerate(prns):
+        ref, rgrid = O.pcps_acquisition_core(sig, codes.gps_l1_ca_code_gen_complex_sampled(p, fs), fs, dmax, step, 0, True)
+        assert np.max(np.abs(grid[k] - rgrid)) / rgrid.max() < 1e-5, p
+        flat = np.sort(rgrid.ravel())
+        if flat[-1] / flat[-2] > 1.0 + 1e-4:
+            assert (res[k].doppler_index, res[k].code_index) == (ref.doppler_index, ref.code_index), p
+            assert res[k].acq_delay_samples == ref.acq_delay_samples
+        np.testing.assert_allclose(res[k].test_statistic, ref.test_statistic, rtol=2e-3)
+    assert min(res[0].test_statistic, res[1].test_statistic) > 2 * res[2].test_statistic
+
+
+@pytest.mark.parametrize("cboc", [False, True])
+def test_huge_galileo_e1_25msps(ctx, cboc):
+    """Galileo E1 acquisition (GalileoE1PcpsAmbiguousAcquisition: ms_per_code 4,
+    galileo_e1_pcps_ambiguous_acquisition.cc:51): 4 ms at 25 Msps, N = 100000 = 8 × 12500, E1-B
+    replica from galileo_e1_code_gen_complex_sampled, against the oracle core."""
+    fs, n, dmax, step = 25000000, 100000, 1000, 250
+    present = [signals.Satellite(prn=p, doppler_hz=d, code_delay_chips=c, cn0_dbhz=45.0, system="GAL")
+               for p, d, c in [(11, 400.0, 2222.2), (30, -650.0, 7001.5)]]
+    prns = [11, 30, 4]
+    sig = signals.generate_if(fs, n, present, seed=91)
+    acq = engine.PcpsAcquisition(ctx, fs, n, dmax, step, 0, False, max_prns=3, ms_per_code=4)
+    lc = [codes.galileo_e1_code_gen_complex_sampled("1B", cboc, p, fs) for p in prns]
+    for k in range(3):
+        acq.set_local_code(lc[k], k)
+    res, grid = acq.run(sig, n_prns=3, want_grid=True)
+    acq.close()
+    spc, spcode = int(np.ceil(np.float32(fs) / np.float32(1023000.0))), float(np.float32(np.float32(fs) * np.float32(0.001)) * 4)
+    for k, p in enumerate(prns):
+        ref, rgrid = O.pcps_acquisition_core(sig, lc[k], fs, dmax, step, 0, False, samples_per_chip=spc, samples_per_code=spcode)
+        assert np.max(np.abs(grid[k] - rgrid)) / rgrid.max() < 1e-5, p
+        flat = np.sort(rgrid.ravel())
+        if flat[-1] / flat[-2] > 1.0 + 1e-4:
+            assert (res[k].doppler_index, res[k].code_index) == (ref.doppler_index, ref.code_index), p
+        np.testing.assert_allclose(res[k].test_statistic, ref.test_statistic, rtol=2e-3)
+    # the present satellites are found at their code delay (sinBOC samples → IF samples)
+    for k, s in enumerate(present):
+        exp = (s.code_delay_chips / s.code_freq() * fs) % n
+        assert min(abs(res[k].code_index - exp), n - abs(res[k].code_index - exp)) <= 2, (s.prn, res[k].code_index, exp)
+
+
+def test_huge_limits(ctx):
+    from gnss_sim_receiver_amd import abi
+    with pytest.raises(abi.GnssHipError):
+        engine.PcpsAcquisition(ctx, 600000000, 600000, 5000, 250)  # > 32 × 16384
