@@ -179,6 +179,15 @@ __device__ __forceinline__ f2 cmul_pk2(f2 x, f2 p)
     return r;
 }
 
+// x·q with q wave-uniform (an anchor from the chunk's scalar block): q stays in its SGPR pair.
+__device__ __forceinline__ f2 cmul_pk2_s(f2 x, f2 q)
+{
+    f2 t, r;
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]" : "=v"(t) : "v"(x), "s"(q));
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[0,1,0]" : "=v"(r) : "v"(x), "s"(q), "v"(t));
+    return r;
+}
+
 // (int)floor(x) in one instruction (V_CVT_FLR_I32_F32), as the resampler's (int)floor(...) for
 // in-range values.
 __device__ __forceinline__ int cvt_floor_i32(float x)
@@ -269,12 +278,33 @@ __device__ __forceinline__ void correlate_group(const DevJob& job, const ChunkDe
         const int r = tid + (g * kGroup + u) * kCorrThreads;
         const float fn = FULL ? fn0 + static_cast<float>(u * kCorrThreads) : static_cast<float>(ch.start + (r < ch.len ? r : ch.len - 1));
         const float sn = job.code_step * fn;  // reference loop counter n, as float
+#ifndef GNSSHIP_CORR_SCALAR_INDEX
+        // two taps per packed add: (sn + shift) then + (−rem) — x + (−r) ≡ x − r bit for bit
+#pragma unroll
+        for (int t = 0; t < NT; t += 2) {
+            if (t + 1 < NT) {
+                const f2 v = (f2{sn, sn} + f2{shifts[t], shifts[t + 1]}) + f2{-job.rem_code, -job.rem_code};
+                int i0 = cvt_floor_i32(v.x), i1 = cvt_floor_i32(v.y);
+                if constexpr (!IN_MARGIN) {
+                    i0 = wrap_index(i0, L);
+                    i1 = wrap_index(i1, L);
+                }
+                cv[u][t] = code[i0];
+                cv[u][t + 1] = code[i1];
+            } else {
+                int idx = cvt_floor_i32((sn + shifts[t]) - job.rem_code);
+                if constexpr (!IN_MARGIN) idx = wrap_index(idx, L);
+                cv[u][t] = code[idx];
+            }
+        }
+#else
 #pragma unroll
         for (int t = 0; t < NT; t++) {
             int idx = cvt_floor_i32((sn + shifts[t]) - job.rem_code);
             if constexpr (!IN_MARGIN) idx = wrap_index(idx, L);
             cv[u][t] = code[idx];
         }
+#endif
     }
     // phase 2: phasor at sample n = 256k + j: q_k · E_j, with E_0 = 1 — lane 0 uses the
     // renormalised anchor q_k where the reference uses a_k = |a_k|·q_k (|a_k| − 1 ≲ 1.5e-5 on one
@@ -282,9 +312,17 @@ __device__ __forceinline__ void correlate_group(const DevJob& job, const ChunkDe
 #pragma unroll
     for (int u = 0; u < kGroup; u++) {
         const Anchor& a = qk[g * kGroup + u];  // block of sample u: chunk-uniform (SGPRs)
-        const f2 p = cmul_pk(f2{a.q_re, a.q_im}, e, esw);
         const f2 x = xg[u];  // zero past the chunk end (buffer range check)
+#ifndef GNSSHIP_CORR_NO_EFACTOR
+        // E_j is the same for every sample of this lane (j = tid in every block): the sums are
+        // kept in the anchor frame, Σ (x·q_k)·c, and rotated by E_j once per chunk (rotate_sums)
+        (void)e;
+        (void)esw;
+        const f2 tt = cmul_pk2_s(x, f2{a.q_re, a.q_im});
+#else
+        const f2 p = cmul_pk(f2{a.q_re, a.q_im}, e, esw);
         const f2 tt = cmul_pk2(x, p);
+#endif
 #pragma unroll
         for (int t = 0; t < NT; t++) acc[t] = __builtin_elementwise_fma(tt, f2{cv[u][t], cv[u][t]}, acc[t]);
     }
@@ -439,6 +477,10 @@ __global__ __launch_bounds__(kCorrThreads, (corr_waves_per_simd<NT, IN_MARGIN>()
             for (int u = 0; u < kGroup; u++) xa[u] = xb[u];
         }
         GNSSHIP_PROF_STAMP(c == 0 ? 3 : 7);
+#ifndef GNSSHIP_CORR_NO_EFACTOR
+#pragma unroll
+        for (int t = 0; t < NT; t++) acc[t] = cmul_pk(acc[t], e, esw);  // anchor frame → sample frame (× E_j)
+#endif
 #pragma unroll
         for (int t = 0; t < NT; t++) {
             const float wr = row_sum(acc[t].x), wi = row_sum(acc[t].y);
