@@ -73,16 +73,16 @@ __device__ __forceinline__ int hd_chip_index(const HdJob& job, uint32_t m)
 
 }  // namespace
 
-__global__ void hd_anchor_kernel(const HdJob* __restrict__ jobs, int n_jobs, Anchor* __restrict__ anchors)
+__global__ void hd_anchor_kernel(const HdJob* __restrict__ jobs, int n_jobs, HdAnchor* __restrict__ anchors)
 {
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= n_jobs) return;
     const HdJob job = jobs[j];
     const int nblk = (job.n_samples + kRenorm - 1) / kRenorm;
-    Anchor* out = anchors + job.anchor_offset;
+    HdAnchor* out = anchors + job.anchor_offset;
     float pr = job.p0_re, pi = job.p0_im;
     for (int k = 0; k < nblk; k++) {
-        out[k] = Anchor{pr, pi};
+        out[k] = HdAnchor{pr, pi};
         if (k == nblk - 1) break;
         for (int s = 0; s < kRenorm; s++) {
             const float2 p = cmul_rn(pr, pi, job.inc_re, job.inc_im);
@@ -94,7 +94,7 @@ __global__ void hd_anchor_kernel(const HdJob* __restrict__ jobs, int n_jobs, Anc
 
 template <int FMT>
 __global__ __launch_bounds__(kHdThreads) void hd_corr_kernel(const void* __restrict__ samples, const HdJob* __restrict__ jobs,
-    const HdChunk* __restrict__ chunks, const Anchor* __restrict__ anchors, float* __restrict__ partials)
+    const HdChunk* __restrict__ chunks, const HdAnchor* __restrict__ anchors, float* __restrict__ partials)
 {
     extern __shared__ float code_lds[];
     __shared__ float red[kHdThreads / 64][2 * kMaxTaps];
@@ -126,7 +126,7 @@ __global__ __launch_bounds__(kHdThreads) void hd_corr_kernel(const void* __restr
             pr = __fdiv_rn(job.p0_re, m);
             pi = __fdiv_rn(job.p0_im, m);
         } else {
-            const Anchor a = anchors[job.anchor_offset + (n >> 8)];
+            const HdAnchor a = anchors[job.anchor_offset + (n >> 8)];
             const float dr = a.q_re * er - a.q_im * ei, di = a.q_re * ei + a.q_im * er;  // pd_n
             const uint32_t k = n - 1u;
             const float theta = __fmul_rn(__uint2float_rn(k * k), job.rate_arg);
@@ -305,7 +305,7 @@ hipError_t hd_plan_upload(HdPlan& plan, hipStream_t stream)
     if (plan.n_anchors > plan.anchor_cap) {
         if (plan.anchors_dev) (void)hipFree(plan.anchors_dev);
         plan.anchors_dev = nullptr;
-        if ((e = hipMalloc(&plan.anchors_dev, sizeof(Anchor) * plan.n_anchors)) != hipSuccess) return e;
+        if ((e = hipMalloc(&plan.anchors_dev, sizeof(HdAnchor) * plan.n_anchors)) != hipSuccess) return e;
         plan.anchor_cap = plan.n_anchors;
     }
     if (nj && (e = hipMemcpyAsync(plan.jobs_dev, plan.jobs.data(), sizeof(HdJob) * nj, hipMemcpyHostToDevice, stream)) != hipSuccess) return e;

@@ -14,14 +14,15 @@
 //     stores, for every 256-sample block k, the phasor used at sample 256k and its renormalised
 //     value.  Only arithmetic on NCO arguments: no IF samples are read.  The recursion is serial
 //     by definition; one lane per job keeps every job's chain in flight at once.
-//  2. corr_batch_kernel — one 256-thread workgroup (4 wave64) per chunk of ≤4096 samples.  Lane t
-//     owns samples {start + t + 256m}, so every wave-load is 64 consecutive samples (coalesced) and
-//     lane t is always at offset j = t inside its 256-sample block: the rotation from the block's
-//     renormalised anchor to sample j, E_j = |phase_inc|^j·e^{i·j·Δ}, is computed ONCE per lane
-//     (double-precision sincos) and reused for all its samples; per sample the phasor is one complex
-//     product q_k·E_j.  Per-tap sums live in registers, are reduced with wave64 xor-shuffles and then
-//     across the 4 waves in LDS.  Jobs longer than one chunk write per-chunk partials that a third
-//     tiny kernel sums in chunk order (deterministic, no atomics).
+//  2. corr_batch_kernel — one 256-thread workgroup (4 wave64) per work item of up to four
+//     ≤4096-sample chunks sharing one code replica (staged once in LDS); wave w correlates chunk w.
+//     Lane t owns samples {256k + 4t + s : s < 4} of every 256-sample block k, so a wave-load is
+//     2 KiB of consecutive samples and lane t always sits at offsets 4t..4t+3 of its blocks: the
+//     block's four phasors q_k·inc^s are uniform (scalar loads of the anchor), the lane factor
+//     E_{4t} = |phase_inc|^{4t}·e^{i·4t·Δ} is applied once per chunk to the tap sums.  Per sample:
+//     chip indices + LDS code reads, one complex product with a scalar operand, one packed FMA per
+//     tap.  Sums are reduced within the wave (DPP + lane shuffles).  Jobs longer than one chunk
+//     write per-chunk partials that a third tiny kernel sums in chunk order (no atomics).
 //
 // Numerics (parity contract |Δ|/|ref| ≤ 1e-5 per tap vs the generic reference):
 //  * chip index: floor(step·(float)n + shift − rem) with __fmul_rn/__fadd_rn/__fsub_rn in the
@@ -59,8 +60,9 @@ __device__ __forceinline__ int segment_block(int seg, int nblk)
 }
 
 // The reference rotator recursion of one job, stored at every renormalisation point — blocks of
-// segments [seg_lo, seg_hi).  A later segment resumes from the stored anchor of the block before
-// it: the chain after a renormalisation depends only on the renormalised phasor q.
+// segments [seg_lo, seg_hi).  Block k stores the renormalised q_k and the chain's next three phasors
+// q_k·inc, q_k·inc², q_k·inc³ (engine.h Anchor).  A later segment resumes from the stored q of the
+// block before it: the chain after a renormalisation depends only on q.
 __device__ __forceinline__ void replay_anchors(const DevJob& job, Anchor* __restrict__ anchors, int seg_lo, int seg_hi)
 {
     const int nblk = (job.n_samples + kRenorm - 1) / kRenorm;
@@ -77,7 +79,7 @@ __device__ __forceinline__ void replay_anchors(const DevJob& job, Anchor* __rest
     if (kb == 0) {
         p = f2v{job.p0_re, job.p0_im};
     } else {
-        p = f2v{out[kb - 1].q_re, out[kb - 1].q_im};
+        p = f2v{out[kb - 1].p[0], out[kb - 1].p[1]};
 #pragma unroll 16
         for (int s = 0; s < kRenorm; s++) p = f2v{p.x, p.x} * inc_a + f2v{p.y, p.y} * inc_b;
     }
@@ -85,14 +87,29 @@ __device__ __forceinline__ void replay_anchors(const DevJob& job, Anchor* __rest
         // sample 256k uses `a = phase`; then phase /= |phase|; then 256 rotations reach 256(k+1)
         const float m = hypotf_glibc(p.x, p.y);
         const float qr = __fdiv_rn(p.x, m), qi = __fdiv_rn(p.y, m);
-        out[k] = Anchor{qr, qi};
+        Anchor A;
+        A.p[0] = qr;
+        A.p[1] = qi;
         p = f2v{qr, qi};
+        // the first 16 rotations peeled: q·inc^1..3 are stored on the way (the chain keeps the
+        // shape of a 16-step unrolled loop — 15 more such steps reach 256(k+1))
+#pragma unroll
+        for (int s = 1; s <= 16; s++) {
+            p = f2v{p.x, p.x} * inc_a + f2v{p.y, p.y} * inc_b;
+            if (s < 4) {
+                A.p[2 * s] = p.x;
+                A.p[2 * s + 1] = p.y;
+            }
+        }
+        out[k] = A;
         if (k != ke - 1) {
-#pragma unroll 16
-            for (int s = 0; s < kRenorm; s++) {
-                const f2v m1 = f2v{p.x, p.x} * inc_a;
-                const f2v m2 = f2v{p.y, p.y} * inc_b;
-                p = m1 + m2;
+            for (int s0 = 16; s0 < kRenorm; s0 += 16) {
+#pragma unroll
+                for (int s = 0; s < 16; s++) {
+                    const f2v m1 = f2v{p.x, p.x} * inc_a;
+                    const f2v m2 = f2v{p.y, p.y} * inc_b;
+                    p = m1 + m2;
+                }
             }
         }
     }
@@ -116,6 +133,11 @@ typedef int i4v __attribute__((ext_vector_type(4)));
 extern "C" __device__ f2v_t gnsship_raw_buffer_load_f32x2(i4v rsrc, int voffset, int soffset, int aux) __asm("llvm.amdgcn.raw.buffer.load.v2f32");
 extern "C" __device__ int gnsship_raw_buffer_load_i32(i4v rsrc, int voffset, int soffset, int aux) __asm("llvm.amdgcn.raw.buffer.load.i32");
 extern "C" __device__ short gnsship_raw_buffer_load_i16(i4v rsrc, int voffset, int soffset, int aux) __asm("llvm.amdgcn.raw.buffer.load.i16");
+typedef float f4v_t __attribute__((ext_vector_type(4)));
+typedef int i2v_t __attribute__((ext_vector_type(2)));
+extern "C" __device__ f4v_t gnsship_raw_buffer_load_f32x4(i4v rsrc, int voffset, int soffset, int aux) __asm("llvm.amdgcn.raw.buffer.load.v4f32");
+extern "C" __device__ i4v gnsship_raw_buffer_load_i32x4(i4v rsrc, int voffset, int soffset, int aux) __asm("llvm.amdgcn.raw.buffer.load.v4i32");
+extern "C" __device__ i2v_t gnsship_raw_buffer_load_i32x2(i4v rsrc, int voffset, int soffset, int aux) __asm("llvm.amdgcn.raw.buffer.load.v2i32");
 
 template <int FMT>
 constexpr int sample_bytes() { return FMT == GNSSHIP_FMT_CF32 ? 8 : (FMT == GNSSHIP_FMT_CI16 ? 4 : 2); }
@@ -209,80 +231,101 @@ __device__ __forceinline__ int wrap_index(int idx, int L)
     return idx;
 }
 
-#ifndef GNSSHIP_CORR_GROUP
-#define GNSSHIP_CORR_GROUP 4
-#endif
-constexpr int kGroup = GNSSHIP_CORR_GROUP;  // samples per lane per pipeline stage
-constexpr int kGroups = kCorrSamplesPerThread / kGroup;
-constexpr int kGroupSpan = kGroup * kCorrThreads;
-static_assert(kGroups % 2 == 0, "ping-pong over pairs of groups");
+// Lane layout: one wave per chunk; lane t covers samples 256k + 4t + s (s = 0..3) of every
+// 256-sample block k of the chunk — four consecutive samples per lane per block, one 2 KiB
+// contiguous span per wave-load (CF32: two dwordx4 per lane).
+constexpr int kLaneSamples = 4;
+constexpr int kWave = 64;
 
-// Samples of pipeline group g of a chunk for this lane (zeros past the chunk end).
+// The four samples of this lane in block kb of a chunk (full block: wide loads).
 template <int FMT>
-__device__ __forceinline__ void load_group(i4v span, int g, f2 (&dstx)[kGroup])
+__device__ __forceinline__ void load_block(i4v span, int lane, int kb, f2 (&x)[kLaneSamples])
 {
-    const int voff = static_cast<int>(threadIdx.x) * sample_bytes<FMT>();
+    const int off = (kb * kRenorm + kLaneSamples * lane) * sample_bytes<FMT>();
+    if constexpr (FMT == GNSSHIP_FMT_CF32) {
+        const f4v_t a = gnsship_raw_buffer_load_f32x4(span, off, 0, 0);
+        const f4v_t b = gnsship_raw_buffer_load_f32x4(span, off + 16, 0, 0);
+        x[0] = f2{a.x, a.y};
+        x[1] = f2{a.z, a.w};
+        x[2] = f2{b.x, b.y};
+        x[3] = f2{b.z, b.w};
+    } else if constexpr (FMT == GNSSHIP_FMT_CI16) {
+        const i4v v = gnsship_raw_buffer_load_i32x4(span, off, 0, 0);
 #pragma unroll
-    for (int u = 0; u < kGroup; u++) dstx[u] = load_sample<FMT>(span, voff, (g * kGroup + u) * kCorrThreads * sample_bytes<FMT>());
+        for (int u = 0; u < 4; u++)
+            x[u] = f2{static_cast<float>(static_cast<short>(v[u] & 0xffff)), static_cast<float>(static_cast<short>(v[u] >> 16))};
+    } else {
+        const i2v_t v = gnsship_raw_buffer_load_i32x2(span, off, 0, 0);
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int w = v[u >> 1] >> (16 * (u & 1));
+            x[u] = f2{static_cast<float>(static_cast<signed char>(w & 0xff)), static_cast<float>(static_cast<signed char>((w >> 8) & 0xff))};
+        }
+    }
 }
 
-// s_waitcnt immediates (gfx9 encoding: vmcnt [3:0]+[15:14], expcnt [6:4], lgkmcnt [11:8]) that
-// wait on the vector-memory counter only.
-constexpr int waitcnt_vm(int n) { return (n & 0xF) | ((n >> 4) << 14) | (0x7 << 4) | (0xF << 8); }
-constexpr int kWaitVmcntGroup = waitcnt_vm(kGroup);
-
-// E_j = |inc|^j · e^{i j Δ}: rotation from a renormalised anchor to sample 256k + j, for this
-// lane's j = threadIdx.x (angle formed and range-reduced in double, then an accurate float sincos).
-__device__ __forceinline__ f2 anchor_to_lane_rotation(const DevJob& job)
+// The same samples one load each (the chunk's partial last block: the buffer range check zeroes
+// every sample past the chunk end on its own).
+template <int FMT>
+__device__ __forceinline__ void load_block_tail(i4v span, int lane, int kb, f2 (&x)[kLaneSamples])
 {
-    constexpr double kTwoPi = 6.283185307179586476925286766559;
+    const int off = (kb * kRenorm + kLaneSamples * lane) * sample_bytes<FMT>();
+#pragma unroll
+    for (int u = 0; u < kLaneSamples; u++) x[u] = load_sample<FMT>(span, off + u * sample_bytes<FMT>(), 0);
+}
+
+template <int FMT>
+__device__ __forceinline__ void load_any(i4v span, int lane, int kb, int len, f2 (&x)[kLaneSamples])
+{
+    if ((kb + 1) * kRenorm <= len)  // wave-uniform
+        load_block<FMT>(span, lane, kb, x);
+    else
+        load_block_tail<FMT>(span, lane, kb, x);
+}
+
+// E_j = |inc|^j · e^{i j Δ} for this lane's j = 4·lane (angle formed and range-reduced in double,
+// hardware sin/cos in revolutions — E_j to a few 1e-7, against the 1e-5 tolerance).
+__device__ __forceinline__ f2 lane_rotation(const DevJob& job, int j)
+{
     constexpr double kInvTwoPi = 0.15915494309189533576888376337251;
-    const int tid = threadIdx.x;
 #ifndef GNSSHIP_EJ_LIBM
-    // angle in revolutions, range-reduced in double; the hardware sin/cos (V_SIN/V_COS_F32) take
-    // revolutions — E_j to a few 1e-7, against the 1e-5 correlation tolerance (the libm sincosf
-    // form, GNSSHIP_EJ_LIBM, costs ~50 more VALU per chunk)
-    const double rev = static_cast<double>(tid) * (job.dtheta * kInvTwoPi);
+    const double rev = static_cast<double>(j) * (job.dtheta * kInvTwoPi);
     const float rf = static_cast<float>(rev - rint(rev));
     const float s = __builtin_amdgcn_sinf(rf), c = __builtin_amdgcn_cosf(rf);
-    (void)kTwoPi;
 #else
-    double th = static_cast<double>(tid) * job.dtheta;
+    constexpr double kTwoPi = 6.283185307179586476925286766559;
+    double th = static_cast<double>(j) * job.dtheta;
     th = fma(-kTwoPi, rint(th * kInvTwoPi), th);
     float s, c;
     sincosf(static_cast<float>(th), &s, &c);
 #endif
-    const float mag = __fmaf_rn(static_cast<float>(tid), job.log_mag_inc, 1.0f);
+    const float mag = __fmaf_rn(static_cast<float>(j), job.log_mag_inc, 1.0f);
     return f2{mag * c, mag * s};
 }
 
-// Correlation of one pipeline group (kGroup samples per lane) of one chunk into acc.
-// `code` points at chip 0 of the padded LDS replica (valid indices [−kCodeMargin, L + kCodeMargin)).
+// Correlation of one block (four samples per lane) into acc, kept in the lane's anchor frame:
+// Σ (x·P_s)·c with P_s = the block's uniform phasor of offset s (Anchor), the lane factor E_{4t}
+// applied once per chunk.  `code` = chip 0 of the padded LDS replica.
 // IN_MARGIN: the host proved every chip index of the job lies in the padded range (no modulo).
-// FULL: the whole group lies inside the chunk (group-uniform; only a chunk's last group can be
-// partial) — no tail clamps in the fast path.
+// FULL: the whole block lies inside the chunk (wave-uniform; only the last block can be partial).
 template <int NT, bool IN_MARGIN, bool FULL>
-__device__ __forceinline__ void correlate_group(const DevJob& job, const ChunkDesc& ch, const Anchor (&qk)[kBlocksPerChunk], f2 e,
-    f2 esw, const float (&shifts)[NT], const float* __restrict__ code, int L, int g, const f2 (&xg)[kGroup], f2 (&acc)[NT])
+__device__ __forceinline__ void correlate_block(const DevJob& job, const ChunkDesc& ch, const Anchor& A, const float (&shifts)[NT],
+    const float* __restrict__ code, int L, int lane, int kb, const f2 (&x)[kLaneSamples], f2 (&acc)[NT])
 {
-    const int tid = threadIdx.x;  // == offset j inside every 256-sample block this lane visits
-    // phase 1: every chip index of the group and its LDS read, all in flight together (the code
-    // resampler, generic association order ((step*n) + shift) - rem, each rounded on its own; the
-    // file is built with -ffp-contract=off)
-    float cv[kGroup][NT];
-    // (float)n for the group's first sample; the later ones are exact float increments of 256
-    // (n + 256u is representable whenever (float)n's ulp divides 256, i.e. for every int32 n)
-    const float fn0 = static_cast<float>(ch.start + tid + g * kGroupSpan);
+    // phase 1: every chip index of the block and its LDS read (the code resampler, generic
+    // association order ((step*n) + shift) - rem, each rounded on its own; built with
+    // -ffp-contract=off).  (float)n of the lane's first sample; the next three are exact float
+    // increments (jobs are at most 2^24 samples, derive_job).
+    float cv[kLaneSamples][NT];
+    const int r0 = kb * kRenorm + kLaneSamples * lane;
+    const float fn0 = static_cast<float>(ch.start + r0);
 #pragma unroll
-    for (int u = 0; u < kGroup; u++) {
-        const int r = tid + (g * kGroup + u) * kCorrThreads;
-        const float fn = FULL ? fn0 + static_cast<float>(u * kCorrThreads) : static_cast<float>(ch.start + (r < ch.len ? r : ch.len - 1));
+    for (int u = 0; u < kLaneSamples; u++) {
+        const float fn = FULL ? fn0 + static_cast<float>(u) : static_cast<float>(ch.start + (r0 + u < ch.len ? r0 + u : ch.len - 1));
         const float sn = job.code_step * fn;  // reference loop counter n, as float
-#ifndef GNSSHIP_CORR_SCALAR_INDEX
-        // two taps per packed add: (sn + shift) then + (−rem) — x + (−r) ≡ x − r bit for bit
 #pragma unroll
         for (int t = 0; t < NT; t += 2) {
-            if (t + 1 < NT) {
+            if (t + 1 < NT) {  // two taps per packed add: (sn + shift) + (−rem) ≡ (sn + shift) − rem
                 const f2 v = (f2{sn, sn} + f2{shifts[t], shifts[t + 1]}) + f2{-job.rem_code, -job.rem_code};
                 int i0 = cvt_floor_i32(v.x), i1 = cvt_floor_i32(v.y);
                 if constexpr (!IN_MARGIN) {
@@ -297,41 +340,28 @@ __device__ __forceinline__ void correlate_group(const DevJob& job, const ChunkDe
                 cv[u][t] = code[idx];
             }
         }
-#else
-#pragma unroll
-        for (int t = 0; t < NT; t++) {
-            int idx = cvt_floor_i32((sn + shifts[t]) - job.rem_code);
-            if constexpr (!IN_MARGIN) idx = wrap_index(idx, L);
-            cv[u][t] = code[idx];
-        }
-#endif
     }
-    // phase 2: phasor at sample n = 256k + j: q_k · E_j, with E_0 = 1 — lane 0 uses the
-    // renormalised anchor q_k where the reference uses a_k = |a_k|·q_k (|a_k| − 1 ≲ 1.5e-5 on one
-    // sample in 256: ≲ 6e-8 of a tap sum); then in_common[n]·phase and the tap sums
+    // phase 2: in_common[n]·phase (anchor frame) and the tap sums
 #pragma unroll
-    for (int u = 0; u < kGroup; u++) {
-        const Anchor& a = qk[g * kGroup + u];  // block of sample u: chunk-uniform (SGPRs)
-        const f2 x = xg[u];  // zero past the chunk end (buffer range check)
-#ifndef GNSSHIP_CORR_NO_EFACTOR
-        // E_j is the same for every sample of this lane (j = tid in every block): the sums are
-        // kept in the anchor frame, Σ (x·q_k)·c, and rotated by E_j once per chunk (rotate_sums)
-        (void)e;
-        (void)esw;
-        const f2 tt = cmul_pk2_s(x, f2{a.q_re, a.q_im});
-#else
-        const f2 p = cmul_pk(f2{a.q_re, a.q_im}, e, esw);
-        const f2 tt = cmul_pk2(x, p);
-#endif
+    for (int u = 0; u < kLaneSamples; u++) {
+        const f2 tt = cmul_pk2_s(x[u], f2{A.p[2 * u], A.p[2 * u + 1]});
 #pragma unroll
         for (int t = 0; t < NT; t++) acc[t] = __builtin_elementwise_fma(tt, f2{cv[u][t], cv[u][t]}, acc[t]);
     }
 }
 
+// Sum over the 64 lanes of the wave (every lane gets it): DPP row sums, then the four rows.
+__device__ __forceinline__ float wave_sum(float v)
+{
+    v = row_sum(v);
+    v += __shfl_xor(v, 16, kWave);
+    v += __shfl_xor(v, 32, kWave);
+    return v;
+}
+
 // Waves per SIMD the register allocation must allow: the 1- and 3-tap in-margin classes (GPS/B1I
-// E-P-L, E1 data prompt) are held to 7 waves (≤ 72 VGPRs, spill-free): residency hides the sample
-// and LDS latency of a kernel whose issue is otherwise VALU-bound; wider tap classes keep the
-// general bound.  (Measured: 6 → 7 waves +1%, 8 slower.)
+// E-P-L, E1 data prompt) are held to 7 waves (≤ 72 VGPRs, spill-free); wider tap classes keep the
+// general bound.
 #ifndef GNSSHIP_CORR_WAVES_EPL
 #define GNSSHIP_CORR_WAVES_EPL 7
 #endif
@@ -343,22 +373,21 @@ constexpr int corr_waves_per_simd()
 
 // One launch per chunk class (tap-count template × in-margin flag), so each kernel is compiled
 // for exactly its path and the register allocation is not the worst case over all variants.
-// One workgroup per WORK ITEM: up to kMaxChunksPerItem chunks sharing one code replica
+// One workgroup per WORK ITEM: up to kMaxChunksPerItem (4) chunks sharing one code replica
 // (consecutive chunks of one long job, or same-code jobs such as consecutive epochs of one
-// channel).  Per workgroup the replica is staged in LDS once, the sample pipeline runs on across
-// chunk boundaries (the next chunk's first group loads while this chunk's last group is
-// correlated), per-chunk wave sums park in LDS, and one barrier closes the item.
+// channel).  The replica is staged in LDS once per workgroup; then wave w correlates chunk w of the
+// item on its own — 64 samples per lane, a block of four per step with the next block's samples in
+// flight — and reduces it within the wave (no further barrier).
 template <int FMT, int NT, bool IN_MARGIN>
 __global__ __launch_bounds__(kCorrThreads, (corr_waves_per_simd<NT, IN_MARGIN>())) void corr_batch_kernel(const void* __restrict__ samples,
     const DevJob* __restrict__ jobs, const ChunkDesc* __restrict__ chunks, const WorkItem* __restrict__ items, int n_items,
     const Anchor* __restrict__ anchors, float* __restrict__ partials, float* __restrict__ out, AnchorPrefetch pf)
 {
     extern __shared__ __attribute__((aligned(16))) float lds_code[];
-    __shared__ float red[kMaxChunksPerItem][kCorrThreads / 16][2 * NT];  // per chunk: 16 row sums per value
     GNSSHIP_PROF_STAMP(0);
-    // Leading workgroups replay the rotator anchors of ANOTHER batch (the next one of a
-    // double-buffered pair): one lane per job, latency-bound chains that run beside the
-    // correlation instead of in a separate stream behind a cross-queue event.
+    // Leading workgroups replay the rotator anchors of OTHER batches (the next ones of a
+    // pipelined ring): one lane per job, latency-bound chains that run beside the correlation
+    // instead of in a separate stream behind a cross-queue event.
     if (static_cast<int>(blockIdx.x) < pf.n_blocks) {
 #ifndef GNSSHIP_NO_REPLAY_PRIO
         __builtin_amdgcn_s_setprio(3);  // a latency-bound serial chain: first pick of its SIMD's issue slots
@@ -379,25 +408,24 @@ __global__ __launch_bounds__(kCorrThreads, (corr_waves_per_simd<NT, IN_MARGIN>()
     // multiple of 8, so b keeps the hardware's b mod 8 placement.
     const int nb = static_cast<int>(gridDim.x) - pf.n_blocks;
     const int b = blockIdx.x - pf.n_blocks;
-    const int q = nb >> 3, rmd = nb & 7, x = b & 7;
-    const int ii = x * q + (x < rmd ? x : rmd) + (b >> 3);
+    const int q = nb >> 3, rmd = nb & 7, xcd = b & 7;
+    const int ii = xcd * q + (xcd < rmd ? xcd : rmd) + (b >> 3);
     if (ii >= n_items) return;
     const WorkItem it = items[ii];
+    const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x) >> 6), lane = static_cast<int>(threadIdx.x) & (kWave - 1);
     const ChunkDesc c0 = chunks[it.first];
     const int L = c0.code_len;  // one replica for the whole item
     if (L <= 0 || c0.code == nullptr) {  // no code (never happens for a valid plan): outputs zero
-        for (int c = 0; c < it.count; c++) {
-            const ChunkDesc cz = chunks[it.first + c];
+        if (wave < it.count) {
+            const ChunkDesc cz = chunks[it.first + wave];
             const DevJob& jz = jobs[cz.job];
-            float* dz = (jz.n_chunks == 1) ? out + static_cast<int64_t>(cz.job) * 2 * kMaxTaps : partials + static_cast<int64_t>(it.first + c) * 2 * kMaxTaps;
-            if (threadIdx.x < 2 * kMaxTaps) dz[threadIdx.x] = 0.0f;
+            float* dz = (jz.n_chunks == 1) ? out + static_cast<int64_t>(cz.job) * 2 * kMaxTaps : partials + static_cast<int64_t>(it.first + wave) * 2 * kMaxTaps;
+            if (lane < 2 * kMaxTaps) dz[lane] = 0.0f;
         }
         return;
     }
-    // Latency order: the code replica first, loaded straight into LDS (global_load_lds_dwordx4: no
-    // VGPRs, nothing to spill, in flight across the sample prefetch), then this lane's first sample
-    // group, then E_j while both are in flight.  The replica is pre-wrapped in HBM (engine.h:
-    // padded_code_quads): lds[kCodeMargin + i] = code[i mod L], i in [−kCodeMargin, L + kCodeMargin).
+    // The code replica straight into LDS (global_load_lds_dwordx4: no VGPRs), pre-wrapped in HBM
+    // (engine.h padded_code_quads): lds[kCodeMargin + i] = code[i mod L], i in [−kCodeMargin, L + kCodeMargin).
     {
         typedef __attribute__((address_space(1))) const void* gptr;
         typedef __attribute__((address_space(3))) void* lptr;
@@ -410,100 +438,76 @@ __global__ __launch_bounds__(kCorrThreads, (corr_waves_per_simd<NT, IN_MARGIN>()
                 __builtin_amdgcn_global_load_lds((gptr)(src4 + q0 + threadIdx.x), (lptr)(lds4 + q0 + wave_base), 16, 0, 0);
         }
     }
-    f2 xa[kGroup], xb[kGroup];
-    f2 e;
-    {
-        const DevJob& j0 = jobs[c0.job];
-        load_group<FMT>(sample_span<FMT>(samples, j0.sample_offset + c0.start, c0.len), 0, xa);
-        e = anchor_to_lane_rotation(j0);  // ALU work while the loads are in flight
-        // the replica's loads were issued before the kGroup sample loads (vmcnt retires in order)
-        __builtin_amdgcn_s_waitcnt(kWaitVmcntGroup);
-    }
+    // this wave's chunk: an item of 1 or 2 chunks spreads each chunk over 4 or 2 waves (block ranges,
+    // combined in LDS below), so a lone chunk — a closed-loop epoch, the tail of a long job — still
+    // runs on the whole workgroup; the first sample block is in flight while the barrier waits for
+    // the replica
+    const int wpc = it.count >= 3 ? 1 : (it.count == 2 ? 2 : 4);  // waves per chunk (workgroup-uniform)
+    const int cidx = wave / wpc, part = wave - cidx * wpc;
+    const bool active = cidx < it.count;
+    const ChunkDesc ch = chunks[it.first + (active ? cidx : 0)];
+    const DevJob job = jobs[ch.job];
+    const i4v span = sample_span<FMT>(samples, job.sample_offset + ch.start, active ? ch.len : 0);
+    const int nblk_all = active ? (ch.len + kRenorm - 1) / kRenorm : 0;  // blocks of this chunk (0..16)
+    const int per = (nblk_all + wpc - 1) / wpc;
+    const int kb0 = part * per < nblk_all ? part * per : nblk_all;
+    const int kb1 = kb0 + per < nblk_all ? kb0 + per : nblk_all;  // this wave's blocks [kb0, kb1)
+    f2 xa[kLaneSamples], xb[kLaneSamples];
+    if (kb0 < kb1) load_any<FMT>(span, lane, kb0, ch.len, xa);
+    __builtin_amdgcn_s_waitcnt(0);  // the replica's LDS-DMA (and the first block) landed
     __syncthreads();
+    if (!active) return;  // only when wpc == 1: no barrier follows
     GNSSHIP_PROF_STAMP(1);
     const float* code = lds_code + kCodeMargin;
-    int prev_job = c0.job;
-
-    for (int c = 0; c < it.count; c++) {
-        const ChunkDesc ch = chunks[it.first + c];
-        const DevJob job = jobs[ch.job];
-        if (c > 0 && ch.job != prev_job) e = anchor_to_lane_rotation(job);  // same job: same E_j
-        prev_job = ch.job;
-        // only what the next chunk's first sample group needs is carried across the chunk
-        const bool has_next = c + 1 < it.count;
-        i4v next_span = i4v{0, 0, 0, 0x00020000};
-        if (has_next) {
-            const ChunkDesc chn = chunks[it.first + c + 1];
-            next_span = sample_span<FMT>(samples, jobs[chn.job].sample_offset + chn.start, chn.len);
-        }
-        const f2 esw = f2{-e.y, e.x};
-        float shifts[NT];
+    float shifts[NT];
 #pragma unroll
-        for (int t = 0; t < NT; t++) shifts[t] = (t < job.n_taps) ? job.shifts[t] : 0.0f;
-        // the chunk's 16 anchors as one contiguous uniform block (scalar loads, one wait before the
-        // loop: in the loop only in-order LDS reads use lgkmcnt).  Blocks past the chunk end (the
-        // job's tail, padded buffer end) are finite values multiplied by zero samples.
-        const Anchor* anc = anchors + job.anchor_offset + (ch.start >> 8);
-        Anchor qk[kBlocksPerChunk];
+    for (int t = 0; t < NT; t++) shifts[t] = (t < job.n_taps) ? job.shifts[t] : 0.0f;
+    // the block's four uniform phasors (scalar loads; the next block's issued one step ahead —
+    // anchor buffers are padded past the last job)
+    const Anchor* anc = anchors + job.anchor_offset + (ch.start >> 8);
+    f2 acc[NT];
 #pragma unroll
-        for (int m = 0; m < kBlocksPerChunk; m++) qk[m] = anc[m];
-        const i4v span = sample_span<FMT>(samples, job.sample_offset + ch.start, ch.len);
-        const int ng = (ch.len + kGroupSpan - 1) / kGroupSpan;  // groups in this chunk (0..kGroups)
-        GNSSHIP_PROF_STAMP(c == 0 ? 2 : 6);
-        f2 acc[NT];
-#pragma unroll
-        for (int t = 0; t < NT; t++) acc[t] = f2{0.0f, 0.0f};
-        // ping-pong over groups: group g in xa (g even) / xb (g odd); the load issued with group g
-        // is group g+1 of this chunk, or — after the last group — group 0 of the next chunk.
-#pragma unroll
-        for (int g = 0; g < kGroups; g++) {
-            if (g < ng) {  // chunk-uniform
-                f2(&cur)[kGroup] = (g & 1) ? xb : xa;
-                f2(&nxt)[kGroup] = (g & 1) ? xa : xb;
-                if (g + 1 < ng)
-                    load_group<FMT>(span, g + 1, nxt);
-                else if (has_next)
-                    load_group<FMT>(next_span, 0, nxt);
-                if ((g + 1) * kGroupSpan <= ch.len)
-                    correlate_group<NT, IN_MARGIN, true>(job, ch, qk, e, esw, shifts, code, L, g, cur, acc);
-                else
-                    correlate_group<NT, IN_MARGIN, false>(job, ch, qk, e, esw, shifts, code, L, g, cur, acc);
-            }
-        }
-        // next chunk's group 0 sits in buffer ng & 1 → move it to xa (an empty chunk issued none)
-        if (ng == 0 && has_next) load_group<FMT>(next_span, 0, xa);
-        if (ng & 1) {
-#pragma unroll
-            for (int u = 0; u < kGroup; u++) xa[u] = xb[u];
-        }
-        GNSSHIP_PROF_STAMP(c == 0 ? 3 : 7);
-#ifndef GNSSHIP_CORR_NO_EFACTOR
-#pragma unroll
-        for (int t = 0; t < NT; t++) acc[t] = cmul_pk(acc[t], e, esw);  // anchor frame → sample frame (× E_j)
-#endif
-#pragma unroll
-        for (int t = 0; t < NT; t++) {
-            const float wr = row_sum(acc[t].x), wi = row_sum(acc[t].y);
-            if ((threadIdx.x & 15) == 0) {
-                red[c][threadIdx.x >> 4][2 * t] = wr;
-                red[c][threadIdx.x >> 4][2 * t + 1] = wi;
-            }
-        }
+    for (int t = 0; t < NT; t++) acc[t] = f2{0.0f, 0.0f};
+    Anchor A = anc[kb0];
+    // ping-pong over blocks: block kb0 + 2i in xa, kb0 + 2i + 1 in xb
+    for (int kb = kb0; kb < kb1; kb += 2) {
+        const Anchor An = anc[kb + 1];
+        if (kb + 1 < kb1) load_any<FMT>(span, lane, kb + 1, ch.len, xb);
+        if ((kb + 1) * kRenorm <= ch.len)
+            correlate_block<NT, IN_MARGIN, true>(job, ch, A, shifts, code, L, lane, kb, xa, acc);
+        else
+            correlate_block<NT, IN_MARGIN, false>(job, ch, A, shifts, code, L, lane, kb, xa, acc);
+        if (kb + 1 >= kb1) break;
+        A = anc[kb + 2];
+        if (kb + 2 < kb1) load_any<FMT>(span, lane, kb + 2, ch.len, xa);
+        if ((kb + 2) * kRenorm <= ch.len)
+            correlate_block<NT, IN_MARGIN, true>(job, ch, An, shifts, code, L, lane, kb + 1, xb, acc);
+        else
+            correlate_block<NT, IN_MARGIN, false>(job, ch, An, shifts, code, L, lane, kb + 1, xb, acc);
     }
-    __syncthreads();
-    // per-chunk outputs: thread (c, v) sums the 16 row partials of value v of chunk c, in lane order
-    for (int k = threadIdx.x; k < it.count * 2 * kMaxTaps; k += kCorrThreads) {
-        const int c = k / (2 * kMaxTaps), v = k % (2 * kMaxTaps);
-        const ChunkDesc cc = chunks[it.first + c];
-        const DevJob& jc = jobs[cc.job];
-        float* dst = (jc.n_chunks == 1) ? out + static_cast<int64_t>(cc.job) * 2 * kMaxTaps : partials + static_cast<int64_t>(it.first + c) * 2 * kMaxTaps;
-        float s = 0.0f;
-        if (v < 2 * NT && v < 2 * jc.n_taps && cc.len > 0) {
+    GNSSHIP_PROF_STAMP(3);
+    // anchor frame → sample frame (× E_{4·lane}), then the wave's sums (lane v holds value v)
+    const f2 e = lane_rotation(job, kLaneSamples * lane);
+    const f2 esw = f2{-e.y, e.x};
+    float val = 0.0f;
 #pragma unroll
-            for (int w = 0; w < kCorrThreads / 16; w++) s += red[c][w][v];
-        }
-        dst[v] = s;
+    for (int t = 0; t < NT; t++) {
+        const f2 r = cmul_pk(acc[t], e, esw);
+        const float sr = wave_sum(r.x), si = wave_sum(r.y);
+        val = (lane == 2 * t) ? sr : val;
+        val = (lane == 2 * t + 1) ? si : val;
     }
+    if (wpc > 1) {  // the chunk's waves combine in LDS, in block order (deterministic)
+        __shared__ float red[kCorrThreads / kWave][2 * kMaxTaps];
+        if (lane < 2 * kMaxTaps) red[wave][lane] = val;
+        __syncthreads();
+        if (part != 0) return;
+        float sum = 0.0f;
+        for (int w = 0; w < wpc; w++) sum += (lane < 2 * kMaxTaps) ? red[wave + w][lane] : 0.0f;
+        val = sum;
+    }
+    float* dst = (job.n_chunks == 1) ? out + static_cast<int64_t>(ch.job) * 2 * kMaxTaps : partials + static_cast<int64_t>(it.first + cidx) * 2 * kMaxTaps;
+    if (lane < 2 * kMaxTaps) dst[lane] = (lane < 2 * job.n_taps && ch.len > 0) ? val : 0.0f;
     GNSSHIP_PROF_STAMP(4);
 }
 

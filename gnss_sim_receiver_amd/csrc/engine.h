@@ -11,7 +11,7 @@ namespace gnsship {
 
 constexpr int kMaxTaps = GNSSHIP_MAX_TAPS;
 constexpr int kCorrThreads = 256;        // one workgroup = 4 wave64
-constexpr int kCorrSamplesPerThread = 16;
+constexpr int kCorrSamplesPerThread = 16;  // 4096-sample chunk = 64 lanes × 64 samples (one wave per chunk)
 constexpr int kCorrChunk = kCorrThreads * kCorrSamplesPerThread;  // 4096 samples per workgroup
 constexpr int kCorrWavesPerSimd = 4;     // ≥4 resident workgroups per CU (≤128 VGPRs)
 constexpr int kMaxCodeLen = 16384;       // LDS budget for the local code replica (64 KiB + margins)
@@ -59,14 +59,15 @@ constexpr int padded_code_quads(int len) { return (len + 2 * kCodeMargin + 3) / 
 hipError_t upload_padded_code(const float* code, int len, float** chip0);  // allocates; *chip0 = chip 0
 hipError_t free_padded_code(const float* chip0);
 
-// Rotator anchor of one 256-sample block k of a job: the renormalised phasor q = a/|a| the
-// reference rotates from sample 256k on (a = the phasor it multiplies sample 256k by; the
-// correlation uses q·E_j for every lane, including j = 0 — see corr_kernel.hip).
+// Rotator anchor of one 256-sample block k of a job: the phasors the reference rotates samples
+// 256k + s by, s = 0..3 — p[0..1] = the renormalised q = a/|a| (the reference multiplies sample 256k
+// by a = |a|·q; see corr_kernel.hip), p[2s..2s+1] = q·inc^s in the reference's float recursion.
+// A lane covering samples 256k + 4t + s rotates them by p_s · E_{4t}.
 struct Anchor {
-    float q_re, q_im;
+    float p[8];
 };
-// Anchor buffers carry kAnchorPad zero entries past the last job: a chunk reads its 16 anchors as
-// one contiguous scalar block even when its job ends early.
+// Anchor buffers carry kAnchorPad entries past the last job: a wave reads the anchor of the block
+// after its current one unconditionally (scalar prefetch).
 constexpr int kBlocksPerChunk = kCorrChunk / 256;  // renormalisation blocks per chunk (16)
 constexpr int kAnchorPad = kBlocksPerChunk;
 
@@ -81,7 +82,7 @@ struct ChunkDesc {
 // A workgroup's work: chunks [first, first + count) of the (reordered) chunk array, all sharing
 // one code replica (corr_batch_kernel stages it in LDS once per item).
 constexpr int kMaxChunksPerItem = 4;
-constexpr int kChunksPerItemDefault = 2;
+constexpr int kChunksPerItemDefault = 4;
 struct WorkItem {
     int32_t first;
     int32_t count;
@@ -156,6 +157,9 @@ struct HdJob {
     int32_t code_len;
     int32_t pad;
 };
+struct HdAnchor {  // the Doppler chain at sample 256k (unnormalised)
+    float q_re, q_im;
+};
 struct HdChunk {
     int32_t job, start, len, pad;
 };
@@ -167,7 +171,7 @@ struct HdPlan {
     int max_code_len = 1;
     HdJob* jobs_dev = nullptr;
     HdChunk* chunks_dev = nullptr;
-    Anchor* anchors_dev = nullptr;
+    HdAnchor* anchors_dev = nullptr;
     float* partials_dev = nullptr;
     int job_cap = 0, chunk_cap = 0;
     int64_t anchor_cap = 0;

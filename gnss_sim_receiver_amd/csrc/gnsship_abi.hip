@@ -67,7 +67,8 @@ int sync_code_table(gnsship_ctx* ctx)
 //   phase_inc = std::exp(complex<float>(0, -phase_step_rad))     :123  (glibc cexpf → cosf/sinf)
 bool derive_job(const gnsship_corr_job& in, int code_len, DevJob& out)
 {
-    if (in.n_samples < 0 || in.n_taps < 1 || in.n_taps > kMaxTaps || in.sample_offset < 0) return false;
+    // ≤ 2^24 samples per call: (float)n then steps exactly by 1 in the correlator's lanes
+    if (in.n_samples < 0 || in.n_samples > (1 << 24) || in.n_taps < 1 || in.n_taps > kMaxTaps || in.sample_offset < 0) return false;
     if (in.flags & 1) return false;  // high-dynamics variants: not on the device path yet
     const float p0r = std::cos(in.rem_carrier_phase_rad), p0i = -std::sin(in.rem_carrier_phase_rad);
     const float incr = std::cos(-in.phase_step_rad), inci = std::sin(-in.phase_step_rad);
