@@ -214,9 +214,13 @@ __device__ __forceinline__ f2 cmul_pk2_s(f2 x, f2 q)
 // in-range values.
 __device__ __forceinline__ int cvt_floor_i32(float x)
 {
+#ifndef GNSSHIP_FLOOR_TWO_OPS
     int r;
     asm("v_cvt_flr_i32_f32 %0, %1" : "=v"(r) : "v"(x));
     return r;
+#else
+    return static_cast<int>(__builtin_floorf(x));  // v_floor_f32 + v_cvt_i32_f32
+#endif
 }
 
 // Positive modulo of the reference's wrap (volk_gnsssdr_32f_xn_resampler_32f_xn.h:75-77).
@@ -319,26 +323,46 @@ __device__ __forceinline__ void correlate_block(const DevJob& job, const ChunkDe
     float cv[kLaneSamples][NT];
     const int r0 = kb * kRenorm + kLaneSamples * lane;
     const float fn0 = static_cast<float>(ch.start + r0);
+    // (float)n and step·(float)n of the four samples, two per packed operation
+    f2 sn2[kLaneSamples / 2];
+#pragma unroll
+    for (int h = 0; h < kLaneSamples / 2; h++) {
+        f2 fn;
+        if constexpr (FULL) {
+            fn = f2{fn0, fn0} + f2{static_cast<float>(2 * h), static_cast<float>(2 * h + 1)};
+        } else {
+            const int ra = r0 + 2 * h, rb = ra + 1;
+            fn = f2{static_cast<float>(ch.start + (ra < ch.len ? ra : ch.len - 1)), static_cast<float>(ch.start + (rb < ch.len ? rb : ch.len - 1))};
+        }
+        sn2[h] = f2{job.code_step, job.code_step} * fn;  // reference loop counter n, as float
+    }
+    const f2 nrem = f2{-job.rem_code, -job.rem_code};  // x + (−rem) ≡ x − rem, bit for bit
 #pragma unroll
     for (int u = 0; u < kLaneSamples; u++) {
-        const float fn = FULL ? fn0 + static_cast<float>(u) : static_cast<float>(ch.start + (r0 + u < ch.len ? r0 + u : ch.len - 1));
-        const float sn = job.code_step * fn;  // reference loop counter n, as float
+        const float sn = (u & 1) ? sn2[u >> 1].y : sn2[u >> 1].x;
 #pragma unroll
-        for (int t = 0; t < NT; t += 2) {
-            if (t + 1 < NT) {  // two taps per packed add: (sn + shift) + (−rem) ≡ (sn + shift) − rem
-                const f2 v = (f2{sn, sn} + f2{shifts[t], shifts[t + 1]}) + f2{-job.rem_code, -job.rem_code};
-                int i0 = cvt_floor_i32(v.x), i1 = cvt_floor_i32(v.y);
-                if constexpr (!IN_MARGIN) {
-                    i0 = wrap_index(i0, L);
-                    i1 = wrap_index(i1, L);
-                }
-                cv[u][t] = code[i0];
-                cv[u][t + 1] = code[i1];
-            } else {
-                int idx = cvt_floor_i32((sn + shifts[t]) - job.rem_code);
-                if constexpr (!IN_MARGIN) idx = wrap_index(idx, L);
-                cv[u][t] = code[idx];
+        for (int t = 0; t + 1 < NT; t += 2) {  // two taps of one sample per packed add
+            const f2 v = (f2{sn, sn} + f2{shifts[t], shifts[t + 1]}) + nrem;
+            int i0 = cvt_floor_i32(v.x), i1 = cvt_floor_i32(v.y);
+            if constexpr (!IN_MARGIN) {
+                i0 = wrap_index(i0, L);
+                i1 = wrap_index(i1, L);
             }
+            cv[u][t] = code[i0];
+            cv[u][t + 1] = code[i1];
+        }
+    }
+    if constexpr (NT & 1) {  // the odd tap of two samples per packed add
+#pragma unroll
+        for (int h = 0; h < kLaneSamples / 2; h++) {
+            const f2 v = (sn2[h] + f2{shifts[NT - 1], shifts[NT - 1]}) + nrem;
+            int i0 = cvt_floor_i32(v.x), i1 = cvt_floor_i32(v.y);
+            if constexpr (!IN_MARGIN) {
+                i0 = wrap_index(i0, L);
+                i1 = wrap_index(i1, L);
+            }
+            cv[2 * h][NT - 1] = code[i0];
+            cv[2 * h + 1][NT - 1] = code[i1];
         }
     }
     // phase 2: in_common[n]·phase (anchor frame) and the tap sums
@@ -464,21 +488,31 @@ __global__ __launch_bounds__(kCorrThreads, (corr_waves_per_simd<NT, IN_MARGIN>()
     for (int t = 0; t < NT; t++) shifts[t] = (t < job.n_taps) ? job.shifts[t] : 0.0f;
     // the block's four uniform phasors (scalar loads; the next block's issued one step ahead —
     // anchor buffers are padded past the last job)
-    const Anchor* anc = anchors + job.anchor_offset + (ch.start >> 8);
+    // read through the constant address space: scalar loads (this launch never writes the
+    // anchors it correlates with — its replay workgroups write other batches' — but the compiler
+    // cannot prove that and would otherwise load them per lane)
+    typedef __attribute__((address_space(4))) const float* cfloat_ptr;
+    const cfloat_ptr anc_c = (cfloat_ptr)(anchors + job.anchor_offset + (ch.start >> 8));
+    auto anc = [&](int k) {
+        Anchor a;
+#pragma unroll
+        for (int i = 0; i < 8; i++) a.p[i] = anc_c[8 * k + i];
+        return a;
+    };
     f2 acc[NT];
 #pragma unroll
     for (int t = 0; t < NT; t++) acc[t] = f2{0.0f, 0.0f};
-    Anchor A = anc[kb0];
+    Anchor A = anc(kb0);
     // ping-pong over blocks: block kb0 + 2i in xa, kb0 + 2i + 1 in xb
     for (int kb = kb0; kb < kb1; kb += 2) {
-        const Anchor An = anc[kb + 1];
+        const Anchor An = anc(kb + 1);
         if (kb + 1 < kb1) load_any<FMT>(span, lane, kb + 1, ch.len, xb);
         if ((kb + 1) * kRenorm <= ch.len)
             correlate_block<NT, IN_MARGIN, true>(job, ch, A, shifts, code, L, lane, kb, xa, acc);
         else
             correlate_block<NT, IN_MARGIN, false>(job, ch, A, shifts, code, L, lane, kb, xa, acc);
         if (kb + 1 >= kb1) break;
-        A = anc[kb + 2];
+        A = anc(kb + 2);
         if (kb + 2 < kb1) load_any<FMT>(span, lane, kb + 2, ch.len, xa);
         if ((kb + 2) * kRenorm <= ch.len)
             correlate_block<NT, IN_MARGIN, true>(job, ch, An, shifts, code, L, lane, kb + 1, xb, acc);
