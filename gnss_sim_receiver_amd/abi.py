@@ -55,6 +55,8 @@ class AcqConf(ctypes.Structure):
         ("samples_per_chip", ctypes.c_int32),
         ("samples_per_code", ctypes.c_float),
         ("max_prns", ctypes.c_int32),
+        ("consumed_samples", ctypes.c_int32),
+        ("bit_transition_flag", ctypes.c_int32),
     ]
 
 
@@ -169,6 +171,7 @@ _SIGNATURES = {
     "gnsship_batch_destroy": ([_vp], _i),
     "gnsship_acq_create": ([_vp, ctypes.POINTER(AcqConf), _vpp], _i),
     "gnsship_acq_set_grid": ([_vp, _i, _i, _i], _i),
+    "gnsship_acq_set_grid_step2": ([_vp, _f, _f, _i, _f], _i),
     "gnsship_acq_set_local_code": ([_vp, _i, _f32p], _i),
     "gnsship_acq_run": ([_vp, _vp, _i, _i, _i, ctypes.POINTER(AcqResult), _f32p], _i),
     "gnsship_acq_num_bins": ([_vp, ctypes.POINTER(_i)], _i),

@@ -99,6 +99,14 @@ struct gnsship_acq {
     float* grid_dev = nullptr;   // optional |Y|² grid (max_prns × n_bins × N)
     size_t grid_bytes = 0;
     std::vector<char> code_set;
+    int consumed = 0;            // d_consumed_samples: input samples used, the rest zero-padded
+    Step2Spec step2{};           // make_2_steps: step-two grid active
+    RowSpec rows() const
+    {
+        const int N = conf.fft_size;
+        const bool bt = conf.bit_transition_flag != 0;
+        return RowSpec{conf.samples_per_chip, bt ? N / 2 : 0, bt ? N / 2 : N, N};
+    }
 };
 
 static void acq_free_grid_buffers(gnsship_acq* a)
@@ -135,16 +143,12 @@ extern "C" int gnsship_acq_destroy(gnsship_acq* a)
     return GNSSHIP_OK;
 }
 
-// update_grid_doppler_wipeoffs (pcps_acquisition.cc:295-302) with update_local_carrier (:232-245):
-// row i = volk_gnsssdr_s32f_sincos_32fc_generic(−2π·f_i/fs) — cosf/sinf of a float-accumulated
-// phase, computed here on the host with the same libm so the table is bit-identical.
-extern "C" int gnsship_acq_set_grid(gnsship_acq* a, int doppler_max, int doppler_step, int doppler_center)
+// Doppler wipeoff rows: row i = volk_gnsssdr_s32f_sincos_32fc_generic(−2π·f_i/fs) (update_local_carrier,
+// pcps_acquisition.cc:232-245) — cosf/sinf of a float-accumulated phase, computed here on the host
+// with the same libm so the table is bit-identical.
+static int acq_upload_wipeoffs(gnsship_acq* a, int nb, const std::vector<float>& freqs)
 {
-    if (!a) return GNSSHIP_E_INVAL;
     gnsship_ctx* ctx = a->ctx;
-    if (doppler_max < 0 || doppler_step <= 0) return fail(ctx, GNSSHIP_E_INVAL, "gnsship_acq_set_grid: doppler_max >= 0, doppler_step > 0");
-    const int nb = static_cast<int>(std::ceil(static_cast<double>(2 * doppler_max) / static_cast<double>(doppler_step)));  // :261
-    if (nb < 1) return fail(ctx, GNSSHIP_E_INVAL, "gnsship_acq_set_grid: empty Doppler grid");
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     const int N = a->conf.fft_size;
@@ -169,9 +173,7 @@ extern "C" int gnsship_acq_set_grid(gnsship_acq* a, int doppler_max, int doppler
     std::vector<float2> host(static_cast<size_t>(nb) * N);
     const float two_pi = static_cast<float>(2.0 * M_PI);
     for (int i = 0; i < nb; i++) {
-        const int32_t doppler = -doppler_max + doppler_center + doppler_step * i;
-        const float freq = static_cast<float>(doppler);  // + d_doppler_bias (0: CDMA signals)
-        const float step = -(two_pi * freq / static_cast<float>(a->conf.fs_in));
+        const float step = -(two_pi * freqs[i] / static_cast<float>(a->conf.fs_in));
         float ph = 0.0F;
         float2* row = host.data() + static_cast<size_t>(i) * N;
         for (int n = 0; n < N; n++) {
@@ -180,10 +182,46 @@ extern "C" int gnsship_acq_set_grid(gnsship_acq* a, int doppler_max, int doppler
         }
     }
     HIP_TRY(ctx, hipMemcpy(a->wipe, host.data(), sizeof(float2) * host.size(), hipMemcpyHostToDevice));
+    a->dwell_count = 0;
+    return GNSSHIP_OK;
+}
+
+// update_grid_doppler_wipeoffs (pcps_acquisition.cc:295-302): f_i = −dmax + center + step·i (+ GLONASS
+// bias, 0 for CDMA signals), nb = ceil(2·dmax/step) (:261).  Leaves step two.
+extern "C" int gnsship_acq_set_grid(gnsship_acq* a, int doppler_max, int doppler_step, int doppler_center)
+{
+    if (!a) return GNSSHIP_E_INVAL;
+    gnsship_ctx* ctx = a->ctx;
+    if (doppler_max < 0 || doppler_step <= 0) return fail(ctx, GNSSHIP_E_INVAL, "gnsship_acq_set_grid: doppler_max >= 0, doppler_step > 0");
+    const int nb = static_cast<int>(std::ceil(static_cast<double>(2 * doppler_max) / static_cast<double>(doppler_step)));  // :261
+    if (nb < 1) return fail(ctx, GNSSHIP_E_INVAL, "gnsship_acq_set_grid: empty Doppler grid");
+    std::vector<float> f(nb);
+    for (int i = 0; i < nb; i++) f[i] = static_cast<float>(-doppler_max + doppler_center + doppler_step * i);
+    if (int rc = acq_upload_wipeoffs(a, nb, f)) return rc;
     a->conf.doppler_max = doppler_max;
     a->conf.doppler_step = doppler_step;
     a->conf.doppler_center = doppler_center;
-    a->dwell_count = 0;
+    a->step2 = Step2Spec{};
+    return GNSSHIP_OK;
+}
+
+// update_grid_doppler_wipeoffs_step2 (pcps_acquisition.cc:305-312): the narrow grid of make_2_steps,
+// f_i = center + (i − floor(nb2/2))·step2 in float.  Until the next gnsship_acq_set_grid, results
+// report the step-two Doppler (:553-556) and, with the CFAR statistic, divide by the step-one input
+// power passed here (d_input_power is not recomputed in step two, :516-525).
+extern "C" int gnsship_acq_set_grid_step2(gnsship_acq* a, float doppler_center_step_two, float doppler_step2, int num_doppler_bins_step2,
+    float step_one_input_power)
+{
+    if (!a) return GNSSHIP_E_INVAL;
+    if (num_doppler_bins_step2 < 1 || !(doppler_step2 > 0.0f))
+        return fail(a->ctx, GNSSHIP_E_INVAL, "gnsship_acq_set_grid_step2: num_doppler_bins_step2 >= 1, doppler_step2 > 0");
+    std::vector<float> f(num_doppler_bins_step2);
+    for (int i = 0; i < num_doppler_bins_step2; i++) {
+        const float doppler = (static_cast<float>(i) - static_cast<float>(std::floor(num_doppler_bins_step2 / 2.0))) * doppler_step2;
+        f[i] = doppler_center_step_two + doppler;
+    }
+    if (int rc = acq_upload_wipeoffs(a, num_doppler_bins_step2, f)) return rc;
+    a->step2 = Step2Spec{1, doppler_center_step_two, doppler_step2, step_one_input_power};
     return GNSSHIP_OK;
 }
 
@@ -202,6 +240,8 @@ extern "C" int gnsship_acq_create(gnsship_ctx* ctx, const gnsship_acq_conf* conf
             "gnsship_acq_create: fft_size must be 2^a 3^b 5^c: <= 16384, or P*M (P in {16..32}, M <= 1024), or P*M (P in {4..32}, M <= 16384), max 524288");
     if (conf->fs_in <= 0 || conf->max_prns < 1 || conf->max_dwells < 1 || conf->samples_per_chip < 0 || conf->samples_per_code <= 0.0f)
         return fail(ctx, GNSSHIP_E_INVAL, "gnsship_acq_create: bad configuration");
+    if (conf->consumed_samples < 0 || conf->consumed_samples > conf->fft_size || (conf->bit_transition_flag && (conf->fft_size & 1)))
+        return fail(ctx, GNSSHIP_E_INVAL, "gnsship_acq_create: consumed_samples in [0, fft_size]; bit_transition_flag needs an even fft_size");
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     gnsship_acq* a = new (std::nothrow) gnsship_acq();
     if (!a) return GNSSHIP_E_NOMEM;
@@ -211,6 +251,7 @@ extern "C" int gnsship_acq_create(gnsship_ctx* ctx, const gnsship_acq_conf* conf
     a->P = P;
     a->huge = huge;
     a->code_set.assign(conf->max_prns, 0);
+    a->consumed = conf->consumed_samples > 0 ? conf->consumed_samples : conf->fft_size;
     const int N = conf->fft_size;
     std::vector<float2> tw(N);
     for (int t = 0; t < N; t++) {
@@ -260,14 +301,20 @@ extern "C" int gnsship_acq_set_local_code(gnsship_acq* a, int prn_slot, const fl
     if (!code || prn_slot < 0 || prn_slot >= a->conf.max_prns) return fail(ctx, GNSSHIP_E_INVAL, "gnsship_acq_set_local_code: bad slot / code");
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     const int N = a->conf.fft_size;
-    HIP_TRY(ctx, hipMemcpyAsync(a->sig_dev, code, sizeof(float2) * N, hipMemcpyHostToDevice, ctx->stream));
+    // the FFT input buffer as set_local_code fills it (pcps_acquisition.cc:186-203): with
+    // bit_transition_flag [N/2 zeros | code[0, N/2)]; with sampled_ms != ms_per_code
+    // [N − consumed zeros | code[0, consumed)]; else code[0, N)
+    const int n_code = a->conf.bit_transition_flag ? N / 2 : a->consumed;
+    std::vector<float2> buf(static_cast<size_t>(N), make_float2(0.0f, 0.0f));
+    std::memcpy(buf.data() + (N - n_code), code, sizeof(float2) * n_code);
+    HIP_TRY(ctx, hipMemcpyAsync(a->sig_dev, buf.data(), sizeof(float2) * N, hipMemcpyHostToDevice, ctx->stream));
     float2* dst = a->codes_fft + static_cast<size_t>(prn_slot) * N;
     if (a->huge)
-        HIP_TRY(ctx, launch_acq_fft_huge(a->sig_dev, GNSSHIP_FMT_CF32, nullptr, 1, a->P, a->plan, a->tw, a->twM, a->T, dst, 1, ctx->stream));
+        HIP_TRY(ctx, launch_acq_fft_huge(a->sig_dev, GNSSHIP_FMT_CF32, nullptr, 1, a->P, a->plan, a->tw, a->twM, a->T, dst, 1, N, ctx->stream));
     else if (a->P)
-        HIP_TRY(ctx, launch_acq_fft_big(a->sig_dev, GNSSHIP_FMT_CF32, nullptr, 1, a->P, a->plan, a->tw, dst, 1, ctx->stream));
+        HIP_TRY(ctx, launch_acq_fft_big(a->sig_dev, GNSSHIP_FMT_CF32, nullptr, 1, a->P, a->plan, a->tw, dst, 1, N, ctx->stream));
     else
-        HIP_TRY(ctx, launch_acq_fft_rows(a->sig_dev, GNSSHIP_FMT_CF32, nullptr, 1, a->plan, a->tw, dst, 1, ctx->stream));
+        HIP_TRY(ctx, launch_acq_fft_rows(a->sig_dev, GNSSHIP_FMT_CF32, nullptr, 1, a->plan, a->tw, dst, 1, N, ctx->stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     a->code_set[prn_slot] = 1;
     return GNSSHIP_OK;
@@ -288,11 +335,12 @@ extern "C" int gnsship_acq_run(gnsship_acq* a, const void* sig, int fmt, int sig
     const int N = a->conf.fft_size;
     const void* src = sig;
     if (!sig_on_device) {
-        HIP_TRY(ctx, hipMemcpyAsync(a->sig_dev, sig, fmt_bytes(fmt) * N, hipMemcpyHostToDevice, ctx->stream));
+        HIP_TRY(ctx, hipMemcpyAsync(a->sig_dev, sig, fmt_bytes(fmt) * a->consumed, hipMemcpyHostToDevice, ctx->stream));
         src = a->sig_dev;
     }
     const bool keep_grid = (grid != nullptr) || a->conf.max_dwells > 1;
-    const size_t gbytes = sizeof(float) * static_cast<size_t>(a->conf.max_prns) * a->n_bins * N;
+    const RowSpec rs = a->rows();
+    const size_t gbytes = sizeof(float) * static_cast<size_t>(a->conf.max_prns) * a->n_bins * rs.row_len;
     if (keep_grid && a->grid_bytes < gbytes) {
         if (a->grid_dev) HIP_TRY(ctx, hipFree(a->grid_dev));
         a->grid_dev = nullptr;
@@ -304,28 +352,29 @@ extern "C" int gnsship_acq_run(gnsship_acq* a, const void* sig, int fmt, int sig
     const int accumulate = (a->conf.max_dwells > 1 && a->dwell_count > 0) ? 1 : 0;
     a->dwell_count++;
     if (a->huge) {
-        HIP_TRY(ctx, launch_acq_fft_huge(src, fmt, a->wipe, a->n_bins, a->P, a->plan, a->tw, a->twM, a->T, a->X, 0, ctx->stream));
+        HIP_TRY(ctx, launch_acq_fft_huge(src, fmt, a->wipe, a->n_bins, a->P, a->plan, a->tw, a->twM, a->T, a->X, 0, a->consumed, ctx->stream));
         for (int p0 = 0; p0 < n_prns; p0 += a->prn_batch) {
             const int np = std::min(a->prn_batch, n_prns - p0);
-            float* g = keep_grid ? a->grid_dev + static_cast<size_t>(p0) * a->n_bins * N : a->grid_scratch;
+            float* g = keep_grid ? a->grid_dev + static_cast<size_t>(p0) * a->n_bins * rs.row_len : a->grid_scratch;
             HIP_TRY(ctx, launch_acq_search_huge(a->X, a->codes_fft, p0, np, a->n_bins, a->P, a->plan, a->tw, a->twM, a->U, g,
-                             keep_grid ? accumulate : 0, a->tiles, a->conf.samples_per_chip, a->rowstat, ctx->stream));
+                             keep_grid ? accumulate : 0, a->tiles, rs, a->rowstat, ctx->stream));
         }
     } else if (a->P) {
-        HIP_TRY(ctx, launch_acq_fft_big(src, fmt, a->wipe, a->n_bins, a->P, a->plan, a->tw, a->X, 0, ctx->stream));
-        HIP_TRY(ctx, launch_acq_search_big(a->X, a->codes_fft, n_prns, a->n_bins, a->P, a->plan, a->tw, a->conf.samples_per_chip, accumulate,
+        HIP_TRY(ctx, launch_acq_fft_big(src, fmt, a->wipe, a->n_bins, a->P, a->plan, a->tw, a->X, 0, a->consumed, ctx->stream));
+        HIP_TRY(ctx, launch_acq_search_big(a->X, a->codes_fft, n_prns, a->n_bins, a->P, a->plan, a->tw, rs, accumulate,
                          a->rowstat, keep_grid ? a->grid_dev : nullptr, ctx->stream));
     } else {
-        HIP_TRY(ctx, launch_acq_fft_rows(src, fmt, a->wipe, a->n_bins, a->plan, a->tw, a->X, 0, ctx->stream));
-        HIP_TRY(ctx, launch_acq_search(a->X, a->codes_fft, n_prns, a->n_bins, a->plan, a->tw, a->conf.samples_per_chip, accumulate,
+        HIP_TRY(ctx, launch_acq_fft_rows(src, fmt, a->wipe, a->n_bins, a->plan, a->tw, a->X, 0, a->consumed, ctx->stream));
+        HIP_TRY(ctx, launch_acq_search(a->X, a->codes_fft, n_prns, a->n_bins, a->plan, a->tw, rs, accumulate,
                          a->rowstat, keep_grid ? a->grid_dev : nullptr, ctx->stream));
     }
-    HIP_TRY(ctx, launch_acq_decide(a->rowstat, n_prns, a->n_bins, N, a->conf.doppler_max, a->conf.doppler_step, a->conf.doppler_center,
-                     a->dwell_count, a->conf.use_cfar, a->conf.samples_per_code, a->res_dev, ctx->stream));
+    HIP_TRY(ctx, launch_acq_decide(a->rowstat, n_prns, a->n_bins, rs.row_len, a->conf.doppler_max, a->conf.doppler_step, a->conf.doppler_center,
+                     a->dwell_count, a->conf.use_cfar, a->conf.samples_per_code, a->step2, a->res_dev, ctx->stream));
     HIP_TRY(ctx, hipMemcpyAsync(results, a->res_dev, sizeof(gnsship_acq_result) * n_prns, hipMemcpyDeviceToHost, ctx->stream));
     if (grid)
-        HIP_TRY(ctx, hipMemcpyAsync(grid, a->grid_dev, sizeof(float) * static_cast<size_t>(n_prns) * a->n_bins * N, hipMemcpyDeviceToHost,
+        HIP_TRY(ctx, hipMemcpyAsync(grid, a->grid_dev, sizeof(float) * static_cast<size_t>(n_prns) * a->n_bins * rs.row_len, hipMemcpyDeviceToHost,
                          ctx->stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     return GNSSHIP_OK;
 }
+static_assert(sizeof(gnsship_acq_conf) == 56, "gnsship_acq_conf layout (abi.AcqConf)");

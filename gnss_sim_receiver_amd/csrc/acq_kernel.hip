@@ -161,14 +161,14 @@ __device__ void fft_lds(float2* __restrict__ buf, const FftPlan& plan, const flo
 // rows[b] = FFT(sig ⊙ mult[b])  (mult == nullptr: FFT(sig)); conj_out: store conj (code FFT).
 template <int FMT>
 __global__ __launch_bounds__(kAcqThreads) void acq_fft_rows_kernel(const void* __restrict__ sig, const float2* __restrict__ mult,
-    FftPlan plan, const float2* __restrict__ tw, float2* __restrict__ rows, int conj_out)
+    FftPlan plan, const float2* __restrict__ tw, float2* __restrict__ rows, int conj_out, int n_valid)
 {
     extern __shared__ __attribute__((aligned(16))) float2 lds[];
     const int b = blockIdx.x;
     const int N = plan.n;
     const float2* m = mult ? mult + static_cast<int64_t>(b) * N : nullptr;
     for (int i = threadIdx.x; i < N; i += blockDim.x) {
-        float2 x = load_if<FMT>(sig, i);
+        float2 x = i < n_valid ? load_if<FMT>(sig, i) : make_float2(0.0f, 0.0f);  // zero-padded past the consumed samples
         if (m) x = cmulf(x, m[i]);  // volk_32fc_x2_multiply_32fc(in, wipeoff)
         lds[i] = x;
     }
@@ -322,7 +322,7 @@ __device__ __forceinline__ void dft_reg(float2* x, const float2* __restrict__ tw
 // rowsT[b] = transposed FFT(sig ⊙ mult[b]); conj_out for the code spectrum.
 template <int FMT, int P>
 __global__ __launch_bounds__(kAcqThreads) void acq_fft_big_kernel(const void* __restrict__ sig, const float2* __restrict__ mult,
-    FftPlan row_plan, const float2* __restrict__ tw, float2* __restrict__ rowsT, int conj_out)
+    FftPlan row_plan, const float2* __restrict__ tw, float2* __restrict__ rowsT, int conj_out, int n_valid)
 {
     extern __shared__ __attribute__((aligned(16))) float2 lds[];
     const int M = row_plan.n;
@@ -334,7 +334,7 @@ __global__ __launch_bounds__(kAcqThreads) void acq_fft_big_kernel(const void* __
     if (t < M) {
 #pragma unroll
         for (int q = 0; q < P; q++) {
-            float2 x = load_if<FMT>(sig, t + M * q);
+            float2 x = (t + M * q < n_valid) ? load_if<FMT>(sig, t + M * q) : make_float2(0.0f, 0.0f);
             if (m) x = cmulf(x, m[t + M * q]);  // volk_32fc_x2_multiply_32fc(in, wipeoff)
             v[q] = x;
         }
@@ -405,9 +405,11 @@ __device__ __forceinline__ float block_sum(float s, float* red)
     return r;
 }
 
-// grid: (n_bins, n_prns).  rowstat[(p*n_bins + b)] ; grid_out optional [p][b][N].
+// grid: (n_bins, n_prns).  rowstat[(p*n_bins + b)] ; grid_out optional [p][b][row_len].
+// Row = |Y[row_off + i]|², i < row_len (the second half of the transform with bit_transition_flag,
+// pcps_acquisition.cc:663-664); the second-peak window wraps modulo win_mod (d_fft_size, :573-580).
 __global__ __launch_bounds__(kAcqThreads) void acq_search_kernel(const float2* __restrict__ X, const float2* __restrict__ codes_fft,
-    FftPlan plan, const float2* __restrict__ tw, int n_bins, int samples_per_chip, int accumulate, RowStat* __restrict__ rowstat,
+    FftPlan plan, const float2* __restrict__ tw, int n_bins, RowSpec rs, int accumulate, RowStat* __restrict__ rowstat,
     float* __restrict__ grid_out)
 {
     extern __shared__ __attribute__((aligned(16))) float2 lds[];
@@ -421,29 +423,29 @@ __global__ __launch_bounds__(kAcqThreads) void acq_search_kernel(const float2* _
     __syncthreads();
     fft_lds<+1>(lds, plan, tw);
     // |Y|² in place (as float in the .x slot) + optional grid row (accumulated over dwells)
-    float* row = grid_out ? grid_out + (static_cast<int64_t>(p) * n_bins + b) * N : nullptr;
+    float* row = grid_out ? grid_out + (static_cast<int64_t>(p) * n_bins + b) * rs.row_len : nullptr;
     MaxIdx m{-1.0f, 0x7fffffff};
     float s = 0.0f;
-    for (int i = threadIdx.x; i < N; i += blockDim.x) {
-        const float2 y = lds[i];
+    for (int i = threadIdx.x; i < rs.row_len; i += blockDim.x) {
+        const float2 y = lds[rs.row_off + i];
         float mag = __fadd_rn(__fmul_rn(y.x, y.x), __fmul_rn(y.y, y.y));  // volk_32fc_magnitude_squared_32f
         if (row) {
             if (accumulate) mag = __fadd_rn(row[i], mag);  // volk_32f_x2_add_32f
             row[i] = mag;
         }
-        lds[i].x = mag;
+        lds[rs.row_off + i].x = mag;
         m = better(m, MaxIdx{mag, i});
         s += mag;
     }
     const MaxIdx best = block_argmax(m, red_m);
     const float sum = block_sum(s, red_s);
     // second peak outside the circular window [best-spc, best+spc) (first_vs_second_peak_statistic :566-593)
-    int e1 = best.i - samples_per_chip, e2 = best.i + samples_per_chip;
-    if (e1 < 0) e1 += N; else if (e2 >= N) e2 -= N;
+    int e1 = best.i - rs.spc, e2 = best.i + rs.spc;
+    if (e1 < 0) e1 += rs.win_mod; else if (e2 >= rs.win_mod) e2 -= rs.win_mod;
     MaxIdx m2{0.0f, 0x7fffffff};
-    for (int i = threadIdx.x; i < N; i += blockDim.x) {
+    for (int i = threadIdx.x; i < rs.row_len; i += blockDim.x) {
         const bool in_win = (e1 < e2) ? (i >= e1 && i < e2) : (i >= e1 || i < e2);
-        const float v = in_win ? 0.0f : lds[i].x;
+        const float v = in_win ? 0.0f : lds[rs.row_off + i].x;
         m2 = better(m2, MaxIdx{v, i});
     }
     const MaxIdx second = block_argmax(m2, red_m);
@@ -462,7 +464,7 @@ __global__ __launch_bounds__(kAcqThreads) void acq_search_kernel(const float2* _
 // y[t + M·q] for q < P, i.e. the natural index n = t + M·q.
 template <int P>
 __global__ __launch_bounds__(kAcqThreads) void acq_search_big_kernel(const float2* __restrict__ XT, const float2* __restrict__ codesT,
-    FftPlan row_plan, const float2* __restrict__ tw, int n_bins, int samples_per_chip, int accumulate, RowStat* __restrict__ rowstat,
+    FftPlan row_plan, const float2* __restrict__ tw, int n_bins, RowSpec rs, int accumulate, RowStat* __restrict__ rowstat,
     float* __restrict__ grid_out)
 {
     extern __shared__ __attribute__((aligned(16))) float2 lds[];
@@ -501,32 +503,29 @@ __global__ __launch_bounds__(kAcqThreads) void acq_search_big_kernel(const float
     float s = 0.0f;
     if (t < M) {
         dft_reg<P, 1, +1>(v, tw, N);
-        float* row = grid_out ? grid_out + (static_cast<int64_t>(p) * n_bins + b) * N : nullptr;
+        float* row = grid_out ? grid_out + (static_cast<int64_t>(p) * n_bins + b) * rs.row_len : nullptr;
 #pragma unroll
         for (int q = 0; q < P; q++) {
-            const int n = t + M * q;
+            const int i = t + M * q - rs.row_off;  // index in the row
+            if (i < 0 || i >= rs.row_len) continue;
             float g = __fadd_rn(__fmul_rn(v[q].x, v[q].x), __fmul_rn(v[q].y, v[q].y));  // volk_32fc_magnitude_squared_32f
             if (row) {
-                if (accumulate) g = __fadd_rn(row[n], g);  // volk_32f_x2_add_32f
-                row[n] = g;
+                if (accumulate) g = __fadd_rn(row[i], g);  // volk_32f_x2_add_32f
+                row[i] = g;
             }
-            mag[n] = g;
-            m = better(m, MaxIdx{g, n});
+            mag[i] = g;
+            m = better(m, MaxIdx{g, i});
             s += g;
         }
     }
     const MaxIdx best = block_argmax(m, red_m);
     const float sum = block_sum(s, red_s);
-    int e1 = best.i - samples_per_chip, e2 = best.i + samples_per_chip;
-    if (e1 < 0) e1 += N; else if (e2 >= N) e2 -= N;
+    int e1 = best.i - rs.spc, e2 = best.i + rs.spc;
+    if (e1 < 0) e1 += rs.win_mod; else if (e2 >= rs.win_mod) e2 -= rs.win_mod;
     MaxIdx m2{0.0f, 0x7fffffff};
-    if (t < M) {
-#pragma unroll
-        for (int q = 0; q < P; q++) {
-            const int n = t + M * q;
-            const bool in_win = (e1 < e2) ? (n >= e1 && n < e2) : (n >= e1 || n < e2);
-            m2 = better(m2, MaxIdx{in_win ? 0.0f : mag[n], n});
-        }
+    for (int i = t; i < rs.row_len; i += kAcqThreads) {
+        const bool in_win = (e1 < e2) ? (i >= e1 && i < e2) : (i >= e1 || i < e2);
+        m2 = better(m2, MaxIdx{in_win ? 0.0f : mag[i], i});
     }
     const MaxIdx second = block_argmax(m2, red_m);
     if (t == 0) {
@@ -540,8 +539,10 @@ __global__ __launch_bounds__(kAcqThreads) void acq_search_big_kernel(const float
 }
 
 // One thread per PRN: the reference's row scan (strict >, ascending bin) and decision values.
+// Step two of make_2_steps (step2.active): Doppler = (int)(center + (bin − floor(nb/2))·step2) in float
+// and the CFAR input power left at its step-one value (pcps_acquisition.cc:516-525).
 __global__ void acq_decide_kernel(const RowStat* __restrict__ rowstat, int n_prns, int n_bins, int N, int doppler_max, int doppler_step,
-    int doppler_center, int dwells, int use_cfar, float samples_per_code, gnsship_acq_result* __restrict__ out)
+    int doppler_center, int dwells, int use_cfar, float samples_per_code, Step2Spec step2, gnsship_acq_result* __restrict__ out)
 {
     const int p = blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= n_prns) return;
@@ -559,8 +560,13 @@ __global__ void acq_decide_kernel(const RowStat* __restrict__ rowstat, int n_prn
     r.doppler_index = static_cast<uint32_t>(bi);
     r.code_index = static_cast<uint32_t>(ti);
     r.doppler_hz = -doppler_max + doppler_center + doppler_step * bi;
+    if (step2.active)
+        r.doppler_hz = static_cast<int32_t>(step2.center + (static_cast<float>(bi) - static_cast<float>(floor(n_bins / 2.0))) * step2.step);
     r.peak = gmax;
-    if (use_cfar) {
+    if (use_cfar && step2.active) {
+        r.input_power = step2.input_power;
+        r.test_statistic = gmax / r.input_power;
+    } else if (use_cfar) {
         const int opp = (bi + n_bins / 2) % n_bins;
         // (float)(sum / N / 2.0 / dwells)  (pcps_acquisition.cc:518)
         const float s = rs[opp].sum;
@@ -592,7 +598,7 @@ constexpr int kHugeColThreads = 256;
 
 template <int FMT, int P>
 __global__ __launch_bounds__(kHugeColThreads) void acq_huge_cols_fwd_kernel(const void* __restrict__ sig, const float2* __restrict__ mult,
-    int M, const float2* __restrict__ twN, float2* __restrict__ T)
+    int M, const float2* __restrict__ twN, float2* __restrict__ T, int n_valid)
 {
     const int m = blockIdx.x * kHugeColThreads + threadIdx.x;
     const int b = blockIdx.y;
@@ -602,7 +608,7 @@ __global__ __launch_bounds__(kHugeColThreads) void acq_huge_cols_fwd_kernel(cons
     float2 v[P];
 #pragma unroll
     for (int q = 0; q < P; q++) {
-        float2 x = load_if<FMT>(sig, m + M * q);
+        float2 x = (m + M * q < n_valid) ? load_if<FMT>(sig, m + M * q) : make_float2(0.0f, 0.0f);
         if (w) x = cmulf(x, w[m + M * q]);  // volk_32fc_x2_multiply_32fc(in, wipeoff)
         v[q] = x;
     }
@@ -640,7 +646,7 @@ __global__ __launch_bounds__(kAcqThreads) void acq_huge_rows_kernel(const float2
 // g = grid + (z·n_bins + y)·N (accumulated over dwells when `accumulate`), tile statistics.
 template <int P>
 __global__ __launch_bounds__(kHugeColThreads) void acq_huge_cols_inv_kernel(const float2* __restrict__ U, int M, int n_bins,
-    const float2* __restrict__ twN, float* __restrict__ grid, int accumulate, TileStat* __restrict__ tiles)
+    const float2* __restrict__ twN, float* __restrict__ grid, int accumulate, TileStat* __restrict__ tiles, RowSpec rs)
 {
     __shared__ MaxIdx red_m[kHugeColThreads / 64];
     __shared__ float red_s[kHugeColThreads / 64];
@@ -663,10 +669,11 @@ __global__ __launch_bounds__(kHugeColThreads) void acq_huge_cols_inv_kernel(cons
             v[kq] = x;
         }
         dft_reg<P, 1, +1>(v, twN, N);
-        float* g = grid + cell * N;
+        float* g = grid + cell * rs.row_len;
 #pragma unroll
         for (int q = 0; q < P; q++) {
-            const int n = m + M * q;
+            const int n = m + M * q - rs.row_off;  // index in the row
+            if (n < 0 || n >= rs.row_len) continue;
             float mag = __fadd_rn(__fmul_rn(v[q].x, v[q].x), __fmul_rn(v[q].y, v[q].y));  // volk_32fc_magnitude_squared_32f
             if (accumulate) mag = __fadd_rn(g[n], mag);                                      // volk_32f_x2_add_32f
             g[n] = mag;
@@ -681,7 +688,7 @@ __global__ __launch_bounds__(kHugeColThreads) void acq_huge_cols_inv_kernel(cons
 
 // Row statistics of cell (prn blockIdx.y, bin blockIdx.x) from its tiles and grid row.
 __global__ __launch_bounds__(kAcqThreads) void acq_huge_finalize_kernel(const float* __restrict__ grid, const TileStat* __restrict__ tiles,
-    int n_tiles, int N, int n_bins, int prn_offset, int samples_per_chip, RowStat* __restrict__ rowstat)
+    int n_tiles, int n_bins, int prn_offset, RowSpec rs, RowStat* __restrict__ rowstat)
 {
     __shared__ MaxIdx red_m[kAcqThreads / 64];
     __shared__ float red_s[kAcqThreads / 64];
@@ -695,11 +702,11 @@ __global__ __launch_bounds__(kAcqThreads) void acq_huge_finalize_kernel(const fl
     }
     const MaxIdx best = block_argmax(m, red_m);
     const float sum = block_sum(s, red_s);
-    int e1 = best.i - samples_per_chip, e2 = best.i + samples_per_chip;
-    if (e1 < 0) e1 += N; else if (e2 >= N) e2 -= N;
-    const float* g = grid + cell * N;
+    int e1 = best.i - rs.spc, e2 = best.i + rs.spc;
+    if (e1 < 0) e1 += rs.win_mod; else if (e2 >= rs.win_mod) e2 -= rs.win_mod;
+    const float* g = grid + cell * rs.row_len;
     MaxIdx m2{0.0f, 0x7fffffff};
-    for (int i = threadIdx.x; i < N; i += kAcqThreads) {
+    for (int i = threadIdx.x; i < rs.row_len; i += kAcqThreads) {
         const bool in_win = (e1 < e2) ? (i >= e1 && i < e2) : (i >= e1 || i < e2);
         m2 = better(m2, MaxIdx{in_win ? 0.0f : g[i], i});
     }
@@ -718,7 +725,7 @@ bool huge_p_supported(int P)
 }
 
 hipError_t launch_acq_fft_huge(const void* sig, int fmt, const float2* mult, int n_rows, int P, const FftPlan& row_plan, const float2* twN,
-    const float2* twM, float2* scratch, float2* rowsT, int conj_out, hipStream_t stream)
+    const float2* twM, float2* scratch, float2* rowsT, int conj_out, int n_valid, hipStream_t stream)
 {
     const int M = row_plan.n;
     const int64_t N = static_cast<int64_t>(P) * M;
@@ -727,13 +734,13 @@ hipError_t launch_acq_fft_huge(const void* sig, int fmt, const float2* mult, int
     case p:                                                                                                                               \
         if (fmt == GNSSHIP_FMT_CF32)                                                                                                      \
             hipLaunchKernelGGL((acq_huge_cols_fwd_kernel<GNSSHIP_FMT_CF32, p>), cgrid, dim3(kHugeColThreads), 0, stream, sig, mult, M, twN, \
-                scratch);                                                                                                                 \
+                scratch, n_valid);                                                                                                                 \
         else if (fmt == GNSSHIP_FMT_CI16)                                                                                                 \
             hipLaunchKernelGGL((acq_huge_cols_fwd_kernel<GNSSHIP_FMT_CI16, p>), cgrid, dim3(kHugeColThreads), 0, stream, sig, mult, M, twN, \
-                scratch);                                                                                                                 \
+                scratch, n_valid);                                                                                                                 \
         else if (fmt == GNSSHIP_FMT_CI8)                                                                                                  \
             hipLaunchKernelGGL((acq_huge_cols_fwd_kernel<GNSSHIP_FMT_CI8, p>), cgrid, dim3(kHugeColThreads), 0, stream, sig, mult, M, twN,  \
-                scratch);                                                                                                                 \
+                scratch, n_valid);                                                                                                                 \
         else                                                                                                                              \
             return hipErrorInvalidValue;                                                                                                  \
         break;
@@ -751,7 +758,7 @@ hipError_t launch_acq_fft_huge(const void* sig, int fmt, const float2* mult, int
 }
 
 hipError_t launch_acq_search_huge(const float2* XT, const float2* codesT, int prn_offset, int n_prns, int n_bins, int P, const FftPlan& row_plan,
-    const float2* twN, const float2* twM, float2* U, float* grid, int accumulate, TileStat* tiles, int samples_per_chip, RowStat* rowstat,
+    const float2* twN, const float2* twM, float2* U, float* grid, int accumulate, TileStat* tiles, RowSpec rs, RowStat* rowstat,
     hipStream_t stream)
 {
     const int M = row_plan.n;
@@ -767,7 +774,7 @@ hipError_t launch_acq_search_huge(const float2* XT, const float2* codesT, int pr
 #define GNSSHIP_P_CASE(p)                                                                                                              \
     case p:                                                                                                                            \
         hipLaunchKernelGGL((acq_huge_cols_inv_kernel<p>), cgrid, dim3(kHugeColThreads), 0, stream, U, M, n_bins, twN, grid, accumulate, \
-            tiles);                                                                                                                    \
+            tiles, rs);                                                                                                                    \
         break;
     switch (P) {
         GNSSHIP_HUGE_P_LIST(GNSSHIP_P_CASE)
@@ -776,24 +783,24 @@ hipError_t launch_acq_search_huge(const float2* XT, const float2* codesT, int pr
 #undef GNSSHIP_P_CASE
     e = hipGetLastError();
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(acq_huge_finalize_kernel, dim3(n_bins, n_prns), dim3(kAcqThreads), 0, stream, grid, tiles, n_tiles, static_cast<int>(N), n_bins,
-        prn_offset, samples_per_chip, rowstat);
+    hipLaunchKernelGGL(acq_huge_finalize_kernel, dim3(n_bins, n_prns), dim3(kAcqThreads), 0, stream, grid, tiles, n_tiles, n_bins, prn_offset, rs,
+        rowstat);
     return hipGetLastError();
 }
 
 hipError_t launch_acq_fft_rows(const void* sig, int fmt, const float2* mult, int n_rows, const FftPlan& plan, const float2* tw, float2* rows,
-    int conj_out, hipStream_t stream)
+    int conj_out, int n_valid, hipStream_t stream)
 {
     const size_t lds = sizeof(float2) * static_cast<size_t>(plan.n);
     switch (fmt) {
     case GNSSHIP_FMT_CF32:
-        hipLaunchKernelGGL(acq_fft_rows_kernel<GNSSHIP_FMT_CF32>, dim3(n_rows), dim3(kAcqThreads), lds, stream, sig, mult, plan, tw, rows, conj_out);
+        hipLaunchKernelGGL(acq_fft_rows_kernel<GNSSHIP_FMT_CF32>, dim3(n_rows), dim3(kAcqThreads), lds, stream, sig, mult, plan, tw, rows, conj_out, n_valid);
         break;
     case GNSSHIP_FMT_CI16:
-        hipLaunchKernelGGL(acq_fft_rows_kernel<GNSSHIP_FMT_CI16>, dim3(n_rows), dim3(kAcqThreads), lds, stream, sig, mult, plan, tw, rows, conj_out);
+        hipLaunchKernelGGL(acq_fft_rows_kernel<GNSSHIP_FMT_CI16>, dim3(n_rows), dim3(kAcqThreads), lds, stream, sig, mult, plan, tw, rows, conj_out, n_valid);
         break;
     case GNSSHIP_FMT_CI8:
-        hipLaunchKernelGGL(acq_fft_rows_kernel<GNSSHIP_FMT_CI8>, dim3(n_rows), dim3(kAcqThreads), lds, stream, sig, mult, plan, tw, rows, conj_out);
+        hipLaunchKernelGGL(acq_fft_rows_kernel<GNSSHIP_FMT_CI8>, dim3(n_rows), dim3(kAcqThreads), lds, stream, sig, mult, plan, tw, rows, conj_out, n_valid);
         break;
     default: return hipErrorInvalidValue;
     }
@@ -801,11 +808,11 @@ hipError_t launch_acq_fft_rows(const void* sig, int fmt, const float2* mult, int
 }
 
 hipError_t launch_acq_search(const float2* X, const float2* codes_fft, int n_prns, int n_bins, const FftPlan& plan, const float2* tw,
-    int samples_per_chip, int accumulate, RowStat* rowstat, float* grid, hipStream_t stream)
+    RowSpec rs, int accumulate, RowStat* rowstat, float* grid, hipStream_t stream)
 {
     const size_t lds = sizeof(float2) * static_cast<size_t>(plan.n);
     hipLaunchKernelGGL(acq_search_kernel, dim3(n_bins, n_prns), dim3(kAcqThreads), lds, stream, X, codes_fft, plan, tw, n_bins,
-        samples_per_chip, accumulate, rowstat, grid);
+        rs, accumulate, rowstat, grid);
     return hipGetLastError();
 }
 
@@ -820,7 +827,7 @@ bool big_p_supported(int P)
 }
 
 hipError_t launch_acq_fft_big(const void* sig, int fmt, const float2* mult, int n_rows, int P, const FftPlan& row_plan, const float2* tw,
-    float2* rowsT, int conj_out, hipStream_t stream)
+    float2* rowsT, int conj_out, int n_valid, hipStream_t stream)
 {
     const size_t lds = 2 * sizeof(float2) * static_cast<size_t>(kBigRows) * row_plan.n;
     if (row_plan.n > kAcqThreads) return hipErrorInvalidValue;
@@ -828,13 +835,13 @@ hipError_t launch_acq_fft_big(const void* sig, int fmt, const float2* mult, int 
     case p:                                                                                                                          \
         if (fmt == GNSSHIP_FMT_CF32)                                                                                                 \
             hipLaunchKernelGGL((acq_fft_big_kernel<GNSSHIP_FMT_CF32, p>), dim3(n_rows), dim3(kAcqThreads), lds, stream, sig, mult,   \
-                row_plan, tw, rowsT, conj_out);                                                                                      \
+                row_plan, tw, rowsT, conj_out, n_valid);                                                                                      \
         else if (fmt == GNSSHIP_FMT_CI16)                                                                                            \
             hipLaunchKernelGGL((acq_fft_big_kernel<GNSSHIP_FMT_CI16, p>), dim3(n_rows), dim3(kAcqThreads), lds, stream, sig, mult,   \
-                row_plan, tw, rowsT, conj_out);                                                                                      \
+                row_plan, tw, rowsT, conj_out, n_valid);                                                                                      \
         else if (fmt == GNSSHIP_FMT_CI8)                                                                                             \
             hipLaunchKernelGGL((acq_fft_big_kernel<GNSSHIP_FMT_CI8, p>), dim3(n_rows), dim3(kAcqThreads), lds, stream, sig, mult,    \
-                row_plan, tw, rowsT, conj_out);                                                                                      \
+                row_plan, tw, rowsT, conj_out, n_valid);                                                                                      \
         else                                                                                                                         \
             return hipErrorInvalidValue;                                                                                             \
         break;
@@ -847,14 +854,14 @@ hipError_t launch_acq_fft_big(const void* sig, int fmt, const float2* mult, int 
 }
 
 hipError_t launch_acq_search_big(const float2* XT, const float2* codesT, int n_prns, int n_bins, int P, const FftPlan& row_plan,
-    const float2* tw, int samples_per_chip, int accumulate, RowStat* rowstat, float* grid, hipStream_t stream)
+    const float2* tw, RowSpec rs, int accumulate, RowStat* rowstat, float* grid, hipStream_t stream)
 {
     const size_t lds = 2 * sizeof(float2) * static_cast<size_t>(kBigRows) * row_plan.n;
     if (row_plan.n > kAcqThreads) return hipErrorInvalidValue;
 #define GNSSHIP_P_CASE(p)                                                                                                            \
     case p:                                                                                                                          \
         hipLaunchKernelGGL((acq_search_big_kernel<p>), dim3(n_bins, n_prns), dim3(kAcqThreads), lds, stream, XT, codesT, row_plan, tw, \
-            n_bins, samples_per_chip, accumulate, rowstat, grid);                                                                    \
+            n_bins, rs, accumulate, rowstat, grid);                                                                    \
         break;
     switch (P) {
         GNSSHIP_BIG_P_LIST(GNSSHIP_P_CASE)
@@ -865,10 +872,10 @@ hipError_t launch_acq_search_big(const float2* XT, const float2* codesT, int n_p
 }
 
 hipError_t launch_acq_decide(const RowStat* rowstat, int n_prns, int n_bins, int N, int doppler_max, int doppler_step, int doppler_center,
-    int dwells, int use_cfar, float samples_per_code, gnsship_acq_result* out, hipStream_t stream)
+    int dwells, int use_cfar, float samples_per_code, Step2Spec step2, gnsship_acq_result* out, hipStream_t stream)
 {
     hipLaunchKernelGGL(acq_decide_kernel, dim3((n_prns + 63) / 64), dim3(64), 0, stream, rowstat, n_prns, n_bins, N, doppler_max, doppler_step,
-        doppler_center, dwells, use_cfar, samples_per_code, out);
+        doppler_center, dwells, use_cfar, samples_per_code, step2, out);
     return hipGetLastError();
 }
 

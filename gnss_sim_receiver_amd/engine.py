@@ -260,7 +260,8 @@ class PcpsAcquisition:
 
     def __init__(self, ctx: Context, fs_in: int, fft_size: int, doppler_max: int, doppler_step: int, doppler_center: int = 0,
                  use_cfar: bool = True, samples_per_chip: int = None, samples_per_code: float = None, max_prns: int = 1,
-                 max_dwells: int = 1, chip_rate: float = 1023000.0, ms_per_code: int = 1):
+                 max_dwells: int = 1, chip_rate: float = 1023000.0, ms_per_code: int = 1, consumed_samples: int = 0,
+                 bit_transition_flag: bool = False):
         self.ctx = ctx
         conf = abi.AcqConf()
         conf.fs_in = fs_in
@@ -275,7 +276,12 @@ class PcpsAcquisition:
         conf.samples_per_chip = int(np.ceil(np.float32(fs_in) / np.float32(chip_rate))) if samples_per_chip is None else samples_per_chip
         conf.samples_per_code = float(np.float32(spms * np.float32(ms_per_code))) if samples_per_code is None else samples_per_code
         conf.max_prns = max_prns
+        conf.consumed_samples = consumed_samples
+        conf.bit_transition_flag = int(bit_transition_flag)
         self.conf = conf
+        self.consumed = consumed_samples or fft_size
+        self.code_len = fft_size // 2 if bit_transition_flag else self.consumed  # samples set_local_code reads
+        self.row_len = fft_size // 2 if bit_transition_flag else fft_size       # grid row length
         h = ctypes.c_void_p()
         check(ctx.lib.gnsship_acq_create(ctx.h, ctypes.byref(conf), ctypes.byref(h)), "gnsship_acq_create", ctx.h)
         self.h = h
@@ -289,17 +295,27 @@ class PcpsAcquisition:
         check(self.ctx.lib.gnsship_acq_num_bins(self.h, ctypes.byref(nb)), "gnsship_acq_num_bins", self.ctx.h)
         self.n_bins = nb.value
 
+    def set_grid_step2(self, doppler_center_step_two: float, doppler_step2: float, num_doppler_bins_step2: int,
+                       step_one_input_power: float):
+        """update_grid_doppler_wipeoffs_step2 (pcps_acquisition.cc:305-312): make_2_steps' narrow grid."""
+        check(self.ctx.lib.gnsship_acq_set_grid_step2(self.h, doppler_center_step_two, doppler_step2, num_doppler_bins_step2,
+                                                      step_one_input_power), "gnsship_acq_set_grid_step2", self.ctx.h)
+        nb = ctypes.c_int()
+        check(self.ctx.lib.gnsship_acq_num_bins(self.h, ctypes.byref(nb)), "gnsship_acq_num_bins", self.ctx.h)
+        self.n_bins = nb.value
+
     def set_local_code(self, code: np.ndarray, prn_slot: int = 0):
         code = np.ascontiguousarray(code, np.complex64)
-        if len(code) != self.conf.fft_size:
-            raise ValueError("local code must have fft_size samples")
+        if len(code) < self.code_len:
+            raise ValueError(f"local code must have at least {self.code_len} samples")
+        code = np.ascontiguousarray(code[: self.code_len])
         check(self.ctx.lib.gnsship_acq_set_local_code(self.h, prn_slot, fptr(code.view(np.float32))), "gnsship_acq_set_local_code",
               self.ctx.h)
 
     def run(self, sig, n_prns: int = 1, want_grid: bool = False, fmt: int = None):
         """sig: host ndarray (CF32/CI16/CI8) or DeviceBuffer (then pass fmt)."""
         res = (abi.AcqResult * n_prns)()
-        grid = np.zeros((n_prns, self.n_bins, self.conf.fft_size), np.float32) if want_grid else None
+        grid = np.zeros((n_prns, self.n_bins, self.row_len), np.float32) if want_grid else None
         if isinstance(sig, DeviceBuffer):
             ptr, on_dev, f = sig.ptr, 1, FMT_CF32 if fmt is None else fmt
         else:

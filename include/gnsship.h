@@ -176,6 +176,11 @@ typedef struct gnsship_acq_conf {
     int32_t samples_per_chip;   /* ceil(fs / chip_rate)                                       */
     float samples_per_code;     /* samples_per_ms * ms_per_code                               */
     int32_t max_prns;           /* number of local-code slots (PRNs searched per call)        */
+    int32_t consumed_samples;   /* d_consumed_samples (:71): input samples per dwell, the rest of
+                                   the fft_size buffer zero-padded (sampled_ms != ms_per_code:
+                                   fft_size = 2 x consumed, :84-91); 0 = fft_size              */
+    int32_t bit_transition_flag; /* code in the second half after N/2 zeros, grid rows = the
+                                   second half of |IFFT|^2 (:187-192, :663-664)                 */
 } gnsship_acq_conf;
 
 /* What acquisition_core leaves in Gnss_Synchro + block members (pcps_acquisition.cc:683-696). */
@@ -193,8 +198,15 @@ int gnsship_acq_create(gnsship_ctx* ctx, const gnsship_acq_conf* conf, gnsship_a
 /* Rebuild the Doppler wipeoff table (update_grid_doppler_wipeoffs): row i is exp(j*phi_n),
  * phi accumulated in float32 exactly as volk_gnsssdr_s32f_sincos_32fc_generic. */
 int gnsship_acq_set_grid(gnsship_acq* a, int doppler_max, int doppler_step, int doppler_center);
-/* set_local_code: `code` is fft_size complex<float> (sampled, replicated); FFT + conj on device. */
+/* set_local_code (:175-208): `code` is the sampled code, complex<float>: fft_size/2 values with
+ * bit_transition_flag, else consumed_samples values (zero-padded in front to fft_size); FFT + conj on device. */
 int gnsship_acq_set_local_code(gnsship_acq* a, int prn_slot, const float* code);
+/* update_grid_doppler_wipeoffs_step2 (:305-312), make_2_steps: nb2 bins around the step-one Doppler.
+ * Results then carry the step-two Doppler (:553-556); with CFAR the statistic divides by
+ * step_one_input_power, as the reference leaves d_input_power at its step-one value (:516-525).
+ * gnsship_acq_set_grid returns to step one. */
+int gnsship_acq_set_grid_step2(gnsship_acq* a, float doppler_center_step_two, float doppler_step2, int num_doppler_bins_step2,
+    float step_one_input_power);
 /* acquisition_core over prn slots [0, n_prns): one dwell of fft_size samples, all bins.
  * results[n_prns]; grid (optional, host, n_prns*n_bins*fft_size floats) receives |IFFT|^2. */
 int gnsship_acq_run(gnsship_acq* a, const void* sig, int fmt, int sig_on_device, int n_prns,

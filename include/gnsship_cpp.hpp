@@ -145,6 +145,10 @@ struct Acq_Conf {
     int32_t doppler_max{5000};
     bool bit_transition_flag{false};
     bool use_CFAR_algorithm_flag{true};
+    bool make_2_steps{false};
+    float doppler_step2{125.0};
+    uint32_t num_doppler_bins_step2{4U};
+    float pfa2{0.0};
     // derived
     float samples_per_ms{0.0};
     float samples_per_code{0.0};
@@ -153,7 +157,7 @@ struct Acq_Conf {
     {
         if (pfa < 0.0F || pfa > 1.0F) pfa = 0.0F;       // acq_conf.cc:63-67
         if (pfa <= 0.0F) use_CFAR_algorithm_flag = false;  // :75-79
-        if (bit_transition_flag) throw std::invalid_argument("gnsship: bit_transition_flag is not supported by the HIP PCPS core yet");
+        if (pfa2 <= 0.0F || pfa2 > 1.0F) pfa2 = pfa;
         samples_per_ms = static_cast<float>(fs_in) * 0.001F;
         samples_per_chip = static_cast<unsigned int>(std::ceil(static_cast<float>(fs_in) / static_cast<float>(chips_per_second)));
         samples_per_code = samples_per_ms * static_cast<float>(ms_per_code);
@@ -215,10 +219,14 @@ public:
     explicit Pcps_Acquisition_Hip(const Acq_Conf& conf, int device = 0) : conf_(conf), dev_(Device::get(device))
     {
         conf_.SetDerivedParams();
-        fft_size_ = static_cast<int>(conf_.sampled_ms * static_cast<uint32_t>(conf_.samples_per_ms));  // :71, :84-91
+        // d_consumed_samples (:71), d_fft_size (:84-91)
+        consumed_ = static_cast<int>(conf_.sampled_ms * conf_.samples_per_ms * (conf_.bit_transition_flag ? 2.0 : 1.0));
+        fft_size_ = conf_.sampled_ms == conf_.ms_per_code ? consumed_ : 2 * consumed_;
         gnsship_acq_conf c{};
         c.fs_in = conf_.fs_in;
         c.fft_size = fft_size_;
+        c.consumed_samples = consumed_;
+        c.bit_transition_flag = conf_.bit_transition_flag ? 1 : 0;
         c.doppler_max = conf_.doppler_max;
         c.doppler_step = static_cast<int32_t>(conf_.doppler_step);
         c.doppler_center = 0;
@@ -240,7 +248,8 @@ public:
     void set_doppler_max(uint32_t doppler_max) { conf_.doppler_max = static_cast<int32_t>(doppler_max); }
     void set_doppler_step(uint32_t doppler_step) { doppler_step_ = doppler_step; }
     void set_doppler_center(int32_t doppler_center) { doppler_center_ = doppler_center; }
-    // set_local_code (:175-208): FFT of the sampled code + conjugate, on the device
+    int consumed_samples() const { return consumed_; }
+    // set_local_code (:175-208): FFT of the zero-padded sampled code + conjugate, on the device
     bool set_local_code(const std::complex<float>* code)
     {
         std::lock_guard<std::mutex> lk(dev_->mutex());
@@ -252,21 +261,27 @@ public:
         std::lock_guard<std::mutex> lk(dev_->mutex());
         const int step = doppler_step_ ? static_cast<int>(doppler_step_) : static_cast<int>(conf_.doppler_step);
         if (gnsship_acq_set_grid(h_, conf_.doppler_max, step, doppler_center_) != GNSSHIP_OK) return false;
+        step_two_ = false;
         calculate_threshold();
         return true;
     }
     // calculate_threshold (:884-899)
     void calculate_threshold()
     {
-        if (conf_.pfa <= 0.0F) return;
+        const float pfa = step_two_ ? conf_.pfa2 : conf_.pfa;
+        if (pfa <= 0.0F) return;
         int nb = 0;
         gnsship_acq_num_bins(h_, &nb);
-        const int num_bins = fft_size_ * nb;
-        threshold_ = static_cast<float>(2.0 * gamma_p_inv_int(2 * static_cast<int>(conf_.max_dwells),
-                                                  std::pow(1.0 - conf_.pfa, 1.0 / static_cast<float>(num_bins))));
+        const int effective_fft_size = conf_.bit_transition_flag ? fft_size_ / 2 : fft_size_;
+        const int num_bins = effective_fft_size * nb;
+        threshold_ = static_cast<float>(2.0 * gamma_p_inv_int(2 * (conf_.bit_transition_flag ? 1 : static_cast<int>(conf_.max_dwells)),
+                                                  std::pow(1.0 - pfa, 1.0 / static_cast<float>(num_bins))));
     }
+    bool step_two() const { return step_two_; }
     float threshold() const { return threshold_; }
-    // acquisition_core (:600-871) over fft_size gr_complex samples (one dwell)
+    // acquisition_core (:600-871) over consumed_samples() gr_complex samples (one dwell).  With
+    // make_2_steps a step-one detection switches to the narrow step-two grid around its Doppler
+    // (:771-787) and reports positive only from step two; a step-two miss returns to step one.
     bool acquisition_core(const std::complex<float>* in, uint64_t samp_count, Acq_Outcome& out)
     {
         gnsship_acq_result r{};
@@ -277,10 +292,27 @@ public:
         out.Acq_delay_samples = r.acq_delay_samples;
         out.Acq_doppler_hz = static_cast<double>(r.doppler_hz);
         out.Acq_samplestamp_samples = samp_count;
+        out.Acq_doppler_step = step_two_ ? static_cast<uint32_t>(conf_.doppler_step2) : out.Acq_doppler_step;
         out.test_statistics = r.test_statistic;
-        out.input_power = r.input_power;
+        if (!step_two_) last_input_power_ = r.input_power;
+        out.input_power = step_two_ ? last_input_power_ : r.input_power;
         out.peak = r.peak;
-        out.positive = r.test_statistic > threshold_;  // :765-816 (step one, no bit-transition)
+        const bool hit = r.test_statistic > threshold_;
+        out.positive = hit && (!conf_.make_2_steps || step_two_);
+        if (conf_.make_2_steps) {
+            std::lock_guard<std::mutex> lk(dev_->mutex());
+            if (hit && !step_two_) {
+                if (gnsship_acq_set_grid_step2(h_, static_cast<float>(r.doppler_hz), conf_.doppler_step2,
+                        static_cast<int>(conf_.num_doppler_bins_step2), r.input_power) != GNSSHIP_OK)
+                    return false;
+                step_two_ = true;
+            } else if (step_two_) {
+                const int step = doppler_step_ ? static_cast<int>(doppler_step_) : static_cast<int>(conf_.doppler_step);
+                if (gnsship_acq_set_grid(h_, conf_.doppler_max, step, doppler_center_) != GNSSHIP_OK) return false;
+                step_two_ = false;
+            }
+        }
+        calculate_threshold();
         return true;
     }
     const char* last_error() const { return gnsship_last_error(dev_->ctx()); }
@@ -290,6 +322,9 @@ private:
     std::shared_ptr<Device> dev_;
     gnsship_acq* h_ = nullptr;
     int fft_size_ = 0;
+    int consumed_ = 0;
+    bool step_two_ = false;
+    float last_input_power_ = 0.0F;
     float threshold_ = 0.0F;
     uint32_t doppler_step_ = 0;
     int32_t doppler_center_ = 0;

@@ -259,3 +259,58 @@ def pcps_acquisition_core(sig, code_sampled, fs, doppler_max, doppler_step, dopp
     res = acquisition_statistic(grid, doppler_max, doppler_step, doppler_center, use_cfar, samples_per_chip,
                                 samples_per_code)
     return res, grid
+
+
+def pcps_acquisition_core_ex(sig, code, fs, fft_size, doppler_max, doppler_step, doppler_center=0, use_cfar=True,
+                             consumed=None, bit_transition=False, step2=None, samples_per_chip=None, samples_per_code=None,
+                             fft_dtype=np.complex128):
+    """acquisition_core with the reference's buffer layouts (pcps_acquisition.cc:175-208, 600-672):
+    input = the first `consumed` samples zero-padded to fft_size; local-code buffer
+    [N/2 zeros | code[0, N/2)] with bit_transition_flag, [N − consumed zeros | code[0, consumed)] when
+    consumed < fft_size, else code; grid rows = |IFFT|² (second half with bit_transition_flag).
+    CFAR runs on the effective rows; first-vs-second on rows of fft_size (zeros past the effective
+    part, as the reference's d_magnitude_grid rows), both as the reference (:496-597).
+    step2 = (center_hz, step2_hz, nbins2, step_one_input_power): make_2_steps' second grid
+    (:305-312) and its Doppler/statistic (:516-525, :553-556)."""
+    n = fft_size
+    consumed = n if consumed is None else consumed
+    x = np.zeros(n, np.complex64)
+    x[:consumed] = sig[:consumed]
+    n_code = n // 2 if bit_transition else consumed
+    c = np.zeros(n, np.complex64)
+    c[n - n_code:] = np.asarray(code, np.complex64)[:n_code]
+    if step2 is None:
+        nb = num_doppler_bins(doppler_max, doppler_step)
+        w = doppler_wipeoff_grid(nb, n, doppler_max, doppler_step, doppler_center, fs)
+    else:
+        center, st2, nb, _ = step2
+        w = np.empty((nb, n), np.complex64)
+        for i in range(nb):
+            d = np.float32((np.float32(i) - np.float32(np.floor(nb / 2.0))) * np.float32(st2))
+            f = np.float32(np.float32(center) + d)
+            step = -np.float32(np.float32(np.float32(2.0 * np.pi) * f) / np.float32(fs))  # update_local_carrier (:232-245)
+            row = np.zeros(2 * n, np.float32)
+            ph = np.zeros(1, np.float32)
+            lib().orc_sincos_generic(_ptr(row), ctypes.c_float(step), _ptr(ph), ctypes.c_uint(n))
+            w[i] = row.view(np.complex64)
+    full = acquisition_grid(x, c, w, fft_dtype)
+    eff = n // 2 if bit_transition else n
+    rows = full[:, eff:] if bit_transition else full
+    if samples_per_chip is None:
+        samples_per_chip = int(np.ceil(np.float32(fs) / np.float32(1023000.0)))
+    if samples_per_code is None:
+        samples_per_code = float(np.float32(np.float32(fs) * np.float32(0.001)))
+    if use_cfar:
+        res = acquisition_statistic(rows, doppler_max, doppler_step, doppler_center, True, samples_per_chip, samples_per_code)
+    else:
+        padded = np.zeros((rows.shape[0], n), np.float32)
+        padded[:, :eff] = rows
+        res = acquisition_statistic(padded, doppler_max, doppler_step, doppler_center, False, samples_per_chip, samples_per_code)
+    if step2 is not None:
+        center, st2, nb, ip = step2
+        res.doppler_hz = int(np.int32(np.float32(np.float32(center) + np.float32(
+            np.float32(np.float32(res.doppler_index) - np.float32(np.floor(nb / 2.0))) * np.float32(st2)))))
+        if use_cfar:
+            res.input_power = float(np.float32(ip))
+            res.test_statistic = float(np.float32(np.float32(res.peak) / np.float32(ip)))
+    return res, rows

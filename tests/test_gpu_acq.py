@@ -255,3 +255,68 @@ def test_huge_limits(ctx):
     from gnss_sim_receiver_amd import abi
     with pytest.raises(abi.GnssHipError):
         engine.PcpsAcquisition(ctx, 600000000, 600000, 5000, 250)  # > 32 × 16384
+
+
+# ---- acquisition variants: bit_transition_flag, sampled_ms != ms_per_code, make_2_steps
+
+def _variant_case(ctx, fs, fft, consumed, bt, cfar, prn, seed, monkeypatch=None, force=None):
+    if force:
+        monkeypatch.setenv(force, "1")
+    sat = signals.Satellite(prn=prn, doppler_hz=-1830.0, code_delay_chips=511.7, cn0_dbhz=47.0)
+    sig = signals.generate_if(fs, fft, [sat], seed=seed)
+    code = np.tile(codes.gps_l1_ca_code_gen_complex_sampled(prn, fs), 4)
+    acq = engine.PcpsAcquisition(ctx, fs, fft, 5000, 250, 0, cfar, consumed_samples=consumed, bit_transition_flag=bt)
+    acq.set_local_code(code)
+    (r,), grid = acq.run(sig[:consumed or fft], want_grid=True)
+    acq.close()
+    ref, rgrid = O.pcps_acquisition_core_ex(sig, code, fs, fft, 5000, 250, 0, cfar, consumed=consumed or fft, bit_transition=bt)
+    assert grid.shape[1:] == rgrid.shape
+    assert np.max(np.abs(grid[0] - rgrid)) / rgrid.max() < 1e-5
+    assert (r.doppler_index, r.code_index, r.doppler_hz) == (ref.doppler_index, ref.code_index, ref.doppler_hz)
+    assert r.acq_delay_samples == ref.acq_delay_samples
+    np.testing.assert_allclose([r.peak, r.input_power, r.test_statistic], [ref.peak, ref.input_power, ref.test_statistic], rtol=2e-4)
+
+
+@pytest.mark.parametrize("cfar", [True, False])
+def test_bit_transition_flag(ctx, cfar):
+    """bit_transition_flag: 2 ms of input against [1 ms zeros | 1 ms code], grid rows = the second half
+    of |IFFT|² (pcps_acquisition.cc:187-192, 663-664), first-vs-second window modulo d_fft_size."""
+    _variant_case(ctx, 4000000, 8000, 0, True, cfar, 17, 41)
+
+
+@pytest.mark.parametrize("cfar", [True, False])
+def test_zero_padded_input_sampled_ms_ne_ms_per_code(ctx, cfar):
+    """sampled_ms != ms_per_code: fft_size = 2 × consumed, input and code zero-padded (:84-91, :197-202, :612-619)."""
+    _variant_case(ctx, 4000000, 8000, 4000, False, cfar, 23, 42)
+
+
+def test_bit_transition_four_step_and_huge(ctx, monkeypatch):
+    _variant_case(ctx, 25000000, 50000, 0, True, True, 9, 43)              # huge layout (4 × 12500)
+    _variant_case(ctx, 8000000, 16000, 0, True, False, 9, 44, monkeypatch, "GNSSHIP_ACQ_FORCE_BIG")  # four-step (16 × 1000)
+
+
+@pytest.mark.parametrize("cfar", [True, False])
+def test_make_2_steps_narrow_grid(ctx, cfar):
+    """make_2_steps: step-two grid of nb2 bins × step2 around the step-one Doppler (:305-312); its
+    Doppler formula (:553-556) and, with CFAR, the step-one input power (:516-525)."""
+    fs, n = 4000000, 4000
+    sat = signals.Satellite(prn=3, doppler_hz=1130.0, code_delay_chips=300.3, cn0_dbhz=48.0)
+    sig = signals.generate_if(fs, n, [sat], seed=45)
+    code = codes.gps_l1_ca_code_gen_complex_sampled(3, fs)
+    acq = engine.PcpsAcquisition(ctx, fs, n, 5000, 250, 0, cfar)
+    acq.set_local_code(code)
+    (r1,), _ = acq.run(sig)
+    ref1, _ = O.pcps_acquisition_core(sig, code, fs, 5000, 250, 0, cfar)
+    assert (r1.doppler_index, r1.code_index) == (ref1.doppler_index, ref1.code_index)
+    acq.set_grid_step2(float(r1.doppler_hz), 62.5, 8, r1.input_power)
+    assert acq.n_bins == 8
+    (r2,), grid = acq.run(sig, want_grid=True)
+    ref2, rgrid = O.pcps_acquisition_core_ex(sig, code, fs, n, 5000, 250, 0, cfar, step2=(float(r1.doppler_hz), 62.5, 8, r1.input_power))
+    assert np.max(np.abs(grid[0] - rgrid)) / rgrid.max() < 1e-5
+    assert (r2.doppler_index, r2.code_index, r2.doppler_hz) == (ref2.doppler_index, ref2.code_index, ref2.doppler_hz)
+    np.testing.assert_allclose([r2.peak, r2.input_power, r2.test_statistic], [ref2.peak, ref2.input_power, ref2.test_statistic], rtol=2e-4)
+    assert abs(r2.doppler_hz - 1130) <= 62.5  # the finer grid closes in on the true Doppler
+    acq.set_grid(5000, 250, 0)  # back to step one
+    (r3,), _ = acq.run(sig)
+    assert (r3.doppler_index, r3.code_index, r3.doppler_hz) == (r1.doppler_index, r1.code_index, r1.doppler_hz)
+    acq.close()
