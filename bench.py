@@ -283,7 +283,7 @@ def trk_bench(ctx, block, sats, n_ch, rounds):
     t0 = time.perf_counter()
     _, done = trk.run(dev, 0, rounds, n_buffer_samples=n, records=False)
     dt = time.perf_counter() - t0
-    tracking = sum(1 for ch in range(n_ch) if trk.channel_state(ch)[0] in (2, 4))
+    tracking = sum(1 for ch in range(n_ch) if trk.channel_state(ch)[0] in (2, 3, 4))
     trk.close()
     dev.free()
     sig_s = done * 1e-3

@@ -92,6 +92,8 @@ class TrkConf(ctypes.Structure):
         ("carrier_lock_test_smoother_samples", ctypes.c_int32), ("cn0_min", ctypes.c_int32),
         ("max_code_lock_fail", ctypes.c_int32), ("max_carrier_lock_fail", ctypes.c_int32),
         ("carrier_aiding", ctypes.c_int32), ("track_pilot", ctypes.c_int32), ("system", ctypes.c_int32),
+        ("extend_correlation_symbols", ctypes.c_int32), ("pll_bw_narrow_hz", ctypes.c_float), ("dll_bw_narrow_hz", ctypes.c_float),
+        ("early_late_space_narrow_chips", ctypes.c_float), ("very_early_late_space_narrow_chips", ctypes.c_float),
     ]
 
     @classmethod
@@ -101,7 +103,9 @@ class TrkConf(ctypes.Structure):
                 cn0_smoother_alpha=0.002, carrier_lock_test_smoother_alpha=0.002, pull_in_time_s=10,
                 bit_synchronization_time_limit_s=20, vector_length=vector_length, pll_filter_order=3, dll_filter_order=2,
                 cn0_samples=20, cn0_smoother_samples=200, carrier_lock_test_smoother_samples=25, cn0_min=25,
-                max_code_lock_fail=50, max_carrier_lock_fail=5000, carrier_aiding=1, track_pilot=1, system=system)
+                max_code_lock_fail=50, max_carrier_lock_fail=5000, carrier_aiding=1, track_pilot=1, system=system,
+                extend_correlation_symbols=1, pll_bw_narrow_hz=5.0, dll_bw_narrow_hz=0.75, early_late_space_narrow_chips=0.15,
+                very_early_late_space_narrow_chips=0.5)
         for k, v in kw.items():
             setattr(c, k, v)
         return c

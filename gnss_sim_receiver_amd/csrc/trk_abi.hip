@@ -81,7 +81,7 @@ void gps_preamble_symbols(char* out)
 
 // Tracking_loop_filter::update_coefficients (tracking_loop_filter.cc:100-200), no last integrator
 // (the tracking block constructs it with include_last_integrator = false, :465).
-void loop_filter_coefficients(float T, float bw, int order, TrkParams& p)
+void loop_filter_coefficients(float T, float bw, int order, LoopSet& p)
 {
     const float zeta = 1.0F / std::sqrt(2.0F);
     float g1, g2, g3, wn;
@@ -185,23 +185,44 @@ bool build_params(const gnsship_trk_conf& c, TrkParams& p)
         p.shifts[1] = 0.0F;
         p.shifts[2] = c.early_late_space_chips * spcf;
     }
-    loop_filter_coefficients(static_cast<float>(p.code_period), c.dll_bw_hz, c.dll_filter_order, p);
-    // Tracking_FLL_PLL_filter::set_params (tracking_FLL_PLL_filter.cc:23-55)
-    p.fp_order = c.pll_filter_order;
-    if (p.fp_order == 3) {
-        p.fp_b3 = 2.400F;
-        p.fp_a3 = 1.100F;
-        p.fp_a2 = 1.414F;
-        p.fp_w0p = c.pll_bw_hz / 0.7845F;
-        p.fp_w0p2 = p.fp_w0p * p.fp_w0p;
-        p.fp_w0p3 = p.fp_w0p2 * p.fp_w0p;
-        p.fp_w0f = c.fll_bw_hz / 0.53F;
-        p.fp_w0f2 = p.fp_w0f * p.fp_w0f;
+    // extended integration (:515-523): enabled when extend_correlation_symbols > 1
+    p.extend = c.extend_correlation_symbols > 1 ? c.extend_correlation_symbols : 1;
+    p.T_ext = static_cast<float>(p.extend) * static_cast<float>(p.code_period);
+    if (p.veml) {
+        p.shifts_n[0] = -c.very_early_late_space_narrow_chips * spcf;
+        p.shifts_n[1] = -c.early_late_space_narrow_chips * spcf;
+        p.shifts_n[2] = 0.0F;
+        p.shifts_n[3] = c.early_late_space_narrow_chips * spcf;
+        p.shifts_n[4] = c.very_early_late_space_narrow_chips * spcf;
     } else {
-        p.fp_a2 = 1.414F;
-        p.fp_w0p = c.pll_bw_hz / 0.53F;
-        p.fp_w0p2 = p.fp_w0p * p.fp_w0p;
-        p.fp_w0f = c.fll_bw_hz / 0.25F;
+        p.shifts_n[0] = -c.early_late_space_narrow_chips * spcf;
+        p.shifts_n[1] = 0.0F;
+        p.shifts_n[2] = c.early_late_space_narrow_chips * spcf;
+    }
+    p.spc_n = c.early_late_space_narrow_chips;
+    // wide: (code period, dll_bw); narrow: set_update_interval(T_ext) + set_noise_bandwidth(dll_bw_narrow)
+    loop_filter_coefficients(static_cast<float>(p.code_period), c.dll_bw_hz, c.dll_filter_order, p.ls[0]);
+    loop_filter_coefficients(p.T_ext, c.dll_bw_narrow_hz, c.dll_filter_order, p.ls[1]);
+    // Tracking_FLL_PLL_filter::set_params (tracking_FLL_PLL_filter.cc:23-55): wide, then narrow (:1904)
+    p.fp_order = c.pll_filter_order;
+    for (int s = 0; s < 2; s++) {
+        LoopSet& q = p.ls[s];
+        const float pll_bw = s ? c.pll_bw_narrow_hz : c.pll_bw_hz;
+        if (p.fp_order == 3) {
+            q.fp_b3 = 2.400F;
+            q.fp_a3 = 1.100F;
+            q.fp_a2 = 1.414F;
+            q.fp_w0p = pll_bw / 0.7845F;
+            q.fp_w0p2 = q.fp_w0p * q.fp_w0p;
+            q.fp_w0p3 = q.fp_w0p2 * q.fp_w0p;
+            q.fp_w0f = c.fll_bw_hz / 0.53F;
+            q.fp_w0f2 = q.fp_w0f * q.fp_w0f;
+        } else {
+            q.fp_a2 = 1.414F;
+            q.fp_w0p = pll_bw / 0.53F;
+            q.fp_w0p2 = q.fp_w0p * q.fp_w0p;
+            q.fp_w0f = c.fll_bw_hz / 0.25F;
+        }
     }
     // Exponential_Smoother settings (:540-553, exponential_smoother.cc:29-73)
     auto clamp01 = [](float a) { return a < 0.0F ? 0.0F : (a > 1.0F ? 1.0F : a); };

@@ -13,6 +13,12 @@ constexpr int kTrkMaxCn0Samples = 64;  // prompt buffer of the CN0 / carrier-loc
 
 // Signal constants the reference selects per system/signal (dll_pll_veml_tracking.cc:142-330,
 // start_tracking :662-826) plus the loop-filter coefficients derived from Dll_Pll_Conf once.
+struct LoopSet {
+    float lf_in[4], lf_out[3];
+    int32_t lf_n_in, lf_n_out;
+    float fp_w0p3, fp_w0f2, fp_a2, fp_w0f, fp_a3, fp_w0p2, fp_b3, fp_w0p;
+};
+
 struct TrkParams {
     gnsship_trk_conf conf;
     double code_chip_rate, carrier_freq, code_period;
@@ -21,12 +27,14 @@ struct TrkParams {
     uint32_t secondary_bits[kTrkMaxSecondary / 32];       // bit i = character i == '1'
     uint32_t data_secondary_bits[kTrkMaxSecondary / 32];
     float shifts[5];                                        // d_local_code_shift_chips (× samples per chip)
-    // Tracking_loop_filter (code) coefficients
-    float lf_in[4], lf_out[3];
-    int32_t lf_n_in, lf_n_out;
-    // Tracking_FLL_PLL_filter constants
-    float fp_w0p3, fp_w0f2, fp_a2, fp_w0f, fp_a3, fp_w0p2, fp_b3, fp_w0p;
+    // Tracking_loop_filter (code) coefficients and Tracking_FLL_PLL_filter constants; set [1] is
+    // the narrow configuration of extended integration (:1902-1904)
+    LoopSet ls[2];
     int32_t fp_order;
+    int32_t extend;      // extend_correlation_symbols (> 1: extended integration enabled)
+    float T_ext;         // (float)extend · (float)code_period
+    float shifts_n[5];   // narrow taps
+    float spc_n;
     // Exponential_Smoother settings
     float cn0_alpha, cn0_one_minus_alpha, cn0_min_value, cn0_offset;
     int32_t cn0_init_samples;
@@ -44,7 +52,9 @@ struct Smoother {
 
 // One channel: the dll_pll_veml_tracking members the per-epoch path reads or writes.
 struct TrkChannel {
-    int32_t state;  // 0 idle / lost, 2 wide tracking, 4 narrow tracking
+    int32_t state;  // 0 idle / lost, 2 wide tracking, 3 coherent integration, 4 narrow tracking
+    int32_t narrow;     // loop set / taps in use (1 after entering extended integration)
+    int32_t ext_count;  // d_extend_correlation_symbols_count
     int32_t cloop, pull_in, pll_180, ran, acc_phase_init;
     int32_t code_id, data_code_id;
     uint64_t acq_sample_stamp;

@@ -116,27 +116,29 @@ __device__ bool lock_status(const TrkParams& k, TrkChannel& c, double coh_integr
 
 __device__ float loop_filter_apply(const TrkParams& k, TrkChannel& c, float x)
 {
+    const LoopSet& q = k.ls[c.narrow];
     float result = 0.0f;
-    for (int ii = 0; ii < k.lf_n_out; ii++) result = __fadd_rn(result, __fmul_rn(k.lf_out[ii], c.lf_outputs[(c.lf_idx + ii) % 4]));
+    for (int ii = 0; ii < q.lf_n_out; ii++) result = __fadd_rn(result, __fmul_rn(q.lf_out[ii], c.lf_outputs[(c.lf_idx + ii) % 4]));
     c.lf_idx--;
     if (c.lf_idx < 0) c.lf_idx += 4;
     c.lf_inputs[c.lf_idx] = x;
-    for (int ii = 0; ii < k.lf_n_in; ii++) result = __fadd_rn(result, __fmul_rn(k.lf_in[ii], c.lf_inputs[(c.lf_idx + ii) % 4]));
+    for (int ii = 0; ii < q.lf_n_in; ii++) result = __fadd_rn(result, __fmul_rn(q.lf_in[ii], c.lf_inputs[(c.lf_idx + ii) % 4]));
     c.lf_outputs[c.lf_idx] = result;
     return result;
 }
 
 __device__ float carrier_filter(const TrkParams& k, TrkChannel& c, float fll, float pll, float T)
 {
+    const LoopSet& q = k.ls[c.narrow];
     if (k.fp_order == 3) {
-        c.fp_w = __fadd_rn(c.fp_w, __fmul_rn(T, __fadd_rn(__fmul_rn(k.fp_w0p3, pll), __fmul_rn(k.fp_w0f2, fll))));
-        const float inner = __fadd_rn(__fadd_rn(__fmul_rn(0.5f, c.fp_w), __fmul_rn(__fmul_rn(k.fp_a2, k.fp_w0f), fll)),
-            __fmul_rn(__fmul_rn(k.fp_a3, k.fp_w0p2), pll));
+        c.fp_w = __fadd_rn(c.fp_w, __fmul_rn(T, __fadd_rn(__fmul_rn(q.fp_w0p3, pll), __fmul_rn(q.fp_w0f2, fll))));
+        const float inner = __fadd_rn(__fadd_rn(__fmul_rn(0.5f, c.fp_w), __fmul_rn(__fmul_rn(q.fp_a2, q.fp_w0f), fll)),
+            __fmul_rn(__fmul_rn(q.fp_a3, q.fp_w0p2), pll));
         c.fp_x = __fadd_rn(c.fp_x, __fmul_rn(T, inner));
-        return __fadd_rn(__fmul_rn(0.5f, c.fp_x), __fmul_rn(__fmul_rn(k.fp_b3, k.fp_w0p), pll));
+        return __fadd_rn(__fmul_rn(0.5f, c.fp_x), __fmul_rn(__fmul_rn(q.fp_b3, q.fp_w0p), pll));
     }
-    const float w_new = __fadd_rn(__fadd_rn(c.fp_w, __fmul_rn(__fmul_rn(pll, k.fp_w0p2), T)), __fmul_rn(__fmul_rn(fll, k.fp_w0f), T));
-    const float e = __fadd_rn(__fmul_rn(0.5f, __fadd_rn(w_new, c.fp_w)), __fmul_rn(__fmul_rn(k.fp_a2, k.fp_w0p), pll));
+    const float w_new = __fadd_rn(__fadd_rn(c.fp_w, __fmul_rn(__fmul_rn(pll, q.fp_w0p2), T)), __fmul_rn(__fmul_rn(fll, q.fp_w0f), T));
+    const float e = __fadd_rn(__fmul_rn(0.5f, __fadd_rn(w_new, c.fp_w)), __fmul_rn(__fmul_rn(q.fp_a2, q.fp_w0p), pll));
     c.fp_w = w_new;
     return e;
 }
@@ -149,7 +151,9 @@ __device__ void run_dll_pll(const TrkParams& k, TrkChannel& c)
     else
         disc = static_cast<double>(atan2f(c.p[1], c.p[0]));  // gr::fast_atan2f restated as atan2f
     c.carr_phase_error_hz = disc / kTwoPi;
-    c.carr_error_filt_hz = carrier_filter(k, c, 0.0f, static_cast<float>(c.carr_phase_error_hz), static_cast<float>(k.code_period));
+    // d_current_correlation_time_s: the code period, or extend × code period once extended
+    const float T = c.narrow ? k.T_ext : static_cast<float>(k.code_period);
+    c.carr_error_filt_hz = carrier_filter(k, c, 0.0f, static_cast<float>(c.carr_phase_error_hz), T);
     c.carrier_doppler_hz = c.carr_error_filt_hz;
     if (k.veml) {
         const double early = static_cast<double>(sqrtf(__fadd_rn(__fadd_rn(__fadd_rn(__fmul_rn(c.ve[0], c.ve[0]), __fmul_rn(c.ve[1], c.ve[1])),
@@ -304,7 +308,14 @@ __device__ bool epoch_update(const TrkParams& k, TrkChannel& c, const float* tap
                 c.sign_count = 0;
                 c.current_symbol = 0;
                 c.current_data_symbol = 0;
-                c.state = 4;
+                if (k.extend > 1) {  // extended integration (:1890-1926): narrow loops and taps, state 3
+                    c.ext_count = 0;
+                    c.narrow = 1;
+                    c.spc = k.spc_n;
+                    c.state = 3;
+                } else {
+                    c.state = 4;
+                }
             }
         }
     } else {
@@ -335,7 +346,20 @@ __device__ bool epoch_update(const TrkParams& k, TrkChannel& c, const float* tap
             c.p_data[1] = src[1];
         }
         c.cloop = k.track_pilot ? 0 : 1;
-        if (!lock_status(k, c, k.code_period)) {
+        if (st == 3) {  // coherent integration (:1933-1970): accumulate, NCO advance only
+            update_tracking_vars(k, c);
+            if (c.current_data_symbol == 0) {
+                rec.prompt_i = static_cast<double>(c.p_data[0]);
+                rec.prompt_q = static_cast<double>(c.p_data[1]);
+                rec.flags |= 1;
+                c.p_data[0] = c.p_data[1] = 0.0f;
+            }
+            c.ext_count++;
+            if (c.ext_count == k.extend - 1) {
+                c.ext_count = 0;
+                c.state = 4;
+            }
+        } else if (!lock_status(k, c, k.code_period * static_cast<double>(k.extend))) {
             clear_tracking_vars(c);
             c.state = 0;
             loss = true;
@@ -353,6 +377,7 @@ __device__ bool epoch_update(const TrkParams& k, TrkChannel& c, const float* tap
                 c.p_data[0] = c.p_data[1] = 0.0f;
             }
             zero_accu(c);
+            if (k.extend > 1) c.state = 3;  // next coherent integration cycle
         }
     }
     rec.state = st;
@@ -419,13 +444,13 @@ __global__ void trk_step_kernel(const TrkParams* __restrict__ pk, TrkChannel* __
     c.ran = 0;
     if (emit) {
         const uint64_t vl = k.conf.vector_length;
-        const bool runnable = (c.state == 2 || c.state == 4) && c.nitems_read >= buf_first &&
+        const bool runnable = (c.state == 2 || c.state == 3 || c.state == 4) && c.nitems_read >= buf_first &&
                               c.nitems_read + vl <= buf_first + static_cast<uint64_t>(buf_len);
         for (int q = 0; q < k.jobs_per_channel; q++) {
             DevJob& j = jobs[jb + q];
             if (runnable) {
                 if (q == 0) {
-                    fill_job(j, k, c, static_cast<int64_t>(c.nitems_read - buf_first), c.code_id, k.n_taps, k.shifts);
+                    fill_job(j, k, c, static_cast<int64_t>(c.nitems_read - buf_first), c.code_id, k.n_taps, c.narrow ? k.shifts_n : k.shifts);
                 } else {
                     const float zero[1] = {0.0f};
                     fill_job(j, k, c, static_cast<int64_t>(c.nitems_read - buf_first), c.data_code_id, 1, zero);

@@ -221,9 +221,9 @@ int gnsship_acq_destroy(gnsship_acq* a);
  * do_correlation_step (:1037-1062): cn0_and_tracking_lock_status (:972-1029), run_dll_pll
  * (:1065-1152), update_tracking_vars (:1189-1260), save_correlation_results and the bit /
  * secondary-code synchronisation of states 2 and 4.  start_tracking (:643-883) and the state-1
- * pull-in (:1757-1788) run on the host in gnsship_trk_start.  Not covered: extended coherent
- * integration (state 3; extend_correlation_symbols = 1 is the default), high_dyn rate smoothing,
- * the FLL branches (enable_fll_* default false) and BeiDou GEO satellites.
+ * pull-in (:1757-1788) run on the host in gnsship_trk_start.  States 2, 3 (extended coherent
+ * integration, extend_correlation_symbols > 1) and 4.  Not covered: high_dyn rate smoothing, the
+ * FLL branches (enable_fll_* default false) and BeiDou GEO satellites.
  * ------------------------------------------------------------------------------------------- */
 #define GNSSHIP_SYS_GPS_L1CA 0 /* GPS L1 C/A: 3 taps, bit sync on the 160-symbol preamble */
 #define GNSSHIP_SYS_GAL_E1 1   /* Galileo E1 B/C: VEML 5 taps on the pilot + data prompt, CS25 secondary */
@@ -256,6 +256,11 @@ typedef struct gnsship_trk_conf { /* Dll_Pll_Conf (dll_pll_conf.h:33-80), same n
     int32_t carrier_aiding;
     int32_t track_pilot;
     int32_t system; /* GNSSHIP_SYS_*: the signal constants the adapter selects */
+    int32_t extend_correlation_symbols; /* > 1: extended coherent integration, state 3 (:515-523) */
+    float pll_bw_narrow_hz;
+    float dll_bw_narrow_hz;
+    float early_late_space_narrow_chips;
+    float very_early_late_space_narrow_chips;
 } gnsship_trk_conf;
 
 typedef struct gnsship_trk_start_args { /* Gnss_Synchro fields start_tracking reads (:647-649) */
@@ -275,7 +280,7 @@ typedef struct gnsship_trk_epoch { /* one general_work call of one channel (Gnss
     double carrier_doppler_hz;
     double cn0_db_hz;
     float carrier_lock_test;
-    int32_t state;                 /* state the epoch ran in (2 or 4) */
+    int32_t state;                 /* state the epoch ran in (2, 3 or 4) */
     int32_t flags;                 /* 1 valid symbol, 2 loss of lock, 4 PLL 180°, 8 epoch ran */
     int32_t pad;
     double code_freq_chips;

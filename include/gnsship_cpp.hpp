@@ -337,6 +337,9 @@ struct Dll_Pll_Conf {
     double carrier_lock_th{0.7};
     float pll_bw_hz{35.0F}, dll_bw_hz{2.0F}, fll_bw_hz{35.0F};
     float early_late_space_chips{0.25F}, very_early_late_space_chips{0.5F};
+    float early_late_space_narrow_chips{0.15F}, very_early_late_space_narrow_chips{0.5F};
+    float pll_bw_narrow_hz{5.0F}, dll_bw_narrow_hz{0.75F};
+    int32_t extend_correlation_symbols{1};
     float slope{1.0F}, spc{0.5F}, y_intercept{1.0F};
     float cn0_smoother_alpha{0.002F}, carrier_lock_test_smoother_alpha{0.002F};
     uint32_t pull_in_time_s{10U}, bit_synchronization_time_limit_s{20U}, vector_length{0U};
@@ -381,6 +384,11 @@ public:
         c.max_carrier_lock_fail = conf.max_carrier_lock_fail;
         c.carrier_aiding = conf.carrier_aiding ? 1 : 0;
         c.track_pilot = conf.track_pilot ? 1 : 0;
+        c.extend_correlation_symbols = conf.extend_correlation_symbols;
+        c.pll_bw_narrow_hz = conf.pll_bw_narrow_hz;
+        c.dll_bw_narrow_hz = conf.dll_bw_narrow_hz;
+        c.early_late_space_narrow_chips = conf.early_late_space_narrow_chips;
+        c.very_early_late_space_narrow_chips = conf.very_early_late_space_narrow_chips;
         c.system = conf.system == 'E' ? GNSSHIP_SYS_GAL_E1 : conf.system == 'C' ? GNSSHIP_SYS_BDS_B1I : GNSSHIP_SYS_GPS_L1CA;
         code_base_ = 1024 + 2 * max_channels * next_engine_id();
         std::lock_guard<std::mutex> lk(dev_->mutex());

@@ -32,6 +32,8 @@ class OrcTrkConf(ctypes.Structure):
         ("code_length_chips", ctypes.c_int32), ("code_samples_per_chip", ctypes.c_int32), ("symbols_per_bit", ctypes.c_int32),
         ("secondary", ctypes.c_int32), ("secondary_code_length", ctypes.c_int32), ("data_secondary_code_length", ctypes.c_int32),
         ("secondary_code", ctypes.c_char * (TRK_MAX_SEC + 1)), ("data_secondary_code", ctypes.c_char * (TRK_MAX_SEC + 1)),
+        ("extend_correlation_symbols", ctypes.c_int32), ("pll_bw_narrow_hz", ctypes.c_float), ("dll_bw_narrow_hz", ctypes.c_float),
+        ("early_late_space_narrow_chips", ctypes.c_float), ("very_early_late_space_narrow_chips", ctypes.c_float),
     ]
 
 
@@ -69,7 +71,9 @@ def conf(system: str, fs_in: float, vector_length: int, **kw) -> OrcTrkConf:
                    max_code_lock_fail=50, max_carrier_lock_fail=5000, carrier_aiding=1, track_pilot=track_pilot, veml=veml,
                    code_length_chips=L, code_samples_per_chip=spc, symbols_per_bit=spb, secondary=sec,
                    secondary_code_length=len(sec_code), data_secondary_code_length=len(dsec),
-                   secondary_code=sec_code.encode(), data_secondary_code=dsec.encode())
+                   secondary_code=sec_code.encode(), data_secondary_code=dsec.encode(),
+                   extend_correlation_symbols=1, pll_bw_narrow_hz=5.0, dll_bw_narrow_hz=0.75, early_late_space_narrow_chips=0.15,
+                   very_early_late_space_narrow_chips=0.5)
     for k, v in kw.items():
         setattr(c, k, v)
     return c

@@ -314,6 +314,9 @@ typedef struct {
     int32_t code_length_chips, code_samples_per_chip, symbols_per_bit, secondary, secondary_code_length, data_secondary_code_length;
     char secondary_code[TRK_MAX_SEC + 1];
     char data_secondary_code[TRK_MAX_SEC + 1];
+    /* extended coherent integration (dll_pll_conf.h:48-53,66): enabled when extend > 1 (:515-523) */
+    int32_t extend_correlation_symbols;
+    float pll_bw_narrow_hz, dll_bw_narrow_hz, early_late_space_narrow_chips, very_early_late_space_narrow_chips;
 } orc_trk_conf;
 
 typedef struct {
@@ -337,6 +340,7 @@ typedef struct {
     orc_loop_filter code_filter;
     orc_fll_pll carrier_filter;
     orc_smoother cn0_sm, lock_sm;
+    int extend_count; /* d_extend_correlation_symbols_count */
 } orc_trk_channel;
 
 typedef struct { /* Gnss_Synchro subset emitted per epoch (dll_pll_veml_tracking.cc:1996-2091) */
@@ -569,14 +573,41 @@ static void push_prompt_sign(const orc_trk_conf* k, orc_trk_channel* c, float pr
     }
 }
 
-/* One general_work call in state 2 or 4 for the epoch starting at c->nitems_read, given the
+static int extend_symbols(const orc_trk_conf* k) { return k->extend_correlation_symbols > 1 ? k->extend_correlation_symbols : 1; }
+
+/* State 2 → extended integration (dll_pll_veml_tracking.cc:1890-1926): integration time
+ * extend × code period, narrow DLL/PLL bandwidths (the filters keep their state), narrow taps. */
+static void enter_extended_integration(const orc_trk_conf* k, orc_trk_channel* c)
+{
+    c->extend_count = 0;
+    c->current_correlation_time_s = (float)extend_symbols(k) * (float)k->code_period;
+    c->code_filter.update_interval = (float)c->current_correlation_time_s; /* set_update_interval */
+    orc_lf_update_coefficients(&c->code_filter);
+    c->code_filter.noise_bandwidth = k->dll_bw_narrow_hz; /* set_noise_bandwidth */
+    orc_lf_update_coefficients(&c->code_filter);
+    orc_fp_set_params(&c->carrier_filter, k->fll_bw_hz, k->pll_bw_narrow_hz, k->pll_filter_order);
+    const float spcf = (float)k->code_samples_per_chip;
+    if (c->veml) {
+        c->shifts[0] = -k->very_early_late_space_narrow_chips * spcf;
+        c->shifts[1] = -k->early_late_space_narrow_chips * spcf;
+        c->shifts[3] = k->early_late_space_narrow_chips * spcf;
+        c->shifts[4] = k->very_early_late_space_narrow_chips * spcf;
+    } else {
+        c->shifts[0] = -k->early_late_space_narrow_chips * spcf;
+        c->shifts[2] = k->early_late_space_narrow_chips * spcf;
+    }
+    c->spc = k->early_late_space_narrow_chips;
+    c->state = 3;
+}
+
+/* One general_work call in state 2, 3 or 4 for the epoch starting at c->nitems_read, given the
  * correlator outputs of that epoch (taps: n_taps complex, pdata: data-prompt complex).
  * Advances nitems_read by the new current_prn_length_samples.  Returns 0 when the channel is
  * (or becomes) idle. */
 int orc_trk_epoch_update(const orc_trk_conf* k, orc_trk_channel* c, const float* taps, const float* pdata, orc_trk_epoch* rec)
 {
     memset(rec, 0, sizeof(*rec));
-    if (c->state != 2 && c->state != 4) return 0;
+    if (c->state != 2 && c->state != 3 && c->state != 4) return 0;
     const uint64_t nir = c->nitems_read;
     rec->sample_counter = nir;
     if (c->pull_in) {
@@ -633,12 +664,29 @@ int orc_trk_epoch_update(const orc_trk_conf* k, orc_trk_channel* c, const float*
                 c->prompt_count = 0;
                 c->current_symbol = 0;
                 c->current_data_symbol = 0;
-                c->state = 4;
+                if (extend_symbols(k) > 1)
+                    enter_extended_integration(k, c);
+                else
+                    c->state = 4;
             }
+        }
+    } else if (st == 3) { /* coherent integration (:1933-1970): accumulate, no loop update */
+        save_correlation_results(k, c, taps, pdata);
+        update_tracking_vars(k, c);
+        if (c->current_data_symbol == 0) {
+            rec->prompt_i = (double)c->p_data[0];
+            rec->prompt_q = (double)c->p_data[1];
+            rec->flags |= 1;
+            c->p_data[0] = c->p_data[1] = 0.0F;
+        }
+        c->extend_count++;
+        if (c->extend_count == extend_symbols(k) - 1) {
+            c->extend_count = 0;
+            c->state = 4;
         }
     } else {
         save_correlation_results(k, c, taps, pdata);
-        if (!cn0_and_tracking_lock_status(k, c, k->code_period)) {
+        if (!cn0_and_tracking_lock_status(k, c, k->code_period * (double)extend_symbols(k))) {
             clear_tracking_vars(c);
             c->state = 0;
             loss = 1;
@@ -660,6 +708,7 @@ int orc_trk_epoch_update(const orc_trk_conf* k, orc_trk_channel* c, const float*
             memset(c->p, 0, sizeof(c->p));
             memset(c->l, 0, sizeof(c->l));
             memset(c->vl, 0, sizeof(c->vl));
+            if (extend_symbols(k) > 1) c->state = 3; /* next coherent integration cycle */
         }
     }
     rec->state = st;
@@ -701,7 +750,7 @@ int orc_trk_run(const orc_trk_conf* k, orc_trk_channel* c, const float* samples,
     float* scratch = (float*)malloc((size_t)5 * (size_t)vl * sizeof(float));
     int e = 0;
     for (; e < max_epochs; e++) {
-        if (c->state != 2 && c->state != 4) break;
+        if (c->state != 2 && c->state != 3 && c->state != 4) break;
         if (c->nitems_read < buffer_first || (int64_t)(c->nitems_read - buffer_first) + vl > n_samples) break;
         float args[6];
         orc_trk_correlation_args(k, c, args);

@@ -21,7 +21,8 @@ SHARED = ["fs_in", "carrier_lock_th", "pll_bw_hz", "dll_bw_hz", "fll_bw_hz", "ea
           "slope", "spc", "y_intercept", "cn0_smoother_alpha", "carrier_lock_test_smoother_alpha", "pull_in_time_s",
           "bit_synchronization_time_limit_s", "vector_length", "pll_filter_order", "dll_filter_order", "cn0_samples",
           "cn0_smoother_samples", "carrier_lock_test_smoother_samples", "cn0_min", "max_code_lock_fail", "max_carrier_lock_fail",
-          "carrier_aiding", "track_pilot"]
+          "carrier_aiding", "track_pilot", "extend_correlation_symbols", "pll_bw_narrow_hz", "dll_bw_narrow_hz",
+          "early_late_space_narrow_chips", "very_early_late_space_narrow_chips"]
 
 
 def dev_conf(k, system):
@@ -85,6 +86,26 @@ def test_sync_to_state_4_matches_oracle(ctx, system, fs, epochs):
     assert ref["state"][-1] == 4
     compare(rec[:, 1], ref, system)
     assert not np.any(rec[:, 0]["flags"])
+    trk.close()
+
+
+@pytest.mark.parametrize("system,fs,epochs,ext", [("GPS", 4e6, 600, 10), ("GPS", 4e6, 500, 20), ("GAL", 25e6 / 4, 110, 4),
+                                                  ("BDS", 4.092e6, 400, 5)])
+def test_extended_integration_state_3_matches_oracle(ctx, system, fs, epochs, ext):
+    """extend_correlation_symbols > 1: after synchronisation the loop runs extend − 1 coherent
+    integration epochs (state 3) per narrow-loop update (state 4), narrow taps and bandwidths
+    (dll_pll_veml_tracking.cc:1890-1970)."""
+    sat, k, x, stamp, first, delay, dop = S.sync(system, fs, epochs, extend_correlation_symbols=ext)
+    trk = engine.DllPllVemlTracking(ctx, dev_conf(k, system), 1)
+    ctx.set_code(30, sat.code)
+    if sat.code_data is not None:
+        ctx.set_code(31, sat.code_data)
+    trk.start(0, 30, delay, dop, stamp, first, data_code_id=31)
+    rec, rounds = trk.run(x, first, epochs)
+    ref = T.track(k, x, sat.code, delay, dop, stamp, first, epochs, data_code=sat.code_data, buffer_first=first)
+    st = ref["state"]
+    assert np.sum(st == 3) >= 3 * (ext - 1) and np.sum(st == 4) >= 3
+    compare(rec[:, 0], ref, f"{system} x{ext}")
     trk.close()
 
 

@@ -130,3 +130,21 @@ def test_oracle_buffers_in_pieces_equal_one_buffer():
     pieces = np.concatenate(parts)
     assert len(parts[0]) < 120 and len(pieces) == len(whole)
     assert np.array_equal(pieces, whole)
+
+
+def test_extended_integration_cycle(built):
+    """State machine of extended coherent integration (dll_pll_veml_tracking.cc:1890-2028): after
+    synchronisation, extend − 1 state-3 epochs (no loop update) per state-4 epoch; GPS symbols
+    (20 per bit) are still emitted once per bit."""
+    import trk_scenarios as S
+    for ext in (2, 10, 20):
+        sat, k, x, stamp, first, delay, dop = S.sync("GPS", 4e6, 400, extend_correlation_symbols=ext)
+        r = T.track(k, x, sat.code, delay, dop, stamp, first, 400, buffer_first=first)
+        st = r["state"]
+        i0 = int(np.argmax(st != 2))
+        assert i0 > 0 and np.all(st[:i0] == 2)
+        cyc = st[i0:i0 + 3 * ext]
+        expect = np.array(([3] * (ext - 1) + [4]) * 3)
+        assert np.array_equal(cyc, expect), (ext, cyc)
+        sym = np.nonzero(r["flags"][i0:] & 1)[0]
+        assert len(sym) >= 5 and np.all(np.diff(sym) == 20), (ext, sym[:6])
