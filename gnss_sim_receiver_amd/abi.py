@@ -94,6 +94,7 @@ class TrkConf(ctypes.Structure):
         ("carrier_aiding", ctypes.c_int32), ("track_pilot", ctypes.c_int32), ("system", ctypes.c_int32),
         ("extend_correlation_symbols", ctypes.c_int32), ("pll_bw_narrow_hz", ctypes.c_float), ("dll_bw_narrow_hz", ctypes.c_float),
         ("early_late_space_narrow_chips", ctypes.c_float), ("very_early_late_space_narrow_chips", ctypes.c_float),
+        ("enable_fll_pull_in", ctypes.c_int32), ("enable_fll_steady_state", ctypes.c_int32),
     ]
 
     @classmethod
@@ -105,7 +106,7 @@ class TrkConf(ctypes.Structure):
                 cn0_samples=20, cn0_smoother_samples=200, carrier_lock_test_smoother_samples=25, cn0_min=25,
                 max_code_lock_fail=50, max_carrier_lock_fail=5000, carrier_aiding=1, track_pilot=1, system=system,
                 extend_correlation_symbols=1, pll_bw_narrow_hz=5.0, dll_bw_narrow_hz=0.75, early_late_space_narrow_chips=0.15,
-                very_early_late_space_narrow_chips=0.5)
+                very_early_late_space_narrow_chips=0.5, enable_fll_pull_in=0, enable_fll_steady_state=0)
         for k, v in kw.items():
             setattr(c, k, v)
         return c

@@ -347,7 +347,7 @@ extern "C" int gnsship_trk_start(gnsship_trk* t, int channel, const gnsship_trk_
     c.data_code_id = p.track_pilot ? a->data_code_id : a->code_id;
     c.acq_sample_stamp = a->acq_samplestamp_samples;
     c.carrier_doppler_hz = a->acq_doppler_hz;
-    c.carrier_phase_step_rad = 2.0 * M_PI * c.carrier_doppler_hz / k.fs_in;
+    c.carrier_phase_step_rad = 6.2831853071796 * c.carrier_doppler_hz / k.fs_in;  // TWO_PI = 2·GNSS_PI (MATH_CONSTANTS.h:47-49)
     c.carrier_lock_test = 1.0F;
     c.cn0_db_hz = 0.0F;
     c.spc = k.spc;

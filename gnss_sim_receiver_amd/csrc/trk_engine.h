@@ -67,6 +67,7 @@ struct TrkChannel {
     int32_t current_prn_length_samples;
     float spc;
     float ve[2], e[2], p[2], l[2], vl[2], p_data[2];
+    float p_old[2];  // d_P_accu_old (FLL discriminator)
     int32_t cn0_counter, carrier_fail, code_fail, current_symbol, current_data_symbol;
     float cn0_db_hz, carrier_lock_test;
     float prompt_buf[2 * kTrkMaxCn0Samples];

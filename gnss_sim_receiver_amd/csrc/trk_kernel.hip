@@ -27,7 +27,22 @@ namespace gnsship {
 
 namespace {
 
-constexpr double kTwoPi = 6.283185307179586476925286766559;
+// MATH_CONSTANTS.h:47-49: the reference's pi is the GNSS value 3.1415926535898
+constexpr double kGnssPi = 3.1415926535898;
+constexpr double kTwoPi = 2.0 * kGnssPi;
+constexpr double kHalfPi = kGnssPi / 2.0;
+
+// fll_diff_atan + phase_unwrap (tracking_discriminators.cc:27-41, 68-76)
+__device__ double fll_diff_atan(const float* s1, const float* s2, double t1, double t2)
+{
+    double d = static_cast<double>(__fsub_rn(atanf(__fdiv_rn(s2[1], s2[0])), atanf(__fdiv_rn(s1[1], s1[0]))));
+    if (isnan(d)) d = 0.0;
+    if (d >= kHalfPi)
+        d -= kGnssPi;
+    else if (d <= -kHalfPi)
+        d += kGnssPi;
+    return d / (t2 - t1);
+}
 
 __device__ float smooth(Smoother& s, float raw, float alpha, float one_minus_alpha, float min_value, float offset, int init_samples)
 {
@@ -153,7 +168,17 @@ __device__ void run_dll_pll(const TrkParams& k, TrkChannel& c)
     c.carr_phase_error_hz = disc / kTwoPi;
     // d_current_correlation_time_s: the code period, or extend × code period once extended
     const float T = c.narrow ? k.T_ext : static_cast<float>(k.code_period);
-    c.carr_error_filt_hz = carrier_filter(k, c, 0.0f, static_cast<float>(c.carr_phase_error_hz), T);
+    if ((c.pull_in && k.conf.enable_fll_pull_in) || k.conf.enable_fll_steady_state) {  // :1080-1097
+        // d_current_correlation_time_s is a double: the code period, or (float)extend·(float)period
+        const double Td = c.narrow ? static_cast<double>(k.T_ext) : k.code_period;
+        const double fe = fll_diff_atan(c.p_old, c.p, 0.0, Td) / kTwoPi;
+        c.p_old[0] = c.p[0];
+        c.p_old[1] = c.p[1];
+        const float pll = (c.pull_in && k.conf.enable_fll_pull_in) ? 0.0f : static_cast<float>(c.carr_phase_error_hz);
+        c.carr_error_filt_hz = carrier_filter(k, c, static_cast<float>(fe), pll, T);
+    } else {
+        c.carr_error_filt_hz = carrier_filter(k, c, 0.0f, static_cast<float>(c.carr_phase_error_hz), T);
+    }
     c.carrier_doppler_hz = c.carr_error_filt_hz;
     if (k.veml) {
         const double early = static_cast<double>(sqrtf(__fadd_rn(__fadd_rn(__fadd_rn(__fmul_rn(c.ve[0], c.ve[0]), __fmul_rn(c.ve[1], c.ve[1])),
@@ -233,6 +258,7 @@ __device__ bool acquire_secondary(const TrkParams& k, TrkChannel& c)
 __device__ void clear_tracking_vars(TrkChannel& c)
 {
     c.p_data[0] = c.p_data[1] = 0.0f;
+    c.p_old[0] = c.p_old[1] = 0.0f;
     c.carr_phase_error_hz = 0.0;
     c.carr_error_filt_hz = 0.0;
     c.code_error_chips = 0.0;

@@ -302,6 +302,27 @@ float orc_sm_smooth(orc_smoother* s, float raw)
     return v;
 }
 
+/* MATH_CONSTANTS.h:47-49: the GNSS value of pi (not M_PI) */
+#define TRK_GNSS_PI 3.1415926535898
+#define TRK_HALF_PI (TRK_GNSS_PI / 2.0)
+#define TRK_TWO_PI (2.0 * TRK_GNSS_PI)
+
+/* phase_unwrap / fll_diff_atan (tracking_discriminators.cc:27-41, 68-76): std::atan of the float
+ * quotients (float overload), difference as float, NaN → 0, unwrapped by ±pi. */
+static double orc_phase_unwrap(double phase_rad)
+{
+    if (phase_rad >= TRK_HALF_PI) return phase_rad - TRK_GNSS_PI;
+    if (phase_rad <= -TRK_HALF_PI) return phase_rad + TRK_GNSS_PI;
+    return phase_rad;
+}
+
+double orc_fll_diff_atan(const float* s1, const float* s2, double t1, double t2)
+{
+    double diff_atan = (double)(atanf(s2[1] / s2[0]) - atanf(s1[1] / s1[0]));
+    if (isnan(diff_atan)) diff_atan = 0;
+    return orc_phase_unwrap(diff_atan) / (t2 - t1);
+}
+
 /* ---- channel ---------------------------------------------------------------------------- */
 typedef struct {
     /* Dll_Pll_Conf subset + signal constants (set by the caller, as the adapters do) */
@@ -317,6 +338,7 @@ typedef struct {
     /* extended coherent integration (dll_pll_conf.h:48-53,66): enabled when extend > 1 (:515-523) */
     int32_t extend_correlation_symbols;
     float pll_bw_narrow_hz, dll_bw_narrow_hz, early_late_space_narrow_chips, very_early_late_space_narrow_chips;
+    int32_t enable_fll_pull_in, enable_fll_steady_state; /* dll_pll_conf.h:75-76 */
 } orc_trk_conf;
 
 typedef struct {
@@ -376,7 +398,7 @@ void orc_trk_start(const orc_trk_conf* k, orc_trk_channel* c, double acq_delay_s
     c->acq_carrier_doppler_hz = acq_doppler_hz;
     c->acq_sample_stamp = acq_samplestamp;
     c->carrier_doppler_hz = acq_doppler_hz;
-    c->carrier_phase_step_rad = 2.0 * M_PI * c->carrier_doppler_hz / k->fs_in;
+    c->carrier_phase_step_rad = TRK_TWO_PI * c->carrier_doppler_hz / k->fs_in;
     c->veml = k->veml;
     c->n_taps = k->veml ? 5 : 3;
     const float spcf = (float)k->code_samples_per_chip;
@@ -473,10 +495,20 @@ static int cn0_and_tracking_lock_status(const orc_trk_conf* k, orc_trk_channel* 
 static void run_dll_pll(const orc_trk_conf* k, orc_trk_channel* c)
 {
     if (c->cloop)
-        c->carr_phase_error_hz = orc_pll_cloop_two_quadrant_atan(c->p[0], c->p[1]) / (2.0 * M_PI);
+        c->carr_phase_error_hz = orc_pll_cloop_two_quadrant_atan(c->p[0], c->p[1]) / TRK_TWO_PI;
     else
-        c->carr_phase_error_hz = orc_pll_four_quadrant_atan(c->p[0], c->p[1]) / (2.0 * M_PI);
-    c->carr_error_filt_hz = orc_fp_get_carrier_error(&c->carrier_filter, 0.0F, (float)c->carr_phase_error_hz, (float)c->current_correlation_time_s);
+        c->carr_phase_error_hz = orc_pll_four_quadrant_atan(c->p[0], c->p[1]) / TRK_TWO_PI;
+    if ((c->pull_in && k->enable_fll_pull_in) || k->enable_fll_steady_state) { /* :1080-1097 */
+        const double fe = orc_fll_diff_atan(c->p_old, c->p, 0.0, c->current_correlation_time_s) / TRK_TWO_PI;
+        c->p_old[0] = c->p[0];
+        c->p_old[1] = c->p[1];
+        if (c->pull_in && k->enable_fll_pull_in)
+            c->carr_error_filt_hz = orc_fp_get_carrier_error(&c->carrier_filter, (float)fe, 0.0F, (float)c->current_correlation_time_s);
+        else
+            c->carr_error_filt_hz = orc_fp_get_carrier_error(&c->carrier_filter, (float)fe, (float)c->carr_phase_error_hz, (float)c->current_correlation_time_s);
+    } else {
+        c->carr_error_filt_hz = orc_fp_get_carrier_error(&c->carrier_filter, 0.0F, (float)c->carr_phase_error_hz, (float)c->current_correlation_time_s);
+    }
     c->carrier_doppler_hz = c->carr_error_filt_hz;
     if (c->veml)
         c->code_error_chips = orc_dll_nc_vemlp_normalized(c->ve, c->e, c->l, c->vl);
@@ -494,10 +526,10 @@ static void update_tracking_vars(const orc_trk_conf* k, orc_trk_channel* c)
     c->T_prn_samples = c->T_prn_seconds * k->fs_in;
     c->K_blk_samples = c->T_prn_samples + c->rem_code_phase_samples;
     c->current_prn_length_samples = (int32_t)floor(c->K_blk_samples);
-    c->carrier_phase_step_rad = 2.0 * M_PI * c->carrier_doppler_hz / k->fs_in;
+    c->carrier_phase_step_rad = TRK_TWO_PI * c->carrier_doppler_hz / k->fs_in;
     const double n = (double)c->current_prn_length_samples;
     c->rem_carr_phase_rad += (float)(c->carrier_phase_step_rad * n + 0.5 * 0.0 * n * n);
-    c->rem_carr_phase_rad = (float)fmod((double)c->rem_carr_phase_rad, 2.0 * M_PI);
+    c->rem_carr_phase_rad = (float)fmod((double)c->rem_carr_phase_rad, TRK_TWO_PI);
     c->acc_carrier_phase_rad -= (c->carrier_phase_step_rad * n + 0.5 * 0.0 * n * n);
     c->code_phase_step_chips = c->code_freq_chips / k->fs_in;
     c->rem_code_phase_samples = c->K_blk_samples - n;

@@ -22,7 +22,7 @@ SHARED = ["fs_in", "carrier_lock_th", "pll_bw_hz", "dll_bw_hz", "fll_bw_hz", "ea
           "bit_synchronization_time_limit_s", "vector_length", "pll_filter_order", "dll_filter_order", "cn0_samples",
           "cn0_smoother_samples", "carrier_lock_test_smoother_samples", "cn0_min", "max_code_lock_fail", "max_carrier_lock_fail",
           "carrier_aiding", "track_pilot", "extend_correlation_symbols", "pll_bw_narrow_hz", "dll_bw_narrow_hz",
-          "early_late_space_narrow_chips", "very_early_late_space_narrow_chips"]
+          "early_late_space_narrow_chips", "very_early_late_space_narrow_chips", "enable_fll_pull_in", "enable_fll_steady_state"]
 
 
 def dev_conf(k, system):
@@ -106,6 +106,24 @@ def test_extended_integration_state_3_matches_oracle(ctx, system, fs, epochs, ex
     st = ref["state"]
     assert np.sum(st == 3) >= 3 * (ext - 1) and np.sum(st == 4) >= 3
     compare(rec[:, 0], ref, f"{system} x{ext}")
+    trk.close()
+
+
+@pytest.mark.parametrize("pull_in,steady", [(1, 0), (1, 1), (0, 1)])
+def test_fll_assisted_loop_matches_oracle(ctx, pull_in, steady):
+    """enable_fll_pull_in / enable_fll_steady_state (run_dll_pll :1080-1097): fll_diff_atan of
+    consecutive prompts drives the carrier filter's FLL input (alone during the pull-in)."""
+    sat, k, x, stamp, first, delay, dop = S.pull_in("GPS", 4e6, 46.0, -2600.0, 321.0, 60.0, 0.3, 400, pull_in_time_s=0,
+                                                     enable_fll_pull_in=pull_in, enable_fll_steady_state=steady)
+    if pull_in:
+        k.pull_in_time_s = 1 if not steady else 0
+    ctx.set_code(40, sat.code)
+    trk = engine.DllPllVemlTracking(ctx, dev_conf(k, "GPS"), 1)
+    trk.start(0, 40, delay, dop, stamp, first)
+    rec, rounds = trk.run(x, 0, 400)
+    ref = T.track(k, x, sat.code, delay, dop, stamp, first, 400)
+    assert len(ref) > 100
+    compare(rec[:, 0], ref, f"fll {pull_in}{steady}")
     trk.close()
 
 

@@ -148,3 +148,22 @@ def test_extended_integration_cycle(built):
         assert np.array_equal(cyc, expect), (ext, cyc)
         sym = np.nonzero(r["flags"][i0:] & 1)[0]
         assert len(sym) >= 5 and np.all(np.diff(sym) == 20), (ext, sym[:6])
+
+
+def test_fll_diff_atan_identities(built):
+    """fll_diff_atan (tracking_discriminators.cc:68-76): phase difference of two prompts over the
+    interval, unwrapped into (−pi/2, pi/2); 0/0 prompts give 0 (the NaN branch)."""
+    import ctypes
+    L = T.lib()
+    f32p = ctypes.POINTER(ctypes.c_float)
+    L.orc_fll_diff_atan.argtypes = [f32p, f32p, ctypes.c_double, ctypes.c_double]
+    L.orc_fll_diff_atan.restype = ctypes.c_double
+    # (100 Hz, 4 ms): 2.51 rad is outside atan's (−pi/2, pi/2) → aliased by 1/(2T) to −25 Hz
+    for f_hz, T_s, want in [(12.5, 0.001, 12.5), (-40.0, 0.001, -40.0), (3.0, 0.02, 3.0), (100.0, 0.004, -25.0)]:
+        a = np.array([0.8, 0.3], np.float32)
+        ph = 2 * np.pi * f_hz * T_s
+        b = np.array([a[0] * np.cos(ph) - a[1] * np.sin(ph), a[0] * np.sin(ph) + a[1] * np.cos(ph)], np.float32)
+        got = L.orc_fll_diff_atan(a.ctypes.data_as(f32p), b.ctypes.data_as(f32p), 0.0, T_s) / (2 * 3.1415926535898)
+        assert abs(got - want) < 1e-3 * max(1.0, abs(want)), (f_hz, got)
+    z = np.zeros(2, np.float32)
+    assert L.orc_fll_diff_atan(z.ctypes.data_as(f32p), z.ctypes.data_as(f32p), 0.0, 0.001) == 0.0
