@@ -95,6 +95,7 @@ class TrkConf(ctypes.Structure):
         ("extend_correlation_symbols", ctypes.c_int32), ("pll_bw_narrow_hz", ctypes.c_float), ("dll_bw_narrow_hz", ctypes.c_float),
         ("early_late_space_narrow_chips", ctypes.c_float), ("very_early_late_space_narrow_chips", ctypes.c_float),
         ("enable_fll_pull_in", ctypes.c_int32), ("enable_fll_steady_state", ctypes.c_int32),
+        ("high_dyn", ctypes.c_int32), ("smoother_length", ctypes.c_uint32),
     ]
 
     @classmethod
@@ -106,7 +107,8 @@ class TrkConf(ctypes.Structure):
                 cn0_samples=20, cn0_smoother_samples=200, carrier_lock_test_smoother_samples=25, cn0_min=25,
                 max_code_lock_fail=50, max_carrier_lock_fail=5000, carrier_aiding=1, track_pilot=1, system=system,
                 extend_correlation_symbols=1, pll_bw_narrow_hz=5.0, dll_bw_narrow_hz=0.75, early_late_space_narrow_chips=0.15,
-                very_early_late_space_narrow_chips=0.5, enable_fll_pull_in=0, enable_fll_steady_state=0)
+                very_early_late_space_narrow_chips=0.5, enable_fll_pull_in=0, enable_fll_steady_state=0,
+                high_dyn=0, smoother_length=10)
         for k, v in kw.items():
             setattr(c, k, v)
         return c

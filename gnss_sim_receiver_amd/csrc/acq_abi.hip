@@ -332,7 +332,6 @@ extern "C" int gnsship_acq_run(gnsship_acq* a, const void* sig, int fmt, int sig
     for (int p = 0; p < n_prns; p++)
         if (!a->code_set[p]) return fail(ctx, GNSSHIP_E_STATE, "gnsship_acq_run: set_local_code missing for a prn slot");
     HIP_TRY(ctx, hipSetDevice(ctx->device));
-    const int N = a->conf.fft_size;
     const void* src = sig;
     if (!sig_on_device) {
         HIP_TRY(ctx, hipMemcpyAsync(a->sig_dev, sig, fmt_bytes(fmt) * a->consumed, hipMemcpyHostToDevice, ctx->stream));

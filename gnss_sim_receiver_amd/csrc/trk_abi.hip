@@ -59,6 +59,11 @@ struct gnsship_trk {
     size_t ran_cap = 0;
     void* stage_dev = nullptr;
     size_t stage_cap = 0;
+    // high_dyn: the high-dynamics correlator's fixed plan (one HdJob per job, out_index = job) and
+    // the channels' rate-smoother rings
+    bool high_dyn = false;
+    HdPlan hd;
+    TrkHist* hist_dev = nullptr;
 };
 
 namespace {
@@ -124,6 +129,7 @@ bool build_params(const gnsship_trk_conf& c, TrkParams& p)
 {
     std::memset(&p, 0, sizeof(p));
     p.conf = c;
+    if (p.conf.smoother_length < 1) p.conf.smoother_length = 1;  // dll_pll_conf.cc:119-123
     char sec[kTrkMaxSecondary + 1] = {0};
     switch (c.system) {
     case GNSSHIP_SYS_GPS_L1CA:  // :142-200 (1C), start_tracking :662-668 forces track_pilot = false
@@ -242,12 +248,24 @@ bool build_params(const gnsship_trk_conf& c, TrkParams& p)
     return true;
 }
 
+// high_dyn: bind a job's code replica in its HdJob (the step kernel keeps these fields).
+hipError_t upload_hd_code(gnsship_trk* t, int job, const CodeDesc& cd)
+{
+    static_assert(offsetof(HdJob, code_len) == offsetof(HdJob, code) + sizeof(const float*), "HdJob code fields");
+    HdJob& j = t->hd.jobs[job];
+    j.code = cd.ptr;
+    j.code_len = cd.ptr ? cd.len : 0;
+    return hipMemcpyAsync(reinterpret_cast<char*>(t->hd.jobs_dev + job) + offsetof(HdJob, code), &j.code, sizeof(const float*) + sizeof(int32_t),
+        hipMemcpyHostToDevice, t->ctx->stream);
+}
+
 void release(gnsship_trk* t)
 {
     void* ptrs[] = {t->params_dev, t->chans_dev, t->jobs_dev, t->chunks_dev, t->items_dev, t->anchors_dev, t->partials_dev, t->out_dev, t->rec_dev,
-        t->ran_dev, t->stage_dev};
+        t->ran_dev, t->stage_dev, t->hist_dev};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
+    hd_plan_free(t->hd);
 }
 
 }  // namespace
@@ -267,8 +285,10 @@ extern "C" int gnsship_trk_create(gnsship_ctx* ctx, const gnsship_trk_conf* conf
     if (!ctx || !conf || !out) return GNSSHIP_E_INVAL;
     *out = nullptr;
     if (max_channels < 1 || conf->fs_in <= 0.0 || conf->vector_length < 1 || conf->cn0_samples < 1 || conf->cn0_samples > kTrkMaxCn0Samples ||
-        conf->pll_filter_order < 2 || conf->pll_filter_order > 3 || conf->dll_filter_order < 1 || conf->dll_filter_order > 3)
-        return fail(ctx, GNSSHIP_E_INVAL, "gnsship_trk_create: bad configuration (cn0_samples 1..64, pll order 2..3, dll order 1..3)");
+        conf->pll_filter_order < 2 || conf->pll_filter_order > 3 || conf->dll_filter_order < 1 || conf->dll_filter_order > 3 ||
+        (conf->high_dyn && conf->smoother_length > static_cast<uint32_t>(kTrkMaxSmoother)))
+        return fail(ctx, GNSSHIP_E_INVAL,
+            "gnsship_trk_create: bad configuration (cn0_samples 1..64, pll order 2..3, dll order 1..3, smoother_length <= 64)");
     gnsship_trk* t = new (std::nothrow) gnsship_trk();
     if (!t) return GNSSHIP_E_NOMEM;
     t->ctx = ctx;
@@ -319,6 +339,24 @@ extern "C" int gnsship_trk_create(gnsship_ctx* ctx, const gnsship_trk_conf* conf
     if (e == hipSuccess) e = hipMemset(t->anchors_dev, 0, sizeof(Anchor) * static_cast<size_t>(n_anchors + kAnchorPad));
     if (e == hipSuccess) e = hipMalloc(&t->partials_dev, sizeof(float) * 2 * kMaxTaps * static_cast<size_t>(t->n_chunks));
     if (e == hipSuccess) e = hipMalloc(&t->out_dev, sizeof(float) * 2 * kMaxTaps * static_cast<size_t>(t->n_jobs));
+    t->high_dyn = conf->high_dyn != 0;
+    if (e == hipSuccess && t->high_dyn) {
+        t->hd.jobs.assign(t->n_jobs, HdJob{});
+        for (int i = 0; i < t->n_jobs; i++) {
+            HdJob& j = t->hd.jobs[i];
+            j.n_samples = static_cast<int32_t>(conf->vector_length);
+            j.n_taps = (p.jobs_per_channel == 2 && (i % 2) == 1) ? 1 : p.n_taps;
+            j.out_index = i;
+        }
+        e = hd_plan_upload(t->hd, ctx->stream);  // chunk layout and anchor offsets for vector_length
+        if (e == hipSuccess) {  // idle until a channel starts (the step kernel rewrites both every round)
+            for (auto& j : t->hd.jobs) j.n_samples = 0;
+            for (auto& c : t->hd.chunks) c.len = 0;
+            e = hipMemcpy(t->hd.jobs_dev, t->hd.jobs.data(), sizeof(HdJob) * t->hd.jobs.size(), hipMemcpyHostToDevice);
+        }
+        if (e == hipSuccess) e = hipMemcpy(t->hd.chunks_dev, t->hd.chunks.data(), sizeof(HdChunk) * t->hd.chunks.size(), hipMemcpyHostToDevice);
+        if (e == hipSuccess) e = hipMalloc(&t->hist_dev, sizeof(TrkHist) * static_cast<size_t>(max_channels));
+    }
     if (e != hipSuccess) {
         release(t);
         delete t;
@@ -393,6 +431,7 @@ extern "C" int gnsship_trk_start(gnsship_trk* t, int channel, const gnsship_trk_
             HIP_TRY(ctx, hipMemcpyAsync(reinterpret_cast<char*>(t->chunks_dev + ci) + offsetof(ChunkDesc, code_len), &d.code_len,
                              sizeof(ChunkDesc) - offsetof(ChunkDesc, code_len), hipMemcpyHostToDevice, ctx->stream));
         }
+        if (t->high_dyn) HIP_TRY(ctx, upload_hd_code(t, job, cd));
     }
     HIP_TRY(ctx, hipMemcpyAsync(t->chans_dev + channel, &c, sizeof(TrkChannel), hipMemcpyHostToDevice, ctx->stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
@@ -449,6 +488,7 @@ extern "C" int gnsship_trk_run(gnsship_trk* t, const void* sig, int fmt, int sig
                 d.code_len = ok ? ctx->codes_host[id].len : 0;
                 d.len = 0;  // rewritten by the first step kernel of this run before any correlation
             }
+            if (t->high_dyn) HIP_TRY(ctx, upload_hd_code(t, job, ok ? ctx->codes_host[id] : CodeDesc{nullptr, 0, 0}));
         }
         HIP_TRY(ctx, hipMemcpyAsync(t->chunks_dev, t->chunks_host.data(), sizeof(ChunkDesc) * t->n_chunks, hipMemcpyHostToDevice, ctx->stream));
         t->attached_version = ctx->codes_version;
@@ -484,9 +524,16 @@ extern "C" int gnsship_trk_run(gnsship_trk* t, const void* sig, int fmt, int sig
         const int consume = r > 0 ? 1 : 0, emit = r < max_rounds ? 1 : 0;
         gnsship_trk_epoch* rec = (out && r > 0) ? t->rec_dev + static_cast<size_t>(r - 1) * nc : nullptr;
         hipError_t e = launch_trk_step(t->params_dev, t->chans_dev, nc, t->jobs_dev, t->chunks_dev, t->out_dev, buffer_first_sample, n_buffer_samples,
-            consume, emit, rec, t->ran_dev + r, ctx->stream);
+            consume, emit, rec, t->ran_dev + r, t->hist_dev, t->high_dyn ? t->hd.jobs_dev : nullptr, t->high_dyn ? t->hd.chunks_dev : nullptr,
+            ctx->stream);
         if (e != hipSuccess) return hip_fail(ctx, e, "launch_trk_step");
         if (!emit) break;
+        if (t->high_dyn) {
+            t->hd.max_code_len = max_len;
+            e = launch_corr_hd(src, fmt, t->hd, t->out_dev, ctx->stream);
+            if (e != hipSuccess) return hip_fail(ctx, e, "launch_corr_hd(tracking)");
+            continue;
+        }
         e = launch_corr_batch(src, fmt, t->jobs_dev, t->n_jobs, t->chunks_dev, t->items_dev, t->n_items, t->classes, max_len, t->any_multi,
             t->anchors_dev, t->partials_dev, t->out_dev, ctx->stream);
         if (e != hipSuccess) return hip_fail(ctx, e, "launch_corr_batch(tracking)");

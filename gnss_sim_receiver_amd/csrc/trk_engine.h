@@ -10,6 +10,7 @@ namespace gnsship {
 
 constexpr int kTrkMaxSecondary = 256;  // longest sign pattern searched (GPS preamble: 160 symbols)
 constexpr int kTrkMaxCn0Samples = 64;  // prompt buffer of the CN0 / carrier-lock estimators
+constexpr int kTrkMaxSmoother = 64;    // high_dyn: smoother_length bound (ring of 2·smoother_length)
 
 // Signal constants the reference selects per system/signal (dll_pll_veml_tracking.cc:142-330,
 // start_tracking :662-826) plus the loop-filter coefficients derived from Dll_Pll_Conf once.
@@ -79,11 +80,27 @@ struct TrkChannel {
     // Tracking_FLL_PLL_filter state
     float fp_w, fp_x;
     Smoother cn0_sm, lock_sm;
+    // high_dyn (:1205-1255): the smoothed NCO rates and the ring state of TrkHist
+    double carrier_phase_rate_step_rad, code_phase_rate_step_chips;
+    int32_t hist_head, hist_count;
+};
+
+// high_dyn: d_carr_ph_history and d_code_ph_history of one channel (boost::circular_buffer of
+// capacity 2·smoother_length, :557-566).  Both are pushed together with the same sample count, so
+// they share one ring; kept out of TrkChannel (which the step kernel holds in registers).
+struct TrkHist {
+    double carr[2 * kTrkMaxSmoother];
+    double code[2 * kTrkMaxSmoother];
+    int32_t samples[2 * kTrkMaxSmoother];
 };
 
 // One round: consume the previous epoch's correlations (when `consume`), then lay down the next
 // epoch's jobs / chunk lengths for every channel whose window is in the buffer (when `emit`).
+// With high_dyn the epoch's correlations are high-dynamics jobs (hd_jobs / hd_chunks, the fixed
+// HdPlan of the engine) and `hist` holds the channels' rate-smoother rings; otherwise all three are
+// null and the jobs go to the standard correlator (jobs / chunks).
 hipError_t launch_trk_step(const TrkParams* params, TrkChannel* chans, int n_chans, DevJob* jobs, ChunkDesc* chunks, const float* corr_out,
-    uint64_t buf_first, int64_t buf_len, int consume, int emit, gnsship_trk_epoch* rec, int* ran_count, hipStream_t stream);
+    uint64_t buf_first, int64_t buf_len, int consume, int emit, gnsship_trk_epoch* rec, int* ran_count, TrkHist* hist, HdJob* hd_jobs,
+    HdChunk* hd_chunks, hipStream_t stream);
 
 }  // namespace gnsship

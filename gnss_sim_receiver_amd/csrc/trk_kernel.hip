@@ -202,7 +202,27 @@ __device__ void run_dll_pll(const TrkParams& k, TrkChannel& c)
     if (k.conf.carrier_aiding) c.code_freq_chips += c.carrier_doppler_hz * k.code_chip_rate / k.carrier_freq;
 }
 
-__device__ void update_tracking_vars(const TrkParams& k, TrkChannel& c)
+// high_dyn rate estimate (:1208-1221, :1241-1254): mean step of the newest smoother_length entries
+// minus the mean of the oldest, over the newest entries' samples; sums in the reference's order.
+__device__ double smoothed_rate(const TrkChannel& c, const TrkHist& h, const double* first, int L)
+{
+    const int cap = 2 * L;
+    double cp1 = 0.0, cp2 = 0.0, samples = 0.0;
+    for (int i = 0; i < L; i++) {
+        int a = c.hist_head + i;
+        if (a >= cap) a -= cap;
+        int b = c.hist_head + cap - i - 1;
+        if (b >= cap) b -= cap;
+        cp1 += first[a];
+        cp2 += first[b];
+        samples += static_cast<double>(h.samples[b]);
+    }
+    cp1 /= static_cast<double>(L);
+    cp2 /= static_cast<double>(L);
+    return (cp2 - cp1) / samples;
+}
+
+__device__ void update_tracking_vars(const TrkParams& k, TrkChannel& c, TrkHist* h)
 {
     const double fs = k.conf.fs_in;
     const double T_chip = 1.0 / c.code_freq_chips;
@@ -212,11 +232,30 @@ __device__ void update_tracking_vars(const TrkParams& k, TrkChannel& c)
     c.current_prn_length_samples = static_cast<int32_t>(floor(c.K_blk_samples));
     c.carrier_phase_step_rad = kTwoPi * c.carrier_doppler_hz / fs;
     const double n = static_cast<double>(c.current_prn_length_samples);
-    const double adv = c.carrier_phase_step_rad * n + 0.5 * 0.0 * n * n;
+    c.code_phase_step_chips = c.code_freq_chips / fs;
+    if (h) {  // high_dyn: push_back on the ring (full: drop the oldest), rates once it is full
+        const int L = static_cast<int>(k.conf.smoother_length), cap = 2 * L;
+        int slot;
+        if (c.hist_count < cap) {
+            slot = c.hist_head + c.hist_count;
+            if (slot >= cap) slot -= cap;
+            c.hist_count++;
+        } else {
+            slot = c.hist_head;
+            c.hist_head = c.hist_head + 1 == cap ? 0 : c.hist_head + 1;
+        }
+        h->carr[slot] = c.carrier_phase_step_rad;
+        h->code[slot] = c.code_phase_step_chips;
+        h->samples[slot] = c.current_prn_length_samples;
+        if (c.hist_count == cap) {
+            c.carrier_phase_rate_step_rad = smoothed_rate(c, *h, h->carr, L);
+            c.code_phase_rate_step_chips = smoothed_rate(c, *h, h->code, L);
+        }
+    }
+    const double adv = c.carrier_phase_step_rad * n + 0.5 * c.carrier_phase_rate_step_rad * n * n;
     c.rem_carr_phase_rad = __fadd_rn(c.rem_carr_phase_rad, static_cast<float>(adv));
     c.rem_carr_phase_rad = static_cast<float>(fmod(static_cast<double>(c.rem_carr_phase_rad), kTwoPi));
     c.acc_carrier_phase_rad -= adv;
-    c.code_phase_step_chips = c.code_freq_chips / fs;
     c.rem_code_phase_samples = c.K_blk_samples - n;
     c.rem_code_phase_chips = c.code_freq_chips * c.rem_code_phase_samples / fs;
 }
@@ -266,6 +305,10 @@ __device__ void clear_tracking_vars(TrkChannel& c)
     c.current_symbol = 0;
     c.current_data_symbol = 0;
     c.sign_count = 0;
+    c.carrier_phase_rate_step_rad = 0.0;  // :1182-1185
+    c.code_phase_rate_step_chips = 0.0;
+    c.hist_head = 0;
+    c.hist_count = 0;
 }
 
 __device__ __forceinline__ void cadd(float* acc, const float* v, float sgn)
@@ -282,7 +325,7 @@ __device__ void zero_accu(TrkChannel& c)
 
 // One general_work call for the epoch that started at c.epoch_start; returns false when the
 // channel stops (loss of lock).
-__device__ bool epoch_update(const TrkParams& k, TrkChannel& c, const float* taps, const float* pdata, gnsship_trk_epoch& rec)
+__device__ bool epoch_update(const TrkParams& k, TrkChannel& c, const float* taps, const float* pdata, gnsship_trk_epoch& rec, TrkHist* h)
 {
     const uint64_t nir = c.epoch_start;
     const uint64_t fs_int = static_cast<uint64_t>(static_cast<int>(k.conf.fs_in));
@@ -319,7 +362,7 @@ __device__ bool epoch_update(const TrkParams& k, TrkChannel& c, const float* tap
         } else {
             bool next_state = false;
             run_dll_pll(k, c);
-            update_tracking_vars(k, c);
+            update_tracking_vars(k, c, h);
             if (!c.pull_in) {
                 if (k.secondary || k.symbols_per_bit > 1) {
                     push_sign(k, c, taps[eo + 2]);
@@ -373,7 +416,7 @@ __device__ bool epoch_update(const TrkParams& k, TrkChannel& c, const float* tap
         }
         c.cloop = k.track_pilot ? 0 : 1;
         if (st == 3) {  // coherent integration (:1933-1970): accumulate, NCO advance only
-            update_tracking_vars(k, c);
+            update_tracking_vars(k, c, h);
             if (c.current_data_symbol == 0) {
                 rec.prompt_i = static_cast<double>(c.p_data[0]);
                 rec.prompt_q = static_cast<double>(c.p_data[1]);
@@ -391,7 +434,7 @@ __device__ bool epoch_update(const TrkParams& k, TrkChannel& c, const float* tap
             loss = true;
         } else {
             run_dll_pll(k, c);
-            update_tracking_vars(k, c);
+            update_tracking_vars(k, c, h);
             if (!c.acc_phase_init) {
                 c.acc_carrier_phase_rad = -static_cast<double>(c.rem_carr_phase_rad);
                 c.acc_phase_init = 1;
@@ -447,9 +490,46 @@ __device__ void fill_job(DevJob& j, const TrkParams& k, const TrkChannel& c, int
     for (int t = 0; t < kMaxTaps; t++) j.shifts[t] = t < n_taps ? shifts[t] : 0.0f;
 }
 
+// derive_hd_job (corr_hd_kernel.hip) for a tracking epoch with the smoothed rates
+// (do_correlation_step :1041-1048); the plan fields and the code replica of `j` are kept.
+__device__ void fill_hd_job(HdJob& j, const TrkParams& k, const TrkChannel& c, int64_t offset, int n_taps, const float* shifts)
+{
+    const float spcf = static_cast<float>(k.code_samples_per_chip);
+    const float rem_carr = c.rem_carr_phase_rad;
+    const float step = static_cast<float>(c.carrier_phase_step_rad);
+    const float rate = static_cast<float>(c.carrier_phase_rate_step_rad);
+    j.sample_offset = offset;
+    j.n_samples = static_cast<int32_t>(k.conf.vector_length);
+    j.n_taps = n_taps;
+    j.p0_re = cosf(rem_carr);
+    j.p0_im = -sinf(rem_carr);
+    j.inc_re = cosf(-step);
+    j.inc_im = sinf(-step);
+    j.dtheta = atan2(static_cast<double>(j.inc_im), static_cast<double>(j.inc_re));
+    j.log_mag_inc = static_cast<float>(log(hypot(static_cast<double>(j.inc_re), static_cast<double>(j.inc_im))));
+    j.rate_arg = atan2f(sinf(-rate), cosf(-rate));
+    j.rem_code = __fmul_rn(static_cast<float>(c.rem_code_phase_chips), spcf);
+    j.code_step = __fmul_rn(static_cast<float>(c.code_phase_step_chips), spcf);
+    j.code_rate = __fmul_rn(static_cast<float>(c.code_phase_rate_step_chips), spcf);
+    j.shift0 = shifts[0];
+    // cumulative circular shifts (…_high_dynamics_resampler_32f_xn.h:83-90); tracking taps increase,
+    // so the sum stays within [0, N] (clamped for safety: a shift of N is the identity)
+    uint32_t sum = 0;
+    j.shift_samples[0] = 0;
+    for (int t = 1; t < kMaxTaps; t++) {
+        if (t < n_taps) {
+            const float q = __fdiv_rn(__fsub_rn(shifts[t], shifts[t - 1]), j.code_step);
+            sum += static_cast<uint32_t>(static_cast<int>(round(static_cast<double>(q))));
+            if (sum > static_cast<uint32_t>(j.n_samples)) sum = static_cast<uint32_t>(j.n_samples);
+        }
+        j.shift_samples[t] = t < n_taps ? sum : 0u;
+    }
+}
+
 __global__ void trk_step_kernel(const TrkParams* __restrict__ pk, TrkChannel* __restrict__ chans, int n_chans, DevJob* __restrict__ jobs,
     ChunkDesc* __restrict__ chunks, const float* __restrict__ corr_out, uint64_t buf_first, int64_t buf_len, int consume, int emit,
-    gnsship_trk_epoch* __restrict__ rec, int* __restrict__ ran_count)
+    gnsship_trk_epoch* __restrict__ rec, int* __restrict__ ran_count, TrkHist* __restrict__ hist, HdJob* __restrict__ hd_jobs,
+    HdChunk* __restrict__ hd_chunks)
 {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n_chans) return;
@@ -461,7 +541,7 @@ __global__ void trk_step_kernel(const TrkParams* __restrict__ pk, TrkChannel* __
         r.flags = 8;
         const float* taps = corr_out + static_cast<int64_t>(jb) * 2 * kMaxTaps;
         const float* pdata = k.jobs_per_channel > 1 ? corr_out + static_cast<int64_t>(jb + 1) * 2 * kMaxTaps : taps;
-        epoch_update(k, c, taps, pdata, r);
+        epoch_update(k, c, taps, pdata, r, hist ? hist + i : nullptr);
         if (rec) rec[i] = r;
     } else if (consume && rec) {
         gnsship_trk_epoch r = {};
@@ -472,15 +552,27 @@ __global__ void trk_step_kernel(const TrkParams* __restrict__ pk, TrkChannel* __
         const uint64_t vl = k.conf.vector_length;
         const bool runnable = (c.state == 2 || c.state == 3 || c.state == 4) && c.nitems_read >= buf_first &&
                               c.nitems_read + vl <= buf_first + static_cast<uint64_t>(buf_len);
+        const int64_t off = static_cast<int64_t>(c.nitems_read - buf_first);
+        const float zero[1] = {0.0f};
         for (int q = 0; q < k.jobs_per_channel; q++) {
+            const int n_taps = q == 0 ? k.n_taps : 1;
+            const float* sh = q == 0 ? (c.narrow ? k.shifts_n : k.shifts) : zero;
+            if (hd_jobs) {  // high_dyn: the high-dynamics pair (dll_pll_veml_tracking.cc:530,536)
+                HdJob& j = hd_jobs[jb + q];
+                if (runnable) {
+                    fill_hd_job(j, k, c, off, n_taps, sh);
+                } else {
+                    j.n_samples = 0;
+                }
+                for (int m = 0; m < j.n_chunks; m++) {
+                    const int rem = static_cast<int>(vl) - m * kCorrChunk;  // HD chunks are kCorrChunk samples too
+                    hd_chunks[j.first_chunk + m].len = runnable ? (rem < kCorrChunk ? rem : kCorrChunk) : 0;
+                }
+                continue;
+            }
             DevJob& j = jobs[jb + q];
             if (runnable) {
-                if (q == 0) {
-                    fill_job(j, k, c, static_cast<int64_t>(c.nitems_read - buf_first), c.code_id, k.n_taps, c.narrow ? k.shifts_n : k.shifts);
-                } else {
-                    const float zero[1] = {0.0f};
-                    fill_job(j, k, c, static_cast<int64_t>(c.nitems_read - buf_first), c.data_code_id, 1, zero);
-                }
+                fill_job(j, k, c, off, q == 0 ? c.code_id : c.data_code_id, n_taps, sh);
             } else {
                 j.n_samples = 0;
             }
@@ -502,10 +594,11 @@ __global__ void trk_step_kernel(const TrkParams* __restrict__ pk, TrkChannel* __
 }  // namespace
 
 hipError_t launch_trk_step(const TrkParams* params, TrkChannel* chans, int n_chans, DevJob* jobs, ChunkDesc* chunks, const float* corr_out,
-    uint64_t buf_first, int64_t buf_len, int consume, int emit, gnsship_trk_epoch* rec, int* ran_count, hipStream_t stream)
+    uint64_t buf_first, int64_t buf_len, int consume, int emit, gnsship_trk_epoch* rec, int* ran_count, TrkHist* hist, HdJob* hd_jobs,
+    HdChunk* hd_chunks, hipStream_t stream)
 {
     hipLaunchKernelGGL(trk_step_kernel, dim3((n_chans + 63) / 64), dim3(64), 0, stream, params, chans, n_chans, jobs, chunks, corr_out, buf_first,
-        buf_len, consume, emit, rec, ran_count);
+        buf_len, consume, emit, rec, ran_count, hist, hd_jobs, hd_chunks);
     return hipGetLastError();
 }
 

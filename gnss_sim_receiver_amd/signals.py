@@ -50,6 +50,8 @@ class Satellite:
     # cyclic secondary code, one chip per code period: E1-C CS25 on the Galileo pilot, the B1I NH
     # code on the BeiDou signal
     secondary: str = None
+    # line-of-sight dynamics: the Doppler ramps at this rate from doppler_hz at sample 0
+    doppler_rate_hz_s: float = 0.0
 
     def __post_init__(self):
         if self.code is None:
@@ -71,10 +73,17 @@ class Satellite:
 
     def chip_phase(self, n: np.ndarray, fs: float) -> np.ndarray:
         """Received code phase [chips] at sample n (unwrapped)."""
-        return n / fs * self.code_freq() - self.code_delay_chips
+        ph = n / fs * self.code_freq() - self.code_delay_chips
+        if self.doppler_rate_hz_s:
+            rate, _, fc, _ = SYSTEMS[self.system]
+            ph = ph + 0.5 * rate * self.doppler_rate_hz_s / fc * (n / fs) ** 2
+        return ph
 
     def carrier_phase(self, n: np.ndarray, fs: float) -> np.ndarray:
-        return 2.0 * np.pi * (self.f_if_hz + self.doppler_hz) * (n / fs) + self.carrier_phase_rad
+        ph = 2.0 * np.pi * (self.f_if_hz + self.doppler_hz) * (n / fs) + self.carrier_phase_rad
+        if self.doppler_rate_hz_s:
+            ph = ph + np.pi * self.doppler_rate_hz_s * (n / fs) ** 2
+        return ph
 
 
 def generate_if(fs: float, n_samples: int, sats: list, seed: int = 0, noise: bool = True, start: int = 0,

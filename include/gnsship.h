@@ -222,8 +222,8 @@ int gnsship_acq_destroy(gnsship_acq* a);
  * (:1065-1152), update_tracking_vars (:1189-1260), save_correlation_results and the bit /
  * secondary-code synchronisation of states 2 and 4.  start_tracking (:643-883) and the state-1
  * pull-in (:1757-1788) run on the host in gnsship_trk_start.  States 2, 3 (extended coherent
- * integration, extend_correlation_symbols > 1) and 4, with the FLL branches (enable_fll_*).  Not
- * covered: high_dyn rate smoothing and BeiDou GEO satellites.
+ * integration, extend_correlation_symbols > 1) and 4, with the FLL branches (enable_fll_*) and
+ * high_dyn (high-dynamics correlator fed by the smoothed NCO rates).  Not covered: BeiDou GEO.
  * ------------------------------------------------------------------------------------------- */
 #define GNSSHIP_SYS_GPS_L1CA 0 /* GPS L1 C/A: 3 taps, bit sync on the 160-symbol preamble */
 #define GNSSHIP_SYS_GAL_E1 1   /* Galileo E1 B/C: VEML 5 taps on the pilot + data prompt, CS25 secondary */
@@ -263,6 +263,8 @@ typedef struct gnsship_trk_conf { /* Dll_Pll_Conf (dll_pll_conf.h:33-80), same n
     float very_early_late_space_narrow_chips;
     int32_t enable_fll_pull_in;      /* FLL-assisted carrier loop during the pull-in (:1080-1097) */
     int32_t enable_fll_steady_state; /* ... and after it */
+    int32_t high_dyn;                /* high-dynamics correlator + NCO rate smoothing (:1205-1255) */
+    uint32_t smoother_length;        /* rate smoother length, 1..64 (0 is raised to 1, dll_pll_conf.cc:118-123) */
 } gnsship_trk_conf;
 
 typedef struct gnsship_trk_start_args { /* Gnss_Synchro fields start_tracking reads (:647-649) */

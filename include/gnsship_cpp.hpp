@@ -341,6 +341,8 @@ struct Dll_Pll_Conf {
     float pll_bw_narrow_hz{5.0F}, dll_bw_narrow_hz{0.75F};
     int32_t extend_correlation_symbols{1};
     bool enable_fll_pull_in{false}, enable_fll_steady_state{false};
+    bool high_dyn{false};
+    uint32_t smoother_length{10U};
     float slope{1.0F}, spc{0.5F}, y_intercept{1.0F};
     float cn0_smoother_alpha{0.002F}, carrier_lock_test_smoother_alpha{0.002F};
     uint32_t pull_in_time_s{10U}, bit_synchronization_time_limit_s{20U}, vector_length{0U};
@@ -392,6 +394,8 @@ public:
         c.very_early_late_space_narrow_chips = conf.very_early_late_space_narrow_chips;
         c.enable_fll_pull_in = conf.enable_fll_pull_in ? 1 : 0;
         c.enable_fll_steady_state = conf.enable_fll_steady_state ? 1 : 0;
+        c.high_dyn = conf.high_dyn ? 1 : 0;
+        c.smoother_length = conf.smoother_length;
         c.system = conf.system == 'E' ? GNSSHIP_SYS_GAL_E1 : conf.system == 'C' ? GNSSHIP_SYS_BDS_B1I : GNSSHIP_SYS_GPS_L1CA;
         code_base_ = 1024 + 2 * max_channels * next_engine_id();
         std::lock_guard<std::mutex> lk(dev_->mutex());

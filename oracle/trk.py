@@ -35,6 +35,7 @@ class OrcTrkConf(ctypes.Structure):
         ("extend_correlation_symbols", ctypes.c_int32), ("pll_bw_narrow_hz", ctypes.c_float), ("dll_bw_narrow_hz", ctypes.c_float),
         ("early_late_space_narrow_chips", ctypes.c_float), ("very_early_late_space_narrow_chips", ctypes.c_float),
         ("enable_fll_pull_in", ctypes.c_int32), ("enable_fll_steady_state", ctypes.c_int32),
+        ("high_dyn", ctypes.c_int32), ("smoother_length", ctypes.c_uint32),
     ]
 
 
@@ -74,7 +75,8 @@ def conf(system: str, fs_in: float, vector_length: int, **kw) -> OrcTrkConf:
                    secondary_code_length=len(sec_code), data_secondary_code_length=len(dsec),
                    secondary_code=sec_code.encode(), data_secondary_code=dsec.encode(),
                    extend_correlation_symbols=1, pll_bw_narrow_hz=5.0, dll_bw_narrow_hz=0.75, early_late_space_narrow_chips=0.15,
-                   very_early_late_space_narrow_chips=0.5, enable_fll_pull_in=0, enable_fll_steady_state=0)
+                   very_early_late_space_narrow_chips=0.5, enable_fll_pull_in=0, enable_fll_steady_state=0,
+                   high_dyn=0, smoother_length=10)
     for k, v in kw.items():
         setattr(c, k, v)
     return c

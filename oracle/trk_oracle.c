@@ -16,8 +16,9 @@
  *       cn0_and_tracking_lock_status :972-1029, do_correlation_step :1037-1062,
  *       run_dll_pll :1065-1152, save_correlation_results :1262-1350, update_tracking_vars :1189-1260,
  *       acquire_secondary :925-970.
- * Extended coherent integration (state 3, extend_correlation_symbols > 1), high_dyn smoothing,
- * the FLL branches and the Doppler-correction experiment are not restated (defaults off).
+ * Also restated: extended coherent integration (state 3, extend_correlation_symbols > 1), the FLL
+ * branches of run_dll_pll (:1080-1097) and the high_dyn NCO rate smoothing (:1205-1255) with the
+ * high-dynamics multicorrelator.  The Doppler-correction experiment is not (default off).
  */
 #include <math.h>
 #include <stdint.h>
@@ -339,7 +340,11 @@ typedef struct {
     int32_t extend_correlation_symbols;
     float pll_bw_narrow_hz, dll_bw_narrow_hz, early_late_space_narrow_chips, very_early_late_space_narrow_chips;
     int32_t enable_fll_pull_in, enable_fll_steady_state; /* dll_pll_conf.h:75-76 */
+    int32_t high_dyn;         /* dll_pll_conf.h:80: high-dynamics correlator + NCO rate smoothing */
+    uint32_t smoother_length; /* dll_pll_conf.h:62 (dll_pll_conf.cc:118-123 raises 0 to 1) */
 } orc_trk_conf;
+
+#define TRK_MAX_SMOOTHER 64
 
 typedef struct {
     int state, cloop, pull_in, veml, n_taps, pll_180;
@@ -363,6 +368,11 @@ typedef struct {
     orc_fll_pll carrier_filter;
     orc_smoother cn0_sm, lock_sm;
     int extend_count; /* d_extend_correlation_symbols_count */
+    /* high_dyn: d_carr_ph_history / d_code_ph_history (boost::circular_buffer of capacity
+     * 2·smoother_length, :557-566) — pushed together with the same sample count, so one ring */
+    double carrier_phase_rate_step_rad, code_phase_rate_step_chips;
+    double hist_carr[2 * TRK_MAX_SMOOTHER], hist_code[2 * TRK_MAX_SMOOTHER], hist_samples[2 * TRK_MAX_SMOOTHER];
+    int hist_head, hist_count;
 } orc_trk_channel;
 
 typedef struct { /* Gnss_Synchro subset emitted per epoch (dll_pll_veml_tracking.cc:1996-2091) */
@@ -386,6 +396,10 @@ static void clear_tracking_vars(orc_trk_channel* c)
     c->current_symbol = 0;
     c->current_data_symbol = 0;
     c->prompt_count = 0;
+    c->carrier_phase_rate_step_rad = 0.0; /* :1182-1185 */
+    c->code_phase_rate_step_chips = 0.0;
+    c->hist_head = 0;
+    c->hist_count = 0;
 }
 
 /* start_tracking (:643-883) then the state-1 pull-in alignment (:1757-1788) evaluated when the
@@ -453,10 +467,10 @@ void orc_trk_correlation_args(const orc_trk_conf* k, const orc_trk_channel* c, f
     const float spcf = (float)k->code_samples_per_chip;
     out[0] = c->rem_carr_phase_rad;
     out[1] = (float)c->carrier_phase_step_rad;
-    out[2] = 0.0F;
+    out[2] = (float)c->carrier_phase_rate_step_rad;
     out[3] = (float)c->rem_code_phase_chips * spcf;
     out[4] = (float)c->code_phase_step_chips * spcf;
-    out[5] = 0.0F;
+    out[5] = (float)c->code_phase_rate_step_chips * spcf; /* do_correlation_step :1043-1048 */
 }
 
 static int cn0_and_tracking_lock_status(const orc_trk_conf* k, orc_trk_channel* c, double coh_integration_time_s)
@@ -519,6 +533,24 @@ static void run_dll_pll(const orc_trk_conf* k, orc_trk_channel* c)
     if (k->carrier_aiding) c->code_freq_chips += c->carrier_doppler_hz * k->code_chip_rate / k->signal_carrier_freq;
 }
 
+/* The high_dyn rate estimate (:1205-1222, :1238-1255): mean phase step of the newest
+ * smoother_length entries minus the mean of the oldest, over the newest entries' sample count.
+ * Both sums run in the reference's index order. */
+static double smoothed_rate(const orc_trk_channel* c, const double* first, int L)
+{
+    const int cap = 2 * L;
+    double cp1 = 0.0, cp2 = 0.0, samples = 0.0;
+    for (int i = 0; i < L; i++) {
+        const int a = (c->hist_head + i) % cap, b = (c->hist_head + cap - i - 1) % cap;
+        cp1 += first[a];
+        cp2 += first[b];
+        samples += c->hist_samples[b];
+    }
+    cp1 /= (double)L;
+    cp2 /= (double)L;
+    return (cp2 - cp1) / samples;
+}
+
 static void update_tracking_vars(const orc_trk_conf* k, orc_trk_channel* c)
 {
     c->T_chip_seconds = 1.0 / c->code_freq_chips;
@@ -528,10 +560,30 @@ static void update_tracking_vars(const orc_trk_conf* k, orc_trk_channel* c)
     c->current_prn_length_samples = (int32_t)floor(c->K_blk_samples);
     c->carrier_phase_step_rad = TRK_TWO_PI * c->carrier_doppler_hz / k->fs_in;
     const double n = (double)c->current_prn_length_samples;
-    c->rem_carr_phase_rad += (float)(c->carrier_phase_step_rad * n + 0.5 * 0.0 * n * n);
-    c->rem_carr_phase_rad = (float)fmod((double)c->rem_carr_phase_rad, TRK_TWO_PI);
-    c->acc_carrier_phase_rad -= (c->carrier_phase_step_rad * n + 0.5 * 0.0 * n * n);
     c->code_phase_step_chips = c->code_freq_chips / k->fs_in;
+    if (k->high_dyn) {
+        /* push_back on the ring (a full circular_buffer drops its oldest entry) */
+        const int L = (int)(k->smoother_length < 1 ? 1 : k->smoother_length), cap = 2 * L;
+        int slot;
+        if (c->hist_count < cap) {
+            slot = (c->hist_head + c->hist_count) % cap;
+            c->hist_count++;
+        } else {
+            slot = c->hist_head;
+            c->hist_head = (c->hist_head + 1) % cap;
+        }
+        c->hist_carr[slot] = c->carrier_phase_step_rad;
+        c->hist_code[slot] = c->code_phase_step_chips;
+        c->hist_samples[slot] = n;
+        if (c->hist_count == cap) {
+            c->carrier_phase_rate_step_rad = smoothed_rate(c, c->hist_carr, L);
+            c->code_phase_rate_step_chips = smoothed_rate(c, c->hist_code, L);
+        }
+    }
+    const double adv = c->carrier_phase_step_rad * n + 0.5 * c->carrier_phase_rate_step_rad * n * n;
+    c->rem_carr_phase_rad += (float)adv;
+    c->rem_carr_phase_rad = (float)fmod((double)c->rem_carr_phase_rad, TRK_TWO_PI);
+    c->acc_carrier_phase_rad -= adv;
     c->rem_code_phase_samples = c->K_blk_samples - n;
     c->rem_code_phase_chips = c->code_freq_chips * c->rem_code_phase_samples / k->fs_in;
 }
@@ -788,11 +840,11 @@ int orc_trk_run(const orc_trk_conf* k, orc_trk_channel* c, const float* samples,
         orc_trk_correlation_args(k, c, args);
         float taps[10] = {0}, pdata[2] = {0};
         const float* x = samples + 2 * (c->nitems_read - buffer_first);
-        orc_multicorrelator_real_codes(taps, x, code, code_len, c->shifts, c->n_taps, 0, args[0], args[1], args[2], args[3], args[4], args[5], vl,
+        orc_multicorrelator_real_codes(taps, x, code, code_len, c->shifts, c->n_taps, k->high_dyn, args[0], args[1], args[2], args[3], args[4], args[5], vl,
             scratch);
         if (k->track_pilot && data_code) {
             const float zero = 0.0F;
-            orc_multicorrelator_real_codes(pdata, x, data_code, code_len, &zero, 1, 0, args[0], args[1], args[2], args[3], args[4], args[5], vl,
+            orc_multicorrelator_real_codes(pdata, x, data_code, code_len, &zero, 1, k->high_dyn, args[0], args[1], args[2], args[3], args[4], args[5], vl,
                 scratch);
         }
         if (!orc_trk_epoch_update(k, c, taps, pdata, &out[e])) {

@@ -22,7 +22,8 @@ SHARED = ["fs_in", "carrier_lock_th", "pll_bw_hz", "dll_bw_hz", "fll_bw_hz", "ea
           "bit_synchronization_time_limit_s", "vector_length", "pll_filter_order", "dll_filter_order", "cn0_samples",
           "cn0_smoother_samples", "carrier_lock_test_smoother_samples", "cn0_min", "max_code_lock_fail", "max_carrier_lock_fail",
           "carrier_aiding", "track_pilot", "extend_correlation_symbols", "pll_bw_narrow_hz", "dll_bw_narrow_hz",
-          "early_late_space_narrow_chips", "very_early_late_space_narrow_chips", "enable_fll_pull_in", "enable_fll_steady_state"]
+          "early_late_space_narrow_chips", "very_early_late_space_narrow_chips", "enable_fll_pull_in", "enable_fll_steady_state",
+          "high_dyn", "smoother_length"]
 
 
 def dev_conf(k, system):
@@ -125,6 +126,34 @@ def test_fll_assisted_loop_matches_oracle(ctx, pull_in, steady):
     assert len(ref) > 100
     compare(rec[:, 0], ref, f"fll {pull_in}{steady}")
     trk.close()
+
+
+@pytest.mark.parametrize("system,fs,epochs,rate_hz_s,smoother", [("GPS", 4e6, 500, 40.0, 10), ("GPS", 4e6, 300, -25.0, 1),
+                                                                  ("GAL", 25e6 / 4, 100, 30.0, 10), ("BDS", 4.092e6, 300, 20.0, 7)])
+def test_high_dyn_loop_matches_oracle(ctx, system, fs, epochs, rate_hz_s, smoother):
+    """high_dyn (dll_pll_veml_tracking.cc:1205-1255 with the high-dynamics correlator pair
+    :530,536): the carrier / code NCO rates are the smoothed differences of the last
+    2·smoother_length phase steps and drive the high-dynamics resampler and rotator (taps 1.. are
+    circular shifts of tap 0).  A Doppler ramp of tens of Hz/s; every epoch compared.  (Not E1 with
+    smoother_length 4: there the rate feedback amplifies a 1e-4 Hz start perturbation to 0.08 Hz
+    in the oracle itself, so rounding-level device/oracle differences grow the same way.)"""
+    sat, k, x, stamp, first, delay, dop = S.sync(system, fs, epochs, high_dyn=1, smoother_length=smoother, rate_hz_s=rate_hz_s)
+    trk = engine.DllPllVemlTracking(ctx, dev_conf(k, system), 1)
+    ctx.set_code(50, sat.code)
+    if sat.code_data is not None:
+        ctx.set_code(51, sat.code_data)
+    trk.start(0, 50, delay, dop, stamp, first, data_code_id=51)
+    rec, rounds = trk.run(x, first, epochs)
+    ref = T.track(k, x, sat.code, delay, dop, stamp, first, epochs, data_code=sat.code_data, buffer_first=first)
+    assert len(ref) == epochs and ref["state"][-1] in (2, 4)
+    compare(rec[:, 0], ref, f"high_dyn {system}")
+    trk.close()
+
+
+def test_high_dyn_smoother_length_bound(ctx):
+    k = abi.TrkConf.defaults(abi.SYS_GPS_L1CA, 4e6, 4000, high_dyn=1, smoother_length=65)
+    with pytest.raises(abi.GnssHipError):
+        engine.DllPllVemlTracking(ctx, k, 1)
 
 
 def test_buffers_in_pieces_and_channel_state(ctx):

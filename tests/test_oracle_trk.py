@@ -167,3 +167,19 @@ def test_fll_diff_atan_identities(built):
         assert abs(got - want) < 1e-3 * max(1.0, abs(want)), (f_hz, got)
     z = np.zeros(2, np.float32)
     assert L.orc_fll_diff_atan(z.ctypes.data_as(f32p), z.ctypes.data_as(f32p), 0.0, 0.001) == 0.0
+
+
+@pytest.mark.parametrize("system,fs,epochs,rate", [("GPS", 4e6, 500, 40.0), ("GAL", 25e6 / 4, 100, 30.0)])
+def test_high_dyn_loop_follows_doppler_ramp(built, system, fs, epochs, rate):
+    """high_dyn (dll_pll_veml_tracking.cc:1205-1255): the oracle loop with the rate smoother and the
+    high-dynamics correlator synchronises on a Doppler ramp and follows it."""
+    sat, k, x, stamp, first, delay, dop = S.sync(system, fs, epochs, high_dyn=1, smoother_length=10, rate_hz_s=rate)
+    rec = T.track(k, x, sat.code, delay, dop, stamp, first, epochs, data_code=sat.code_data, buffer_first=first)
+    assert len(rec) == epochs and rec["state"][-1] == 4
+    truth = sat.doppler_hz + rate * rec["sample_counter"] / fs
+    h = epochs // 2
+    assert np.sqrt(np.mean((rec["carrier_doppler_hz"][h:] - truth[h:]) ** 2)) < 6.0
+    # the rate actually enters: the same loop without high_dyn differs
+    k0 = T.conf(system, fs, k.vector_length, pull_in_time_s=0, high_dyn=0)
+    rec0 = T.track(k0, x, sat.code, delay, dop, stamp, first, epochs, data_code=sat.code_data, buffer_first=first)
+    assert np.any(rec0["carrier_doppler_hz"] != rec["carrier_doppler_hz"])

@@ -27,19 +27,19 @@ SYNC_PATTERNS = {"GPS": dict(bits="1000101100110"), "GAL": dict(secondary=T.E1C_
                  "BDS": dict(secondary=T.B1I_NH, bits="0111")}
 
 
-def sync(system, fs, epochs, prn=9, dop=1210.0, delay_chips=100.3, seed=5, cn0=50.0, **conf_kw):
+def sync(system, fs, epochs, prn=9, dop=1210.0, delay_chips=100.3, seed=5, cn0=50.0, rate_hz_s=0.0, **conf_kw):
     """A signal carrying the pattern the block synchronises on (GPS navigation bits with the
     10001011 preamble, CS25 on the E1-C pilot, the B1I NH code), acquisition stamped one second
     before tracking starts so that pull_in_time_s = 0 ends the pull-in at once.  x[0] is absolute
-    sample `first` = fs."""
+    sample `first` = fs.  rate_hz_s: Doppler ramp (the acquisition reports the Doppler at `first`)."""
     sat = signals.Satellite(prn=prn, doppler_hz=dop, code_delay_chips=delay_chips, cn0_dbhz=cn0, system=system, carrier_phase_rad=1.0,
-                            **SYNC_PATTERNS[system])
+                            doppler_rate_hz_s=rate_hz_s, **SYNC_PATTERNS[system])
     kw = dict(pull_in_time_s=0)
     kw.update(conf_kw)
     k = T.conf(system, fs, int(round(fs * T.SYSTEMS[system][2])), **kw)
     first = int(fs)
     x = signals.generate_if(fs, int(round(fs)) // 4 + k.vector_length * (epochs + 3), [sat], seed=seed, start=first)
-    return sat, k, x, 0, first, acq_delay_for(sat, fs, system, 0, first) + 0.2, sat.doppler_hz + 15.0
+    return sat, k, x, 0, first, acq_delay_for(sat, fs, system, 0, first) + 0.2, sat.doppler_hz + rate_hz_s + 15.0
 
 
 def code_tracking_error_chips(sat, fs, rec, system):
