@@ -117,7 +117,8 @@ class TrkConf(ctypes.Structure):
 class TrkStartArgs(ctypes.Structure):
     """gnsship_trk_start_args — the Gnss_Synchro fields start_tracking reads (:647-649)."""
     _fields_ = [("code_id", ctypes.c_int32), ("data_code_id", ctypes.c_int32), ("acq_delay_samples", ctypes.c_double),
-                ("acq_doppler_hz", ctypes.c_double), ("acq_samplestamp_samples", ctypes.c_uint64), ("first_sample", ctypes.c_uint64)]
+                ("acq_doppler_hz", ctypes.c_double), ("acq_samplestamp_samples", ctypes.c_uint64), ("first_sample", ctypes.c_uint64),
+                ("prn", ctypes.c_int32), ("reserved", ctypes.c_int32)]
 
 
 TRK_EPOCH_DTYPE = np.dtype([

@@ -131,6 +131,7 @@ bool build_params(const gnsship_trk_conf& c, TrkParams& p)
     p.conf = c;
     if (p.conf.smoother_length < 1) p.conf.smoother_length = 1;  // dll_pll_conf.cc:119-123
     char sec[kTrkMaxSecondary + 1] = {0};
+    SymSync& g = p.sync[0];
     switch (c.system) {
     case GNSSHIP_SYS_GPS_L1CA:  // :142-200 (1C), start_tracking :662-668 forces track_pilot = false
         p.code_chip_rate = 1.023e6;
@@ -138,13 +139,13 @@ bool build_params(const gnsship_trk_conf& c, TrkParams& p)
         p.code_period = 0.001;
         p.code_length_chips = 1023;
         p.code_samples_per_chip = 1;
-        p.symbols_per_bit = 20;
+        g.symbols_per_bit = 20;
         p.veml = 0;
         p.track_pilot = 0;
-        p.secondary = 0;
+        g.secondary = 0;
         gps_preamble_symbols(sec);
-        p.secondary_len = 160;
-        set_bits(p.secondary_bits, sec);
+        g.secondary_len = 160;
+        set_bits(g.secondary_bits, sec);
         break;
     case GNSSHIP_SYS_GAL_E1:  // :262-291 (1B); Galileo_E1.h:35-52
         p.code_chip_rate = 1.023e6;
@@ -152,13 +153,13 @@ bool build_params(const gnsship_trk_conf& c, TrkParams& p)
         p.code_period = 0.004;
         p.code_length_chips = 4092;
         p.code_samples_per_chip = 2;
-        p.symbols_per_bit = 1;
+        g.symbols_per_bit = 1;
         p.veml = 1;
         p.track_pilot = c.track_pilot ? 1 : 0;
         if (p.track_pilot) {
-            p.secondary = 1;
-            p.secondary_len = 25;
-            set_bits(p.secondary_bits, "0011100000001010110110010");  // CS25 (GALILEO_E1_C_SECONDARY_CODE)
+            g.secondary = 1;
+            g.secondary_len = 25;
+            set_bits(g.secondary_bits, "0011100000001010110110010");  // CS25 (GALILEO_E1_C_SECONDARY_CODE)
         }
         break;
     case GNSSHIP_SYS_BDS_B1I:  // :762-797 (MEO/IGSO branch); Beidou_B1I.h:35-48
@@ -167,14 +168,14 @@ bool build_params(const gnsship_trk_conf& c, TrkParams& p)
         p.code_period = 0.001;
         p.code_length_chips = 2046;
         p.code_samples_per_chip = 1;
-        p.symbols_per_bit = 20;
+        g.symbols_per_bit = 20;
         p.veml = 0;
         p.track_pilot = 0;
-        p.secondary = 1;
-        p.secondary_len = 20;
-        set_bits(p.secondary_bits, "00000100110101001110");  // NH code (BEIDOU_B1I_SECONDARY_CODE_STR)
-        p.data_secondary_len = 20;
-        set_bits(p.data_secondary_bits, "00000100110101001110");
+        g.secondary = 1;
+        g.secondary_len = 20;
+        set_bits(g.secondary_bits, "00000100110101001110");  // NH code (BEIDOU_B1I_SECONDARY_CODE_STR)
+        g.data_secondary_len = 20;
+        set_bits(g.data_secondary_bits, "00000100110101001110");
         break;
     default: return false;
     }
@@ -192,8 +193,23 @@ bool build_params(const gnsship_trk_conf& c, TrkParams& p)
         p.shifts[2] = c.early_late_space_chips * spcf;
     }
     // extended integration (:515-523): enabled when extend_correlation_symbols > 1
-    p.extend = c.extend_correlation_symbols > 1 ? c.extend_correlation_symbols : 1;
-    p.T_ext = static_cast<float>(p.extend) * static_cast<float>(p.code_period);
+    g.extend = c.extend_correlation_symbols > 1 ? c.extend_correlation_symbols : 1;
+    g.T_ext = static_cast<float>(g.extend) * static_cast<float>(p.code_period);
+    // BeiDou B1I GEO satellites (start_tracking :765-781; Beidou_B1I.h:41-49): D2 navigation at 2
+    // symbols per bit, no NH code, bit synchronisation on the 22-symbol preamble, extend ≤ 2
+    p.sync[1] = g;
+    if (c.system == GNSSHIP_SYS_BDS_B1I) {
+        SymSync& geo = p.sync[1];
+        std::memset(geo.secondary_bits, 0, sizeof(geo.secondary_bits));
+        std::memset(geo.data_secondary_bits, 0, sizeof(geo.data_secondary_bits));
+        geo.symbols_per_bit = 2;
+        geo.secondary = 0;
+        geo.secondary_len = 22;
+        set_bits(geo.secondary_bits, "1111110000001100001100");  // BEIDOU_B1I_GEO_PREAMBLE_SYMBOLS_STR
+        geo.data_secondary_len = 0;
+        if (geo.extend > 2) geo.extend = 2;
+        geo.T_ext = static_cast<float>(geo.extend) * static_cast<float>(p.code_period);
+    }
     if (p.veml) {
         p.shifts_n[0] = -c.very_early_late_space_narrow_chips * spcf;
         p.shifts_n[1] = -c.early_late_space_narrow_chips * spcf;
@@ -208,10 +224,11 @@ bool build_params(const gnsship_trk_conf& c, TrkParams& p)
     p.spc_n = c.early_late_space_narrow_chips;
     // wide: (code period, dll_bw); narrow: set_update_interval(T_ext) + set_noise_bandwidth(dll_bw_narrow)
     loop_filter_coefficients(static_cast<float>(p.code_period), c.dll_bw_hz, c.dll_filter_order, p.ls[0]);
-    loop_filter_coefficients(p.T_ext, c.dll_bw_narrow_hz, c.dll_filter_order, p.ls[1]);
+    loop_filter_coefficients(p.sync[0].T_ext, c.dll_bw_narrow_hz, c.dll_filter_order, p.ls[1]);
+    loop_filter_coefficients(p.sync[1].T_ext, c.dll_bw_narrow_hz, c.dll_filter_order, p.ls[2]);
     // Tracking_FLL_PLL_filter::set_params (tracking_FLL_PLL_filter.cc:23-55): wide, then narrow (:1904)
     p.fp_order = c.pll_filter_order;
-    for (int s = 0; s < 2; s++) {
+    for (int s = 0; s < 3; s++) {
         LoopSet& q = p.ls[s];
         const float pll_bw = s ? c.pll_bw_narrow_hz : c.pll_bw_hz;
         if (p.fp_order == 3) {
@@ -382,6 +399,8 @@ extern "C" int gnsship_trk_start(gnsship_trk* t, int channel, const gnsship_trk_
     std::memset(&c, 0, sizeof(c));
     const gnsship_trk_conf& k = p.conf;
     c.code_id = a->code_id;
+    // GEO satellites use the D2 symbol-sync profile (start_tracking :765-781)
+    c.geo = (p.conf.system == GNSSHIP_SYS_BDS_B1I && ((a->prn > 0 && a->prn < 6) || a->prn > 58)) ? 1 : 0;
     c.data_code_id = p.track_pilot ? a->data_code_id : a->code_id;
     c.acq_sample_stamp = a->acq_samplestamp_samples;
     c.carrier_doppler_hz = a->acq_doppler_hz;

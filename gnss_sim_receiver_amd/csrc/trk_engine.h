@@ -20,20 +20,27 @@ struct LoopSet {
     float fp_w0p3, fp_w0f2, fp_a2, fp_w0f, fp_a3, fp_w0p2, fp_b3, fp_w0p;
 };
 
+// Symbol synchronisation of one satellite class: the members start_tracking sets per PRN
+// (:762-797).  Profile 0 is the system's; profile 1 the BeiDou B1I GEO one (PRN 1-5, 59+: D2
+// navigation at 2 symbols per bit, 22-symbol preamble search, no NH code, extend capped at 2).
+struct SymSync {
+    int32_t symbols_per_bit, secondary, secondary_len, data_secondary_len;
+    int32_t extend;   // d_extend_correlation_symbols (> 1: extended integration enabled)
+    float T_ext;      // (float)extend · (float)code_period
+    uint32_t secondary_bits[kTrkMaxSecondary / 32];       // bit i = character i == '1'
+    uint32_t data_secondary_bits[kTrkMaxSecondary / 32];
+};
+
 struct TrkParams {
     gnsship_trk_conf conf;
     double code_chip_rate, carrier_freq, code_period;
-    int32_t code_length_chips, code_samples_per_chip, symbols_per_bit, veml, track_pilot;
-    int32_t secondary, secondary_len, data_secondary_len, n_taps;
-    uint32_t secondary_bits[kTrkMaxSecondary / 32];       // bit i = character i == '1'
-    uint32_t data_secondary_bits[kTrkMaxSecondary / 32];
+    int32_t code_length_chips, code_samples_per_chip, veml, track_pilot, n_taps;
+    SymSync sync[2];
     float shifts[5];                                        // d_local_code_shift_chips (× samples per chip)
-    // Tracking_loop_filter (code) coefficients and Tracking_FLL_PLL_filter constants; set [1] is
-    // the narrow configuration of extended integration (:1902-1904)
-    LoopSet ls[2];
+    // Tracking_loop_filter (code) coefficients and Tracking_FLL_PLL_filter constants; set 1 + geo is
+    // the narrow configuration of extended integration (:1902-1904) for sync profile geo
+    LoopSet ls[3];
     int32_t fp_order;
-    int32_t extend;      // extend_correlation_symbols (> 1: extended integration enabled)
-    float T_ext;         // (float)extend · (float)code_period
     float shifts_n[5];   // narrow taps
     float spc_n;
     // Exponential_Smoother settings
@@ -54,6 +61,7 @@ struct Smoother {
 // One channel: the dll_pll_veml_tracking members the per-epoch path reads or writes.
 struct TrkChannel {
     int32_t state;  // 0 idle / lost, 2 wide tracking, 3 coherent integration, 4 narrow tracking
+    int32_t geo;    // symbol-sync profile (TrkParams::sync): 1 for a BeiDou B1I GEO satellite
     int32_t narrow;     // loop set / taps in use (1 after entering extended integration)
     int32_t ext_count;  // d_extend_correlation_symbols_count
     int32_t cloop, pull_in, pll_180, ran, acc_phase_init;

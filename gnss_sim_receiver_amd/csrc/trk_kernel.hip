@@ -131,7 +131,7 @@ __device__ bool lock_status(const TrkParams& k, TrkChannel& c, double coh_integr
 
 __device__ float loop_filter_apply(const TrkParams& k, TrkChannel& c, float x)
 {
-    const LoopSet& q = k.ls[c.narrow];
+    const LoopSet& q = k.ls[c.narrow ? 1 + c.geo : 0];
     float result = 0.0f;
     for (int ii = 0; ii < q.lf_n_out; ii++) result = __fadd_rn(result, __fmul_rn(q.lf_out[ii], c.lf_outputs[(c.lf_idx + ii) % 4]));
     c.lf_idx--;
@@ -144,7 +144,7 @@ __device__ float loop_filter_apply(const TrkParams& k, TrkChannel& c, float x)
 
 __device__ float carrier_filter(const TrkParams& k, TrkChannel& c, float fll, float pll, float T)
 {
-    const LoopSet& q = k.ls[c.narrow];
+    const LoopSet& q = k.ls[c.narrow ? 1 + c.geo : 0];
     if (k.fp_order == 3) {
         c.fp_w = __fadd_rn(c.fp_w, __fmul_rn(T, __fadd_rn(__fmul_rn(q.fp_w0p3, pll), __fmul_rn(q.fp_w0f2, fll))));
         const float inner = __fadd_rn(__fadd_rn(__fmul_rn(0.5f, c.fp_w), __fmul_rn(__fmul_rn(q.fp_a2, q.fp_w0f), fll)),
@@ -167,10 +167,10 @@ __device__ void run_dll_pll(const TrkParams& k, TrkChannel& c)
         disc = static_cast<double>(atan2f(c.p[1], c.p[0]));  // gr::fast_atan2f restated as atan2f
     c.carr_phase_error_hz = disc / kTwoPi;
     // d_current_correlation_time_s: the code period, or extend × code period once extended
-    const float T = c.narrow ? k.T_ext : static_cast<float>(k.code_period);
+    const float T = c.narrow ? k.sync[c.geo].T_ext : static_cast<float>(k.code_period);
     if ((c.pull_in && k.conf.enable_fll_pull_in) || k.conf.enable_fll_steady_state) {  // :1080-1097
         // d_current_correlation_time_s is a double: the code period, or (float)extend·(float)period
-        const double Td = c.narrow ? static_cast<double>(k.T_ext) : k.code_period;
+        const double Td = c.narrow ? static_cast<double>(k.sync[c.geo].T_ext) : k.code_period;
         const double fe = fll_diff_atan(c.p_old, c.p, 0.0, Td) / kTwoPi;
         c.p_old[0] = c.p[0];
         c.p_old[1] = c.p[1];
@@ -264,7 +264,7 @@ __device__ __forceinline__ int bit_at(const uint32_t* bits, int i) { return (bit
 
 __device__ void push_sign(const TrkParams& k, TrkChannel& c, float prompt_re)
 {
-    const int cap = k.secondary_len;
+    const int cap = k.sync[c.geo].secondary_len;
     const uint32_t neg = prompt_re < 0.0f ? 1u : 0u;
     if (c.sign_count == cap) {  // boost::circular_buffer::push_back on a full buffer drops the oldest
         for (int w = 0; w < kTrkMaxSecondary / 32; w++) {
@@ -282,12 +282,12 @@ __device__ void push_sign(const TrkParams& k, TrkChannel& c, float prompt_re)
 __device__ bool acquire_secondary(const TrkParams& k, TrkChannel& c)
 {
     int corr = 0;
-    for (int i = 0; i < k.secondary_len; i++) {
+    for (int i = 0; i < k.sync[c.geo].secondary_len; i++) {
         const int neg = bit_at(c.sign_bits, i);
-        const int one = bit_at(k.secondary_bits, i);
+        const int one = bit_at(k.sync[c.geo].secondary_bits, i);
         corr += (neg ^ one) ? 1 : -1;  // +1 for (real < 0, '0') and (real ≥ 0, '1')
     }
-    if (abs(corr) == k.secondary_len) {
+    if (abs(corr) == k.sync[c.geo].secondary_len) {
         c.pll_180 = corr < 0 ? 1 : 0;
         return true;
     }
@@ -364,9 +364,9 @@ __device__ bool epoch_update(const TrkParams& k, TrkChannel& c, const float* tap
             run_dll_pll(k, c);
             update_tracking_vars(k, c, h);
             if (!c.pull_in) {
-                if (k.secondary || k.symbols_per_bit > 1) {
+                if (k.sync[c.geo].secondary || k.sync[c.geo].symbols_per_bit > 1) {
                     push_sign(k, c, taps[eo + 2]);
-                    if (c.sign_count == k.secondary_len) next_state = acquire_secondary(k, c);
+                    if (c.sign_count == k.sync[c.geo].secondary_len) next_state = acquire_secondary(k, c);
                 } else {
                     next_state = true;
                 }
@@ -377,7 +377,7 @@ __device__ bool epoch_update(const TrkParams& k, TrkChannel& c, const float* tap
                 c.sign_count = 0;
                 c.current_symbol = 0;
                 c.current_data_symbol = 0;
-                if (k.extend > 1) {  // extended integration (:1890-1926): narrow loops and taps, state 3
+                if (k.sync[c.geo].extend > 1) {  // extended integration (:1890-1926): narrow loops and taps, state 3
                     c.ext_count = 0;
                     c.narrow = 1;
                     c.spc = k.spc_n;
@@ -390,9 +390,9 @@ __device__ bool epoch_update(const TrkParams& k, TrkChannel& c, const float* tap
     } else {
         // save_correlation_results
         float sgn = 1.0f;
-        if (k.secondary) {
-            sgn = bit_at(k.secondary_bits, c.current_symbol) ? -1.0f : 1.0f;
-            c.current_symbol = (c.current_symbol + 1) % k.secondary_len;
+        if (k.sync[c.geo].secondary) {
+            sgn = bit_at(k.sync[c.geo].secondary_bits, c.current_symbol) ? -1.0f : 1.0f;
+            c.current_symbol = (c.current_symbol + 1) % k.sync[c.geo].secondary_len;
         }
         if (k.veml) {
             cadd(c.ve, taps, sgn);
@@ -402,13 +402,13 @@ __device__ bool epoch_update(const TrkParams& k, TrkChannel& c, const float* tap
         cadd(c.p, taps + eo + 2, sgn);
         cadd(c.l, taps + eo + 4, sgn);
         const float* src = k.track_pilot ? pdata : taps + eo + 2;
-        if (k.symbols_per_bit > 1) {
-            if (k.data_secondary_len > 0) {
-                cadd(c.p_data, src, bit_at(k.data_secondary_bits, c.current_data_symbol) ? -1.0f : 1.0f);
-                c.current_data_symbol = (c.current_data_symbol + 1) % k.data_secondary_len;
+        if (k.sync[c.geo].symbols_per_bit > 1) {
+            if (k.sync[c.geo].data_secondary_len > 0) {
+                cadd(c.p_data, src, bit_at(k.sync[c.geo].data_secondary_bits, c.current_data_symbol) ? -1.0f : 1.0f);
+                c.current_data_symbol = (c.current_data_symbol + 1) % k.sync[c.geo].data_secondary_len;
             } else {
                 cadd(c.p_data, src, 1.0f);
-                c.current_data_symbol = (c.current_data_symbol + 1) % k.symbols_per_bit;
+                c.current_data_symbol = (c.current_data_symbol + 1) % k.sync[c.geo].symbols_per_bit;
             }
         } else {
             c.p_data[0] = src[0];
@@ -424,11 +424,11 @@ __device__ bool epoch_update(const TrkParams& k, TrkChannel& c, const float* tap
                 c.p_data[0] = c.p_data[1] = 0.0f;
             }
             c.ext_count++;
-            if (c.ext_count == k.extend - 1) {
+            if (c.ext_count == k.sync[c.geo].extend - 1) {
                 c.ext_count = 0;
                 c.state = 4;
             }
-        } else if (!lock_status(k, c, k.code_period * static_cast<double>(k.extend))) {
+        } else if (!lock_status(k, c, k.code_period * static_cast<double>(k.sync[c.geo].extend))) {
             clear_tracking_vars(c);
             c.state = 0;
             loss = true;
@@ -446,7 +446,7 @@ __device__ bool epoch_update(const TrkParams& k, TrkChannel& c, const float* tap
                 c.p_data[0] = c.p_data[1] = 0.0f;
             }
             zero_accu(c);
-            if (k.extend > 1) c.state = 3;  // next coherent integration cycle
+            if (k.sync[c.geo].extend > 1) c.state = 3;  // next coherent integration cycle
         }
     }
     rec.state = st;

@@ -352,9 +352,10 @@ class DllPllVemlTracking:
         self.h = h
 
     def start(self, channel: int, code_id: int, acq_delay_samples: float, acq_doppler_hz: float, acq_samplestamp: int,
-              first_sample: int, data_code_id: int = -1):
+              first_sample: int, data_code_id: int = -1, prn: int = 0):
         a = abi.TrkStartArgs(code_id=code_id, data_code_id=data_code_id, acq_delay_samples=acq_delay_samples,
-                             acq_doppler_hz=acq_doppler_hz, acq_samplestamp_samples=acq_samplestamp, first_sample=first_sample)
+                             acq_doppler_hz=acq_doppler_hz, acq_samplestamp_samples=acq_samplestamp, first_sample=first_sample,
+                             prn=prn)
         check(self.ctx.lib.gnsship_trk_start(self.h, channel, ctypes.byref(a)), "gnsship_trk_start", self.ctx.h)
 
     def stop(self, channel: int):

@@ -52,6 +52,8 @@ class Satellite:
     secondary: str = None
     # line-of-sight dynamics: the Doppler ramps at this rate from doppler_hz at sample 0
     doppler_rate_hz_s: float = 0.0
+    # code periods per navigation bit when not the system default (BeiDou GEO D2: 2)
+    symbols_per_bit: int = None
 
     def __post_init__(self):
         if self.code is None:
@@ -107,7 +109,7 @@ def generate_if(fs: float, n_samples: int, sats: list, seed: int = 0, noise: boo
             data_sign = 1.0
             if s.bits:
                 pat = np.array([1.0 if b == "0" else -1.0 for b in s.bits])
-                per_bit = 1 if s.code_data is not None else 20
+                per_bit = s.symbols_per_bit or (1 if s.code_data is not None else 20)
                 data_sign = pat[np.mod(np.floor_divide(period, per_bit), len(pat))]
             if s.code_data is not None:  # Galileo E1 OS: (E1B − E1C)/√2 with sinBOC(1,1) subcarriers
                 c = (data_sign * s.code_data[np.mod(chip, s.code_len)].astype(np.float64) - c) / np.sqrt(2.0)

@@ -223,7 +223,8 @@ int gnsship_acq_destroy(gnsship_acq* a);
  * secondary-code synchronisation of states 2 and 4.  start_tracking (:643-883) and the state-1
  * pull-in (:1757-1788) run on the host in gnsship_trk_start.  States 2, 3 (extended coherent
  * integration, extend_correlation_symbols > 1) and 4, with the FLL branches (enable_fll_*) and
- * high_dyn (high-dynamics correlator fed by the smoothed NCO rates).  Not covered: BeiDou GEO.
+ * high_dyn (high-dynamics correlator fed by the smoothed NCO rates); BeiDou B1I GEO satellites by
+ * the start arguments' PRN.
  * ------------------------------------------------------------------------------------------- */
 #define GNSSHIP_SYS_GPS_L1CA 0 /* GPS L1 C/A: 3 taps, bit sync on the 160-symbol preamble */
 #define GNSSHIP_SYS_GAL_E1 1   /* Galileo E1 B/C: VEML 5 taps on the pilot + data prompt, CS25 secondary */
@@ -274,6 +275,8 @@ typedef struct gnsship_trk_start_args { /* Gnss_Synchro fields start_tracking re
     double acq_doppler_hz;
     uint64_t acq_samplestamp_samples;
     uint64_t first_sample; /* nitems_read when the block first runs after start (state-1 pull-in) */
+    int32_t prn;           /* Gnss_Synchro::PRN: BeiDou B1I PRN 1-5 and 59+ are GEO satellites (:765-781) */
+    int32_t reserved;      /* 0 */
 } gnsship_trk_start_args;
 
 typedef struct gnsship_trk_epoch { /* one general_work call of one channel (Gnss_Synchro subset) */

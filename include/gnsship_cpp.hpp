@@ -407,9 +407,10 @@ public:
         if (h_) gnsship_trk_destroy(h_);
     }
     // start_tracking for one channel: the local code(s) as the block generates them (d_tracking_code,
-    // d_data_code; code_len = samples per chip × chips) and the acquisition's Gnss_Synchro fields.
+    // d_data_code; code_len = samples per chip × chips) and the acquisition's Gnss_Synchro fields
+    // (prn selects the BeiDou GEO symbol synchronisation).
     bool start_tracking(int channel, const float* tracking_code, const float* data_code, int code_len, double acq_delay_samples,
-        double acq_doppler_hz, uint64_t acq_samplestamp_samples, uint64_t first_sample)
+        double acq_doppler_hz, uint64_t acq_samplestamp_samples, uint64_t first_sample, int prn = 0)
     {
         if (channel < 0 || channel >= channels_) return false;
         std::lock_guard<std::mutex> lk(dev_->mutex());
@@ -423,6 +424,7 @@ public:
         a.acq_doppler_hz = acq_doppler_hz;
         a.acq_samplestamp_samples = acq_samplestamp_samples;
         a.first_sample = first_sample;
+        a.prn = prn;
         return gnsship_trk_start(h_, channel, &a) == GNSSHIP_OK;
     }
     bool stop_tracking(int channel)

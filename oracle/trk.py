@@ -49,6 +49,12 @@ EPOCH_DTYPE = np.dtype([
 GPS_PREAMBLE_SYMBOLS = "1" * 20 + "0" * 60 + "1" * 20 + "0" * 20 + "1" * 40  # GPS_L1_CA.h:73 (10001011 × 20)
 E1C_SECONDARY = "0011100000001010110110010"                               # Galileo_E1.h:52
 B1I_NH = "00000100110101001110"                                           # Beidou_B1I.h:48
+B1I_GEO_PREAMBLE = "1111110000001100001100"                               # Beidou_B1I.h:49 (11100010010 × 2)
+
+
+def is_bds_geo(prn: int) -> bool:
+    """start_tracking's GEO test (dll_pll_veml_tracking.cc:766)."""
+    return (0 < prn < 6) or prn > 58
 
 SYSTEMS = {
     # system: chip rate, carrier, code period, code length, samples/chip, symbols/bit, veml, secondary, sec code, data sec
@@ -58,9 +64,11 @@ SYSTEMS = {
 }
 
 
-def conf(system: str, fs_in: float, vector_length: int, **kw) -> OrcTrkConf:
+def conf(system: str, fs_in: float, vector_length: int, prn: int = 0, **kw) -> OrcTrkConf:
     """Dll_Pll_Conf defaults (dll_pll_conf.h:33-80 + gnss_sdr_flags.cc:48-57) plus the signal
-    constants of `system`; keyword overrides for any field."""
+    constants of `system`; keyword overrides for any field.  `prn`: a BeiDou GEO PRN applies
+    start_tracking's GEO settings (:765-781) — D2 symbols (2 per bit), no NH code, the 22-symbol
+    preamble as the bit-synchronisation pattern, extend_correlation_symbols capped at 2."""
     rate, fc, period, L, spc, spb, veml, sec, sec_code, dsec = SYSTEMS[system]
     track_pilot = kw.pop("track_pilot", 1) if system == "GAL" else 0
     if system == "GAL" and not track_pilot:
@@ -79,6 +87,14 @@ def conf(system: str, fs_in: float, vector_length: int, **kw) -> OrcTrkConf:
                    high_dyn=0, smoother_length=10)
     for k, v in kw.items():
         setattr(c, k, v)
+    if system == "BDS" and is_bds_geo(prn):
+        c.symbols_per_bit = 2
+        c.secondary = 0
+        c.secondary_code = B1I_GEO_PREAMBLE.encode()
+        c.secondary_code_length = len(B1I_GEO_PREAMBLE)
+        c.data_secondary_code_length = 0
+        c.data_secondary_code = b""
+        c.extend_correlation_symbols = min(c.extend_correlation_symbols, 2)
     return c
 
 

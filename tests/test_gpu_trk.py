@@ -150,6 +150,31 @@ def test_high_dyn_loop_matches_oracle(ctx, system, fs, epochs, rate_hz_s, smooth
     trk.close()
 
 
+@pytest.mark.parametrize("ext", [1, 5])
+def test_bds_geo_matches_oracle(ctx, ext):
+    """BeiDou B1I GEO satellite (start args PRN 3; start_tracking :765-781): D2 preamble bit sync at
+    2 symbols per bit, no NH code, extend capped at 2 — next to a MEO channel (PRN 9) of the same
+    engine, which keeps the NH-code profile and the configured extend."""
+    fs, epochs = 4.092e6, 300
+    sat, k, x, stamp, first, delay, dop = S.sync("BDS", fs, epochs, prn=3, extend_correlation_symbols=ext)
+    meo, km, xm, _, _, delay_m, dop_m = S.sync("BDS", fs, epochs, prn=9, dop=-830.0, delay_chips=1500.6,
+                                                  extend_correlation_symbols=ext, seed=6)
+    c = dev_conf(km, "BDS")  # the engine's configuration: the MEO one (GEO settings come from the PRN)
+    trk = engine.DllPllVemlTracking(ctx, c, 2)
+    ctx.set_code(60, sat.code)
+    ctx.set_code(61, meo.code)
+    both = (x + xm).astype(np.complex64)
+    trk.start(0, 60, delay, dop, stamp, first, prn=3)
+    trk.start(1, 61, delay_m, dop_m, stamp, first, prn=9)
+    rec, rounds = trk.run(both, first, epochs)
+    ref = T.track(k, both, sat.code, delay, dop, stamp, first, epochs, buffer_first=first)
+    ref_m = T.track(km, both, meo.code, delay_m, dop_m, stamp, first, epochs, buffer_first=first)
+    assert ref["state"][-1] in (3, 4) and ref_m["state"][-1] in (3, 4)
+    compare(rec[:, 0], ref, f"geo x{ext}")
+    compare(rec[:, 1], ref_m, f"meo x{ext}")
+    trk.close()
+
+
 def test_high_dyn_smoother_length_bound(ctx):
     k = abi.TrkConf.defaults(abi.SYS_GPS_L1CA, 4e6, 4000, high_dyn=1, smoother_length=65)
     with pytest.raises(abi.GnssHipError):

@@ -183,3 +183,20 @@ def test_high_dyn_loop_follows_doppler_ramp(built, system, fs, epochs, rate):
     k0 = T.conf(system, fs, k.vector_length, pull_in_time_s=0, high_dyn=0)
     rec0 = T.track(k0, x, sat.code, delay, dop, stamp, first, epochs, data_code=sat.code_data, buffer_first=first)
     assert np.any(rec0["carrier_doppler_hz"] != rec["carrier_doppler_hz"])
+
+
+@pytest.mark.parametrize("ext", [1, 5])
+def test_bds_geo_d2_preamble_sync(built, ext):
+    """BeiDou GEO (start_tracking :765-781): 2 symbols per bit, no NH code, bit synchronisation on
+    the 22-symbol D2 preamble; extend_correlation_symbols capped at 2."""
+    sat, k, x, stamp, first, delay, dop = S.sync("BDS", 4.092e6, 300, prn=3, extend_correlation_symbols=ext)
+    assert k.symbols_per_bit == 2 and k.secondary == 0 and k.secondary_code_length == 22
+    assert k.extend_correlation_symbols == min(ext, 2)
+    rec = T.track(k, x, sat.code, delay, dop, stamp, first, 300, buffer_first=first)
+    st = rec["state"]
+    assert st[-1] in (3, 4) and np.sum(st == 2) < 80
+    if ext > 1:
+        assert np.sum(st == 3) >= 50
+    # valid symbols every 2 code periods in state 4 (one per D2 bit)
+    s4 = rec[(st == 4) | (st == 3)]
+    assert np.all(np.diff(np.nonzero(s4["flags"] & 1)[0]) == 2)

@@ -24,7 +24,9 @@ def pull_in(system, fs, cn0, dop, delay_chips, dop_err, delay_err_samples, epoch
 
 
 SYNC_PATTERNS = {"GPS": dict(bits="1000101100110"), "GAL": dict(secondary=T.E1C_SECONDARY, bits="0110"),
-                 "BDS": dict(secondary=T.B1I_NH, bits="0111")}
+                 "BDS": dict(secondary=T.B1I_NH, bits="0111"),
+                 # GEO D2: the 11-bit preamble 11100010010 at 2 code periods per bit, no NH code
+                 "BDS_GEO": dict(bits="111000100100110", symbols_per_bit=2)}
 
 
 def sync(system, fs, epochs, prn=9, dop=1210.0, delay_chips=100.3, seed=5, cn0=50.0, rate_hz_s=0.0, **conf_kw):
@@ -32,11 +34,12 @@ def sync(system, fs, epochs, prn=9, dop=1210.0, delay_chips=100.3, seed=5, cn0=5
     10001011 preamble, CS25 on the E1-C pilot, the B1I NH code), acquisition stamped one second
     before tracking starts so that pull_in_time_s = 0 ends the pull-in at once.  x[0] is absolute
     sample `first` = fs.  rate_hz_s: Doppler ramp (the acquisition reports the Doppler at `first`)."""
+    geo = system == "BDS" and T.is_bds_geo(prn)
     sat = signals.Satellite(prn=prn, doppler_hz=dop, code_delay_chips=delay_chips, cn0_dbhz=cn0, system=system, carrier_phase_rad=1.0,
-                            doppler_rate_hz_s=rate_hz_s, **SYNC_PATTERNS[system])
+                            doppler_rate_hz_s=rate_hz_s, **SYNC_PATTERNS["BDS_GEO" if geo else system])
     kw = dict(pull_in_time_s=0)
     kw.update(conf_kw)
-    k = T.conf(system, fs, int(round(fs * T.SYSTEMS[system][2])), **kw)
+    k = T.conf(system, fs, int(round(fs * T.SYSTEMS[system][2])), prn=prn, **kw)
     first = int(fs)
     x = signals.generate_if(fs, int(round(fs)) // 4 + k.vector_length * (epochs + 3), [sat], seed=seed, start=first)
     return sat, k, x, 0, first, acq_delay_for(sat, fs, system, 0, first) + 0.2, sat.doppler_hz + rate_hz_s + 15.0
