@@ -57,6 +57,8 @@ class AcqConf(ctypes.Structure):
         ("max_prns", ctypes.c_int32),
         ("consumed_samples", ctypes.c_int32),
         ("bit_transition_flag", ctypes.c_int32),
+        ("resampler_ratio", ctypes.c_float),
+        ("resampler_latency_samples", ctypes.c_uint32),
     ]
 
 
@@ -184,6 +186,12 @@ _SIGNATURES = {
     "gnsship_acq_run": ([_vp, _vp, _i, _i, _i, ctypes.POINTER(AcqResult), _f32p], _i),
     "gnsship_acq_num_bins": ([_vp, ctypes.POINTER(_i)], _i),
     "gnsship_acq_destroy": ([_vp], _i),
+    "gnsship_firdes_low_pass": ([ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double, _f32p, _i, ctypes.POINTER(_i)], _i),
+    "gnsship_acq_resampler_design": ([ctypes.c_int64, ctypes.c_double, ctypes.POINTER(_i), _f32p, _i, ctypes.POINTER(_i)], _i),
+    "gnsship_acq_resampler_create": ([_vp, _f32p, _i, _i, ctypes.c_int64, _vpp], _i),
+    "gnsship_acq_resampler_run": ([_vp, _vp, _i, _i, ctypes.c_int64, _f32p, _vpp, ctypes.POINTER(ctypes.c_int64)], _i),
+    "gnsship_acq_resampler_reset": ([_vp], _i),
+    "gnsship_acq_resampler_destroy": ([_vp], _i),
     "gnsship_trk_create": ([_vp, ctypes.POINTER(TrkConf), _i, _vpp], _i),
     "gnsship_trk_start": ([_vp, _i, ctypes.POINTER(TrkStartArgs)], _i),
     "gnsship_trk_stop": ([_vp, _i], _i),

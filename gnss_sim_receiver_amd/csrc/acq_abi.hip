@@ -368,7 +368,8 @@ extern "C" int gnsship_acq_run(gnsship_acq* a, const void* sig, int fmt, int sig
                          a->rowstat, keep_grid ? a->grid_dev : nullptr, ctx->stream));
     }
     HIP_TRY(ctx, launch_acq_decide(a->rowstat, n_prns, a->n_bins, rs.row_len, a->conf.doppler_max, a->conf.doppler_step, a->conf.doppler_center,
-                     a->dwell_count, a->conf.use_cfar, a->conf.samples_per_code, a->step2, a->res_dev, ctx->stream));
+                     a->dwell_count, a->conf.use_cfar, a->conf.samples_per_code, a->conf.resampler_ratio > 0.0f ? a->conf.resampler_ratio : 1.0f,
+                     a->conf.resampler_latency_samples, a->step2, a->res_dev, ctx->stream));
     HIP_TRY(ctx, hipMemcpyAsync(results, a->res_dev, sizeof(gnsship_acq_result) * n_prns, hipMemcpyDeviceToHost, ctx->stream));
     if (grid)
         HIP_TRY(ctx, hipMemcpyAsync(grid, a->grid_dev, sizeof(float) * static_cast<size_t>(n_prns) * a->n_bins * rs.row_len, hipMemcpyDeviceToHost,
@@ -376,4 +377,4 @@ extern "C" int gnsship_acq_run(gnsship_acq* a, const void* sig, int fmt, int sig
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     return GNSSHIP_OK;
 }
-static_assert(sizeof(gnsship_acq_conf) == 56, "gnsship_acq_conf layout (abi.AcqConf)");
+static_assert(sizeof(gnsship_acq_conf) == 64, "gnsship_acq_conf layout (abi.AcqConf)");

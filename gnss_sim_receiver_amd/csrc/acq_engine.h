@@ -71,6 +71,7 @@ hipError_t launch_acq_search_huge(const float2* XT, const float2* codesT, int pr
     const float2* twN, const float2* twM, float2* U, float* grid, int accumulate, TileStat* tiles, RowSpec rs, RowStat* rowstat,
     hipStream_t stream);
 hipError_t launch_acq_decide(const RowStat* rowstat, int n_prns, int n_bins, int N, int doppler_max, int doppler_step, int doppler_center,
-    int dwells, int use_cfar, float samples_per_code, Step2Spec step2, gnsship_acq_result* out, hipStream_t stream);
+    int dwells, int use_cfar, float samples_per_code, float resampler_ratio, uint32_t resampler_latency, Step2Spec step2, gnsship_acq_result* out,
+    hipStream_t stream);
 
 }  // namespace gnsship

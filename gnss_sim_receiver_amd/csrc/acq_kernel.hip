@@ -542,7 +542,8 @@ __global__ __launch_bounds__(kAcqThreads) void acq_search_big_kernel(const float
 // Step two of make_2_steps (step2.active): Doppler = (int)(center + (bin − floor(nb/2))·step2) in float
 // and the CFAR input power left at its step-one value (pcps_acquisition.cc:516-525).
 __global__ void acq_decide_kernel(const RowStat* __restrict__ rowstat, int n_prns, int n_bins, int N, int doppler_max, int doppler_step,
-    int doppler_center, int dwells, int use_cfar, float samples_per_code, Step2Spec step2, gnsship_acq_result* __restrict__ out)
+    int doppler_center, int dwells, int use_cfar, float samples_per_code, float resampler_ratio, uint32_t resampler_latency, Step2Spec step2,
+    gnsship_acq_result* __restrict__ out)
 {
     const int p = blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= n_prns) return;
@@ -576,7 +577,9 @@ __global__ void acq_decide_kernel(const RowStat* __restrict__ rowstat, int n_prn
         r.input_power = rs[bi].second;
         r.test_statistic = gmax / rs[bi].second;
     }
-    r.acq_delay_samples = static_cast<double>(fmodf(static_cast<float>(ti), samples_per_code));
+    // :686-687: the delay at the resampled rate scaled back to input samples, minus the FIR latency
+    r.acq_delay_samples = static_cast<double>(fmodf(static_cast<float>(ti), samples_per_code)) * static_cast<double>(resampler_ratio);
+    r.acq_delay_samples -= static_cast<double>(resampler_latency);
     out[p] = r;
 }
 
@@ -872,10 +875,11 @@ hipError_t launch_acq_search_big(const float2* XT, const float2* codesT, int n_p
 }
 
 hipError_t launch_acq_decide(const RowStat* rowstat, int n_prns, int n_bins, int N, int doppler_max, int doppler_step, int doppler_center,
-    int dwells, int use_cfar, float samples_per_code, Step2Spec step2, gnsship_acq_result* out, hipStream_t stream)
+    int dwells, int use_cfar, float samples_per_code, float resampler_ratio, uint32_t resampler_latency, Step2Spec step2, gnsship_acq_result* out,
+    hipStream_t stream)
 {
     hipLaunchKernelGGL(acq_decide_kernel, dim3((n_prns + 63) / 64), dim3(64), 0, stream, rowstat, n_prns, n_bins, N, doppler_max, doppler_step,
-        doppler_center, dwells, use_cfar, samples_per_code, step2, out);
+        doppler_center, dwells, use_cfar, samples_per_code, resampler_ratio, resampler_latency, step2, out);
     return hipGetLastError();
 }
 

@@ -261,7 +261,7 @@ class PcpsAcquisition:
     def __init__(self, ctx: Context, fs_in: int, fft_size: int, doppler_max: int, doppler_step: int, doppler_center: int = 0,
                  use_cfar: bool = True, samples_per_chip: int = None, samples_per_code: float = None, max_prns: int = 1,
                  max_dwells: int = 1, chip_rate: float = 1023000.0, ms_per_code: int = 1, consumed_samples: int = 0,
-                 bit_transition_flag: bool = False):
+                 bit_transition_flag: bool = False, resampler_ratio: float = 1.0, resampler_latency_samples: int = 0):
         self.ctx = ctx
         conf = abi.AcqConf()
         conf.fs_in = fs_in
@@ -278,6 +278,8 @@ class PcpsAcquisition:
         conf.max_prns = max_prns
         conf.consumed_samples = consumed_samples
         conf.bit_transition_flag = int(bit_transition_flag)
+        conf.resampler_ratio = resampler_ratio
+        conf.resampler_latency_samples = resampler_latency_samples
         self.conf = conf
         self.consumed = consumed_samples or fft_size
         self.code_len = fft_size // 2 if bit_transition_flag else self.consumed  # samples set_local_code reads
@@ -336,6 +338,69 @@ class PcpsAcquisition:
                 self.close()
         except Exception:
             pass
+
+
+def firdes_low_pass(lib, gain: float, fs: float, cutoff: float, transition: float) -> np.ndarray:
+    """gr::filter::firdes::low_pass (Hamming) as the library restates it."""
+    n = ctypes.c_int()
+    rc = lib.gnsship_firdes_low_pass(gain, fs, cutoff, transition, None, 0, ctypes.byref(n))
+    if rc != abi.OK:
+        raise abi.GnssHipError(rc, "gnsship_firdes_low_pass: bad arguments")
+    taps = np.zeros(n.value, np.float32)
+    check(lib.gnsship_firdes_low_pass(gain, fs, cutoff, transition, fptr(taps), len(taps), ctypes.byref(n)), "gnsship_firdes_low_pass")
+    return taps
+
+
+def acq_resampler_design(lib, fs_in: int, opt_acq_fs: float):
+    """gnss_flowgraph.cc:1070-1113: (decimation, taps); decimation 1 and no taps when not needed."""
+    d, n = ctypes.c_int(), ctypes.c_int()
+    check(lib.gnsship_acq_resampler_design(fs_in, opt_acq_fs, ctypes.byref(d), None, 0, ctypes.byref(n)), "gnsship_acq_resampler_design")
+    taps = np.zeros(n.value, np.float32)
+    if n.value:
+        check(lib.gnsship_acq_resampler_design(fs_in, opt_acq_fs, ctypes.byref(d), fptr(taps), len(taps), ctypes.byref(n)),
+              "gnsship_acq_resampler_design")
+    return d.value, taps
+
+
+class AcqResampler:
+    """The acquisition resampler FIR (fir_filter_ccf(decimation, taps)) over a sample stream."""
+
+    def __init__(self, ctx: Context, taps: np.ndarray, decimation: int, max_in_samples: int):
+        self.ctx = ctx
+        self.taps = np.ascontiguousarray(taps, np.float32)
+        self.decimation = decimation
+        h = ctypes.c_void_p()
+        check(ctx.lib.gnsship_acq_resampler_create(ctx.h, fptr(self.taps), len(self.taps), decimation, max_in_samples, ctypes.byref(h)),
+              "gnsship_acq_resampler_create", ctx.h)
+        self.h = h
+
+    @property
+    def latency(self) -> int:
+        return (len(self.taps) - 1) // 2
+
+    def run(self, x, fmt: int = None, on_device: bool = False, n_in: int = None):
+        """Filter a host array (or a device pointer with on_device=True and n_in): returns the
+        decimated complex64 samples (host arrays) or (device pointer, n_out)."""
+        dev = ctypes.c_void_p()
+        n_out = ctypes.c_int64()
+        if on_device:
+            check(self.ctx.lib.gnsship_acq_resampler_run(self.h, x, fmt, 1, n_in, None, ctypes.byref(dev), ctypes.byref(n_out)),
+                  "gnsship_acq_resampler_run", self.ctx.h)
+            return dev.value, n_out.value
+        fmt = sample_format(x) if fmt is None else fmt
+        n = len(x) if x.dtype == np.complex64 else len(x) // 2
+        out = np.zeros(n // self.decimation, np.complex64)
+        check(self.ctx.lib.gnsship_acq_resampler_run(self.h, x.ctypes.data, fmt, 0, n, fptr(out.view(np.float32)), ctypes.byref(dev),
+                                                      ctypes.byref(n_out)), "gnsship_acq_resampler_run", self.ctx.h)
+        return out
+
+    def reset(self):
+        check(self.ctx.lib.gnsship_acq_resampler_reset(self.h), "gnsship_acq_resampler_reset", self.ctx.h)
+
+    def close(self):
+        if self.h:
+            self.ctx.lib.gnsship_acq_resampler_destroy(self.h)
+            self.h = None
 
 
 class DllPllVemlTracking:

@@ -181,6 +181,10 @@ typedef struct gnsship_acq_conf {
                                    fft_size = 2 x consumed, :84-91); 0 = fft_size              */
     int32_t bit_transition_flag; /* code in the second half after N/2 zeros, grid rows = the
                                    second half of |IFFT|^2 (:187-192, :663-664)                 */
+    float resampler_ratio;       /* acquisition resampler decimation (Acq_Conf::resampler_ratio,
+                                   acq_conf.cc:91-107); 0 or 1 = no resampler. Acq_delay_samples
+                                   is scaled by it and reduced by the latency (:686-687)        */
+    uint32_t resampler_latency_samples; /* (taps - 1) / 2 of the resampler FIR (gnss_flowgraph.cc:1113) */
 } gnsship_acq_conf;
 
 /* What acquisition_core leaves in Gnss_Synchro + block members (pcps_acquisition.cc:683-696). */
@@ -191,7 +195,7 @@ typedef struct gnsship_acq_result {
     float peak;                  /* grid maximum (or first peak)                             */
     float input_power;           /* d_input_power (CFAR) / second peak (first_vs_second)     */
     float test_statistic;        /* d_test_statistics                                         */
-    double acq_delay_samples;    /* fmod(indext, samples_per_code)                            */
+    double acq_delay_samples;    /* fmod(indext, samples_per_code)·resampler_ratio − latency   */
 } gnsship_acq_result;
 
 int gnsship_acq_create(gnsship_ctx* ctx, const gnsship_acq_conf* conf, gnsship_acq** out);
@@ -213,6 +217,32 @@ int gnsship_acq_run(gnsship_acq* a, const void* sig, int fmt, int sig_on_device,
     gnsship_acq_result* results, float* grid);
 int gnsship_acq_num_bins(gnsship_acq* a, int* n_bins);
 int gnsship_acq_destroy(gnsship_acq* a);
+
+/* Acquisition resampler (GNSS-SDR.use_acquisition_resampler; gnss_flowgraph.cc:1028-1113): the
+ * decimating low-pass FIR in front of a channel's acquisition, and the Acq_Conf side
+ * (ConfigureAutomaticResampler, acq_conf.cc:91-107).  Taps are GNU Radio's
+ * firdes::low_pass(gain, fs, cutoff, transition) with the default Hamming window (GNU Radio is not
+ * in the reference tree; restated from its published algorithm). */
+typedef struct gnsship_acq_resampler gnsship_acq_resampler;
+/* taps == NULL: only *n_taps.  E_INVAL for the arguments firdes rejects (sanity_check_1f). */
+int gnsship_firdes_low_pass(double gain, double sampling_freq, double cutoff_freq, double transition_width, float* taps, int taps_cap,
+    int* n_taps);
+/* The flowgraph's design for a signal whose optimum acquisition rate is opt_acq_fs (e.g.
+ * GPS_L1_CA_OPT_ACQ_FS_SPS = 2e6): decimation = floor(fs/opt) lowered until it divides fs, taps =
+ * firdes::low_pass(1, fs, fs_dec/2.1, fs_dec/2).  *decimation = 1 and *n_taps = 0 when no resampler
+ * is used (opt >= fs or decimation 1).  resampler_latency_samples = (n_taps - 1) / 2. */
+int gnsship_acq_resampler_design(int64_t fs_in, double opt_acq_fs, int* decimation, float* taps, int taps_cap, int* n_taps);
+/* fir_filter_ccf(decimation, taps) over a sample stream: ntaps - 1 samples of history carried
+ * between runs (zeros after create / reset). */
+int gnsship_acq_resampler_create(gnsship_ctx* ctx, const float* taps, int n_taps, int decimation, int64_t max_in_samples,
+    gnsship_acq_resampler** out);
+/* Filter n_in samples (a multiple of the decimation) in `fmt` (converted in the loads, no scaling):
+ * n_in / decimation CF32 outputs, left in device memory (*dev_out, valid until the next run) and,
+ * when host_out != NULL, copied there before returning.  Asynchronous otherwise (context stream). */
+int gnsship_acq_resampler_run(gnsship_acq_resampler* r, const void* in, int fmt, int in_on_device, int64_t n_in, float* host_out,
+    void** dev_out, int64_t* n_out);
+int gnsship_acq_resampler_reset(gnsship_acq_resampler* r);
+int gnsship_acq_resampler_destroy(gnsship_acq_resampler* r);
 
 /* ---------------------------------------------------------------------------------------------
  * Closed-loop tracking engine: the per-epoch DLL/PLL of dll_pll_veml_tracking

@@ -149,6 +149,11 @@ struct Acq_Conf {
     float doppler_step2{125.0};
     uint32_t num_doppler_bins_step2{4U};
     float pfa2{0.0};
+    // acquisition resampler (GNSS-SDR.use_acquisition_resampler): resampled_fs = fs_in when unused
+    bool use_automatic_resampler{false};
+    int64_t resampled_fs{0LL};
+    float resampler_ratio{1.0};
+    uint32_t resampler_latency_samples{0U};
     // derived
     float samples_per_ms{0.0};
     float samples_per_code{0.0};
@@ -158,10 +163,67 @@ struct Acq_Conf {
         if (pfa < 0.0F || pfa > 1.0F) pfa = 0.0F;       // acq_conf.cc:63-67
         if (pfa <= 0.0F) use_CFAR_algorithm_flag = false;  // :75-79
         if (pfa2 <= 0.0F || pfa2 > 1.0F) pfa2 = pfa;
-        samples_per_ms = static_cast<float>(fs_in) * 0.001F;
-        samples_per_chip = static_cast<unsigned int>(std::ceil(static_cast<float>(fs_in) / static_cast<float>(chips_per_second)));
+        if (resampled_fs == 0) resampled_fs = fs_in;       // SetFromConfiguration (:41)
+        samples_per_ms = static_cast<float>(resampled_fs) * 0.001F;
+        samples_per_chip = static_cast<unsigned int>(std::ceil(static_cast<float>(resampled_fs) / static_cast<float>(chips_per_second)));
         samples_per_code = samples_per_ms * static_cast<float>(ms_per_code);
     }
+    // ConfigureAutomaticResampler (acq_conf.cc:91-107), called by the adapters with the signal's
+    // optimum acquisition rate (GPS_L1_CA_OPT_ACQ_FS_SPS = 2e6, ...)
+    void ConfigureAutomaticResampler(double opt_freq)
+    {
+        if (!use_automatic_resampler) return;
+        if (static_cast<double>(fs_in) > opt_freq) {
+            uint32_t decimation = static_cast<uint32_t>(static_cast<double>(fs_in) / opt_freq);
+            while (fs_in % decimation > 0) decimation--;
+            resampler_ratio = static_cast<float>(decimation);
+            resampled_fs = fs_in / static_cast<int>(resampler_ratio);
+        }
+        SetDerivedParams();
+    }
+};
+
+// The acquisition resampler the flowgraph puts in front of a channel's acquisition
+// (gnss_flowgraph.cc:1028-1113): decimating low-pass FIR designed for the signal's optimum
+// acquisition rate.  Feed it the IF stream; its output is the acquisition's input at resampled_fs;
+// latency() is what the flowgraph passes to set_resampler_latency.
+class Acq_Resampler_Hip {
+public:
+    Acq_Resampler_Hip(int64_t fs_in, double opt_acq_fs, int64_t max_in_samples, int device = 0) : dev_(Device::get(device))
+    {
+        int n = 0;
+        if (gnsship_acq_resampler_design(fs_in, opt_acq_fs, &decimation_, nullptr, 0, &n) != GNSSHIP_OK)
+            throw std::invalid_argument("gnsship_acq_resampler_design");
+        taps_.resize(static_cast<size_t>(n));
+        if (n > 0) {
+            if (gnsship_acq_resampler_design(fs_in, opt_acq_fs, &decimation_, taps_.data(), n, &n) != GNSSHIP_OK)
+                throw std::invalid_argument("gnsship_acq_resampler_design");
+            std::lock_guard<std::mutex> lk(dev_->mutex());
+            if (gnsship_acq_resampler_create(dev_->ctx(), taps_.data(), n, decimation_, max_in_samples, &h_) != GNSSHIP_OK)
+                throw std::invalid_argument(std::string("gnsship_acq_resampler_create: ") + gnsship_last_error(dev_->ctx()));
+        }
+    }
+    ~Acq_Resampler_Hip()
+    {
+        if (h_) gnsship_acq_resampler_destroy(h_);
+    }
+    bool enabled() const { return h_ != nullptr; }  // false: "input sampling frequency is too low"
+    int decimation() const { return decimation_; }
+    uint32_t latency() const { return taps_.empty() ? 0U : static_cast<uint32_t>((taps_.size() - 1) / 2); }
+    const std::vector<float>& taps() const { return taps_; }
+    // n_in gr_complex samples (a multiple of decimation()) -> n_in / decimation() into out
+    bool work(const std::complex<float>* in, int64_t n_in, std::complex<float>* out)
+    {
+        if (!h_) return false;
+        std::lock_guard<std::mutex> lk(dev_->mutex());
+        return gnsship_acq_resampler_run(h_, in, GNSSHIP_FMT_CF32, 0, n_in, reinterpret_cast<float*>(out), nullptr, nullptr) == GNSSHIP_OK;
+    }
+
+private:
+    std::shared_ptr<Device> dev_;
+    gnsship_acq_resampler* h_ = nullptr;
+    int decimation_ = 1;
+    std::vector<float> taps_;
 };
 
 // What acquisition_core writes into Gnss_Synchro (gnss_synchro.h:52-55; pcps_acquisition.cc:683-696).
@@ -223,7 +285,7 @@ public:
         consumed_ = static_cast<int>(conf_.sampled_ms * conf_.samples_per_ms * (conf_.bit_transition_flag ? 2.0 : 1.0));
         fft_size_ = conf_.sampled_ms == conf_.ms_per_code ? consumed_ : 2 * consumed_;
         gnsship_acq_conf c{};
-        c.fs_in = conf_.fs_in;
+        c.fs_in = conf_.resampled_fs;  // the wipeoff grid runs at the resampled rate (:237)
         c.fft_size = fft_size_;
         c.consumed_samples = consumed_;
         c.bit_transition_flag = conf_.bit_transition_flag ? 1 : 0;
@@ -234,6 +296,7 @@ public:
         c.use_cfar = conf_.use_CFAR_algorithm_flag ? 1 : 0;
         c.samples_per_chip = static_cast<int32_t>(conf_.samples_per_chip);
         c.samples_per_code = conf_.samples_per_code;
+        c.resampler_ratio = conf_.resampler_ratio;
         c.max_prns = 1;
         std::lock_guard<std::mutex> lk(dev_->mutex());
         if (gnsship_acq_create(dev_->ctx(), &c, &h_) != GNSSHIP_OK)
@@ -245,6 +308,7 @@ public:
     }
     int fft_size() const { return fft_size_; }
     void set_threshold(float threshold) { threshold_ = threshold; }
+    void set_resampler_latency(uint32_t latency_samples) { resampler_latency_ = latency_samples; }  // :168-172
     void set_doppler_max(uint32_t doppler_max) { conf_.doppler_max = static_cast<int32_t>(doppler_max); }
     void set_doppler_step(uint32_t doppler_step) { doppler_step_ = doppler_step; }
     void set_doppler_center(int32_t doppler_center) { doppler_center_ = doppler_center; }
@@ -289,9 +353,9 @@ public:
             std::lock_guard<std::mutex> lk(dev_->mutex());
             if (gnsship_acq_run(h_, in, GNSSHIP_FMT_CF32, 0, 1, &r, nullptr) != GNSSHIP_OK) return false;
         }
-        out.Acq_delay_samples = r.acq_delay_samples;
+        out.Acq_delay_samples = r.acq_delay_samples - static_cast<double>(resampler_latency_);  // :686-687
         out.Acq_doppler_hz = static_cast<double>(r.doppler_hz);
-        out.Acq_samplestamp_samples = samp_count;
+        out.Acq_samplestamp_samples = static_cast<uint64_t>(std::rint(static_cast<double>(samp_count) * conf_.resampler_ratio));  // :689
         out.Acq_doppler_step = step_two_ ? static_cast<uint32_t>(conf_.doppler_step2) : out.Acq_doppler_step;
         out.test_statistics = r.test_statistic;
         if (!step_two_) last_input_power_ = r.input_power;
@@ -328,6 +392,7 @@ private:
     float threshold_ = 0.0F;
     uint32_t doppler_step_ = 0;
     int32_t doppler_center_ = 0;
+    uint32_t resampler_latency_ = 0;
 };
 
 // Mirror of Dll_Pll_Conf (src/algorithms/tracking/libs/dll_pll_conf.h:33-80): same field names and

@@ -695,3 +695,62 @@ void orc_cf32_magnitude_squared(float* out, const float* a, uint32_t n)
 }
 
 int orc_abi_version(void) { return 1; }
+
+/* ---- acquisition resampler (gnss_flowgraph.cc:1070-1113) ------------------------------------
+ * GNU Radio (absent here, version unpinned) restated from its published algorithm:
+ * gr::filter::firdes::low_pass(gain, fs, cutoff, transition) with the default Hamming window —
+ * compute_ntaps: (int)(53 · fs / (22 · transition)), forced odd; window w[n] = 0.54 − 0.46·cosf(2πn/M)
+ * (fft::window::coswindow, M = ntaps − 1, float); windowed sinc h[n+M'] = sin(n·ω)/(nπ)·w (ω = 2π·
+ * cutoff/fs, centre ω/π·w); DC gain normalised in double.  Returns ntaps (taps == NULL: count). */
+int orc_firdes_low_pass(double gain, double fs, double cutoff, double transition, float* taps)
+{
+    int ntaps = (int)(53.0 * fs / (22.0 * transition));
+    if (!(ntaps & 1)) ntaps += 1;
+    if (!taps) return ntaps;
+    const int half = (ntaps - 1) / 2;
+    const float Mw = (float)(ntaps - 1);
+    const double omega = 2.0 * M_PI * cutoff / fs;
+    for (int i = 0; i < ntaps; i++) {
+        const float w = 0.54F - 0.46F * cosf((float)((2.0 * M_PI * (double)i) / (double)Mw));
+        const int n = i - half;
+        taps[i] = (n == 0) ? (float)(omega / M_PI * (double)w) : (float)(sin((double)n * omega) / ((double)n * M_PI) * (double)w);
+    }
+    double dc = (double)taps[half];
+    for (int n = 1; n <= half; n++) dc += (double)(2.0F * taps[half + n]);
+    const double g = gain / dc;
+    for (int i = 0; i < ntaps; i++) taps[i] = (float)((double)taps[i] * g);
+    return ntaps;
+}
+
+/* gr::filter::fir_filter_ccf(decimation, taps) over CF32 input with ntaps − 1 history samples
+ * (hist[0..ntaps−2], oldest first; updated in place): out[k] = volk_32fc_32f_dot_prod_32fc_generic
+ * of x_ext[k·D .. k·D + ntaps − 1] with the reversed taps (serial float sums).  n_in % D == 0. */
+void orc_fir_decimate(const float* in, int64_t n_in, float* hist, const float* taps, int ntaps, int decim, float* out)
+{
+    const int nh = ntaps - 1;
+    const int64_t n_out = n_in / decim;
+    for (int64_t k = 0; k < n_out; k++) {
+        float re = 0.0F, im = 0.0F;
+        for (int t = 0; t < ntaps; t++) {
+            const int64_t g = k * decim + t - nh;
+            const float* x = g < 0 ? &hist[2 * (nh + g)] : &in[2 * g];
+            const float h = taps[ntaps - 1 - t];
+            re += x[0] * h;
+            im += x[1] * h;
+        }
+        out[2 * k] = re;
+        out[2 * k + 1] = im;
+    }
+    /* history: the last nh samples of (hist ‖ in) */
+    if (nh > 0) {
+        float* tmp = (float*)malloc(sizeof(float) * 2 * (size_t)nh);
+        for (int i = 0; i < nh; i++) {
+            const int64_t g = n_in - nh + i;
+            const float* x = g < 0 ? &hist[2 * (nh + g)] : &in[2 * g];
+            tmp[2 * i] = x[0];
+            tmp[2 * i + 1] = x[1];
+        }
+        memcpy(hist, tmp, sizeof(float) * 2 * (size_t)nh);
+        free(tmp);
+    }
+}

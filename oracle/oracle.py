@@ -113,6 +113,9 @@ def lib(fast: bool = False) -> ctypes.CDLL:
         ctypes.c_float, ctypes.POINTER(AcqStat)]
     L.orc_cf32_multiply.argtypes = [_f32p, _f32p, _f32p, ctypes.c_uint32]
     L.orc_cf32_magnitude_squared.argtypes = [_f32p, _f32p, ctypes.c_uint32]
+    L.orc_firdes_low_pass.argtypes = [ctypes.c_double] * 4 + [_f32p]
+    L.orc_firdes_low_pass.restype = ctypes.c_int
+    L.orc_fir_decimate.argtypes = [_f32p, ctypes.c_int64, _f32p, _f32p, ctypes.c_int, ctypes.c_int, _f32p]
     _LIBS[name] = L
     return L
 
@@ -314,3 +317,42 @@ def pcps_acquisition_core_ex(sig, code, fs, fft_size, doppler_max, doppler_step,
             res.input_power = float(np.float32(ip))
             res.test_statistic = float(np.float32(np.float32(res.peak) / np.float32(ip)))
     return res, rows
+
+
+def firdes_low_pass(gain: float, fs: float, cutoff: float, transition: float) -> np.ndarray:
+    """gr::filter::firdes::low_pass with the Hamming window (oracle/gnss_oracle.c restatement)."""
+    L = lib()
+    n = L.orc_firdes_low_pass(gain, fs, cutoff, transition, None)
+    taps = np.zeros(n, np.float32)
+    L.orc_firdes_low_pass(gain, fs, cutoff, transition, _ptr(taps))
+    return taps
+
+
+def acq_resampler_design(fs: int, opt_acq_fs: float):
+    """gnss_flowgraph.cc:1070-1088: decimation lowered until it divides fs; firdes taps."""
+    if opt_acq_fs >= fs:
+        return 1, np.zeros(0, np.float32)
+    d = int(np.floor(fs / opt_acq_fs))
+    while d > 1 and fs % d:
+        d -= 1
+    if d <= 1:
+        return 1, np.zeros(0, np.float32)
+    fdec = fs / d
+    return d, firdes_low_pass(1.0, float(fs), fdec / 2.1, fdec / 2.0)
+
+
+class FirDecimator:
+    """fir_filter_ccf(decimation, taps) over a CF32 stream (history carried between calls)."""
+
+    def __init__(self, taps: np.ndarray, decimation: int):
+        self.taps = np.ascontiguousarray(taps, np.float32)
+        self.d = decimation
+        self.hist = np.zeros(2 * max(len(taps) - 1, 1), np.float32)
+
+    def __call__(self, x: np.ndarray) -> np.ndarray:
+        x = np.ascontiguousarray(x, np.complex64)
+        assert len(x) % self.d == 0
+        out = np.zeros(len(x) // self.d, np.complex64)
+        lib().orc_fir_decimate(_ptr(x.view(np.float32)), len(x), _ptr(self.hist), _ptr(self.taps), len(self.taps), self.d,
+                               _ptr(out.view(np.float32)))
+        return out

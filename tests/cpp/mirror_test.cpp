@@ -189,6 +189,58 @@ static int trk_test()
     return (bad == 0 && std::fabs(dop - fd) < 5.0 && trk.state(1) == 2) ? 0 : 1;
 }
 
+// Acquisition behind the acquisition resampler: 20.48 Msps IF, Acq_Conf::ConfigureAutomaticResampler(2e6)
+// (decimation 10, resampled_fs 2.048 Msps, fft 2048) and Acq_Resampler_Hip in front; PRN 12 at
+// fD = 1250 Hz, code start at input sample 10000.  The second 1-ms dwell (warm filter) is acquired.
+static int acq_resampler_test()
+{
+    const int64_t fs = 20480000;
+    gnsship::Acq_Conf conf;
+    conf.fs_in = fs;
+    conf.doppler_max = 5000;
+    conf.doppler_step = 250.0F;
+    conf.pfa = 0.01F;
+    conf.use_automatic_resampler = true;
+    conf.ConfigureAutomaticResampler(2000000.0);
+    gnsship::Acq_Resampler_Hip rs(fs, 2000000.0, 2 * fs / 1000);
+    if (!rs.enabled() || rs.decimation() != 10 || conf.resampler_ratio != 10.0F || conf.resampled_fs != 2048000) {
+        std::printf("resampler design mismatch: decimation %d ratio %.1f resampled_fs %lld\n", rs.decimation(), conf.resampler_ratio,
+            static_cast<long long>(conf.resampled_fs));
+        return 1;
+    }
+    gnsship::Pcps_Acquisition_Hip acq(conf);
+    acq.set_resampler_latency(rs.latency());
+    const int n = acq.fft_size();
+    std::vector<float> code(2 * n);
+    orc_gps_l1_ca_code_gen_complex_sampled(code.data(), 12, 2048000, 0);
+    acq.set_local_code(reinterpret_cast<const std::complex<float>*>(code.data()));
+    acq.init();
+    const int n_in = static_cast<int>(2 * fs / 1000);
+    std::mt19937 gen(11);
+    std::normal_distribution<double> g(0.0, 1.0);
+    std::vector<std::complex<float>> sig(n_in), dec(n_in / 10);
+    const double amp = std::sqrt(2 * std::pow(10.0, 4.8) / static_cast<double>(fs));
+    float chips[1023];
+    orc_gps_l1_ca_code_gen_float(chips, 12, 0);
+    for (int i = 0; i < n_in; i++) {
+        const double t = i / static_cast<double>(fs);
+        const long c = static_cast<long>(std::floor((i - 10000) / static_cast<double>(fs) * 1023000.0 * (1 + 1250.0 / 1575.42e6)));
+        const double cv = chips[((c % 1023) + 1023) % 1023];
+        sig[i] = std::complex<float>(amp * cv * std::cos(2 * M_PI * 1250.0 * t) + g(gen), amp * cv * std::sin(2 * M_PI * 1250.0 * t) + g(gen));
+    }
+    if (!rs.work(sig.data(), n_in, dec.data())) return 1;
+    gnsship::Acq_Outcome out;
+    if (!acq.acquisition_core(dec.data() + n, static_cast<uint64_t>(n), out)) return 1;
+    const double period = static_cast<double>(fs) / 1000.0;
+    double err = std::fmod(out.Acq_delay_samples - 10000.0 + 1.5 * period, period) - 0.5 * period;
+    std::printf("acq resampled: delay %.1f (truth 10000, err %.1f) doppler %.1f stamp %llu stat %.2f thr %.2f positive %d latency %u\n",
+        out.Acq_delay_samples, err, out.Acq_doppler_hz, static_cast<unsigned long long>(out.Acq_samplestamp_samples), out.test_statistics,
+        acq.threshold(), out.positive ? 1 : 0, rs.latency());
+    const bool ok = out.positive && std::fabs(err) <= 20.0 && std::fabs(out.Acq_doppler_hz - 1250.0) <= 250.0 &&
+                    out.Acq_samplestamp_samples == static_cast<uint64_t>(10 * n);
+    return ok ? 0 : 1;
+}
+
 int main(int argc, char** argv)
 {
     const char* mode = argc > 1 ? argv[1] : "corr";
@@ -200,6 +252,7 @@ int main(int argc, char** argv)
         return 0;
     }
     if (!std::strcmp(mode, "acq")) return acq_test();
+    if (!std::strcmp(mode, "acqrs")) return acq_resampler_test();
     if (!std::strcmp(mode, "trk")) return trk_test();
     return corr_test();
 }

@@ -57,4 +57,4 @@ def test_null_arguments_are_rejected_without_device(built):
 def test_job_layout_matches_header(built):
     assert abi.JOB_DTYPE.itemsize == 80
     assert ctypes.sizeof(abi.AcqResult) == 32
-    assert ctypes.sizeof(abi.AcqConf) == 56
+    assert ctypes.sizeof(abi.AcqConf) == 64

@@ -41,6 +41,15 @@ def test_pcps_acquisition_mirror(mirror_bin):
 
 
 @pytest.mark.gpu
+def test_acquisition_resampler_mirror(mirror_bin):
+    """Acq_Conf::ConfigureAutomaticResampler + Acq_Resampler_Hip + Pcps_Acquisition_Hip (resampled rate,
+    set_resampler_latency, samplestamp × ratio)."""
+    r = subprocess.run([mirror_bin, "acqrs"], capture_output=True, text=True, timeout=300)
+    print(r.stdout)
+    assert r.returncode == 0, r.stdout + r.stderr
+
+
+@pytest.mark.gpu
 def test_dll_pll_veml_tracking_mirror(mirror_bin):
     r = subprocess.run([mirror_bin, "trk"], capture_output=True, text=True, timeout=300)
     print(r.stdout)
