@@ -131,6 +131,17 @@ TRK_EPOCH_DTYPE = np.dtype([
 ])
 assert TRK_EPOCH_DTYPE.itemsize == 96
 
+# gnsship_trk_dump_record = the record dll_pll_veml_tracking::log_data writes (:1376-1466), packed
+TRK_DUMP_DTYPE = np.dtype([
+    ("abs_VE", "<f4"), ("abs_E", "<f4"), ("abs_P", "<f4"), ("abs_L", "<f4"), ("abs_VL", "<f4"), ("prompt_I", "<f4"), ("prompt_Q", "<f4"),
+    ("PRN_start_sample_count", "<u8"), ("acc_carrier_phase_rad", "<f4"), ("carrier_doppler_hz", "<f4"), ("carrier_doppler_rate_hz", "<f4"),
+    ("code_freq_chips", "<f4"), ("code_freq_rate_chips", "<f4"), ("carr_error_hz", "<f4"), ("carr_error_filt_hz", "<f4"),
+    ("code_error_chips", "<f4"), ("code_error_filt_chips", "<f4"), ("CN0_SNV_dB_Hz", "<f4"), ("carrier_lock_test", "<f4"),
+    ("aux1", "<f4"), ("aux2", "<f8"), ("PRN", "<u4"),
+])
+assert TRK_DUMP_DTYPE.itemsize == 96
+TRK_FLAG_DUMP = 16
+
 
 class GnssHipError(RuntimeError):
     def __init__(self, code: int, what: str):
@@ -196,6 +207,7 @@ _SIGNATURES = {
     "gnsship_trk_start": ([_vp, _i, ctypes.POINTER(TrkStartArgs)], _i),
     "gnsship_trk_stop": ([_vp, _i], _i),
     "gnsship_trk_run": ([_vp, _vp, _i, _i, ctypes.c_uint64, ctypes.c_int64, _i, _vp, ctypes.POINTER(_i)], _i),
+    "gnsship_trk_run_dump": ([_vp, _vp, _i, _i, ctypes.c_uint64, ctypes.c_int64, _i, _vp, _vp, ctypes.POINTER(_i)], _i),
     "gnsship_trk_channel_state": ([_vp, _i, ctypes.POINTER(_i), ctypes.POINTER(ctypes.c_uint64)], _i),
     "gnsship_trk_destroy": ([_vp], _i),
 }

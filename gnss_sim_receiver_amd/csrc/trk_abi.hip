@@ -25,6 +25,9 @@ int chunks_per_item_setting();
 
 using namespace gnsship;
 static_assert(sizeof(gnsship_trk_epoch) == 96, "gnsship_trk_epoch layout");
+static_assert(sizeof(gnsship_trk_dump_record) == 96 && offsetof(gnsship_trk_dump_record, PRN_start_sample_count) == 28 &&
+                  offsetof(gnsship_trk_dump_record, aux2) == 84 && offsetof(gnsship_trk_dump_record, PRN) == 92,
+    "gnsship_trk_dump_record = the log_data file record");
 
 #define HIP_TRY(ctx, expr)                                       \
     do {                                                         \
@@ -55,6 +58,8 @@ struct gnsship_trk {
     float* out_dev = nullptr;
     gnsship_trk_epoch* rec_dev = nullptr;
     size_t rec_cap = 0;
+    gnsship_trk_dump_record* dump_dev = nullptr;
+    size_t dump_cap = 0;
     int* ran_dev = nullptr;
     size_t ran_cap = 0;
     void* stage_dev = nullptr;
@@ -279,7 +284,7 @@ hipError_t upload_hd_code(gnsship_trk* t, int job, const CodeDesc& cd)
 void release(gnsship_trk* t)
 {
     void* ptrs[] = {t->params_dev, t->chans_dev, t->jobs_dev, t->chunks_dev, t->items_dev, t->anchors_dev, t->partials_dev, t->out_dev, t->rec_dev,
-        t->ran_dev, t->stage_dev, t->hist_dev};
+        t->ran_dev, t->stage_dev, t->hist_dev, t->dump_dev};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     hd_plan_free(t->hd);
@@ -399,6 +404,7 @@ extern "C" int gnsship_trk_start(gnsship_trk* t, int channel, const gnsship_trk_
     std::memset(&c, 0, sizeof(c));
     const gnsship_trk_conf& k = p.conf;
     c.code_id = a->code_id;
+    c.prn = a->prn > 0 ? static_cast<uint32_t>(a->prn) : 0u;
     // GEO satellites use the D2 symbol-sync profile (start_tracking :765-781)
     c.geo = (p.conf.system == GNSSHIP_SYS_BDS_B1I && ((a->prn > 0 && a->prn < 6) || a->prn > 58)) ? 1 : 0;
     c.data_code_id = p.track_pilot ? a->data_code_id : a->code_id;
@@ -487,6 +493,12 @@ extern "C" int gnsship_trk_channel_state(gnsship_trk* t, int channel, int* state
 extern "C" int gnsship_trk_run(gnsship_trk* t, const void* sig, int fmt, int sig_on_device, uint64_t buffer_first_sample, int64_t n_buffer_samples,
     int max_rounds, gnsship_trk_epoch* out, int* rounds_done)
 {
+    return gnsship_trk_run_dump(t, sig, fmt, sig_on_device, buffer_first_sample, n_buffer_samples, max_rounds, out, nullptr, rounds_done);
+}
+
+extern "C" int gnsship_trk_run_dump(gnsship_trk* t, const void* sig, int fmt, int sig_on_device, uint64_t buffer_first_sample,
+    int64_t n_buffer_samples, int max_rounds, gnsship_trk_epoch* out, gnsship_trk_dump_record* dump, int* rounds_done)
+{
     if (!t) return GNSSHIP_E_INVAL;
     gnsship_ctx* ctx = t->ctx;
     if (!sig || n_buffer_samples < 0 || max_rounds < 0 || fmt_bytes(fmt) == 0) return fail(ctx, GNSSHIP_E_INVAL, "gnsship_trk_run: bad arguments");
@@ -525,6 +537,12 @@ extern "C" int gnsship_trk_run(gnsship_trk* t, const void* sig, int fmt, int sig
         src = t->stage_dev;
     }
     const size_t nrec = static_cast<size_t>(max_rounds) * t->max_channels;
+    if (dump && t->dump_cap < nrec) {
+        if (t->dump_dev) HIP_TRY(ctx, hipFree(t->dump_dev));
+        t->dump_dev = nullptr;
+        HIP_TRY(ctx, hipMalloc(&t->dump_dev, sizeof(gnsship_trk_dump_record) * nrec));
+        t->dump_cap = nrec;
+    }
     if (out && t->rec_cap < nrec) {
         if (t->rec_dev) HIP_TRY(ctx, hipFree(t->rec_dev));
         t->rec_dev = nullptr;
@@ -542,8 +560,9 @@ extern "C" int gnsship_trk_run(gnsship_trk* t, const void* sig, int fmt, int sig
     for (int r = 0; r <= max_rounds; r++) {
         const int consume = r > 0 ? 1 : 0, emit = r < max_rounds ? 1 : 0;
         gnsship_trk_epoch* rec = (out && r > 0) ? t->rec_dev + static_cast<size_t>(r - 1) * nc : nullptr;
+        gnsship_trk_dump_record* drec = (dump && r > 0) ? t->dump_dev + static_cast<size_t>(r - 1) * nc : nullptr;
         hipError_t e = launch_trk_step(t->params_dev, t->chans_dev, nc, t->jobs_dev, t->chunks_dev, t->out_dev, buffer_first_sample, n_buffer_samples,
-            consume, emit, rec, t->ran_dev + r, t->hist_dev, t->high_dyn ? t->hd.jobs_dev : nullptr, t->high_dyn ? t->hd.chunks_dev : nullptr,
+            consume, emit, rec, drec, t->ran_dev + r, t->hist_dev, t->high_dyn ? t->hd.jobs_dev : nullptr, t->high_dyn ? t->hd.chunks_dev : nullptr,
             ctx->stream);
         if (e != hipSuccess) return hip_fail(ctx, e, "launch_trk_step");
         if (!emit) break;
@@ -560,6 +579,7 @@ extern "C" int gnsship_trk_run(gnsship_trk* t, const void* sig, int fmt, int sig
     std::vector<int> ran(max_rounds + 1);
     HIP_TRY(ctx, hipMemcpyAsync(ran.data(), t->ran_dev, sizeof(int) * (max_rounds + 1), hipMemcpyDeviceToHost, ctx->stream));
     if (out) HIP_TRY(ctx, hipMemcpyAsync(out, t->rec_dev, sizeof(gnsship_trk_epoch) * nrec, hipMemcpyDeviceToHost, ctx->stream));
+    if (dump) HIP_TRY(ctx, hipMemcpyAsync(dump, t->dump_dev, sizeof(gnsship_trk_dump_record) * nrec, hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     if (rounds_done) {
         int n = 0;

@@ -62,6 +62,7 @@ struct Smoother {
 struct TrkChannel {
     int32_t state;  // 0 idle / lost, 2 wide tracking, 3 coherent integration, 4 narrow tracking
     int32_t geo;    // symbol-sync profile (TrkParams::sync): 1 for a BeiDou B1I GEO satellite
+    uint32_t prn;   // Gnss_Synchro::PRN (dump records)
     int32_t narrow;     // loop set / taps in use (1 after entering extended integration)
     int32_t ext_count;  // d_extend_correlation_symbols_count
     int32_t cloop, pull_in, pll_180, ran, acc_phase_init;
@@ -108,7 +109,7 @@ struct TrkHist {
 // HdPlan of the engine) and `hist` holds the channels' rate-smoother rings; otherwise all three are
 // null and the jobs go to the standard correlator (jobs / chunks).
 hipError_t launch_trk_step(const TrkParams* params, TrkChannel* chans, int n_chans, DevJob* jobs, ChunkDesc* chunks, const float* corr_out,
-    uint64_t buf_first, int64_t buf_len, int consume, int emit, gnsship_trk_epoch* rec, int* ran_count, TrkHist* hist, HdJob* hd_jobs,
-    HdChunk* hd_chunks, hipStream_t stream);
+    uint64_t buf_first, int64_t buf_len, int consume, int emit, gnsship_trk_epoch* rec, gnsship_trk_dump_record* dump, int* ran_count,
+    TrkHist* hist, HdJob* hd_jobs, HdChunk* hd_chunks, hipStream_t stream);
 
 }  // namespace gnsship

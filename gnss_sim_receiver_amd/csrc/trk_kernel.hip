@@ -325,7 +325,39 @@ __device__ void zero_accu(TrkChannel& c)
 
 // One general_work call for the epoch that started at c.epoch_start; returns false when the
 // channel stops (loss of lock).
-__device__ bool epoch_update(const TrkParams& k, TrkChannel& c, const float* taps, const float* pdata, gnsship_trk_epoch& rec, TrkHist* h)
+// log_data (:1376-1466) at epoch start nir, after update_tracking_vars.
+__device__ void log_data(const TrkParams& k, const TrkChannel& c, const float* taps, const float* pdata, uint64_t nir, gnsship_trk_dump_record* d)
+{
+    if (!d) return;
+    const int eo = k.veml ? 2 : 0;
+    const float* prompt = k.track_pilot ? pdata : taps + eo + 2;
+    const double fs = k.conf.fs_in;
+    d->abs_VE = k.veml ? hypotf(c.ve[0], c.ve[1]) : 0.0f;
+    d->abs_E = hypotf(c.e[0], c.e[1]);
+    d->abs_P = hypotf(c.p[0], c.p[1]);
+    d->abs_L = hypotf(c.l[0], c.l[1]);
+    d->abs_VL = k.veml ? hypotf(c.vl[0], c.vl[1]) : 0.0f;
+    d->prompt_I = prompt[0];
+    d->prompt_Q = prompt[1];
+    d->PRN_start_sample_count = nir + static_cast<uint64_t>(c.current_prn_length_samples);
+    d->acc_carrier_phase_rad = static_cast<float>(c.acc_carrier_phase_rad);
+    d->carrier_doppler_hz = static_cast<float>(c.carrier_doppler_hz);
+    d->carrier_doppler_rate_hz = static_cast<float>(c.carrier_phase_rate_step_rad * fs * fs / kTwoPi);
+    d->code_freq_chips = static_cast<float>(c.code_freq_chips);
+    d->code_freq_rate_chips = static_cast<float>(c.code_phase_rate_step_chips * fs * fs);
+    d->carr_error_hz = static_cast<float>(c.carr_phase_error_hz);
+    d->carr_error_filt_hz = static_cast<float>(c.carr_error_filt_hz);
+    d->code_error_chips = static_cast<float>(c.code_error_chips);
+    d->code_error_filt_chips = static_cast<float>(c.code_error_filt_chips);
+    d->CN0_SNV_dB_Hz = c.cn0_db_hz;
+    d->carrier_lock_test = c.carrier_lock_test;
+    d->aux1 = static_cast<float>(c.rem_code_phase_samples);
+    d->aux2 = static_cast<double>(nir + static_cast<uint64_t>(c.current_prn_length_samples));
+    d->PRN = c.prn;
+}
+
+__device__ bool epoch_update(const TrkParams& k, TrkChannel& c, const float* taps, const float* pdata, gnsship_trk_epoch& rec, TrkHist* h,
+    gnsship_trk_dump_record* dump)
 {
     const uint64_t nir = c.epoch_start;
     const uint64_t fs_int = static_cast<uint64_t>(static_cast<int>(k.conf.fs_in));
@@ -363,6 +395,8 @@ __device__ bool epoch_update(const TrkParams& k, TrkChannel& c, const float* tap
             bool next_state = false;
             run_dll_pll(k, c);
             update_tracking_vars(k, c, h);
+            log_data(k, c, taps, pdata, nir, dump);
+            rec.flags |= 16;
             if (!c.pull_in) {
                 if (k.sync[c.geo].secondary || k.sync[c.geo].symbols_per_bit > 1) {
                     push_sign(k, c, taps[eo + 2]);
@@ -418,6 +452,8 @@ __device__ bool epoch_update(const TrkParams& k, TrkChannel& c, const float* tap
         if (st == 3) {  // coherent integration (:1933-1970): accumulate, NCO advance only
             update_tracking_vars(k, c, h);
             if (c.current_data_symbol == 0) {
+                log_data(k, c, taps, pdata, nir, dump);
+                rec.flags |= 16;
                 rec.prompt_i = static_cast<double>(c.p_data[0]);
                 rec.prompt_q = static_cast<double>(c.p_data[1]);
                 rec.flags |= 1;
@@ -440,6 +476,8 @@ __device__ bool epoch_update(const TrkParams& k, TrkChannel& c, const float* tap
                 c.acc_phase_init = 1;
             }
             if (c.current_data_symbol == 0) {
+                log_data(k, c, taps, pdata, nir, dump);
+                rec.flags |= 16;
                 rec.prompt_i = static_cast<double>(c.p_data[0]);
                 rec.prompt_q = static_cast<double>(c.p_data[1]);
                 rec.flags |= 1;
@@ -528,8 +566,8 @@ __device__ void fill_hd_job(HdJob& j, const TrkParams& k, const TrkChannel& c, i
 
 __global__ void trk_step_kernel(const TrkParams* __restrict__ pk, TrkChannel* __restrict__ chans, int n_chans, DevJob* __restrict__ jobs,
     ChunkDesc* __restrict__ chunks, const float* __restrict__ corr_out, uint64_t buf_first, int64_t buf_len, int consume, int emit,
-    gnsship_trk_epoch* __restrict__ rec, int* __restrict__ ran_count, TrkHist* __restrict__ hist, HdJob* __restrict__ hd_jobs,
-    HdChunk* __restrict__ hd_chunks)
+    gnsship_trk_epoch* __restrict__ rec, gnsship_trk_dump_record* __restrict__ dump, int* __restrict__ ran_count, TrkHist* __restrict__ hist,
+    HdJob* __restrict__ hd_jobs, HdChunk* __restrict__ hd_chunks)
 {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n_chans) return;
@@ -541,7 +579,9 @@ __global__ void trk_step_kernel(const TrkParams* __restrict__ pk, TrkChannel* __
         r.flags = 8;
         const float* taps = corr_out + static_cast<int64_t>(jb) * 2 * kMaxTaps;
         const float* pdata = k.jobs_per_channel > 1 ? corr_out + static_cast<int64_t>(jb + 1) * 2 * kMaxTaps : taps;
-        epoch_update(k, c, taps, pdata, r, hist ? hist + i : nullptr);
+        gnsship_trk_dump_record dr;
+        epoch_update(k, c, taps, pdata, r, hist ? hist + i : nullptr, dump ? &dr : nullptr);
+        if (dump && (r.flags & 16)) dump[i] = dr;
         if (rec) rec[i] = r;
     } else if (consume && rec) {
         gnsship_trk_epoch r = {};
@@ -594,11 +634,11 @@ __global__ void trk_step_kernel(const TrkParams* __restrict__ pk, TrkChannel* __
 }  // namespace
 
 hipError_t launch_trk_step(const TrkParams* params, TrkChannel* chans, int n_chans, DevJob* jobs, ChunkDesc* chunks, const float* corr_out,
-    uint64_t buf_first, int64_t buf_len, int consume, int emit, gnsship_trk_epoch* rec, int* ran_count, TrkHist* hist, HdJob* hd_jobs,
-    HdChunk* hd_chunks, hipStream_t stream)
+    uint64_t buf_first, int64_t buf_len, int consume, int emit, gnsship_trk_epoch* rec, gnsship_trk_dump_record* dump, int* ran_count,
+    TrkHist* hist, HdJob* hd_jobs, HdChunk* hd_chunks, hipStream_t stream)
 {
     hipLaunchKernelGGL(trk_step_kernel, dim3((n_chans + 63) / 64), dim3(64), 0, stream, params, chans, n_chans, jobs, chunks, corr_out, buf_first,
-        buf_len, consume, emit, rec, ran_count, hist, hd_jobs, hd_chunks);
+        buf_len, consume, emit, rec, dump, ran_count, hist, hd_jobs, hd_chunks);
     return hipGetLastError();
 }
 

@@ -433,10 +433,14 @@ class DllPllVemlTracking:
         return st.value, nx.value
 
     def run(self, sig, buffer_first_sample: int, max_rounds: int, fmt: int = None, n_buffer_samples: int = None,
-            records: bool = True):
+            records: bool = True, dump: bool = False):
         """sig: host ndarray or DeviceBuffer (pass fmt and n_buffer_samples).  Returns (records
-        [max_rounds, max_channels] or None, rounds_done)."""
+        [max_rounds, max_channels] or None, rounds_done), plus the log_data dump records
+        [max_rounds, max_channels] (TRK_DUMP_DTYPE; valid where the record has flags & 16) when dump."""
         out = np.zeros((max_rounds, self.max_channels), abi.TRK_EPOCH_DTYPE) if records else None
+        dmp = np.zeros((max_rounds, self.max_channels), abi.TRK_DUMP_DTYPE) if dump else None
+        if dump and not records:
+            raise ValueError("dump records need the epoch records (flags & 16 marks them)")
         if isinstance(sig, DeviceBuffer):
             ptr, on_dev, f = sig.ptr, 1, FMT_CF32 if fmt is None else fmt
             n = n_buffer_samples if n_buffer_samples is not None else sig.nbytes // _FMT_BYTES[f]
@@ -445,9 +449,23 @@ class DllPllVemlTracking:
             ptr, on_dev, f = sig.ctypes.data, 0, sample_format(sig)
             n = sig.nbytes // _FMT_BYTES[f]
         done = ctypes.c_int()
-        check(self.ctx.lib.gnsship_trk_run(self.h, ptr, f, on_dev, buffer_first_sample, n, max_rounds,
-                                           out.ctypes.data if records else None, ctypes.byref(done)), "gnsship_trk_run", self.ctx.h)
-        return out, done.value
+        check(self.ctx.lib.gnsship_trk_run_dump(self.h, ptr, f, on_dev, buffer_first_sample, n, max_rounds,
+                                                out.ctypes.data if records else None, dmp.ctypes.data if dump else None,
+                                                ctypes.byref(done)), "gnsship_trk_run_dump", self.ctx.h)
+        return (out, done.value, dmp) if dump else (out, done.value)
+
+    @staticmethod
+    def write_dump_files(prefix: str, records: np.ndarray, dumps: np.ndarray, append: bool = False) -> list:
+        """The reference's per-channel tracking dump files (<prefix><channel>.dat, dll_pll_veml_tracking.cc:
+        set_channel :1674-1700, log_data :1376-1466): the records log_data wrote, in round order."""
+        paths = []
+        for ch in range(records.shape[1]):
+            sel = (records[:, ch]["flags"] & abi.TRK_FLAG_DUMP) != 0
+            path = f"{prefix}{ch}.dat"
+            with open(path, "ab" if append else "wb") as f:
+                f.write(np.ascontiguousarray(dumps[sel, ch]).tobytes())
+            paths.append(path)
+        return paths
 
     def close(self):
         if self.h:

@@ -123,7 +123,7 @@ typedef struct gnsship_corr_job {
     int32_t n_samples;       /* correlation length (vector_length)                            */
     int32_t code_id;         /* code bank id                                                   */
     int32_t n_taps;          /* 1..GNSSHIP_MAX_TAPS                                            */
-    int32_t flags;           /* bit0: high-dynamics resampler/rotator (unsupported: E_INVAL)   */
+    int32_t flags;           /* bit0: high-dynamics resampler/rotator (set_high_dynamics_resampler) */
     float rem_carrier_phase_rad;
     float phase_step_rad;
     float phase_rate_step_rad;
@@ -318,7 +318,8 @@ typedef struct gnsship_trk_epoch { /* one general_work call of one channel (Gnss
     double cn0_db_hz;
     float carrier_lock_test;
     int32_t state;                 /* state the epoch ran in (2, 3 or 4) */
-    int32_t flags;                 /* 1 valid symbol, 2 loss of lock, 4 PLL 180°, 8 epoch ran */
+    int32_t flags;                 /* 1 valid symbol, 2 loss of lock, 4 PLL 180°, 8 epoch ran,
+                                      16 log_data record written (gnsship_trk_run_dump) */
     int32_t pad;
     double code_freq_chips;
     double rem_code_phase_chips;
@@ -338,6 +339,32 @@ int gnsship_trk_stop(gnsship_trk* t, int channel);
  * least one channel ran. */
 int gnsship_trk_run(gnsship_trk* t, const void* sig, int fmt, int sig_on_device, uint64_t buffer_first_sample, int64_t n_buffer_samples,
     int max_rounds, gnsship_trk_epoch* out, int* rounds_done);
+/* The tracking dump record dll_pll_veml_tracking::log_data writes per valid loop update when
+ * `dump` is on (:1376-1466; read back by tracking_dump_reader.cc:26-47): 96 bytes, packed exactly
+ * as the file — a per-channel .dat dump is the concatenation of the records whose epoch has
+ * flags & 16, in round order. */
+#pragma pack(push, 4)
+typedef struct gnsship_trk_dump_record {
+    float abs_VE, abs_E, abs_P, abs_L, abs_VL; /* |accumulators| (VE/VL 0 without VEML)            */
+    float prompt_I, prompt_Q;                 /* this epoch's prompt (data prompt with track_pilot) */
+    uint64_t PRN_start_sample_count;          /* nitems_read + d_current_prn_length_samples     */
+    float acc_carrier_phase_rad;
+    float carrier_doppler_hz;
+    float carrier_doppler_rate_hz;            /* carrier_phase_rate_step_rad·fs²/2π (high_dyn)   */
+    float code_freq_chips;
+    float code_freq_rate_chips;               /* code_phase_rate_step_chips·fs²                  */
+    float carr_error_hz, carr_error_filt_hz;
+    float code_error_chips, code_error_filt_chips;
+    float CN0_SNV_dB_Hz, carrier_lock_test;
+    float aux1;                               /* d_rem_code_phase_samples                        */
+    double aux2;                              /* (double)(nitems_read + prn length)              */
+    uint32_t PRN;
+} gnsship_trk_dump_record;
+#pragma pack(pop)
+/* gnsship_trk_run that also fills dump[max_rounds × max_channels] (optional) with the log_data
+ * records of the epochs flagged 16. */
+int gnsship_trk_run_dump(gnsship_trk* t, const void* sig, int fmt, int sig_on_device, uint64_t buffer_first_sample, int64_t n_buffer_samples,
+    int max_rounds, gnsship_trk_epoch* out, gnsship_trk_dump_record* dump, int* rounds_done);
 int gnsship_trk_channel_state(gnsship_trk* t, int channel, int* state, uint64_t* next_sample);
 int gnsship_trk_destroy(gnsship_trk* t);
 

@@ -11,6 +11,7 @@
 #include <cmath>
 #include <complex>
 #include <cstdint>
+#include <cstdio>
 #include <atomic>
 #include <map>
 #include <memory>
@@ -506,6 +507,33 @@ public:
         std::lock_guard<std::mutex> lk(dev_->mutex());
         if (gnsship_trk_run(h_, in, GNSSHIP_FMT_CF32, in_on_device ? 1 : 0, first_sample, n, max_epochs, records, &done) != GNSSHIP_OK) return -1;
         return done;
+    }
+    // work() with Dll_Pll_Conf::dump on: dumps (max_epochs × max_channels) receives the log_data
+    // records (:1376-1466) of the epochs whose record has flags & 16.
+    int work_dump(const std::complex<float>* in, uint64_t first_sample, int64_t n, int max_epochs, gnsship_trk_epoch* records,
+        gnsship_trk_dump_record* dumps, bool in_on_device = false)
+    {
+        int done = 0;
+        std::lock_guard<std::mutex> lk(dev_->mutex());
+        if (gnsship_trk_run_dump(h_, in, GNSSHIP_FMT_CF32, in_on_device ? 1 : 0, first_sample, n, max_epochs, records, dumps, &done) !=
+            GNSSHIP_OK)
+            return -1;
+        return done;
+    }
+    // Append channel `channel`'s records to its dump file (<dump_filename><channel>.dat, as the
+    // block's d_dump_file): the binary layout tracking_dump_reader reads.
+    bool append_dump_file(const std::string& dump_filename, int channel, const gnsship_trk_epoch* records, const gnsship_trk_dump_record* dumps,
+        int rounds) const
+    {
+        const std::string path = dump_filename + std::to_string(channel) + ".dat";
+        std::FILE* f = std::fopen(path.c_str(), "ab");
+        if (!f) return false;
+        bool ok = true;
+        for (int r = 0; r < rounds && ok; r++) {
+            const size_t i = static_cast<size_t>(r) * channels_ + channel;
+            if (records[i].flags & 16) ok = std::fwrite(&dumps[i], sizeof(gnsship_trk_dump_record), 1, f) == 1;
+        }
+        return std::fclose(f) == 0 && ok;
     }
     int state(int channel, uint64_t* next_sample = nullptr)
     {

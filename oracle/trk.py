@@ -46,6 +46,16 @@ EPOCH_DTYPE = np.dtype([
     ("rem_carr_phase_rad", "<f4"), ("prn_length_samples", "<i4"),
 ])
 
+# log_data's record (dll_pll_veml_tracking.cc:1376-1466 = tracking_dump_reader.cc:26-47), packed
+DUMP_DTYPE = np.dtype([
+    ("abs_VE", "<f4"), ("abs_E", "<f4"), ("abs_P", "<f4"), ("abs_L", "<f4"), ("abs_VL", "<f4"), ("prompt_I", "<f4"), ("prompt_Q", "<f4"),
+    ("PRN_start_sample_count", "<u8"), ("acc_carrier_phase_rad", "<f4"), ("carrier_doppler_hz", "<f4"), ("carrier_doppler_rate_hz", "<f4"),
+    ("code_freq_chips", "<f4"), ("code_freq_rate_chips", "<f4"), ("carr_error_hz", "<f4"), ("carr_error_filt_hz", "<f4"),
+    ("code_error_chips", "<f4"), ("code_error_filt_chips", "<f4"), ("CN0_SNV_dB_Hz", "<f4"), ("carrier_lock_test", "<f4"),
+    ("aux1", "<f4"), ("aux2", "<f8"), ("PRN", "<u4"),
+])
+assert DUMP_DTYPE.itemsize == 96
+
 GPS_PREAMBLE_SYMBOLS = "1" * 20 + "0" * 60 + "1" * 20 + "0" * 20 + "1" * 40  # GPS_L1_CA.h:73 (10001011 × 20)
 E1C_SECONDARY = "0011100000001010110110010"                               # Galileo_E1.h:52
 B1I_NH = "00000100110101001110"                                           # Beidou_B1I.h:48
@@ -126,15 +136,17 @@ def _L():
     L.orc_carrier_lock_detector.restype = ctypes.c_float
     L.orc_trk_start.argtypes = [ctypes.POINTER(OrcTrkConf), vp, ctypes.c_double, ctypes.c_double, ctypes.c_uint64, ctypes.c_uint64]
     L.orc_trk_run.argtypes = [ctypes.POINTER(OrcTrkConf), vp, _f32p, ctypes.c_uint64, ctypes.c_int64, _f32p, ctypes.c_int, _f32p, ctypes.c_int,
-                              vp]
+                              vp, vp]
+    L.orc_trk_set_prn.argtypes = [vp, ctypes.c_uint32]
     L.orc_trk_nitems_read.argtypes = [vp]
     L.orc_trk_nitems_read.restype = ctypes.c_uint64
     L.orc_trk_state.argtypes = [vp]
-    for name in ("orc_trk_sizeof_channel", "orc_trk_sizeof_conf", "orc_trk_sizeof_epoch", "orc_trk_sizeof_loop_filter",
+    for name in ("orc_trk_sizeof_channel", "orc_trk_sizeof_conf", "orc_trk_sizeof_epoch", "orc_trk_sizeof_dump", "orc_trk_sizeof_loop_filter",
                  "orc_trk_sizeof_fll_pll", "orc_trk_sizeof_smoother"):
         getattr(L, name).restype = ctypes.c_int
     assert L.orc_trk_sizeof_conf() == ctypes.sizeof(OrcTrkConf)
     assert L.orc_trk_sizeof_epoch() == EPOCH_DTYPE.itemsize
+    assert L.orc_trk_sizeof_dump() == DUMP_DTYPE.itemsize
     L._trk_ready = True
     return L
 
@@ -197,22 +209,26 @@ class Channel:
     """One oracle channel: start_tracking, then run() over successive buffers."""
 
     def __init__(self, k: OrcTrkConf, code: np.ndarray, acq_delay_samples: float, acq_doppler_hz: float, acq_samplestamp: int,
-                 first_sample: int, data_code: np.ndarray = None):
+                 first_sample: int, data_code: np.ndarray = None, prn: int = 0):
         L = _L()
         self.k = k
         self.buf = ctypes.create_string_buffer(L.orc_trk_sizeof_channel())
         self.code = np.ascontiguousarray(code, np.float32)
         self.data_code = np.ascontiguousarray(data_code, np.float32) if data_code is not None else None
         L.orc_trk_start(ctypes.byref(k), self.buf, acq_delay_samples, acq_doppler_hz, acq_samplestamp, first_sample)
+        L.orc_trk_set_prn(self.buf, prn)
 
-    def run(self, samples: np.ndarray, buffer_first: int, max_epochs: int) -> np.ndarray:
+    def run(self, samples: np.ndarray, buffer_first: int, max_epochs: int, dump: bool = False):
+        """EPOCH_DTYPE records (and, with dump=True, the per-epoch DUMP_DTYPE records; rows whose
+        epoch has flags & 16 are the ones log_data writes)."""
         L = _L()
         x = np.ascontiguousarray(samples, np.complex64)
         out = np.zeros(max_epochs, EPOCH_DTYPE)
+        d = np.zeros(max_epochs, DUMP_DTYPE) if dump else None
         dc = self.data_code
         n = L.orc_trk_run(ctypes.byref(self.k), self.buf, _ptr(x.view(np.float32)), buffer_first, len(x), _ptr(self.code), len(self.code),
-                          _ptr(dc) if dc is not None else None, max_epochs, out.ctypes.data)
-        return out[:n]
+                          _ptr(dc) if dc is not None else None, max_epochs, out.ctypes.data, d.ctypes.data if dump else None)
+        return (out[:n], d[:n]) if dump else out[:n]
 
     @property
     def state(self) -> int:
@@ -224,8 +240,8 @@ class Channel:
 
 
 def track(k: OrcTrkConf, samples: np.ndarray, code: np.ndarray, acq_delay_samples: float, acq_doppler_hz: float, acq_samplestamp: int,
-          first_sample: int, max_epochs: int, data_code: np.ndarray = None, buffer_first: int = 0) -> np.ndarray:
+          first_sample: int, max_epochs: int, data_code: np.ndarray = None, buffer_first: int = 0, dump: bool = False, prn: int = 0):
     """start_tracking + general_work until max_epochs / loss of lock / end of `samples`
-    (samples[i] = absolute sample buffer_first + i).  Returns EPOCH_DTYPE records."""
-    ch = Channel(k, code, acq_delay_samples, acq_doppler_hz, acq_samplestamp, first_sample, data_code)
-    return ch.run(samples, buffer_first, max_epochs)
+    (samples[i] = absolute sample buffer_first + i).  Returns EPOCH_DTYPE records (+ DUMP_DTYPE)."""
+    ch = Channel(k, code, acq_delay_samples, acq_doppler_hz, acq_samplestamp, first_sample, data_code, prn)
+    return ch.run(samples, buffer_first, max_epochs, dump)

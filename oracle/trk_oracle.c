@@ -373,13 +373,28 @@ typedef struct {
     double carrier_phase_rate_step_rad, code_phase_rate_step_chips;
     double hist_carr[2 * TRK_MAX_SMOOTHER], hist_code[2 * TRK_MAX_SMOOTHER], hist_samples[2 * TRK_MAX_SMOOTHER];
     int hist_head, hist_count;
+    uint32_t prn; /* Gnss_Synchro::PRN (dump records) */
 } orc_trk_channel;
+
+/* The tracking dump record log_data writes field by field (dll_pll_veml_tracking.cc:1376-1466;
+ * read back by tracking_dump_reader.cc:26-47): 96 bytes, no padding. */
+#pragma pack(push, 4)
+typedef struct {
+    float abs_VE, abs_E, abs_P, abs_L, abs_VL, prompt_I, prompt_Q;
+    uint64_t PRN_start_sample_count;
+    float acc_carrier_phase_rad, carrier_doppler_hz, carrier_doppler_rate_hz, code_freq_chips, code_freq_rate_chips;
+    float carr_error_hz, carr_error_filt_hz, code_error_chips, code_error_filt_chips, CN0_SNV_dB_Hz, carrier_lock_test;
+    float aux1;
+    double aux2;
+    uint32_t PRN;
+} orc_trk_dump;
+#pragma pack(pop)
 
 typedef struct { /* Gnss_Synchro subset emitted per epoch (dll_pll_veml_tracking.cc:1996-2091) */
     uint64_t sample_counter;
     double prompt_i, prompt_q, code_phase_samples, carrier_phase_rads, carrier_doppler_hz, cn0_db_hz;
     float carrier_lock_test;
-    int32_t state, flags; /* flags: 1 valid symbol, 2 loss of lock, 4 PLL 180° */
+    int32_t state, flags; /* flags: 1 valid symbol, 2 loss of lock, 4 PLL 180°, 16 log_data record written */
     double code_freq_chips, rem_code_phase_chips;
     float rem_carr_phase_rad;
     int32_t prn_length_samples;
@@ -688,8 +703,39 @@ static void enter_extended_integration(const orc_trk_conf* k, orc_trk_channel* c
  * correlator outputs of that epoch (taps: n_taps complex, pdata: data-prompt complex).
  * Advances nitems_read by the new current_prn_length_samples.  Returns 0 when the channel is
  * (or becomes) idle. */
-int orc_trk_epoch_update(const orc_trk_conf* k, orc_trk_channel* c, const float* taps, const float* pdata, orc_trk_epoch* rec)
+/* log_data (:1376-1466) at epoch start `nir`, after update_tracking_vars. */
+static void log_data(const orc_trk_conf* k, const orc_trk_channel* c, const float* taps, const float* pdata, uint64_t nir, orc_trk_dump* d)
 {
+    if (!d) return;
+    const int eo = c->veml ? 2 : 0;
+    const float* prompt = k->track_pilot ? pdata : taps + eo + 2;
+    d->prompt_I = prompt[0];
+    d->prompt_Q = prompt[1];
+    d->abs_VE = c->veml ? hypotf(c->ve[0], c->ve[1]) : 0.0F;
+    d->abs_VL = c->veml ? hypotf(c->vl[0], c->vl[1]) : 0.0F;
+    d->abs_E = hypotf(c->e[0], c->e[1]);
+    d->abs_P = hypotf(c->p[0], c->p[1]);
+    d->abs_L = hypotf(c->l[0], c->l[1]);
+    d->PRN_start_sample_count = nir + (uint64_t)c->current_prn_length_samples;
+    d->acc_carrier_phase_rad = (float)c->acc_carrier_phase_rad;
+    d->carrier_doppler_hz = (float)c->carrier_doppler_hz;
+    d->carrier_doppler_rate_hz = (float)(c->carrier_phase_rate_step_rad * k->fs_in * k->fs_in / TRK_TWO_PI);
+    d->code_freq_chips = (float)c->code_freq_chips;
+    d->code_freq_rate_chips = (float)(c->code_phase_rate_step_chips * k->fs_in * k->fs_in);
+    d->carr_error_hz = (float)c->carr_phase_error_hz;
+    d->carr_error_filt_hz = (float)c->carr_error_filt_hz;
+    d->code_error_chips = (float)c->code_error_chips;
+    d->code_error_filt_chips = (float)c->code_error_filt_chips;
+    d->CN0_SNV_dB_Hz = c->cn0_db_hz;
+    d->carrier_lock_test = c->carrier_lock_test;
+    d->aux1 = (float)c->rem_code_phase_samples;
+    d->aux2 = (double)(nir + (uint64_t)c->current_prn_length_samples);
+    d->PRN = c->prn;
+}
+
+int orc_trk_epoch_update(const orc_trk_conf* k, orc_trk_channel* c, const float* taps, const float* pdata, orc_trk_epoch* rec, orc_trk_dump* dump)
+{
+    if (dump) memset(dump, 0, sizeof(*dump));
     memset(rec, 0, sizeof(*rec));
     if (c->state != 2 && c->state != 3 && c->state != 4) return 0;
     const uint64_t nir = c->nitems_read;
@@ -730,6 +776,8 @@ int orc_trk_epoch_update(const orc_trk_conf* k, orc_trk_channel* c, const float*
             int next_state = 0;
             run_dll_pll(k, c);
             update_tracking_vars(k, c);
+            log_data(k, c, taps, pdata, nir, dump);
+            rec->flags |= 16;
             if (!c->pull_in) {
                 if (k->secondary || k->symbols_per_bit > 1) {
                     push_prompt_sign(k, c, taps[eo + 2]);
@@ -758,6 +806,8 @@ int orc_trk_epoch_update(const orc_trk_conf* k, orc_trk_channel* c, const float*
         save_correlation_results(k, c, taps, pdata);
         update_tracking_vars(k, c);
         if (c->current_data_symbol == 0) {
+            log_data(k, c, taps, pdata, nir, dump);
+            rec->flags |= 16;
             rec->prompt_i = (double)c->p_data[0];
             rec->prompt_q = (double)c->p_data[1];
             rec->flags |= 1;
@@ -782,6 +832,8 @@ int orc_trk_epoch_update(const orc_trk_conf* k, orc_trk_channel* c, const float*
                 c->acc_carrier_phase_initialized = 1;
             }
             if (c->current_data_symbol == 0) {
+                log_data(k, c, taps, pdata, nir, dump);
+                rec->flags |= 16;
                 rec->prompt_i = (double)c->p_data[0];
                 rec->prompt_q = (double)c->p_data[1];
                 rec->flags |= 1;
@@ -815,6 +867,8 @@ int orc_trk_epoch_update(const orc_trk_conf* k, orc_trk_channel* c, const float*
 int orc_trk_sizeof_channel(void) { return (int)sizeof(orc_trk_channel); }
 int orc_trk_sizeof_conf(void) { return (int)sizeof(orc_trk_conf); }
 int orc_trk_sizeof_epoch(void) { return (int)sizeof(orc_trk_epoch); }
+int orc_trk_sizeof_dump(void) { return (int)sizeof(orc_trk_dump); }
+void orc_trk_set_prn(orc_trk_channel* c, uint32_t prn) { c->prn = prn; }
 uint64_t orc_trk_nitems_read(const orc_trk_channel* c) { return c->nitems_read; }
 int orc_trk_state(const orc_trk_channel* c) { return c->state; }
 
@@ -828,7 +882,7 @@ int orc_multicorrelator_real_codes(float* corr_out, const float* sig_in, const f
  * when track_pilot, the data code with one prompt tap), then update.  Stops after max_epochs,
  * when the channel goes idle, or when the next window leaves the buffer.  Returns epochs run. */
 int orc_trk_run(const orc_trk_conf* k, orc_trk_channel* c, const float* samples, uint64_t buffer_first, int64_t n_samples, const float* code,
-    int code_len, const float* data_code, int max_epochs, orc_trk_epoch* out)
+    int code_len, const float* data_code, int max_epochs, orc_trk_epoch* out, orc_trk_dump* dump)
 {
     const int vl = (int)k->vector_length;
     float* scratch = (float*)malloc((size_t)5 * (size_t)vl * sizeof(float));
@@ -847,7 +901,7 @@ int orc_trk_run(const orc_trk_conf* k, orc_trk_channel* c, const float* samples,
             orc_multicorrelator_real_codes(pdata, x, data_code, code_len, &zero, 1, k->high_dyn, args[0], args[1], args[2], args[3], args[4], args[5], vl,
                 scratch);
         }
-        if (!orc_trk_epoch_update(k, c, taps, pdata, &out[e])) {
+        if (!orc_trk_epoch_update(k, c, taps, pdata, &out[e], dump ? &dump[e] : NULL)) {
             e++;
             break;
         }

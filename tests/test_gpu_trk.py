@@ -175,6 +175,46 @@ def test_bds_geo_matches_oracle(ctx, ext):
     trk.close()
 
 
+@pytest.mark.parametrize("system,fs,epochs,kw", [("GPS", 4e6, 400, {}), ("GAL", 25e6 / 4, 90, {}),
+                                                 ("GPS", 4e6, 300, dict(high_dyn=1, smoother_length=5, rate_hz_s=30.0))])
+def test_dump_records_match_oracle(ctx, tmp_path, system, fs, epochs, kw):
+    """log_data records (dll_pll_veml_tracking.cc:1376-1466) from the device loop vs the oracle's:
+    written on the same epochs, same stamps/PRN, values within the loop tolerances."""
+    sat, k, x, stamp, first, delay, dop = S.sync(system, fs, epochs, **kw)
+    trk = engine.DllPllVemlTracking(ctx, dev_conf(k, system), 1)
+    ctx.set_code(70, sat.code)
+    if sat.code_data is not None:
+        ctx.set_code(71, sat.code_data)
+    trk.start(0, 70, delay, dop, stamp, first, data_code_id=71, prn=sat.prn)
+    rec, rounds, dump = trk.run(x, first, epochs, dump=True)
+    ref, rdump = T.track(k, x, sat.code, delay, dop, stamp, first, epochs, data_code=sat.code_data, buffer_first=first, dump=True,
+                         prn=sat.prn)
+    ran = (rec[:, 0]["flags"] & 8) != 0
+    d_rec, d_dump = rec[ran, 0], dump[ran, 0]
+    assert np.array_equal(d_rec["flags"] & 16, ref["flags"] & 16)
+    w = (ref["flags"] & 16) != 0
+    a, b = d_dump[w], rdump[w]
+    assert len(a) > 20
+    for f in ("PRN_start_sample_count", "aux2", "PRN"):
+        assert np.array_equal(a[f], b[f]), f
+    tol = {"abs_VE": 1e-4, "abs_E": 1e-4, "abs_P": 1e-4, "abs_L": 1e-4, "abs_VL": 1e-4, "prompt_I": 1e-4, "prompt_Q": 1e-4}
+    for f, rt in tol.items():
+        np.testing.assert_allclose(a[f], b[f], rtol=rt, atol=1e-3, err_msg=f)
+    for f, at in [("acc_carrier_phase_rad", 1e-2), ("carrier_doppler_hz", 2e-3),
+                  ("code_freq_chips", 2e-3), ("carr_error_hz", 1e-3), ("carr_error_filt_hz", 2e-3), ("code_error_chips", 1e-4),
+                  ("code_error_filt_chips", 1e-4), ("CN0_SNV_dB_Hz", 5e-3), ("carrier_lock_test", 1e-4), ("aux1", 1e-4),
+                  # rates: differences of smoothed steps over ~smoother_length epochs amplify the
+                  # ≤ 2e-3 Hz Doppler agreement to ~0.1-0.5 Hz/s
+                  ("carrier_doppler_rate_hz", 0.5), ("code_freq_rate_chips", 0.5)]:
+        np.testing.assert_allclose(a[f], b[f], rtol=1e-5, atol=at, err_msg=f)
+    if kw.get("high_dyn"):
+        assert np.any(a["carrier_doppler_rate_hz"] != 0)
+    paths = engine.DllPllVemlTracking.write_dump_files(str(tmp_path / "trk_channel_"), rec, dump)
+    data = np.fromfile(paths[0], abi.TRK_DUMP_DTYPE)
+    assert np.array_equal(data, a)
+    trk.close()
+
+
 def test_high_dyn_smoother_length_bound(ctx):
     k = abi.TrkConf.defaults(abi.SYS_GPS_L1CA, 4e6, 4000, high_dyn=1, smoother_length=65)
     with pytest.raises(abi.GnssHipError):

@@ -200,3 +200,27 @@ def test_bds_geo_d2_preamble_sync(built, ext):
     # valid symbols every 2 code periods in state 4 (one per D2 bit)
     s4 = rec[(st == 4) | (st == 3)]
     assert np.all(np.diff(np.nonzero(s4["flags"] & 1)[0]) == 2)
+
+
+def test_dump_records_follow_log_data(built):
+    """log_data (dll_pll_veml_tracking.cc:1376-1466): one record per state-2 loop update and per
+    valid symbol in states 3/4, fields consistent with the epoch's Gnss_Synchro output."""
+    sat, k, x, stamp, first, delay, dop = S.sync("GPS", 4e6, 300)
+    rec, dump = T.track(k, x, sat.code, delay, dop, stamp, first, 300, buffer_first=first, dump=True, prn=sat.prn)
+    w = (rec["flags"] & 16) != 0
+    st = rec["state"]
+    assert np.all(w[st == 2] | ((rec["flags"][st == 2] & 2) != 0))
+    assert np.array_equal(w[st == 4], (rec["flags"][st == 4] & 1) != 0)
+    d, r = dump[w], rec[w]
+    assert np.array_equal(d["PRN_start_sample_count"], r["sample_counter"] + r["prn_length_samples"].astype(np.uint64))
+    assert np.array_equal(d["aux2"], (r["sample_counter"] + r["prn_length_samples"].astype(np.uint64)).astype(np.float64))
+    assert np.array_equal(d["carrier_doppler_hz"], r["carrier_doppler_hz"].astype(np.float32))
+    assert np.array_equal(d["CN0_SNV_dB_Hz"], r["cn0_db_hz"].astype(np.float32))
+    assert np.array_equal(d["code_freq_chips"], r["code_freq_chips"].astype(np.float32))
+    assert np.all(d["PRN"] == sat.prn) and np.all(d["abs_VE"] == 0) and np.all(d["carrier_doppler_rate_hz"] == 0)
+    assert np.all(d["abs_P"] > d["abs_E"]) and np.all(d["abs_P"] > d["abs_L"])
+    # the file is the packed concatenation, readable field by field as tracking_dump_reader does
+    raw = d.tobytes()
+    assert len(raw) == 96 * len(d)
+    assert np.frombuffer(raw[28:36], "<u8")[0] == d["PRN_start_sample_count"][0]
+    assert np.frombuffer(raw[92:96], "<u4")[0] == sat.prn
