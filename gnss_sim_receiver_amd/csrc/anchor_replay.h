@@ -1,0 +1,75 @@
+// anchor_replay.h — the reference rotator recursion replayed on the device (shared by the batched
+// correlator's anchor stage, corr_kernel.hip, and the tracking step kernel, trk_kernel.hip, which
+// replays its channels' next-epoch anchors right after deriving their NCO).
+#pragma once
+#include "engine.h"
+#include "nco_math.h"
+
+#pragma clang fp contract(off)
+
+namespace gnsship {
+
+// First renormalisation block of replay segment seg of a job with nblk blocks (segments split at
+// the middle block; kAnchorSegments == 2).
+__device__ __forceinline__ int segment_block(int seg, int nblk)
+{
+    return seg <= 0 ? 0 : (seg >= kAnchorSegments ? nblk : (nblk + 1) / 2);
+}
+
+// The reference rotator recursion of one job, stored at every renormalisation point — blocks of
+// segments [seg_lo, seg_hi).  Block k stores the renormalised q_k and the chain's next three phasors
+// q_k·inc, q_k·inc², q_k·inc³ (engine.h Anchor).  A later segment resumes from the stored q of the
+// block before it: the chain after a renormalisation depends only on q.
+__device__ __forceinline__ void replay_anchors(const DevJob& job, Anchor* __restrict__ anchors, int seg_lo, int seg_hi)
+{
+    const int nblk = (job.n_samples + kRenorm - 1) / kRenorm;
+    const int kb = segment_block(seg_lo, nblk), ke = segment_block(seg_hi, nblk);
+    if (kb >= ke) return;
+    Anchor* out = anchors + job.anchor_offset;
+    typedef float f2v __attribute__((ext_vector_type(2)));
+    // phase·inc = (pr·ir − pi·ii, pr·ii + pi·ir) as two packed products + one packed add, each
+    // rounded separately like the reference's written-out complex product (no FMA).  The sign
+    // sits in the constant: fl(pi·(−ii)) = −fl(pi·ii) and x + (−y) ≡ x − y, bit for bit.
+    const f2v inc_a = {job.inc_re, job.inc_im};   // × pr
+    const f2v inc_b = {-job.inc_im, job.inc_re};  // × pi
+    f2v p;
+    if (kb == 0) {
+        p = f2v{job.p0_re, job.p0_im};
+    } else {
+        p = f2v{out[kb - 1].p[0], out[kb - 1].p[1]};
+#pragma unroll 16
+        for (int s = 0; s < kRenorm; s++) p = f2v{p.x, p.x} * inc_a + f2v{p.y, p.y} * inc_b;
+    }
+    for (int k = kb; k < ke; k++) {
+        // sample 256k uses `a = phase`; then phase /= |phase|; then 256 rotations reach 256(k+1)
+        const float m = hypotf_glibc(p.x, p.y);
+        const float qr = __fdiv_rn(p.x, m), qi = __fdiv_rn(p.y, m);
+        Anchor A;
+        A.p[0] = qr;
+        A.p[1] = qi;
+        p = f2v{qr, qi};
+        // the first 16 rotations peeled: q·inc^1..3 are stored on the way (the chain keeps the
+        // shape of a 16-step unrolled loop — 15 more such steps reach 256(k+1))
+#pragma unroll
+        for (int s = 1; s <= 16; s++) {
+            p = f2v{p.x, p.x} * inc_a + f2v{p.y, p.y} * inc_b;
+            if (s < 4) {
+                A.p[2 * s] = p.x;
+                A.p[2 * s + 1] = p.y;
+            }
+        }
+        out[k] = A;
+        if (k != ke - 1) {
+            for (int s0 = 16; s0 < kRenorm; s0 += 16) {
+#pragma unroll
+                for (int s = 0; s < 16; s++) {
+                    const f2v m1 = f2v{p.x, p.x} * inc_a;
+                    const f2v m2 = f2v{p.y, p.y} * inc_b;
+                    p = m1 + m2;
+                }
+            }
+        }
+    }
+}
+
+}  // namespace gnsship

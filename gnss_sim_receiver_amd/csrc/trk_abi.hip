@@ -563,7 +563,7 @@ extern "C" int gnsship_trk_run_dump(gnsship_trk* t, const void* sig, int fmt, in
         gnsship_trk_dump_record* drec = (dump && r > 0) ? t->dump_dev + static_cast<size_t>(r - 1) * nc : nullptr;
         hipError_t e = launch_trk_step(t->params_dev, t->chans_dev, nc, t->jobs_dev, t->chunks_dev, t->out_dev, buffer_first_sample, n_buffer_samples,
             consume, emit, rec, drec, t->ran_dev + r, t->hist_dev, t->high_dyn ? t->hd.jobs_dev : nullptr, t->high_dyn ? t->hd.chunks_dev : nullptr,
-            ctx->stream);
+            t->high_dyn ? nullptr : t->anchors_dev, ctx->stream);
         if (e != hipSuccess) return hip_fail(ctx, e, "launch_trk_step");
         if (!emit) break;
         if (t->high_dyn) {
@@ -573,7 +573,7 @@ extern "C" int gnsship_trk_run_dump(gnsship_trk* t, const void* sig, int fmt, in
             continue;
         }
         e = launch_corr_batch(src, fmt, t->jobs_dev, t->n_jobs, t->chunks_dev, t->items_dev, t->n_items, t->classes, max_len, t->any_multi,
-            t->anchors_dev, t->partials_dev, t->out_dev, ctx->stream);
+            t->anchors_dev, t->partials_dev, t->out_dev, ctx->stream, GNSSHIP_STAGE_CORRELATE);  // anchors: replayed by the step kernel
         if (e != hipSuccess) return hip_fail(ctx, e, "launch_corr_batch(tracking)");
     }
     std::vector<int> ran(max_rounds + 1);

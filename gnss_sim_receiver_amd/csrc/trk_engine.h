@@ -104,12 +104,14 @@ struct TrkHist {
 };
 
 // One round: consume the previous epoch's correlations (when `consume`), then lay down the next
-// epoch's jobs / chunk lengths for every channel whose window is in the buffer (when `emit`).
+// epoch's jobs / chunk lengths for every channel whose window is in the buffer (when `emit`) and
+// replay their rotator anchors into `anchors` (standard path; the correlation launch then runs
+// only its CORRELATE stage).
 // With high_dyn the epoch's correlations are high-dynamics jobs (hd_jobs / hd_chunks, the fixed
 // HdPlan of the engine) and `hist` holds the channels' rate-smoother rings; otherwise all three are
 // null and the jobs go to the standard correlator (jobs / chunks).
 hipError_t launch_trk_step(const TrkParams* params, TrkChannel* chans, int n_chans, DevJob* jobs, ChunkDesc* chunks, const float* corr_out,
     uint64_t buf_first, int64_t buf_len, int consume, int emit, gnsship_trk_epoch* rec, gnsship_trk_dump_record* dump, int* ran_count,
-    TrkHist* hist, HdJob* hd_jobs, HdChunk* hd_chunks, hipStream_t stream);
+    TrkHist* hist, HdJob* hd_jobs, HdChunk* hd_chunks, Anchor* anchors, hipStream_t stream);
 
 }  // namespace gnsship

@@ -21,6 +21,7 @@
 // (cosf/sinf) may differ from glibc's in the last ulp, i.e. ~1e-7 in the correlations.
 #include <cmath>
 
+#include "anchor_replay.h"
 #include "trk_engine.h"
 
 namespace gnsship {
@@ -567,7 +568,7 @@ __device__ void fill_hd_job(HdJob& j, const TrkParams& k, const TrkChannel& c, i
 __global__ void trk_step_kernel(const TrkParams* __restrict__ pk, TrkChannel* __restrict__ chans, int n_chans, DevJob* __restrict__ jobs,
     ChunkDesc* __restrict__ chunks, const float* __restrict__ corr_out, uint64_t buf_first, int64_t buf_len, int consume, int emit,
     gnsship_trk_epoch* __restrict__ rec, gnsship_trk_dump_record* __restrict__ dump, int* __restrict__ ran_count, TrkHist* __restrict__ hist,
-    HdJob* __restrict__ hd_jobs, HdChunk* __restrict__ hd_chunks)
+    HdJob* __restrict__ hd_jobs, HdChunk* __restrict__ hd_chunks, Anchor* __restrict__ anchors)
 {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n_chans) return;
@@ -613,6 +614,15 @@ __global__ void trk_step_kernel(const TrkParams* __restrict__ pk, TrkChannel* __
             DevJob& j = jobs[jb + q];
             if (runnable) {
                 fill_job(j, k, c, off, q == 0 ? c.code_id : c.data_code_id, n_taps, sh);
+                // the next epoch's rotator anchors, replayed here instead of by a separate anchor
+                // launch; the data job shares the pilot job's NCO, hence its anchors
+                if (q == 0) {
+                    replay_anchors(j, anchors, 0, kAnchorSegments);
+                } else {
+                    const DevJob& j0 = jobs[jb];
+                    const int nblk = (j.n_samples + kRenorm - 1) / kRenorm;
+                    for (int b = 0; b < nblk; b++) anchors[j.anchor_offset + b] = anchors[j0.anchor_offset + b];
+                }
             } else {
                 j.n_samples = 0;
             }
@@ -635,10 +645,10 @@ __global__ void trk_step_kernel(const TrkParams* __restrict__ pk, TrkChannel* __
 
 hipError_t launch_trk_step(const TrkParams* params, TrkChannel* chans, int n_chans, DevJob* jobs, ChunkDesc* chunks, const float* corr_out,
     uint64_t buf_first, int64_t buf_len, int consume, int emit, gnsship_trk_epoch* rec, gnsship_trk_dump_record* dump, int* ran_count,
-    TrkHist* hist, HdJob* hd_jobs, HdChunk* hd_chunks, hipStream_t stream)
+    TrkHist* hist, HdJob* hd_jobs, HdChunk* hd_chunks, Anchor* anchors, hipStream_t stream)
 {
     hipLaunchKernelGGL(trk_step_kernel, dim3((n_chans + 63) / 64), dim3(64), 0, stream, params, chans, n_chans, jobs, chunks, corr_out, buf_first,
-        buf_len, consume, emit, rec, dump, ran_count, hist, hd_jobs, hd_chunks);
+        buf_len, consume, emit, rec, dump, ran_count, hist, hd_jobs, hd_chunks, anchors);
     return hipGetLastError();
 }
 
