@@ -196,6 +196,7 @@ _SIGNATURES = {
     "gnsship_acq_set_local_code": ([_vp, _i, _f32p], _i),
     "gnsship_acq_run": ([_vp, _vp, _i, _i, _i, ctypes.POINTER(AcqResult), _f32p], _i),
     "gnsship_acq_num_bins": ([_vp, ctypes.POINTER(_i)], _i),
+    "gnsship_acq_reset_dwells": ([_vp], _i),
     "gnsship_acq_destroy": ([_vp], _i),
     "gnsship_firdes_low_pass": ([ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double, _f32p, _i, ctypes.POINTER(_i)], _i),
     "gnsship_acq_resampler_design": ([ctypes.c_int64, ctypes.c_double, ctypes.POINTER(_i), _f32p, _i, ctypes.POINTER(_i)], _i),

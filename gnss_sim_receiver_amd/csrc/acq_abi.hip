@@ -285,6 +285,13 @@ extern "C" int gnsship_acq_create(gnsship_ctx* ctx, const gnsship_acq_conf* conf
     return GNSSHIP_OK;
 }
 
+extern "C" int gnsship_acq_reset_dwells(gnsship_acq* a)
+{
+    if (!a) return GNSSHIP_E_INVAL;
+    a->dwell_count = 0;
+    return GNSSHIP_OK;
+}
+
 extern "C" int gnsship_acq_num_bins(gnsship_acq* a, int* n_bins)
 {
     if (!a || !n_bins) return GNSSHIP_E_INVAL;

@@ -216,6 +216,9 @@ int gnsship_acq_set_grid_step2(gnsship_acq* a, float doppler_center_step_two, fl
 int gnsship_acq_run(gnsship_acq* a, const void* sig, int fmt, int sig_on_device, int n_prns,
     gnsship_acq_result* results, float* grid);
 int gnsship_acq_num_bins(gnsship_acq* a, int* n_bins);
+/* Restart the non-coherent dwell accumulation (d_num_noncoherent_integrations_counter = 0 after a
+ * decision, pcps_acquisition.cc:783,835,860-864): the next gnsship_acq_run is dwell 1. */
+int gnsship_acq_reset_dwells(gnsship_acq* a);
 int gnsship_acq_destroy(gnsship_acq* a);
 
 /* Acquisition resampler (GNSS-SDR.use_acquisition_resampler; gnss_flowgraph.cc:1028-1113): the

@@ -382,7 +382,153 @@ public:
     }
     const char* last_error() const { return gnsship_last_error(dev_->ctx()); }
 
+    // ---- the block's buffering / decision state machine (general_work :902-1031, blocking mode,
+    // with the decision part of acquisition_core :760-864) ----
+    enum Acq_Event { ACQ_NONE = 0, ACQ_SUCCESS = 1, ACQ_FAIL = 2 };  // the channel messages (:339-390)
+    // set_active (:344-352 of the header) / set_state (:315-336)
+    void set_active(bool active) { active_ = active; }
+    void set_state(int state)
+    {
+        fsm_state_ = state;
+        if (state == 1) {
+            synchro_ = Acq_Outcome{};
+            active_ = true;
+        }
+    }
+    bool blocking_on_standby{false};  // Acq_Conf::blocking_on_standby
+    uint64_t sample_counter() const { return sample_counter_; }
+    const Acq_Outcome& gnss_synchro() const { return synchro_; }
+    // One general_work call over n gr_complex samples: returns how many it consumed (consume_each)
+    // and, when acquisition_core ran and decided, ACQ_SUCCESS / ACQ_FAIL in *event.
+    int general_work(const std::complex<float>* in, int n, Acq_Event* event)
+    {
+        *event = ACQ_NONE;
+        if (!active_) {
+            const int c = blocking_on_standby ? 0 : n;
+            sample_counter_ += static_cast<uint64_t>(c);
+            if (step_two_) {
+                fsm_state_ = 0;
+                active_ = true;
+            }
+            return c;
+        }
+        switch (fsm_state_) {
+        case 0: {
+            synchro_ = Acq_Outcome{};
+            fsm_state_ = 1;
+            buffer_count_ = 0;
+            if (blocking_on_standby) return 0;
+            sample_counter_ += static_cast<uint64_t>(n);
+            return n;
+        }
+        case 1: {
+            if (buffer_.size() != static_cast<size_t>(consumed_)) buffer_.assign(static_cast<size_t>(consumed_), std::complex<float>{});
+            const int inc = (n + buffer_count_ <= consumed_) ? n : consumed_ - buffer_count_;
+            std::copy(in, in + inc, buffer_.begin() + buffer_count_);
+            if (buffer_count_ >= consumed_) fsm_state_ = 2;  // checked before the increment, as :967-970
+            buffer_count_ += inc;
+            sample_counter_ += static_cast<uint64_t>(inc);
+            return inc;
+        }
+        default: {
+            decide(buffer_.data(), event);
+            buffer_count_ = 0;
+            return 0;
+        }
+        }
+    }
+
 private:
+    // acquisition_core's counter update, core and decision block (:623, :683-696, :760-864)
+    void decide(const std::complex<float>* in, Acq_Event* event)
+    {
+        counter_++;
+        gnsship_acq_result r{};
+        {
+            std::lock_guard<std::mutex> lk(dev_->mutex());
+            if (gnsship_acq_run(h_, in, GNSSHIP_FMT_CF32, 0, 1, &r, nullptr) != GNSSHIP_OK) return;
+        }
+        synchro_.Acq_delay_samples = r.acq_delay_samples - static_cast<double>(resampler_latency_);
+        synchro_.Acq_doppler_hz = static_cast<double>(r.doppler_hz);
+        synchro_.Acq_samplestamp_samples = static_cast<uint64_t>(std::rint(static_cast<double>(sample_counter_) * conf_.resampler_ratio));
+        synchro_.Acq_doppler_step = step_two_ ? static_cast<uint32_t>(conf_.doppler_step2) : static_cast<uint32_t>(conf_.doppler_step);
+        synchro_.test_statistics = r.test_statistic;
+        if (!step_two_) last_input_power_ = r.input_power;
+        synchro_.input_power = step_two_ ? last_input_power_ : r.input_power;
+        synchro_.peak = r.peak;
+        bool positive_acq = false;
+        const bool hit = r.test_statistic > threshold_;
+        auto to_step_one = [&]() {
+            const int step = doppler_step_ ? static_cast<int>(doppler_step_) : static_cast<int>(conf_.doppler_step);
+            std::lock_guard<std::mutex> lk(dev_->mutex());
+            gnsship_acq_set_grid(h_, conf_.doppler_max, step, doppler_center_);
+            step_two_ = false;
+        };
+        auto on_hit = [&]() {
+            if (conf_.make_2_steps) {
+                if (step_two_) {
+                    *event = ACQ_SUCCESS;
+                    positive_acq = true;
+                    to_step_one();
+                    fsm_state_ = 0;
+                } else {
+                    std::lock_guard<std::mutex> lk(dev_->mutex());
+                    gnsship_acq_set_grid_step2(h_, static_cast<float>(r.doppler_hz), conf_.doppler_step2, static_cast<int>(conf_.num_doppler_bins_step2),
+                        r.input_power);
+                    step_two_ = true;
+                    counter_ = 0;
+                    fsm_state_ = 0;
+                }
+                calculate_threshold();
+            } else {
+                *event = ACQ_SUCCESS;
+                positive_acq = true;
+                fsm_state_ = 0;
+            }
+        };
+        if (!conf_.bit_transition_flag) {
+            if (hit) {
+                active_ = false;
+                on_hit();
+            } else {
+                fsm_state_ = 1;
+            }
+            if (counter_ == conf_.max_dwells) {
+                if (fsm_state_ != 0) *event = ACQ_FAIL;
+                fsm_state_ = 0;
+                active_ = false;
+                if (step_two_) {
+                    to_step_one();
+                    calculate_threshold();
+                }
+            }
+        } else {
+            active_ = false;
+            if (hit) {
+                on_hit();
+            } else {
+                fsm_state_ = 0;
+                if (step_two_) {
+                    to_step_one();
+                    calculate_threshold();
+                }
+                *event = ACQ_FAIL;
+            }
+        }
+        if (counter_ == conf_.max_dwells || positive_acq || conf_.bit_transition_flag) counter_ = 0;
+        if (counter_ == 0) {
+            std::lock_guard<std::mutex> lk(dev_->mutex());
+            gnsship_acq_reset_dwells(h_);
+        }
+    }
+
+    bool active_ = false;
+    int fsm_state_ = 0;
+    int buffer_count_ = 0;
+    uint32_t counter_ = 0;
+    uint64_t sample_counter_ = 0;
+    std::vector<std::complex<float>> buffer_;
+    Acq_Outcome synchro_{};
     Acq_Conf conf_;
     std::shared_ptr<Device> dev_;
     gnsship_acq* h_ = nullptr;

@@ -241,6 +241,62 @@ static int acq_resampler_test()
     return ok ? 0 : 1;
 }
 
+// The block's general_work state machine (pcps_acquisition.cc:902-1031 + decisions :760-864) fed in
+// 700-sample pieces: PRN 12 present → ACQ_SUCCESS on the first dwell (samplestamp = one dwell);
+// PRN 20 absent with max_dwells = 3 → ACQ_FAIL after three non-coherent dwells.
+static int acq_fsm_test()
+{
+    const int fs = 2048000;
+    std::mt19937 gen(5);
+    std::normal_distribution<double> g(0.0, 1.0);
+    const int total = 20 * fs / 1000;
+    std::vector<std::complex<float>> sig(total);
+    const double amp = std::sqrt(2 * std::pow(10.0, 4.7) / fs);
+    float chips[1023];
+    orc_gps_l1_ca_code_gen_float(chips, 12, 0);
+    for (int i = 0; i < total; i++) {
+        const double t = i / static_cast<double>(fs);
+        const long c = static_cast<long>(std::floor((i - 700) / static_cast<double>(fs) * 1023000.0 * (1 + 1500.0 / 1575.42e6)));
+        const double cv = chips[((c % 1023) + 1023) % 1023];
+        sig[i] = std::complex<float>(amp * cv * std::cos(2 * M_PI * 1500.0 * t) + g(gen), amp * cv * std::sin(2 * M_PI * 1500.0 * t) + g(gen));
+    }
+    int failures = 0;
+    for (int prn : {12, 20}) {
+        gnsship::Acq_Conf conf;
+        conf.fs_in = fs;
+        conf.doppler_max = 5000;
+        conf.doppler_step = 500.0F;
+        conf.pfa = 0.01F;
+        conf.max_dwells = prn == 12 ? 1U : 3U;
+        gnsship::Pcps_Acquisition_Hip acq(conf);
+        const int n = acq.fft_size();
+        std::vector<float> code(2 * n);
+        orc_gps_l1_ca_code_gen_complex_sampled(code.data(), prn, fs, 0);
+        acq.set_local_code(reinterpret_cast<const std::complex<float>*>(code.data()));
+        acq.init();
+        acq.set_state(1);
+        int pos = 0, calls = 0;
+        gnsship::Pcps_Acquisition_Hip::Acq_Event ev = gnsship::Pcps_Acquisition_Hip::ACQ_NONE;
+        while (ev == gnsship::Pcps_Acquisition_Hip::ACQ_NONE && pos < total && calls < 10000) {
+            pos += acq.general_work(sig.data() + pos, std::min(700, total - pos), &ev);
+            calls++;
+        }
+        const auto& r = acq.gnss_synchro();
+        std::printf("acq fsm prn %d: event %d after %d calls, %d samples; delay %.1f doppler %.1f stamp %llu stat %.2f thr %.2f\n", prn,
+            static_cast<int>(ev), calls, pos, r.Acq_delay_samples, r.Acq_doppler_hz, static_cast<unsigned long long>(r.Acq_samplestamp_samples),
+            r.test_statistics, acq.threshold());
+        if (prn == 12) {
+            const bool ok = ev == gnsship::Pcps_Acquisition_Hip::ACQ_SUCCESS && pos == n && r.Acq_samplestamp_samples == static_cast<uint64_t>(n) &&
+                            std::fabs(r.Acq_delay_samples - 700.0) <= 2.0 && std::fabs(r.Acq_doppler_hz - 1500.0) <= 250.0;
+            if (!ok) failures++;
+        } else {
+            const bool ok = ev == gnsship::Pcps_Acquisition_Hip::ACQ_FAIL && pos == 3 * n && r.Acq_samplestamp_samples == static_cast<uint64_t>(3 * n);
+            if (!ok) failures++;
+        }
+    }
+    return failures;
+}
+
 int main(int argc, char** argv)
 {
     const char* mode = argc > 1 ? argv[1] : "corr";
@@ -253,6 +309,7 @@ int main(int argc, char** argv)
     }
     if (!std::strcmp(mode, "acq")) return acq_test();
     if (!std::strcmp(mode, "acqrs")) return acq_resampler_test();
+    if (!std::strcmp(mode, "acqfsm")) return acq_fsm_test();
     if (!std::strcmp(mode, "trk")) return trk_test();
     return corr_test();
 }

@@ -50,6 +50,15 @@ def test_acquisition_resampler_mirror(mirror_bin):
 
 
 @pytest.mark.gpu
+def test_acquisition_general_work_fsm_mirror(mirror_bin):
+    """Pcps_Acquisition_Hip::general_work: buffering states 0/1/2 and the dwell / decision logic of
+    pcps_acquisition.cc:902-1031, :760-864 (positive on a present PRN, negative after max_dwells)."""
+    r = subprocess.run([mirror_bin, "acqfsm"], capture_output=True, text=True, timeout=300)
+    print(r.stdout)
+    assert r.returncode == 0, r.stdout + r.stderr
+
+
+@pytest.mark.gpu
 def test_dll_pll_veml_tracking_mirror(mirror_bin):
     r = subprocess.run([mirror_bin, "trk"], capture_output=True, text=True, timeout=300)
     print(r.stdout)
