@@ -11,19 +11,21 @@ namespace gnsship {
 
 // First renormalisation block of replay segment seg of a job with nblk blocks (segments split at
 // the middle block; kAnchorSegments == 2).
-__device__ __forceinline__ int segment_block(int seg, int nblk)
+__device__ __forceinline__ int segment_block(int seg, int nblk, int n_segs = kAnchorSegments)
 {
-    return seg <= 0 ? 0 : (seg >= kAnchorSegments ? nblk : (nblk + 1) / 2);
+    // n_segs near-equal block ranges; for 2 segments the split is at (nblk + 1) / 2
+    return seg <= 0 ? 0 : (seg >= n_segs ? nblk : (nblk * seg + n_segs - 1) / n_segs);
 }
 
 // The reference rotator recursion of one job, stored at every renormalisation point — blocks of
 // segments [seg_lo, seg_hi).  Block k stores the renormalised q_k and the chain's next three phasors
 // q_k·inc, q_k·inc², q_k·inc³ (engine.h Anchor).  A later segment resumes from the stored q of the
 // block before it: the chain after a renormalisation depends only on q.
-__device__ __forceinline__ void replay_anchors(const DevJob& job, Anchor* __restrict__ anchors, int seg_lo, int seg_hi)
+__device__ __forceinline__ void replay_anchors(const DevJob& job, Anchor* __restrict__ anchors, int seg_lo, int seg_hi,
+    int n_segs = kAnchorSegments)
 {
     const int nblk = (job.n_samples + kRenorm - 1) / kRenorm;
-    const int kb = segment_block(seg_lo, nblk), ke = segment_block(seg_hi, nblk);
+    const int kb = segment_block(seg_lo, nblk, n_segs), ke = segment_block(seg_hi, nblk, n_segs);
     if (kb >= ke) return;
     Anchor* out = anchors + job.anchor_offset;
     typedef float f2v __attribute__((ext_vector_type(2)));

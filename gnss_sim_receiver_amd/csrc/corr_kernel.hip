@@ -53,12 +53,12 @@ __device__ unsigned long long* g_corr_prof = nullptr;
     } while (0)
 #endif
 
-__global__ void corr_anchor_kernel(const DevJob* __restrict__ jobs, int n_jobs, Anchor* __restrict__ anchors, int seg_lo, int seg_hi)
+__global__ void corr_anchor_kernel(const DevJob* __restrict__ jobs, int n_jobs, Anchor* __restrict__ anchors, int seg_lo, int seg_hi, int n_segs)
 {
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= n_jobs) return;
     const DevJob job = jobs[j];
-    replay_anchors(job, anchors, seg_lo, seg_hi);
+    replay_anchors(job, anchors, seg_lo, seg_hi, n_segs);
 }
 
 typedef float f2v_t __attribute__((ext_vector_type(2)));
@@ -354,12 +354,13 @@ __global__ __launch_bounds__(kCorrThreads, (corr_waves_per_simd<NT, IN_MARGIN>()
 #ifndef GNSSHIP_NO_REPLAY_PRIO
         __builtin_amdgcn_s_setprio(3);  // a latency-bound serial chain: first pick of its SIMD's issue slots
 #endif
-        const bool t1 = static_cast<int>(blockIdx.x) >= pf.task[0].n_blocks;
-        const ReplayTask& t = pf.task[t1 ? 1 : 0];
-        const int j = (blockIdx.x - (t1 ? pf.task[0].n_blocks : 0)) * kCorrThreads + threadIdx.x;
+        int ti = 0, base = 0;
+        while (ti + 1 < kAnchorRingMax && static_cast<int>(blockIdx.x) >= base + pf.task[ti].n_blocks) base += pf.task[ti++].n_blocks;
+        const ReplayTask& t = pf.task[ti];
+        const int j = (blockIdx.x - base) * kCorrThreads + threadIdx.x;
         if (j < t.n_jobs) {
             const DevJob pj = t.jobs[j];
-            replay_anchors(pj, t.anchors, t.seg_lo, t.seg_hi);
+            replay_anchors(pj, t.anchors, t.seg_lo, t.seg_hi, t.n_segs);
         }
         GNSSHIP_PROF_STAMP(5);
         return;
@@ -522,7 +523,8 @@ hipError_t launch_corr_batch(const void* samples, int fmt, const DevJob* jobs, i
     if (n_chunks <= 0) {
         for (const auto& t : pf.task) {
             if (t.n_blocks == 0) continue;
-            hipLaunchKernelGGL(corr_anchor_kernel, dim3((t.n_jobs + 63) / 64), dim3(64), 0, stream, t.jobs, t.n_jobs, t.anchors, t.seg_lo, t.seg_hi);
+            hipLaunchKernelGGL(corr_anchor_kernel, dim3((t.n_jobs + 63) / 64), dim3(64), 0, stream, t.jobs, t.n_jobs, t.anchors, t.seg_lo, t.seg_hi,
+                t.n_segs);
             hipError_t e = hipGetLastError();
             if (e != hipSuccess) return e;
         }
@@ -531,7 +533,8 @@ hipError_t launch_corr_batch(const void* samples, int fmt, const DevJob* jobs, i
     if (max_code_len < 1 || max_code_len > kMaxCodeLen) return hipErrorInvalidValue;
     hipError_t e = hipSuccess;
     if (stages & GNSSHIP_STAGE_ANCHORS) {
-        hipLaunchKernelGGL(corr_anchor_kernel, dim3((n_jobs + 63) / 64), dim3(64), 0, stream, jobs, n_jobs, anchors, 0, kAnchorSegments);
+        hipLaunchKernelGGL(corr_anchor_kernel, dim3((n_jobs + 63) / 64), dim3(64), 0, stream, jobs, n_jobs, anchors, 0, kAnchorSegments,
+            kAnchorSegments);
         e = hipGetLastError();
         if (e != hipSuccess) return e;
     }

@@ -107,16 +107,18 @@ inline int chunk_class(int n_taps, int in_margin)
 // A job's replay chain is split at its middle renormalisation block into kAnchorSegments
 // segments; segment s > 0 resumes from the anchor segment s − 1 stored (gnsship_batch_launch_pipelined2
 // spreads one batch's replay over two consecutive launches).
-constexpr int kAnchorSegments = 2;
+constexpr int kAnchorSegments = 2;     // the pair / three-batch ring (gnsship_batch_launch_pipelined2)
+constexpr int kAnchorRingMax = 4;      // gnsship_batch_launch_ring: up to 4 following batches, 4 segments
 struct ReplayTask {
     const DevJob* jobs;
     Anchor* anchors;
     int32_t n_jobs;
-    int32_t seg_lo, seg_hi;  // segments [seg_lo, seg_hi)
+    int32_t seg_lo, seg_hi;  // segments [seg_lo, seg_hi) of n_segs equal block ranges
+    int32_t n_segs;
     int32_t n_blocks;        // workgroups (set by launch_corr_batch)
 };
 struct AnchorPrefetch {
-    ReplayTask task[2];
+    ReplayTask task[kAnchorRingMax];
     int32_t n_blocks;        // all leading workgroups, a multiple of 8 (set by launch_corr_batch)
 };
 
