@@ -76,6 +76,9 @@ class AcqResult(ctypes.Structure):
 
 
 SYS_GPS_L1CA, SYS_GAL_E1, SYS_BDS_B1I = 0, 1, 2
+# rotator dot-product variant (include/gnsship.h GNSSHIP_ROTATOR_*, job flag bits GNSSHIP_JOB_*)
+ROTATOR_GENERIC, ROTATOR_AVX, ROTATOR_AUTO = 0, 1, -1
+JOB_HIGH_DYN, JOB_ROTATOR_AVX = 1, 2
 
 
 class TrkConf(ctypes.Structure):
@@ -97,7 +100,7 @@ class TrkConf(ctypes.Structure):
         ("extend_correlation_symbols", ctypes.c_int32), ("pll_bw_narrow_hz", ctypes.c_float), ("dll_bw_narrow_hz", ctypes.c_float),
         ("early_late_space_narrow_chips", ctypes.c_float), ("very_early_late_space_narrow_chips", ctypes.c_float),
         ("enable_fll_pull_in", ctypes.c_int32), ("enable_fll_steady_state", ctypes.c_int32),
-        ("high_dyn", ctypes.c_int32), ("smoother_length", ctypes.c_uint32),
+        ("high_dyn", ctypes.c_int32), ("smoother_length", ctypes.c_uint32), ("rotator", ctypes.c_int32),
     ]
 
     @classmethod
@@ -110,7 +113,7 @@ class TrkConf(ctypes.Structure):
                 max_code_lock_fail=50, max_carrier_lock_fail=5000, carrier_aiding=1, track_pilot=1, system=system,
                 extend_correlation_symbols=1, pll_bw_narrow_hz=5.0, dll_bw_narrow_hz=0.75, early_late_space_narrow_chips=0.15,
                 very_early_late_space_narrow_chips=0.5, enable_fll_pull_in=0, enable_fll_steady_state=0,
-                high_dyn=0, smoother_length=10)
+                high_dyn=0, smoother_length=10, rotator=ROTATOR_GENERIC)
         for k, v in kw.items():
             setattr(c, k, v)
         return c
@@ -157,6 +160,7 @@ _f = ctypes.c_float
 
 _SIGNATURES = {
     "gnsship_abi_version": ([], _i),
+    "gnsship_rotator_dispatch": ([ctypes.POINTER(_i)], _i),
     "gnsship_device_count": ([ctypes.POINTER(_i)], _i),
     "gnsship_ctx_create": ([_i, _vpp], _i),
     "gnsship_ctx_destroy": ([_vp], _i),
@@ -255,3 +259,11 @@ def check(rc: int, what: str, ctx=None) -> None:
 
 def fptr(a: np.ndarray):
     return a.ctypes.data_as(_f32p)
+
+
+def rotator_dispatch() -> int:
+    """The volk_gnsssdr rotator variant the reference would run on this host (gnsship_rotator_dispatch):
+    ROTATOR_GENERIC or ROTATOR_AVX.  Host-only: no device needed."""
+    v = ctypes.c_int(-1)
+    check(load().gnsship_rotator_dispatch(ctypes.byref(v)), "gnsship_rotator_dispatch")
+    return v.value

@@ -218,6 +218,7 @@ size_t fmt_bytes(int fmt)
 // ============================================================================ context / buffers
 extern "C" int gnsship_abi_version(void) { return GNSSHIP_ABI_VERSION; }
 
+
 extern "C" int gnsship_device_count(int* n)
 {
     if (!n) return GNSSHIP_E_INVAL;

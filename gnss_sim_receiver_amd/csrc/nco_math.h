@@ -18,4 +18,12 @@ __device__ __forceinline__ float hypotf_glibc(float x, float y)
     return static_cast<float>(__dsqrt_rn(__dadd_rn(__dmul_rn(dx, dx), __dmul_rn(dy, dy))));
 }
 
+// cos / sin of a float argument as the double-precision result rounded once to float: the
+// correctly rounded value except at rare double-rounding ties.  The reference's phasors come from
+// glibc cosf/sinf (std::cos(float), cexpf), which agree with this in ~99 % of arguments (glibc's
+// float routines are not correctly rounded, and its FMA and non-FMA variants differ between
+// hosts); the device's own single-precision cosf/sinf agree far less often.
+__device__ __forceinline__ float cos_f32_rn(float x) { return static_cast<float>(cos(static_cast<double>(x))); }
+__device__ __forceinline__ float sin_f32_rn(float x) { return static_cast<float>(sin(static_cast<double>(x))); }
+
 }  // namespace gnsship

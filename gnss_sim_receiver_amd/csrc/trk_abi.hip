@@ -7,6 +7,7 @@
 // device (trk_kernel.hip) between fixed-plan correlator launches.
 #include <cmath>
 #include <cstddef>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <vector>
@@ -69,6 +70,7 @@ struct gnsship_trk {
     bool high_dyn = false;
     HdPlan hd;
     TrkHist* hist_dev = nullptr;
+    bool force_rounds = false;  // GNSSHIP_TRK_ROUNDS=1: the round-based loop even where the persistent one applies
 };
 
 namespace {
@@ -308,7 +310,8 @@ extern "C" int gnsship_trk_create(gnsship_ctx* ctx, const gnsship_trk_conf* conf
     *out = nullptr;
     if (max_channels < 1 || conf->fs_in <= 0.0 || conf->vector_length < 1 || conf->cn0_samples < 1 || conf->cn0_samples > kTrkMaxCn0Samples ||
         conf->pll_filter_order < 2 || conf->pll_filter_order > 3 || conf->dll_filter_order < 1 || conf->dll_filter_order > 3 ||
-        (conf->high_dyn && conf->smoother_length > static_cast<uint32_t>(kTrkMaxSmoother)))
+        (conf->high_dyn && conf->smoother_length > static_cast<uint32_t>(kTrkMaxSmoother)) || conf->rotator < GNSSHIP_ROTATOR_AUTO ||
+        conf->rotator > GNSSHIP_ROTATOR_AVX)
         return fail(ctx, GNSSHIP_E_INVAL,
             "gnsship_trk_create: bad configuration (cn0_samples 1..64, pll order 2..3, dll order 1..3, smoother_length <= 64)");
     gnsship_trk* t = new (std::nothrow) gnsship_trk();
@@ -317,6 +320,12 @@ extern "C" int gnsship_trk_create(gnsship_ctx* ctx, const gnsship_trk_conf* conf
     if (!build_params(*conf, t->params)) {
         delete t;
         return fail(ctx, GNSSHIP_E_INVAL, "gnsship_trk_create: unknown system");
+    }
+    if (t->params.conf.rotator == GNSSHIP_ROTATOR_AUTO) gnsship_rotator_dispatch(&t->params.conf.rotator);
+    if (t->params.conf.high_dyn) t->params.conf.rotator = GNSSHIP_ROTATOR_GENERIC;  // only generic high-dynamics variants exist
+    {
+        const char* env = std::getenv("GNSSHIP_TRK_ROUNDS");  // A/B: force the round-based loop
+        t->force_rounds = env && env[0] == '1';
     }
     if (int rc = set_device(ctx)) {
         delete t;
@@ -557,7 +566,20 @@ extern "C" int gnsship_trk_run_dump(gnsship_trk* t, const void* sig, int fmt, in
     }
     HIP_TRY(ctx, hipMemsetAsync(t->ran_dev, 0, sizeof(int) * (max_rounds + 1), ctx->stream));
     const int nc = t->max_channels;
-    for (int r = 0; r <= max_rounds; r++) {
+    const bool avx = t->params.conf.rotator == GNSSHIP_ROTATOR_AVX;
+    const int code_cap = padded_code_quads(max_len) * 4;
+    const bool persist = !t->high_dyn && trk_persist_lds_bytes(t->params, code_cap, avx) <= kTrkPersistMaxLds && !(t->force_rounds && !avx);
+    if (avx && !persist) return fail(ctx, GNSSHIP_E_INVAL, "gnsship_trk_run: the AVX rotator needs the persistent loop (epoch too long for LDS)");
+    if (persist) {
+        // records of epochs a channel did not run stay zero (flags 0), as in the round-based loop
+        if (out) HIP_TRY(ctx, hipMemsetAsync(t->rec_dev, 0, sizeof(gnsship_trk_epoch) * nrec, ctx->stream));
+        if (dump) HIP_TRY(ctx, hipMemsetAsync(t->dump_dev, 0, sizeof(gnsship_trk_dump_record) * nrec, ctx->stream));
+        hipError_t e = launch_trk_persist(t->params_dev, t->params, t->chans_dev, nc, ctx->codes_dev, static_cast<int>(ctx->codes_host.size()),
+            code_cap, src, fmt, buffer_first_sample, n_buffer_samples, max_rounds, out ? t->rec_dev : nullptr, dump ? t->dump_dev : nullptr,
+            t->ran_dev, avx, ctx->stream);
+        if (e != hipSuccess) return hip_fail(ctx, e, "launch_trk_persist");
+    }
+    for (int r = 0; r <= max_rounds && !persist; r++) {
         const int consume = r > 0 ? 1 : 0, emit = r < max_rounds ? 1 : 0;
         gnsship_trk_epoch* rec = (out && r > 0) ? t->rec_dev + static_cast<size_t>(r - 1) * nc : nullptr;
         gnsship_trk_dump_record* drec = (dump && r > 0) ? t->dump_dev + static_cast<size_t>(r - 1) * nc : nullptr;

@@ -114,4 +114,13 @@ hipError_t launch_trk_step(const TrkParams* params, TrkChannel* chans, int n_cha
     uint64_t buf_first, int64_t buf_len, int consume, int emit, gnsship_trk_epoch* rec, gnsship_trk_dump_record* dump, int* ran_count,
     TrkHist* hist, HdJob* hd_jobs, HdChunk* hd_chunks, Anchor* anchors, hipStream_t stream);
 
+// Persistent closed loop (trk_persist.hip): one workgroup per channel runs all of its epochs in the
+// buffer within one launch (standard correlator only; not high_dyn).  code_cap_floats: LDS floats per
+// code replica (padded_code_quads(max code length) · 4).  LDS bytes of the dynamic region:
+size_t trk_persist_lds_bytes(const TrkParams& p, int code_cap_floats, bool avx);
+constexpr size_t kTrkPersistMaxLds = 150 * 1024;  // of the 160 KiB per CU, beside the static state
+hipError_t launch_trk_persist(const TrkParams* params_dev, const TrkParams& params, TrkChannel* chans, int n_chans, const CodeDesc* codes,
+    int n_codes, int code_cap_floats, const void* samples, int fmt, uint64_t buf_first, int64_t buf_len, int max_rounds, gnsship_trk_epoch* rec,
+    gnsship_trk_dump_record* dump, int* ran_count, bool avx, hipStream_t stream);
+
 }  // namespace gnsship

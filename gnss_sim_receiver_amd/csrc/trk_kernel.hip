@@ -17,493 +17,18 @@
 //   cn0_and_tracking_lock_status :972-1029, run_dll_pll :1065-1152, update_tracking_vars
 //   :1189-1260, save_correlation_results :1262-1350, acquire_secondary :925-970,
 //   general_work states 2 (:1789-1932) and 4 (:1971-2028).
-// The job derivation repeats derive_job (gnsship_abi.hip) with the device libm: the phasors
-// (cosf/sinf) may differ from glibc's in the last ulp, i.e. ~1e-7 in the correlations.
+// The job derivation repeats derive_job (gnsship_abi.hip) on the device: the phasors are the
+// double-precision cos/sin rounded to float (nco_math.h), glibc's cosf/sinf in ~99 % of epochs and
+// one ulp away otherwise.
 #include <cmath>
 
 #include "anchor_replay.h"
 #include "trk_engine.h"
+#include "trk_loop.h"
 
 namespace gnsship {
 
 namespace {
-
-// MATH_CONSTANTS.h:47-49: the reference's pi is the GNSS value 3.1415926535898
-constexpr double kGnssPi = 3.1415926535898;
-constexpr double kTwoPi = 2.0 * kGnssPi;
-constexpr double kHalfPi = kGnssPi / 2.0;
-
-// fll_diff_atan + phase_unwrap (tracking_discriminators.cc:27-41, 68-76)
-__device__ double fll_diff_atan(const float* s1, const float* s2, double t1, double t2)
-{
-    double d = static_cast<double>(__fsub_rn(atanf(__fdiv_rn(s2[1], s2[0])), atanf(__fdiv_rn(s1[1], s1[0]))));
-    if (isnan(d)) d = 0.0;
-    if (d >= kHalfPi)
-        d -= kGnssPi;
-    else if (d <= -kHalfPi)
-        d += kGnssPi;
-    return d / (t2 - t1);
-}
-
-__device__ float smooth(Smoother& s, float raw, float alpha, float one_minus_alpha, float min_value, float offset, int init_samples)
-{
-    float v;
-    if (s.initializing) {
-        s.counter++;
-        v = raw;
-        s.init_sum = __fadd_rn(s.init_sum, v);
-        if (s.counter == init_samples) {
-            s.old_value = __fdiv_rn(s.init_sum, static_cast<float>(s.counter));
-            if (s.old_value < __fadd_rn(min_value, offset)) {
-                s.counter = 0;
-                s.init_sum = 0.0f;
-            } else {
-                s.initializing = 0;
-            }
-        }
-    } else {
-        v = __fadd_rn(__fmul_rn(alpha, raw), __fmul_rn(one_minus_alpha, s.old_value));
-        s.old_value = v;
-    }
-    return v;
-}
-
-__device__ float cn0_m2m4(const float* prompt, int length, float coh_integration_time_s)
-{
-    float psig = 0.0f, m_2 = 0.0f, m_4 = 0.0f, aux;
-    const float n = static_cast<float>(length);
-    for (int i = 0; i < length; i++) {
-        psig = __fadd_rn(psig, fabsf(prompt[2 * i]));
-        aux = __fadd_rn(__fmul_rn(prompt[2 * i + 1], prompt[2 * i + 1]), __fmul_rn(prompt[2 * i], prompt[2 * i]));
-        m_2 = __fadd_rn(m_2, aux);
-        m_4 = __fadd_rn(m_4, __fmul_rn(aux, aux));
-    }
-    psig = __fdiv_rn(psig, n);
-    psig = __fmul_rn(psig, psig);
-    m_2 = __fdiv_rn(m_2, n);
-    m_4 = __fdiv_rn(m_4, n);
-    aux = sqrtf(__fsub_rn(__fmul_rn(__fmul_rn(2.0f, m_2), m_2), m_4));
-    const float snr = isnan(aux) ? __fdiv_rn(psig, __fsub_rn(m_2, psig)) : __fdiv_rn(aux, __fsub_rn(m_2, aux));
-    return __fsub_rn(__fmul_rn(10.0f, log10f(snr)), __fmul_rn(10.0f, log10f(coh_integration_time_s)));
-}
-
-__device__ float carrier_lock_detector(const float* prompt)  // called with length 1 (:989)
-{
-    const float si = prompt[0], sq = prompt[1];
-    const float nbp = __fadd_rn(__fmul_rn(si, si), __fmul_rn(sq, sq));
-    const float nbd = __fsub_rn(__fmul_rn(si, si), __fmul_rn(sq, sq));
-    return __fdiv_rn(nbd, nbp);
-}
-
-__device__ bool lock_status(const TrkParams& k, TrkChannel& c, double coh_integration_time_s)
-{
-    const int ns = k.conf.cn0_samples;
-    if (c.cn0_counter < ns) {
-        c.prompt_buf[2 * c.cn0_counter] = c.p[0];
-        c.prompt_buf[2 * c.cn0_counter + 1] = c.p[1];
-        c.cn0_counter++;
-        return true;
-    }
-    const int slot = c.cn0_counter % ns;
-    c.prompt_buf[2 * slot] = c.p[0];
-    c.prompt_buf[2 * slot + 1] = c.p[1];
-    c.cn0_counter++;
-    const float raw = cn0_m2m4(c.prompt_buf, ns, static_cast<float>(coh_integration_time_s));
-    c.cn0_db_hz = smooth(c.cn0_sm, raw, k.cn0_alpha, k.cn0_one_minus_alpha, k.cn0_min_value, k.cn0_offset, k.cn0_init_samples);
-    c.carrier_lock_test = smooth(c.lock_sm, carrier_lock_detector(c.prompt_buf), k.lock_alpha, k.lock_one_minus_alpha, k.lock_min_value,
-        k.lock_offset, k.lock_init_samples);
-    if (!c.pull_in) {
-        if (static_cast<double>(c.carrier_lock_test) < k.conf.carrier_lock_th)
-            c.carrier_fail++;
-        else if (c.carrier_fail > 0)
-            c.carrier_fail--;
-        if (c.cn0_db_hz < static_cast<float>(k.conf.cn0_min))
-            c.code_fail++;
-        else if (c.code_fail > 0)
-            c.code_fail--;
-    }
-    if (c.carrier_fail > k.conf.max_carrier_lock_fail || c.code_fail > k.conf.max_code_lock_fail) {
-        c.carrier_fail = 0;
-        c.code_fail = 0;
-        return false;
-    }
-    return true;
-}
-
-__device__ float loop_filter_apply(const TrkParams& k, TrkChannel& c, float x)
-{
-    const LoopSet& q = k.ls[c.narrow ? 1 + c.geo : 0];
-    float result = 0.0f;
-    for (int ii = 0; ii < q.lf_n_out; ii++) result = __fadd_rn(result, __fmul_rn(q.lf_out[ii], c.lf_outputs[(c.lf_idx + ii) % 4]));
-    c.lf_idx--;
-    if (c.lf_idx < 0) c.lf_idx += 4;
-    c.lf_inputs[c.lf_idx] = x;
-    for (int ii = 0; ii < q.lf_n_in; ii++) result = __fadd_rn(result, __fmul_rn(q.lf_in[ii], c.lf_inputs[(c.lf_idx + ii) % 4]));
-    c.lf_outputs[c.lf_idx] = result;
-    return result;
-}
-
-__device__ float carrier_filter(const TrkParams& k, TrkChannel& c, float fll, float pll, float T)
-{
-    const LoopSet& q = k.ls[c.narrow ? 1 + c.geo : 0];
-    if (k.fp_order == 3) {
-        c.fp_w = __fadd_rn(c.fp_w, __fmul_rn(T, __fadd_rn(__fmul_rn(q.fp_w0p3, pll), __fmul_rn(q.fp_w0f2, fll))));
-        const float inner = __fadd_rn(__fadd_rn(__fmul_rn(0.5f, c.fp_w), __fmul_rn(__fmul_rn(q.fp_a2, q.fp_w0f), fll)),
-            __fmul_rn(__fmul_rn(q.fp_a3, q.fp_w0p2), pll));
-        c.fp_x = __fadd_rn(c.fp_x, __fmul_rn(T, inner));
-        return __fadd_rn(__fmul_rn(0.5f, c.fp_x), __fmul_rn(__fmul_rn(q.fp_b3, q.fp_w0p), pll));
-    }
-    const float w_new = __fadd_rn(__fadd_rn(c.fp_w, __fmul_rn(__fmul_rn(pll, q.fp_w0p2), T)), __fmul_rn(__fmul_rn(fll, q.fp_w0f), T));
-    const float e = __fadd_rn(__fmul_rn(0.5f, __fadd_rn(w_new, c.fp_w)), __fmul_rn(__fmul_rn(q.fp_a2, q.fp_w0p), pll));
-    c.fp_w = w_new;
-    return e;
-}
-
-__device__ void run_dll_pll(const TrkParams& k, TrkChannel& c)
-{
-    double disc;
-    if (c.cloop)
-        disc = (c.p[0] != 0.0f) ? static_cast<double>(atanf(__fdiv_rn(c.p[1], c.p[0]))) : 0.0;
-    else
-        disc = static_cast<double>(atan2f(c.p[1], c.p[0]));  // gr::fast_atan2f restated as atan2f
-    c.carr_phase_error_hz = disc / kTwoPi;
-    // d_current_correlation_time_s: the code period, or extend × code period once extended
-    const float T = c.narrow ? k.sync[c.geo].T_ext : static_cast<float>(k.code_period);
-    if ((c.pull_in && k.conf.enable_fll_pull_in) || k.conf.enable_fll_steady_state) {  // :1080-1097
-        // d_current_correlation_time_s is a double: the code period, or (float)extend·(float)period
-        const double Td = c.narrow ? static_cast<double>(k.sync[c.geo].T_ext) : k.code_period;
-        const double fe = fll_diff_atan(c.p_old, c.p, 0.0, Td) / kTwoPi;
-        c.p_old[0] = c.p[0];
-        c.p_old[1] = c.p[1];
-        const float pll = (c.pull_in && k.conf.enable_fll_pull_in) ? 0.0f : static_cast<float>(c.carr_phase_error_hz);
-        c.carr_error_filt_hz = carrier_filter(k, c, static_cast<float>(fe), pll, T);
-    } else {
-        c.carr_error_filt_hz = carrier_filter(k, c, 0.0f, static_cast<float>(c.carr_phase_error_hz), T);
-    }
-    c.carrier_doppler_hz = c.carr_error_filt_hz;
-    if (k.veml) {
-        const double early = static_cast<double>(sqrtf(__fadd_rn(__fadd_rn(__fadd_rn(__fmul_rn(c.ve[0], c.ve[0]), __fmul_rn(c.ve[1], c.ve[1])),
-                                                                          __fmul_rn(c.e[0], c.e[0])),
-            __fmul_rn(c.e[1], c.e[1]))));
-        const double late = static_cast<double>(sqrtf(__fadd_rn(__fadd_rn(__fadd_rn(__fmul_rn(c.l[0], c.l[0]), __fmul_rn(c.l[1], c.l[1])),
-                                                                         __fmul_rn(c.vl[0], c.vl[0])),
-            __fmul_rn(c.vl[1], c.vl[1]))));
-        const double s = early + late;
-        c.code_error_chips = (s == 0.0) ? 0.0 : (early - late) / s;
-    } else {
-        const double pe = static_cast<double>(hypotf(c.e[0], c.e[1]));
-        const double pl = static_cast<double>(hypotf(c.l[0], c.l[1]));
-        const double s = pe + pl;
-        const float slope = k.conf.slope;
-        const float norm = __fdiv_rn(__fsub_rn(k.conf.y_intercept, __fmul_rn(slope, c.spc)), slope);
-        c.code_error_chips = (s == 0.0) ? 0.0 : static_cast<double>(norm) * (pe - pl) / s;
-    }
-    c.code_error_filt_chips = loop_filter_apply(k, c, static_cast<float>(c.code_error_chips));
-    c.code_freq_chips = k.code_chip_rate - c.code_error_filt_chips;
-    if (k.conf.carrier_aiding) c.code_freq_chips += c.carrier_doppler_hz * k.code_chip_rate / k.carrier_freq;
-}
-
-// high_dyn rate estimate (:1208-1221, :1241-1254): mean step of the newest smoother_length entries
-// minus the mean of the oldest, over the newest entries' samples; sums in the reference's order.
-__device__ double smoothed_rate(const TrkChannel& c, const TrkHist& h, const double* first, int L)
-{
-    const int cap = 2 * L;
-    double cp1 = 0.0, cp2 = 0.0, samples = 0.0;
-    for (int i = 0; i < L; i++) {
-        int a = c.hist_head + i;
-        if (a >= cap) a -= cap;
-        int b = c.hist_head + cap - i - 1;
-        if (b >= cap) b -= cap;
-        cp1 += first[a];
-        cp2 += first[b];
-        samples += static_cast<double>(h.samples[b]);
-    }
-    cp1 /= static_cast<double>(L);
-    cp2 /= static_cast<double>(L);
-    return (cp2 - cp1) / samples;
-}
-
-__device__ void update_tracking_vars(const TrkParams& k, TrkChannel& c, TrkHist* h)
-{
-    const double fs = k.conf.fs_in;
-    const double T_chip = 1.0 / c.code_freq_chips;
-    const double T_prn = T_chip * static_cast<double>(k.code_length_chips);
-    const double T_prn_samples = T_prn * fs;
-    c.K_blk_samples = T_prn_samples + c.rem_code_phase_samples;
-    c.current_prn_length_samples = static_cast<int32_t>(floor(c.K_blk_samples));
-    c.carrier_phase_step_rad = kTwoPi * c.carrier_doppler_hz / fs;
-    const double n = static_cast<double>(c.current_prn_length_samples);
-    c.code_phase_step_chips = c.code_freq_chips / fs;
-    if (h) {  // high_dyn: push_back on the ring (full: drop the oldest), rates once it is full
-        const int L = static_cast<int>(k.conf.smoother_length), cap = 2 * L;
-        int slot;
-        if (c.hist_count < cap) {
-            slot = c.hist_head + c.hist_count;
-            if (slot >= cap) slot -= cap;
-            c.hist_count++;
-        } else {
-            slot = c.hist_head;
-            c.hist_head = c.hist_head + 1 == cap ? 0 : c.hist_head + 1;
-        }
-        h->carr[slot] = c.carrier_phase_step_rad;
-        h->code[slot] = c.code_phase_step_chips;
-        h->samples[slot] = c.current_prn_length_samples;
-        if (c.hist_count == cap) {
-            c.carrier_phase_rate_step_rad = smoothed_rate(c, *h, h->carr, L);
-            c.code_phase_rate_step_chips = smoothed_rate(c, *h, h->code, L);
-        }
-    }
-    const double adv = c.carrier_phase_step_rad * n + 0.5 * c.carrier_phase_rate_step_rad * n * n;
-    c.rem_carr_phase_rad = __fadd_rn(c.rem_carr_phase_rad, static_cast<float>(adv));
-    c.rem_carr_phase_rad = static_cast<float>(fmod(static_cast<double>(c.rem_carr_phase_rad), kTwoPi));
-    c.acc_carrier_phase_rad -= adv;
-    c.rem_code_phase_samples = c.K_blk_samples - n;
-    c.rem_code_phase_chips = c.code_freq_chips * c.rem_code_phase_samples / fs;
-}
-
-__device__ __forceinline__ int bit_at(const uint32_t* bits, int i) { return (bits[i >> 5] >> (i & 31)) & 1; }
-
-__device__ void push_sign(const TrkParams& k, TrkChannel& c, float prompt_re)
-{
-    const int cap = k.sync[c.geo].secondary_len;
-    const uint32_t neg = prompt_re < 0.0f ? 1u : 0u;
-    if (c.sign_count == cap) {  // boost::circular_buffer::push_back on a full buffer drops the oldest
-        for (int w = 0; w < kTrkMaxSecondary / 32; w++) {
-            const uint32_t carry = (w + 1 < kTrkMaxSecondary / 32) ? (c.sign_bits[w + 1] & 1u) : 0u;
-            c.sign_bits[w] = (c.sign_bits[w] >> 1) | (carry << 31);
-        }
-        const int i = cap - 1;
-        c.sign_bits[i >> 5] = (c.sign_bits[i >> 5] & ~(1u << (i & 31))) | (neg << (i & 31));
-    } else {
-        const int i = c.sign_count++;
-        c.sign_bits[i >> 5] = (c.sign_bits[i >> 5] & ~(1u << (i & 31))) | (neg << (i & 31));
-    }
-}
-
-__device__ bool acquire_secondary(const TrkParams& k, TrkChannel& c)
-{
-    int corr = 0;
-    for (int i = 0; i < k.sync[c.geo].secondary_len; i++) {
-        const int neg = bit_at(c.sign_bits, i);
-        const int one = bit_at(k.sync[c.geo].secondary_bits, i);
-        corr += (neg ^ one) ? 1 : -1;  // +1 for (real < 0, '0') and (real ≥ 0, '1')
-    }
-    if (abs(corr) == k.sync[c.geo].secondary_len) {
-        c.pll_180 = corr < 0 ? 1 : 0;
-        return true;
-    }
-    return false;
-}
-
-__device__ void clear_tracking_vars(TrkChannel& c)
-{
-    c.p_data[0] = c.p_data[1] = 0.0f;
-    c.p_old[0] = c.p_old[1] = 0.0f;
-    c.carr_phase_error_hz = 0.0;
-    c.carr_error_filt_hz = 0.0;
-    c.code_error_chips = 0.0;
-    c.code_error_filt_chips = 0.0;
-    c.current_symbol = 0;
-    c.current_data_symbol = 0;
-    c.sign_count = 0;
-    c.carrier_phase_rate_step_rad = 0.0;  // :1182-1185
-    c.code_phase_rate_step_chips = 0.0;
-    c.hist_head = 0;
-    c.hist_count = 0;
-}
-
-__device__ __forceinline__ void cadd(float* acc, const float* v, float sgn)
-{
-    acc[0] = __fadd_rn(acc[0], __fmul_rn(sgn, v[0]));
-    acc[1] = __fadd_rn(acc[1], __fmul_rn(sgn, v[1]));
-}
-
-__device__ void zero_accu(TrkChannel& c)
-{
-    c.ve[0] = c.ve[1] = c.e[0] = c.e[1] = c.p[0] = c.p[1] = 0.0f;
-    c.l[0] = c.l[1] = c.vl[0] = c.vl[1] = 0.0f;
-}
-
-// One general_work call for the epoch that started at c.epoch_start; returns false when the
-// channel stops (loss of lock).
-// log_data (:1376-1466) at epoch start nir, after update_tracking_vars.
-__device__ void log_data(const TrkParams& k, const TrkChannel& c, const float* taps, const float* pdata, uint64_t nir, gnsship_trk_dump_record* d)
-{
-    if (!d) return;
-    const int eo = k.veml ? 2 : 0;
-    const float* prompt = k.track_pilot ? pdata : taps + eo + 2;
-    const double fs = k.conf.fs_in;
-    d->abs_VE = k.veml ? hypotf(c.ve[0], c.ve[1]) : 0.0f;
-    d->abs_E = hypotf(c.e[0], c.e[1]);
-    d->abs_P = hypotf(c.p[0], c.p[1]);
-    d->abs_L = hypotf(c.l[0], c.l[1]);
-    d->abs_VL = k.veml ? hypotf(c.vl[0], c.vl[1]) : 0.0f;
-    d->prompt_I = prompt[0];
-    d->prompt_Q = prompt[1];
-    d->PRN_start_sample_count = nir + static_cast<uint64_t>(c.current_prn_length_samples);
-    d->acc_carrier_phase_rad = static_cast<float>(c.acc_carrier_phase_rad);
-    d->carrier_doppler_hz = static_cast<float>(c.carrier_doppler_hz);
-    d->carrier_doppler_rate_hz = static_cast<float>(c.carrier_phase_rate_step_rad * fs * fs / kTwoPi);
-    d->code_freq_chips = static_cast<float>(c.code_freq_chips);
-    d->code_freq_rate_chips = static_cast<float>(c.code_phase_rate_step_chips * fs * fs);
-    d->carr_error_hz = static_cast<float>(c.carr_phase_error_hz);
-    d->carr_error_filt_hz = static_cast<float>(c.carr_error_filt_hz);
-    d->code_error_chips = static_cast<float>(c.code_error_chips);
-    d->code_error_filt_chips = static_cast<float>(c.code_error_filt_chips);
-    d->CN0_SNV_dB_Hz = c.cn0_db_hz;
-    d->carrier_lock_test = c.carrier_lock_test;
-    d->aux1 = static_cast<float>(c.rem_code_phase_samples);
-    d->aux2 = static_cast<double>(nir + static_cast<uint64_t>(c.current_prn_length_samples));
-    d->PRN = c.prn;
-}
-
-__device__ bool epoch_update(const TrkParams& k, TrkChannel& c, const float* taps, const float* pdata, gnsship_trk_epoch& rec, TrkHist* h,
-    gnsship_trk_dump_record* dump)
-{
-    const uint64_t nir = c.epoch_start;
-    const uint64_t fs_int = static_cast<uint64_t>(static_cast<int>(k.conf.fs_in));
-    rec.sample_counter = nir;
-    if (c.pull_in && static_cast<uint64_t>(k.conf.pull_in_time_s) < (nir - c.acq_sample_stamp) / fs_int) {
-        c.pull_in = 0;
-        c.carrier_fail = 0;
-        c.code_fail = 0;
-    }
-    const int eo = k.veml ? 2 : 0;
-    const int st = c.state;
-    bool loss = false;
-    if (st == 2) {
-        if (k.veml) {
-            c.ve[0] = taps[0];
-            c.ve[1] = taps[1];
-            c.vl[0] = taps[8];
-            c.vl[1] = taps[9];
-        }
-        c.e[0] = taps[eo];
-        c.e[1] = taps[eo + 1];
-        c.p[0] = taps[eo + 2];
-        c.p[1] = taps[eo + 3];
-        c.l[0] = taps[eo + 4];
-        c.l[1] = taps[eo + 5];
-        c.spc = k.conf.early_late_space_chips;
-        rec.prompt_i = static_cast<double>(c.p[0]);  // diagnostic: the epoch's prompt (no symbol flag in state 2)
-        rec.prompt_q = static_cast<double>(c.p[1]);
-        if (static_cast<uint64_t>(k.conf.bit_synchronization_time_limit_s) < (nir - c.acq_sample_stamp) / fs_int) c.carrier_fail = 300000;
-        if (!lock_status(k, c, k.code_period)) {
-            clear_tracking_vars(c);
-            c.state = 0;
-            loss = true;
-        } else {
-            bool next_state = false;
-            run_dll_pll(k, c);
-            update_tracking_vars(k, c, h);
-            log_data(k, c, taps, pdata, nir, dump);
-            rec.flags |= 16;
-            if (!c.pull_in) {
-                if (k.sync[c.geo].secondary || k.sync[c.geo].symbols_per_bit > 1) {
-                    push_sign(k, c, taps[eo + 2]);
-                    if (c.sign_count == k.sync[c.geo].secondary_len) next_state = acquire_secondary(k, c);
-                } else {
-                    next_state = true;
-                }
-            }
-            if (next_state) {
-                zero_accu(c);
-                c.p_data[0] = c.p_data[1] = 0.0f;
-                c.sign_count = 0;
-                c.current_symbol = 0;
-                c.current_data_symbol = 0;
-                if (k.sync[c.geo].extend > 1) {  // extended integration (:1890-1926): narrow loops and taps, state 3
-                    c.ext_count = 0;
-                    c.narrow = 1;
-                    c.spc = k.spc_n;
-                    c.state = 3;
-                } else {
-                    c.state = 4;
-                }
-            }
-        }
-    } else {
-        // save_correlation_results
-        float sgn = 1.0f;
-        if (k.sync[c.geo].secondary) {
-            sgn = bit_at(k.sync[c.geo].secondary_bits, c.current_symbol) ? -1.0f : 1.0f;
-            c.current_symbol = (c.current_symbol + 1) % k.sync[c.geo].secondary_len;
-        }
-        if (k.veml) {
-            cadd(c.ve, taps, sgn);
-            cadd(c.vl, taps + 8, sgn);
-        }
-        cadd(c.e, taps + eo, sgn);
-        cadd(c.p, taps + eo + 2, sgn);
-        cadd(c.l, taps + eo + 4, sgn);
-        const float* src = k.track_pilot ? pdata : taps + eo + 2;
-        if (k.sync[c.geo].symbols_per_bit > 1) {
-            if (k.sync[c.geo].data_secondary_len > 0) {
-                cadd(c.p_data, src, bit_at(k.sync[c.geo].data_secondary_bits, c.current_data_symbol) ? -1.0f : 1.0f);
-                c.current_data_symbol = (c.current_data_symbol + 1) % k.sync[c.geo].data_secondary_len;
-            } else {
-                cadd(c.p_data, src, 1.0f);
-                c.current_data_symbol = (c.current_data_symbol + 1) % k.sync[c.geo].symbols_per_bit;
-            }
-        } else {
-            c.p_data[0] = src[0];
-            c.p_data[1] = src[1];
-        }
-        c.cloop = k.track_pilot ? 0 : 1;
-        if (st == 3) {  // coherent integration (:1933-1970): accumulate, NCO advance only
-            update_tracking_vars(k, c, h);
-            if (c.current_data_symbol == 0) {
-                log_data(k, c, taps, pdata, nir, dump);
-                rec.flags |= 16;
-                rec.prompt_i = static_cast<double>(c.p_data[0]);
-                rec.prompt_q = static_cast<double>(c.p_data[1]);
-                rec.flags |= 1;
-                c.p_data[0] = c.p_data[1] = 0.0f;
-            }
-            c.ext_count++;
-            if (c.ext_count == k.sync[c.geo].extend - 1) {
-                c.ext_count = 0;
-                c.state = 4;
-            }
-        } else if (!lock_status(k, c, k.code_period * static_cast<double>(k.sync[c.geo].extend))) {
-            clear_tracking_vars(c);
-            c.state = 0;
-            loss = true;
-        } else {
-            run_dll_pll(k, c);
-            update_tracking_vars(k, c, h);
-            if (!c.acc_phase_init) {
-                c.acc_carrier_phase_rad = -static_cast<double>(c.rem_carr_phase_rad);
-                c.acc_phase_init = 1;
-            }
-            if (c.current_data_symbol == 0) {
-                log_data(k, c, taps, pdata, nir, dump);
-                rec.flags |= 16;
-                rec.prompt_i = static_cast<double>(c.p_data[0]);
-                rec.prompt_q = static_cast<double>(c.p_data[1]);
-                rec.flags |= 1;
-                c.p_data[0] = c.p_data[1] = 0.0f;
-            }
-            zero_accu(c);
-            if (k.sync[c.geo].extend > 1) c.state = 3;  // next coherent integration cycle
-        }
-    }
-    rec.state = st;
-    if (loss) rec.flags |= 2;
-    if (c.pll_180) rec.flags |= 4;
-    rec.code_phase_samples = c.rem_code_phase_samples;
-    rec.carrier_phase_rads = c.acc_carrier_phase_rad;
-    rec.carrier_doppler_hz = c.carrier_doppler_hz;
-    rec.cn0_db_hz = static_cast<double>(c.cn0_db_hz);
-    rec.carrier_lock_test = c.carrier_lock_test;
-    rec.code_freq_chips = c.code_freq_chips;
-    rec.rem_code_phase_chips = c.rem_code_phase_chips;
-    rec.rem_carr_phase_rad = c.rem_carr_phase_rad;
-    rec.prn_length_samples = c.current_prn_length_samples;
-    if (loss) return false;
-    c.nitems_read = nir + static_cast<uint64_t>(c.current_prn_length_samples);  // consume_each (:2061)
-    return true;
-}
 
 // derive_job (gnsship_abi.hip) for a tracking epoch; the plan fields of `j` are kept.
 __device__ void fill_job(DevJob& j, const TrkParams& k, const TrkChannel& c, int64_t offset, int code_id, int n_taps, const float* shifts)
@@ -511,8 +36,8 @@ __device__ void fill_job(DevJob& j, const TrkParams& k, const TrkChannel& c, int
     const float spcf = static_cast<float>(k.code_samples_per_chip);
     const float rem_carr = c.rem_carr_phase_rad;
     const float step = static_cast<float>(c.carrier_phase_step_rad);
-    const float p0r = cosf(rem_carr), p0i = -sinf(rem_carr);
-    const float incr = cosf(-step), inci = sinf(-step);
+    const float p0r = cos_f32_rn(rem_carr), p0i = -sin_f32_rn(rem_carr);
+    const float incr = cos_f32_rn(-step), inci = sin_f32_rn(-step);
     j.sample_offset = offset;
     j.n_samples = static_cast<int32_t>(k.conf.vector_length);
     j.code_id = code_id;
@@ -540,10 +65,10 @@ __device__ void fill_hd_job(HdJob& j, const TrkParams& k, const TrkChannel& c, i
     j.sample_offset = offset;
     j.n_samples = static_cast<int32_t>(k.conf.vector_length);
     j.n_taps = n_taps;
-    j.p0_re = cosf(rem_carr);
-    j.p0_im = -sinf(rem_carr);
-    j.inc_re = cosf(-step);
-    j.inc_im = sinf(-step);
+    j.p0_re = cos_f32_rn(rem_carr);
+    j.p0_im = -sin_f32_rn(rem_carr);
+    j.inc_re = cos_f32_rn(-step);
+    j.inc_im = sin_f32_rn(-step);
     j.dtheta = atan2(static_cast<double>(j.inc_im), static_cast<double>(j.inc_re));
     j.log_mag_inc = static_cast<float>(log(hypot(static_cast<double>(j.inc_re), static_cast<double>(j.inc_im))));
     j.rate_arg = atan2f(sinf(-rate), cosf(-rate));

@@ -1,0 +1,524 @@
+// trk_persist.hip — the closed DLL/PLL loop with one workgroup per channel for a whole run.
+//
+// dll_pll_veml_tracking::general_work (dll_pll_veml_tracking.cc:1728-2094) runs one epoch per call:
+// do_correlation_step (:1037-1062) → Cpu_Multicorrelator_Real_Codes (cpu_multicorrelator_real_codes.cc:
+// 103-126) → the loop update (trk_loop.h).  Epoch k+1's NCO depends on epoch k's correlations, so a
+// channel is a strictly serial chain of epochs, while channels are independent.  This kernel gives
+// every channel its own 256-thread workgroup that runs ALL of the channel's epochs in the IF buffer
+// inside one launch: no kernel boundary, no host round trip and no grid-wide synchronisation
+// between epochs.  Per epoch:
+//   1. thread 0 derives the correlator arguments from the channel state (do_correlation_step);
+//   2. wave 0 replays the reference's rotator recursion and publishes its anchors to LDS block by
+//      block, while waves 1-3 (and wave 0 once the replay is done) correlate every block whose
+//      anchor is published: the replay — the serial floor of the epoch — overlaps the correlation;
+//   3. the tap sums are reduced in LDS and thread 0 runs the loop update on the channel state,
+//      which lives in LDS for the whole run, and writes the epoch's record.
+//
+// Rotator variants (include/gnsship.h GNSSHIP_ROTATOR_*):
+//  * generic (volk_gnsssdr_32fc_32f_rotator_dot_prod_32fc_xn.h:66-98): one phasor, N dependent
+//    products per epoch, renormalised every 256 samples.  The replay is one lane; each 256-sample
+//    block is correlated with the block's exact anchors and the lane factor |inc|^j e^{ijΔ} (the
+//    batched correlator's scheme, corr_device.h correlate_block).
+//  * AVX (…:155-316, what volk_gnsssdr dispatches on AVX hosts): 16 phasors z_l advanced by
+//    dz = normalise(inc^16), renormalised every 64 iterations.  The replay is 16 lanes × N/16 steps
+//    (16× shorter than the generic chain); it publishes z_l at every renormalisation, and the
+//    correlating lane of (segment, l) continues that lane's chain itself — the same float products
+//    in the same order, so every phasor is bit-identical to the reference's.
+//
+// High-dynamics tracking and epochs too long for LDS stay on the round-based path (trk_kernel.hip).
+#include "corr_device.h"
+#include "trk_engine.h"
+#include "trk_loop.h"
+
+#pragma clang fp contract(off)
+
+namespace gnsship {
+namespace {
+
+constexpr int kPThreads = 256;
+constexpr int kPWaves = kPThreads / kWave;
+constexpr int kAvxLanes = 16;  // phasors of the AVX rotator (volk_gnsssdr_32fc_32f_rotator_dot_prod_32fc_xn.h:199-213)
+constexpr int kAvxSeg = 64;    // its renormalisation period in 16-sample iterations (:265-272)
+
+// The epoch being correlated (LDS): the reference's call arguments as a DevJob plus the AVX step.
+struct PEpoch {
+    DevJob job;
+    float dz_re, dz_im;  // normalise(inc^16) (AVX)
+    int32_t runnable;
+    int32_t in_margin;   // every chip index of the epoch lies in the padded LDS replica
+    int32_t published;   // anchors ready: generic blocks, or AVX segments (S + 1 = all, tail included)
+    int32_t next_task;   // work dealer of the correlating waves
+    float red[kPWaves][2 * (kMaxTaps + 1)];
+};
+
+// Complex product rounded exactly as the reference's written-out (ac − bd, ad + bc): two packed
+// products and one packed add, no contraction (fl(x + fl(−y)) ≡ fl(x − y)).
+__device__ __forceinline__ f2 cmul_exact(f2 a, f2 b)
+{
+    const f2 t = f2{a.x, a.x} * b;
+    const f2 u = f2{a.y, a.y} * f2{-b.y, b.x};
+    return t + u;
+}
+
+// _mm256_complexnormalise_ps (volk_gnsssdr_avx_intrinsics.h:56-63): z / sqrt(re² + im²), IEEE sqrt
+// and division.
+__device__ __forceinline__ f2 normalise_avx(f2 z)
+{
+    const float m = __fsqrt_rn(__fadd_rn(__fmul_rn(z.x, z.x), __fmul_rn(z.y, z.y)));
+    return f2{__fdiv_rn(z.x, m), __fdiv_rn(z.y, m)};
+}
+
+__device__ __forceinline__ void publish(int32_t* p, int v) { __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP); }
+
+__device__ __forceinline__ void wait_published(int32_t* p, int need)
+{
+    while (__hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < need) __builtin_amdgcn_s_sleep(1);
+}
+
+// Next task index for the whole wave (lane 0 draws, everyone gets it as a uniform value).
+__device__ __forceinline__ int deal(int32_t* next, int lane)
+{
+    int v = 0;
+    if (lane == 0) v = __hip_atomic_fetch_add(next, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    return __builtin_amdgcn_readfirstlane(__shfl(v, 0, kWave));
+}
+
+// AVX geometry of an N-sample epoch: M = N/16 iterations; segment 0 = iteration 0, segment s ≥ 1 =
+// iterations [64(s−1)+1, 64s] ∩ [0, M); the N mod 16 tail runs serially after them.
+__device__ __forceinline__ int avx_segments(int M) { return M <= 1 ? 1 : 1 + (M - 1 + kAvxSeg - 1) / kAvxSeg; }
+
+// ---- replays ---------------------------------------------------------------------------------
+// Generic (one lane): the anchors of every 256-sample block, as replay_anchors (anchor_replay.h).
+__device__ void replay_generic(const DevJob& job, Anchor* A, int nblk, int32_t* published)
+{
+    const f2 inc = f2{job.inc_re, job.inc_im};
+    f2 p = f2{job.p0_re, job.p0_im};
+    for (int k = 0; k < nblk; k++) {
+        const float m = hypotf_glibc(p.x, p.y);  // sample 256k uses p; then p /= |p| (:86-92)
+        p = f2{__fdiv_rn(p.x, m), __fdiv_rn(p.y, m)};
+        Anchor a;
+        a.p[0] = p.x;
+        a.p[1] = p.y;
+#pragma unroll
+        for (int s = 1; s <= 16; s++) {
+            p = cmul_exact(p, inc);
+            if (s < 4) {
+                a.p[2 * s] = p.x;
+                a.p[2 * s + 1] = p.y;
+            }
+        }
+        A[k] = a;
+        publish(published, k + 1);
+        if (k + 1 < nblk) {
+            for (int s0 = 16; s0 < kRenorm; s0 += 16) {
+#pragma unroll
+                for (int s = 0; s < 16; s++) p = cmul_exact(p, inc);
+            }
+        }
+    }
+}
+
+// AVX (lanes 0..15 = phasor l): Z[s·16 + l] = the phasor lane l starts segment s with; T[j] = the
+// tail phasor of sample 16M + j.  The initial phasors are the generic chain phase·inc^l (:204-208);
+// dz = normalise(inc^16) (:215-225); after iteration m's update, renormalise when m ≡ 0 mod 64.
+__device__ void replay_avx(const PEpoch& ep, f2* Z, f2* T, int N, int lane, int32_t* published)
+{
+    const int M = N / kAvxLanes, S = avx_segments(M);
+    const f2 inc = f2{ep.job.inc_re, ep.job.inc_im};
+    const f2 dz = f2{ep.dz_re, ep.dz_im};
+    f2 z = f2{ep.job.p0_re, ep.job.p0_im};
+    for (int i = 0; i < kAvxLanes - 1; i++)
+        if (i < lane) z = cmul_exact(z, inc);
+    Z[lane] = z;
+    if (lane == 0) publish(published, 1);
+    for (int m = 0; m < M; m++) {
+        z = cmul_exact(z, dz);
+        if (m % kAvxSeg == 0) {  // wave-uniform
+            z = normalise_avx(z);
+            const int s = m / kAvxSeg + 1;
+            if (s < S) {
+                Z[s * kAvxLanes + lane] = z;
+                if (lane == 0) publish(published, s + 1);
+            }
+        }
+    }
+    if (lane == 0) {  // z0 = normalise(z0) after the loop, then the serial tail (:286-304)
+        f2 t = normalise_avx(z);
+        for (int j = 0; j < N - kAvxLanes * M; j++) {
+            T[j] = t;
+            t = cmul_exact(t, inc);
+        }
+        publish(published, S + 1);
+    }
+}
+
+// ---- correlation -------------------------------------------------------------------------------
+// Generic: blocks in publication order, one per wave step (64 lanes × 4 samples), with the block's
+// exact anchor and, once per epoch, the lane factor (corr_device.h correlate_block).
+template <int FMT, int NT, bool DATA, bool IN_MARGIN>
+__device__ void consume_generic(PEpoch& ep, const Anchor* A, i4v span, int N, const float* code0, const float* code1, int L, int lane,
+    f2 (&acc)[NT + 1])
+{
+    const DevJob& job = ep.job;
+    const int nblk = (N + kRenorm - 1) / kRenorm;
+    ChunkDesc ch;
+    ch.job = 0;
+    ch.start = 0;
+    ch.len = N;
+    ch.code_len = L;
+    ch.code = nullptr;
+    float shifts[NT];
+#pragma unroll
+    for (int t = 0; t < NT; t++) shifts[t] = job.shifts[t];
+    const float zero_shift[1] = {0.0f};
+    for (;;) {
+        const int kb = deal(&ep.next_task, lane);
+        if (kb >= nblk) break;
+        f2 x[kLaneSamples];
+        load_any<FMT>(span, lane, kb, N, x);  // in flight while the anchor is awaited
+        wait_published(&ep.published, kb + 1);
+        const Anchor a = A[kb];
+        f2 ap[NT], ad[1];
+#pragma unroll
+        for (int t = 0; t < NT; t++) ap[t] = f2{0.0f, 0.0f};
+        ad[0] = f2{0.0f, 0.0f};
+        if ((kb + 1) * kRenorm <= N) {
+            correlate_block<NT, IN_MARGIN, true>(job, ch, a, shifts, code0, L, lane, kb, x, ap);
+            if constexpr (DATA) correlate_block<1, IN_MARGIN, true>(job, ch, a, zero_shift, code1, L, lane, kb, x, ad);
+        } else {
+            correlate_block<NT, IN_MARGIN, false>(job, ch, a, shifts, code0, L, lane, kb, x, ap);
+            if constexpr (DATA) correlate_block<1, IN_MARGIN, false>(job, ch, a, zero_shift, code1, L, lane, kb, x, ad);
+        }
+        for (int t = 0; t < NT; t++) acc[t] += ap[t];
+        if constexpr (DATA) acc[NT] += ad[0];
+    }
+}
+
+// Chip index of tap shift `sh` at sample n: floor(step·(float)n + shift − rem), each operation
+// rounded in the reference's order (volk_gnsssdr_32f_xn_resampler_32f_xn.h:63-80).
+template <bool IN_MARGIN>
+__device__ __forceinline__ float code_at(const float* code, int L, float sn, float sh, float rem)
+{
+    int i = cvt_floor_i32(__fsub_rn(__fadd_rn(sn, sh), rem));
+    if constexpr (!IN_MARGIN) i = wrap_index(i, L);
+    return code[i];
+}
+
+// AVX: task g = segments 4g..4g+3 × the 16 phasors (64 lanes: lane = 16·(s − 4g) + l), each lane
+// continuing its phasor's chain over the segment's ≤ 64 iterations (sample 16m + l at iteration m);
+// the task after the last group correlates the N mod 16 tail samples.
+template <int FMT, int NT, bool DATA, bool IN_MARGIN>
+__device__ void consume_avx(PEpoch& ep, const f2* Z, const f2* T, i4v span, int N, const float* code0, const float* code1, int L, int lane,
+    f2 (&acc)[NT + 1])
+{
+    const DevJob& job = ep.job;
+    const int M = N / kAvxLanes, S = avx_segments(M);
+    const int n_groups = (S + 3) / 4, tail = N - kAvxLanes * M;
+    const int n_tasks = n_groups + (tail > 0 ? 1 : 0);
+    const f2 dz = f2{ep.dz_re, ep.dz_im};
+    const float step = job.code_step, rem = job.rem_code;
+    float shifts[NT];
+#pragma unroll
+    for (int t = 0; t < NT; t++) shifts[t] = job.shifts[t];
+    constexpr int SB = sample_bytes<FMT>();
+    for (;;) {
+        const int g = deal(&ep.next_task, lane);
+        if (g >= n_tasks) break;
+        if (g == n_groups) {  // the serial tail (:292-304)
+            wait_published(&ep.published, S + 1);
+            if (lane < tail) {
+                const int n = kAvxLanes * M + lane;
+                const f2 x = load_sample<FMT>(span, n * SB, 0);
+                const f2 r = cmul_pk2(x, T[lane]);
+                const float sn = __fmul_rn(step, static_cast<float>(n));
+#pragma unroll
+                for (int t = 0; t < NT; t++) {
+                    const float c = code_at<IN_MARGIN>(code0, L, sn, shifts[t], rem);
+                    acc[t] = __builtin_elementwise_fma(r, f2{c, c}, acc[t]);
+                }
+                if constexpr (DATA) {
+                    const float c = code_at<IN_MARGIN>(code1, L, sn, 0.0f, rem);
+                    acc[NT] = __builtin_elementwise_fma(r, f2{c, c}, acc[NT]);
+                }
+            }
+            continue;
+        }
+        const int s = 4 * g + (lane >> 4), l = lane & (kAvxLanes - 1);
+        const bool active = s < S;
+        const int m_lo = s == 0 ? 0 : kAvxSeg * (s - 1) + 1;
+        int cnt = active ? ((s == 0 ? (M > 0 ? 1 : 0) : (M < kAvxSeg * s + 1 ? M : kAvxSeg * s + 1) - m_lo)) : 0;
+        cnt = cnt < 0 ? 0 : cnt;
+        int cmax = cnt;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) cmax = max(cmax, __shfl_xor(cmax, o, kWave));
+        cmax = __builtin_amdgcn_readfirstlane(cmax);
+        wait_published(&ep.published, (4 * g + 4 < S ? 4 * g + 4 : S));
+        f2 z = active ? Z[(active ? s : 0) * kAvxLanes + l] : f2{0.0f, 0.0f};
+        // sample n = 16m + l: lane voffset advances by 16 samples per iteration
+        const int v0 = (kAvxLanes * m_lo + l) * SB;
+        constexpr int kPre = 4;
+        f2 xa[kPre], xb[kPre];
+#pragma unroll
+        for (int u = 0; u < kPre; u++) xa[u] = load_sample<FMT>(span, v0 + u * kAvxLanes * SB, 0);
+        for (int i0 = 0; i0 < cmax; i0 += kPre) {
+#pragma unroll
+            for (int u = 0; u < kPre; u++) xb[u] = load_sample<FMT>(span, v0 + (i0 + kPre + u) * kAvxLanes * SB, 0);
+#pragma unroll
+            for (int u = 0; u < kPre; u++) {
+                const int i = i0 + u;
+                // past the segment: weight 0, and the chip index of a sample inside the epoch (the
+                // padded replica covers [0, N) only; a product 0·code[far] could meet a NaN)
+                const bool on = i < cnt;
+                const f2 r = on ? cmul_pk2(xa[u], z) : f2{0.0f, 0.0f};
+                z = cmul_exact(z, dz);
+                const int n = on ? kAvxLanes * (m_lo + i) + l : 0;
+                const float sn = __fmul_rn(step, static_cast<float>(n));
+#pragma unroll
+                for (int t = 0; t < NT; t++) {
+                    const float c = code_at<IN_MARGIN>(code0, L, sn, shifts[t], rem);
+                    acc[t] = __builtin_elementwise_fma(r, f2{c, c}, acc[t]);
+                }
+                if constexpr (DATA) {
+                    const float c = code_at<IN_MARGIN>(code1, L, sn, 0.0f, rem);
+                    acc[NT] = __builtin_elementwise_fma(r, f2{c, c}, acc[NT]);
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < kPre; u++) xa[u] = xb[u];
+        }
+    }
+}
+
+// do_correlation_step's arguments for the epoch at c.nitems_read (derive_job on the device; the
+// generic lane factor needs arg/|inc| in double, the AVX path needs dz instead).
+template <bool AVX>
+__device__ void derive_epoch(PEpoch& ep, const TrkParams& k, const TrkChannel& c, int64_t off, int L)
+{
+    const int NT = k.n_taps;
+    const float* sh = c.narrow ? k.shifts_n : k.shifts;
+    DevJob& j = ep.job;
+    const float spcf = static_cast<float>(k.code_samples_per_chip);
+    const float rem_carr = c.rem_carr_phase_rad;
+    const float step = static_cast<float>(c.carrier_phase_step_rad);
+    j.sample_offset = off;
+    j.n_samples = static_cast<int32_t>(k.conf.vector_length);
+    j.code_id = c.code_id;
+    j.n_taps = NT;
+    j.p0_re = cos_f32_rn(rem_carr);
+    j.p0_im = -sin_f32_rn(rem_carr);
+    j.inc_re = cos_f32_rn(-step);
+    j.inc_im = sin_f32_rn(-step);
+    j.rem_code = __fmul_rn(static_cast<float>(c.rem_code_phase_chips), spcf);
+    j.code_step = __fmul_rn(static_cast<float>(c.code_phase_step_chips), spcf);
+    for (int t = 0; t < kMaxTaps; t++) j.shifts[t] = t < NT ? sh[t] : 0.0f;
+    if constexpr (AVX) {
+        f2 d = f2{j.inc_re, j.inc_im};
+        for (int q = 0; q < 4; q++) d = cmul_exact(d, d);  // dz *= dz four times (:221-225)
+        d = normalise_avx(d);
+        ep.dz_re = d.x;
+        ep.dz_im = d.y;
+    } else {
+        j.dtheta = atan2(static_cast<double>(j.inc_im), static_cast<double>(j.inc_re));
+        j.log_mag_inc = static_cast<float>(log(hypot(static_cast<double>(j.inc_re), static_cast<double>(j.inc_im))));
+    }
+    // chip-index range (monotone in n): inside the padded replica the modulo is skipped (the data
+    // prompt's shift 0 lies inside the taps' range)
+    float smin = 0.0f, smax = 0.0f;
+    for (int t = 0; t < NT; t++) {
+        smin = fminf(smin, j.shifts[t]);
+        smax = fmaxf(smax, j.shifts[t]);
+    }
+    const double span = static_cast<double>(j.code_step) * static_cast<double>(j.n_samples > 0 ? j.n_samples - 1 : 0);
+    const double lo = fmin(0.0, span) + smin - j.rem_code - 2.0;
+    const double hi = fmax(0.0, span) + smax - j.rem_code + 2.0;
+    ep.in_margin = (isfinite(lo) && isfinite(hi) && lo >= -kCodeMargin && hi < static_cast<double>(L + kCodeMargin)) ? 1 : 0;
+}
+
+// Stage a padded code replica (engine.h padded_code_quads) in LDS.
+__device__ void stage_code(float* dst, const CodeDesc& cd)
+{
+    const int nq = padded_code_quads(cd.len);
+    const float4* src = reinterpret_cast<const float4*>(cd.ptr - kCodeMargin);
+    float4* d4 = reinterpret_cast<float4*>(dst);
+    for (int q = threadIdx.x; q < nq; q += kPThreads) d4[q] = src[q];
+}
+
+template <int FMT, int NT, bool DATA, bool AVX>
+__global__ __launch_bounds__(kPThreads) void trk_persist_kernel(const TrkParams* __restrict__ pk, TrkChannel* __restrict__ chans,
+    const CodeDesc* __restrict__ codes, int n_codes, const void* __restrict__ samples, uint64_t buf_first, int64_t buf_len, int max_rounds,
+    int n_chans, int code_cap_floats, gnsship_trk_epoch* __restrict__ rec, gnsship_trk_dump_record* __restrict__ dump, int* __restrict__ ran_count)
+{
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    __shared__ TrkChannel sc;
+    __shared__ PEpoch ep;
+    __shared__ int32_t skip;
+    const int ch = blockIdx.x;
+    const int tid = threadIdx.x, lane = tid & (kWave - 1), wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const TrkParams& k = *pk;
+    {
+        const int* src = reinterpret_cast<const int*>(chans + ch);
+        int* dst = reinterpret_cast<int*>(&sc);
+        for (int i = tid; i < static_cast<int>(sizeof(TrkChannel) / 4); i += kPThreads) dst[i] = src[i];
+    }
+    __syncthreads();
+    if (tid == 0) {
+        const bool tracking = sc.state == 2 || sc.state == 3 || sc.state == 4;
+        const bool codes_ok = sc.code_id >= 0 && sc.code_id < n_codes && codes[sc.code_id].ptr && codes[sc.code_id].len > 0 &&
+                              padded_code_quads(codes[sc.code_id].len) * 4 <= code_cap_floats &&
+                              (!DATA || (sc.data_code_id >= 0 && sc.data_code_id < n_codes && codes[sc.data_code_id].ptr &&
+                                            codes[sc.data_code_id].len == codes[sc.code_id].len));
+        skip = (tracking && codes_ok) ? 0 : 1;
+    }
+    __syncthreads();
+    if (skip) return;  // idle channel: its state is untouched
+    float* code0 = lds;
+    float* code1 = lds + code_cap_floats;
+    float* anc = lds + (DATA ? 2 : 1) * code_cap_floats;
+    stage_code(code0, codes[sc.code_id]);
+    if constexpr (DATA) stage_code(code1, codes[sc.data_code_id]);
+    const int L = codes[sc.code_id].len;
+    const float* c0 = code0 + kCodeMargin;
+    const float* c1 = code1 + kCodeMargin;
+    const int N = static_cast<int>(k.conf.vector_length);
+    Anchor* A = reinterpret_cast<Anchor*>(anc);
+    f2* Z = reinterpret_cast<f2*>(anc);
+    f2* T = Z + (avx_segments(N / kAvxLanes) + 1) * kAvxLanes;
+    for (int e = 0; e < max_rounds; e++) {
+        if (tid == 0) {
+            const uint64_t vl = k.conf.vector_length;
+            const bool runnable = (sc.state == 2 || sc.state == 3 || sc.state == 4) && sc.nitems_read >= buf_first &&
+                                  sc.nitems_read + vl <= buf_first + static_cast<uint64_t>(buf_len);
+            ep.runnable = runnable ? 1 : 0;
+            if (runnable) {
+                derive_epoch<AVX>(ep, k, sc, static_cast<int64_t>(sc.nitems_read - buf_first), L);
+                sc.epoch_start = sc.nitems_read;
+            }
+            ep.published = 0;
+            ep.next_task = 0;
+        }
+        __syncthreads();  // also: the code replicas are staged (first epoch)
+        if (!ep.runnable) break;
+        const i4v span = sample_span<FMT>(samples, ep.job.sample_offset, N);
+        f2 acc[NT + 1];
+#pragma unroll
+        for (int t = 0; t <= NT; t++) acc[t] = f2{0.0f, 0.0f};
+        if constexpr (AVX) {
+            if (wave == 0 && lane < kAvxLanes) replay_avx(ep, Z, T, N, lane, &ep.published);
+            if (ep.in_margin)
+                consume_avx<FMT, NT, DATA, true>(ep, Z, T, span, N, c0, c1, L, lane, acc);
+            else
+                consume_avx<FMT, NT, DATA, false>(ep, Z, T, span, N, c0, c1, L, lane, acc);
+        } else {
+            if (wave == 0 && lane == 0) replay_generic(ep.job, A, (N + kRenorm - 1) / kRenorm, &ep.published);
+            if (ep.in_margin)
+                consume_generic<FMT, NT, DATA, true>(ep, A, span, N, c0, c1, L, lane, acc);
+            else
+                consume_generic<FMT, NT, DATA, false>(ep, A, span, N, c0, c1, L, lane, acc);
+            // anchor frame → sample frame: × E_{4·lane} (corr_kernel.hip)
+            const f2 er = lane_rotation(ep.job, kLaneSamples * lane);
+            const f2 esw = f2{-er.y, er.x};
+#pragma unroll
+            for (int t = 0; t <= NT; t++) acc[t] = cmul_pk(acc[t], er, esw);
+        }
+        constexpr int kOut = NT + (DATA ? 1 : 0);
+#pragma unroll
+        for (int t = 0; t < kOut; t++) {
+            const float sr = wave_sum(acc[t].x), si = wave_sum(acc[t].y);
+            if (lane == 0) {
+                ep.red[wave][2 * t] = sr;
+                ep.red[wave][2 * t + 1] = si;
+            }
+        }
+        __syncthreads();
+        if (tid == 0) {
+            float taps[2 * kMaxTaps], pdata[2];
+            for (int v = 0; v < 2 * kMaxTaps; v++) taps[v] = 0.0f;
+            for (int v = 0; v < 2 * NT; v++) {
+                float s = 0.0f;
+                for (int w = 0; w < kPWaves; w++) s += ep.red[w][v];
+                taps[v] = s;
+            }
+            pdata[0] = pdata[1] = 0.0f;
+            if constexpr (DATA) {
+                for (int w = 0; w < kPWaves; w++) {
+                    pdata[0] += ep.red[w][2 * NT];
+                    pdata[1] += ep.red[w][2 * NT + 1];
+                }
+            }
+            gnsship_trk_epoch r = {};
+            r.flags = 8;
+            gnsship_trk_dump_record dr;
+            epoch_update(k, sc, taps, DATA ? pdata : taps, r, nullptr, dump ? &dr : nullptr);
+            const size_t slot = static_cast<size_t>(e) * n_chans + ch;
+            if (rec) rec[slot] = r;
+            if (dump && (r.flags & 16)) dump[slot] = dr;
+            atomicAdd(ran_count + e, 1);
+        }
+        __syncthreads();
+    }
+    if (tid == 0) sc.ran = 0;
+    __syncthreads();
+    {
+        const int* src = reinterpret_cast<const int*>(&sc);
+        int* dst = reinterpret_cast<int*>(chans + ch);
+        for (int i = tid; i < static_cast<int>(sizeof(TrkChannel) / 4); i += kPThreads) dst[i] = src[i];
+    }
+}
+
+}  // namespace
+
+// LDS bytes of the persistent kernel's dynamic region for an engine (codes + anchors), or 0 when the
+// configuration needs the round-based path.
+size_t trk_persist_lds_bytes(const TrkParams& p, int code_cap_floats, bool avx)
+{
+    const int N = static_cast<int>(p.conf.vector_length);
+    const size_t codes = static_cast<size_t>(p.jobs_per_channel > 1 ? 2 : 1) * code_cap_floats * sizeof(float);
+    const int M = N / kAvxLanes;
+    const int S = M <= 1 ? 1 : 1 + (M - 1 + kAvxSeg - 1) / kAvxSeg;
+    const size_t anchors = avx ? static_cast<size_t>(S + 2) * kAvxLanes * sizeof(f2) : static_cast<size_t>((N + kRenorm - 1) / kRenorm) * sizeof(Anchor);
+    return codes + anchors;
+}
+
+hipError_t launch_trk_persist(const TrkParams* params_dev, const TrkParams& params, TrkChannel* chans, int n_chans, const CodeDesc* codes,
+    int n_codes, int code_cap_floats, const void* samples, int fmt, uint64_t buf_first, int64_t buf_len, int max_rounds, gnsship_trk_epoch* rec,
+    gnsship_trk_dump_record* dump, int* ran_count, bool avx, hipStream_t stream)
+{
+    const size_t lds = trk_persist_lds_bytes(params, code_cap_floats, avx);
+    const bool data = params.jobs_per_channel > 1;
+    const int nt = params.n_taps;
+    dim3 grid(n_chans), block(kPThreads);
+#define GNSSHIP_PERSIST(F, NTV, DV, AV)                                                                                                        \
+    do {                                                                                                                                       \
+        auto kfn = trk_persist_kernel<F, NTV, DV, AV>;                                                                                         \
+        hipError_t e0 = hipFuncSetAttribute(reinterpret_cast<const void*>(kfn), hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)); \
+        if (e0 != hipSuccess) return e0;                                                                                                       \
+        hipLaunchKernelGGL(kfn, grid, block, lds, stream, params_dev, chans, codes, n_codes, samples, buf_first, buf_len, max_rounds, n_chans,  \
+            code_cap_floats, rec, dump, ran_count);                                                                                            \
+    } while (0)
+#define GNSSHIP_PERSIST_F(F)                                                      \
+    do {                                                                          \
+        if (nt == 3 && !data) {                                                   \
+            if (avx) GNSSHIP_PERSIST(F, 3, false, true);                          \
+            else GNSSHIP_PERSIST(F, 3, false, false);                             \
+        } else if (nt == 5 && !data) {                                            \
+            if (avx) GNSSHIP_PERSIST(F, 5, false, true);                          \
+            else GNSSHIP_PERSIST(F, 5, false, false);                             \
+        } else if (nt == 5 && data) {                                             \
+            if (avx) GNSSHIP_PERSIST(F, 5, true, true);                           \
+            else GNSSHIP_PERSIST(F, 5, true, false);                              \
+        } else {                                                                  \
+            return hipErrorInvalidValue;                                          \
+        }                                                                         \
+    } while (0)
+    switch (fmt) {
+    case GNSSHIP_FMT_CF32: GNSSHIP_PERSIST_F(GNSSHIP_FMT_CF32); break;
+    case GNSSHIP_FMT_CI16: GNSSHIP_PERSIST_F(GNSSHIP_FMT_CI16); break;
+    case GNSSHIP_FMT_CI8: GNSSHIP_PERSIST_F(GNSSHIP_FMT_CI8); break;
+    default: return hipErrorInvalidValue;
+    }
+#undef GNSSHIP_PERSIST_F
+#undef GNSSHIP_PERSIST
+    return hipGetLastError();
+}
+
+}  // namespace gnsship

@@ -48,6 +48,25 @@ extern "C" {
 
 #define GNSSHIP_MAX_TAPS 8
 
+/* ---- rotator dot-product variant (volk_gnsssdr_32fc_32f_rotator_dot_prod_32fc_xn) ----
+ * The reference's correlations depend on which volk_gnsssdr variant its dispatcher picks
+ * (volk_gnsssdr_rank_archs.c): the generic C kernel (:66-98; VOLK_GENERIC set, or no AVX) or the
+ * u_avx/a_avx kernel (:155-316; any AVX host without a volk_gnsssdr_config override): 16 phasors
+ * advanced by normalise(inc^16), renormalised every 64 iterations.  The two differ by up to 1e-2
+ * relative at 50 Msps with a 7 MHz IF, so the engine reproduces either one exactly (phasors
+ * bit-identical), selected per job / per tracking engine. */
+#define GNSSHIP_ROTATOR_GENERIC 0
+#define GNSSHIP_ROTATOR_AVX 1
+#define GNSSHIP_ROTATOR_AUTO (-1) /* what volk_gnsssdr dispatches on this host (gnsship_rotator_dispatch) */
+/* gnsship_corr_job::flags bits */
+#define GNSSHIP_JOB_HIGH_DYN 1     /* high-dynamics resampler + rotator (set_high_dynamics_resampler) */
+#define GNSSHIP_JOB_ROTATOR_AVX 2  /* the AVX rotator variant (ignored with GNSSHIP_JOB_HIGH_DYN) */
+/* The variant volk_gnsssdr's dispatcher would select for the rotator dot-product on this host:
+ * VOLK_GENERIC set in the environment -> generic; an entry for the kernel in the volk_gnsssdr
+ * preferences file ($VOLK_CONFIGPATH or $HOME/.volk_gnsssdr/volk_gnsssdr_config) -> that entry;
+ * otherwise the AVX variant when the CPU has AVX.  *variant = GNSSHIP_ROTATOR_GENERIC / _AVX. */
+int gnsship_rotator_dispatch(int* variant);
+
 typedef struct gnsship_ctx gnsship_ctx;
 typedef struct gnsship_corr gnsship_corr;
 typedef struct gnsship_batch gnsship_batch;
@@ -123,7 +142,7 @@ typedef struct gnsship_corr_job {
     int32_t n_samples;       /* correlation length (vector_length)                            */
     int32_t code_id;         /* code bank id                                                   */
     int32_t n_taps;          /* 1..GNSSHIP_MAX_TAPS                                            */
-    int32_t flags;           /* bit0: high-dynamics resampler/rotator (set_high_dynamics_resampler) */
+    int32_t flags;           /* GNSSHIP_JOB_HIGH_DYN | GNSSHIP_JOB_ROTATOR_AVX                   */
     float rem_carrier_phase_rad;
     float phase_step_rad;
     float phase_rate_step_rad;
@@ -299,6 +318,8 @@ typedef struct gnsship_trk_conf { /* Dll_Pll_Conf (dll_pll_conf.h:33-80), same n
     int32_t enable_fll_steady_state; /* ... and after it */
     int32_t high_dyn;                /* high-dynamics correlator + NCO rate smoothing (:1205-1255) */
     uint32_t smoother_length;        /* rate smoother length, 1..64 (0 is raised to 1, dll_pll_conf.cc:118-123) */
+    int32_t rotator;                 /* GNSSHIP_ROTATOR_*: which volk_gnsssdr rotator variant the correlations
+                                        reproduce (0 = generic; high_dyn has only the generic variant) */
 } gnsship_trk_conf;
 
 typedef struct gnsship_trk_start_args { /* Gnss_Synchro fields start_tracking reads (:647-649) */

@@ -564,6 +564,9 @@ struct Dll_Pll_Conf {
     bool carrier_aiding{true}, track_pilot{true};
     char system{'G'};    // 'G' GPS L1 C/A, 'E' Galileo E1, 'C' BeiDou B1I
     char signal[3]{"1C"};
+    // Not a Dll_Pll_Conf member: the reference's correlations follow the volk_gnsssdr rotator variant
+    // its dispatcher picks on the host (volk_gnsssdr_rank_archs.c); AUTO makes the same choice.
+    int32_t rotator{GNSSHIP_ROTATOR_AUTO};
 };
 
 // Mirror of dll_pll_veml_tracking (gnuradio_blocks/dll_pll_veml_tracking.cc) for many channels on one
@@ -608,6 +611,7 @@ public:
         c.enable_fll_steady_state = conf.enable_fll_steady_state ? 1 : 0;
         c.high_dyn = conf.high_dyn ? 1 : 0;
         c.smoother_length = conf.smoother_length;
+        c.rotator = conf.rotator;
         c.system = conf.system == 'E' ? GNSSHIP_SYS_GAL_E1 : conf.system == 'C' ? GNSSHIP_SYS_BDS_B1I : GNSSHIP_SYS_GPS_L1CA;
         code_base_ = 1024 + 2 * max_channels * next_engine_id();
         std::lock_guard<std::mutex> lk(dev_->mutex());

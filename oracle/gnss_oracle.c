@@ -333,6 +333,123 @@ static void orc_rotator_dot_prod_acc64(float* result, const float* in_common, fl
     phase[1] = pi;
 }
 
+/* volk_gnsssdr_32fc_32f_rotator_dot_prod_32fc_xn_u_avx / _a_avx —
+ *   volk_gnsssdr_32fc_32f_rotator_dot_prod_32fc_xn.h:155-316 (a_avx :322-, same arithmetic), with
+ *   _mm256_complexmul_ps / _mm256_complexnormalise_ps of volk_gnsssdr_avx_intrinsics.h:20-29,56-63.
+ * The variant volk_gnsssdr dispatches on any AVX host (the only non-generic x86 variants of this
+ * kernel).  Restated lane by lane in scalar C: every AVX op here is an IEEE single op (mul, add/sub
+ * of addsub, hadd = re²+im², sqrt_ps, div_ps), so the scalar form is bit-identical.
+ *   - 16 phasors z_l = phase·inc^l (generic chain, :204-208), advanced by dz = normalise(inc^16)
+ *     (four complex<float> squarings, :215-225) once per 16-sample iteration;
+ *   - the phasors are renormalised after the update of iterations m ≡ 0 (mod 64) (:265-272);
+ *   - accumulators: 4 registers × 4 complex lanes per tap (sample 16m + 4g + j → register g, lane
+ *     j), summed at the end as ((r0 + r1) + r2) + r3, then lanes 0..3 serially (:276-290);
+ *   - the N mod 16 tail continues serially from normalise(z_0) (:292-304).
+ * accum_f64: test-only, the same float products summed in double. */
+static void orc_rotator_dot_prod_avx_impl(float* result, const float* in_common, float inc_re, float inc_im, float* phase,
+    const float* in_a, int num_a_vectors, unsigned int num_points, int accum_f64)
+{
+    const unsigned int sixteenth = num_points / 16;
+    float zr[16], zi[16];
+    float pr = phase[0], pi = phase[1];
+    for (int l = 0; l < 16; l++) {
+        zr[l] = pr;
+        zi[l] = pi;
+        float nr, ni;
+        cmul(pr, pi, inc_re, inc_im, &nr, &ni);
+        pr = nr;
+        pi = ni;
+    }
+    float dr = inc_re, di = inc_im;
+    for (int k = 0; k < 4; k++) {
+        float nr, ni;
+        cmul(dr, di, dr, di, &nr, &ni);
+        dr = nr;
+        di = ni;
+    }
+    {
+        const float m = sqrtf(dr * dr + di * di);
+        dr = dr / m;
+        di = di / m;
+    }
+    float acc[4][ORC_MAX_TAPS][8];
+    double acc64[2 * ORC_MAX_TAPS];
+    memset(acc, 0, sizeof(acc));
+    for (int t = 0; t < 2 * num_a_vectors; t++) acc64[t] = 0.0;
+    for (unsigned int m = 0; m < sixteenth; m++) {
+        float ar[16], ai[16];
+        for (int l = 0; l < 16; l++) {
+            const unsigned int n = 16 * m + l;
+            cmul(in_common[2 * n], in_common[2 * n + 1], zr[l], zi[l], &ar[l], &ai[l]);
+            float nr, ni;
+            cmul(zr[l], zi[l], dr, di, &nr, &ni);
+            zr[l] = nr;
+            zi[l] = ni;
+        }
+        for (int t = 0; t < num_a_vectors; t++)
+            for (int l = 0; l < 16; l++) {
+                const float c = in_a[(size_t)t * num_points + 16 * m + l];
+                if (accum_f64) {
+                    acc64[2 * t] += (double)(ar[l] * c);
+                    acc64[2 * t + 1] += (double)(ai[l] * c);
+                } else {
+                    acc[l / 4][t][2 * (l % 4)] += ar[l] * c;
+                    acc[l / 4][t][2 * (l % 4) + 1] += ai[l] * c;
+                }
+            }
+        if (m % 64 == 0)
+            for (int l = 0; l < 16; l++) {
+                const float mm = sqrtf(zr[l] * zr[l] + zi[l] * zi[l]);
+                zr[l] = zr[l] / mm;
+                zi[l] = zi[l] / mm;
+            }
+    }
+    float res[2 * ORC_MAX_TAPS];
+    for (int t = 0; t < num_a_vectors; t++) {
+        float v[8];
+        for (int e = 0; e < 8; e++) v[e] = ((acc[0][t][e] + acc[1][t][e]) + acc[2][t][e]) + acc[3][t][e];
+        float rr = 0.0F, ri = 0.0F;
+        for (int j = 0; j < 4; j++) {
+            rr += v[2 * j];
+            ri += v[2 * j + 1];
+        }
+        res[2 * t] = rr;
+        res[2 * t + 1] = ri;
+    }
+    {
+        const float mm = sqrtf(zr[0] * zr[0] + zi[0] * zi[0]);
+        pr = zr[0] / mm;
+        pi = zi[0] / mm;
+    }
+    for (unsigned int n = sixteenth * 16; n < num_points; n++) {
+        float wr, wi;
+        cmul(in_common[2 * n], in_common[2 * n + 1], pr, pi, &wr, &wi);
+        float nr, ni;
+        cmul(pr, pi, inc_re, inc_im, &nr, &ni);
+        pr = nr;
+        pi = ni;
+        for (int t = 0; t < num_a_vectors; t++) {
+            const float c = in_a[(size_t)t * num_points + n];
+            if (accum_f64) {
+                acc64[2 * t] += (double)(wr * c);
+                acc64[2 * t + 1] += (double)(wi * c);
+            } else {
+                res[2 * t] += wr * c;
+                res[2 * t + 1] += wi * c;
+            }
+        }
+    }
+    for (int t = 0; t < 2 * num_a_vectors; t++) result[t] = accum_f64 ? (float)acc64[t] : res[t];
+    phase[0] = pr;
+    phase[1] = pi;
+}
+
+void orc_rotator_dot_prod_avx(float* result, const float* in_common, float inc_re, float inc_im, float* phase,
+    const float* in_a, int num_a_vectors, unsigned int num_points)
+{
+    orc_rotator_dot_prod_avx_impl(result, in_common, inc_re, inc_im, phase, in_a, num_a_vectors, num_points, 0);
+}
+
 /* volk_gnsssdr_32fc_32f_high_dynamic_rotator_dot_prod_32fc_xn_generic —
  *   volk_gnsssdr_32fc_32f_high_dynamic_rotator_dot_prod_32fc_xn.h:68-110 (non-Windows branch,
  *   cpowf; note (n*n) is unsigned int and wraps for n >= 65536, as in the reference). */
@@ -395,25 +512,41 @@ static void orc_high_dynamic_rotator_dot_prod_impl(float* result, const float* i
  * phase_offset = (cos rem, −sin rem); phase_inc = exp(−j·step) (std::exp of complex<float>, i.e.
  * glibc cexpf → (cosf(−step), sinf(−step))).  scratch: n_taps*signal_length floats or NULL. */
 static int orc_multicorrelator_impl(float* corr_out, const float* sig_in, const float* local_code, int code_length_chips,
-    const float* shifts_chips, int n_correlators, int high_dyn, float rem_carrier_phase_in_rad, float phase_step_rad,
+    const float* shifts_chips, int n_correlators, int flags, float rem_carrier_phase_in_rad, float phase_step_rad,
     float phase_rate_step_rad, float rem_code_phase_chips, float code_phase_step_chips, float code_phase_rate_step_chips,
     int signal_length_samples, float* scratch, int accum_f64);
 
+/* accum_f64: test-only double accumulation of the same float products. */
+int orc_multicorrelator_real_codes_ex(float* corr_out, const float* sig_in, const float* local_code, int code_length_chips,
+    const float* shifts_chips, int n_correlators, int flags, float rem_carrier_phase_in_rad, float phase_step_rad,
+    float phase_rate_step_rad, float rem_code_phase_chips, float code_phase_step_chips, float code_phase_rate_step_chips,
+    int signal_length_samples, float* scratch, int accum_f64)
+{
+    return orc_multicorrelator_impl(corr_out, sig_in, local_code, code_length_chips, shifts_chips, n_correlators, flags,
+        rem_carrier_phase_in_rad, phase_step_rad, phase_rate_step_rad, rem_code_phase_chips, code_phase_step_chips,
+        code_phase_rate_step_chips, signal_length_samples, scratch, accum_f64);
+}
+
+/* flags as gnsship_corr_job::flags: bit0 high_dyn, bit1 AVX rotator variant; bit2 (test-only):
+ * phasors from double cos/sin rounded to float instead of glibc cosf/sinf. */
 int orc_multicorrelator_real_codes(float* corr_out, const float* sig_in, const float* local_code, int code_length_chips,
-    const float* shifts_chips, int n_correlators, int high_dyn, float rem_carrier_phase_in_rad, float phase_step_rad,
+    const float* shifts_chips, int n_correlators, int flags, float rem_carrier_phase_in_rad, float phase_step_rad,
     float phase_rate_step_rad, float rem_code_phase_chips, float code_phase_step_chips, float code_phase_rate_step_chips,
     int signal_length_samples, float* scratch)
 {
-    return orc_multicorrelator_impl(corr_out, sig_in, local_code, code_length_chips, shifts_chips, n_correlators, high_dyn,
+    return orc_multicorrelator_impl(corr_out, sig_in, local_code, code_length_chips, shifts_chips, n_correlators, flags,
         rem_carrier_phase_in_rad, phase_step_rad, phase_rate_step_rad, rem_code_phase_chips, code_phase_step_chips,
         code_phase_rate_step_chips, signal_length_samples, scratch, 0);
 }
 
+/* flags: bit0 high-dynamics resampler/rotator, bit1 the AVX rotator variant (the job flags of
+ * gnsship_corr_job; high_dyn has only generic variants, so bit1 is ignored with bit0). */
 static int orc_multicorrelator_impl(float* corr_out, const float* sig_in, const float* local_code, int code_length_chips,
-    const float* shifts_chips, int n_correlators, int high_dyn, float rem_carrier_phase_in_rad, float phase_step_rad,
+    const float* shifts_chips, int n_correlators, int flags, float rem_carrier_phase_in_rad, float phase_step_rad,
     float phase_rate_step_rad, float rem_code_phase_chips, float code_phase_step_chips, float code_phase_rate_step_chips,
     int signal_length_samples, float* scratch, int accum_f64)
 {
+    const int high_dyn = flags & 1;
     if (n_correlators < 1 || n_correlators > ORC_MAX_TAPS || signal_length_samples < 0) return -1;
     if (high_dyn) { /* the reference's memcpy lengths go negative outside [0, N]: refused, not run */
         unsigned int s = 0;
@@ -436,11 +569,20 @@ static int orc_multicorrelator_impl(float* corr_out, const float* sig_in, const 
         orc_resampler_generic(codes, local_code, rem_code_phase_chips, code_phase_step_chips, shifts_chips, (unsigned)code_length_chips,
             n_correlators, (unsigned)signal_length_samples);
     float phase[2] = {cosf(rem_carrier_phase_in_rad), -sinf(rem_carrier_phase_in_rad)};
-    const float inc_re = cosf(-phase_step_rad), inc_im = sinf(-phase_step_rad);
+    float inc_re = cosf(-phase_step_rad), inc_im = sinf(-phase_step_rad);
+    if (flags & 4) { /* test-only: the double-rounded-once trig of the device loop (nco_math.h) */
+        phase[0] = (float)cos((double)rem_carrier_phase_in_rad);
+        phase[1] = -(float)sin((double)rem_carrier_phase_in_rad);
+        inc_re = (float)cos((double)-phase_step_rad);
+        inc_im = (float)sin((double)-phase_step_rad);
+    }
     if (high_dyn) {
         const float rr = cosf(-phase_rate_step_rad), ri = sinf(-phase_rate_step_rad);
         orc_high_dynamic_rotator_dot_prod_impl(corr_out, sig_in, inc_re, inc_im, rr, ri, phase, codes, n_correlators,
             (unsigned)signal_length_samples, accum_f64);
+    } else if (flags & 2) {
+        orc_rotator_dot_prod_avx_impl(corr_out, sig_in, inc_re, inc_im, phase, codes, n_correlators, (unsigned)signal_length_samples,
+            accum_f64);
     } else if (accum_f64) {
         orc_rotator_dot_prod_acc64(corr_out, sig_in, inc_re, inc_im, phase, codes, n_correlators, (unsigned)signal_length_samples);
     } else {
@@ -480,7 +622,7 @@ static void* orc_batch_worker(void* p)
     for (int j = a->j0; j < a->j1; j++) {
         const orc_job* jb = &a->jobs[j];
         orc_multicorrelator_impl(a->out + (size_t)j * 2 * ORC_MAX_TAPS, a->samples + 2 * jb->sample_offset, a->codes[jb->code_id],
-            a->code_lengths[jb->code_id], jb->shifts_chips, jb->n_taps, jb->flags & 1, jb->rem_carrier_phase_rad, jb->phase_step_rad,
+            a->code_lengths[jb->code_id], jb->shifts_chips, jb->n_taps, jb->flags & 3, jb->rem_carrier_phase_rad, jb->phase_step_rad,
             jb->phase_rate_step_rad, jb->rem_code_phase_chips, jb->code_phase_step_chips, jb->code_phase_rate_step_chips, jb->n_samples,
             scratch, a->accum_f64);
     }

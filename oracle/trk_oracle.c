@@ -342,6 +342,12 @@ typedef struct {
     int32_t enable_fll_pull_in, enable_fll_steady_state; /* dll_pll_conf.h:75-76 */
     int32_t high_dyn;         /* dll_pll_conf.h:80: high-dynamics correlator + NCO rate smoothing */
     uint32_t smoother_length; /* dll_pll_conf.h:62 (dll_pll_conf.cc:118-123 raises 0 to 1) */
+    int32_t rotator_avx;      /* 1: the rotator dot-product is volk's u_avx/a_avx variant (what volk_gnsssdr
+                                 dispatches on an AVX host, volk_gnsssdr_rank_archs.c), 0: generic */
+    int32_t accum_f64;        /* test-only: the same float products summed in double (long epochs, see
+                                 orc_rotator_dot_prod_acc64) */
+    int32_t cr_trig;          /* test-only: phasors from double cos/sin rounded to float (the device loop's
+                                 nco_math.h) instead of glibc cosf/sinf */
 } orc_trk_conf;
 
 #define TRK_MAX_SMOOTHER 64
@@ -872,10 +878,10 @@ void orc_trk_set_prn(orc_trk_channel* c, uint32_t prn) { c->prn = prn; }
 uint64_t orc_trk_nitems_read(const orc_trk_channel* c) { return c->nitems_read; }
 int orc_trk_state(const orc_trk_channel* c) { return c->state; }
 
-int orc_multicorrelator_real_codes(float* corr_out, const float* sig_in, const float* local_code, int code_length_chips,
-    const float* shifts_chips, int n_correlators, int high_dyn, float rem_carrier_phase_in_rad, float phase_step_rad,
+int orc_multicorrelator_real_codes_ex(float* corr_out, const float* sig_in, const float* local_code, int code_length_chips,
+    const float* shifts_chips, int n_correlators, int flags, float rem_carrier_phase_in_rad, float phase_step_rad,
     float phase_rate_step_rad, float rem_code_phase_chips, float code_phase_step_chips, float code_phase_rate_step_chips,
-    int signal_length_samples, float* scratch);
+    int signal_length_samples, float* scratch, int accum_f64);
 
 /* Closed loop over host CF32 samples (samples[i] = absolute sample buffer_first + i) for one channel: for each epoch, correlate
  * vector_length samples at nitems_read with the oracle multicorrelator (the tracking code and,
@@ -886,6 +892,7 @@ int orc_trk_run(const orc_trk_conf* k, orc_trk_channel* c, const float* samples,
 {
     const int vl = (int)k->vector_length;
     float* scratch = (float*)malloc((size_t)5 * (size_t)vl * sizeof(float));
+    const int cflags = (k->high_dyn ? 1 : 0) | (k->rotator_avx ? 2 : 0) | (k->cr_trig ? 4 : 0); /* gnsship_corr_job flags (+ test bit) */
     int e = 0;
     for (; e < max_epochs; e++) {
         if (c->state != 2 && c->state != 3 && c->state != 4) break;
@@ -894,12 +901,12 @@ int orc_trk_run(const orc_trk_conf* k, orc_trk_channel* c, const float* samples,
         orc_trk_correlation_args(k, c, args);
         float taps[10] = {0}, pdata[2] = {0};
         const float* x = samples + 2 * (c->nitems_read - buffer_first);
-        orc_multicorrelator_real_codes(taps, x, code, code_len, c->shifts, c->n_taps, k->high_dyn, args[0], args[1], args[2], args[3], args[4], args[5], vl,
-            scratch);
+        orc_multicorrelator_real_codes_ex(taps, x, code, code_len, c->shifts, c->n_taps, cflags, args[0], args[1], args[2], args[3], args[4], args[5], vl,
+            scratch, k->accum_f64);
         if (k->track_pilot && data_code) {
             const float zero = 0.0F;
-            orc_multicorrelator_real_codes(pdata, x, data_code, code_len, &zero, 1, k->high_dyn, args[0], args[1], args[2], args[3], args[4], args[5], vl,
-                scratch);
+            orc_multicorrelator_real_codes_ex(pdata, x, data_code, code_len, &zero, 1, cflags, args[0], args[1], args[2], args[3], args[4], args[5], vl,
+                scratch, k->accum_f64);
         }
         if (!orc_trk_epoch_update(k, c, taps, pdata, &out[e], dump ? &dump[e] : NULL)) {
             e++;

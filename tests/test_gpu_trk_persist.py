@@ -1,0 +1,122 @@
+"""Persistent closed loop (trk_persist.hip: one workgroup per channel for a whole run) vs the oracle
+loop (oracle/trk_oracle.c), for both volk_gnsssdr rotator variants the reference can dispatch
+(generic, and u_avx/a_avx: volk_gnsssdr_32fc_32f_rotator_dot_prod_32fc_xn.h:155-316), and at the
+north_star's 25 Msps rates (GPS L1 C/A N = 25000, Galileo E1 N = 100000 — C3/C4's sampling rate).
+
+Tolerances are test_gpu_trk.compare's: exact epoch boundaries / states / flags, Doppler and code
+frequency ≤ 2e-3, remnant code phase ≤ 1e-5 chip, CN0 ≤ 5e-3 dB, prompt ≤ 1e-4 relative.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from gnss_sim_receiver_amd import abi, engine
+from oracle import trk as T
+
+import trk_scenarios as S
+from test_gpu_trk import compare, dev_conf
+
+pytestmark = pytest.mark.gpu
+
+
+def run_pair(ctx, system, fs, epochs, avx, n_ch=2, **kw):
+    """One channel (index 1) synchronising to state 4 on the device and in the oracle.  At
+    N ≥ 1e5 the oracle sums its float products in double (accum_f64): the reference's serial float
+    sum is itself ~1e-5 off the exact sum there (DESIGN.md §4 'Long integrations'), and the loop
+    turns that into ~0.07 Hz of Doppler walk, so the device (tree sums) is held to the loop on the
+    exact sums of the same products.  Likewise a one-ulp difference in phase_inc (glibc's sinf is
+    not correctly rounded, and differs between its FMA and non-FMA builds) turns the phase by
+    N·6e-8 rad over a 1e5-sample epoch, so at N ≥ 1e5 the oracle's phasors come from the same
+    once-rounded double cos/sin as the device's (cr_trig); test_oracle_trk.py bounds the loop's
+    distance between the two trig choices."""
+    vl = int(round(fs * T.SYSTEMS[system][2]))
+    long_n = 1 if vl >= 100000 else 0
+    sat, k, x, stamp, first, delay, dop = S.sync(system, fs, epochs, rotator_avx=1 if avx else 0, accum_f64=long_n, cr_trig=long_n, **kw)
+    c = dev_conf(k, system)
+    c.rotator = abi.ROTATOR_AVX if avx else abi.ROTATOR_GENERIC
+    trk = engine.DllPllVemlTracking(ctx, c, n_ch)
+    ctx.set_code(40, sat.code)
+    if sat.code_data is not None:
+        ctx.set_code(41, sat.code_data)
+    trk.start(1, 40, delay, dop, stamp, first, data_code_id=41)
+    rec, rounds = trk.run(x, first, epochs)
+    trk.close()
+    ref = T.track(k, x, sat.code, delay, dop, stamp, first, epochs, data_code=sat.code_data, buffer_first=first)
+    return rec, rounds, ref
+
+
+@pytest.mark.parametrize("system,fs,epochs", [("GPS", 4e6, 700), ("GAL", 25e6 / 4, 90), ("BDS", 4.092e6, 300)])
+def test_avx_rotator_loop_matches_oracle(ctx, system, fs, epochs):
+    rec, rounds, ref = run_pair(ctx, system, fs, epochs, avx=True)
+    assert ref["state"][-1] == 4
+    compare(rec[:, 1], ref, f"{system} avx")
+    assert not np.any(rec[:, 0]["flags"])  # the idle channel never ran
+
+
+@pytest.mark.parametrize("avx", [False, True])
+@pytest.mark.parametrize("system,epochs", [("GPS", 300), ("GAL", 90)])
+def test_closed_loop_25msps_matches_oracle(ctx, system, epochs, avx):
+    """The closed loop at 25 Msps: GPS L1 C/A N = 25000 (north_star's second rate) and Galileo E1
+    N = 100000 with the data prompt (configs[3]'s per-channel epoch, dll_pll_veml_tracking.cc:1728-2094)."""
+    rec, rounds, ref = run_pair(ctx, system, 25e6, epochs, avx=avx)
+    assert ref["state"][-1] == 4
+    compare(rec[:, 1], ref, f"{system} 25 Msps avx={avx}")
+
+
+def test_galileo_e1_50msps_avx_matches_oracle(ctx):
+    """E1 at 50 Msps (configs[4]'s N = 200000) with the AVX rotator: 12500-step phasor chains."""
+    rec, rounds, ref = run_pair(ctx, "GAL", 50e6, 40, avx=True)
+    compare(rec[:, 1], ref, "GAL 50 Msps avx")
+
+
+def test_persistent_loop_matches_round_based_loop(ctx):
+    """The persistent kernel and the round-based step/correlate launches (GNSSHIP_TRK_ROUNDS=1)
+    run the same loop code on the same generic-rotator correlations: records agree to the
+    correlations' summation-order differences."""
+    sat, k, x, stamp, first, delay, dop = S.sync("GPS", 4e6, 400)
+    out = []
+    for rounds_env in ("1", None):
+        if rounds_env:
+            os.environ["GNSSHIP_TRK_ROUNDS"] = rounds_env
+        try:
+            trk = engine.DllPllVemlTracking(ctx, dev_conf(k, "GPS"), 3)
+        finally:
+            os.environ.pop("GNSSHIP_TRK_ROUNDS", None)
+        ctx.set_code(50, sat.code)
+        trk.start(2, 50, delay, dop, stamp, first)
+        rec, n = trk.run(x, first, 400)
+        trk.close()
+        out.append(rec[:, 2])
+    a, b = out
+    for f in ("sample_counter", "state", "flags", "prn_length_samples"):
+        assert np.array_equal(a[f], b[f]), f
+    np.testing.assert_allclose(a["carrier_doppler_hz"], b["carrier_doppler_hz"], rtol=0, atol=1e-3)
+    np.testing.assert_allclose(a["rem_code_phase_chips"], b["rem_code_phase_chips"], rtol=0, atol=1e-6)
+
+
+def test_many_channels_and_ragged_buffers(ctx):
+    """64 channels, 2 runs over consecutive buffers: each channel resumes where the previous
+    buffer left it (its next window straddles the boundary), as general_work's consume_each does."""
+    fs, vl, n_ch = 4e6, 4000, 64
+    from gnss_sim_receiver_amd import signals
+    rng = np.random.default_rng(9)
+    sats = [signals.Satellite(prn=1 + (i % 32), doppler_hz=float(rng.uniform(-4000, 4000)), code_delay_chips=float(rng.uniform(0, 1023)),
+                              cn0_dbhz=48.0, carrier_phase_rad=float(rng.uniform(0, 6.28))) for i in range(n_ch)]
+    k = T.conf("GPS", fs, vl)
+    x = signals.generate_if(fs, vl * 130, sats[:8], seed=4)  # 8 real signals; the other channels track noise and lose lock
+    trk = engine.DllPllVemlTracking(ctx, dev_conf(k, "GPS"), n_ch)
+    starts = []
+    for ch, s in enumerate(sats):
+        delay = (s.code_delay_chips / s.code_freq()) * fs
+        ctx.set_code(100 + ch, s.code)
+        trk.start(ch, 100 + ch, delay, s.doppler_hz + 5.0, 0, 0)
+        starts.append((delay, s.doppler_hz + 5.0))
+    half = vl * 64 + 1234
+    r1, n1 = trk.run(x[:half], 0, 200)
+    r2, n2 = trk.run(x[half - vl - 100:], half - vl - 100, 200)
+    trk.close()
+    for ch in (0, 5, 7, 40):
+        ref = T.track(k, x, sats[ch].code, starts[ch][0], starts[ch][1], 0, 0, 200)
+        d = np.concatenate([r1[:, ch][(r1[:, ch]["flags"] & 8) == 8], r2[:, ch][(r2[:, ch]["flags"] & 8) == 8]])
+        compare(d[:len(ref)], ref[:len(d)], f"ch{ch}")
