@@ -17,6 +17,11 @@
 
 #include "trk_engine.h"
 
+// Phase hook for the profiling build of the persistent kernel (trk_persist.hip); empty otherwise.
+#ifndef GNSSHIP_TRK_LOOP_STAMP
+#define GNSSHIP_TRK_LOOP_STAMP(k) ((void)0)
+#endif
+
 namespace gnsship {
 namespace {
 
@@ -381,15 +386,20 @@ __device__ bool epoch_update(const TrkParams& k, TrkChannel& c, const float* tap
         rec.prompt_i = static_cast<double>(c.p[0]);  // diagnostic: the epoch's prompt (no symbol flag in state 2)
         rec.prompt_q = static_cast<double>(c.p[1]);
         if (static_cast<uint64_t>(k.conf.bit_synchronization_time_limit_s) < (nir - c.acq_sample_stamp) / fs_int) c.carrier_fail = 300000;
+        GNSSHIP_TRK_LOOP_STAMP(8);
         if (!lock_status(k, c, k.code_period)) {
             clear_tracking_vars(c);
             c.state = 0;
             loss = true;
         } else {
             bool next_state = false;
+            GNSSHIP_TRK_LOOP_STAMP(9);
             run_dll_pll(k, c);
+            GNSSHIP_TRK_LOOP_STAMP(10);
             update_tracking_vars(k, c, h);
+            GNSSHIP_TRK_LOOP_STAMP(11);
             log_data(k, c, taps, pdata, nir, dump);
+            GNSSHIP_TRK_LOOP_STAMP(12);
             rec.flags |= 16;
             if (!c.pull_in) {
                 if (k.sync[c.geo].secondary || k.sync[c.geo].symbols_per_bit > 1) {
@@ -458,13 +468,16 @@ __device__ bool epoch_update(const TrkParams& k, TrkChannel& c, const float* tap
                 c.ext_count = 0;
                 c.state = 4;
             }
-        } else if (!lock_status(k, c, k.code_period * static_cast<double>(k.sync[c.geo].extend))) {
+        } else if (GNSSHIP_TRK_LOOP_STAMP(8), !lock_status(k, c, k.code_period * static_cast<double>(k.sync[c.geo].extend))) {
             clear_tracking_vars(c);
             c.state = 0;
             loss = true;
         } else {
+            GNSSHIP_TRK_LOOP_STAMP(9);
             run_dll_pll(k, c);
+            GNSSHIP_TRK_LOOP_STAMP(10);
             update_tracking_vars(k, c, h);
+            GNSSHIP_TRK_LOOP_STAMP(11);
             if (!c.acc_phase_init) {
                 c.acc_carrier_phase_rad = -static_cast<double>(c.rem_carr_phase_rad);
                 c.acc_phase_init = 1;

@@ -26,8 +26,33 @@
 //    in the same order, so every phasor is bit-identical to the reference's.
 //
 // High-dynamics tracking and epochs too long for LDS stay on the round-based path (trk_kernel.hip).
+#include <cstdlib>
+
 #include "corr_device.h"
 #include "trk_engine.h"
+
+// Epoch phase timestamps for the profiling build only (make prof → scripts/libgnsship_prof.so,
+// scripts/trk_wg_profile.py): slot [(channel·kProfEpochs + epoch)·16 + k] = wall_clock64() at phase
+// k (0-7 in the kernel, 8-15 inside the loop update, trk_loop.h GNSSHIP_TRK_LOOP_STAMP).
+#ifdef GNSSHIP_CORR_PROFILE
+namespace gnsship {
+constexpr int kProfEpochs = 64;
+constexpr int kProfSlots = 16;
+__device__ unsigned long long* g_trk_prof = nullptr;
+__shared__ int g_prof_epoch;
+__device__ __forceinline__ void trk_prof_stamp(int e, int k)
+{
+    if (g_trk_prof && e < kProfEpochs) g_trk_prof[(static_cast<size_t>(blockIdx.x) * kProfEpochs + e) * kProfSlots + k] = wall_clock64();
+}
+}  // namespace gnsship
+#define GNSSHIP_TRK_STAMP(e, k) gnsship::trk_prof_stamp((e), (k))
+#define GNSSHIP_TRK_LOOP_STAMP(k) gnsship::trk_prof_stamp(gnsship::g_prof_epoch, (k))
+#else
+#define GNSSHIP_TRK_STAMP(e, k) \
+    do {                        \
+    } while (0)
+#endif
+
 #include "trk_loop.h"
 
 #pragma clang fp contract(off)
@@ -83,9 +108,11 @@ __device__ __forceinline__ int deal(int32_t* next, int lane)
     return __builtin_amdgcn_readfirstlane(__shfl(v, 0, kWave));
 }
 
-// AVX geometry of an N-sample epoch: M = N/16 iterations; segment 0 = iteration 0, segment s ≥ 1 =
-// iterations [64(s−1)+1, 64s] ∩ [0, M); the N mod 16 tail runs serially after them.
-__device__ __forceinline__ int avx_segments(int M) { return M <= 1 ? 1 : 1 + (M - 1 + kAvxSeg - 1) / kAvxSeg; }
+// AVX geometry of an N-sample epoch: M = N/16 iterations, cut into tasks of G iterations (G = 16,
+// 32 or 64, a divisor of the renormalisation period, chosen by the LDS budget): task 0 = iteration 0,
+// task t ≥ 1 = iterations [G(t−1)+1, Gt] ∩ [0, M).  Renormalisations (after iterations ≡ 0 mod 64)
+// then only ever fall after a task's last iteration.  The N mod 16 tail runs serially after them.
+__host__ __device__ __forceinline__ int avx_tasks(int M, int G) { return M <= 1 ? 1 : 1 + (M - 1 + G - 1) / G; }
 
 // ---- replays ---------------------------------------------------------------------------------
 // Generic (one lane): the anchors of every 256-sample block, as replay_anchors (anchor_replay.h).
@@ -118,12 +145,14 @@ __device__ void replay_generic(const DevJob& job, Anchor* A, int nblk, int32_t* 
     }
 }
 
-// AVX (lanes 0..15 = phasor l): Z[s·16 + l] = the phasor lane l starts segment s with; T[j] = the
+// AVX (lanes 0..15 = phasor l): Z[t·16 + l] = the phasor lane l starts task t with; T[j] = the
 // tail phasor of sample 16M + j.  The initial phasors are the generic chain phase·inc^l (:204-208);
 // dz = normalise(inc^16) (:215-225); after iteration m's update, renormalise when m ≡ 0 mod 64.
-__device__ void replay_avx(const PEpoch& ep, f2* Z, f2* T, int N, int lane, int32_t* published)
+// A task's G steps run without a branch (16 at a time); each task's start is published for the
+// correlating waves.
+__device__ void replay_avx(const PEpoch& ep, f2* Z, f2* T, int N, int G, int lane, int32_t* published)
 {
-    const int M = N / kAvxLanes, S = avx_segments(M);
+    const int M = N / kAvxLanes, S = avx_tasks(M, G);
     const f2 inc = f2{ep.job.inc_re, ep.job.inc_im};
     const f2 dz = f2{ep.dz_re, ep.dz_im};
     f2 z = f2{ep.job.p0_re, ep.job.p0_im};
@@ -131,16 +160,29 @@ __device__ void replay_avx(const PEpoch& ep, f2* Z, f2* T, int N, int lane, int3
         if (i < lane) z = cmul_exact(z, inc);
     Z[lane] = z;
     if (lane == 0) publish(published, 1);
-    for (int m = 0; m < M; m++) {
-        z = cmul_exact(z, dz);
-        if (m % kAvxSeg == 0) {  // wave-uniform
-            z = normalise_avx(z);
-            const int s = m / kAvxSeg + 1;
-            if (s < S) {
-                Z[s * kAvxLanes + lane] = z;
-                if (lane == 0) publish(published, s + 1);
-            }
+    if (M > 0) {  // iteration 0, renormalised after its update
+        z = normalise_avx(cmul_exact(z, dz));
+        if (S > 1) {
+            Z[kAvxLanes + lane] = z;
+            if (lane == 0) publish(published, 2);
         }
+    }
+    // task t+1's start is stored right after task t and published one task later, when its LDS
+    // write has long landed (the release then costs no wait on the chain)
+    for (int t = 1; t < S; t++) {
+        const int m_lo = G * (t - 1) + 1, m_hi = min(G * t, M - 1);  // task t's iterations
+        const int cnt = m_hi - m_lo + 1;
+        if (t >= 2 && lane == 0) publish(published, t + 1);
+        if (cnt == G) {
+            for (int q = 0; q < G; q += 16) {
+#pragma unroll
+                for (int u = 0; u < 16; u++) z = cmul_exact(z, dz);
+            }
+        } else {
+            for (int u = 0; u < cnt; u++) z = cmul_exact(z, dz);
+        }
+        if (m_hi % kAvxSeg == 0) z = normalise_avx(z);
+        if (t + 1 < S) Z[(t + 1) * kAvxLanes + lane] = z;
     }
     if (lane == 0) {  // z0 = normalise(z0) after the loop, then the serial tail (:286-304)
         f2 t = normalise_avx(z);
@@ -204,17 +246,18 @@ __device__ __forceinline__ float code_at(const float* code, int L, float sn, flo
     return code[i];
 }
 
-// AVX: task g = segments 4g..4g+3 × the 16 phasors (64 lanes: lane = 16·(s − 4g) + l), each lane
-// continuing its phasor's chain over the segment's ≤ 64 iterations (sample 16m + l at iteration m);
-// the task after the last group correlates the N mod 16 tail samples.
-template <int FMT, int NT, bool DATA, bool IN_MARGIN>
-__device__ void consume_avx(PEpoch& ep, const f2* Z, const f2* T, i4v span, int N, const float* code0, const float* code1, int L, int lane,
-    f2 (&acc)[NT + 1])
+// AVX: wave step g = tasks 4g..4g+3 × the 16 phasors (64 lanes: lane = 16·(t − 4g) + l), each lane
+// continuing its phasor's chain over the task's ≤ G iterations (sample 16m + l at iteration m), 16
+// iterations per step with the next 16 samples in flight (the first 16 are loaded before the
+// task's anchors are awaited); the step after the last correlates the N mod 16 tail samples.
+template <int FMT, int NT, bool DATA, bool IN_MARGIN, int kB>
+__device__ void consume_avx(PEpoch& ep, const f2* Z, const f2* T, i4v span, int N, int G, const float* code0, const float* code1, int L,
+    int lane, f2 (&acc)[NT + 1])
 {
     const DevJob& job = ep.job;
-    const int M = N / kAvxLanes, S = avx_segments(M);
+    const int M = N / kAvxLanes, S = avx_tasks(M, G);
     const int n_groups = (S + 3) / 4, tail = N - kAvxLanes * M;
-    const int n_tasks = n_groups + (tail > 0 ? 1 : 0);
+    const int n_steps = n_groups + (tail > 0 ? 1 : 0);
     const f2 dz = f2{ep.dz_re, ep.dz_im};
     const float step = job.code_step, rem = job.rem_code;
     float shifts[NT];
@@ -223,7 +266,7 @@ __device__ void consume_avx(PEpoch& ep, const f2* Z, const f2* T, i4v span, int 
     constexpr int SB = sample_bytes<FMT>();
     for (;;) {
         const int g = deal(&ep.next_task, lane);
-        if (g >= n_tasks) break;
+        if (g >= n_steps) break;
         if (g == n_groups) {  // the serial tail (:292-304)
             wait_published(&ep.published, S + 1);
             if (lane < tail) {
@@ -243,30 +286,31 @@ __device__ void consume_avx(PEpoch& ep, const f2* Z, const f2* T, i4v span, int 
             }
             continue;
         }
-        const int s = 4 * g + (lane >> 4), l = lane & (kAvxLanes - 1);
-        const bool active = s < S;
-        const int m_lo = s == 0 ? 0 : kAvxSeg * (s - 1) + 1;
-        int cnt = active ? ((s == 0 ? (M > 0 ? 1 : 0) : (M < kAvxSeg * s + 1 ? M : kAvxSeg * s + 1) - m_lo)) : 0;
-        cnt = cnt < 0 ? 0 : cnt;
+        const int t = 4 * g + (lane >> 4), l = lane & (kAvxLanes - 1);
+        const bool active = t < S;
+        const int m_lo = t == 0 ? 0 : G * (t - 1) + 1;
+        int cnt = 0;
+        if (active) cnt = t == 0 ? (M > 0 ? 1 : 0) : min(G * t, M - 1) - m_lo + 1;
         int cmax = cnt;
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) cmax = max(cmax, __shfl_xor(cmax, o, kWave));
         cmax = __builtin_amdgcn_readfirstlane(cmax);
-        wait_published(&ep.published, (4 * g + 4 < S ? 4 * g + 4 : S));
-        f2 z = active ? Z[(active ? s : 0) * kAvxLanes + l] : f2{0.0f, 0.0f};
-        // sample n = 16m + l: lane voffset advances by 16 samples per iteration
+        // sample n = 16m + l: the lane's voffset advances by 16 samples per iteration
         const int v0 = (kAvxLanes * m_lo + l) * SB;
-        constexpr int kPre = 4;
-        f2 xa[kPre], xb[kPre];
+        f2 xa[kB], xb[kB];
 #pragma unroll
-        for (int u = 0; u < kPre; u++) xa[u] = load_sample<FMT>(span, v0 + u * kAvxLanes * SB, 0);
-        for (int i0 = 0; i0 < cmax; i0 += kPre) {
+        for (int u = 0; u < kB; u++) xa[u] = load_sample<FMT>(span, v0 + u * kAvxLanes * SB, 0);
+        wait_published(&ep.published, (4 * g + 4 < S ? 4 * g + 4 : S));
+        f2 z = active ? Z[(active ? t : 0) * kAvxLanes + l] : f2{0.0f, 0.0f};
+        for (int i0 = 0; i0 < cmax; i0 += kB) {
+            if (i0 + kB < cmax) {
 #pragma unroll
-            for (int u = 0; u < kPre; u++) xb[u] = load_sample<FMT>(span, v0 + (i0 + kPre + u) * kAvxLanes * SB, 0);
+                for (int u = 0; u < kB; u++) xb[u] = load_sample<FMT>(span, v0 + (i0 + kB + u) * kAvxLanes * SB, 0);
+            }
 #pragma unroll
-            for (int u = 0; u < kPre; u++) {
+            for (int u = 0; u < kB; u++) {
                 const int i = i0 + u;
-                // past the segment: weight 0, and the chip index of a sample inside the epoch (the
+                // past the task: weight 0, and the chip index of a sample inside the epoch (the
                 // padded replica covers [0, N) only; a product 0·code[far] could meet a NaN)
                 const bool on = i < cnt;
                 const f2 r = on ? cmul_pk2(xa[u], z) : f2{0.0f, 0.0f};
@@ -274,9 +318,9 @@ __device__ void consume_avx(PEpoch& ep, const f2* Z, const f2* T, i4v span, int 
                 const int n = on ? kAvxLanes * (m_lo + i) + l : 0;
                 const float sn = __fmul_rn(step, static_cast<float>(n));
 #pragma unroll
-                for (int t = 0; t < NT; t++) {
-                    const float c = code_at<IN_MARGIN>(code0, L, sn, shifts[t], rem);
-                    acc[t] = __builtin_elementwise_fma(r, f2{c, c}, acc[t]);
+                for (int q = 0; q < NT; q++) {
+                    const float c = code_at<IN_MARGIN>(code0, L, sn, shifts[q], rem);
+                    acc[q] = __builtin_elementwise_fma(r, f2{c, c}, acc[q]);
                 }
                 if constexpr (DATA) {
                     const float c = code_at<IN_MARGIN>(code1, L, sn, 0.0f, rem);
@@ -284,30 +328,29 @@ __device__ void consume_avx(PEpoch& ep, const f2* Z, const f2* T, i4v span, int 
                 }
             }
 #pragma unroll
-            for (int u = 0; u < kPre; u++) xa[u] = xb[u];
+            for (int u = 0; u < kB; u++) xa[u] = xb[u];
         }
     }
 }
 
 // do_correlation_step's arguments for the epoch at c.nitems_read (derive_job on the device; the
 // generic lane factor needs arg/|inc| in double, the AVX path needs dz instead).
+// p0 / inc: (cos rem, −sin rem) and (cos −step, sin −step), evaluated by two lanes of wave 0 at once.
 template <bool AVX>
-__device__ void derive_epoch(PEpoch& ep, const TrkParams& k, const TrkChannel& c, int64_t off, int L)
+__device__ void derive_epoch(PEpoch& ep, const TrkParams& k, const TrkChannel& c, int64_t off, int L, f2 p0, f2 inc)
 {
     const int NT = k.n_taps;
     const float* sh = c.narrow ? k.shifts_n : k.shifts;
     DevJob& j = ep.job;
     const float spcf = static_cast<float>(k.code_samples_per_chip);
-    const float rem_carr = c.rem_carr_phase_rad;
-    const float step = static_cast<float>(c.carrier_phase_step_rad);
     j.sample_offset = off;
     j.n_samples = static_cast<int32_t>(k.conf.vector_length);
     j.code_id = c.code_id;
     j.n_taps = NT;
-    j.p0_re = cos_f32_rn(rem_carr);
-    j.p0_im = -sin_f32_rn(rem_carr);
-    j.inc_re = cos_f32_rn(-step);
-    j.inc_im = sin_f32_rn(-step);
+    j.p0_re = p0.x;
+    j.p0_im = p0.y;
+    j.inc_re = inc.x;
+    j.inc_im = inc.y;
     j.rem_code = __fmul_rn(static_cast<float>(c.rem_code_phase_chips), spcf);
     j.code_step = __fmul_rn(static_cast<float>(c.code_phase_step_chips), spcf);
     for (int t = 0; t < kMaxTaps; t++) j.shifts[t] = t < NT ? sh[t] : 0.0f;
@@ -343,10 +386,16 @@ __device__ void stage_code(float* dst, const CodeDesc& cd)
     for (int q = threadIdx.x; q < nq; q += kPThreads) d4[q] = src[q];
 }
 
-template <int FMT, int NT, bool DATA, bool AVX>
-__global__ __launch_bounds__(kPThreads) void trk_persist_kernel(const TrkParams* __restrict__ pk, TrkChannel* __restrict__ chans,
+// THRU: the throughput variant for more channels than CUs — ≤ 128 VGPRs (4 workgroups per CU) and
+// a 4-deep sample prefetch; otherwise one workgroup per CU may use every register for a 16-deep one.
+template <bool THRU>
+constexpr int persist_waves_per_simd() { return THRU ? 4 : 1; }
+
+template <int FMT, int NT, bool DATA, bool AVX, bool THRU>
+__global__ __launch_bounds__(kPThreads, persist_waves_per_simd<THRU>()) void trk_persist_kernel(const TrkParams* __restrict__ pk, TrkChannel* __restrict__ chans,
     const CodeDesc* __restrict__ codes, int n_codes, const void* __restrict__ samples, uint64_t buf_first, int64_t buf_len, int max_rounds,
-    int n_chans, int code_cap_floats, gnsship_trk_epoch* __restrict__ rec, gnsship_trk_dump_record* __restrict__ dump, int* __restrict__ ran_count)
+    int n_chans, int code_cap_floats, int avx_g, gnsship_trk_epoch* __restrict__ rec, gnsship_trk_dump_record* __restrict__ dump,
+    int* __restrict__ ran_count)
 {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     __shared__ TrkChannel sc;
@@ -382,19 +431,34 @@ __global__ __launch_bounds__(kPThreads) void trk_persist_kernel(const TrkParams*
     const int N = static_cast<int>(k.conf.vector_length);
     Anchor* A = reinterpret_cast<Anchor*>(anc);
     f2* Z = reinterpret_cast<f2*>(anc);
-    f2* T = Z + (avx_segments(N / kAvxLanes) + 1) * kAvxLanes;
+    f2* T = AVX ? Z + (avx_tasks(N / kAvxLanes, avx_g) + 1) * kAvxLanes : nullptr;
     for (int e = 0; e < max_rounds; e++) {
-        if (tid == 0) {
-            const uint64_t vl = k.conf.vector_length;
-            const bool runnable = (sc.state == 2 || sc.state == 3 || sc.state == 4) && sc.nitems_read >= buf_first &&
-                                  sc.nitems_read + vl <= buf_first + static_cast<uint64_t>(buf_len);
-            ep.runnable = runnable ? 1 : 0;
-            if (runnable) {
-                derive_epoch<AVX>(ep, k, sc, static_cast<int64_t>(sc.nitems_read - buf_first), L);
-                sc.epoch_start = sc.nitems_read;
+        if (wave == 0) {
+            if (lane == 0) GNSSHIP_TRK_STAMP(e, 0);
+#ifdef GNSSHIP_CORR_PROFILE
+            if (lane == 0) g_prof_epoch = e;
+#endif
+            // the epoch's two phasors (cpu_multicorrelator_real_codes.cc:115,123), lane 0: rem_carr,
+            // lane 1: −step, each as the once-rounded double cos/sin (nco_math.h)
+            const float a = lane == 0 ? sc.rem_carr_phase_rad : -static_cast<float>(sc.carrier_phase_step_rad);
+            double sd, cd;
+            sincos(static_cast<double>(a), &sd, &cd);
+            const float sf = static_cast<float>(sd), cf = static_cast<float>(cd);
+            const f2 p0 = f2{__shfl(cf, 0, kWave), -__shfl(sf, 0, kWave)};
+            const f2 inc = f2{__shfl(cf, 1, kWave), __shfl(sf, 1, kWave)};
+            if (lane == 0) {
+                const uint64_t vl = k.conf.vector_length;
+                const bool runnable = (sc.state == 2 || sc.state == 3 || sc.state == 4) && sc.nitems_read >= buf_first &&
+                                      sc.nitems_read + vl <= buf_first + static_cast<uint64_t>(buf_len);
+                ep.runnable = runnable ? 1 : 0;
+                if (runnable) {
+                    derive_epoch<AVX>(ep, k, sc, static_cast<int64_t>(sc.nitems_read - buf_first), L, p0, inc);
+                    sc.epoch_start = sc.nitems_read;
+                }
+                ep.published = 0;
+                ep.next_task = 0;
+                GNSSHIP_TRK_STAMP(e, 1);
             }
-            ep.published = 0;
-            ep.next_task = 0;
         }
         __syncthreads();  // also: the code replicas are staged (first epoch)
         if (!ep.runnable) break;
@@ -403,13 +467,15 @@ __global__ __launch_bounds__(kPThreads) void trk_persist_kernel(const TrkParams*
 #pragma unroll
         for (int t = 0; t <= NT; t++) acc[t] = f2{0.0f, 0.0f};
         if constexpr (AVX) {
-            if (wave == 0 && lane < kAvxLanes) replay_avx(ep, Z, T, N, lane, &ep.published);
+            if (wave == 0 && lane < kAvxLanes) replay_avx(ep, Z, T, N, avx_g, lane, &ep.published);
+            if (tid == 0) GNSSHIP_TRK_STAMP(e, 2);
             if (ep.in_margin)
-                consume_avx<FMT, NT, DATA, true>(ep, Z, T, span, N, c0, c1, L, lane, acc);
+                consume_avx<FMT, NT, DATA, true, THRU ? 4 : 16>(ep, Z, T, span, N, avx_g, c0, c1, L, lane, acc);
             else
-                consume_avx<FMT, NT, DATA, false>(ep, Z, T, span, N, c0, c1, L, lane, acc);
+                consume_avx<FMT, NT, DATA, false, THRU ? 4 : 16>(ep, Z, T, span, N, avx_g, c0, c1, L, lane, acc);
         } else {
             if (wave == 0 && lane == 0) replay_generic(ep.job, A, (N + kRenorm - 1) / kRenorm, &ep.published);
+            if (tid == 0) GNSSHIP_TRK_STAMP(e, 2);
             if (ep.in_margin)
                 consume_generic<FMT, NT, DATA, true>(ep, A, span, N, c0, c1, L, lane, acc);
             else
@@ -420,6 +486,7 @@ __global__ __launch_bounds__(kPThreads) void trk_persist_kernel(const TrkParams*
 #pragma unroll
             for (int t = 0; t <= NT; t++) acc[t] = cmul_pk(acc[t], er, esw);
         }
+        if (lane == 0 && wave <= 1) GNSSHIP_TRK_STAMP(e, 3 + wave);
         constexpr int kOut = NT + (DATA ? 1 : 0);
 #pragma unroll
         for (int t = 0; t < kOut; t++) {
@@ -431,6 +498,7 @@ __global__ __launch_bounds__(kPThreads) void trk_persist_kernel(const TrkParams*
         }
         __syncthreads();
         if (tid == 0) {
+            GNSSHIP_TRK_STAMP(e, 5);
             float taps[2 * kMaxTaps], pdata[2];
             for (int v = 0; v < 2 * kMaxTaps; v++) taps[v] = 0.0f;
             for (int v = 0; v < 2 * NT; v++) {
@@ -453,6 +521,7 @@ __global__ __launch_bounds__(kPThreads) void trk_persist_kernel(const TrkParams*
             if (rec) rec[slot] = r;
             if (dump && (r.flags & 16)) dump[slot] = dr;
             atomicAdd(ran_count + e, 1);
+            GNSSHIP_TRK_STAMP(e, 6);
         }
         __syncthreads();
     }
@@ -467,33 +536,55 @@ __global__ __launch_bounds__(kPThreads) void trk_persist_kernel(const TrkParams*
 
 }  // namespace
 
-// LDS bytes of the persistent kernel's dynamic region for an engine (codes + anchors), or 0 when the
-// configuration needs the round-based path.
-size_t trk_persist_lds_bytes(const TrkParams& p, int code_cap_floats, bool avx)
+#ifdef GNSSHIP_CORR_PROFILE
+}  // namespace gnsship
+extern "C" int gnsship_debug_trk_profile(void* dev_buf)
+{
+    return hipMemcpyToSymbol(HIP_SYMBOL(gnsship::g_trk_prof), &dev_buf, sizeof(void*)) == hipSuccess ? 0 : -3;
+}
+namespace gnsship {
+#endif
+
+// LDS bytes of the persistent kernel's dynamic region (codes + anchors) and, for the AVX rotator, the
+// task granularity G: 16 iterations where the anchors fit, else 32 or 64.
+static size_t persist_lds(const TrkParams& p, int code_cap_floats, bool avx, int* g_out)
 {
     const int N = static_cast<int>(p.conf.vector_length);
     const size_t codes = static_cast<size_t>(p.jobs_per_channel > 1 ? 2 : 1) * code_cap_floats * sizeof(float);
-    const int M = N / kAvxLanes;
-    const int S = M <= 1 ? 1 : 1 + (M - 1 + kAvxSeg - 1) / kAvxSeg;
-    const size_t anchors = avx ? static_cast<size_t>(S + 2) * kAvxLanes * sizeof(f2) : static_cast<size_t>((N + kRenorm - 1) / kRenorm) * sizeof(Anchor);
-    return codes + anchors;
+    if (!avx) {
+        if (g_out) *g_out = 0;
+        return codes + static_cast<size_t>((N + kRenorm - 1) / kRenorm) * sizeof(Anchor);
+    }
+    size_t bytes = 0;
+    for (int G = 16; G <= kAvxSeg; G *= 2) {
+        bytes = codes + static_cast<size_t>(avx_tasks(N / kAvxLanes, G) + 2) * kAvxLanes * sizeof(f2);
+        if (g_out) *g_out = G;
+        if (bytes <= kTrkPersistMaxLds) break;
+    }
+    return bytes;
 }
+
+size_t trk_persist_lds_bytes(const TrkParams& p, int code_cap_floats, bool avx) { return persist_lds(p, code_cap_floats, avx, nullptr); }
 
 hipError_t launch_trk_persist(const TrkParams* params_dev, const TrkParams& params, TrkChannel* chans, int n_chans, const CodeDesc* codes,
     int n_codes, int code_cap_floats, const void* samples, int fmt, uint64_t buf_first, int64_t buf_len, int max_rounds, gnsship_trk_epoch* rec,
     gnsship_trk_dump_record* dump, int* ran_count, bool avx, hipStream_t stream)
 {
-    const size_t lds = trk_persist_lds_bytes(params, code_cap_floats, avx);
+    int avx_g = 0;
+    const size_t lds = persist_lds(params, code_cap_floats, avx, &avx_g);
     const bool data = params.jobs_per_channel > 1;
+    // more channels than CUs: the throughput variant (GNSSHIP_TRK_THRU=0/1 overrides, for A/B runs)
+    bool thru = n_chans > 256;
+    if (const char* env = std::getenv("GNSSHIP_TRK_THRU")) thru = env[0] == '1';
     const int nt = params.n_taps;
     dim3 grid(n_chans), block(kPThreads);
 #define GNSSHIP_PERSIST(F, NTV, DV, AV)                                                                                                        \
     do {                                                                                                                                       \
-        auto kfn = trk_persist_kernel<F, NTV, DV, AV>;                                                                                         \
+        auto kfn = thru ? trk_persist_kernel<F, NTV, DV, AV, true> : trk_persist_kernel<F, NTV, DV, AV, false>;                                                                                         \
         hipError_t e0 = hipFuncSetAttribute(reinterpret_cast<const void*>(kfn), hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)); \
         if (e0 != hipSuccess) return e0;                                                                                                       \
         hipLaunchKernelGGL(kfn, grid, block, lds, stream, params_dev, chans, codes, n_codes, samples, buf_first, buf_len, max_rounds, n_chans,  \
-            code_cap_floats, rec, dump, ran_count);                                                                                            \
+            code_cap_floats, avx_g, rec, dump, ran_count);                                                                                            \
     } while (0)
 #define GNSSHIP_PERSIST_F(F)                                                      \
     do {                                                                          \

@@ -47,8 +47,9 @@ def main():
     for rot in (0, 1):
         run(ctx, "GPS", fs, 4000, 12, 250, rot, sats=sats, block=block)
     run(ctx, "GPS", fs, 4000, 12, 250, 0, env={"GNSSHIP_TRK_ROUNDS": "1"}, sats=sats, block=block)
-    for n in (256, 1024, 4096):
+    for n in (256, 1024, 4096, 16384):
         run(ctx, "GPS", fs, 4000, n, 100, 1, sats=sats, block=block)
+    run(ctx, "GPS", fs, 4000, 4096, 100, 1, env={"GNSSHIP_TRK_THRU": "0"}, sats=sats, block=block)
     fs = 25e6
     gs = signals.random_sky(8, seed=3, system="GAL")
     b25 = signals.generate_if(fs, int(fs * 0.1) + 300000, gs, seed=2)
