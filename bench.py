@@ -1,25 +1,30 @@
 #!/usr/bin/env python3
 """Benchmark: IF Msamples/s processed & tracked channels sustained (BASELINE.json `metric`).
 
-Workload (N=1: BASELINE.json configs[1], "GPS L1 C/A, 12 channels, 4 Msps synthetic IF, HIP
-multicorrelator on 1 MI355X"):
-  * a 1-second synthetic IF block (4 Msps gr_complex, 32 MB) resident in HBM; 32 GPS satellites
-    present (SURVEY.md §8d model, CN0 45 dB-Hz, seed 0x6E550002);
-  * each rank runs one 12-channel receiver: channel c tracks satellite c mod 32;
-  * one step = the multicorrelator hot path over that block: every channel-epoch of the second
-    (12 × 1000 epochs, N = vector_length = 4000 samples, E/P/L taps at ±0.25 chip) as one
-    batched launch (rotator-anchor replay + correlation).  The NCO of every epoch comes from the
-    synthetic truth, i.e. what a locked DLL/PLL would command (the loop filters are §8f row f1).
-Multi-GPU (torchrun, one process per GPU): rank 0 fans the IF block out over RCCL (the reference
-connects one conditioner output to every channel) before the timed region, so that every rank starts
-with its input resident in HBM as the N=1 run does; every rank correlates its own 12 channels (weak
-scaling).  value = Σ_ranks IF samples processed ÷ max-over-ranks wall time.  The per-step exchange
-of a streaming receiver (RCCL broadcast of the next block, as int8 ibyte, overlapped with the
-correlation) is measured in the same run and reported as `streaming_ibyte`.
+Headline (`value`): a D-second synthetic IF file processed with ALL C channels in
+steady-state closed-loop tracking — BASELINE.json configs[1]: GPS L1 C/A, 12 channels, 4 Msps
+gr_complex, one MI355X per rank.
+  * the file: 32 GPS satellites (SURVEY §8d model, CN0 45 dB-Hz, seed 0x6E550002) with navigation
+    bits (the TLM preamble recurring every 260 ms), generated on the GPU (signals.generate_if_device)
+    and resident in HBM before the timed region;
+  * the receiver: dll_pll_veml_tracking for 12 channels (channel c tracks satellite c), started from
+    an acquisition stamped 11 s before the file's first sample (the reference's 10 s pull-in is over,
+    dll_pll_veml_tracking.cc:1746-1752) and pre-rolled 0.5 s, so every channel is bit-synchronised
+    (state 4) before the warm-up steps;
+  * one step = the closed loop over the next D seconds of the file (every channel runs every epoch
+    whose window lies in it: correlation + DLL/PLL update + lock detectors, on the device, one
+    persistent launch, trk_persist.hip), steps consecutive in the file.
+  value = Σ_ranks fs·D·steps ÷ max-over-ranks wall (weak scaling: every rank tracks its own 12
+  channels of the same RCCL-broadcast file).  The rotator variant is the one volk_gnsssdr dispatches
+  on this host (gnsship_rotator_dispatch: AVX on x86 hosts with AVX), named in `config`.
+tracked_channels_sustained: channel sweep (12 … 65536 channels on one GPU, the same file and loop)
+  → the largest channel count the GPU keeps at ≥ real time, from the measured channel-epochs/s.
 
-Also reported: the dominant kernel's HBM roofline (HIP events on the engine stream), a CPU baseline
-(the oracle port at -O3 -march=native, threaded, on a bounded sample of the same workload, rank 0
-at N=1), and the PCPS acquisition sweep rate (32 PRNs × 40 Doppler bins, N = 4000).
+Auxiliary lines (never `value`): the generic-rotator closed loop, closed loops at 25 Msps (GPS and
+the Galileo E1 C4 share), the open-loop batched correlator (round 1's headline, truth NCOs), PCPS
+acquisition sweeps (C1-shape, C3, E1), the open-loop C4/C5 legs, and the multi-rank streaming leg.
+cpu_baseline: the oracle's closed loop (same loop, same rotator variant, scalar C) with one thread
+per channel on the host's cores, on a bounded sample of the same file, rank 0 at N = 1.
 """
 from __future__ import annotations
 
@@ -27,6 +32,7 @@ import argparse
 import json
 import os
 import sys
+import threading
 import time
 
 import numpy as np
@@ -40,7 +46,11 @@ N_CH = 12               # channels per receiver (configs[1])
 N_SATS = 32
 SHIFTS = [-0.25, 0.0, 0.25]   # Dll_Pll_Conf early_late_space_chips = 0.25 (dll_pll_conf.h:50)
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
+VALU_PEAK = 256 * 4 * 2.4e9 / 2.0  # wave64 VALU instructions/s: 256 CUs x 4 SIMDs, 2 cycles per wave64 op at 2.4 GHz
 SEED = 0x6E550002
+T_START_S = 11.0        # tracking starts this long after the acquisition stamp (pull_in_time_s = 10 elapsed)
+PRE_ROLL_S = 0.5        # untimed: bit synchronisation (state 2 -> 4)
+GPS_NAV = "1000101100110"  # 10001011 preamble + 5 bits: the sync pattern every 13 bits = 260 ms
 
 
 def parse():
@@ -48,22 +58,239 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--seconds", type=float, default=1.0, help="IF block length per step [s]")
-    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline time budget (0 = skip)")
-    ap.add_argument("--no-acq", action="store_true")
-    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_corr.json"),
-                    help="rocprofv3 PMC summary giving HBM bytes per launch (optional)")
+    ap.add_argument("--seconds", type=float, default=1.0, help="IF seconds per step (D)")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline time budget (0 = skip)")
+    ap.add_argument("--no-aux", action="store_true", help="headline only (no auxiliary lines)")
+    ap.add_argument("--rotator", type=int, default=-1, help="-1 volk's dispatch on this host, 0 generic, 1 AVX")
+    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_trk.json"),
+                    help="rocprofv3 PMC summary of the headline kernel (HBM bytes, VALU instructions per launch)")
     return ap.parse_args()
 
 
-def build_block(seconds: float):
+# ---------------------------------------------------------------------------------------------------
+# closed loop
+def gps_sky(n=N_SATS, seed=SEED, fs=FS):
     from gnss_sim_receiver_amd import signals
-    sats = signals.random_sky(N_SATS, seed=SEED)
-    n = int(round(FS * seconds)) + 2 * VL
-    return sats, signals.generate_if(FS, n, sats, seed=SEED), n
+    sats = signals.random_sky(n, seed=seed)
+    for s in sats:
+        s.bits = GPS_NAV
+    return sats
 
 
-N_RING = 3  # receivers per rank, stepped in a ring (pipelined anchor replay, see step())
+class Receiver:
+    """n_ch channels of dll_pll_veml_tracking on one engine, channel c tracking sats[c % len(sats)],
+    started from truth acquisitions stamped at sample 0 with tracking from absolute sample `first`."""
+
+    def __init__(self, ctx, system, fs, vl, sats, n_ch, first, rotator, code_base=300):
+        from gnss_sim_receiver_amd import abi, engine, signals
+        sysid = {"GPS": abi.SYS_GPS_L1CA, "GAL": abi.SYS_GAL_E1, "BDS": abi.SYS_BDS_B1I}[system]
+        self.conf = abi.TrkConf.defaults(sysid, fs, vl, rotator=rotator)
+        self.trk = engine.DllPllVemlTracking(ctx, self.conf, n_ch)
+        self.n_ch, self.vl, self.fs = n_ch, vl, fs
+        for i, s in enumerate(sats):
+            ctx.set_code(code_base + 2 * i, s.code)
+            if s.code_data is not None:
+                ctx.set_code(code_base + 2 * i + 1, s.code_data)
+        for ch in range(n_ch):
+            i = ch % len(sats)
+            s = sats[i]
+            self.trk.start(ch, code_base + 2 * i, signals.acq_delay_samples(s, fs, 0, first), s.doppler_hz, 0, first,
+                           data_code_id=code_base + 2 * i + 1, prn=s.prn)
+
+    def run(self, dev_ptr, fmt, first, n):
+        return self.trk.run_ptr(dev_ptr, fmt, first, n, 1 << 20)
+
+    def close(self):
+        self.trk.close()
+
+
+def rotator_name(r):
+    return {0: "generic (volk_gnsssdr_32fc_32f_rotator_dot_prod_32fc_xn_generic)",
+            1: "u_avx/a_avx (volk_gnsssdr_32fc_32f_rotator_dot_prod_32fc_xn.h:155-316)"}[r]
+
+
+def closed_loop_steps(ctx, rx, dev_ptr, t0_abs, fs, step_s, n_steps, barrier=None, timed=True):
+    """Run n_steps consecutive D-second segments of the file through the receiver.  Each segment is
+    passed with a little slack on both sides (the channels' epoch windows straddle the boundaries;
+    every channel consumes each sample once).  Returns (wall, kernel_ms list)."""
+    step_n = int(round(step_s * fs))
+    slack = 2 * rx.vl
+    kms = []
+    if barrier:
+        barrier()
+    t0 = time.perf_counter()
+    for i in range(n_steps):
+        lo = t0_abs + i * step_n - slack
+        ctx.event_record(0)
+        rx.run(dev_ptr[0] + (lo - dev_ptr[1]) * 8, 0, lo, step_n + 2 * slack)
+        ctx.event_record(1)
+        if timed:
+            kms.append(ctx.event_elapsed_ms(0, 1))
+    if barrier:
+        barrier()
+    return time.perf_counter() - t0, kms
+
+
+def headline(ctx, torch, args, rank, world, device, barrier):
+    from gnss_sim_receiver_amd import abi, sharding, signals
+    rot = args.rotator if args.rotator >= 0 else abi.rotator_dispatch()
+    sats = gps_sky()
+    first = int(T_START_S * FS)
+    n_total = int(round((PRE_ROLL_S + (args.warmup + args.steps) * args.seconds) * FS)) + 4 * VL
+    # the file, resident in HBM on every rank: rank 0 generates it, one RCCL broadcast fans it out
+    if rank == 0:
+        x = signals.generate_if_device(FS, n_total, sats, seed=SEED, start=first - 2 * VL, device=f"cuda:{device}")
+    else:
+        x = torch.empty(n_total, dtype=torch.complex64, device=f"cuda:{device}")
+    if world > 1:
+        sharding.broadcast_block(x, src=0)
+    torch.cuda.synchronize()
+    base = (x.data_ptr(), first - 2 * VL)  # (device pointer, absolute index of x[0])
+    chans = [(rank * N_CH + c) % N_SATS for c in range(N_CH)]
+    rx = Receiver(ctx, "GPS", FS, VL, [sats[i] for i in chans], N_CH, first, rot)
+    # pre-roll: bit synchronisation, then the warm-up steps
+    pre_n = int(round(PRE_ROLL_S * FS))
+    rx.run(base[0] + 2 * VL * 8, 0, first, pre_n + 2 * VL)
+    st = rx.trk.states()
+    closed_loop_steps(ctx, rx, base, first + pre_n, FS, args.seconds, args.warmup, timed=False)
+    t_timed = first + pre_n + int(round(args.warmup * args.seconds * FS))
+    wall, kms = closed_loop_steps(ctx, rx, base, t_timed, FS, args.seconds, args.steps, barrier=barrier)
+    st_end = rx.trk.states()
+    wall = sharding.max_over_ranks(wall)
+    rx.close()
+    return dict(rotator=rot, wall=wall, kernel_ms=float(np.mean(kms)), states_pre=st, states_end=st_end, x=x, base=base, sats=sats,
+                first=first)
+
+
+def sweep(ctx, h, rot, counts, rounds=100):
+    """Tracked channels sustained: channels c -> satellite c mod 32 on the same file, `rounds`
+    epochs each from the steady-state point of the headline run."""
+    out = []
+    t_abs = h["first"]
+    pre = 450  # epochs: every channel bit-synchronised (state 4) before the timed epochs
+    for n in counts:
+        rx = Receiver(ctx, "GPS", FS, VL, h["sats"], n, t_abs, rot, code_base=2000)
+        n_samp = rounds * VL + 4 * VL
+        rx.run(h["base"][0] + (t_abs - h["base"][1]) * 8, 0, t_abs, (pre + 2) * VL)
+        lo = t_abs + pre * VL
+        ctx.event_record(2)
+        t0 = time.perf_counter()
+        done = rx.run(h["base"][0] + (lo - h["base"][1]) * 8, 0, lo, n_samp)
+        dt = time.perf_counter() - t0
+        ctx.event_record(3)
+        k_ms = ctx.event_elapsed_ms(2, 3)
+        idx = np.linspace(0, n - 1, min(n, 64)).astype(int)
+        tracking = float(np.mean([rx.trk.channel_state(int(c))[0] in (2, 3, 4) for c in idx]))
+        rx.close()
+        cps = n * done / dt
+        out.append({"channels": n, "epochs": done, "us_per_epoch_round": round(dt / done * 1e6, 2),
+                    "kernel_us_per_round": round(k_ms * 1e3 / done, 2), "channel_epochs_per_s": round(cps, 0),
+                    "realtime_factor": round(done * 1e-3 / dt, 2), "tracking_fraction_sampled": round(tracking, 3)})
+    return out
+
+
+def closed_loop_aux(ctx, torch, device, system, fs, vl, n_ch, seconds, rot, seed):
+    """Closed loop at another rate / signal: n_ch channels, 0.5 s pre-roll (synchronisation), then `seconds` timed."""
+    from gnss_sim_receiver_amd import signals
+    if system == "GAL":
+        prns = [1, 5, 12, 19, 24, 30, 33, 36, 2, 8, 11, 26][:n_ch]
+        sats = signals.random_sky(n_ch, seed=seed, system="GAL", prns=prns)
+        for s in sats:
+            s.secondary = "0011100000001010110110010"
+            s.bits = "0110"
+        period = 0.004
+    else:
+        sats = gps_sky(n_ch, seed=seed)
+        period = 0.001
+    first = int(T_START_S * fs)
+    pre = int(0.5 * fs)
+    n_total = pre + int(round(seconds * fs)) + 4 * vl
+    x = signals.generate_if_device(fs, n_total, sats, seed=seed, start=first - 2 * vl, device=f"cuda:{device}")
+    torch.cuda.synchronize()
+    base = (x.data_ptr(), first - 2 * vl)
+    rx = Receiver(ctx, system, fs, vl, sats, n_ch, first, rot, code_base=1500)
+    rx.run(base[0] + 2 * vl * 8, 0, first, pre + 2 * vl)
+    lo = first + pre - 2 * vl
+    ctx.event_record(2)
+    t0 = time.perf_counter()
+    done = rx.run(base[0] + (lo - base[1]) * 8, 0, lo, int(round(seconds * fs)) + 4 * vl)
+    dt = time.perf_counter() - t0
+    ctx.event_record(3)
+    st = rx.trk.states()
+    rx.close()
+    del x
+    sig_s = done * period
+    return {"config": f"{system} {'L1 C/A' if system == 'GPS' else 'E1 B/C (5 VEML pilot taps + data prompt)'}, {n_ch} ch, "
+                      f"{fs / 1e6:g} Msps, N={vl}, closed DLL/PLL loop, rotator {rot}",
+            "epochs": done, "ms_per_signal_second": round(dt / sig_s * 1e3, 3), "realtime_factor": round(sig_s / dt, 1),
+            "us_per_epoch_round": round(dt / done * 1e6, 2), "if_msamples_per_s": round(sig_s * fs / dt / 1e6, 1),
+            "channels_in_state_4": int(np.sum(st == 4))}
+
+
+# ---------------------------------------------------------------------------------------------------
+# CPU baseline: the oracle's closed loop, one thread per channel (ctypes releases the GIL)
+def cpu_baseline(h, budget_s):
+    from oracle import trk as T
+    from gnss_sim_receiver_amd import signals
+    import platform
+    from oracle import oracle as O
+    O.build()
+    rot = h["rotator"]
+    # bounded sample of the same file (host copy of the first 0.6 s after the pre-roll start)
+    n_s = int(0.6 * FS)
+    x = h["x"][: n_s + 4 * VL].cpu().numpy()
+    first, base_abs = h["first"], h["base"][1]
+    threads = min(16, len(os.sched_getaffinity(0)))
+    k = T.conf("GPS", FS, VL, rotator_avx=1 if rot == 1 else 0)
+    sats = h["sats"]
+    work = [(c % N_CH) for c in range(threads)]
+    done_epochs = [0] * threads
+    stop = [False]
+
+    def worker(t):
+        s = sats[work[t]]
+        delay = signals.acq_delay_samples(s, FS, 0, first)
+        while not stop[0]:
+            ch = T.Channel(k, s.code, delay, s.doppler_hz, 0, first, fast=True)
+            rec = ch.run(x, base_abs, 500)
+            done_epochs[t] += len(rec)
+            if len(rec) == 0:
+                break
+
+    ths = [threading.Thread(target=worker, args=(t,)) for t in range(threads)]
+    t0 = time.perf_counter()
+    for th in ths:
+        th.start()
+    time.sleep(budget_s)
+    stop[0] = True
+    for th in ths:
+        th.join()
+    dt = time.perf_counter() - t0
+    ep = sum(done_epochs)
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    chan_sps = ep * VL / dt
+    return {"value": round(chan_sps / N_CH / 1e6, 2), "unit": "Msamples/s",
+            "cores": threads, "kind": "port",
+            "sample": f"{ep} channel-epochs of the closed loop (oracle/trk_oracle.c, rotator {rot}, -O3 -march=native) "
+                      f"on 0.6 s of the same file, {threads} threads (one channel each) for {dt:.1f} s; value = channel-samples/s ÷ "
+                      f"{N_CH} channels, i.e. the IF rate at which this host would keep {N_CH} channels",
+            "channel_msamples_per_s": round(chan_sps / 1e6, 2),
+            "cpu_model": model, "machine": platform.machine(),
+            "reference_avx_note": "scalar C restatement; SURVEY §6 measured the reference's own AVX correlator at 268 M "
+                                  "channel-samples/s per core in the survey container"}
+
+
+# ---------------------------------------------------------------------------------------------------
+# round 1's open-loop legs (auxiliary)
+N_RING = 3
 
 
 def receiver_jobs(sats, rank: int, seconds: float):
@@ -74,7 +301,6 @@ def receiver_jobs(sats, rank: int, seconds: float):
         s = sats[c % N_SATS]
         cid = code_ids.setdefault(s.prn, len(code_ids))
         jobs.append(signals.truth_jobs(s, FS, n_ep, VL, SHIFTS, cid))
-    # epoch-major: the channels of one epoch read the same samples back to back (L2 reuse)
     jobs = np.stack(jobs, axis=1).reshape(-1)
     codes = [None] * len(code_ids)
     for prn, cid in code_ids.items():
@@ -82,32 +308,46 @@ def receiver_jobs(sats, rank: int, seconds: float):
     return jobs, codes
 
 
-def cpu_baseline(block, jobs, codes, budget_s):
-    """Oracle port (generic semantics, -O3 -march=native, pthreads) on the same block and jobs,
-    repeated until the time budget is spent (bounded sample)."""
-    from oracle import oracle as O
-    O.build()
-    threads = min(16, len(os.sched_getaffinity(0)))
-    O.corr_batch(block, jobs[: N_CH * 10], codes, n_threads=threads, fast=True)  # warm
-    reps, t0 = 0, time.perf_counter()
-    per = max(N_CH, (len(jobs) // N_CH // 10) * N_CH)  # 1/10 of the block per call
-    done_jobs = 0
-    while time.perf_counter() - t0 < budget_s:
-        lo = (reps * per) % len(jobs)
-        sl = jobs[lo: lo + per]
-        O.corr_batch(block, sl, codes, n_threads=threads, fast=True)
-        done_jobs += len(sl)
-        reps += 1
-    dt = time.perf_counter() - t0
-    epochs = done_jobs / N_CH
-    msps = epochs * VL / dt / 1e6
-    return {"value": round(msps, 2), "unit": "Msamples/s", "cores": threads, "kind": "port",
-            "sample": f"{done_jobs} channel-epochs ({epochs:.0f} epochs × {N_CH} ch, N={VL}, 3 taps) of the same block in {dt:.1f} s, "
-                      f"oracle/gnss_oracle.c generic semantics at -O3 -march=native, {threads} pthreads",
-            "channel_msps": round(done_jobs * VL / dt / 1e6, 2)}
+def open_loop_correlator(ctx, torch, device, steps=20):
+    """Round 1's headline, kept as an auxiliary line: 12 000 channel-epochs of one second with
+    synthetic-truth NCOs (no loop filters) as one batched launch, three receivers in a ring."""
+    from gnss_sim_receiver_amd import abi, engine, signals
+    sats = signals.random_sky(N_SATS, seed=SEED)
+    n = FS + 2 * VL
+    x = signals.generate_if_device(FS, n, sats, seed=SEED, device=f"cuda:{device}")
+    torch.cuda.synchronize()
+    batches = []
+    for k in range(N_RING):
+        jk, ck = receiver_jobs(sats, k, 1.0)
+        jk["code_id"] += 32 * k
+        for cid, c in enumerate(ck):
+            ctx.set_code(32 * k + cid, c)
+        b = engine.CorrelatorBatch(ctx, len(jk))
+        b.set_jobs(jk, n)
+        batches.append(b)
+    for i in range(3):
+        batches[i % 3].launch_pipelined(x.data_ptr(), abi.FMT_CF32, batches[(i + 1) % 3], batches[(i + 2) % 3])
+    ctx.sync()
+    ctx.event_record(4)
+    t0 = time.perf_counter()
+    for i in range(steps):
+        batches[i % 3].launch_pipelined(x.data_ptr(), abi.FMT_CF32, batches[(i + 1) % 3], batches[(i + 2) % 3])
+    ctx.event_record(5)
+    ctx.sync()
+    wall = time.perf_counter() - t0
+    ms = ctx.event_elapsed_ms(4, 5) / steps
+    for b in batches:
+        b.close()
+    jobs = N_CH * 1000
+    byts = jobs * (8 * VL + 3 * 8)
+    return {"config": "12 GPS L1 C/A channels x 1000 epochs (1 s, 4 Msps), synthetic-truth NCOs, one batched launch per "
+                      "receiver-second, 3 receivers in a ring (gnsship_batch_launch_pipelined2)",
+            "if_msamples_per_s": round(FS * steps / wall / 1e6, 1), "ms_per_launch": round(ms, 4),
+            "channel_msamples_per_s": round(jobs * VL / (ms * 1e-3) / 1e6, 1),
+            "algorithmic_GBps": round(byts / (ms * 1e-3) / 1e9, 1)}
 
 
-def acq_bench(ctx, fs, n, sig, label):
+def acq_bench(ctx, fs, n, sig, label, present=None):
     """32-PRN all-sky PCPS sweep: 40 bins (±5 kHz / 250 Hz) × n-sample FFTs at fs."""
     from gnss_sim_receiver_amd import codes as C, engine
     acq = engine.PcpsAcquisition(ctx, fs, n, 5000, 250, 0, True, max_prns=32)
@@ -117,24 +357,27 @@ def acq_bench(ctx, fs, n, sig, label):
     for _ in range(3):
         acq.run(dev, n_prns=32)
     reps = 20
+    ctx.event_record(6)
     t0 = time.perf_counter()
     for _ in range(reps):
         res, _ = acq.run(dev, n_prns=32)
     dt = (time.perf_counter() - t0) / reps
-    found = sum(1 for r in res if r.test_statistic > 40)
+    ctx.event_record(7)
     cells = 32 * acq.n_bins
     out = {"config": label, "sweep_ms": round(dt * 1e3, 3),
-           "sweeps_per_s": round(1 / dt, 1), "cells_per_s": round(cells / dt, 0), "prns_detected": found,
+           "sweeps_per_s": round(1 / dt, 1), "cells_per_s": round(cells / dt, 0),
            "algorithmic_GBps": round(cells * 20 * n / dt / 1e9, 1)}
+    if present is not None:
+        stat = np.array([r.test_statistic for r in res])
+        out["prns_present"] = sorted(present)
+        out["present_min_test_statistic"] = round(float(min(stat[p - 1] for p in present)), 2)
+        out["absent_max_test_statistic"] = round(float(max(stat[k] for k in range(32) if k + 1 not in present)), 2)
     acq.close()
     dev.free()
     return out
 
 
 def acq_e1_bench(ctx, reps=5):
-    """Galileo E1 all-sky PCPS sweep (GalileoE1PcpsAmbiguousAcquisition, ms_per_code 4): 32 PRNs ×
-    40 bins (±5 kHz / 250 Hz) × 100000-point transforms (4 ms at 25 Msps, the huge FFT layout),
-    E1-B sinBOC(1,1) replicas, first-vs-second-peak statistic."""
     from gnss_sim_receiver_amd import codes as C, engine, signals as S
     fs, n = 25000000, 100000
     sats = S.random_sky(6, seed=SEED + 7, system="GAL", prns=[2, 9, 13, 21, 26, 31])
@@ -159,18 +402,13 @@ def acq_e1_bench(ctx, reps=5):
     return out
 
 
-def e1_bench(ctx, seconds=0.2, reps=10):
-    """C4 per-GPU share: 8 Galileo E1 channels at 25 Msps, 4 ms epochs (N = 100000),
-    5-tap VEML on the E1-C pilot + 1-tap prompt on the E1-B data replica per channel-epoch.  Three
-    batches of the block's jobs stepped in a ring with the pipelined anchor replay (as the headline
-    and C5 legs: a streaming receiver's consecutive blocks), so each launch carries half of the next
-    batches' 100000-step rotator chains instead of waiting for a whole one."""
+def e1_open_loop(ctx, seconds=0.2, reps=10):
     from gnss_sim_receiver_amd import abi, engine, signals as S
     fs, vl, nch = 25e6, 100000, 8
     sats = S.random_sky(nch, seed=SEED + 4, system="GAL", prns=[1, 5, 12, 19, 24, 30, 33, 36])
     n_ep = int(round(seconds * 250))
     sig = S.generate_if(fs, vl * (n_ep + 2), sats, seed=SEED + 4)
-    jobs, codes = [], []
+    jobs = []
     for k, s in enumerate(sats):
         pj = S.truth_jobs(s, fs, n_ep, vl, [-1.0, -0.5, 0.0, 0.5, 1.0], 100 + 2 * k)
         dj = pj.copy()
@@ -200,20 +438,13 @@ def e1_bench(ctx, seconds=0.2, reps=10):
         b.close()
     dev.free()
     if_msps = n_ep * vl / (ms * 1e-3) / 1e6
-    return {"config": "C4 per-GPU share: Galileo E1, 8 ch, 25 Msps, N=100000, 5 pilot taps + 1 data tap, gr_complex, "
-                      f"{seconds} s block, 3 batches in a ring",
+    return {"config": "C4 per-GPU share, open loop (truth NCOs): Galileo E1, 8 ch, 25 Msps, N=100000, 5 pilot taps + 1 data tap, "
+                      f"gr_complex, {seconds} s block, 3 batches in a ring",
             "ms_per_signal_second": round(ms / seconds, 4), "if_msamples_per_s": round(if_msps, 1),
-            "realtime_factor": round(if_msps * 1e6 / fs, 1),
-            "channels_sustained_realtime": int(nch * if_msps * 1e6 / fs),
-            "algorithmic_GBps": round(2 * nch * n_ep * vl * 8 / (ms * 1e-3) / 1e9, 1)}
+            "realtime_factor": round(if_msps * 1e6 / fs, 1), "algorithmic_GBps": round(2 * nch * n_ep * vl * 8 / (ms * 1e-3) / 1e9, 1)}
 
 
-def c5_bench(ctx, seconds=0.2, reps=6):
-    """C5 per-GPU share (256 channels over 8 GPUs): 32 channels = 12 GPS L1 C/A
-    (N = 50000, E/P/L) + 12 Galileo E1 (N = 200000, 5 pilot taps + 1 data tap) + 8 BeiDou B1I
-    (N = 50000, E/P/L) on one 50 Msps ibyte block (IF at +7.161 MHz for L1/E1, −7.161 MHz for B1I),
-    correlated straight from the int8 samples.  Three such receivers stepped in a ring with the
-    pipelined anchor replay, as the headline bench."""
+def c5_open_loop(ctx, seconds=0.2, reps=6):
     from gnss_sim_receiver_amd import abi, engine, signals as S
     fs, f_if = 50e6, 7.161e6
     sys_conf = (("GPS", 12, 50000, [-0.25, 0.0, 0.25], 1000), ("GAL", 12, 200000, [-1.0, -0.5, 0.0, 0.5, 1.0], 250),
@@ -261,239 +492,67 @@ def c5_bench(ctx, seconds=0.2, reps=6):
     for b in batches:
         b.close()
     dev.free()
-    span_s = seconds - 2 * 0.004  # the E1 epochs cover seconds − 2 code periods
+    span_s = seconds - 2 * 0.004
     rt = span_s / (ms * 1e-3)
-    return {"config": "C5 per-GPU share: 12 GPS L1 C/A + 12 Galileo E1 (5+1 taps) + 8 BeiDou B1I, 50 Msps ibyte, "
-                      f"{seconds} s block, 3 receivers in a ring",
+    return {"config": "C5 per-GPU share, open loop (truth NCOs): 12 GPS L1 C/A + 12 Galileo E1 (5+1 taps) + 8 BeiDou B1I, "
+                      f"50 Msps ibyte, {seconds} s block, 3 receivers in a ring",
             "ms_per_block": round(ms, 4), "realtime_factor": round(rt, 1),
             "if_msamples_per_s": round(fs * span_s / (ms * 1e-3) / 1e6, 1),
             "channel_msamples_per_s": round(chan_samples / (ms * 1e-3) / 1e6, 1),
-            "channels_sustained_realtime": int(32 * rt),
             "algorithmic_GBps": round(chan_samples * 2 / (ms * 1e-3) / 1e9, 1)}
 
 
-def trk_bench(ctx, block, sats, n_ch, rounds):
-    """Closed-loop tracking (gnsship_trk, §8f f1): n_ch GPS L1 C/A channels (channel c tracks
-    satellite c mod 32, started from truth acquisition at sample 0) stepped `rounds` epochs over the
-    HBM-resident block, loop state and correlator jobs on the device, no host round trip."""
-    from gnss_sim_receiver_amd import abi, engine
-    conf = abi.TrkConf.defaults(abi.SYS_GPS_L1CA, FS, VL)
-    trk = engine.DllPllVemlTracking(ctx, conf, n_ch)
-    for i, s in enumerate(sats):
-        ctx.set_code(300 + i, s.code)
-    for ch in range(n_ch):
-        i = ch % len(sats)
-        s = sats[i]
-        trk.start(ch, 300 + i, (s.code_delay_chips / s.code_freq()) * FS, s.doppler_hz, 0, 0)
-    dev = ctx.upload(block)
-    n = len(block)
-    trk.run(dev, 0, 3, n_buffer_samples=n, records=False)  # warm-up (first epochs of every channel)
-    t0 = time.perf_counter()
-    _, done = trk.run(dev, 0, rounds, n_buffer_samples=n, records=False)
-    dt = time.perf_counter() - t0
-    tracking = sum(1 for ch in range(n_ch) if trk.channel_state(ch)[0] in (2, 3, 4))
-    trk.close()
-    dev.free()
-    sig_s = done * 1e-3
-    return {"config": f"{n_ch} GPS L1 C/A channels, 4 Msps, closed DLL/PLL loop on the device, {done} epochs",
-            "ms_per_signal_second": round(dt / sig_s * 1e3, 3), "realtime_factor": round(sig_s / dt, 1),
-            "us_per_epoch_round": round(dt / done * 1e6, 2), "channel_epochs_per_s": round(n_ch * done / dt, 0),
-            "channels_still_tracking": tracking}
-
-
-def streaming_leg(ctx, torch, device, rank, world, block, n_samples, samples_per_step, batches, steps, warmup):
-    """The same receiver-seconds with the IF block in the front-end's ibyte format (int8 I/Q, 2 B per
-    sample, converted inside the correlator loads — IbyteToComplex, ibyte_to_complex.cc:39) and, at
-    N > 1, the exchange step of a streaming receiver: each step rank 0 broadcasts the NEXT block
-    over RCCL (double-buffered, on the communicator's stream) while every rank correlates the
-    current one.  Reported beside `value`, never as it."""
-    from gnss_sim_receiver_amd import abi, sharding, signals
-    nbytes = 2 * n_samples
-    if torch is not None:
-        bufs = [torch.zeros(nbytes, dtype=torch.int8, device=f"cuda:{device}") for _ in range(2)]
-        if rank == 0:
-            ib = torch.from_numpy(signals.to_ibyte(block).reshape(-1))
-            for t in bufs:
-                t.copy_(ib)
-        for t in bufs:
-            sharding.broadcast_block(t, src=0)
-        torch.cuda.synchronize()
-        ptrs = [t.data_ptr() for t in bufs]
-    else:
-        dbuf = ctx.upload(np.ascontiguousarray(signals.to_ibyte(block).reshape(-1)))
-        ptrs = [dbuf.ptr, dbuf.ptr]
-    cnt = [0]
-
-    def sstep():
-        i = cnt[0]
-        cnt[0] += 1
-        b, nb, nb2 = (batches[(i + m) % N_RING] for m in range(3))
-        if torch is None:
-            b.launch_pipelined(ptrs[0], abi.FMT_CI8, nb, nb2)
-            return
-        work = sharding.broadcast_block(bufs[(i & 1) ^ 1], src=0, async_op=True)
-        b.launch_pipelined(ptrs[i & 1], abi.FMT_CI8, nb, nb2)
-        ctx.sync()
-        work.wait()
-        torch.cuda.current_stream().synchronize()
-
-    def barrier():
-        if torch is not None:
-            torch.distributed.barrier()
-            torch.cuda.synchronize()
-        ctx.sync()
-
-    for _ in range(warmup):
-        sstep()
-    barrier()
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        sstep()
-    barrier()
-    wall = sharding.max_over_ranks(time.perf_counter() - t0)
-    out = {"format": "ibyte: int8 I/Q, 2 B/sample, converted in the correlator loads",
-           "if_msamples_per_s": round(world * samples_per_step * steps / wall / 1e6, 1),
-           "ms_per_step": round(wall / steps * 1e3, 4)}
-    if torch is not None:
-        barrier()
-        t0 = time.perf_counter()
-        for _ in range(steps):
-            sharding.broadcast_block(bufs[0], src=0)
-        torch.cuda.synchronize()
-        bwall = sharding.max_over_ranks(time.perf_counter() - t0)
-        out["exchange"] = f"RCCL broadcast of the next {nbytes / 1e6:.0f} MB ibyte block per step from rank 0, overlapped with the correlation"
-        out["bcast_ms_alone"] = round(bwall / steps * 1e3, 4)
-        out["bcast_GBps"] = round(nbytes / (bwall / steps) / 1e9, 1)
-    else:
-        out["exchange"] = "none (1 rank)"
-        dbuf.free()
-    return out
-
-
+# ---------------------------------------------------------------------------------------------------
 def main():
     args = parse()
-    from gnss_sim_receiver_amd import abi, engine, sharding
+    from gnss_sim_receiver_amd import engine, sharding
+    import torch
 
     rank, world, local_rank = sharding.dist_env()
-    if world != args.gpus:
-        if world == 1 and args.gpus > 1:
+    if world != args.gpus and not (world == 1 and args.gpus == 1):
+        if world == 1:
             raise SystemExit("--gpus N>1 must be launched with torch.distributed.run (one process per GPU)")
-    torch = None
     device = local_rank
     if world > 1:
-        import torch
         import torch.distributed as dist
-        # GNSSHIP_DIST_BACKEND=gloo + several ranks per GPU rehearses the multi-rank flow on a
-        # one-GPU box (RCCL refuses two ranks on one device); the production path is nccl (RCCL).
+        # GNSSHIP_DIST_BACKEND=gloo rehearses the multi-rank flow on a one-GPU box (RCCL refuses two
+        # ranks on one device); the production path is nccl (RCCL over xGMI).
         backend = os.environ.get("GNSSHIP_DIST_BACKEND", "nccl")
         device = local_rank % max(1, torch.cuda.device_count()) if backend != "nccl" else local_rank
         torch.cuda.set_device(device)
         dist.init_process_group(backend)
-
     ctx = engine.Context(device)
-    sats = None
-    if rank == 0:
-        sats, block, n_samples = build_block(args.seconds)
-    else:
-        from gnss_sim_receiver_amd import signals
-        sats = signals.random_sky(N_SATS, seed=SEED)  # same satellites (codes, truth) on every rank
-        n_samples = int(round(FS * args.seconds)) + 2 * VL
-        block = None
-
-    # IF block resident in HBM on every rank before the timed region, as the N=1 input is (the
-    # timed steps re-process the resident block; host→device ingest is not `value`).  Multi-GPU:
-    # rank 0 holds the block and fans it out over RCCL once (sharding.broadcast_block); the
-    # per-step exchange of a streaming receiver is measured separately (streaming_leg).
-    if torch is not None:
-        dev_t = torch.empty(n_samples, dtype=torch.complex64, device=f"cuda:{device}")
-        if rank == 0:
-            dev_t.copy_(torch.from_numpy(block))
-        sharding.broadcast_block(dev_t, src=0)
-        torch.cuda.synchronize()
-        dev_ptr = dev_t.data_ptr()
-    else:
-        dev_buf = ctx.upload(block)
-        dev_ptr = dev_buf.ptr
-
-    # Three 12-channel receivers per rank (channel sets 36r+12k .. 36r+12k+11, channel c tracking
-    # satellite c mod 32), stepped in a ring: each step is one full receiver-second, and the
-    # NCO-only anchor replay of the next two receivers' batches rides inside the current
-    # correlation launch, half a replay chain each (gnsship_batch_launch_pipelined2).
-    receivers, all_codes = [], {}
-    for k in range(N_RING):
-        jk, ck = receiver_jobs(sats, N_RING * rank + k, args.seconds)
-        jk["code_id"] += 32 * k  # receiver k's code-bank entries live at 32·k + id
-        for cid, c in enumerate(ck):
-            all_codes[32 * k + cid] = c
-        receivers.append((jk, ck))
-    jobs, codes = receivers[0]  # receiver 0 (code ids unshifted): CPU baseline + roofline split
-    for cid, c in sorted(all_codes.items()):
-        ctx.set_code(cid, c)
-    batches = []
-    for jk, _ in receivers:
-        b = engine.CorrelatorBatch(ctx, len(jk))
-        b.set_jobs(jk, n_samples)
-        batches.append(b)
-    batch = batches[0]
-
-    step_no = [0]
-
-    def step():
-        i = step_no[0]
-        step_no[0] += 1
-        b, nb, nb2 = (batches[(i + m) % N_RING] for m in range(3))
-        # each launch correlates this receiver, finishes the next one's rotator-anchor replay and
-        # starts the one after's (gnsship_batch_launch_pipelined2): one launch per step, one
-        # stream, no cross-stream event, no host synchronisation
-        b.launch_pipelined(dev_ptr, abi.FMT_CF32, nb, nb2)
-
-    for _ in range(args.warmup):
-        step()
-    ctx.sync()
 
     def barrier():
-        if torch is not None:
+        if world > 1:
             torch.distributed.barrier()
-            torch.cuda.synchronize()
+        torch.cuda.synchronize()
         ctx.sync()
 
-    barrier()
-    t0 = time.perf_counter()
-    ctx.event_record(0)
-    for _ in range(args.steps):
-        step()
-    ctx.event_record(1)
-    barrier()
-    wall = time.perf_counter() - t0
-    wall = sharding.max_over_ranks(wall)
-    launch_ms = ctx.event_elapsed_ms(0, 1) / args.steps
-
-    # per-kernel split on the same stream: anchors-only and correlate-only launches
-    def timed(stages, reps=max(5, args.steps)):
-        ctx.event_record(2)
-        for _ in range(reps):
-            batch.launch_ptr(dev_ptr, abi.FMT_CF32, stages)
-        ctx.event_record(3)
-        return ctx.event_elapsed_ms(2, 3) / reps
-
-    anchor_ms = timed(abi.STAGE_ANCHORS)
-    corr_ms = timed(abi.STAGE_CORRELATE)
-
-    epochs = int(round(args.seconds * 1000))
-    samples_per_step = epochs * VL                # IF samples each 12-channel receiver consumes
-    chan_samples = len(jobs) * VL                 # channel-samples correlated per rank per step
-    value = world * samples_per_step * args.steps / wall / 1e6
-    bytes_per_launch = chan_samples * 8 + len(jobs) * 3 * 8   # s·N + 8·T_out per channel-epoch (SURVEY §8d)
-    # dominant kernel = the one launch per step (correlation + next receiver's anchor replay),
-    # timed with HIP events on the engine stream over the timed region
-    achieved = bytes_per_launch / (launch_ms * 1e-3) / 1e9
-    traffic = None
+    h = headline(ctx, torch, args, rank, world, device, barrier)
+    wall = h["wall"]
+    samples = args.steps * args.seconds * FS
+    value = world * samples / wall / 1e6
+    k_ms = h["kernel_ms"]
+    chan_epochs = N_CH * args.seconds * 1000
+    bytes_launch = chan_epochs * (8 * VL + 8 * 3)          # s·N + 8·T_out per channel-epoch
+    achieved = bytes_launch / (k_ms * 1e-3) / 1e9
+    pmc = {}
     if os.path.exists(args.pmc):
         try:
-            traffic = json.load(open(args.pmc)).get("hbm_bytes_per_launch")
+            pmc = json.load(open(args.pmc))
         except Exception:
-            traffic = None
-
+            pmc = {}
+    valu = pmc.get("valu_insts_per_launch")
+    traffic = pmc.get("hbm_bytes_per_launch")
+    roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+            "kernel": "trk_persist_kernel (one launch per step)", "kernel_ms": round(k_ms, 4),
+            "binding": "latency: per channel the epoch chain derive -> phasor replay (N/16 dependent complex products, AVX "
+                       "variant) -> correlation tail -> reduction -> loop update; 12 channels occupy 12 of 256 CUs"}
+    if valu:
+        roof["valu"] = {"achieved": round(valu / (k_ms * 1e-3), 0), "peak": VALU_PEAK, "unit": "wave64 instr/s",
+                        "frac": round(valu / (k_ms * 1e-3) / VALU_PEAK, 5), "source": os.path.relpath(args.pmc, ROOT)}
     result = {
         "metric": "IF Msamples/sec processed & tracked-channels sustained @1/2/4/8 GPU",
         "value": round(value, 1),
@@ -506,41 +565,54 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f32",
-        "data": "synthetic",
-        "config": {"workload": "GPS L1 C/A, 12 channels, 4 Msps synthetic IF (gr_complex), HIP multicorrelator (configs[1])",
-                   "channels_per_gpu": N_CH, "fs_sps": FS, "vector_length": VL, "taps": 3, "block_s": args.seconds,
-                   "channel_epochs_per_step_per_gpu": int(len(jobs)), "nco": "synthetic truth (locked-loop NCO), loop filters = §8f f1",
-                   "parallelism": f"channels sharded over {world} rank(s); IF block RCCL-broadcast once, resident on every rank"},
-        "tracked_channels_sustained": int(world * chan_samples * args.steps / wall / FS),
-        "channel_msamples_per_s": round(world * chan_samples * args.steps / wall / 1e6, 1),
-        "kernel_ms": {"launch_total": round(launch_ms, 4),
-                      "split_corr_anchor_kernel_alone": round(anchor_ms, 4),
-                      "split_corr_batch_kernel_alone": round(corr_ms, 4)},
-        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic},
+        "data": "synthetic (SURVEY §8d IF model, generated on the GPU, resident in HBM)",
+        "config": {"workload": "GPS L1 C/A, 12 channels, 4 Msps gr_complex, closed-loop DLL/PLL steady-state tracking (configs[1])",
+                   "channels_per_gpu": N_CH, "fs_sps": FS, "vector_length": VL, "taps": 3, "step_s": args.seconds,
+                   "rotator": rotator_name(h["rotator"]), "tracking_states_before": np.bincount(h["states_pre"], minlength=5).tolist(),
+                   "tracking_states_after": np.bincount(h["states_end"], minlength=5).tolist(),
+                   "parallelism": f"channels sharded over {world} rank(s) (weak scaling); IF file RCCL-broadcast once, resident on every rank"},
+        "realtime_factor": round(samples / FS / wall, 1),
+        "us_per_epoch": round(wall / (args.steps * args.seconds * 1000) * 1e6, 2),
+        "roofline": roof,
     }
-    result["streaming_ibyte"] = streaming_leg(ctx, torch, device, rank, world, block, n_samples, samples_per_step, batches, args.steps, args.warmup)
-    if rank == 0 and world == 1 and args.cpu_seconds > 0:
-        result["cpu_baseline"] = cpu_baseline(block, jobs, codes, args.cpu_seconds)
-    if rank == 0 and not args.no_acq:
-        result["acquisition"] = acq_bench(ctx, FS, VL, block, "32 PRN x 40 bins, fft 4000, 4 Msps")
+    if rank == 0 and not args.no_aux:
+        counts = [12, 256, 1024, 4096, 16384, 65536]
+        sw = sweep(ctx, h, h["rotator"], counts)
+        best = max(sw, key=lambda r: r["channel_epochs_per_s"])
+        result["tracked_channels_sustained"] = int(best["channel_epochs_per_s"] / 1000.0)
+        result["channel_sweep"] = sw
+        result["tracked_channels_note"] = ("channel-epochs/s at the sweep's best point ÷ 1000 GPS epochs per channel-second; "
+                                           "channels beyond one workgroup per CU run in successive generations of the persistent kernel")
+        if h["rotator"] != 0:
+            g = Receiver(ctx, "GPS", FS, VL, [h["sats"][i] for i in range(N_CH)], N_CH, h["first"], 0, code_base=800)
+            pre = int(round(PRE_ROLL_S * FS))
+            g.run(h["base"][0] + 2 * VL * 8, 0, h["first"], pre + 2 * VL)
+            gw, _ = closed_loop_steps(ctx, g, h["base"], h["first"] + pre, FS, args.seconds, min(args.steps, 5))
+            g.close()
+            result["closed_loop_generic_rotator"] = {"config": "as value, rotator " + rotator_name(0),
+                                                      "if_msamples_per_s": round(min(args.steps, 5) * args.seconds * FS / gw / 1e6, 1),
+                                                      "realtime_factor": round(min(args.steps, 5) * args.seconds / gw, 1)}
+        result["closed_loop_gps_25msps"] = closed_loop_aux(ctx, torch, device, "GPS", 25e6, 25000, N_CH, 0.3, h["rotator"], SEED + 11)
+        result["closed_loop_e1_25msps_c4_share"] = closed_loop_aux(ctx, torch, device, "GAL", 25e6, 100000, 8, 0.4, h["rotator"], SEED + 12)
+        if world == 1 and args.cpu_seconds > 0:
+            result["cpu_baseline"] = cpu_baseline(h, args.cpu_seconds)
+        result["open_loop_correlator"] = open_loop_correlator(ctx, torch, device)
         from gnss_sim_receiver_amd import signals as S
-        sig25 = S.generate_if(25000000, 25000, sats, seed=2)
-        result["acquisition_c3"] = acq_bench(ctx, 25000000, 25000, sig25,
-                                             "C3: 32 PRN x 40 bins, fft 25000 (four-step), 25 Msps")
+        sky = S.random_sky(N_SATS, seed=SEED)
+        blk = S.generate_if(FS, VL, sky, seed=SEED)
+        result["acquisition"] = acq_bench(ctx, FS, VL, blk, "32 PRN x 40 bins, fft 4000, 4 Msps")
+        c3_present = list(range(1, 11))
+        c3 = S.random_sky(10, seed=0x6E550003, prns=c3_present)
+        sig25 = S.generate_if(25000000, 25000, c3, seed=0x6E550003)
+        result["acquisition_c3"] = acq_bench(ctx, 25000000, 25000, sig25, "C3: 32 PRN (10 present, seed 0x6E550003) x 40 bins, "
+                                             "fft 25000 (four-step), 25 Msps", present=c3_present)
         result["acquisition_e1"] = acq_e1_bench(ctx)
-    if rank == 0 and not args.no_acq:
-        result["tracking_c4_e1"] = e1_bench(ctx)
-        result["tracking_c5_hybrid"] = c5_bench(ctx)
-        if block is not None:
-            rounds = int(round(args.seconds * 1000)) - 8
-            result["closed_loop_c2"] = trk_bench(ctx, block, sats, N_CH, rounds)
-            result["closed_loop_1024ch"] = trk_bench(ctx, block, sats, 1024, min(rounds, 250))
-    for b in batches:
-        b.close()
+        result["tracking_c4_e1_open_loop"] = e1_open_loop(ctx)
+        result["tracking_c5_hybrid_open_loop"] = c5_open_loop(ctx)
+    del h
     if rank == 0:
         print(json.dumps(result), flush=True)
-    if torch is not None:
+    if world > 1:
         torch.distributed.barrier()
         torch.distributed.destroy_process_group()
     ctx.close()

@@ -454,6 +454,18 @@ class DllPllVemlTracking:
                                                 ctypes.byref(done)), "gnsship_trk_run_dump", self.ctx.h)
         return (out, done.value, dmp) if dump else (out, done.value)
 
+    def run_ptr(self, dev_ptr: int, fmt: int, buffer_first_sample: int, n_buffer_samples: int, max_rounds: int) -> int:
+        """general_work over a device IF buffer given as a raw pointer (e.g. a torch tensor's data_ptr,
+        or an offset into one), no records: returns the rounds run."""
+        done = ctypes.c_int()
+        check(self.ctx.lib.gnsship_trk_run_dump(self.h, ctypes.c_void_p(dev_ptr), fmt, 1, buffer_first_sample, n_buffer_samples, max_rounds,
+                                                None, None, ctypes.byref(done)), "gnsship_trk_run_dump", self.ctx.h)
+        return done.value
+
+    def states(self) -> np.ndarray:
+        """Tracking state (0 idle/lost, 2, 3, 4) of every channel."""
+        return np.array([self.channel_state(ch)[0] for ch in range(self.max_channels)], np.int32)
+
     @staticmethod
     def write_dump_files(prefix: str, records: np.ndarray, dumps: np.ndarray, append: bool = False) -> list:
         """The reference's per-channel tracking dump files (<prefix><channel>.dat, dll_pll_veml_tracking.cc:

@@ -179,3 +179,69 @@ def random_sky(n_sats: int, seed: int, system: str = "GPS", cn0: float = 45.0, p
     prns = list(range(1, n_sats + 1)) if prns is None else list(prns)
     return [Satellite(prn=p, doppler_hz=float(rng.uniform(-dmax, dmax)), code_delay_chips=float(rng.uniform(0, L)),
                       carrier_phase_rad=float(rng.uniform(0, 2 * np.pi)), cn0_dbhz=cn0, system=system) for p in prns]
+
+
+def generate_if_device(fs: float, n_samples: int, sats: list, seed: int = 0, start: int = 0, device: str = "cuda",
+                       block: int = 1 << 23, noise: bool = True):
+    """generate_if's signal model evaluated on the GPU with torch (bench inputs of many seconds:
+    ~100 M samples): returns a complex64 torch tensor on `device`.  Same x[n] as generate_if
+    (phases in float64), but the noise comes from torch's generator, so the samples are not
+    numpy's; the bench starts its channels from the same truth either way."""
+    import torch
+    g = torch.Generator(device=device)
+    g.manual_seed(int(seed))
+    out = torch.empty(n_samples, dtype=torch.complex64, device=device)
+    codes = {}
+    for b0 in range(0, n_samples, block):
+        b1 = min(n_samples, b0 + block)
+        n = torch.arange(start + b0, start + b1, dtype=torch.float64, device=device)
+        acc_re = torch.zeros(b1 - b0, dtype=torch.float64, device=device)
+        acc_im = torch.zeros_like(acc_re)
+        for s in sats:
+            key = id(s)
+            if key not in codes:
+                codes[key] = (torch.as_tensor(np.asarray(s.code, np.float64), device=device),
+                              None if s.code_data is None else torch.as_tensor(np.asarray(s.code_data, np.float64), device=device))
+            code, code_d = codes[key]
+            amp = float(np.sqrt(2.0 * 10.0 ** (s.cn0_dbhz / 10.0) / fs))
+            rate, _, fc, _ = SYSTEMS[s.system]
+            ph = n / fs * s.code_freq() - s.code_delay_chips
+            if s.doppler_rate_hz_s:
+                ph = ph + 0.5 * rate * s.doppler_rate_hz_s / fc * (n / fs) ** 2
+            chip = torch.floor(ph).to(torch.int64)
+            idx = torch.remainder(chip, s.code_len)
+            c = code[idx]
+            period = torch.div(chip, s.code_len, rounding_mode="floor")
+            if s.secondary:
+                sec = torch.as_tensor([1.0 if b == "0" else -1.0 for b in s.secondary], dtype=torch.float64, device=device)
+                c = c * sec[torch.remainder(period, len(sec))]
+            sign = 1.0
+            if s.bits:
+                pat = torch.as_tensor([1.0 if b == "0" else -1.0 for b in s.bits], dtype=torch.float64, device=device)
+                per_bit = s.symbols_per_bit or (1 if code_d is not None else 20)
+                sign = pat[torch.remainder(torch.div(period, per_bit, rounding_mode="floor"), len(pat))]
+            if code_d is not None:
+                c = (sign * code_d[idx] - c) / np.sqrt(2.0)
+            else:
+                c = c * sign
+            cp = 2.0 * np.pi * (s.f_if_hz + s.doppler_hz) * (n / fs) + s.carrier_phase_rad
+            if s.doppler_rate_hz_s:
+                cp = cp + np.pi * s.doppler_rate_hz_s * (n / fs) ** 2
+            acc_re += amp * c * torch.cos(cp)
+            acc_im += amp * c * torch.sin(cp)
+        if noise:
+            acc_re += torch.randn(b1 - b0, generator=g, dtype=torch.float64, device=device)
+            acc_im += torch.randn(b1 - b0, generator=g, dtype=torch.float64, device=device)
+        out[b0:b1] = torch.complex(acc_re.to(torch.float32), acc_im.to(torch.float32))
+    return out
+
+
+def acq_delay_samples(sat: Satellite, fs: float, stamp: int, first: int) -> float:
+    """Acq_delay_samples as an acquisition stamped at sample `stamp` reports it for a channel whose
+    tracking starts at `first`: the first code start at or after `first` (with code Doppler),
+    relative to the stamp modulo the nominal code period (pcps_acquisition.cc:693)."""
+    m = np.ceil(sat.chip_phase(np.float64(first), fs) / sat.code_len)
+    n0 = (m * sat.code_len + sat.code_delay_chips) * fs / sat.code_freq()
+    rate, L, _, _ = SYSTEMS[sat.system]
+    t_nom = L / rate * fs
+    return (first - stamp) + float(np.mod(n0 - first, t_nom))

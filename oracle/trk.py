@@ -109,8 +109,8 @@ def conf(system: str, fs_in: float, vector_length: int, prn: int = 0, **kw) -> O
     return c
 
 
-def _L():
-    L = lib()
+def _L(fast: bool = False):
+    L = lib(fast)
     if getattr(L, "_trk_ready", False):
         return L
     vp = ctypes.c_void_p
@@ -210,8 +210,10 @@ class Channel:
     """One oracle channel: start_tracking, then run() over successive buffers."""
 
     def __init__(self, k: OrcTrkConf, code: np.ndarray, acq_delay_samples: float, acq_doppler_hz: float, acq_samplestamp: int,
-                 first_sample: int, data_code: np.ndarray = None, prn: int = 0):
-        L = _L()
+                 first_sample: int, data_code: np.ndarray = None, prn: int = 0, fast: bool = False):
+        """fast: the same source built at -O3 -march=native (liboracle_fast.so), for timing only."""
+        self.fast = fast
+        L = _L(fast)
         self.k = k
         self.buf = ctypes.create_string_buffer(L.orc_trk_sizeof_channel())
         self.code = np.ascontiguousarray(code, np.float32)
@@ -222,7 +224,7 @@ class Channel:
     def run(self, samples: np.ndarray, buffer_first: int, max_epochs: int, dump: bool = False):
         """EPOCH_DTYPE records (and, with dump=True, the per-epoch DUMP_DTYPE records; rows whose
         epoch has flags & 16 are the ones log_data writes)."""
-        L = _L()
+        L = _L(self.fast)
         x = np.ascontiguousarray(samples, np.complex64)
         out = np.zeros(max_epochs, EPOCH_DTYPE)
         d = np.zeros(max_epochs, DUMP_DTYPE) if dump else None
@@ -233,11 +235,11 @@ class Channel:
 
     @property
     def state(self) -> int:
-        return _L().orc_trk_state(self.buf)
+        return _L(self.fast).orc_trk_state(self.buf)
 
     @property
     def next_sample(self) -> int:
-        return _L().orc_trk_nitems_read(self.buf)
+        return _L(self.fast).orc_trk_nitems_read(self.buf)
 
 
 def track(k: OrcTrkConf, samples: np.ndarray, code: np.ndarray, acq_delay_samples: float, acq_doppler_hz: float, acq_samplestamp: int,
