@@ -601,8 +601,8 @@ def main():
         sky = S.random_sky(N_SATS, seed=SEED)
         blk = S.generate_if(FS, VL, sky, seed=SEED)
         result["acquisition"] = acq_bench(ctx, FS, VL, blk, "32 PRN x 40 bins, fft 4000, 4 Msps")
-        c3_present = list(range(1, 11))
-        c3 = S.random_sky(10, seed=0x6E550003, prns=c3_present)
+        c3 = S.c3_sky()
+        c3_present = [s.prn for s in c3]
         sig25 = S.generate_if(25000000, 25000, c3, seed=0x6E550003)
         result["acquisition_c3"] = acq_bench(ctx, 25000000, 25000, sig25, "C3: 32 PRN (10 present, seed 0x6E550003) x 40 bins, "
                                              "fft 25000 (four-step), 25 Msps", present=c3_present)

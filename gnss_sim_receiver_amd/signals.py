@@ -245,3 +245,12 @@ def acq_delay_samples(sat: Satellite, fs: float, stamp: int, first: int) -> floa
     rate, L, _, _ = SYSTEMS[sat.system]
     t_nom = L / rate * fs
     return (first - stamp) + float(np.mod(n0 - first, t_nom))
+
+
+def c3_sky(cn0: float = 45.0):
+    """BASELINE.md C3: a 32-PRN all-sky sweep at 25 Msps with 10 PRNs present (seed 0x6E550003);
+    which 10 is drawn from the same seed."""
+    seed = 0x6E550003
+    rng = np.random.Generator(np.random.PCG64(seed))
+    prns = sorted(int(p) for p in rng.choice(np.arange(1, 33), 10, replace=False))
+    return random_sky(10, seed=seed, cn0=cn0, prns=prns)

@@ -14,6 +14,25 @@ from oracle import oracle as O
 
 pytestmark = pytest.mark.gpu
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
+TIE = 1.0 + 1e-4  # peak / second-largest grid value below this: a near-tie the float FFTs may order differently
+
+
+class ExactCount:
+    """Counts the (bin, index) comparisons made exactly and the near-tie skips, so that a test
+    cannot pass with zero exact comparisons."""
+
+    def __init__(self):
+        self.exact, self.ties = 0, []
+
+    def check(self, r, ref, rgrid, label):
+        flat = np.sort(rgrid.ravel())
+        if flat[-1] / flat[-2] > TIE:
+            assert (r.doppler_index, r.code_index) == (ref.doppler_index, ref.code_index), label
+            assert r.acq_delay_samples == ref.acq_delay_samples, label
+            self.exact += 1
+            return True
+        self.ties.append(label)
+        return False
 
 
 def test_golden_acquisition_cases(ctx):
@@ -61,12 +80,13 @@ def test_multi_prn_sweep_present_and_absent(ctx):
     for k, p in enumerate(prns):
         acq.set_local_code(codes.gps_l1_ca_code_gen_complex_sampled(p, fs), k)
     res, _ = acq.run(sig, n_prns=len(prns))
+    cnt = ExactCount()
     for k, p in enumerate(prns):
         ref, rgrid = O.pcps_acquisition_core(sig, codes.gps_l1_ca_code_gen_complex_sampled(p, fs), fs, dmax, step, 0, True)
-        flat = np.sort(rgrid.ravel())
-        if flat[-1] / flat[-2] > 1.0 + 1e-4:  # peak not a near-tie: must be exact
-            assert (res[k].doppler_index, res[k].code_index) == (ref.doppler_index, ref.code_index), p
+        exact = cnt.check(res[k], ref, rgrid, p)
+        assert exact or k >= 4, p  # every present PRN is compared exactly
         np.testing.assert_allclose(res[k].test_statistic, ref.test_statistic, rtol=2e-3)
+    assert cnt.exact >= 4 and len(cnt.ties) <= 2, (cnt.exact, cnt.ties)
     # noise-only CFAR statistic ≈ 2·ln(cells) ≈ 25 for 80 × 4000 cells; present PRNs far above
     absent_max = max(res[k].test_statistic for k in range(4, 8))
     assert absent_max < 40
@@ -138,12 +158,34 @@ def test_c3_25msps_four_step_matches_oracle(ctx):
         ref, rgrid = O.pcps_acquisition_core(sig, codes.gps_l1_ca_code_gen_complex_sampled(p, fs), fs, dmax, step, 0, True)
         # fp32 four-step vs complex128: grid within 1e-5 of the grid maximum
         assert np.max(np.abs(grid[k] - rgrid)) / rgrid.max() < 1e-5, p
-        flat = np.sort(rgrid.ravel())
-        if flat[-1] / flat[-2] > 1.0 + 1e-4:
-            assert (res[k].doppler_index, res[k].code_index) == (ref.doppler_index, ref.code_index), p
-            assert res[k].acq_delay_samples == ref.acq_delay_samples
+        assert ExactCount().check(res[k], ref, rgrid, p) or k == 2, p  # the present PRNs exactly
         np.testing.assert_allclose(res[k].test_statistic, ref.test_statistic, rtol=2e-3)
     assert res[0].test_statistic > 2 * res[2].test_statistic  # noise-only CFAR ≈ 2·ln(10⁶ cells) ≈ 28
+
+
+def test_c3_full_sweep_32_prns_baseline_signal(ctx):
+    """BASELINE.md C3 as specified: 32 PRNs × 40 bins × 25000 points at 25 Msps, 10 PRNs present
+    (signals.c3_sky, seed 0x6E550003), CFAR statistic.  Every PRN against the oracle; every present
+    PRN's (bin, index) exactly; near-ties (noise-only PRNs whose two largest cells differ by < 1e-4)
+    counted, not silently skipped."""
+    fs, n, dmax, step = 25000000, 25000, 5000, 250
+    present = signals.c3_sky()
+    present_prns = {s.prn for s in present}
+    prns = list(range(1, 33))
+    sig, res, _ = _acq_big_case(ctx, fs, n, prns, present, dmax, step, True, seed=0x6E550003)
+    cnt = ExactCount()
+    for k, p in enumerate(prns):
+        ref, rgrid = O.pcps_acquisition_core(sig, codes.gps_l1_ca_code_gen_complex_sampled(p, fs), fs, dmax, step, 0, True)
+        exact = cnt.check(res[k], ref, rgrid, p)
+        assert exact or p not in present_prns, p
+        np.testing.assert_allclose(res[k].test_statistic, ref.test_statistic, rtol=2e-3)
+    assert cnt.exact >= 28, (cnt.exact, cnt.ties)  # at most a few noise-only near-ties
+    # detection at 45 dB-Hz with 1 ms coherent integration is marginal for the weakest satellites
+    # (Doppler / code straddle losses): most present PRNs clear the noise-only maximum
+    stat = np.array([r.test_statistic for r in res])
+    absent = [stat[p - 1] for p in prns if p not in present_prns]
+    above = sum(stat[p - 1] > max(absent) for p in present_prns)
+    assert above >= 8 and np.median([stat[p - 1] for p in present_prns]) > 1.5 * np.median(absent), (sorted(present_prns), stat)
 
 
 def test_four_step_forced_at_small_size_first_vs_second(ctx, monkeypatch):
@@ -213,10 +255,7 @@ def test_huge_gps_50msps_multi_prn(ctx):
     for k, p in enumerate(prns):
         ref, rgrid = O.pcps_acquisition_core(sig, codes.gps_l1_ca_code_gen_complex_sampled(p, fs), fs, dmax, step, 0, True)
         assert np.max(np.abs(grid[k] - rgrid)) / rgrid.max() < 1e-5, p
-        flat = np.sort(rgrid.ravel())
-        if flat[-1] / flat[-2] > 1.0 + 1e-4:
-            assert (res[k].doppler_index, res[k].code_index) == (ref.doppler_index, ref.code_index), p
-            assert res[k].acq_delay_samples == ref.acq_delay_samples
+        assert ExactCount().check(res[k], ref, rgrid, p) or k == 2, p  # the present PRNs exactly
         np.testing.assert_allclose(res[k].test_statistic, ref.test_statistic, rtol=2e-3)
     assert min(res[0].test_statistic, res[1].test_statistic) > 2 * res[2].test_statistic
 
@@ -242,8 +281,10 @@ def test_huge_galileo_e1_25msps(ctx, cboc):
         ref, rgrid = O.pcps_acquisition_core(sig, lc[k], fs, dmax, step, 0, False, samples_per_chip=spc, samples_per_code=spcode)
         assert np.max(np.abs(grid[k] - rgrid)) / rgrid.max() < 1e-5, p
         flat = np.sort(rgrid.ravel())
-        if flat[-1] / flat[-2] > 1.0 + 1e-4:
+        if flat[-1] / flat[-2] > TIE:
             assert (res[k].doppler_index, res[k].code_index) == (ref.doppler_index, ref.code_index), p
+        else:
+            assert k == 2, p  # only the absent PRN may be a near-tie
         np.testing.assert_allclose(res[k].test_statistic, ref.test_statistic, rtol=2e-3)
     # the present satellites are found at their code delay (sinBOC samples → IF samples)
     for k, s in enumerate(present):

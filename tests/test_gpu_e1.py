@@ -80,3 +80,38 @@ def test_c5_e1_ibyte_50msps(ctx):
     jobs, cl = e1_jobs(sats, fs, 1, vl)
     out = engine.correlate_host(ctx, raw, jobs, cl)
     check(out, as_float, jobs, cl)
+
+
+def test_c5_hybrid_batch_one_launch(ctx):
+    """configs[4]'s per-GPU mix in ONE batched launch from the 50 Msps ibyte block: GPS L1 C/A
+    E/P/L (N = 50000) and Galileo E1 5 VEML pilot taps + data prompt (N = 200000) at IF +7.161 MHz,
+    BeiDou B1I E/P/L (N = 50000, 2046-chip code) at −7.161 MHz (the 1568.259 MHz centre, SURVEY §8d
+    C5).  Each job against the oracle on the same int8 samples (converted without scaling, as
+    IbyteToComplex, ibyte_to_complex.cc:39)."""
+    fs, f_if = 50e6, 7.161e6
+    gps = signals.random_sky(3, seed=551, system="GPS", cn0=48.0, prns=[3, 11, 27])
+    gal = signals.random_sky(2, seed=552, system="GAL", cn0=48.0, prns=[4, 19])
+    bds = signals.random_sky(2, seed=553, system="BDS", cn0=48.0, prns=[7, 30])
+    for s in gps + gal:
+        s.f_if_hz = f_if
+    for s in bds:
+        s.f_if_hz = -f_if
+    x = signals.generate_if(fs, 200000 * 3, gps + gal + bds, seed=56)
+    raw = signals.to_ibyte(x)
+    as_float = raw.astype(np.float32).view(np.complex64)
+    jobs, cl = [], []
+    for s in gps + bds:
+        cl.append(s.code)
+        jobs.append(signals.truth_jobs(s, fs, 4, 50000, [-0.25, 0.0, 0.25], len(cl) - 1))
+    ej, ecl = e1_jobs(gal, fs, 1, 200000)
+    ej["code_id"] += len(cl)
+    cl += ecl
+    jobs = np.concatenate(jobs + [ej])
+    rng = np.random.default_rng(5)
+    jobs["rem_carrier_phase_rad"] += rng.uniform(-0.3, 0.3, len(jobs)).astype(np.float32)
+    out = engine.correlate_host(ctx, raw, jobs, cl)
+    worst = check(out, as_float, jobs, cl)
+    assert worst <= TOL
+    # the locked prompts carry the signal (GPS / B1I prompt >> early/late noise)
+    epl = out[jobs["n_taps"] == 3]
+    assert np.median(np.abs(epl[:, 1]) / np.abs(epl[:, 0])) > 1.2  # ACF(0.25 chip) = 0.75 of the prompt
