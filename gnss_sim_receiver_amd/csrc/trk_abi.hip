@@ -485,6 +485,20 @@ extern "C" int gnsship_trk_stop(gnsship_trk* t, int channel)
     return GNSSHIP_OK;
 }
 
+extern "C" int gnsship_trk_telemetry_event(gnsship_trk* t, int channel, int tlm_event)
+{
+    if (!t) return GNSSHIP_E_INVAL;
+    gnsship_ctx* ctx = t->ctx;
+    if (channel < 0 || channel >= t->max_channels) return fail(ctx, GNSSHIP_E_INVAL, "gnsship_trk_telemetry_event: bad channel");
+    if (tlm_event != 1) return GNSSHIP_OK;  // only the telemetry fault is acted on (:623-629)
+    if (int rc = set_device(ctx)) return rc;
+    const int32_t forced = 200000;  // d_carrier_lock_fail_counter: force the loss-of-lock condition
+    HIP_TRY(ctx, hipMemcpyAsync(reinterpret_cast<char*>(t->chans_dev + channel) + offsetof(TrkChannel, carrier_fail), &forced, sizeof(forced),
+                     hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    return GNSSHIP_OK;
+}
+
 extern "C" int gnsship_trk_channel_state(gnsship_trk* t, int channel, int* state, uint64_t* next_sample)
 {
     if (!t) return GNSSHIP_E_INVAL;

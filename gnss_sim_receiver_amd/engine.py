@@ -426,6 +426,10 @@ class DllPllVemlTracking:
     def stop(self, channel: int):
         check(self.ctx.lib.gnsship_trk_stop(self.h, channel), "gnsship_trk_stop", self.ctx.h)
 
+    def telemetry_event(self, channel: int, tlm_event: int = 1):
+        """msg_handler_telemetry_to_trk (dll_pll_veml_tracking.cc:617-640): event 1 = telemetry fault."""
+        check(self.ctx.lib.gnsship_trk_telemetry_event(self.h, channel, tlm_event), "gnsship_trk_telemetry_event", self.ctx.h)
+
     def channel_state(self, channel: int):
         st, nx = ctypes.c_int(), ctypes.c_uint64()
         check(self.ctx.lib.gnsship_trk_channel_state(self.h, channel, ctypes.byref(st), ctypes.byref(nx)), "gnsship_trk_channel_state",

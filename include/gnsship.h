@@ -355,6 +355,10 @@ typedef struct gnsship_trk gnsship_trk;
 int gnsship_trk_create(gnsship_ctx* ctx, const gnsship_trk_conf* conf, int max_channels, gnsship_trk** out);
 int gnsship_trk_start(gnsship_trk* t, int channel, const gnsship_trk_start_args* args);
 int gnsship_trk_stop(gnsship_trk* t, int channel);
+/* msg_handler_telemetry_to_trk (dll_pll_veml_tracking.cc:617-640): a telemetry fault (tlm_event 1)
+ * from the channel's telemetry decoder sets the carrier lock-fail counter to 200000, so the next
+ * lock check of the loop declares loss of lock.  Other event values are ignored, as there. */
+int gnsship_trk_telemetry_event(gnsship_trk* t, int channel, int tlm_event);
 /* Runs up to max_rounds epochs of every tracking channel over the IF buffer holding absolute
  * samples [buffer_first_sample, +n_buffer_samples) (device pointer when sig_on_device, else host
  * memory staged to the device).  Per round each channel whose next vector_length window lies in

@@ -16,6 +16,7 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <thread>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -305,6 +306,7 @@ public:
     }
     ~Pcps_Acquisition_Hip()
     {
+        if (worker_.joinable()) worker_.join();
         if (h_) gnsship_acq_destroy(h_);
     }
     int fft_size() const { return fft_size_; }
@@ -396,15 +398,24 @@ public:
         }
     }
     bool blocking_on_standby{false};  // Acq_Conf::blocking_on_standby
+    // Acq_Conf::blocking (acq_conf.h, default true).  false: state 2 runs acquisition_core in a worker
+    // thread that holds the block's lock while it runs (pcps_acquisition.cc:602,1002-1006); general_work
+    // returns at once and, while the worker is active, consumes input only when the last dwell is in
+    // flight (:918-932).  The worker's decision is reported by the next general_work call.
+    bool blocking{true};
     uint64_t sample_counter() const { return sample_counter_; }
     const Acq_Outcome& gnss_synchro() const { return synchro_; }
+    bool worker_active() const { return worker_active_; }
     // One general_work call over n gr_complex samples: returns how many it consumed (consume_each)
     // and, when acquisition_core ran and decided, ACQ_SUCCESS / ACQ_FAIL in *event.
     int general_work(const std::complex<float>* in, int n, Acq_Event* event)
     {
-        *event = ACQ_NONE;
-        if (!active_) {
-            const int c = blocking_on_standby ? 0 : n;
+        std::unique_lock<std::mutex> lk(set_lock_);  // d_setlock (:917)
+        *event = pending_event_;
+        pending_event_ = ACQ_NONE;
+        if (!active_ || worker_active_) {
+            const bool consume = !active_ || (worker_active_ && counter_ == conf_.max_dwells);
+            const int c = (!blocking_on_standby && consume) ? n : 0;
             sample_counter_ += static_cast<uint64_t>(c);
             if (step_two_) {
                 fsm_state_ = 0;
@@ -431,11 +442,29 @@ public:
             return inc;
         }
         default: {
-            decide(buffer_.data(), event);
+            if (blocking) {
+                decide(buffer_.data(), event);
+            } else {
+                if (worker_.joinable()) worker_.join();  // the previous worker has released the lock
+                worker_active_ = true;
+                worker_ = std::thread([this]() {
+                    std::lock_guard<std::mutex> g(set_lock_);  // acquisition_core holds d_setlock (:602)
+                    Acq_Event ev = ACQ_NONE;
+                    decide(buffer_.data(), &ev);
+                    worker_active_ = false;  // :858
+                    pending_event_ = ev;
+                });
+            }
             buffer_count_ = 0;
             return 0;
         }
         }
+    }
+    // Wait for a non-blocking acquisition_core in flight (its decision is then pending for the next
+    // general_work call).
+    void join_worker()
+    {
+        if (worker_.joinable()) worker_.join();
     }
 
 private:
@@ -522,6 +551,10 @@ private:
         }
     }
 
+    std::mutex set_lock_;
+    std::thread worker_;
+    bool worker_active_ = false;
+    Acq_Event pending_event_ = ACQ_NONE;
     bool active_ = false;
     int fsm_state_ = 0;
     int buffer_count_ = 0;
@@ -647,6 +680,13 @@ public:
     {
         std::lock_guard<std::mutex> lk(dev_->mutex());
         return gnsship_trk_stop(h_, channel) == GNSSHIP_OK;
+    }
+    // msg_handler_telemetry_to_trk (dll_pll_veml_tracking.cc:617-640): the telemetry decoder's
+    // fault message (event 1) forces loss of lock at the channel's next lock check
+    bool msg_handler_telemetry_to_trk(int channel, int tlm_event)
+    {
+        std::lock_guard<std::mutex> lk(dev_->mutex());
+        return gnsship_trk_telemetry_event(h_, channel, tlm_event) == GNSSHIP_OK;
     }
     // general_work for every channel over gr_complex samples [first_sample, first_sample + n): up to
     // max_epochs epochs per channel; records (max_epochs × max_channels, optional) as gnsship_trk_epoch.

@@ -139,6 +139,7 @@ def _L(fast: bool = False):
     L.orc_trk_run.argtypes = [ctypes.POINTER(OrcTrkConf), vp, _f32p, ctypes.c_uint64, ctypes.c_int64, _f32p, ctypes.c_int, _f32p, ctypes.c_int,
                               vp, vp]
     L.orc_trk_set_prn.argtypes = [vp, ctypes.c_uint32]
+    L.orc_trk_telemetry_fault.argtypes = [vp]
     L.orc_trk_nitems_read.argtypes = [vp]
     L.orc_trk_nitems_read.restype = ctypes.c_uint64
     L.orc_trk_state.argtypes = [vp]
@@ -232,6 +233,10 @@ class Channel:
         n = L.orc_trk_run(ctypes.byref(self.k), self.buf, _ptr(x.view(np.float32)), buffer_first, len(x), _ptr(self.code), len(self.code),
                           _ptr(dc) if dc is not None else None, max_epochs, out.ctypes.data, d.ctypes.data if dump else None)
         return (out[:n], d[:n]) if dump else out[:n]
+
+    def telemetry_fault(self):
+        """msg_handler_telemetry_to_trk with tlm_event 1 (dll_pll_veml_tracking.cc:617-640)."""
+        _L(self.fast).orc_trk_telemetry_fault(self.buf)
 
     @property
     def state(self) -> int:

@@ -877,6 +877,9 @@ int orc_trk_sizeof_dump(void) { return (int)sizeof(orc_trk_dump); }
 void orc_trk_set_prn(orc_trk_channel* c, uint32_t prn) { c->prn = prn; }
 uint64_t orc_trk_nitems_read(const orc_trk_channel* c) { return c->nitems_read; }
 int orc_trk_state(const orc_trk_channel* c) { return c->state; }
+/* msg_handler_telemetry_to_trk (dll_pll_veml_tracking.cc:617-640): telemetry event 1 forces the
+ * loss-of-lock condition at the next lock check. */
+void orc_trk_telemetry_fault(orc_trk_channel* c) { c->carrier_fail = 200000; }
 
 int orc_multicorrelator_real_codes_ex(float* corr_out, const float* sig_in, const float* local_code, int code_length_chips,
     const float* shifts_chips, int n_correlators, int flags, float rem_carrier_phase_in_rad, float phase_step_rad,

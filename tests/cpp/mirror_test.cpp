@@ -261,7 +261,9 @@ static int acq_fsm_test()
         sig[i] = std::complex<float>(amp * cv * std::cos(2 * M_PI * 1500.0 * t) + g(gen), amp * cv * std::sin(2 * M_PI * 1500.0 * t) + g(gen));
     }
     int failures = 0;
-    for (int prn : {12, 20}) {
+    for (int mode = 0; mode < 4; mode++) {  // PRN 12 / 20, blocking / non-blocking worker (:1002-1006)
+        const int prn = (mode & 1) ? 20 : 12;
+        const bool blocking = mode < 2;
         gnsship::Acq_Conf conf;
         conf.fs_in = fs;
         conf.doppler_max = 5000;
@@ -274,23 +276,29 @@ static int acq_fsm_test()
         orc_gps_l1_ca_code_gen_complex_sampled(code.data(), prn, fs, 0);
         acq.set_local_code(reinterpret_cast<const std::complex<float>*>(code.data()));
         acq.init();
+        acq.blocking = blocking;
         acq.set_state(1);
         int pos = 0, calls = 0;
         gnsship::Pcps_Acquisition_Hip::Acq_Event ev = gnsship::Pcps_Acquisition_Hip::ACQ_NONE;
         while (ev == gnsship::Pcps_Acquisition_Hip::ACQ_NONE && pos < total && calls < 10000) {
             pos += acq.general_work(sig.data() + pos, std::min(700, total - pos), &ev);
+            if (!blocking && ev == gnsship::Pcps_Acquisition_Hip::ACQ_NONE) acq.join_worker();  // a GNU Radio scheduler would keep calling
             calls++;
         }
         const auto& r = acq.gnss_synchro();
-        std::printf("acq fsm prn %d: event %d after %d calls, %d samples; delay %.1f doppler %.1f stamp %llu stat %.2f thr %.2f\n", prn,
+        std::printf("acq fsm prn %d %s: event %d after %d calls, %d samples; delay %.1f doppler %.1f stamp %llu stat %.2f thr %.2f\n", prn,
+            blocking ? "blocking" : "non-blocking",
             static_cast<int>(ev), calls, pos, r.Acq_delay_samples, r.Acq_doppler_hz, static_cast<unsigned long long>(r.Acq_samplestamp_samples),
             r.test_statistics, acq.threshold());
+        // non-blocking: the decision is reported by the call after the worker's, which (the block
+        // being inactive again) consumes its 700 samples
+        const int extra = blocking ? 0 : 700;
         if (prn == 12) {
-            const bool ok = ev == gnsship::Pcps_Acquisition_Hip::ACQ_SUCCESS && pos == n && r.Acq_samplestamp_samples == static_cast<uint64_t>(n) &&
+            const bool ok = ev == gnsship::Pcps_Acquisition_Hip::ACQ_SUCCESS && pos == n + extra && r.Acq_samplestamp_samples == static_cast<uint64_t>(n) &&
                             std::fabs(r.Acq_delay_samples - 700.0) <= 2.0 && std::fabs(r.Acq_doppler_hz - 1500.0) <= 250.0;
             if (!ok) failures++;
         } else {
-            const bool ok = ev == gnsship::Pcps_Acquisition_Hip::ACQ_FAIL && pos == 3 * n && r.Acq_samplestamp_samples == static_cast<uint64_t>(3 * n);
+            const bool ok = ev == gnsship::Pcps_Acquisition_Hip::ACQ_FAIL && pos == 3 * n + extra && r.Acq_samplestamp_samples == static_cast<uint64_t>(3 * n);
             if (!ok) failures++;
         }
     }

@@ -120,3 +120,30 @@ def test_many_channels_and_ragged_buffers(ctx):
         ref = T.track(k, x, sats[ch].code, starts[ch][0], starts[ch][1], 0, 0, 200)
         d = np.concatenate([r1[:, ch][(r1[:, ch]["flags"] & 8) == 8], r2[:, ch][(r2[:, ch]["flags"] & 8) == 8]])
         compare(d[:len(ref)], ref[:len(d)], f"ch{ch}")
+
+
+@pytest.mark.parametrize("avx", [False, True])
+def test_telemetry_fault_forces_loss_of_lock(ctx, avx):
+    """msg_handler_telemetry_to_trk (dll_pll_veml_tracking.cc:617-640): a telemetry fault between
+    two runs sets the carrier lock-fail counter to 200000; the next epoch's lock check declares loss
+    of lock — the same epoch, with the same record, as the oracle loop given the same event."""
+    sat, k, x, stamp, first, delay, dop = S.sync("GPS", 4e6, 300, rotator_avx=1 if avx else 0)
+    c = dev_conf(k, "GPS")
+    c.rotator = abi.ROTATOR_AVX if avx else abi.ROTATOR_GENERIC
+    trk = engine.DllPllVemlTracking(ctx, c, 1)
+    ctx.set_code(60, sat.code)
+    trk.start(0, 60, delay, dop, stamp, first)
+    ref_ch = T.Channel(k, sat.code, delay, dop, stamp, first)
+    r1, _ = trk.run(x, first, 120)
+    o1 = ref_ch.run(x, first, 120)
+    compare(r1[:, 0], o1, "before")
+    trk.telemetry_event(0, 2)  # not a fault: ignored
+    trk.telemetry_event(0, 1)
+    ref_ch.telemetry_fault()
+    r2, _ = trk.run(x, first, 20)
+    o2 = ref_ch.run(x, first, 20)
+    d = r2[:, 0][(r2[:, 0]["flags"] & 8) == 8]
+    assert len(d) == len(o2) == 1 and (d["flags"][0] & 2) and (o2["flags"][0] & 2)
+    compare(r2[:, 0], o2, "fault epoch")
+    assert trk.channel_state(0)[0] == 0
+    trk.close()

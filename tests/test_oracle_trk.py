@@ -224,3 +224,15 @@ def test_dump_records_follow_log_data(built):
     assert len(raw) == 96 * len(d)
     assert np.frombuffer(raw[28:36], "<u8")[0] == d["PRN_start_sample_count"][0]
     assert np.frombuffer(raw[92:96], "<u4")[0] == sat.prn
+
+
+def test_oracle_telemetry_fault_loss_of_lock():
+    """dll_pll_veml_tracking.cc:617-640: after the fault the next lock check reports loss of lock."""
+    import trk_scenarios as S
+    sat, k, x, stamp, first, delay, dop = S.sync("GPS", 4e6, 60)
+    ch = T.Channel(k, sat.code, delay, dop, stamp, first)
+    r = ch.run(x, first, 40)
+    assert not np.any(r["flags"] & 2)
+    ch.telemetry_fault()
+    r2 = ch.run(x, first, 10)
+    assert len(r2) == 1 and r2["flags"][0] & 2 and ch.state == 0
