@@ -26,7 +26,7 @@ $(OBJDIR)/%.cpp.o: $(CSRC)/%.cpp $(HDRS)
 	$(HIPCC) $(HIPFLAGS) -x c++ -c $< -o $@
 
 $(LIB): $(OBJS)
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS) -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 
 oracle:
 	$(MAKE) -s -C oracle all
@@ -55,6 +55,6 @@ build/prof_obj/%.cpp.o: $(CSRC)/%.cpp $(HDRS)
 	@mkdir -p build/prof_obj
 	$(HIPCC) $(HIPFLAGS) -x c++ -c $< -o $@
 $(PROF_LIB): $(PROF_OBJS)
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(PROF_OBJS)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(PROF_OBJS) -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 prof: $(PROF_LIB)
 .PHONY: prof

@@ -17,11 +17,12 @@ REPO_DIR = os.path.dirname(PKG_DIR)
 LIB_PATH = os.path.join(PKG_DIR, "libgnsship.so")
 HEADER_PATH = os.path.join(REPO_DIR, "include", "gnsship.h")
 
-OK, E_INVAL, E_NOMEM, E_DEVICE, E_STATE = 0, -1, -2, -3, -4
+OK, E_INVAL, E_NOMEM, E_DEVICE, E_STATE, E_RCCL = 0, -1, -2, -3, -4, -5
 FMT_CF32, FMT_CI16, FMT_CI8 = 0, 1, 2
 STAGE_ANCHORS, STAGE_CORRELATE = 1, 2
 MAX_TAPS = 8
-_ERRNAMES = {E_INVAL: "E_INVAL", E_NOMEM: "E_NOMEM", E_DEVICE: "E_DEVICE", E_STATE: "E_STATE"}
+_ERRNAMES = {E_INVAL: "E_INVAL", E_NOMEM: "E_NOMEM", E_DEVICE: "E_DEVICE", E_STATE: "E_STATE", E_RCCL: "E_RCCL"}
+COMM_ID_BYTES = 128
 
 JOB_DTYPE = np.dtype(
     [
@@ -216,6 +217,13 @@ _SIGNATURES = {
     "gnsship_trk_run_dump": ([_vp, _vp, _i, _i, ctypes.c_uint64, ctypes.c_int64, _i, _vp, _vp, ctypes.POINTER(_i)], _i),
     "gnsship_trk_channel_state": ([_vp, _i, ctypes.POINTER(_i), ctypes.POINTER(ctypes.c_uint64)], _i),
     "gnsship_trk_destroy": ([_vp], _i),
+    "gnsship_comm_unique_id": ([_vp], _i),
+    "gnsship_comm_create": ([_vp, _i, _i, _vp, _vpp], _i),
+    "gnsship_comm_rank": ([_vp, ctypes.POINTER(_i), ctypes.POINTER(_i)], _i),
+    "gnsship_comm_broadcast": ([_vp, _vp, ctypes.c_size_t, _i], _i),
+    "gnsship_comm_allgather": ([_vp, _vp, _vp, ctypes.c_size_t], _i),
+    "gnsship_comm_allreduce_max_f64": ([_vp, _vp, ctypes.c_size_t], _i),
+    "gnsship_comm_destroy": ([_vp], _i),
 }
 
 

@@ -14,6 +14,7 @@
 //   general_work states 2 (:1789-1932), 3 (:1933-1970) and 4 (:1971-2028).
 #pragma once
 #include <cmath>
+#include <type_traits>
 
 #include "trk_engine.h"
 
@@ -128,9 +129,98 @@ __device__ bool lock_status(const TrkParams& k, TrkChannel& c, double coh_integr
     return true;
 }
 
+// The loop filters and NCO update of one epoch (run_dll_pll, update_tracking_vars) on a register
+// copy of the members they use: the persistent kernel loads it in one batch, computes without a
+// memory round trip per member, and stores it back only if the lock test beside it passes.  The
+// Tracking_loop_filter rings are kept in logical order (index 0 = newest).
+struct LoopRegs {
+    int32_t cloop, narrow, geo, pull_in;
+    float p[2], e[2], l[2], ve[2], vl[2], spc;
+    double carrier_phase_rate_step_rad;
+    float p_old[2], fp_w, fp_x, rem_carr_phase_rad;
+    float lfi[4], lfo[4];
+    int32_t lf_idx, current_prn_length_samples;
+    double carr_phase_error_hz, carr_error_filt_hz, carrier_doppler_hz, code_error_chips, code_error_filt_chips, code_freq_chips;
+    double K_blk_samples, carrier_phase_step_rad, code_phase_step_chips, acc_carrier_phase_rad, rem_code_phase_samples, rem_code_phase_chips;
+    LoopSet q;
+};
+
+__device__ __forceinline__ const LoopSet& loopset(const TrkParams& k, const TrkChannel& c) { return k.ls[c.narrow ? 1 + c.geo : 0]; }
+__device__ __forceinline__ const LoopSet& loopset(const TrkParams&, const LoopRegs& c) { return c.q; }
+
+__device__ __forceinline__ void load_regs(const TrkParams& k, const TrkChannel& c, LoopRegs& r)
+{
+    r.cloop = c.cloop;
+    r.narrow = c.narrow;
+    r.geo = c.geo;
+    r.pull_in = c.pull_in;
+    for (int i = 0; i < 2; i++) {
+        r.p[i] = c.p[i];
+        r.e[i] = c.e[i];
+        r.l[i] = c.l[i];
+        r.ve[i] = c.ve[i];
+        r.vl[i] = c.vl[i];
+        r.p_old[i] = c.p_old[i];
+    }
+    r.spc = c.spc;
+    r.carrier_phase_rate_step_rad = c.carrier_phase_rate_step_rad;
+    r.fp_w = c.fp_w;
+    r.fp_x = c.fp_x;
+    r.rem_carr_phase_rad = c.rem_carr_phase_rad;
+    r.lf_idx = c.lf_idx;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        r.lfi[i] = c.lf_inputs[(c.lf_idx + i) & 3];
+        r.lfo[i] = c.lf_outputs[(c.lf_idx + i) & 3];
+    }
+    r.current_prn_length_samples = c.current_prn_length_samples;
+    r.carr_phase_error_hz = c.carr_phase_error_hz;
+    r.carr_error_filt_hz = c.carr_error_filt_hz;
+    r.carrier_doppler_hz = c.carrier_doppler_hz;
+    r.code_error_chips = c.code_error_chips;
+    r.code_error_filt_chips = c.code_error_filt_chips;
+    r.code_freq_chips = c.code_freq_chips;
+    r.K_blk_samples = c.K_blk_samples;
+    r.carrier_phase_step_rad = c.carrier_phase_step_rad;
+    r.code_phase_step_chips = c.code_phase_step_chips;
+    r.acc_carrier_phase_rad = c.acc_carrier_phase_rad;
+    r.rem_code_phase_samples = c.rem_code_phase_samples;
+    r.rem_code_phase_chips = c.rem_code_phase_chips;
+    r.q = loopset(k, c);
+}
+
+// The members run_dll_pll / update_tracking_vars write.
+__device__ __forceinline__ void store_regs(const LoopRegs& r, TrkChannel& c)
+{
+    c.p_old[0] = r.p_old[0];
+    c.p_old[1] = r.p_old[1];
+    c.fp_w = r.fp_w;
+    c.fp_x = r.fp_x;
+    c.rem_carr_phase_rad = r.rem_carr_phase_rad;
+    c.lf_idx = r.lf_idx;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        c.lf_inputs[(r.lf_idx + i) & 3] = r.lfi[i];
+        c.lf_outputs[(r.lf_idx + i) & 3] = r.lfo[i];
+    }
+    c.current_prn_length_samples = r.current_prn_length_samples;
+    c.carr_phase_error_hz = r.carr_phase_error_hz;
+    c.carr_error_filt_hz = r.carr_error_filt_hz;
+    c.carrier_doppler_hz = r.carrier_doppler_hz;
+    c.code_error_chips = r.code_error_chips;
+    c.code_error_filt_chips = r.code_error_filt_chips;
+    c.code_freq_chips = r.code_freq_chips;
+    c.K_blk_samples = r.K_blk_samples;
+    c.carrier_phase_step_rad = r.carrier_phase_step_rad;
+    c.code_phase_step_chips = r.code_phase_step_chips;
+    c.acc_carrier_phase_rad = r.acc_carrier_phase_rad;
+    c.rem_code_phase_samples = r.rem_code_phase_samples;
+    c.rem_code_phase_chips = r.rem_code_phase_chips;
+}
+
 __device__ float loop_filter_apply(const TrkParams& k, TrkChannel& c, float x)
 {
-    const LoopSet& q = k.ls[c.narrow ? 1 + c.geo : 0];
+    const LoopSet& q = loopset(k, c);
     float result = 0.0f;
     for (int ii = 0; ii < q.lf_n_out; ii++) result = __fadd_rn(result, __fmul_rn(q.lf_out[ii], c.lf_outputs[(c.lf_idx + ii) % 4]));
     c.lf_idx--;
@@ -141,9 +231,33 @@ __device__ float loop_filter_apply(const TrkParams& k, TrkChannel& c, float x)
     return result;
 }
 
-__device__ float carrier_filter(const TrkParams& k, TrkChannel& c, float fll, float pll, float T)
+// Tracking_loop_filter::apply (tracking_loop_filter.cc:58-84) on the logical-order rings: the same
+// products in the same order (outputs[(idx+ii)%4] ≡ lfo[ii] before the insert, inputs[(idx'+ii)%4] ≡
+// lfi[ii] after it).
+__device__ float loop_filter_apply(const TrkParams&, LoopRegs& c, float x)
 {
-    const LoopSet& q = k.ls[c.narrow ? 1 + c.geo : 0];
+    const LoopSet& q = c.q;
+    float result = 0.0f;
+#pragma unroll
+    for (int ii = 0; ii < 3; ii++)
+        if (ii < q.lf_n_out) result = __fadd_rn(result, __fmul_rn(q.lf_out[ii], c.lfo[ii]));
+    c.lf_idx = (c.lf_idx + 3) & 3;
+#pragma unroll
+    for (int ii = 3; ii > 0; ii--) c.lfi[ii] = c.lfi[ii - 1];
+    c.lfi[0] = x;
+#pragma unroll
+    for (int ii = 0; ii < 4; ii++)
+        if (ii < q.lf_n_in) result = __fadd_rn(result, __fmul_rn(q.lf_in[ii], c.lfi[ii]));
+#pragma unroll
+    for (int ii = 3; ii > 0; ii--) c.lfo[ii] = c.lfo[ii - 1];
+    c.lfo[0] = result;
+    return result;
+}
+
+template <class C>
+__device__ float carrier_filter(const TrkParams& k, C& c, float fll, float pll, float T)
+{
+    const LoopSet& q = loopset(k, c);
     if (k.fp_order == 3) {
         c.fp_w = __fadd_rn(c.fp_w, __fmul_rn(T, __fadd_rn(__fmul_rn(q.fp_w0p3, pll), __fmul_rn(q.fp_w0f2, fll))));
         const float inner = __fadd_rn(__fadd_rn(__fmul_rn(0.5f, c.fp_w), __fmul_rn(__fmul_rn(q.fp_a2, q.fp_w0f), fll)),
@@ -157,7 +271,8 @@ __device__ float carrier_filter(const TrkParams& k, TrkChannel& c, float fll, fl
     return e;
 }
 
-__device__ void run_dll_pll(const TrkParams& k, TrkChannel& c)
+template <class C>
+__device__ void run_dll_pll(const TrkParams& k, C& c)
 {
     double disc;
     if (c.cloop)
@@ -221,7 +336,8 @@ __device__ double smoothed_rate(const TrkChannel& c, const TrkHist& h, const dou
     return (cp2 - cp1) / samples;
 }
 
-__device__ void update_tracking_vars(const TrkParams& k, TrkChannel& c, TrkHist* h)
+template <class C>
+__device__ void update_tracking_vars(const TrkParams& k, C& c, TrkHist* h)
 {
     const double fs = k.conf.fs_in;
     const double T_chip = 1.0 / c.code_freq_chips;
@@ -232,7 +348,7 @@ __device__ void update_tracking_vars(const TrkParams& k, TrkChannel& c, TrkHist*
     c.carrier_phase_step_rad = kTwoPi * c.carrier_doppler_hz / fs;
     const double n = static_cast<double>(c.current_prn_length_samples);
     c.code_phase_step_chips = c.code_freq_chips / fs;
-    if (h) {  // high_dyn: push_back on the ring (full: drop the oldest), rates once it is full
+    if constexpr (std::is_same<C, TrkChannel>::value) if (h) {  // high_dyn: push_back on the ring (full: drop the oldest), rates once it is full
         const int L = static_cast<int>(k.conf.smoother_length), cap = 2 * L;
         int slot;
         if (c.hist_count < cap) {
@@ -322,8 +438,6 @@ __device__ void zero_accu(TrkChannel& c)
     c.l[0] = c.l[1] = c.vl[0] = c.vl[1] = 0.0f;
 }
 
-// One general_work call for the epoch that started at c.epoch_start; returns false when the
-// channel stops (loss of lock).
 // log_data (:1376-1466) at epoch start nir, after update_tracking_vars.
 __device__ void log_data(const TrkParams& k, const TrkChannel& c, const float* taps, const float* pdata, uint64_t nir, gnsship_trk_dump_record* d)
 {
@@ -355,20 +469,38 @@ __device__ void log_data(const TrkParams& k, const TrkChannel& c, const float* t
     d->PRN = c.prn;
 }
 
-__device__ bool epoch_update(const TrkParams& k, TrkChannel& c, const float* taps, const float* pdata, gnsship_trk_epoch& rec, TrkHist* h,
+// One general_work call is split in phases so that the persistent kernel can run the lock
+// detectors beside the loop filters (the two share no state):
+//   epoch_pre    — pull-in timer, the epoch's correlations into the accumulators (state 2: copy,
+//                  states 3/4: save_correlation_results) and all of state 3 (no lock test there);
+//                  returns the coherent integration time lock_status is called with, or 0;
+//   lock_status  — cn0_and_tracking_lock_status (:972-1029);
+//   epoch_loop   — run_dll_pll + update_tracking_vars (:1065-1260), which the reference runs only
+//                  when the lock test passes (the persistent kernel runs it speculatively beside
+//                  the lock test on a LoopRegs copy and keeps it only on a pass);
+//   epoch_post   — the rest of the state's branch given the lock outcome;
+//   epoch_finish — the epoch record's loop outputs and consume_each.
+// The pull-in and bit-synchronisation timers compare whole seconds of samples:
+// `limit < (nir − stamp) / fs` ⟺ `nir − stamp ≥ (limit + 1)·fs` (unsigned, exact), no 64-bit division.
+__device__ __forceinline__ bool seconds_exceed(uint64_t elapsed, uint32_t limit_s, uint64_t fs_int)
+{
+    return elapsed >= (static_cast<uint64_t>(limit_s) + 1u) * fs_int;
+}
+
+__device__ double epoch_pre(const TrkParams& k, TrkChannel& c, const float* taps, const float* pdata, gnsship_trk_epoch& rec, TrkHist* h,
     gnsship_trk_dump_record* dump)
 {
     const uint64_t nir = c.epoch_start;
     const uint64_t fs_int = static_cast<uint64_t>(static_cast<int>(k.conf.fs_in));
     rec.sample_counter = nir;
-    if (c.pull_in && static_cast<uint64_t>(k.conf.pull_in_time_s) < (nir - c.acq_sample_stamp) / fs_int) {
+    if (c.pull_in && seconds_exceed(nir - c.acq_sample_stamp, k.conf.pull_in_time_s, fs_int)) {
         c.pull_in = 0;
         c.carrier_fail = 0;
         c.code_fail = 0;
     }
     const int eo = k.veml ? 2 : 0;
     const int st = c.state;
-    bool loss = false;
+    rec.state = st;
     if (st == 2) {
         if (k.veml) {
             c.ve[0] = taps[0];
@@ -385,117 +517,129 @@ __device__ bool epoch_update(const TrkParams& k, TrkChannel& c, const float* tap
         c.spc = k.conf.early_late_space_chips;
         rec.prompt_i = static_cast<double>(c.p[0]);  // diagnostic: the epoch's prompt (no symbol flag in state 2)
         rec.prompt_q = static_cast<double>(c.p[1]);
-        if (static_cast<uint64_t>(k.conf.bit_synchronization_time_limit_s) < (nir - c.acq_sample_stamp) / fs_int) c.carrier_fail = 300000;
-        GNSSHIP_TRK_LOOP_STAMP(8);
-        if (!lock_status(k, c, k.code_period)) {
-            clear_tracking_vars(c);
-            c.state = 0;
-            loss = true;
+        if (seconds_exceed(nir - c.acq_sample_stamp, k.conf.bit_synchronization_time_limit_s, fs_int)) c.carrier_fail = 300000;
+        return k.code_period;
+    }
+    // save_correlation_results
+    float sgn = 1.0f;
+    if (k.sync[c.geo].secondary) {
+        sgn = bit_at(k.sync[c.geo].secondary_bits, c.current_symbol) ? -1.0f : 1.0f;
+        c.current_symbol = (c.current_symbol + 1) % k.sync[c.geo].secondary_len;
+    }
+    if (k.veml) {
+        cadd(c.ve, taps, sgn);
+        cadd(c.vl, taps + 8, sgn);
+    }
+    cadd(c.e, taps + eo, sgn);
+    cadd(c.p, taps + eo + 2, sgn);
+    cadd(c.l, taps + eo + 4, sgn);
+    const float* src = k.track_pilot ? pdata : taps + eo + 2;
+    if (k.sync[c.geo].symbols_per_bit > 1) {
+        if (k.sync[c.geo].data_secondary_len > 0) {
+            cadd(c.p_data, src, bit_at(k.sync[c.geo].data_secondary_bits, c.current_data_symbol) ? -1.0f : 1.0f);
+            c.current_data_symbol = (c.current_data_symbol + 1) % k.sync[c.geo].data_secondary_len;
         } else {
-            bool next_state = false;
-            GNSSHIP_TRK_LOOP_STAMP(9);
-            run_dll_pll(k, c);
-            GNSSHIP_TRK_LOOP_STAMP(10);
-            update_tracking_vars(k, c, h);
-            GNSSHIP_TRK_LOOP_STAMP(11);
-            log_data(k, c, taps, pdata, nir, dump);
-            GNSSHIP_TRK_LOOP_STAMP(12);
-            rec.flags |= 16;
-            if (!c.pull_in) {
-                if (k.sync[c.geo].secondary || k.sync[c.geo].symbols_per_bit > 1) {
-                    push_sign(k, c, taps[eo + 2]);
-                    if (c.sign_count == k.sync[c.geo].secondary_len) next_state = acquire_secondary(k, c);
-                } else {
-                    next_state = true;
-                }
-            }
-            if (next_state) {
-                zero_accu(c);
-                c.p_data[0] = c.p_data[1] = 0.0f;
-                c.sign_count = 0;
-                c.current_symbol = 0;
-                c.current_data_symbol = 0;
-                if (k.sync[c.geo].extend > 1) {  // extended integration (:1890-1926): narrow loops and taps, state 3
-                    c.ext_count = 0;
-                    c.narrow = 1;
-                    c.spc = k.spc_n;
-                    c.state = 3;
-                } else {
-                    c.state = 4;
-                }
-            }
+            cadd(c.p_data, src, 1.0f);
+            c.current_data_symbol = (c.current_data_symbol + 1) % k.sync[c.geo].symbols_per_bit;
         }
     } else {
-        // save_correlation_results
-        float sgn = 1.0f;
-        if (k.sync[c.geo].secondary) {
-            sgn = bit_at(k.sync[c.geo].secondary_bits, c.current_symbol) ? -1.0f : 1.0f;
-            c.current_symbol = (c.current_symbol + 1) % k.sync[c.geo].secondary_len;
+        c.p_data[0] = src[0];
+        c.p_data[1] = src[1];
+    }
+    c.cloop = k.track_pilot ? 0 : 1;
+    if (st == 3) {  // coherent integration (:1933-1970): accumulate, NCO advance only
+        update_tracking_vars(k, c, h);
+        if (c.current_data_symbol == 0) {
+            log_data(k, c, taps, pdata, nir, dump);
+            rec.flags |= 16;
+            rec.prompt_i = static_cast<double>(c.p_data[0]);
+            rec.prompt_q = static_cast<double>(c.p_data[1]);
+            rec.flags |= 1;
+            c.p_data[0] = c.p_data[1] = 0.0f;
         }
-        if (k.veml) {
-            cadd(c.ve, taps, sgn);
-            cadd(c.vl, taps + 8, sgn);
+        c.ext_count++;
+        if (c.ext_count == k.sync[c.geo].extend - 1) {
+            c.ext_count = 0;
+            c.state = 4;
         }
-        cadd(c.e, taps + eo, sgn);
-        cadd(c.p, taps + eo + 2, sgn);
-        cadd(c.l, taps + eo + 4, sgn);
-        const float* src = k.track_pilot ? pdata : taps + eo + 2;
-        if (k.sync[c.geo].symbols_per_bit > 1) {
-            if (k.sync[c.geo].data_secondary_len > 0) {
-                cadd(c.p_data, src, bit_at(k.sync[c.geo].data_secondary_bits, c.current_data_symbol) ? -1.0f : 1.0f);
-                c.current_data_symbol = (c.current_data_symbol + 1) % k.sync[c.geo].data_secondary_len;
+        return 0.0;
+    }
+    return k.code_period * static_cast<double>(k.sync[c.geo].extend);
+}
+
+template <class C>
+__device__ __forceinline__ void epoch_loop(const TrkParams& k, C& c, TrkHist* h)
+{
+    GNSSHIP_TRK_LOOP_STAMP(9);
+    run_dll_pll(k, c);
+    GNSSHIP_TRK_LOOP_STAMP(10);
+    update_tracking_vars(k, c, h);
+    GNSSHIP_TRK_LOOP_STAMP(11);
+}
+
+// After epoch_pre returned a coherent time: the rest of state 2 / 4 given the lock outcome (epoch_loop
+// has run iff locked).
+__device__ void epoch_post(const TrkParams& k, TrkChannel& c, const float* taps, const float* pdata, gnsship_trk_epoch& rec, bool locked,
+    gnsship_trk_dump_record* dump)
+{
+    const uint64_t nir = c.epoch_start;
+    const int eo = k.veml ? 2 : 0;
+    if (!locked) {
+        clear_tracking_vars(c);
+        c.state = 0;
+        rec.flags |= 2;
+        return;
+    }
+    if (c.state == 2) {
+        bool next_state = false;
+        log_data(k, c, taps, pdata, nir, dump);
+        GNSSHIP_TRK_LOOP_STAMP(12);
+        rec.flags |= 16;
+        if (!c.pull_in) {
+            if (k.sync[c.geo].secondary || k.sync[c.geo].symbols_per_bit > 1) {
+                push_sign(k, c, taps[eo + 2]);
+                if (c.sign_count == k.sync[c.geo].secondary_len) next_state = acquire_secondary(k, c);
             } else {
-                cadd(c.p_data, src, 1.0f);
-                c.current_data_symbol = (c.current_data_symbol + 1) % k.sync[c.geo].symbols_per_bit;
+                next_state = true;
             }
-        } else {
-            c.p_data[0] = src[0];
-            c.p_data[1] = src[1];
         }
-        c.cloop = k.track_pilot ? 0 : 1;
-        if (st == 3) {  // coherent integration (:1933-1970): accumulate, NCO advance only
-            update_tracking_vars(k, c, h);
-            if (c.current_data_symbol == 0) {
-                log_data(k, c, taps, pdata, nir, dump);
-                rec.flags |= 16;
-                rec.prompt_i = static_cast<double>(c.p_data[0]);
-                rec.prompt_q = static_cast<double>(c.p_data[1]);
-                rec.flags |= 1;
-                c.p_data[0] = c.p_data[1] = 0.0f;
-            }
-            c.ext_count++;
-            if (c.ext_count == k.sync[c.geo].extend - 1) {
+        if (next_state) {
+            zero_accu(c);
+            c.p_data[0] = c.p_data[1] = 0.0f;
+            c.sign_count = 0;
+            c.current_symbol = 0;
+            c.current_data_symbol = 0;
+            if (k.sync[c.geo].extend > 1) {  // extended integration (:1890-1926): narrow loops and taps, state 3
                 c.ext_count = 0;
+                c.narrow = 1;
+                c.spc = k.spc_n;
+                c.state = 3;
+            } else {
                 c.state = 4;
             }
-        } else if (GNSSHIP_TRK_LOOP_STAMP(8), !lock_status(k, c, k.code_period * static_cast<double>(k.sync[c.geo].extend))) {
-            clear_tracking_vars(c);
-            c.state = 0;
-            loss = true;
-        } else {
-            GNSSHIP_TRK_LOOP_STAMP(9);
-            run_dll_pll(k, c);
-            GNSSHIP_TRK_LOOP_STAMP(10);
-            update_tracking_vars(k, c, h);
-            GNSSHIP_TRK_LOOP_STAMP(11);
-            if (!c.acc_phase_init) {
-                c.acc_carrier_phase_rad = -static_cast<double>(c.rem_carr_phase_rad);
-                c.acc_phase_init = 1;
-            }
-            if (c.current_data_symbol == 0) {
-                log_data(k, c, taps, pdata, nir, dump);
-                rec.flags |= 16;
-                rec.prompt_i = static_cast<double>(c.p_data[0]);
-                rec.prompt_q = static_cast<double>(c.p_data[1]);
-                rec.flags |= 1;
-                c.p_data[0] = c.p_data[1] = 0.0f;
-            }
-            zero_accu(c);
-            if (k.sync[c.geo].extend > 1) c.state = 3;  // next coherent integration cycle
         }
+        return;
     }
-    rec.state = st;
-    if (loss) rec.flags |= 2;
+    // state 4 (:1971-2028)
+    if (!c.acc_phase_init) {
+        c.acc_carrier_phase_rad = -static_cast<double>(c.rem_carr_phase_rad);
+        c.acc_phase_init = 1;
+    }
+    if (c.current_data_symbol == 0) {
+        log_data(k, c, taps, pdata, nir, dump);
+        rec.flags |= 16;
+        rec.prompt_i = static_cast<double>(c.p_data[0]);
+        rec.prompt_q = static_cast<double>(c.p_data[1]);
+        rec.flags |= 1;
+        c.p_data[0] = c.p_data[1] = 0.0f;
+    }
+    zero_accu(c);
+    if (k.sync[c.geo].extend > 1) c.state = 3;  // next coherent integration cycle
+}
+
+// The record's loop outputs and consume_each (:2061); false when the channel stopped (loss of lock).
+__device__ bool epoch_finish(TrkChannel& c, gnsship_trk_epoch& rec)
+{
     if (c.pll_180) rec.flags |= 4;
     rec.code_phase_samples = c.rem_code_phase_samples;
     rec.carrier_phase_rads = c.acc_carrier_phase_rad;
@@ -506,9 +650,23 @@ __device__ bool epoch_update(const TrkParams& k, TrkChannel& c, const float* tap
     rec.rem_code_phase_chips = c.rem_code_phase_chips;
     rec.rem_carr_phase_rad = c.rem_carr_phase_rad;
     rec.prn_length_samples = c.current_prn_length_samples;
-    if (loss) return false;
-    c.nitems_read = nir + static_cast<uint64_t>(c.current_prn_length_samples);  // consume_each (:2061)
+    if (rec.flags & 2) return false;
+    c.nitems_read = c.epoch_start + static_cast<uint64_t>(c.current_prn_length_samples);  // consume_each (:2061)
     return true;
+}
+
+// The phases in the reference's order on one lane (the round-based step kernel).
+__device__ bool epoch_update(const TrkParams& k, TrkChannel& c, const float* taps, const float* pdata, gnsship_trk_epoch& rec, TrkHist* h,
+    gnsship_trk_dump_record* dump)
+{
+    const double coh = epoch_pre(k, c, taps, pdata, rec, h, dump);
+    if (coh > 0.0) {
+        GNSSHIP_TRK_LOOP_STAMP(8);
+        const bool locked = lock_status(k, c, coh);
+        if (locked) epoch_loop(k, c, h);
+        epoch_post(k, c, taps, pdata, rec, locked, dump);
+    }
+    return epoch_finish(c, rec);
 }
 
 }  // namespace

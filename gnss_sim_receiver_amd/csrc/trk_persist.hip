@@ -73,7 +73,12 @@ struct PEpoch {
     int32_t in_margin;   // every chip index of the epoch lies in the padded LDS replica
     int32_t published;   // anchors ready: generic blocks, or AVX segments (S + 1 = all, tail included)
     int32_t next_task;   // work dealer of the correlating waves
+    int32_t locked;      // lock_status outcome (wave 1) for the loop update (wave 0)
+    double coh;          // epoch_pre's coherent integration time (0: no lock test this epoch)
     float red[kPWaves][2 * (kMaxTaps + 1)];
+    float taps[2 * kMaxTaps + 2];  // the epoch's tap sums (+ the data prompt), as epoch_update reads them
+    gnsship_trk_epoch rec;
+    gnsship_trk_dump_record dump;
 };
 
 // Complex product rounded exactly as the reference's written-out (ac − bd, ad + bc): two packed
@@ -497,29 +502,50 @@ __global__ __launch_bounds__(kPThreads, persist_waves_per_simd<THRU>()) void trk
             }
         }
         __syncthreads();
+        // tap sums over the waves (each in the serial order w = 0..3), the data prompt at 2·kMaxTaps
+        if (tid < 2 * kMaxTaps + 2) {
+            const int v = tid < 2 * kMaxTaps ? tid : 2 * NT + (tid - 2 * kMaxTaps);
+            float s = 0.0f;
+            if (tid < 2 * NT || (DATA && tid >= 2 * kMaxTaps))
+                for (int w = 0; w < kPWaves; w++) s += ep.red[w][v];
+            ep.taps[tid] = s;
+        }
+        __syncthreads();
+        const float* taps = ep.taps;
+        const float* pdata = DATA ? ep.taps + 2 * kMaxTaps : ep.taps;
+        gnsship_trk_dump_record* dr = dump ? &ep.dump : nullptr;
         if (tid == 0) {
             GNSSHIP_TRK_STAMP(e, 5);
-            float taps[2 * kMaxTaps], pdata[2];
-            for (int v = 0; v < 2 * kMaxTaps; v++) taps[v] = 0.0f;
-            for (int v = 0; v < 2 * NT; v++) {
-                float s = 0.0f;
-                for (int w = 0; w < kPWaves; w++) s += ep.red[w][v];
-                taps[v] = s;
+            ep.rec = gnsship_trk_epoch{};
+            ep.rec.flags = 8;
+            ep.coh = epoch_pre(k, sc, taps, pdata, ep.rec, nullptr, dr);
+        }
+        __syncthreads();
+        // the lock detectors (wave 1) beside the loop filters and NCO update (wave 0), which run
+        // speculatively on a register copy of their members, stored only when the lock test passes
+        // (trk_loop.h epoch phases)
+        const double coh = ep.coh;
+        LoopRegs lr;
+        if (coh > 0.0) {
+            if (tid == kWave) {
+                GNSSHIP_TRK_LOOP_STAMP(8);
+                ep.locked = lock_status(k, sc, coh) ? 1 : 0;
+            } else if (tid == 0) {
+                load_regs(k, sc, lr);
+                epoch_loop(k, lr, nullptr);
             }
-            pdata[0] = pdata[1] = 0.0f;
-            if constexpr (DATA) {
-                for (int w = 0; w < kPWaves; w++) {
-                    pdata[0] += ep.red[w][2 * NT];
-                    pdata[1] += ep.red[w][2 * NT + 1];
-                }
+            __syncthreads();
+        }
+        if (tid == 0) {
+            if (coh > 0.0) {
+                const bool locked = ep.locked != 0;
+                if (locked) store_regs(lr, sc);
+                epoch_post(k, sc, taps, pdata, ep.rec, locked, dr);
             }
-            gnsship_trk_epoch r = {};
-            r.flags = 8;
-            gnsship_trk_dump_record dr;
-            epoch_update(k, sc, taps, DATA ? pdata : taps, r, nullptr, dump ? &dr : nullptr);
+            epoch_finish(sc, ep.rec);
             const size_t slot = static_cast<size_t>(e) * n_chans + ch;
-            if (rec) rec[slot] = r;
-            if (dump && (r.flags & 16)) dump[slot] = dr;
+            if (rec) rec[slot] = ep.rec;
+            if (dump && (ep.rec.flags & 16)) dump[slot] = ep.dump;
             atomicAdd(ran_count + e, 1);
             GNSSHIP_TRK_STAMP(e, 6);
         }

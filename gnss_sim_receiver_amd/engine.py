@@ -126,6 +126,59 @@ class DeviceBuffer:
             pass
 
 
+def comm_unique_id() -> bytes:
+    """A fresh RCCL unique id (rank 0 makes it; the launcher's store carries it to the others)."""
+    buf = ctypes.create_string_buffer(abi.COMM_ID_BYTES)
+    check(abi.load().gnsship_comm_unique_id(buf), "gnsship_comm_unique_id")
+    return buf.raw
+
+
+class Comm:
+    """gnsship_comm: one RCCL communicator per context, collectives on the context stream — the
+    multi-GPU form of the flowgraph's conditioner → channels fan-out (gnss_flowgraph.cc:1127-1136)."""
+
+    def __init__(self, ctx: Context, n_ranks: int, rank: int, uid: bytes):
+        if len(uid) != abi.COMM_ID_BYTES:
+            raise ValueError("RCCL unique id must be 128 bytes")
+        self.ctx = ctx
+        self.rank, self.n_ranks = rank, n_ranks
+        h = ctypes.c_void_p()
+        idbuf = ctypes.create_string_buffer(uid, abi.COMM_ID_BYTES)
+        check(ctx.lib.gnsship_comm_create(ctx.h, n_ranks, rank, idbuf, ctypes.byref(h)), "gnsship_comm_create", ctx.h)
+        self.h = h
+
+    @classmethod
+    def from_process_group(cls, ctx: Context):
+        """Build the communicator over the ranks of the initialised torch.distributed group: rank 0's
+        id travels through the group (any backend), then every rank joins."""
+        import torch.distributed as dist
+        rank, world = dist.get_rank(), dist.get_world_size()
+        obj = [comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        return cls(ctx, world, rank, obj[0])
+
+    def broadcast(self, dev_ptr: int, nbytes: int, root: int = 0):
+        check(self.ctx.lib.gnsship_comm_broadcast(self.h, dev_ptr, nbytes, root), "gnsship_comm_broadcast", self.ctx.h)
+
+    def allgather(self, dev_send: int, dev_recv: int, bytes_per_rank: int):
+        check(self.ctx.lib.gnsship_comm_allgather(self.h, dev_send, dev_recv, bytes_per_rank), "gnsship_comm_allgather", self.ctx.h)
+
+    def max_f64(self, values) -> np.ndarray:
+        """Max over ranks of a few doubles (host in, host out; through a device buffer)."""
+        v = np.ascontiguousarray(values, np.float64).reshape(-1)
+        buf = self.ctx.upload(v)
+        check(self.ctx.lib.gnsship_comm_allreduce_max_f64(self.h, buf.ptr, v.size), "gnsship_comm_allreduce_max_f64", self.ctx.h)
+        self.ctx.sync()
+        out = buf.download(np.empty_like(v))
+        buf.free()
+        return out
+
+    def close(self):
+        if self.h:
+            self.ctx.lib.gnsship_comm_destroy(self.h)
+            self.h = None
+
+
 class MultiCorrelatorRealCodes:
     """Mirror of Cpu_Multicorrelator_Real_Codes (cpu_multicorrelator_real_codes.h:37-61)."""
 

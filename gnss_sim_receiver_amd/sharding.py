@@ -26,6 +26,46 @@ def shard_channels(n_channels: int, world: int, rank: int) -> list:
     return list(range(rank, n_channels, world))
 
 
+def shard_prns(n_prns: int, world: int, rank: int) -> list:
+    """Acquisition cells sharded by PRN slot (round-robin): a rank searches every Doppler bin of its
+    PRNs, so each per-PRN statistic — first-vs-second peak in the peak's row, or the CFAR input power
+    of the row opposite the peak bin ((idx + nb/2) % nb, pcps_acquisition.cc:496-528) — is complete
+    on one rank and only the per-PRN results travel (one all-gather).  Sharding the bins instead
+    would need a second exchange for the opposite-row power."""
+    return shard_channels(n_prns, world, rank)
+
+
+ACQ_ROW_FIELDS = ("prn_slot", "doppler_index", "code_index", "doppler_hz", "peak", "input_power", "test_statistic", "acq_delay_samples")
+
+
+def acq_rows(results, slots) -> np.ndarray:
+    """Per-PRN acquisition results (gnsship_acq_result-like objects) → float64 rows (ACQ_ROW_FIELDS)."""
+    rows = np.zeros((len(slots), len(ACQ_ROW_FIELDS)), np.float64)
+    for i, (r, s) in enumerate(zip(results, slots)):
+        rows[i] = (s, r.doppler_index, r.code_index, r.doppler_hz, r.peak, r.input_power, r.test_statistic, r.acq_delay_samples)
+    return rows
+
+
+def pad_rows(rows: np.ndarray, n: int) -> np.ndarray:
+    """Fixed-size all-gather payload: `n` rows, unused ones with prn_slot = -1."""
+    out = np.zeros((n, rows.shape[1]), np.float64)
+    out[:, 0] = -1
+    out[: len(rows)] = rows
+    return out
+
+
+def merge_acq_rows(gathered: np.ndarray) -> dict:
+    """Rank-ordered gathered rows → {prn_slot: row}, padding dropped (each slot on exactly one rank)."""
+    out = {}
+    for row in np.asarray(gathered).reshape(-1, len(ACQ_ROW_FIELDS)):
+        if row[0] >= 0:
+            slot = int(row[0])
+            if slot in out:
+                raise ValueError(f"PRN slot {slot} reported by two ranks")
+            out[slot] = row
+    return out
+
+
 def weak_channels(per_rank: int, rank: int) -> list:
     """Weak scaling: rank r owns global channels [r·per_rank, (r+1)·per_rank)."""
     return list(range(rank * per_rank, (rank + 1) * per_rank))

@@ -18,6 +18,12 @@
  *  gnsship_acq_*        pcps_acquisition::set_local_code (pcps_acquisition.cc:175-208),
  *                         update_grid_doppler_wipeoffs (:295-302), acquisition_core (:600-871),
  *                         max_to_input_power_statistic / first_vs_second_peak_statistic (:496-597).
+ *  gnsship_trk_*        dll_pll_veml_tracking::{start_tracking, general_work} (dll_pll_veml_tracking.cc:
+ *                         643-883, 1728-2094) for many channels, the loop on the device.
+ *  gnsship_comm_*       The flowgraph's fan-out of one signal-conditioner output to every channel
+ *                         (gnss_flowgraph.cc:1127-1136) across GPUs: one RCCL communicator over
+ *                         xGMI, the IF block broadcast from the reading rank, per-PRN acquisition
+ *                         results all-gathered.
  *
  * Threading: handles are not re-entrant; distinct handles may be used from distinct threads
  * (each context owns one HIP stream).  All *_run calls are synchronous unless named *_launch.
@@ -40,6 +46,7 @@ extern "C" {
 #define GNSSHIP_E_NOMEM (-2)   /* device or host allocation failed */
 #define GNSSHIP_E_DEVICE (-3)  /* HIP runtime error (message in gnsship_last_error) */
 #define GNSSHIP_E_STATE (-4)   /* call order violated (e.g. run before set_local_code) */
+#define GNSSHIP_E_RCCL (-5)    /* RCCL (collective) error (message in gnsship_last_error)   */
 
 /* ---- IF sample formats (reference item types: gr_complex, cshort, ibyte/cbyte) ---- */
 #define GNSSHIP_FMT_CF32 0 /* interleaved float32 I,Q  (gr_complex)            */
@@ -395,6 +402,28 @@ int gnsship_trk_run_dump(gnsship_trk* t, const void* sig, int fmt, int sig_on_de
     int max_rounds, gnsship_trk_epoch* out, gnsship_trk_dump_record* dump, int* rounds_done);
 int gnsship_trk_channel_state(gnsship_trk* t, int channel, int* state, uint64_t* next_sample);
 int gnsship_trk_destroy(gnsship_trk* t);
+
+/* ------------------------------------------------------------------------------------------ */
+/* Multi-GPU fan-out: one process per GPU, one RCCL communicator per context.  */
+/* The reference connects one conditioner output to every channel block (gnss_flowgraph.cc:    */
+/* 1127-1136); across GPUs that connection is a broadcast of the raw IF block from the rank     */
+/* that reads the front end, after which every rank tracks / acquires its own channel or PRN    */
+/* shard with no further data-path collective.  Collectives are enqueued on the context stream  */
+/* (ordered before any later launch of that context; gnsship_ctx_sync waits for them).          */
+/* ------------------------------------------------------------------------------------------ */
+typedef struct gnsship_comm gnsship_comm;
+#define GNSSHIP_COMM_ID_BYTES 128
+/* Rank 0 creates the id and hands it to the other ranks out of band (e.g. the launcher's store). */
+int gnsship_comm_unique_id(void* id);
+int gnsship_comm_create(gnsship_ctx* ctx, int n_ranks, int rank, const void* id, gnsship_comm** out);
+int gnsship_comm_rank(gnsship_comm* c, int* rank, int* n_ranks);
+/* In-place broadcast of `bytes` of a device buffer from `root` (raw IF samples in any format). */
+int gnsship_comm_broadcast(gnsship_comm* c, void* dev_buf, size_t bytes, int root);
+/* dev_recv[r·bytes_per_rank ...] = rank r's dev_send (per-PRN acquisition results, records). */
+int gnsship_comm_allgather(gnsship_comm* c, const void* dev_send, void* dev_recv, size_t bytes_per_rank);
+/* In-place max over ranks of `count` doubles (timing: the slowest rank's wall time). */
+int gnsship_comm_allreduce_max_f64(gnsship_comm* c, double* dev_buf, size_t count);
+int gnsship_comm_destroy(gnsship_comm* c);
 
 #ifdef __cplusplus
 }
