@@ -61,6 +61,7 @@ def parse():
     ap.add_argument("--seconds", type=float, default=1.0, help="IF seconds per step (D)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline time budget (0 = skip)")
     ap.add_argument("--no-aux", action="store_true", help="headline only (no auxiliary lines)")
+    ap.add_argument("--sharded-aux-only", action="store_true", help="of the auxiliary lines, only the multi-rank ones")
     ap.add_argument("--rotator", type=int, default=-1, help="-1 volk's dispatch on this host, 0 generic, 1 AVX")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_trk.json"),
                     help="rocprofv3 PMC summary of the headline kernel (HBM bytes, VALU instructions per launch)")
@@ -142,9 +143,7 @@ def headline(ctx, torch, args, rank, world, device, barrier):
         x = signals.generate_if_device(FS, n_total, sats, seed=SEED, start=first - 2 * VL, device=f"cuda:{device}")
     else:
         x = torch.empty(n_total, dtype=torch.complex64, device=f"cuda:{device}")
-    if world > 1:
-        sharding.broadcast_block(x, src=0)
-    torch.cuda.synchronize()
+    fan_out(ctx, torch, x, world)
     base = (x.data_ptr(), first - 2 * VL)  # (device pointer, absolute index of x[0])
     chans = [(rank * N_CH + c) % N_SATS for c in range(N_CH)]
     rx = Receiver(ctx, "GPS", FS, VL, [sats[i] for i in chans], N_CH, first, rot)
@@ -225,6 +224,92 @@ def closed_loop_aux(ctx, torch, device, system, fs, vl, n_ch, seconds, rot, seed
             "epochs": done, "ms_per_signal_second": round(dt / sig_s * 1e3, 3), "realtime_factor": round(sig_s / dt, 1),
             "us_per_epoch_round": round(dt / done * 1e6, 2), "if_msamples_per_s": round(sig_s * fs / dt / 1e6, 1),
             "channels_in_state_4": int(np.sum(st == 4))}
+
+
+# ---------------------------------------------------------------------------------------------------
+# multi-GPU fan-out: the C ABI's RCCL communicator (gnsship_comm_*) when it could be
+# created, else torch.distributed — the transport used is reported in the JSON line.
+COMM = {"comm": None, "transport": "single rank"}
+
+
+def fan_out(ctx, torch, x, world):
+    """Broadcast the IF tensor x (device, any dtype) from rank 0 to every rank."""
+    torch.cuda.synchronize()
+    if world > 1:
+        c = COMM["comm"]
+        if c is not None:
+            c.broadcast(x.data_ptr(), x.numel() * x.element_size(), 0)
+            ctx.sync()
+        else:
+            from gnss_sim_receiver_amd import sharding
+            sharding.broadcast_block(x, src=0)
+            torch.cuda.synchronize()
+
+
+def allgather_rows(ctx, torch, rows, world):
+    """All-gather equal-shaped float64 row blocks → rank-ordered stack."""
+    if world == 1:
+        return rows
+    c = COMM["comm"]
+    if c is not None:
+        send = ctx.upload(np.ascontiguousarray(rows, np.float64))
+        from gnss_sim_receiver_amd import engine
+        recv = engine.DeviceBuffer(ctx, rows.nbytes * world)
+        c.allgather(send.ptr, recv.ptr, rows.nbytes)
+        ctx.sync()
+        out = recv.download(np.empty((world,) + rows.shape, np.float64))
+        send.free()
+        recv.free()
+        return out.reshape(-1, rows.shape[1])
+    import torch.distributed as dist
+    t = torch.from_numpy(np.ascontiguousarray(rows, np.float64))
+    if dist.get_backend() == "nccl":
+        t = t.cuda()
+    outs = [torch.empty_like(t) for _ in range(world)]
+    dist.all_gather(outs, t)
+    return torch.cat(outs).cpu().numpy()
+
+
+def acq_c3_sharded(ctx, torch, rank, world, device, barrier, reps=20):
+    """C3 (32 PRN x 40 bins x 25000 at 25 Msps, BASELINE's signal: 10 present, seed 0x6E550003) with
+    the (PRN x bin) cells sharded by PRN over the ranks: the 25000-sample block fanned out from rank 0,
+    every rank searches all bins of its PRNs in one launch, per-PRN results all-gathered.  Whole-job
+    sweeps/s = reps / max-over-ranks wall."""
+    from gnss_sim_receiver_amd import codes as C, engine, sharding, signals as S
+    fs, n = 25000000, 25000
+    c3 = S.c3_sky()
+    x = torch.empty(n, dtype=torch.complex64, device=f"cuda:{device}")
+    if rank == 0:
+        x.copy_(torch.from_numpy(S.generate_if(fs, n, c3, seed=0x6E550003)))
+    fan_out(ctx, torch, x, world)
+    mine = sharding.shard_prns(32, world, rank)
+    acq = engine.PcpsAcquisition(ctx, fs, n, 5000, 250, 0, True, max_prns=len(mine))
+    for j, k in enumerate(mine):
+        acq.set_local_code(C.gps_l1_ca_code_gen_complex_sampled(k + 1, fs), j)
+    dev = engine.DeviceBuffer.wrap(ctx, x.data_ptr(), n * 8)
+    for _ in range(3):
+        acq.run(dev, n_prns=len(mine))
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        res, _ = acq.run(dev, n_prns=len(mine))
+    barrier()
+    wall = sharding.max_over_ranks(time.perf_counter() - t0)
+    rows = sharding.pad_rows(sharding.acq_rows(res, mine), -(-32 // world))
+    merged = sharding.merge_acq_rows(allgather_rows(ctx, torch, rows, world))
+    acq.close()
+    present = sorted(s.prn for s in c3)
+    stat = {k + 1: float(merged[k][6]) for k in merged}
+    dt = wall / reps
+    cells = 32 * 40
+    return {"config": "C3: 32 PRN (10 present, seed 0x6E550003) x 40 bins, fft 25000 (four-step), 25 Msps; "
+                      f"cells sharded by PRN over {world} rank(s), per-PRN results all-gathered",
+            "n_ranks": world, "prns_per_rank": len(mine), "sweep_ms": round(dt * 1e3, 3), "sweeps_per_s": round(1 / dt, 1),
+            "cells_per_s": round(cells / dt, 0), "algorithmic_GBps": round(cells * 20 * n / dt / 1e9, 1),
+            "prns_present": present, "prns_reported": len(merged),
+            "present_min_test_statistic": round(min(stat[p] for p in present), 2),
+            "absent_max_test_statistic": round(max(v for p, v in stat.items() if p not in present), 2),
+            "fanout": COMM["transport"]}
 
 
 # ---------------------------------------------------------------------------------------------------
@@ -522,6 +607,13 @@ def main():
         torch.cuda.set_device(device)
         dist.init_process_group(backend)
     ctx = engine.Context(device)
+    if world > 1:
+        try:
+            COMM["comm"] = engine.Comm.from_process_group(ctx)
+            COMM["transport"] = "gnsship_comm (RCCL, C ABI)"
+        except Exception as e:  # reported, never silent: the data then travels over torch.distributed
+            COMM["transport"] = f"torch.distributed ({type(e).__name__}: {e})"
+            print(f"[bench] gnsship_comm unavailable, IF fan-out over torch.distributed: {e}", file=sys.stderr)
 
     def barrier():
         if world > 1:
@@ -575,7 +667,10 @@ def main():
         "us_per_epoch": round(wall / (args.steps * args.seconds * 1000) * 1e6, 2),
         "roofline": roof,
     }
-    if rank == 0 and not args.no_aux:
+    result["config"]["fanout"] = COMM["transport"]
+    if not args.no_aux:  # every rank: its PRN shard of the C3 sweep
+        result["acquisition_c3"] = acq_c3_sharded(ctx, torch, rank, world, device, barrier)
+    if rank == 0 and not args.no_aux and not args.sharded_aux_only:
         counts = [12, 256, 1024, 4096, 16384, 65536]
         sw = sweep(ctx, h, h["rotator"], counts)
         best = max(sw, key=lambda r: r["channel_epochs_per_s"])
@@ -601,17 +696,14 @@ def main():
         sky = S.random_sky(N_SATS, seed=SEED)
         blk = S.generate_if(FS, VL, sky, seed=SEED)
         result["acquisition"] = acq_bench(ctx, FS, VL, blk, "32 PRN x 40 bins, fft 4000, 4 Msps")
-        c3 = S.c3_sky()
-        c3_present = [s.prn for s in c3]
-        sig25 = S.generate_if(25000000, 25000, c3, seed=0x6E550003)
-        result["acquisition_c3"] = acq_bench(ctx, 25000000, 25000, sig25, "C3: 32 PRN (10 present, seed 0x6E550003) x 40 bins, "
-                                             "fft 25000 (four-step), 25 Msps", present=c3_present)
         result["acquisition_e1"] = acq_e1_bench(ctx)
         result["tracking_c4_e1_open_loop"] = e1_open_loop(ctx)
         result["tracking_c5_hybrid_open_loop"] = c5_open_loop(ctx)
     del h
     if rank == 0:
         print(json.dumps(result), flush=True)
+    if COMM["comm"] is not None:
+        COMM["comm"].close()
     if world > 1:
         torch.distributed.barrier()
         torch.distributed.destroy_process_group()

@@ -100,6 +100,14 @@ class DeviceBuffer:
         check(ctx.lib.gnsship_dev_alloc(ctx.h, nbytes, ctypes.byref(p)), f"gnsship_dev_alloc({nbytes})", ctx.h)
         self.ptr = p.value
         self.nbytes = nbytes
+        self.owned = True
+
+    @classmethod
+    def wrap(cls, ctx: Context, ptr: int, nbytes: int) -> "DeviceBuffer":
+        """A non-owning view of device memory allocated elsewhere (e.g. a torch tensor's storage)."""
+        b = cls.__new__(cls)
+        b.ctx, b.ptr, b.nbytes, b.owned = ctx, ptr, nbytes, False
+        return b
 
     def upload(self, host: np.ndarray, offset: int = 0):
         host = np.ascontiguousarray(host)
@@ -114,9 +122,9 @@ class DeviceBuffer:
         return out
 
     def free(self):
-        if self.ptr:
+        if self.ptr and self.owned:
             self.ctx.lib.gnsship_dev_free(self.ctx.h, self.ptr)
-            self.ptr = None
+        self.ptr = None
 
     def __del__(self):
         try:
