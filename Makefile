@@ -58,3 +58,9 @@ $(PROF_LIB): $(PROF_OBJS)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(PROF_OBJS) -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 prof: $(PROF_LIB)
 .PHONY: prof
+
+# Standalone receiver core (the Channel role over the C ABI: include/gnsship_receiver.hpp)
+RX_TOOL := tools/gnsship_rx
+$(RX_TOOL): tools/gnsship_rx.cpp include/gnsship_receiver.hpp include/gnsship_cpp.hpp include/gnsship.h $(LIB)
+	g++ -O2 -std=c++17 -Wall -Iinclude tools/gnsship_rx.cpp -o $@ -L$(PKG) -lgnsship -Wl,-rpath,'$$ORIGIN/../$(PKG)' -lpthread -lm
+all: $(RX_TOOL)

@@ -9,8 +9,10 @@
 // between epochs.  Per epoch:
 //   1. thread 0 derives the correlator arguments from the channel state (do_correlation_step);
 //   2. wave 0 replays the reference's rotator recursion and publishes its anchors to LDS block by
-//      block, while waves 1-3 (and wave 0 once the replay is done) correlate every block whose
-//      anchor is published: the replay — the serial floor of the epoch — overlaps the correlation;
+//      block, while waves 1-3 correlate every block whose anchor is published, in a static order
+//      (wave w takes work items w − 1 mod 3): the replay — the serial floor of the epoch — overlaps
+//      the correlation, and every sum is formed in the same order on every run (the results are
+//      bit-reproducible, independent of wave scheduling and of the other channels in the launch);
 //   3. the tap sums are reduced in LDS and thread 0 runs the loop update on the channel state,
 //      which lives in LDS for the whole run, and writes the epoch's record.
 //
@@ -72,7 +74,6 @@ struct PEpoch {
     int32_t runnable;
     int32_t in_margin;   // every chip index of the epoch lies in the padded LDS replica
     int32_t published;   // anchors ready: generic blocks, or AVX segments (S + 1 = all, tail included)
-    int32_t next_task;   // work dealer of the correlating waves
     int32_t locked;      // lock_status outcome (wave 1) for the loop update (wave 0)
     double coh;          // epoch_pre's coherent integration time (0: no lock test this epoch)
     float red[kPWaves][2 * (kMaxTaps + 1)];
@@ -103,14 +104,6 @@ __device__ __forceinline__ void publish(int32_t* p, int v) { __hip_atomic_store(
 __device__ __forceinline__ void wait_published(int32_t* p, int need)
 {
     while (__hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < need) __builtin_amdgcn_s_sleep(1);
-}
-
-// Next task index for the whole wave (lane 0 draws, everyone gets it as a uniform value).
-__device__ __forceinline__ int deal(int32_t* next, int lane)
-{
-    int v = 0;
-    if (lane == 0) v = __hip_atomic_fetch_add(next, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    return __builtin_amdgcn_readfirstlane(__shfl(v, 0, kWave));
 }
 
 // AVX geometry of an N-sample epoch: M = N/16 iterations, cut into tasks of G iterations (G = 16,
@@ -204,7 +197,7 @@ __device__ void replay_avx(const PEpoch& ep, f2* Z, f2* T, int N, int G, int lan
 // exact anchor and, once per epoch, the lane factor (corr_device.h correlate_block).
 template <int FMT, int NT, bool DATA, bool IN_MARGIN>
 __device__ void consume_generic(PEpoch& ep, const Anchor* A, i4v span, int N, const float* code0, const float* code1, int L, int lane,
-    f2 (&acc)[NT + 1])
+    int wave, f2 (&acc)[NT + 1])
 {
     const DevJob& job = ep.job;
     const int nblk = (N + kRenorm - 1) / kRenorm;
@@ -218,9 +211,8 @@ __device__ void consume_generic(PEpoch& ep, const Anchor* A, i4v span, int N, co
 #pragma unroll
     for (int t = 0; t < NT; t++) shifts[t] = job.shifts[t];
     const float zero_shift[1] = {0.0f};
-    for (;;) {
-        const int kb = deal(&ep.next_task, lane);
-        if (kb >= nblk) break;
+    if (wave == 0) return;  // the replay wave
+    for (int kb = wave - 1; kb < nblk; kb += kPWaves - 1) {  // static: wave w ≥ 1 takes blocks w − 1 (mod 3)
         f2 x[kLaneSamples];
         load_any<FMT>(span, lane, kb, N, x);  // in flight while the anchor is awaited
         wait_published(&ep.published, kb + 1);
@@ -257,7 +249,7 @@ __device__ __forceinline__ float code_at(const float* code, int L, float sn, flo
 // task's anchors are awaited); the step after the last correlates the N mod 16 tail samples.
 template <int FMT, int NT, bool DATA, bool IN_MARGIN, int kB>
 __device__ void consume_avx(PEpoch& ep, const f2* Z, const f2* T, i4v span, int N, int G, const float* code0, const float* code1, int L,
-    int lane, f2 (&acc)[NT + 1])
+    int lane, int wave, f2 (&acc)[NT + 1])
 {
     const DevJob& job = ep.job;
     const int M = N / kAvxLanes, S = avx_tasks(M, G);
@@ -269,9 +261,8 @@ __device__ void consume_avx(PEpoch& ep, const f2* Z, const f2* T, i4v span, int 
 #pragma unroll
     for (int t = 0; t < NT; t++) shifts[t] = job.shifts[t];
     constexpr int SB = sample_bytes<FMT>();
-    for (;;) {
-        const int g = deal(&ep.next_task, lane);
-        if (g >= n_steps) break;
+    if (wave == 0) return;  // the replay wave
+    for (int g = wave - 1; g < n_steps; g += kPWaves - 1) {  // static: wave w ≥ 1 takes steps w − 1 (mod 3)
         if (g == n_groups) {  // the serial tail (:292-304)
             wait_published(&ep.published, S + 1);
             if (lane < tail) {
@@ -461,7 +452,6 @@ __global__ __launch_bounds__(kPThreads, persist_waves_per_simd<THRU>()) void trk
                     sc.epoch_start = sc.nitems_read;
                 }
                 ep.published = 0;
-                ep.next_task = 0;
                 GNSSHIP_TRK_STAMP(e, 1);
             }
         }
@@ -475,16 +465,16 @@ __global__ __launch_bounds__(kPThreads, persist_waves_per_simd<THRU>()) void trk
             if (wave == 0 && lane < kAvxLanes) replay_avx(ep, Z, T, N, avx_g, lane, &ep.published);
             if (tid == 0) GNSSHIP_TRK_STAMP(e, 2);
             if (ep.in_margin)
-                consume_avx<FMT, NT, DATA, true, THRU ? 4 : 16>(ep, Z, T, span, N, avx_g, c0, c1, L, lane, acc);
+                consume_avx<FMT, NT, DATA, true, THRU ? 4 : 16>(ep, Z, T, span, N, avx_g, c0, c1, L, lane, wave, acc);
             else
-                consume_avx<FMT, NT, DATA, false, THRU ? 4 : 16>(ep, Z, T, span, N, avx_g, c0, c1, L, lane, acc);
+                consume_avx<FMT, NT, DATA, false, THRU ? 4 : 16>(ep, Z, T, span, N, avx_g, c0, c1, L, lane, wave, acc);
         } else {
             if (wave == 0 && lane == 0) replay_generic(ep.job, A, (N + kRenorm - 1) / kRenorm, &ep.published);
             if (tid == 0) GNSSHIP_TRK_STAMP(e, 2);
             if (ep.in_margin)
-                consume_generic<FMT, NT, DATA, true>(ep, A, span, N, c0, c1, L, lane, acc);
+                consume_generic<FMT, NT, DATA, true>(ep, A, span, N, c0, c1, L, lane, wave, acc);
             else
-                consume_generic<FMT, NT, DATA, false>(ep, A, span, N, c0, c1, L, lane, acc);
+                consume_generic<FMT, NT, DATA, false>(ep, A, span, N, c0, c1, L, lane, wave, acc);
             // anchor frame → sample frame: × E_{4·lane} (corr_kernel.hip)
             const f2 er = lane_rotation(ep.job, kLaneSamples * lane);
             const f2 esw = f2{-er.y, er.x};

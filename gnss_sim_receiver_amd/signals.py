@@ -254,3 +254,16 @@ def c3_sky(cn0: float = 45.0):
     rng = np.random.Generator(np.random.PCG64(seed))
     prns = sorted(int(p) for p in rng.choice(np.arange(1, 33), 10, replace=False))
     return random_sky(10, seed=seed, cn0=cn0, prns=prns)
+
+
+def c1_sky(cn0: float = 45.0, extra=()):
+    """BASELINE.md / SURVEY §8d C1: GPS PRN 7 at fD = 1730 Hz with its code delayed 1234 samples at
+    4 Msps (315.6 chips), GPS navigation bits (the TLM preamble pattern, so bit synchronisation
+    completes); `extra`: more satellites (prn, doppler_hz, delay_samples) for multi-channel runs."""
+    fs = 4e6
+    sats = []
+    for prn, fd, delay in ((7, 1730.0, 1234.0),) + tuple(extra):
+        s = Satellite(prn=prn, doppler_hz=fd, code_delay_chips=delay * 1.023e6 / fs, carrier_phase_rad=0.7, cn0_dbhz=cn0)
+        s.bits = "1000101100110"
+        sats.append(s)
+    return sats

@@ -1,11 +1,10 @@
 """The multi-GPU fan-out of the C ABI (gnsship_comm_*, comm_abi.hip) and the sharded paths, on the
 one-GPU box: a one-rank RCCL communicator (broadcast / all-gather / max through the real RCCL calls
 on the context stream), and the sharding invariances the multi-rank runs rely on — a PRN's
-acquisition result does not depend on which other PRNs share its launch (bit-identical), and a
-channel's closed loop does not depend on which other channels share the persistent kernel (identical
-sample counters and states; loop values within the tolerances of the oracle parity tests, since the
-correlating waves deal their tasks dynamically and the float tap sums are not bit-reproducible from
-run to run).  Multi-rank orchestration is covered with gloo on CPU
+acquisition result does not depend on which other PRNs share its launch, and a channel's closed
+loop does not depend on which other channels share the persistent kernel (the correlating waves
+follow a static schedule, so every float sum is formed in the same order): a rank's shard gives
+bit-identical results to the single-GPU run, and so does a repeated run.  Multi-rank orchestration is covered with gloo on CPU
 (tests/test_dist.py); RCCL refuses two ranks on one device."""
 import numpy as np
 import pytest
@@ -89,13 +88,11 @@ def test_closed_loop_channel_shards_equal_full_run(ctx):
         return {c: rec[:, j] for j, c in enumerate(chans)}
 
     full = run(list(range(n_ch)))
+    again = run(list(range(n_ch)))
+    for c in range(n_ch):
+        assert full[c].tobytes() == again[c].tobytes(), c  # bit-reproducible run to run
     for rank in range(2):
         part = run(sharding.shard_channels(n_ch, 2, rank))
         for c, r in part.items():
-            for f in ("sample_counter", "state", "prn_length_samples"):
-                np.testing.assert_array_equal(r[f], full[c][f])
-            np.testing.assert_allclose(r["carrier_doppler_hz"], full[c]["carrier_doppler_hz"], rtol=0, atol=2e-3)
-            np.testing.assert_allclose(r["code_phase_samples"], full[c]["code_phase_samples"], rtol=0, atol=1e-4)
-            p, q = r["prompt_i"] + 1j * r["prompt_q"], full[c]["prompt_i"] + 1j * full[c]["prompt_q"]
-            assert np.max(np.abs(p - q) / np.maximum(np.abs(q), 1e-30)) < 1e-4
+            assert r.tobytes() == full[c].tobytes(), c  # and independent of the other channels
     dev.free()
