@@ -141,7 +141,7 @@ def test_oracle_f64_accumulation_variant():
     from gnss_sim_receiver_amd import signals
     sats = signals.random_sky(2, seed=8)
     for n, lo, hi in [(4000, 0.0, 5e-6), (100000, 1e-7, 5e-5)]:
-        sig = signals.generate_if(4e6 if n == 4000 else 25e6, n + 8000, sats, seed=2)
+        sig = signals.generate_if(4e6 if n == 4000 else 25e6, 2 * n + 8000, sats, seed=2)  # jobs start up to one code period in
         jobs = np.concatenate([signals.truth_jobs(s, 4e6 if n == 4000 else 25e6, 1, n, [-0.25, 0, 0.25], k)
                                for k, s in enumerate(sats)])
         codes = [s.code for s in sats]
