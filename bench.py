@@ -312,6 +312,60 @@ def acq_c3_sharded(ctx, torch, rank, world, device, barrier, reps=20):
             "fanout": COMM["transport"]}
 
 
+def c1_receiver(torch, device, seconds=10.0, cpu_seconds=1.0):
+    """BASELINE configs[0] (C1): a 10-s 4 Msps gr_complex file with GPS PRN 7 (fD 1730 Hz, delay 1234
+    samples) through the Channel role end to end — tools/gnsship_rx (include/gnsship_receiver.hpp:
+    5 channels, 1 in acquisition, pfa 0.01, ±10 kHz / 250 Hz, pll 40 / dll 4 — conf/gnss-sdr_GPS_L1_
+    gr_complex.conf) — timed as a process over the file; beside it the oracle restatement of the same
+    receiver (oracle/receiver.py: numpy FFT acquisition, scalar-C tracking, one thread) on the first
+    `cpu_seconds` of the same file."""
+    import subprocess
+    import tempfile
+    from gnss_sim_receiver_amd import signals as S
+    fs = 4000000
+    sats = S.c1_sky()
+    d = tempfile.mkdtemp(prefix="gnsship_c1_")
+    path = os.path.join(d, "c1.dat")
+    n = int(seconds * fs)
+    x = S.generate_if_device(fs, n, sats, seed=0x6E550001, device=f"cuda:{device}")
+    x.cpu().numpy().tofile(path)
+    del x
+    rx = os.path.join(ROOT, "tools", "gnsship_rx")
+    t0 = time.perf_counter()
+    out = subprocess.run([rx, "--file", path, "--fs", str(fs), "--channels", "5", "--in-acquisition", "1", "--events",
+                          os.path.join(d, "ev.csv"), "--dump", os.path.join(d, "trk_ch_")], capture_output=True, text=True, timeout=600)
+    wall = time.perf_counter() - t0
+    if out.returncode != 0:
+        raise RuntimeError(f"gnsship_rx failed: {out.stderr[-400:]}")
+    summ = json.loads(out.stdout.strip().splitlines()[-1])
+    ev = np.loadtxt(os.path.join(d, "ev.csv"), delimiter=",", skiprows=1, ndmin=2)
+    pos = ev[ev[:, 2] == 1]
+    res = {"config": "C1 (configs[0]): GPS L1 C/A PRN 7, 4 Msps gr_complex file, 10 s; 5 channels, 1 in acquisition, pfa 0.01, "
+                     "dmax 10000 / step 250, pll 40 / dll 4 (conf/gnss-sdr_GPS_L1_gr_complex.conf) — tools/gnsship_rx end to end",
+           "signal_s": summ["signal_s"], "process_wall_s": round(wall, 3), "receiver_wall_s": round(summ["wall_s"], 3),
+           "init_s": round(summ["init_s"], 3), "file_read_s": round(summ["io_s"], 3),
+           "realtime_factor": round(summ["signal_s"] / summ["wall_s"], 1),
+           "acq_attempts": summ["acq_positive"] + summ["acq_negative"], "acq_positive": summ["acq_positive"],
+           "prn7_acquired_at_s": round(float(pos[pos[:, 3] == 7][0, 0]) / fs, 4) if (pos[:, 3] == 7).any() else None,
+           "prn7_doppler_hz": float(pos[pos[:, 3] == 7][0, 4]) if (pos[:, 3] == 7).any() else None,
+           "channels": summ["channels"]}
+    if cpu_seconds > 0:
+        from oracle import receiver as R
+        xs = np.fromfile(path, np.complex64, count=int(cpu_seconds * fs))
+        t0 = time.perf_counter()
+        orx = R.Receiver(R.ReceiverConf(channels=5, in_acquisition=1, rotator_avx=1, block_samples=fs // 10))
+        orx.work(xs)
+        dt = time.perf_counter() - t0
+        res["cpu_baseline"] = {"kind": "port", "cores": 1, "sample": f"first {cpu_seconds} s of the same file",
+                               "realtime_factor": round(cpu_seconds / dt, 2), "wall_s": round(dt, 3),
+                               "note": "oracle/receiver.py: the same control logic, numpy (pocketfft) acquisition, scalar-C DLL/PLL"}
+        res["gpu_vs_cpu"] = round(res["realtime_factor"] / res["cpu_baseline"]["realtime_factor"], 1)
+    for f in os.listdir(d):
+        os.remove(os.path.join(d, f))
+    os.rmdir(d)
+    return res
+
+
 # ---------------------------------------------------------------------------------------------------
 # CPU baseline: the oracle's closed loop, one thread per channel (ctypes releases the GIL)
 def cpu_baseline(h, budget_s):
@@ -697,6 +751,8 @@ def main():
         blk = S.generate_if(FS, VL, sky, seed=SEED)
         result["acquisition"] = acq_bench(ctx, FS, VL, blk, "32 PRN x 40 bins, fft 4000, 4 Msps")
         result["acquisition_e1"] = acq_e1_bench(ctx)
+        if world == 1:
+            result["c1_receiver"] = c1_receiver(torch, device, cpu_seconds=1.0 if args.cpu_seconds > 0 else 0.0)
         result["tracking_c4_e1_open_loop"] = e1_open_loop(ctx)
         result["tracking_c5_hybrid_open_loop"] = c5_open_loop(ctx)
     del h
