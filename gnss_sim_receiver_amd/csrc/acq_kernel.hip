@@ -20,6 +20,20 @@
 
 namespace gnsship {
 
+// Phase timestamps of acq_search_big_kernel for the profiling build only (make prof,
+// scripts/acq_wg_profile.py): slot [workgroup·16 + k] = wall_clock64() at phase k, thread 0.
+#ifdef GNSSHIP_CORR_PROFILE
+__device__ unsigned long long* g_acq_prof = nullptr;
+#define GNSSHIP_ACQ_STAMP(k) \
+    do { \
+        if (g_acq_prof && threadIdx.x == 0) g_acq_prof[(static_cast<size_t>(blockIdx.y) * gridDim.x + blockIdx.x) * 16 + (k)] = wall_clock64(); \
+    } while (0)
+#else
+#define GNSSHIP_ACQ_STAMP(k) \
+    do { \
+    } while (0)
+#endif
+
 __device__ __forceinline__ float2 cmulf(float2 a, float2 b)
 {
     return make_float2(__fsub_rn(__fmul_rn(a.x, b.x), __fmul_rn(a.y, b.y)), __fadd_rn(__fmul_rn(a.x, b.y), __fmul_rn(a.y, b.x)));
@@ -118,7 +132,7 @@ __device__ __forceinline__ void stockham_pass(float2* __restrict__ buf, int N, i
             for (int r = 0; r < R; r++) {
                 float2 x = buf[j + r * nb];
                 if (r > 0 && k > 0) {
-                    float2 w = tw[(k * r * tstep) % N];
+                    float2 w = tw[k * r * tstep];  // k·r·tstep < Ns·R·tstep = N
                     if (SIGN > 0) w.y = -w.y;
                     x = cmulf(x, w);
                 }
@@ -158,6 +172,17 @@ __device__ void fft_lds(float2* __restrict__ buf, const FftPlan& plan, const flo
     }
 }
 
+// Transforms of up to kTwLdsMax points read their twiddles from LDS: the N-entry table is staged
+// next to the data once per workgroup (every Stockham pass otherwise waits on L2 for its R − 1
+// twiddle loads, with only one or two butterflies per thread to hide them).
+constexpr int kTwLdsMax = 4096;
+
+__device__ __forceinline__ const float2* stage_twiddles(float2* dst, const float2* __restrict__ tw, int n)
+{
+    for (int i = threadIdx.x; i < n; i += blockDim.x) dst[i] = tw[i];
+    return dst;  // visible after the caller's next barrier
+}
+
 // rows[b] = FFT(sig ⊙ mult[b])  (mult == nullptr: FFT(sig)); conj_out: store conj (code FFT).
 template <int FMT>
 __global__ __launch_bounds__(kAcqThreads) void acq_fft_rows_kernel(const void* __restrict__ sig, const float2* __restrict__ mult,
@@ -167,13 +192,14 @@ __global__ __launch_bounds__(kAcqThreads) void acq_fft_rows_kernel(const void* _
     const int b = blockIdx.x;
     const int N = plan.n;
     const float2* m = mult ? mult + static_cast<int64_t>(b) * N : nullptr;
+    const float2* twl = N <= kTwLdsMax ? stage_twiddles(lds + N, tw, N) : tw;
     for (int i = threadIdx.x; i < N; i += blockDim.x) {
         float2 x = i < n_valid ? load_if<FMT>(sig, i) : make_float2(0.0f, 0.0f);  // zero-padded past the consumed samples
         if (m) x = cmulf(x, m[i]);  // volk_32fc_x2_multiply_32fc(in, wipeoff)
         lds[i] = x;
     }
     __syncthreads();
-    fft_lds<-1>(lds, plan, tw);
+    fft_lds<-1>(lds, plan, twl);
     float2* out = rows + static_cast<int64_t>(b) * N;
     for (int i = threadIdx.x; i < N; i += blockDim.x) {
         float2 y = lds[i];
@@ -187,76 +213,142 @@ __global__ __launch_bounds__(kAcqThreads) void acq_fft_rows_kernel(const void* _
 // 25 Msps): four-step with one workgroup per transform, N = P·M, M ≤ 1024 rows of the LDS stage and
 // P ≤ 32 points per thread in registers.  Thread t owns column t: x[t + M·q], q < P.
 //   forward:  X[kq + P·k] = Σ_t W_M^{t·k} · W_N^{t·kq} · Σ_q x[t + M·q] W_P^{q·kq}
-//             (register P-point DFT, twiddle, then M-point row DFTs in LDS, 16 rows per round);
+//             (register P-point DFT, twiddle, then M-point row DFTs in LDS: 16 rows per round,
+//             one per wave, each wave running its row's passes with no workgroup barrier);
 //             stored row-major TRANSPOSED: XT[kq·M + k] = X[kq + P·k].
 //   inverse:  y[t + M·q] = Σ_kq W_P^{−q·kq} · W_N^{−t·kq} · Σ_k Z[kq + P·k] W_M^{−t·k}
 //             reads Z in the same transposed layout (rows first, registers last) and so returns
 //             natural order.  Point-wise products between two transposed spectra need no reorder.
 // Pass twiddles come from the N-entry table: exp(−2πi m/M) = tw[m·P].
 // ---------------------------------------------------------------------------------------------
-constexpr int kBigRows = 8;  // rows per LDS round: two ping-pong buffers of 8 × M ≤ 8192 complex (2 × 64 KiB)
-
-// Out-of-place Stockham pass over `rows` rows of length M: src → dst, one barrier.  Out of place so
-// a butterfly's R values are the only registers it needs (the P register points of the four-step
-// stay live across the row passes; 1024 threads leave 128 VGPRs per lane).
-template <int R, int SIGN>
-__device__ __forceinline__ void stockham_pass_rows(const float2* __restrict__ src, float2* __restrict__ dst, int M, int rows, int Ns,
-    const float2* __restrict__ tw, int tw_stride)
-{
-    const int nb = M / R;
-    const int total = rows * nb;
-    const int tstep = (M / (Ns * R)) * tw_stride;
-    for (int j = threadIdx.x; j < total; j += kAcqThreads) {
-        const int row = j / nb;
-        const int jl = j - row * nb;
-        const int k = jl % Ns;
-        const float2* in = src + row * M + jl;
-        float2 v[R];
-#pragma unroll
-        for (int r = 0; r < R; r++) {
-            float2 x = in[r * nb];
-            if (r > 0 && k > 0) {
-                float2 w = tw[k * r * tstep];
-                if (SIGN > 0) w.y = -w.y;
-                x = cmulf(x, w);
-            }
-            v[r] = x;
-        }
-        dft_small<R, SIGN>(v);
-        float2* out = dst + row * M + (jl / Ns) * Ns * R + k;
-#pragma unroll
-        for (int r = 0; r < R; r++) out[r * Ns] = v[r];
-    }
-    __syncthreads();
-}
-
-// Row FFTs from buffer a; returns the buffer (a or b) holding the result.
-template <int SIGN>
-__device__ __forceinline__ float2* fft_rows_lds(float2* __restrict__ a, float2* __restrict__ b, const FftPlan& plan, int rows,
-    const float2* __restrict__ tw, int tw_stride)
-{
-    int Ns = 1;
-    for (int p = 0; p < plan.n_passes; p++) {
-        const int R = plan.radix[p];
-        switch (R) {
-        case 2: stockham_pass_rows<2, SIGN>(a, b, plan.n, rows, Ns, tw, tw_stride); break;
-        case 3: stockham_pass_rows<3, SIGN>(a, b, plan.n, rows, Ns, tw, tw_stride); break;
-        case 4: stockham_pass_rows<4, SIGN>(a, b, plan.n, rows, Ns, tw, tw_stride); break;
-        case 5: stockham_pass_rows<5, SIGN>(a, b, plan.n, rows, Ns, tw, tw_stride); break;
-        default: stockham_pass_rows<8, SIGN>(a, b, plan.n, rows, Ns, tw, tw_stride); break;
-        }
-        float2* t = a;
-        a = b;
-        b = t;
-        Ns *= R;
-    }
-    return a;
-}
-
 constexpr int first_radix(int m)
 {
     return (m % 8 == 0) ? 8 : (m % 5 == 0) ? 5 : (m % 4 == 0) ? 4 : (m % 3 == 0) ? 3 : 2;
 }
+
+// Column twiddles W_N^{t·kq} of the four-step with the row length known at compile time, from two
+// small LDS tables instead of the N-entry table in HBM: t = B·a + b (B | M) gives
+// W_N^{t·kq} = W_N^{B·a·kq} · W_N^{b·kq}, tables tw[B·e] (e = a·kq < (M/B)·P) and tw[e] (e = b·kq < B·P).
+constexpr int col_split(int m)
+{
+    int b = 1;
+    while (b * b < m || m % b) b++;
+    return b;
+}
+
+// Wave-level row transforms: each wave owns whole rows of the four-step and runs every Stockham
+// pass of its row in place, with no workgroup barrier — a pass loads all of the lane's butterflies
+// into registers before any store, and a wave's LDS operations complete in program order (the fence
+// keeps the compiler from moving a store above the loads).  The workgroup meets only at the
+// column↔row transposes.  tw[m] = exp(−2πi m/M) (the row table staged in LDS).
+constexpr int kWaveRows = kAcqThreads / 64;  // rows transformed per round (one per wave)
+
+template <int R, int SIGN>
+__device__ __forceinline__ void wave_pass(float2* __restrict__ buf, int M, int Ns, const float2* __restrict__ tw, int lane)
+{
+    constexpr int MAXB = (kAcqThreads / R + 63) / 64;  // butterflies per lane for M ≤ 1024
+    const int nb = M / R;
+    const int tstep = M / (Ns * R);
+    float2 v[MAXB][R];
+#pragma unroll
+    for (int c = 0; c < MAXB; c++) {
+        const int j = lane + 64 * c;
+        if (j < nb) {
+            const int k = j % Ns;
+#pragma unroll
+            for (int r = 0; r < R; r++) {
+                float2 x = buf[j + r * nb];
+                if (r > 0 && k > 0) {
+                    float2 w = tw[k * r * tstep];
+                    if (SIGN > 0) w.y = -w.y;
+                    x = cmulf(x, w);
+                }
+                v[c][r] = x;
+            }
+            dft_small<R, SIGN>(v[c]);
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int c = 0; c < MAXB; c++) {
+        const int j = lane + 64 * c;
+        if (j < nb) {
+            const int k = j % Ns;
+            const int base = (j / Ns) * Ns * R + k;
+#pragma unroll
+            for (int r = 0; r < R; r++) buf[base + r * Ns] = v[c][r];
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
+// The same passes with the row length known at compile time (MC > 0): radices first_radix(M / Ns)
+// in order, every index split j / Ns, j % Ns and twiddle stride a constant (the runtime form spends
+// more VALU on integer division than on the butterflies).
+template <int MC, int NsC, int SIGN>
+__device__ __forceinline__ void wave_fft_row_ct(float2* __restrict__ buf, const float2* __restrict__ tw, int lane)
+{
+    if constexpr (NsC < MC) {
+        constexpr int R = first_radix(MC / NsC);
+        constexpr int nb = MC / R;
+        constexpr int tstep = MC / (NsC * R);
+        constexpr int MAXB = (nb + 63) / 64;
+        float2 v[MAXB][R];
+#pragma unroll
+        for (int c = 0; c < MAXB; c++) {
+            const int j = lane + 64 * c;
+            if (j < nb) {
+                const int k = j % NsC;
+#pragma unroll
+                for (int r = 0; r < R; r++) {
+                    float2 x = buf[j + r * nb];
+                    if (r > 0 && NsC > 1) {
+                        float2 w = tw[k * r * tstep];
+                        if (SIGN > 0) w.y = -w.y;
+                        x = cmulf(x, w);
+                    }
+                    v[c][r] = x;
+                }
+                dft_small<R, SIGN>(v[c]);
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int c = 0; c < MAXB; c++) {
+            const int j = lane + 64 * c;
+            if (j < nb) {
+                const int k = j % NsC;
+                const int base = (j / NsC) * NsC * R + k;
+#pragma unroll
+                for (int r = 0; r < R; r++) buf[base + r * NsC] = v[c][r];
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_sched_barrier(0);  // keep the next pass's loads from being hoisted into this one (register pressure)
+        wave_fft_row_ct<MC, NsC * R, SIGN>(buf, tw, lane);
+    }
+}
+
+template <int SIGN>
+__device__ __forceinline__ void wave_fft_row(float2* __restrict__ row, const FftPlan& plan, const float2* __restrict__ tw, int lane)
+{
+    int Ns = 1;
+    for (int p = 0; p < plan.n_passes; p++) {
+        switch (plan.radix[p]) {
+        case 2: wave_pass<2, SIGN>(row, plan.n, Ns, tw, lane); break;
+        case 3: wave_pass<3, SIGN>(row, plan.n, Ns, tw, lane); break;
+        case 4: wave_pass<4, SIGN>(row, plan.n, Ns, tw, lane); break;
+        case 5: wave_pass<5, SIGN>(row, plan.n, Ns, tw, lane); break;
+        default: wave_pass<8, SIGN>(row, plan.n, Ns, tw, lane); break;
+        }
+        Ns *= plan.radix[p];
+    }
+}
+
 
 // cos/sin of 2π·m/L in double by Taylor series, for compile-time register-DFT twiddles (L ≤ 32).
 constexpr double ct_sin_red(double x)
@@ -319,8 +411,62 @@ __device__ __forceinline__ void dft_reg(float2* x, const float2* __restrict__ tw
     }
 }
 
+// In-place register DFT for P = R1·R2 (R1 = first_radix(P), R2 a supported radix): with
+// n = R2·n1 + n2,  X[k1 + R1·k2] = Σ_n2 W_P^{n2·k1} W_R2^{n2·k2} Σ_n1 x[R2·n1 + n2] W_R1^{n1·k1}.
+// Stage 1 writes the R1-point results back into the slots they came from, stage 2 likewise, so only
+// one butterfly's values are live beside the P points (the Stockham form above holds a second P-point
+// array and spills at 128 VGPRs).  Output X[q] is left in slot reg_slot<P>(q) = R2·(q mod R1) + q/R1.
+constexpr bool small_radix(int r) { return r == 2 || r == 3 || r == 4 || r == 5 || r == 8; }
+template <int P>
+constexpr bool two_factor() { return small_radix(first_radix(P)) && small_radix(P / first_radix(P)) && first_radix(P) * (P / first_radix(P)) == P; }
+template <int P>
+constexpr int reg_slot(int q)
+{
+    if constexpr (two_factor<P>()) {
+        constexpr int R1 = first_radix(P), R2 = P / R1;
+        return R2 * (q % R1) + q / R1;
+    } else {
+        return q;
+    }
+}
+
+template <int P, int SIGN>
+__device__ __forceinline__ void dft_reg_inplace(float2* x, const float2* __restrict__ tw, int N)
+{
+    if constexpr (two_factor<P>()) {
+        constexpr int R1 = first_radix(P), R2 = P / R1;
+#pragma unroll
+        for (int n2 = 0; n2 < R2; n2++) {
+            float2 v[R1];
+#pragma unroll
+            for (int n1 = 0; n1 < R1; n1++) v[n1] = x[R2 * n1 + n2];
+            dft_small<R1, SIGN>(v);
+#pragma unroll
+            for (int k1 = 0; k1 < R1; k1++) {
+                float2 a = v[k1];
+                if (n2 > 0 && k1 > 0) {
+                    const double ang = ct_angle(n2 * k1, P);
+                    a = cmulf(a, make_float2(static_cast<float>(ct_cos_red(ang)), static_cast<float>(SIGN * ct_sin_red(ang))));
+                }
+                x[R2 * k1 + n2] = a;
+            }
+        }
+#pragma unroll
+        for (int k1 = 0; k1 < R1; k1++) {
+            float2 v[R2];
+#pragma unroll
+            for (int n2 = 0; n2 < R2; n2++) v[n2] = x[R2 * k1 + n2];
+            dft_small<R2, SIGN>(v);
+#pragma unroll
+            for (int k2 = 0; k2 < R2; k2++) x[R2 * k1 + k2] = v[k2];
+        }
+    } else {
+        dft_reg<P, 1, SIGN>(x, tw, N);
+    }
+}
+
 // rowsT[b] = transposed FFT(sig ⊙ mult[b]); conj_out for the code spectrum.
-template <int FMT, int P>
+template <int FMT, int P, int MC = 0>
 __global__ __launch_bounds__(kAcqThreads) void acq_fft_big_kernel(const void* __restrict__ sig, const float2* __restrict__ mult,
     FftPlan row_plan, const float2* __restrict__ tw, float2* __restrict__ rowsT, int conj_out, int n_valid)
 {
@@ -338,23 +484,35 @@ __global__ __launch_bounds__(kAcqThreads) void acq_fft_big_kernel(const void* __
             if (m) x = cmulf(x, m[t + M * q]);  // volk_32fc_x2_multiply_32fc(in, wipeoff)
             v[q] = x;
         }
-        dft_reg<P, 1, -1>(v, tw, N);
+        dft_reg_inplace<P, -1>(v, tw, N);  // X[kq] in v[reg_slot<P>(kq)]
     }
     float2* out = rowsT + static_cast<int64_t>(b) * N;
+    float2* rtw = lds + kWaveRows * M;  // row twiddles exp(−2πi m/M) = tw[m·P], m < M
+    for (int i = t; i < M; i += kAcqThreads) rtw[i] = tw[i * P];
+    const int lane = t & 63, wave = t >> 6;
 #pragma unroll
-    for (int r0 = 0; r0 < P; r0 += kBigRows) {
-        const int nrows = (P - r0) < kBigRows ? (P - r0) : kBigRows;
+    for (int r0 = 0; r0 < P; r0 += kWaveRows) {
+        const int nrows = (P - r0) < kWaveRows ? (P - r0) : kWaveRows;
         if (t < M) {
 #pragma unroll
-            for (int kk = 0; kk < kBigRows; kk++) {
+            for (int kk = 0; kk < kWaveRows; kk++) {
                 const int kq = r0 + kk;
-                if (kq < P) lds[kk * M + t] = kq ? cmulf(v[kq], tw[t * kq]) : v[kq];  // W_N^{t·kq}, t·kq < N
+                if (kq < P) {
+                    const float2 xk = v[reg_slot<P>(kq)];
+                    lds[kk * M + t] = kq ? cmulf(xk, tw[t * kq]) : xk;  // W_N^{t·kq}, t·kq < N
+                }
             }
         }
         __syncthreads();
-        const float2* res = fft_rows_lds<-1>(lds, lds + kBigRows * M, row_plan, nrows, tw, P);
+        if (wave < nrows) {
+            int lane_r = lane;
+            asm volatile("" : "+v"(lane_r));
+            if constexpr (MC > 0) wave_fft_row_ct<MC, 1, -1>(lds + wave * M, rtw, lane_r);
+            else wave_fft_row<-1>(lds + wave * M, row_plan, rtw, lane);
+        }
+        __syncthreads();
         for (int i = t; i < nrows * M; i += kAcqThreads) {
-            float2 y = res[i];
+            float2 y = lds[i];
             if (conj_out) y.y = -y.y;
             out[r0 * M + i] = y;
         }
@@ -374,15 +532,44 @@ __device__ __forceinline__ MaxIdx better(MaxIdx a, MaxIdx b)
     return a;
 }
 
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v)
+{
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
+template <int CTRL>
+__device__ __forceinline__ int dpp_i(int v)
+{
+    return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false);
+}
+
+// Wave reductions: within each 16-lane row by DPP (quad xor 1, xor 2, half-row mirror, row mirror —
+// each step pairs two already-reduced groups), across the four rows by two shuffles.
+__device__ __forceinline__ MaxIdx wave_argmax(MaxIdx m)
+{
+    m = better(m, MaxIdx{dpp_f<0xB1>(m.v), dpp_i<0xB1>(m.i)});    // quad_perm [1,0,3,2]
+    m = better(m, MaxIdx{dpp_f<0x4E>(m.v), dpp_i<0x4E>(m.i)});    // quad_perm [2,3,0,1]
+    m = better(m, MaxIdx{dpp_f<0x141>(m.v), dpp_i<0x141>(m.i)});  // row_half_mirror
+    m = better(m, MaxIdx{dpp_f<0x140>(m.v), dpp_i<0x140>(m.i)});  // row_mirror
+#pragma unroll
+    for (int o = 16; o <= 32; o <<= 1) m = better(m, MaxIdx{__shfl_xor(m.v, o, 64), __shfl_xor(m.i, o, 64)});
+    return m;
+}
+
+__device__ __forceinline__ float wave_sum_f(float s)
+{
+    s += dpp_f<0xB1>(s);
+    s += dpp_f<0x4E>(s);
+    s += dpp_f<0x141>(s);
+    s += dpp_f<0x140>(s);
+    s += __shfl_xor(s, 16, 64);
+    s += __shfl_xor(s, 32, 64);
+    return s;
+}
+
 __device__ __forceinline__ MaxIdx block_argmax(MaxIdx m, MaxIdx* red)
 {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) {
-        MaxIdx q;
-        q.v = __shfl_xor(m.v, o, 64);
-        q.i = __shfl_xor(m.i, o, 64);
-        m = better(m, q);
-    }
+    m = wave_argmax(m);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     if (lane == 0) red[wave] = m;
     __syncthreads();
@@ -394,8 +581,7 @@ __device__ __forceinline__ MaxIdx block_argmax(MaxIdx m, MaxIdx* red)
 
 __device__ __forceinline__ float block_sum(float s, float* red)
 {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o, 64);
+    s = wave_sum_f(s);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     if (lane == 0) red[wave] = s;
     __syncthreads();
@@ -403,6 +589,28 @@ __device__ __forceinline__ float block_sum(float s, float* red)
     for (int w = 0; w < static_cast<int>(blockDim.x >> 6); w++) r += red[w];
     __syncthreads();
     return r;
+}
+
+// Both at once (one barrier pair): the row maximum with its first index and the row sum.
+__device__ __forceinline__ void block_argmax_sum(MaxIdx& m, float& s, MaxIdx* redm, float* reds)
+{
+    m = wave_argmax(m);
+    s = wave_sum_f(s);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (lane == 0) {
+        redm[wave] = m;
+        reds[wave] = s;
+    }
+    __syncthreads();
+    MaxIdx r = redm[0];
+    float t = 0.0f;
+    for (int w = 0; w < static_cast<int>(blockDim.x >> 6); w++) {
+        if (w) r = better(r, redm[w]);
+        t += reds[w];
+    }
+    __syncthreads();
+    m = r;
+    s = t;
 }
 
 // grid: (n_bins, n_prns).  rowstat[(p*n_bins + b)] ; grid_out optional [p][b][row_len].
@@ -419,9 +627,10 @@ __global__ __launch_bounds__(kAcqThreads) void acq_search_kernel(const float2* _
     const int N = plan.n;
     const float2* x = X + static_cast<int64_t>(b) * N;
     const float2* c = codes_fft + static_cast<int64_t>(p) * N;
+    const float2* twl = N <= kTwLdsMax ? stage_twiddles(lds + N, tw, N) : tw;
     for (int i = threadIdx.x; i < N; i += blockDim.x) lds[i] = cmulf(x[i], c[i]);  // ×conj(code FFT)
     __syncthreads();
-    fft_lds<+1>(lds, plan, tw);
+    fft_lds<+1>(lds, plan, twl);
     // |Y|² in place (as float in the .x slot) + optional grid row (accumulated over dwells)
     float* row = grid_out ? grid_out + (static_cast<int64_t>(p) * n_bins + b) * rs.row_len : nullptr;
     MaxIdx m{-1.0f, 0x7fffffff};
@@ -437,8 +646,9 @@ __global__ __launch_bounds__(kAcqThreads) void acq_search_kernel(const float2* _
         m = better(m, MaxIdx{mag, i});
         s += mag;
     }
-    const MaxIdx best = block_argmax(m, red_m);
-    const float sum = block_sum(s, red_s);
+    block_argmax_sum(m, s, red_m, red_s);
+    const MaxIdx best = m;
+    const float sum = s;
     // second peak outside the circular window [best-spc, best+spc) (first_vs_second_peak_statistic :566-593)
     int e1 = best.i - rs.spc, e2 = best.i + rs.spc;
     if (e1 < 0) e1 += rs.win_mod; else if (e2 >= rs.win_mod) e2 -= rs.win_mod;
@@ -462,7 +672,7 @@ __global__ __launch_bounds__(kAcqThreads) void acq_search_kernel(const float2* _
 // Large-N search: Y = IFFT(XT_b ⊙ CT_p) by the transposed four-step (rows in LDS, then the
 // register P-point stage), |Y|² and the same row statistics as acq_search_kernel.  Thread t holds
 // y[t + M·q] for q < P, i.e. the natural index n = t + M·q.
-template <int P>
+template <int P, int MC = 0>
 __global__ __launch_bounds__(kAcqThreads) void acq_search_big_kernel(const float2* __restrict__ XT, const float2* __restrict__ codesT,
     FftPlan row_plan, const float2* __restrict__ tw, int n_bins, RowSpec rs, int accumulate, RowStat* __restrict__ rowstat,
     float* __restrict__ grid_out)
@@ -477,49 +687,98 @@ __global__ __launch_bounds__(kAcqThreads) void acq_search_big_kernel(const float
     const float2* x = XT + static_cast<int64_t>(b) * N;
     const float2* c = codesT + static_cast<int64_t>(p) * N;
     float2 v[P];
+    float2* rtw = lds + kWaveRows * M;  // row twiddles exp(−2πi m/M) = tw[m·P], m < M
+    for (int i = t; i < M; i += kAcqThreads) rtw[i] = tw[i * P];
+    constexpr int kB = MC > 0 ? col_split(MC) : 1;
+    float2* ct_lo = rtw + M;                      // tw[e], e < B·P        (MC > 0)
+    float2* ct_hi = ct_lo + kB * P;               // tw[B·e], e < (M/B)·P  (MC > 0)
+    if constexpr (MC > 0) {
+        for (int i = t; i < kB * P; i += kAcqThreads) ct_lo[i] = tw[i];
+        for (int i = t; i < (MC / kB) * P; i += kAcqThreads) ct_hi[i] = tw[kB * i];
+    }
+    const int lane = t & 63, wave = t >> 6;
+    // the short round first: the v[kq] of finished rounds stay live in registers through the later
+    // rounds' row passes, so the fewer of them the better (P = 25: 9 rows, then 16)
+    constexpr int kFirst = P - kWaveRows * ((P - 1) / kWaveRows);
+    constexpr int kRounds = 1 + (P - kFirst) / kWaveRows;
+    GNSSHIP_ACQ_STAMP(0);
 #pragma unroll
-    for (int r0 = 0; r0 < P; r0 += kBigRows) {
-        const int nrows = (P - r0) < kBigRows ? (P - r0) : kBigRows;
+    for (int rr = 0; rr < kRounds; rr++) {  // constant trip count: unrolled, v[] indices compile-time
+        const int r0 = rr == 0 ? 0 : kFirst + (rr - 1) * kWaveRows;
+        const int nrows = rr == 0 ? kFirst : kWaveRows;
         for (int i = t; i < nrows * M; i += kAcqThreads) lds[i] = cmulf(x[r0 * M + i], c[r0 * M + i]);  // ×conj(code FFT)
         __syncthreads();
-        const float2* res = fft_rows_lds<+1>(lds, lds + kBigRows * M, row_plan, nrows, tw, P);
+        GNSSHIP_ACQ_STAMP(r0 == 0 ? 1 : 4);
+        if (wave < nrows) {
+            // an opaque copy of the lane id per round: the row's index arithmetic is recomputed rather
+            // than kept live across rounds by common-subexpression elimination (register pressure)
+            int lane_r = lane;
+            asm volatile("" : "+v"(lane_r));
+            if constexpr (MC > 0) wave_fft_row_ct<MC, 1, +1>(lds + wave * M, rtw, lane_r);
+            else wave_fft_row<+1>(lds + wave * M, row_plan, rtw, lane);
+        }
+        __syncthreads();
+        GNSSHIP_ACQ_STAMP(r0 == 0 ? 2 : 5);
         if (t < M) {
 #pragma unroll
-            for (int kk = 0; kk < kBigRows; kk++) {
+            for (int kk = 0; kk < kWaveRows; kk++) {
                 const int kq = r0 + kk;
-                if (kq < P) {
-                    float2 w = tw[t * kq];  // W_N^{−t·kq}
-                    w.y = -w.y;
-                    v[kq] = kq ? cmulf(res[kk * M + t], w) : res[kk * M + t];
+                if (kk < nrows) {
+                    float2 w;
+                    if constexpr (MC > 0) {
+                        w = cmulf(ct_hi[(t / kB) * kq], ct_lo[(t % kB) * kq]);
+                    } else {
+                        w = tw[t * kq];
+                    }
+                    w.y = -w.y;  // W_N^{−t·kq}
+                    v[kq] = kq ? cmulf(lds[kk * M + t], w) : lds[kk * M + t];
                 }
             }
         }
         __syncthreads();
+        GNSSHIP_ACQ_STAMP(r0 == 0 ? 3 : 6);
     }
-    // |Y|² is parked in LDS (N floats ≤ the 2·kBigRows·M complex of the row buffers) for the
+    // |Y|² is parked in LDS (N floats ≤ the kWaveRows·M complex of the row buffer, P ≤ 32) for the
     // second-peak scan; all row-pass reads of LDS finished at the last round's barrier.
     float* mag = reinterpret_cast<float*>(lds);
     MaxIdx m{-1.0f, 0x7fffffff};
     float s = 0.0f;
     if (t < M) {
-        dft_reg<P, 1, +1>(v, tw, N);
-        float* row = grid_out ? grid_out + (static_cast<int64_t>(p) * n_bins + b) * rs.row_len : nullptr;
+        dft_reg_inplace<P, +1>(v, tw, N);  // y[t + M·q] in v[reg_slot<P>(q)]
+        // |y|² first (the complex points die as their magnitudes appear), then the optional grid
+        // row and the row statistics in separate branch-light loops
+        float g[P];
+#pragma unroll
+        for (int q = 0; q < P; q++) {
+            const float2 y = v[reg_slot<P>(q)];
+            g[q] = __fadd_rn(__fmul_rn(y.x, y.x), __fmul_rn(y.y, y.y));  // volk_32fc_magnitude_squared_32f
+        }
+        if (grid_out) {
+            float* row = grid_out + (static_cast<int64_t>(p) * n_bins + b) * rs.row_len;
+#pragma unroll
+            for (int q = 0; q < P; q++) {
+                const int i = t + M * q - rs.row_off;
+                if (i >= 0 && i < rs.row_len) {
+                    if (accumulate) g[q] = __fadd_rn(row[i], g[q]);  // volk_32f_x2_add_32f
+                    row[i] = g[q];
+                }
+            }
+        }
 #pragma unroll
         for (int q = 0; q < P; q++) {
             const int i = t + M * q - rs.row_off;  // index in the row
-            if (i < 0 || i >= rs.row_len) continue;
-            float g = __fadd_rn(__fmul_rn(v[q].x, v[q].x), __fmul_rn(v[q].y, v[q].y));  // volk_32fc_magnitude_squared_32f
-            if (row) {
-                if (accumulate) g = __fadd_rn(row[i], g);  // volk_32f_x2_add_32f
-                row[i] = g;
+            if (i >= 0 && i < rs.row_len) {
+                mag[i] = g[q];
+                m = better(m, MaxIdx{g[q], i});
+                s += g[q];
             }
-            mag[i] = g;
-            m = better(m, MaxIdx{g, i});
-            s += g;
         }
     }
-    const MaxIdx best = block_argmax(m, red_m);
-    const float sum = block_sum(s, red_s);
+    GNSSHIP_ACQ_STAMP(7);
+    block_argmax_sum(m, s, red_m, red_s);
+    const MaxIdx best = m;
+    const float sum = s;
+    GNSSHIP_ACQ_STAMP(8);
     int e1 = best.i - rs.spc, e2 = best.i + rs.spc;
     if (e1 < 0) e1 += rs.win_mod; else if (e2 >= rs.win_mod) e2 -= rs.win_mod;
     MaxIdx m2{0.0f, 0x7fffffff};
@@ -528,6 +787,7 @@ __global__ __launch_bounds__(kAcqThreads) void acq_search_big_kernel(const float
         m2 = better(m2, MaxIdx{in_win ? 0.0f : mag[i], i});
     }
     const MaxIdx second = block_argmax(m2, red_m);
+    GNSSHIP_ACQ_STAMP(9);
     if (t == 0) {
         RowStat r;
         r.max = best.v;
@@ -703,8 +963,9 @@ __global__ __launch_bounds__(kAcqThreads) void acq_huge_finalize_kernel(const fl
         m = better(m, MaxIdx{ts[i].max, ts[i].argmax});
         s += ts[i].sum;
     }
-    const MaxIdx best = block_argmax(m, red_m);
-    const float sum = block_sum(s, red_s);
+    block_argmax_sum(m, s, red_m, red_s);
+    const MaxIdx best = m;
+    const float sum = s;
     int e1 = best.i - rs.spc, e2 = best.i + rs.spc;
     if (e1 < 0) e1 += rs.win_mod; else if (e2 >= rs.win_mod) e2 -= rs.win_mod;
     const float* g = grid + cell * rs.row_len;
@@ -794,7 +1055,7 @@ hipError_t launch_acq_search_huge(const float2* XT, const float2* codesT, int pr
 hipError_t launch_acq_fft_rows(const void* sig, int fmt, const float2* mult, int n_rows, const FftPlan& plan, const float2* tw, float2* rows,
     int conj_out, int n_valid, hipStream_t stream)
 {
-    const size_t lds = sizeof(float2) * static_cast<size_t>(plan.n);
+    const size_t lds = sizeof(float2) * static_cast<size_t>(plan.n) * (plan.n <= kTwLdsMax ? 2 : 1);
     switch (fmt) {
     case GNSSHIP_FMT_CF32:
         hipLaunchKernelGGL(acq_fft_rows_kernel<GNSSHIP_FMT_CF32>, dim3(n_rows), dim3(kAcqThreads), lds, stream, sig, mult, plan, tw, rows, conj_out, n_valid);
@@ -813,7 +1074,7 @@ hipError_t launch_acq_fft_rows(const void* sig, int fmt, const float2* mult, int
 hipError_t launch_acq_search(const float2* X, const float2* codes_fft, int n_prns, int n_bins, const FftPlan& plan, const float2* tw,
     RowSpec rs, int accumulate, RowStat* rowstat, float* grid, hipStream_t stream)
 {
-    const size_t lds = sizeof(float2) * static_cast<size_t>(plan.n);
+    const size_t lds = sizeof(float2) * static_cast<size_t>(plan.n) * (plan.n <= kTwLdsMax ? 2 : 1);
     hipLaunchKernelGGL(acq_search_kernel, dim3(n_bins, n_prns), dim3(kAcqThreads), lds, stream, X, codes_fft, plan, tw, n_bins,
         rs, accumulate, rowstat, grid);
     return hipGetLastError();
@@ -832,8 +1093,13 @@ bool big_p_supported(int P)
 hipError_t launch_acq_fft_big(const void* sig, int fmt, const float2* mult, int n_rows, int P, const FftPlan& row_plan, const float2* tw,
     float2* rowsT, int conj_out, int n_valid, hipStream_t stream)
 {
-    const size_t lds = 2 * sizeof(float2) * static_cast<size_t>(kBigRows) * row_plan.n;
+    const size_t lds = (static_cast<size_t>(kWaveRows) + 1) * sizeof(float2) * row_plan.n;
     if (row_plan.n > kAcqThreads) return hipErrorInvalidValue;
+    if (P == 25 && row_plan.n == 1000 && fmt == GNSSHIP_FMT_CF32) {  // C3: N = 25000 (GPS 1 ms at 25 Msps)
+        hipLaunchKernelGGL((acq_fft_big_kernel<GNSSHIP_FMT_CF32, 25, 1000>), dim3(n_rows), dim3(kAcqThreads), lds, stream, sig, mult, row_plan, tw,
+            rowsT, conj_out, n_valid);
+        return hipGetLastError();
+    }
 #define GNSSHIP_P_CASE(p)                                                                                                            \
     case p:                                                                                                                          \
         if (fmt == GNSSHIP_FMT_CF32)                                                                                                 \
@@ -859,8 +1125,15 @@ hipError_t launch_acq_fft_big(const void* sig, int fmt, const float2* mult, int 
 hipError_t launch_acq_search_big(const float2* XT, const float2* codesT, int n_prns, int n_bins, int P, const FftPlan& row_plan,
     const float2* tw, RowSpec rs, int accumulate, RowStat* rowstat, float* grid, hipStream_t stream)
 {
-    const size_t lds = 2 * sizeof(float2) * static_cast<size_t>(kBigRows) * row_plan.n;
+    const size_t lds = (static_cast<size_t>(kWaveRows) + 1) * sizeof(float2) * row_plan.n;
     if (row_plan.n > kAcqThreads) return hipErrorInvalidValue;
+    if (P == 25 && row_plan.n == 1000) {  // C3: N = 25000
+        constexpr int kB = col_split(1000);
+        const size_t lds_c3 = lds + sizeof(float2) * static_cast<size_t>(kB * 25 + (1000 / kB) * 25);
+        hipLaunchKernelGGL((acq_search_big_kernel<25, 1000>), dim3(n_bins, n_prns), dim3(kAcqThreads), lds_c3, stream, XT, codesT, row_plan, tw, n_bins,
+            rs, accumulate, rowstat, grid);
+        return hipGetLastError();
+    }
 #define GNSSHIP_P_CASE(p)                                                                                                            \
     case p:                                                                                                                          \
         hipLaunchKernelGGL((acq_search_big_kernel<p>), dim3(n_bins, n_prns), dim3(kAcqThreads), lds, stream, XT, codesT, row_plan, tw, \
@@ -884,3 +1157,10 @@ hipError_t launch_acq_decide(const RowStat* rowstat, int n_prns, int n_bins, int
 }
 
 }  // namespace gnsship
+
+#ifdef GNSSHIP_CORR_PROFILE
+extern "C" int gnsship_debug_acq_profile(void* dev_buf)
+{
+    return hipMemcpyToSymbol(HIP_SYMBOL(gnsship::g_acq_prof), &dev_buf, sizeof(void*)) == hipSuccess ? 0 : -3;
+}
+#endif

@@ -1,0 +1,43 @@
+"""Acquisition sweeps for profiling (rocprofv3): C3 (32 PRN x 40 bins x 25000, 25 Msps, BASELINE's
+signal) and the C1 shape (32 PRN x 40 bins x 4000, 4 Msps), `reps` each after a warm-up.
+    python scripts/acq_probe.py [reps]"""
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np  # noqa: E402
+
+from gnss_sim_receiver_amd import codes as C, engine, signals as S  # noqa: E402
+
+
+def sweep(ctx, fs, n, sig, reps):
+    acq = engine.PcpsAcquisition(ctx, fs, n, 5000, 250, 0, True, max_prns=32)
+    for k in range(32):
+        acq.set_local_code(C.gps_l1_ca_code_gen_complex_sampled(k + 1, fs), k)
+    dev = ctx.upload(np.ascontiguousarray(sig[:n]))
+    res, _ = acq.run(dev, n_prns=32)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        res, _ = acq.run(dev, n_prns=32)
+    dt = (time.perf_counter() - t0) / reps
+    acq.close()
+    dev.free()
+    return dt, res
+
+
+def main():
+    reps = int(sys.argv[1]) if len(sys.argv) > 1 else 20
+    ctx = engine.Context(0)
+    c3 = S.c3_sky()
+    dt3, r3 = sweep(ctx, 25000000, 25000, S.generate_if(25000000, 25000, c3, seed=0x6E550003), reps)
+    sky = S.random_sky(32, seed=0x6E550002)
+    dt1, r1 = sweep(ctx, 4000000, 4000, S.generate_if(4000000, 4000, sky, seed=0x6E550002), reps)
+    present = sorted(s.prn for s in c3)
+    top = sorted(range(32), key=lambda k: -r3[k].test_statistic)[:10]
+    print(f"C3 sweep {dt3 * 1e3:.3f} ms, C1-shape sweep {dt1 * 1e3:.3f} ms; C3 top-10 = present: {sorted(k + 1 for k in top) == present}")
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()
