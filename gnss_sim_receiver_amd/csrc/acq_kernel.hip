@@ -287,11 +287,19 @@ __device__ __forceinline__ void wave_pass(float2* __restrict__ buf, int M, int N
 // The same passes with the row length known at compile time (MC > 0): radices first_radix(M / Ns)
 // in order, every index split j / Ns, j % Ns and twiddle stride a constant (the runtime form spends
 // more VALU on integer division than on the butterflies).
+// Radix order of the compile-time rows: odd radices first.  The first Stockham pass (Ns = 1) writes
+// butterfly j's outputs at R·j…R·j+R−1, a lane stride of 8R bytes: 16-way LDS bank conflicts for
+// R = 8 (64 B), 2-way for R = 5 (40 B); the radix-8 pass goes last, where its writes are contiguous.
+constexpr int ct_radix(int m)
+{
+    return (m % 5 == 0) ? 5 : (m % 3 == 0) ? 3 : (m % 8 == 0) ? 8 : (m % 4 == 0) ? 4 : 2;
+}
+
 template <int MC, int NsC, int SIGN>
 __device__ __forceinline__ void wave_fft_row_ct(float2* __restrict__ buf, const float2* __restrict__ tw, int lane)
 {
     if constexpr (NsC < MC) {
-        constexpr int R = first_radix(MC / NsC);
+        constexpr int R = ct_radix(MC / NsC);
         constexpr int nb = MC / R;
         constexpr int tstep = MC / (NsC * R);
         constexpr int MAXB = (nb + 63) / 64;
@@ -741,7 +749,7 @@ __global__ __launch_bounds__(kAcqThreads) void acq_search_big_kernel(const float
     // |Y|² is parked in LDS (N floats ≤ the kWaveRows·M complex of the row buffer, P ≤ 32) for the
     // second-peak scan; all row-pass reads of LDS finished at the last round's barrier.
     float* mag = reinterpret_cast<float*>(lds);
-    MaxIdx m{-1.0f, 0x7fffffff};
+    MaxIdx m{-1.0f, 0x7fffffff}, m2t{-1.0f, 0x7fffffff};
     float s = 0.0f;
     if (t < M) {
         dft_reg_inplace<P, +1>(v, tw, N);  // y[t + M·q] in v[reg_slot<P>(q)]
@@ -769,22 +777,40 @@ __global__ __launch_bounds__(kAcqThreads) void acq_search_big_kernel(const float
             const int i = t + M * q - rs.row_off;  // index in the row
             if (i >= 0 && i < rs.row_len) {
                 mag[i] = g[q];
-                m = better(m, MaxIdx{g[q], i});
+                const MaxIdx x{g[q], i};
+                if (x.v > m.v || (x.v == m.v && x.i < m.i)) {  // the thread's top two, in better() order
+                    m2t = m;
+                    m = x;
+                } else {
+                    m2t = better(m2t, x);
+                }
                 s += g[q];
             }
         }
     }
     GNSSHIP_ACQ_STAMP(7);
+    const MaxIdx m1t = m;  // this thread's best, before the block reduction
     block_argmax_sum(m, s, red_m, red_s);
     const MaxIdx best = m;
     const float sum = s;
     GNSSHIP_ACQ_STAMP(8);
     int e1 = best.i - rs.spc, e2 = best.i + rs.spc;
     if (e1 < 0) e1 += rs.win_mod; else if (e2 >= rs.win_mod) e2 -= rs.win_mod;
+    // Second peak outside the window (first_vs_second_peak_statistic :566-593): only its value is
+    // kept, i.e. max(0, the largest |y|² outside the window).  The window spans 2·spc < M
+    // consecutive indices, so it holds at most one of a thread's indices unless it wraps: the
+    // thread's best outside it is its first or second value, and a thread with both inside rescans.
+    auto in_win = [&](int i) { return (e1 < e2) ? (i >= e1 && i < e2) : (i >= e1 || i < e2); };
     MaxIdx m2{0.0f, 0x7fffffff};
-    for (int i = t; i < rs.row_len; i += kAcqThreads) {
-        const bool in_win = (e1 < e2) ? (i >= e1 && i < e2) : (i >= e1 || i < e2);
-        m2 = better(m2, MaxIdx{in_win ? 0.0f : mag[i], i});
+    if (m1t.i != 0x7fffffff && !in_win(m1t.i)) {
+        m2 = better(m2, m1t);
+    } else if (m2t.i != 0x7fffffff && !in_win(m2t.i)) {
+        m2 = better(m2, m2t);
+    } else if (m1t.i != 0x7fffffff) {
+        for (int q = 0; q < P; q++) {  // this thread's indices (natural t + M·q, row-shifted)
+            const int i = t + M * q - rs.row_off;
+            if (i >= 0 && i < rs.row_len && !in_win(i)) m2 = better(m2, MaxIdx{mag[i], i});
+        }
     }
     const MaxIdx second = block_argmax(m2, red_m);
     GNSSHIP_ACQ_STAMP(9);

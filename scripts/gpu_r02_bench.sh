@@ -16,4 +16,7 @@ for grp in FETCH_SIZE WRITE_SIZE SQ_INSTS_VALU; do
 done
 cd $R && python3 scripts/pmc_traffic.py $O/pmc trk_persist_kernel > $O/pmc_trk.json && cat $O/pmc_trk.json
 find $O/prof -name "*kernel_stats.csv" | head -3
+
+# acquisition kernels (C3 + C1 shape): kernel stats and PMC
+bash $R/scripts/gpu_acq_pmc.sh acq || { echo "acq pmc failed"; exit 1; }
 echo "all ok"
