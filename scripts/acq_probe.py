@@ -35,7 +35,8 @@ def main():
     dt1, r1 = sweep(ctx, 4000000, 4000, S.generate_if(4000000, 4000, sky, seed=0x6E550002), reps)
     present = sorted(s.prn for s in c3)
     top = sorted(range(32), key=lambda k: -r3[k].test_statistic)[:10]
-    print(f"C3 sweep {dt3 * 1e3:.3f} ms, C1-shape sweep {dt1 * 1e3:.3f} ms; C3 top-10 = present: {sorted(k + 1 for k in top) == present}")
+    hits = len(set(k + 1 for k in top) & set(present))  # a sanity count only: parity is tests/test_gpu_acq.py
+    print(f"C3 sweep {dt3 * 1e3:.3f} ms, C1-shape sweep {dt1 * 1e3:.3f} ms; present PRNs among the 10 largest C3 statistics: {hits}/10")
     ctx.close()
 
 
