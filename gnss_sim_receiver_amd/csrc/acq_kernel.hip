@@ -210,11 +210,12 @@ __global__ __launch_bounds__(kAcqThreads) void acq_fft_rows_kernel(const void* _
 
 // ---------------------------------------------------------------------------------------------
 // Large transforms (kMaxAcqN < N ≤ 32768, e.g. the 25000-point transform of a 1 ms GPS code at
-// 25 Msps): four-step with one workgroup per transform, N = P·M, M ≤ 1024 rows of the LDS stage and
-// P ≤ 32 points per thread in registers.  Thread t owns column t: x[t + M·q], q < P.
+// 25 Msps): four-step, N = P·M, M ≤ 1024 rows of the LDS stage and P ≤ 32 points per thread in
+// registers.  Thread t owns column t: x[t + M·q], q < P.
 //   forward:  X[kq + P·k] = Σ_t W_M^{t·k} · W_N^{t·kq} · Σ_q x[t + M·q] W_P^{q·kq}
-//             (register P-point DFT, twiddle, then M-point row DFTs in LDS: 16 rows per round,
-//             one per wave, each wave running its row's passes with no workgroup barrier);
+//             (register P-point DFT and twiddle in one launch, then the M-point row DFTs in place
+//             in a second, one wave per row, each wave running its row's passes in LDS with no
+//             workgroup barrier);
 //             stored row-major TRANSPOSED: XT[kq·M + k] = X[kq + P·k].
 //   inverse:  y[t + M·q] = Σ_kq W_P^{−q·kq} · W_N^{−t·kq} · Σ_k Z[kq + P·k] W_M^{−t·k}
 //             reads Z in the same transposed layout (rows first, registers last) and so returns
@@ -473,58 +474,62 @@ __device__ __forceinline__ void dft_reg_inplace(float2* x, const float2* __restr
     }
 }
 
-// rowsT[b] = transposed FFT(sig ⊙ mult[b]); conj_out for the code spectrum.
-template <int FMT, int P, int MC = 0>
-__global__ __launch_bounds__(kAcqThreads) void acq_fft_big_kernel(const void* __restrict__ sig, const float2* __restrict__ mult,
-    FftPlan row_plan, const float2* __restrict__ tw, float2* __restrict__ rowsT, int conj_out, int n_valid)
+// rowsT[b] = transposed FFT(sig ⊙ mult[b]) in two launches over the whole chip (one workgroup per
+// transform would occupy n_bins CUs): the column stage writes each column's register P-point DFT,
+// twiddled by W_N^{t·kq}, to row kq of the output, then the row stage transforms every row in
+// place, one wave per row.  The same operations in the same order as the one-workgroup-per-transform
+// form this replaces (and as the inverse in acq_search_big_kernel, mirrored).
+constexpr int kBigColThreads = 64;
+constexpr int kBigRowWaves = 4;
+
+template <int FMT, int P>
+__global__ __launch_bounds__(kBigColThreads) void acq_fft_big_cols_kernel(const void* __restrict__ sig, const float2* __restrict__ mult, int M,
+    const float2* __restrict__ tw, float2* __restrict__ rowsT, int n_valid)
+{
+    const int N = P * M;
+    const int t = blockIdx.x * kBigColThreads + threadIdx.x;
+    const int b = blockIdx.y;
+    if (t >= M) return;
+    const float2* m = mult ? mult + static_cast<int64_t>(b) * N : nullptr;
+    float2 v[P];
+#pragma unroll
+    for (int q = 0; q < P; q++) {
+        float2 x = (t + M * q < n_valid) ? load_if<FMT>(sig, t + M * q) : make_float2(0.0f, 0.0f);
+        if (m) x = cmulf(x, m[t + M * q]);  // volk_32fc_x2_multiply_32fc(in, wipeoff)
+        v[q] = x;
+    }
+    dft_reg_inplace<P, -1>(v, tw, N);  // X[kq] in v[reg_slot<P>(kq)]
+    float2* out = rowsT + static_cast<int64_t>(b) * N;
+#pragma unroll
+    for (int kq = 0; kq < P; kq++) {
+        const float2 xk = v[reg_slot<P>(kq)];
+        out[kq * M + t] = kq ? cmulf(xk, tw[t * kq]) : xk;  // W_N^{t·kq}, t·kq < N
+    }
+}
+
+// grid: ceil(n_bins·P / kBigRowWaves); row r = b·P + kq of rowsT, transformed in place.
+template <int MC>
+__global__ __launch_bounds__(kBigRowWaves * 64) void acq_fft_big_rows_kernel(FftPlan row_plan, int P, const float2* __restrict__ tw,
+    float2* __restrict__ rowsT, int n_rows_total, int conj_out)
 {
     extern __shared__ __attribute__((aligned(16))) float2 lds[];
     const int M = row_plan.n;
-    const int N = P * M;
-    const int t = threadIdx.x;
-    const int b = blockIdx.x;
-    const float2* m = mult ? mult + static_cast<int64_t>(b) * N : nullptr;
-    float2 v[P];
-    if (t < M) {
-#pragma unroll
-        for (int q = 0; q < P; q++) {
-            float2 x = (t + M * q < n_valid) ? load_if<FMT>(sig, t + M * q) : make_float2(0.0f, 0.0f);
-            if (m) x = cmulf(x, m[t + M * q]);  // volk_32fc_x2_multiply_32fc(in, wipeoff)
-            v[q] = x;
-        }
-        dft_reg_inplace<P, -1>(v, tw, N);  // X[kq] in v[reg_slot<P>(kq)]
-    }
-    float2* out = rowsT + static_cast<int64_t>(b) * N;
-    float2* rtw = lds + kWaveRows * M;  // row twiddles exp(−2πi m/M) = tw[m·P], m < M
-    for (int i = t; i < M; i += kAcqThreads) rtw[i] = tw[i * P];
-    const int lane = t & 63, wave = t >> 6;
-#pragma unroll
-    for (int r0 = 0; r0 < P; r0 += kWaveRows) {
-        const int nrows = (P - r0) < kWaveRows ? (P - r0) : kWaveRows;
-        if (t < M) {
-#pragma unroll
-            for (int kk = 0; kk < kWaveRows; kk++) {
-                const int kq = r0 + kk;
-                if (kq < P) {
-                    const float2 xk = v[reg_slot<P>(kq)];
-                    lds[kk * M + t] = kq ? cmulf(xk, tw[t * kq]) : xk;  // W_N^{t·kq}, t·kq < N
-                }
-            }
-        }
-        __syncthreads();
-        if (wave < nrows) {
-            int lane_r = lane;
-            asm volatile("" : "+v"(lane_r));
-            if constexpr (MC > 0) wave_fft_row_ct<MC, 1, -1>(lds + wave * M, rtw, lane_r);
-            else wave_fft_row<-1>(lds + wave * M, row_plan, rtw, lane);
-        }
-        __syncthreads();
-        for (int i = t; i < nrows * M; i += kAcqThreads) {
-            float2 y = lds[i];
-            if (conj_out) y.y = -y.y;
-            out[r0 * M + i] = y;
-        }
-        __syncthreads();
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    float2* rtw = lds + kBigRowWaves * M;  // row twiddles exp(−2πi m/M) = tw[m·P], m < M
+    for (int i = threadIdx.x; i < M; i += kBigRowWaves * 64) rtw[i] = tw[i * P];
+    const int r = blockIdx.x * kBigRowWaves + wave;
+    float2* row = lds + wave * M;
+    float2* g = rowsT + static_cast<int64_t>(r) * M;  // rows are contiguous: b·N + kq·M = (b·P + kq)·M
+    if (r < n_rows_total)
+        for (int i = lane; i < M; i += 64) row[i] = g[i];
+    __syncthreads();
+    if (r >= n_rows_total) return;
+    if constexpr (MC > 0) wave_fft_row_ct<MC, 1, -1>(row, rtw, lane);
+    else wave_fft_row<-1>(row, row_plan, rtw, lane);
+    for (int i = lane; i < M; i += 64) {
+        float2 y = row[i];
+        if (conj_out) y.y = -y.y;
+        g[i] = y;
     }
 }
 
@@ -680,14 +685,18 @@ __global__ __launch_bounds__(kAcqThreads) void acq_search_kernel(const float2* _
 // Large-N search: Y = IFFT(XT_b ⊙ CT_p) by the transposed four-step (rows in LDS, then the
 // register P-point stage), |Y|² and the same row statistics as acq_search_kernel.  Thread t holds
 // y[t + M·q] for q < P, i.e. the natural index n = t + M·q.
-template <int P, int MC = 0>
-__global__ __launch_bounds__(kAcqThreads) void acq_search_big_kernel(const float2* __restrict__ XT, const float2* __restrict__ codesT,
-    FftPlan row_plan, const float2* __restrict__ tw, int n_bins, RowSpec rs, int accumulate, RowStat* __restrict__ rowstat,
-    float* __restrict__ grid_out)
+// NT threads per workgroup (NT ≥ M; NT/64 rows per round).  (A 40 × 625 layout of the C3 transform
+// in 640 threads, two workgroups per CU, needs ≤ 96 VGPRs and spills: 0.50 ms per C3 sweep; at one
+// workgroup per CU it ties 25 × 1000.)
+template <int P, int MC = 0, int NT = kAcqThreads>
+__global__ __launch_bounds__(NT) void acq_search_big_kernel(const float2* __restrict__ XT,
+    const float2* __restrict__ codesT, FftPlan row_plan, const float2* __restrict__ tw, int n_bins, RowSpec rs, int accumulate,
+    RowStat* __restrict__ rowstat, float* __restrict__ grid_out)
 {
+    constexpr int kRoundRows = NT / 64;  // rows transformed per round (one per wave)
     extern __shared__ __attribute__((aligned(16))) float2 lds[];
-    __shared__ MaxIdx red_m[kAcqThreads / 64];
-    __shared__ float red_s[kAcqThreads / 64];
+    __shared__ MaxIdx red_m[NT / 64];
+    __shared__ float red_s[NT / 64];
     const int b = blockIdx.x, p = blockIdx.y;
     const int M = row_plan.n;
     const int N = P * M;
@@ -695,26 +704,26 @@ __global__ __launch_bounds__(kAcqThreads) void acq_search_big_kernel(const float
     const float2* x = XT + static_cast<int64_t>(b) * N;
     const float2* c = codesT + static_cast<int64_t>(p) * N;
     float2 v[P];
-    float2* rtw = lds + kWaveRows * M;  // row twiddles exp(−2πi m/M) = tw[m·P], m < M
-    for (int i = t; i < M; i += kAcqThreads) rtw[i] = tw[i * P];
+    float2* rtw = lds + kRoundRows * M;  // row twiddles exp(−2πi m/M) = tw[m·P], m < M
+    for (int i = t; i < M; i += NT) rtw[i] = tw[i * P];
     constexpr int kB = MC > 0 ? col_split(MC) : 1;
     float2* ct_lo = rtw + M;                      // tw[e], e < B·P        (MC > 0)
     float2* ct_hi = ct_lo + kB * P;               // tw[B·e], e < (M/B)·P  (MC > 0)
     if constexpr (MC > 0) {
-        for (int i = t; i < kB * P; i += kAcqThreads) ct_lo[i] = tw[i];
-        for (int i = t; i < (MC / kB) * P; i += kAcqThreads) ct_hi[i] = tw[kB * i];
+        for (int i = t; i < kB * P; i += NT) ct_lo[i] = tw[i];
+        for (int i = t; i < (MC / kB) * P; i += NT) ct_hi[i] = tw[kB * i];
     }
     const int lane = t & 63, wave = t >> 6;
     // the short round first: the v[kq] of finished rounds stay live in registers through the later
     // rounds' row passes, so the fewer of them the better (P = 25: 9 rows, then 16)
-    constexpr int kFirst = P - kWaveRows * ((P - 1) / kWaveRows);
-    constexpr int kRounds = 1 + (P - kFirst) / kWaveRows;
+    constexpr int kFirst = P - kRoundRows * ((P - 1) / kRoundRows);
+    constexpr int kRounds = 1 + (P - kFirst) / kRoundRows;
     GNSSHIP_ACQ_STAMP(0);
 #pragma unroll
     for (int rr = 0; rr < kRounds; rr++) {  // constant trip count: unrolled, v[] indices compile-time
-        const int r0 = rr == 0 ? 0 : kFirst + (rr - 1) * kWaveRows;
-        const int nrows = rr == 0 ? kFirst : kWaveRows;
-        for (int i = t; i < nrows * M; i += kAcqThreads) lds[i] = cmulf(x[r0 * M + i], c[r0 * M + i]);  // ×conj(code FFT)
+        const int r0 = rr == 0 ? 0 : kFirst + (rr - 1) * kRoundRows;
+        const int nrows = rr == 0 ? kFirst : kRoundRows;
+        for (int i = t; i < nrows * M; i += NT) lds[i] = cmulf(x[r0 * M + i], c[r0 * M + i]);  // ×conj(code FFT)
         __syncthreads();
         GNSSHIP_ACQ_STAMP(r0 == 0 ? 1 : 4);
         if (wave < nrows) {
@@ -729,7 +738,7 @@ __global__ __launch_bounds__(kAcqThreads) void acq_search_big_kernel(const float
         GNSSHIP_ACQ_STAMP(r0 == 0 ? 2 : 5);
         if (t < M) {
 #pragma unroll
-            for (int kk = 0; kk < kWaveRows; kk++) {
+            for (int kk = 0; kk < kRoundRows; kk++) {
                 const int kq = r0 + kk;
                 if (kk < nrows) {
                     float2 w;
@@ -746,16 +755,14 @@ __global__ __launch_bounds__(kAcqThreads) void acq_search_big_kernel(const float
         __syncthreads();
         GNSSHIP_ACQ_STAMP(r0 == 0 ? 3 : 6);
     }
-    // |Y|² is parked in LDS (N floats ≤ the kWaveRows·M complex of the row buffer, P ≤ 32) for the
-    // second-peak scan; all row-pass reads of LDS finished at the last round's barrier.
-    float* mag = reinterpret_cast<float*>(lds);
+    // |y|² stays in registers (g[], the thread's own P points) for the rare second-peak rescan below.
     MaxIdx m{-1.0f, 0x7fffffff}, m2t{-1.0f, 0x7fffffff};
     float s = 0.0f;
+    float g[P];
     if (t < M) {
         dft_reg_inplace<P, +1>(v, tw, N);  // y[t + M·q] in v[reg_slot<P>(q)]
         // |y|² first (the complex points die as their magnitudes appear), then the optional grid
         // row and the row statistics in separate branch-light loops
-        float g[P];
 #pragma unroll
         for (int q = 0; q < P; q++) {
             const float2 y = v[reg_slot<P>(q)];
@@ -776,7 +783,6 @@ __global__ __launch_bounds__(kAcqThreads) void acq_search_big_kernel(const float
         for (int q = 0; q < P; q++) {
             const int i = t + M * q - rs.row_off;  // index in the row
             if (i >= 0 && i < rs.row_len) {
-                mag[i] = g[q];
                 const MaxIdx x{g[q], i};
                 if (x.v > m.v || (x.v == m.v && x.i < m.i)) {  // the thread's top two, in better() order
                     m2t = m;
@@ -807,9 +813,10 @@ __global__ __launch_bounds__(kAcqThreads) void acq_search_big_kernel(const float
     } else if (m2t.i != 0x7fffffff && !in_win(m2t.i)) {
         m2 = better(m2, m2t);
     } else if (m1t.i != 0x7fffffff) {
+#pragma unroll
         for (int q = 0; q < P; q++) {  // this thread's indices (natural t + M·q, row-shifted)
             const int i = t + M * q - rs.row_off;
-            if (i >= 0 && i < rs.row_len && !in_win(i)) m2 = better(m2, MaxIdx{mag[i], i});
+            if (i >= 0 && i < rs.row_len && !in_win(i)) m2 = better(m2, MaxIdx{g[q], i});
         }
     }
     const MaxIdx second = block_argmax(m2, red_m);
@@ -1119,24 +1126,20 @@ bool big_p_supported(int P)
 hipError_t launch_acq_fft_big(const void* sig, int fmt, const float2* mult, int n_rows, int P, const FftPlan& row_plan, const float2* tw,
     float2* rowsT, int conj_out, int n_valid, hipStream_t stream)
 {
-    const size_t lds = (static_cast<size_t>(kWaveRows) + 1) * sizeof(float2) * row_plan.n;
-    if (row_plan.n > kAcqThreads) return hipErrorInvalidValue;
-    if (P == 25 && row_plan.n == 1000 && fmt == GNSSHIP_FMT_CF32) {  // C3: N = 25000 (GPS 1 ms at 25 Msps)
-        hipLaunchKernelGGL((acq_fft_big_kernel<GNSSHIP_FMT_CF32, 25, 1000>), dim3(n_rows), dim3(kAcqThreads), lds, stream, sig, mult, row_plan, tw,
-            rowsT, conj_out, n_valid);
-        return hipGetLastError();
-    }
+    const int M = row_plan.n;
+    if (M > kAcqThreads) return hipErrorInvalidValue;
+    const dim3 cgrid((M + kBigColThreads - 1) / kBigColThreads, n_rows);
 #define GNSSHIP_P_CASE(p)                                                                                                            \
     case p:                                                                                                                          \
         if (fmt == GNSSHIP_FMT_CF32)                                                                                                 \
-            hipLaunchKernelGGL((acq_fft_big_kernel<GNSSHIP_FMT_CF32, p>), dim3(n_rows), dim3(kAcqThreads), lds, stream, sig, mult,   \
-                row_plan, tw, rowsT, conj_out, n_valid);                                                                                      \
+            hipLaunchKernelGGL((acq_fft_big_cols_kernel<GNSSHIP_FMT_CF32, p>), cgrid, dim3(kBigColThreads), 0, stream, sig, mult, M, tw, \
+                rowsT, n_valid);                                                                                                     \
         else if (fmt == GNSSHIP_FMT_CI16)                                                                                            \
-            hipLaunchKernelGGL((acq_fft_big_kernel<GNSSHIP_FMT_CI16, p>), dim3(n_rows), dim3(kAcqThreads), lds, stream, sig, mult,   \
-                row_plan, tw, rowsT, conj_out, n_valid);                                                                                      \
+            hipLaunchKernelGGL((acq_fft_big_cols_kernel<GNSSHIP_FMT_CI16, p>), cgrid, dim3(kBigColThreads), 0, stream, sig, mult, M, tw, \
+                rowsT, n_valid);                                                                                                     \
         else if (fmt == GNSSHIP_FMT_CI8)                                                                                             \
-            hipLaunchKernelGGL((acq_fft_big_kernel<GNSSHIP_FMT_CI8, p>), dim3(n_rows), dim3(kAcqThreads), lds, stream, sig, mult,    \
-                row_plan, tw, rowsT, conj_out, n_valid);                                                                                      \
+            hipLaunchKernelGGL((acq_fft_big_cols_kernel<GNSSHIP_FMT_CI8, p>), cgrid, dim3(kBigColThreads), 0, stream, sig, mult, M, tw,  \
+                rowsT, n_valid);                                                                                                     \
         else                                                                                                                         \
             return hipErrorInvalidValue;                                                                                             \
         break;
@@ -1145,6 +1148,13 @@ hipError_t launch_acq_fft_big(const void* sig, int fmt, const float2* mult, int 
     default: return hipErrorInvalidValue;
     }
 #undef GNSSHIP_P_CASE
+    const int rows_total = n_rows * P;
+    const size_t lds = (static_cast<size_t>(kBigRowWaves) + 1) * sizeof(float2) * M;
+    const dim3 rgrid((rows_total + kBigRowWaves - 1) / kBigRowWaves);
+    if (M == 1000)  // C3: N = 25000 (GPS 1 ms at 25 Msps), compile-time row plan
+        hipLaunchKernelGGL((acq_fft_big_rows_kernel<1000>), rgrid, dim3(kBigRowWaves * 64), lds, stream, row_plan, P, tw, rowsT, rows_total, conj_out);
+    else
+        hipLaunchKernelGGL((acq_fft_big_rows_kernel<0>), rgrid, dim3(kBigRowWaves * 64), lds, stream, row_plan, P, tw, rowsT, rows_total, conj_out);
     return hipGetLastError();
 }
 
