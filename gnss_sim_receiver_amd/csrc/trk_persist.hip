@@ -35,11 +35,12 @@
 
 // Epoch phase timestamps for the profiling build only (make prof → scripts/libgnsship_prof.so,
 // scripts/trk_wg_profile.py): slot [(channel·kProfEpochs + epoch)·16 + k] = wall_clock64() at phase
-// k (0-7 in the kernel, 8-15 inside the loop update, trk_loop.h GNSSHIP_TRK_LOOP_STAMP).
+// k (0-6 and 16-21 in the kernel, 8-12 inside the loop update — trk_loop.h GNSSHIP_TRK_LOOP_STAMP —
+// 13-15 inside the AVX replay; slot 7 holds the replay's shader cycles).
 #ifdef GNSSHIP_CORR_PROFILE
 namespace gnsship {
 constexpr int kProfEpochs = 64;
-constexpr int kProfSlots = 16;
+constexpr int kProfSlots = 32;
 __device__ unsigned long long* g_trk_prof = nullptr;
 __shared__ int g_prof_epoch;
 __device__ __forceinline__ void trk_prof_stamp(int e, int k)
@@ -99,7 +100,15 @@ __device__ __forceinline__ f2 normalise_avx(f2 z)
     return f2{__fdiv_rn(z.x, m), __fdiv_rn(z.y, m)};
 }
 
-__device__ __forceinline__ void publish(int32_t* p, int v) { __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP); }
+// The publishing wave's LDS operations complete in program order, so a counter stored after the
+// data it announces lands after it: a relaxed store behind a wavefront-scope fence (which only
+// keeps the compiler from reordering) needs no wait for the data store, and a reader that acquires
+// the counter then sees the data.
+__device__ __forceinline__ void publish(int32_t* p, int v)
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
 
 __device__ __forceinline__ void wait_published(int32_t* p, int need)
 {
@@ -146,10 +155,14 @@ __device__ void replay_generic(const DevJob& job, Anchor* A, int nblk, int32_t* 
 // AVX (lanes 0..15 = phasor l): Z[t·16 + l] = the phasor lane l starts task t with; T[j] = the
 // tail phasor of sample 16M + j.  The initial phasors are the generic chain phase·inc^l (:204-208);
 // dz = normalise(inc^16) (:215-225); after iteration m's update, renormalise when m ≡ 0 mod 64.
-// A task's G steps run without a branch (16 at a time); each task's start is published for the
-// correlating waves.
-__device__ void replay_avx(const PEpoch& ep, f2* Z, f2* T, int N, int G, int lane, int32_t* published)
+// Whole renormalisation periods (iterations 64s+1 … 64(s+1), tasks 1 + P·s … P·(s+1) for P = 64/G)
+// run as one unrolled block each — G steps, store and publish the next task's start, per task; the
+// renormalisation after the block — with no per-task bookkeeping on the chain; the < 64 iterations
+// after the last whole period hold no renormalisation.
+template <int G>
+__device__ void replay_avx(const PEpoch& ep, f2* Z, f2* T, int N, int lane, int32_t* published)
 {
+    constexpr int kPer = kAvxSeg / G;
     const int M = N / kAvxLanes, S = avx_tasks(M, G);
     const f2 inc = f2{ep.job.inc_re, ep.job.inc_im};
     const f2 dz = f2{ep.dz_re, ep.dz_im};
@@ -158,37 +171,57 @@ __device__ void replay_avx(const PEpoch& ep, f2* Z, f2* T, int N, int G, int lan
         if (i < lane) z = cmul_exact(z, inc);
     Z[lane] = z;
     if (lane == 0) publish(published, 1);
-    if (M > 0) {  // iteration 0, renormalised after its update
+    if (M > 0) {  // iteration 0 (task 0), renormalised after its update
         z = normalise_avx(cmul_exact(z, dz));
         if (S > 1) {
             Z[kAvxLanes + lane] = z;
             if (lane == 0) publish(published, 2);
         }
     }
-    // task t+1's start is stored right after task t and published one task later, when its LDS
-    // write has long landed (the release then costs no wait on the chain)
-    for (int t = 1; t < S; t++) {
-        const int m_lo = G * (t - 1) + 1, m_hi = min(G * t, M - 1);  // task t's iterations
-        const int cnt = m_hi - m_lo + 1;
-        if (t >= 2 && lane == 0) publish(published, t + 1);
-        if (cnt == G) {
-            for (int q = 0; q < G; q += 16) {
+    if (lane == 0) GNSSHIP_TRK_LOOP_STAMP(13);
+#ifdef GNSSHIP_CORR_PROFILE
+    const long long c13 = clock64();  // shader cycles of the task loop → slot 7 (not a timestamp)
+#endif
+    const int n_per = M > 0 ? (M - 1) / kAvxSeg : 0;
+    for (int sg = 0; sg < n_per; sg++) {
 #pragma unroll
-                for (int u = 0; u < 16; u++) z = cmul_exact(z, dz);
+        for (int u = 0; u < kPer; u++) {
+#pragma unroll
+            for (int i = 0; i < G; i++) z = cmul_exact(z, dz);
+            if (u == kPer - 1) z = normalise_avx(z);
+            const int t = 1 + kPer * sg + u;  // the task just run
+            if (t + 1 < S) {
+                Z[(t + 1) * kAvxLanes + lane] = z;
+                if (lane == 0) publish(published, t + 2);
             }
-        } else {
-            for (int u = 0; u < cnt; u++) z = cmul_exact(z, dz);
         }
-        if (m_hi % kAvxSeg == 0) z = normalise_avx(z);
-        if (t + 1 < S) Z[(t + 1) * kAvxLanes + lane] = z;
+    }
+    for (int t = 1 + kPer * n_per; t < S; t++) {
+        const int cnt = min(G * t, M - 1) - G * (t - 1);
+        if (cnt == G) {
+#pragma unroll
+            for (int i = 0; i < G; i++) z = cmul_exact(z, dz);
+        } else {
+            for (int i = 0; i < cnt; i++) z = cmul_exact(z, dz);
+        }
+        if (t + 1 < S) {
+            Z[(t + 1) * kAvxLanes + lane] = z;
+            if (lane == 0) publish(published, t + 2);
+        }
     }
     if (lane == 0) {  // z0 = normalise(z0) after the loop, then the serial tail (:286-304)
+        GNSSHIP_TRK_LOOP_STAMP(14);
+#ifdef GNSSHIP_CORR_PROFILE
+        if (g_trk_prof && g_prof_epoch < kProfEpochs)
+            g_trk_prof[(static_cast<size_t>(blockIdx.x) * kProfEpochs + g_prof_epoch) * kProfSlots + 7] = static_cast<unsigned long long>(clock64() - c13);
+#endif
         f2 t = normalise_avx(z);
         for (int j = 0; j < N - kAvxLanes * M; j++) {
             T[j] = t;
             t = cmul_exact(t, inc);
         }
         publish(published, S + 1);
+        GNSSHIP_TRK_LOOP_STAMP(15);
     }
 }
 
@@ -462,7 +495,11 @@ __global__ __launch_bounds__(kPThreads, persist_waves_per_simd<THRU>()) void trk
 #pragma unroll
         for (int t = 0; t <= NT; t++) acc[t] = f2{0.0f, 0.0f};
         if constexpr (AVX) {
-            if (wave == 0 && lane < kAvxLanes) replay_avx(ep, Z, T, N, avx_g, lane, &ep.published);
+            if (wave == 0 && lane < kAvxLanes) {
+                if (avx_g == 16) replay_avx<16>(ep, Z, T, N, lane, &ep.published);
+                else if (avx_g == 32) replay_avx<32>(ep, Z, T, N, lane, &ep.published);
+                else replay_avx<64>(ep, Z, T, N, lane, &ep.published);
+            }
             if (tid == 0) GNSSHIP_TRK_STAMP(e, 2);
             if (ep.in_margin)
                 consume_avx<FMT, NT, DATA, true, THRU ? 4 : 16>(ep, Z, T, span, N, avx_g, c0, c1, L, lane, wave, acc);
@@ -481,7 +518,7 @@ __global__ __launch_bounds__(kPThreads, persist_waves_per_simd<THRU>()) void trk
 #pragma unroll
             for (int t = 0; t <= NT; t++) acc[t] = cmul_pk(acc[t], er, esw);
         }
-        if (lane == 0 && wave <= 1) GNSSHIP_TRK_STAMP(e, 3 + wave);
+        if (lane == 0) GNSSHIP_TRK_STAMP(e, wave <= 1 ? 3 + wave : 14 + wave);  // waves 2, 3: slots 16, 17
         constexpr int kOut = NT + (DATA ? 1 : 0);
 #pragma unroll
         for (int t = 0; t < kOut; t++) {
@@ -491,6 +528,7 @@ __global__ __launch_bounds__(kPThreads, persist_waves_per_simd<THRU>()) void trk
                 ep.red[wave][2 * t + 1] = si;
             }
         }
+        if (lane == 0) GNSSHIP_TRK_STAMP(e, 18 + wave);  // wave sums stored: slots 18-21
         __syncthreads();
         // tap sums over the waves (each in the serial order w = 0..3), the data prompt at 2·kMaxTaps
         if (tid < 2 * kMaxTaps + 2) {

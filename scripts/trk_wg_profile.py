@@ -7,7 +7,9 @@ Stamps (wall_clock64, 100 MHz) per channel-epoch: 0 epoch start, 1 job derived (
 inside the loop update 8 before lock_status, 9 after it, 10 after run_dll_pll, 11 after
 update_tracking_vars, 12 after log_data (state 2 only).  `sync`: the satellites carry GPS
 navigation bits and the acquisition is stamped pull_in_time_s before the block, so the channels
-bit-synchronise and the profiled epochs run in state 4 (steady state)."""
+bit-synchronise and the profiled epochs run in state 4 (steady state), as in bench.py.
+Inside the AVX replay (wave 0, lane 0): 13 start phasors and iteration 0 done, 14 task loop done,
+15 tail published."""
 import ctypes
 import os
 import sys
@@ -19,6 +21,7 @@ import numpy as np  # noqa: E402
 from gnss_sim_receiver_amd import abi, engine, signals  # noqa: E402
 
 EP = 64
+SLOTS = 32
 
 
 def main():
@@ -30,38 +33,47 @@ def main():
     lib.gnsship_debug_trk_profile.argtypes = [ctypes.c_void_p]
     ctx = engine.Context(0)
     sats = signals.random_sky(32, seed=0x6E550002)
-    first = int(10 * fs) if state4 else 0  # acquisition stamped 10 s (pull_in_time_s) before the block
+    # sync: bench.py's steady state — GPS navigation bits (the preamble recurring every 260 ms),
+    # tracking from 11 s after the acquisition stamp (pull_in_time_s elapsed), 0.5 s of pre-roll
+    first = int(11 * fs) if state4 else 0
     if state4:
         for s in sats:
-            s.bits = "10001011" + "0110100111010010" * 8  # GPS preamble + filler bits (bit sync, state 4)
-    block = signals.generate_if(fs, int(fs * (0.4 if state4 else 0.1)) + 8000, sats, seed=1, start=first)
+            s.bits = "1000101100110"
+    pre = 500 if state4 else 4
+    block = signals.generate_if(fs, (pre + EP + 4) * vl, sats, seed=1, start=first - 2 * vl)
     trk = engine.DllPllVemlTracking(ctx, abi.TrkConf.defaults(abi.SYS_GPS_L1CA, fs, vl, rotator=rot), n_ch)
     for i, s in enumerate(sats):
         ctx.set_code(300 + i, s.code)
     for ch in range(n_ch):
         s = sats[ch % 32]
-        # Acq_delay_samples of an acquisition stamped at sample 0 (the code start after `first`, with code Doppler)
-        m = np.ceil(s.chip_phase(np.float64(first), fs) / s.code_len)
-        n0 = (m * s.code_len + s.code_delay_chips) * fs / s.code_freq()
-        delay = first + np.mod(n0 - first, 1e-3 * fs)
-        trk.start(ch, 300 + ch % 32, delay, s.doppler_hz, 0, first)
+        trk.start(ch, 300 + ch % 32, signals.acq_delay_samples(s, fs, 0, first), s.doppler_hz, 0, first)
     dev = ctx.upload(block)
-    trk.run(dev, first, 300 if state4 else 4, n_buffer_samples=len(block), records=False)
-    prof = engine.DeviceBuffer(ctx, n_ch * EP * 16 * 8)
-    prof.upload(np.zeros(n_ch * EP * 16, np.uint64))
+    trk.run(dev, first - 2 * vl, pre, n_buffer_samples=len(block), records=False)
+    prof = engine.DeviceBuffer(ctx, n_ch * EP * SLOTS * 8)
+    prof.upload(np.zeros(n_ch * EP * SLOTS, np.uint64))
     lib.gnsship_debug_trk_profile(ctypes.c_void_p(prof.ptr))
-    trk.run(dev, first, EP, n_buffer_samples=len(block), records=False)
+    trk.run(dev, first - 2 * vl, EP, n_buffer_samples=len(block), records=False)
     ctx.sync()
     lib.gnsship_debug_trk_profile(ctypes.c_void_p(0))
     print("states:", sorted(set(trk.channel_state(ch)[0] for ch in range(n_ch))))
-    t = np.zeros(n_ch * EP * 16, np.uint64)
+    t = np.zeros(n_ch * EP * SLOTS, np.uint64)
     prof.download(t)
-    t = t.reshape(n_ch, EP, 16).astype(np.int64)
+    t = t.reshape(n_ch, EP, SLOTS).astype(np.int64)
     us = lambda v: v / 100.0  # noqa: E731
     names = ["derive", "->replay done", "->wave0 corr done", "->wave1 corr done", "->reduced", "->loop update",
              " update: to lock_status", " update: lock_status", " update: run_dll_pll", " update: tracking_vars",
-             " update: log_data (st2)", " update: sync+rest (st2)", " update: rest (st4)"]
-    refs = [(0, 1), (1, 2), (1, 3), (1, 4), (1, 5), (5, 6), (5, 8), (8, 9), (9, 10), (10, 11), (11, 12), (12, 6), (11, 6)]
+             " update: log_data (st2)", " update: sync+rest (st2)", " update: rest (st4)",
+             " replay: start phasors", " replay: task loop", " replay: tail + publish", "end -> next epoch",
+             "->wave2 corr done", "->wave3 corr done", "->wave0 sums stored", "->wave1 sums stored", "->wave2 sums stored",
+             "->wave3 sums stored"]
+    refs = [(0, 1), (1, 2), (1, 3), (1, 4), (1, 5), (5, 6), (5, 8), (8, 9), (9, 10), (10, 11), (11, 12), (12, 6), (11, 6),
+            (1, 13), (13, 14), (14, 15), (6, 32), (1, 16), (1, 17), (1, 18), (1, 19), (1, 20), (1, 21)]
+    cyc = t[:, 1:-1, 7]
+    loop_us = (t[:, 1:-1, 14] - t[:, 1:-1, 13]) / 100.0
+    if (cyc > 0).any():
+        print(f"replay task loop: {np.median(cyc):.0f} shader cycles, effective clock {np.median(cyc / loop_us) / 1e3:.2f} GHz")
+    nxt = np.concatenate([t[:, 1:, 0:1], np.zeros((n_ch, 1, 1), np.int64)], axis=1)
+    t = np.concatenate([t, nxt], axis=2)
     v = t[:, 1:-1, :]  # drop first/last epoch
     print(f"rotator {rot}, {n_ch} channels: epoch period {us(np.median(np.diff(t[:, :, 0], axis=1))):.2f} us (median)")
     for nm, (a, b) in zip(names, refs):
