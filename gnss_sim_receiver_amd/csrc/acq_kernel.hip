@@ -28,8 +28,15 @@ __device__ unsigned long long* g_acq_prof = nullptr;
     do { \
         if (g_acq_prof && threadIdx.x == 0) g_acq_prof[(static_cast<size_t>(blockIdx.y) * gridDim.x + blockIdx.x) * 16 + (k)] = wall_clock64(); \
     } while (0)
+#define GNSSHIP_ACQ_STAMP_LANE(k, tid) \
+    do { \
+        if (g_acq_prof && threadIdx.x == (tid)) g_acq_prof[(static_cast<size_t>(blockIdx.y) * gridDim.x + blockIdx.x) * 16 + (k)] = wall_clock64(); \
+    } while (0)
 #else
 #define GNSSHIP_ACQ_STAMP(k) \
+    do { \
+    } while (0)
+#define GNSSHIP_ACQ_STAMP_LANE(k, tid) \
     do { \
     } while (0)
 #endif
@@ -296,14 +303,41 @@ constexpr int ct_radix(int m)
     return (m % 5 == 0) ? 5 : (m % 3 == 0) ? 3 : (m % 8 == 0) ? 8 : (m % 4 == 0) ? 4 : 2;
 }
 
+// Twiddles of the compile-time rows, one table per pass laid out [r − 1][k] (k < Ns, 1 ≤ r < R):
+// consecutive lanes (consecutive k) read consecutive entries, where the single M-entry table read at
+// k·r·tstep put up to eight lanes of a wave on one LDS bank.  Same values (tw[k·r·tstep]), so the
+// transform is bit-identical.  ct_tw_count(M, Ns) = entries of the passes from Ns on (< M in total).
+constexpr int ct_tw_count(int m, int ns)
+{
+    return ns >= m ? 0 : (ns > 1 ? (ct_radix(m / ns) - 1) * ns : 0) + ct_tw_count(m, ns * ct_radix(m / ns));
+}
+
+// dst[pass table] = exp(−2πi·k·r·tstep/M) = tw[k·r·tstep·stride]  (tw: the N-entry table, stride = N/M)
+template <int MC, int NsC>
+__device__ __forceinline__ void fill_row_pass_tw(float2* __restrict__ dst, const float2* __restrict__ tw, int stride, int tid, int nt)
+{
+    if constexpr (NsC < MC) {
+        constexpr int R = ct_radix(MC / NsC);
+        constexpr int tstep = MC / (NsC * R);
+        if constexpr (NsC > 1) {
+            constexpr int off = ct_tw_count(MC, 1) - ct_tw_count(MC, NsC);
+            for (int i = tid; i < (R - 1) * NsC; i += nt) {
+                const int r = 1 + i / NsC, k = i % NsC;
+                dst[off + i] = tw[k * r * tstep * stride];
+            }
+        }
+        fill_row_pass_tw<MC, NsC * R>(dst, tw, stride, tid, nt);
+    }
+}
+
 template <int MC, int NsC, int SIGN>
 __device__ __forceinline__ void wave_fft_row_ct(float2* __restrict__ buf, const float2* __restrict__ tw, int lane)
 {
     if constexpr (NsC < MC) {
         constexpr int R = ct_radix(MC / NsC);
         constexpr int nb = MC / R;
-        constexpr int tstep = MC / (NsC * R);
         constexpr int MAXB = (nb + 63) / 64;
+        constexpr int off = ct_tw_count(MC, 1) - ct_tw_count(MC, NsC);
         float2 v[MAXB][R];
 #pragma unroll
         for (int c = 0; c < MAXB; c++) {
@@ -314,7 +348,7 @@ __device__ __forceinline__ void wave_fft_row_ct(float2* __restrict__ buf, const 
                 for (int r = 0; r < R; r++) {
                     float2 x = buf[j + r * nb];
                     if (r > 0 && NsC > 1) {
-                        float2 w = tw[k * r * tstep];
+                        float2 w = tw[off + (r - 1) * NsC + k];
                         if (SIGN > 0) w.y = -w.y;
                         x = cmulf(x, w);
                     }
@@ -515,8 +549,9 @@ __global__ __launch_bounds__(kBigRowWaves * 64) void acq_fft_big_rows_kernel(Fft
     extern __shared__ __attribute__((aligned(16))) float2 lds[];
     const int M = row_plan.n;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    float2* rtw = lds + kBigRowWaves * M;  // row twiddles exp(−2πi m/M) = tw[m·P], m < M
-    for (int i = threadIdx.x; i < M; i += kBigRowWaves * 64) rtw[i] = tw[i * P];
+    float2* rtw = lds + kBigRowWaves * M;  // row twiddles exp(−2πi m/M) = tw[m·P], m < M (per-pass tables for MC > 0)
+    if constexpr (MC > 0) fill_row_pass_tw<MC, 1>(rtw, tw, P, threadIdx.x, kBigRowWaves * 64);
+    else for (int i = threadIdx.x; i < M; i += kBigRowWaves * 64) rtw[i] = tw[i * P];
     const int r = blockIdx.x * kBigRowWaves + wave;
     float2* row = lds + wave * M;
     float2* g = rowsT + static_cast<int64_t>(r) * M;  // rows are contiguous: b·N + kq·M = (b·P + kq)·M
@@ -601,6 +636,29 @@ __device__ __forceinline__ float block_sum(float s, float* red)
     float r = 0.0f;
     for (int w = 0; w < static_cast<int>(blockDim.x >> 6); w++) r += red[w];
     __syncthreads();
+    return r;
+}
+
+__device__ __forceinline__ float wave_max_f(float s)
+{
+    s = fmaxf(s, dpp_f<0xB1>(s));
+    s = fmaxf(s, dpp_f<0x4E>(s));
+    s = fmaxf(s, dpp_f<0x141>(s));
+    s = fmaxf(s, dpp_f<0x140>(s));
+    s = fmaxf(s, __shfl_xor(s, 16, 64));
+    s = fmaxf(s, __shfl_xor(s, 32, 64));
+    return s;
+}
+
+// Block maximum of values (no index): the second peak keeps only its value.
+__device__ __forceinline__ float block_max(float s, float* red)
+{
+    s = wave_max_f(s);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (lane == 0) red[wave] = s;
+    __syncthreads();
+    float r = red[0];
+    for (int w = 1; w < static_cast<int>(blockDim.x >> 6); w++) r = fmaxf(r, red[w]);
     return r;
 }
 
@@ -705,25 +763,37 @@ __global__ __launch_bounds__(NT) void acq_search_big_kernel(const float2* __rest
     const float2* c = codesT + static_cast<int64_t>(p) * N;
     float2 v[P];
     float2* rtw = lds + kRoundRows * M;  // row twiddles exp(−2πi m/M) = tw[m·P], m < M
-    for (int i = t; i < M; i += NT) rtw[i] = tw[i * P];
+    if constexpr (MC > 0) fill_row_pass_tw<MC, 1>(rtw, tw, P, t, NT);  // per-pass tables (conflict-free reads)
+    else for (int i = t; i < M; i += NT) rtw[i] = tw[i * P];
+    // column twiddles W_N^{t·kq} = tw[B·a·kq]·tw[b·kq] (t = B·a + b), tables laid out [kq][a] and
+    // [kq][b] so that the lanes of a wave (consecutive t) read consecutive or equal entries
     constexpr int kB = MC > 0 ? col_split(MC) : 1;
-    float2* ct_lo = rtw + M;                      // tw[e], e < B·P        (MC > 0)
-    float2* ct_hi = ct_lo + kB * P;               // tw[B·e], e < (M/B)·P  (MC > 0)
+    constexpr int kA = MC > 0 ? MC / kB : 1;
+    float2* ct_lo = rtw + M;       // ct_lo[kq·B + b] = tw[b·kq]     (MC > 0)
+    float2* ct_hi = ct_lo + kB * P;  // ct_hi[kq·A + a] = tw[B·a·kq]  (MC > 0)
     if constexpr (MC > 0) {
-        for (int i = t; i < kB * P; i += NT) ct_lo[i] = tw[i];
-        for (int i = t; i < (MC / kB) * P; i += NT) ct_hi[i] = tw[kB * i];
+        for (int i = t; i < kB * P; i += NT) ct_lo[i] = tw[(i % kB) * (i / kB)];
+        for (int i = t; i < kA * P; i += NT) ct_hi[i] = tw[kB * (i % kA) * (i / kA)];
     }
     const int lane = t & 63, wave = t >> 6;
     // the short round first: the v[kq] of finished rounds stay live in registers through the later
     // rounds' row passes, so the fewer of them the better (P = 25: 9 rows, then 16)
     constexpr int kFirst = P - kRoundRows * ((P - 1) / kRoundRows);
     constexpr int kRounds = 1 + (P - kFirst) / kRoundRows;
+    // Two rounds with a short first one: the waves with no row in round 0 load rows kFirst..kRoundRows−1
+    // of round 1 into their own (free) slots meanwhile; round 1 then loads only rows kRoundRows..P−1,
+    // into slots 0..kFirst−1.  Slot kk of round 1 holds row kk (kk ≥ kFirst) or kk + kRoundRows.
+    constexpr bool kPrefetch = kRounds == 2 && kFirst < kRoundRows;
     GNSSHIP_ACQ_STAMP(0);
 #pragma unroll
     for (int rr = 0; rr < kRounds; rr++) {  // constant trip count: unrolled, v[] indices compile-time
         const int r0 = rr == 0 ? 0 : kFirst + (rr - 1) * kRoundRows;
         const int nrows = rr == 0 ? kFirst : kRoundRows;
-        for (int i = t; i < nrows * M; i += NT) lds[i] = cmulf(x[r0 * M + i], c[r0 * M + i]);  // ×conj(code FFT)
+        if (kPrefetch && rr == 1) {
+            for (int i = t; i < kFirst * M; i += NT) lds[i] = cmulf(x[kRoundRows * M + i], c[kRoundRows * M + i]);  // ×conj(code FFT)
+        } else {
+            for (int i = t; i < nrows * M; i += NT) lds[i] = cmulf(x[r0 * M + i], c[r0 * M + i]);
+        }
         __syncthreads();
         GNSSHIP_ACQ_STAMP(r0 == 0 ? 1 : 4);
         if (wave < nrows) {
@@ -733,17 +803,19 @@ __global__ __launch_bounds__(NT) void acq_search_big_kernel(const float2* __rest
             asm volatile("" : "+v"(lane_r));
             if constexpr (MC > 0) wave_fft_row_ct<MC, 1, +1>(lds + wave * M, rtw, lane_r);
             else wave_fft_row<+1>(lds + wave * M, row_plan, rtw, lane);
+        } else if (kPrefetch && rr == 0) {
+            for (int i = lane; i < M; i += 64) lds[wave * M + i] = cmulf(x[wave * M + i], c[wave * M + i]);
         }
         __syncthreads();
         GNSSHIP_ACQ_STAMP(r0 == 0 ? 2 : 5);
         if (t < M) {
 #pragma unroll
             for (int kk = 0; kk < kRoundRows; kk++) {
-                const int kq = r0 + kk;
+                const int kq = (kPrefetch && rr == 1) ? (kk < kFirst ? kk + kRoundRows : kk) : r0 + kk;
                 if (kk < nrows) {
                     float2 w;
                     if constexpr (MC > 0) {
-                        w = cmulf(ct_hi[(t / kB) * kq], ct_lo[(t % kB) * kq]);
+                        w = cmulf(ct_hi[kq * kA + t / kB], ct_lo[kq * kB + t % kB]);
                     } else {
                         w = tw[t * kq];
                     }
@@ -761,6 +833,8 @@ __global__ __launch_bounds__(NT) void acq_search_big_kernel(const float2* __rest
     float g[P];
     if (t < M) {
         dft_reg_inplace<P, +1>(v, tw, N);  // y[t + M·q] in v[reg_slot<P>(q)]
+        GNSSHIP_ACQ_STAMP_LANE(10, 0);
+        GNSSHIP_ACQ_STAMP_LANE(11, 960);
         // |y|² first (the complex points die as their magnitudes appear), then the optional grid
         // row and the row statistics in separate branch-light loops
 #pragma unroll
@@ -779,22 +853,33 @@ __global__ __launch_bounds__(NT) void acq_search_big_kernel(const float2* __rest
                 }
             }
         }
+        // The thread's top two and its row sum, branch-free (selects, no divergent exec masks).  A
+        // thread's row indices rise with q, so "x beats m" in better() order (strict >, ties to the
+        // smaller index) is plain x > m for every earlier m; a point outside the row adds +0 to s.
+        auto stat = [&](int q, bool valid) {
+            const float x = g[q];
+            const int i = t + M * q - rs.row_off;
+            const bool gt = valid && x > m.v;
+            const bool gt2 = valid && !gt && x > m2t.v;
+            m2t.v = gt ? m.v : (gt2 ? x : m2t.v);
+            m2t.i = gt ? m.i : (gt2 ? i : m2t.i);
+            m.v = gt ? x : m.v;
+            m.i = gt ? i : m.i;
+            s += valid ? x : 0.0f;
+        };
+        if (rs.row_off == 0 && rs.row_len == N) {  // the whole transform is the row (uniform branch)
 #pragma unroll
-        for (int q = 0; q < P; q++) {
-            const int i = t + M * q - rs.row_off;  // index in the row
-            if (i >= 0 && i < rs.row_len) {
-                const MaxIdx x{g[q], i};
-                if (x.v > m.v || (x.v == m.v && x.i < m.i)) {  // the thread's top two, in better() order
-                    m2t = m;
-                    m = x;
-                } else {
-                    m2t = better(m2t, x);
-                }
-                s += g[q];
+            for (int q = 0; q < P; q++) stat(q, true);
+        } else {
+#pragma unroll
+            for (int q = 0; q < P; q++) {
+                const int i = t + M * q - rs.row_off;
+                stat(q, i >= 0 && i < rs.row_len);
             }
         }
     }
     GNSSHIP_ACQ_STAMP(7);
+    GNSSHIP_ACQ_STAMP_LANE(12, 960);
     const MaxIdx m1t = m;  // this thread's best, before the block reduction
     block_argmax_sum(m, s, red_m, red_s);
     const MaxIdx best = m;
@@ -819,14 +904,14 @@ __global__ __launch_bounds__(NT) void acq_search_big_kernel(const float2* __rest
             if (i >= 0 && i < rs.row_len && !in_win(i)) m2 = better(m2, MaxIdx{g[q], i});
         }
     }
-    const MaxIdx second = block_argmax(m2, red_m);
+    const float second = block_max(m2.v, red_s);  // values ≥ 0: max(0, the largest outside the window)
     GNSSHIP_ACQ_STAMP(9);
     if (t == 0) {
         RowStat r;
         r.max = best.v;
         r.argmax = best.i;
         r.sum = sum;
-        r.second = second.v;
+        r.second = second;
         rowstat[static_cast<int64_t>(p) * n_bins + b] = r;
     }
 }

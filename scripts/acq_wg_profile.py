@@ -40,6 +40,9 @@ def main():
     for k, nm in enumerate(names):
         d = (t[:, k + 1] - t[:, k]) / 100.0
         print(f"  {nm:18s} median {np.median(d):7.2f} us  p90 {np.percentile(d, 90):7.2f}")
+    w = lambda a, b: np.median(t[:, b] - t[:, a]) / 100.0
+    print(f"  per wave: wave 0 col DFT {w(6, 10):.2f} us, stats {w(10, 7):.2f}; wave 15 col DFT {w(6, 11):.2f}, stats {w(11, 12):.2f}; "
+          f"wave 15 done -> reduced {w(12, 8):.2f}")
     ctx.close()
 
 
