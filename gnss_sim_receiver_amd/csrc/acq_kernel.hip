@@ -102,6 +102,22 @@ __device__ __forceinline__ void dft_small(float2* v)
         v[4] = make_float2(m1.x + n1.y, m1.y - n1.x);
         v[2] = make_float2(m2.x - n2.y, m2.y + n2.x);
         v[3] = make_float2(m2.x + n2.y, m2.y - n2.x);
+    } else if constexpr (R == 10) {
+        // prime-factor (Good-Thomas) 2 x 5, no internal twiddles: input n = (5·n1 + 2·n2) mod 10,
+        // output k ≡ k1 (mod 2), k ≡ k2 (mod 5), i.e. k = (5·k1 + 6·k2) mod 10
+        float2 a[2][5];
+#pragma unroll
+        for (int n1 = 0; n1 < 2; n1++)
+#pragma unroll
+            for (int n2 = 0; n2 < 5; n2++) a[n1][n2] = v[(5 * n1 + 2 * n2) % 10];
+        dft_small<5, SIGN>(a[0]);
+        dft_small<5, SIGN>(a[1]);
+#pragma unroll
+        for (int k2 = 0; k2 < 5; k2++) {
+            const float2 p = a[0][k2], q = a[1][k2];
+            v[(6 * k2) % 10] = make_float2(p.x + q.x, p.y + q.y);
+            v[(5 + 6 * k2) % 10] = make_float2(p.x - q.x, p.y - q.y);
+        }
     } else if constexpr (R == 8) {
         // radix-8 as 2 x 4: even/odd radix-4 then combine with w8^k
         float2 e[8], o[8];
@@ -298,9 +314,11 @@ __device__ __forceinline__ void wave_pass(float2* __restrict__ buf, int M, int N
 // Radix order of the compile-time rows: odd radices first.  The first Stockham pass (Ns = 1) writes
 // butterfly j's outputs at R·j…R·j+R−1, a lane stride of 8R bytes: 16-way LDS bank conflicts for
 // R = 8 (64 B), 2-way for R = 5 (40 B); the radix-8 pass goes last, where its writes are contiguous.
+// Radix 10 (a twiddle-free 2 x 5 prime-factor butterfly) where it divides: 1000 = 10·10·10 runs in
+// three passes instead of four (5·5·5·8), a quarter fewer LDS round trips per row.
 constexpr int ct_radix(int m)
 {
-    return (m % 5 == 0) ? 5 : (m % 3 == 0) ? 3 : (m % 8 == 0) ? 8 : (m % 4 == 0) ? 4 : 2;
+    return (m % 10 == 0) ? 10 : (m % 5 == 0) ? 5 : (m % 3 == 0) ? 3 : (m % 8 == 0) ? 8 : (m % 4 == 0) ? 4 : 2;
 }
 
 // Twiddles of the compile-time rows, one table per pass laid out [r − 1][k] (k < Ns, 1 ≤ r < R):
@@ -746,6 +764,29 @@ __global__ __launch_bounds__(kAcqThreads) void acq_search_kernel(const float2* _
 // NT threads per workgroup (NT ≥ M; NT/64 rows per round).  (A 40 × 625 layout of the C3 transform
 // in 640 threads, two workgroups per CU, needs ≤ 96 VGPRs and spills: 0.50 ms per C3 sweep; at one
 // workgroup per CU it ties 25 × 1000.)
+// dst[i] = x[i] ⊙ c[i], i < n, by threads tid, tid + nt, …  With an even compile-time row length
+// (MC > 0) the pairs of points go as 16-byte loads and stores (rows start 16-byte aligned), the trip
+// count is known and the loads are issued back to back.
+template <int MC>
+__device__ __forceinline__ void load_rows_prod(float2* __restrict__ dst, const float2* __restrict__ x, const float2* __restrict__ c, int n,
+    int tid, int nt)
+{
+    if constexpr (MC > 0 && MC % 2 == 0) {
+        const float4* x4 = reinterpret_cast<const float4*>(x);
+        const float4* c4 = reinterpret_cast<const float4*>(c);
+        float4* d4 = reinterpret_cast<float4*>(dst);
+#pragma unroll 4
+        for (int i = tid; i < n / 2; i += nt) {
+            const float4 a = x4[i], b = c4[i];
+            const float2 p0 = cmulf(make_float2(a.x, a.y), make_float2(b.x, b.y));
+            const float2 p1 = cmulf(make_float2(a.z, a.w), make_float2(b.z, b.w));
+            d4[i] = make_float4(p0.x, p0.y, p1.x, p1.y);
+        }
+    } else {
+        for (int i = tid; i < n; i += nt) dst[i] = cmulf(x[i], c[i]);
+    }
+}
+
 template <int P, int MC = 0, int NT = kAcqThreads>
 __global__ __launch_bounds__(NT) void acq_search_big_kernel(const float2* __restrict__ XT,
     const float2* __restrict__ codesT, FftPlan row_plan, const float2* __restrict__ tw, int n_bins, RowSpec rs, int accumulate,
@@ -756,7 +797,7 @@ __global__ __launch_bounds__(NT) void acq_search_big_kernel(const float2* __rest
     __shared__ MaxIdx red_m[NT / 64];
     __shared__ float red_s[NT / 64];
     const int b = blockIdx.x, p = blockIdx.y;
-    const int M = row_plan.n;
+    const int M = MC > 0 ? MC : row_plan.n;  // compile-time for the C3 plan: the load loops unroll
     const int N = P * M;
     const int t = threadIdx.x;
     const float2* x = XT + static_cast<int64_t>(b) * N;
@@ -790,9 +831,9 @@ __global__ __launch_bounds__(NT) void acq_search_big_kernel(const float2* __rest
         const int r0 = rr == 0 ? 0 : kFirst + (rr - 1) * kRoundRows;
         const int nrows = rr == 0 ? kFirst : kRoundRows;
         if (kPrefetch && rr == 1) {
-            for (int i = t; i < kFirst * M; i += NT) lds[i] = cmulf(x[kRoundRows * M + i], c[kRoundRows * M + i]);  // ×conj(code FFT)
+            load_rows_prod<MC>(lds, x + kRoundRows * M, c + kRoundRows * M, kFirst * M, t, NT);  // ×conj(code FFT)
         } else {
-            for (int i = t; i < nrows * M; i += NT) lds[i] = cmulf(x[r0 * M + i], c[r0 * M + i]);
+            load_rows_prod<MC>(lds, x + r0 * M, c + r0 * M, nrows * M, t, NT);
         }
         __syncthreads();
         GNSSHIP_ACQ_STAMP(r0 == 0 ? 1 : 4);
@@ -804,7 +845,7 @@ __global__ __launch_bounds__(NT) void acq_search_big_kernel(const float2* __rest
             if constexpr (MC > 0) wave_fft_row_ct<MC, 1, +1>(lds + wave * M, rtw, lane_r);
             else wave_fft_row<+1>(lds + wave * M, row_plan, rtw, lane);
         } else if (kPrefetch && rr == 0) {
-            for (int i = lane; i < M; i += 64) lds[wave * M + i] = cmulf(x[wave * M + i], c[wave * M + i]);
+            load_rows_prod<MC>(lds + wave * M, x + wave * M, c + wave * M, M, lane, 64);
         }
         __syncthreads();
         GNSSHIP_ACQ_STAMP(r0 == 0 ? 2 : 5);
