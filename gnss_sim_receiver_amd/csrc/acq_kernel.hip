@@ -633,6 +633,7 @@ __device__ __forceinline__ float wave_sum_f(float s)
     return s;
 }
 
+template <int NW = kAcqThreads / 64>  // waves per workgroup (the cross-wave loops unroll)
 __device__ __forceinline__ MaxIdx block_argmax(MaxIdx m, MaxIdx* red)
 {
     m = wave_argmax(m);
@@ -640,11 +641,13 @@ __device__ __forceinline__ MaxIdx block_argmax(MaxIdx m, MaxIdx* red)
     if (lane == 0) red[wave] = m;
     __syncthreads();
     MaxIdx r = red[0];
-    for (int w = 1; w < static_cast<int>(blockDim.x >> 6); w++) r = better(r, red[w]);
+#pragma unroll
+    for (int w = 1; w < NW; w++) r = better(r, red[w]);
     __syncthreads();
     return r;
 }
 
+template <int NW = kAcqThreads / 64>  // waves per workgroup (the cross-wave loops unroll)
 __device__ __forceinline__ float block_sum(float s, float* red)
 {
     s = wave_sum_f(s);
@@ -652,7 +655,8 @@ __device__ __forceinline__ float block_sum(float s, float* red)
     if (lane == 0) red[wave] = s;
     __syncthreads();
     float r = 0.0f;
-    for (int w = 0; w < static_cast<int>(blockDim.x >> 6); w++) r += red[w];
+#pragma unroll
+    for (int w = 0; w < NW; w++) r += red[w];
     __syncthreads();
     return r;
 }
@@ -669,6 +673,7 @@ __device__ __forceinline__ float wave_max_f(float s)
 }
 
 // Block maximum of values (no index): the second peak keeps only its value.
+template <int NW = kAcqThreads / 64>  // waves per workgroup (the cross-wave loops unroll)
 __device__ __forceinline__ float block_max(float s, float* red)
 {
     s = wave_max_f(s);
@@ -676,11 +681,13 @@ __device__ __forceinline__ float block_max(float s, float* red)
     if (lane == 0) red[wave] = s;
     __syncthreads();
     float r = red[0];
-    for (int w = 1; w < static_cast<int>(blockDim.x >> 6); w++) r = fmaxf(r, red[w]);
+#pragma unroll
+    for (int w = 1; w < NW; w++) r = fmaxf(r, red[w]);
     return r;
 }
 
 // Both at once (one barrier pair): the row maximum with its first index and the row sum.
+template <int NW = kAcqThreads / 64>  // waves per workgroup (the cross-wave loops unroll)
 __device__ __forceinline__ void block_argmax_sum(MaxIdx& m, float& s, MaxIdx* redm, float* reds)
 {
     m = wave_argmax(m);
@@ -693,7 +700,8 @@ __device__ __forceinline__ void block_argmax_sum(MaxIdx& m, float& s, MaxIdx* re
     __syncthreads();
     MaxIdx r = redm[0];
     float t = 0.0f;
-    for (int w = 0; w < static_cast<int>(blockDim.x >> 6); w++) {
+#pragma unroll
+    for (int w = 0; w < NW; w++) {
         if (w) r = better(r, redm[w]);
         t += reds[w];
     }
@@ -922,7 +930,7 @@ __global__ __launch_bounds__(NT) void acq_search_big_kernel(const float2* __rest
     GNSSHIP_ACQ_STAMP(7);
     GNSSHIP_ACQ_STAMP_LANE(12, 960);
     const MaxIdx m1t = m;  // this thread's best, before the block reduction
-    block_argmax_sum(m, s, red_m, red_s);
+    block_argmax_sum<NT / 64>(m, s, red_m, red_s);
     const MaxIdx best = m;
     const float sum = s;
     GNSSHIP_ACQ_STAMP(8);
@@ -945,7 +953,7 @@ __global__ __launch_bounds__(NT) void acq_search_big_kernel(const float2* __rest
             if (i >= 0 && i < rs.row_len && !in_win(i)) m2 = better(m2, MaxIdx{g[q], i});
         }
     }
-    const float second = block_max(m2.v, red_s);  // values ≥ 0: max(0, the largest outside the window)
+    const float second = block_max<NT / 64>(m2.v, red_s);  // values ≥ 0: max(0, the largest outside the window)
     GNSSHIP_ACQ_STAMP(9);
     if (t == 0) {
         RowStat r;
@@ -960,22 +968,24 @@ __global__ __launch_bounds__(NT) void acq_search_big_kernel(const float2* __rest
 // One thread per PRN: the reference's row scan (strict >, ascending bin) and decision values.
 // Step two of make_2_steps (step2.active): Doppler = (int)(center + (bin − floor(nb/2))·step2) in float
 // and the CFAR input power left at its step-one value (pcps_acquisition.cc:516-525).
-__global__ void acq_decide_kernel(const RowStat* __restrict__ rowstat, int n_prns, int n_bins, int N, int doppler_max, int doppler_step,
-    int doppler_center, int dwells, int use_cfar, float samples_per_code, float resampler_ratio, uint32_t resampler_latency, Step2Spec step2,
-    gnsship_acq_result* __restrict__ out)
+__global__ __launch_bounds__(64) void acq_decide_kernel(const RowStat* __restrict__ rowstat, int n_prns, int n_bins, int N, int doppler_max,
+    int doppler_step, int doppler_center, int dwells, int use_cfar, float samples_per_code, float resampler_ratio, uint32_t resampler_latency,
+    Step2Spec step2, gnsship_acq_result* __restrict__ out)
 {
-    const int p = blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= n_prns) return;
+    // one wave per PRN: lane b scans bins b, b + 64, …, then a wave arg-max.  The reference's scan
+    // (gmax = 0; strict >, ascending bin) selects the first bin holding the row maximum, and none
+    // (bin 0, peak 0) when no row maximum exceeds 0: better() with ties to the smaller index, from a
+    // start of {0, −1} that an equal 0 never displaces.
+    const int p = blockIdx.x;
+    const int lane = threadIdx.x;
     const RowStat* rs = rowstat + static_cast<int64_t>(p) * n_bins;
-    float gmax = 0.0f;
-    int bi = 0, ti = 0;
-    for (int b = 0; b < n_bins; b++) {
-        if (rs[b].max > gmax) {
-            gmax = rs[b].max;
-            bi = b;
-            ti = rs[b].argmax;
-        }
-    }
+    MaxIdx m{0.0f, -1};
+    for (int b = lane; b < n_bins; b += 64) m = better(m, MaxIdx{rs[b].max, b});
+    m = wave_argmax(m);
+    if (lane != 0) return;
+    const float gmax = m.i < 0 ? 0.0f : m.v;
+    const int bi = m.i < 0 ? 0 : m.i;
+    const int ti = m.i < 0 ? 0 : rs[bi].argmax;
     gnsship_acq_result r;
     r.doppler_index = static_cast<uint32_t>(bi);
     r.code_index = static_cast<uint32_t>(ti);
@@ -1313,7 +1323,7 @@ hipError_t launch_acq_decide(const RowStat* rowstat, int n_prns, int n_bins, int
     int dwells, int use_cfar, float samples_per_code, float resampler_ratio, uint32_t resampler_latency, Step2Spec step2, gnsship_acq_result* out,
     hipStream_t stream)
 {
-    hipLaunchKernelGGL(acq_decide_kernel, dim3((n_prns + 63) / 64), dim3(64), 0, stream, rowstat, n_prns, n_bins, N, doppler_max, doppler_step,
+    hipLaunchKernelGGL(acq_decide_kernel, dim3(n_prns), dim3(64), 0, stream, rowstat, n_prns, n_bins, N, doppler_max, doppler_step,
         doppler_center, dwells, use_cfar, samples_per_code, resampler_ratio, resampler_latency, step2, out);
     return hipGetLastError();
 }
