@@ -17,6 +17,11 @@ OBJS := $(patsubst $(CSRC)/%.hip,$(OBJDIR)/%.o,$(HIP_SRCS)) $(patsubst $(CSRC)/%
 
 all: $(LIB) oracle
 
+# The acquisition FFTs are plain f32 VALU work: SLP packing into v_pk_add/mul_f32 buys no rate on
+# gfx950 (a packed f32 op issues in 4 cycles, a scalar one in 2) and costs register-pair moves
+# and VGPRs (C3 search kernel: 128 VGPRs + scratch packed, 84 unpacked).  Same IEEE ops either way.
+$(OBJDIR)/acq_kernel.o build/prof_obj/acq_kernel.o: HIPFLAGS += -fno-slp-vectorize
+
 $(OBJDIR)/%.o: $(CSRC)/%.hip $(HDRS)
 	@mkdir -p $(OBJDIR)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@

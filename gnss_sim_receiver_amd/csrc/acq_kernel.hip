@@ -542,13 +542,23 @@ __global__ __launch_bounds__(kBigColThreads) void acq_fft_big_cols_kernel(const 
     const int t = blockIdx.x * kBigColThreads + threadIdx.x;
     const int b = blockIdx.y;
     if (t >= M) return;
-    const float2* m = mult ? mult + static_cast<int64_t>(b) * N : nullptr;
     float2 v[P];
+    // branch-free loads (every load of the column in flight at once): past the consumed samples the
+    // index is clamped in bounds and the value replaced by zero (the zero padding)
+    const int last = n_valid > 0 ? n_valid - 1 : 0;
 #pragma unroll
     for (int q = 0; q < P; q++) {
-        float2 x = (t + M * q < n_valid) ? load_if<FMT>(sig, t + M * q) : make_float2(0.0f, 0.0f);
-        if (m) x = cmulf(x, m[t + M * q]);  // volk_32fc_x2_multiply_32fc(in, wipeoff)
-        v[q] = x;
+        const int i = t + M * q;
+        const float2 x = load_if<FMT>(sig, i < n_valid ? i : last);
+        v[q] = i < n_valid ? x : make_float2(0.0f, 0.0f);
+    }
+    if (mult) {  // uniform: the Doppler wipeoff of bin b (volk_32fc_x2_multiply_32fc(in, wipeoff))
+        const float2* m = mult + static_cast<int64_t>(b) * N;
+        float2 w[P];
+#pragma unroll
+        for (int q = 0; q < P; q++) w[q] = m[t + M * q];
+#pragma unroll
+        for (int q = 0; q < P; q++) v[q] = cmulf(v[q], w[q]);
     }
     dft_reg_inplace<P, -1>(v, tw, N);  // X[kq] in v[reg_slot<P>(kq)]
     float2* out = rowsT + static_cast<int64_t>(b) * N;
@@ -565,7 +575,7 @@ __global__ __launch_bounds__(kBigRowWaves * 64) void acq_fft_big_rows_kernel(Fft
     float2* __restrict__ rowsT, int n_rows_total, int conj_out)
 {
     extern __shared__ __attribute__((aligned(16))) float2 lds[];
-    const int M = row_plan.n;
+    const int M = MC > 0 ? MC : row_plan.n;  // compile-time for the C3 plan: the row copies unroll (loads in flight together)
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     float2* rtw = lds + kBigRowWaves * M;  // row twiddles exp(−2πi m/M) = tw[m·P], m < M (per-pass tables for MC > 0)
     if constexpr (MC > 0) fill_row_pass_tw<MC, 1>(rtw, tw, P, threadIdx.x, kBigRowWaves * 64);
@@ -573,16 +583,39 @@ __global__ __launch_bounds__(kBigRowWaves * 64) void acq_fft_big_rows_kernel(Fft
     const int r = blockIdx.x * kBigRowWaves + wave;
     float2* row = lds + wave * M;
     float2* g = rowsT + static_cast<int64_t>(r) * M;  // rows are contiguous: b·N + kq·M = (b·P + kq)·M
-    if (r < n_rows_total)
-        for (int i = lane; i < M; i += 64) row[i] = g[i];
+    if constexpr (MC > 0 && MC % 2 == 0) {  // 16-byte pairs (rows start 16-byte aligned)
+        const float4* g4 = reinterpret_cast<const float4*>(g);
+        float4* row4 = reinterpret_cast<float4*>(row);
+        if (r < n_rows_total) {
+#pragma unroll
+            for (int i = lane; i < MC / 2; i += 64) row4[i] = g4[i];
+        }
+    } else {
+        if (r < n_rows_total)
+            for (int i = lane; i < M; i += 64) row[i] = g[i];
+    }
     __syncthreads();
     if (r >= n_rows_total) return;
     if constexpr (MC > 0) wave_fft_row_ct<MC, 1, -1>(row, rtw, lane);
     else wave_fft_row<-1>(row, row_plan, rtw, lane);
-    for (int i = lane; i < M; i += 64) {
-        float2 y = row[i];
-        if (conj_out) y.y = -y.y;
-        g[i] = y;
+    if constexpr (MC > 0 && MC % 2 == 0) {
+        const float4* row4 = reinterpret_cast<const float4*>(row);
+        float4* g4 = reinterpret_cast<float4*>(g);
+#pragma unroll
+        for (int i = lane; i < MC / 2; i += 64) {
+            float4 y = row4[i];
+            if (conj_out) {
+                y.y = -y.y;
+                y.w = -y.w;
+            }
+            g4[i] = y;
+        }
+    } else {
+        for (int i = lane; i < M; i += 64) {
+            float2 y = row[i];
+            if (conj_out) y.y = -y.y;
+            g[i] = y;
+        }
     }
 }
 
