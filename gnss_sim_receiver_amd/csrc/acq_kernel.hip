@@ -206,6 +206,37 @@ __device__ __forceinline__ const float2* stage_twiddles(float2* dst, const float
     return dst;  // visible after the caller's next barrier
 }
 
+// dst[i] = a[i] ⊙ b[i] (b == nullptr: a[i]), i < n, by threads tid, tid + nt, … with a runtime n:
+// the loads go in batches of kLdsBatch per thread (index clamped in bounds, the store guarded), so a
+// batch is in flight together instead of one load-wait-store round trip per element.
+constexpr int kLdsBatch = 8;
+__device__ __forceinline__ void lds_load_prod(float2* __restrict__ dst, const float2* __restrict__ a, const float2* __restrict__ b, int n,
+    int tid, int nt)
+{
+    for (int base = tid; base < n; base += kLdsBatch * nt) {
+        float2 av[kLdsBatch], bv[kLdsBatch];
+#pragma unroll
+        for (int u = 0; u < kLdsBatch; u++) {
+            const int i = base + u * nt;
+            av[u] = a[i < n ? i : n - 1];
+        }
+        if (b) {
+#pragma unroll
+            for (int u = 0; u < kLdsBatch; u++) {
+                const int i = base + u * nt;
+                bv[u] = b[i < n ? i : n - 1];
+            }
+#pragma unroll
+            for (int u = 0; u < kLdsBatch; u++) av[u] = cmulf(av[u], bv[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < kLdsBatch; u++) {
+            const int i = base + u * nt;
+            if (i < n) dst[i] = av[u];
+        }
+    }
+}
+
 // rows[b] = FFT(sig ⊙ mult[b])  (mult == nullptr: FFT(sig)); conj_out: store conj (code FFT).
 template <int FMT>
 __global__ __launch_bounds__(kAcqThreads) void acq_fft_rows_kernel(const void* __restrict__ sig, const float2* __restrict__ mult,
@@ -216,10 +247,30 @@ __global__ __launch_bounds__(kAcqThreads) void acq_fft_rows_kernel(const void* _
     const int N = plan.n;
     const float2* m = mult ? mult + static_cast<int64_t>(b) * N : nullptr;
     const float2* twl = N <= kTwLdsMax ? stage_twiddles(lds + N, tw, N) : tw;
-    for (int i = threadIdx.x; i < N; i += blockDim.x) {
-        float2 x = i < n_valid ? load_if<FMT>(sig, i) : make_float2(0.0f, 0.0f);  // zero-padded past the consumed samples
-        if (m) x = cmulf(x, m[i]);  // volk_32fc_x2_multiply_32fc(in, wipeoff)
-        lds[i] = x;
+    const int last = n_valid > 0 ? n_valid - 1 : 0;
+    for (int base = threadIdx.x; base < N; base += kLdsBatch * blockDim.x) {  // batches of loads in flight
+        float2 xv[kLdsBatch];
+#pragma unroll
+        for (int u = 0; u < kLdsBatch; u++) {
+            const int i = base + u * blockDim.x;
+            const float2 x = load_if<FMT>(sig, i < n_valid ? i : last);
+            xv[u] = i < n_valid ? x : make_float2(0.0f, 0.0f);  // zero-padded past the consumed samples
+        }
+        if (m) {
+            float2 wv[kLdsBatch];
+#pragma unroll
+            for (int u = 0; u < kLdsBatch; u++) {
+                const int i = base + u * blockDim.x;
+                wv[u] = m[i < N ? i : N - 1];
+            }
+#pragma unroll
+            for (int u = 0; u < kLdsBatch; u++) xv[u] = cmulf(xv[u], wv[u]);  // volk_32fc_x2_multiply_32fc(in, wipeoff)
+        }
+#pragma unroll
+        for (int u = 0; u < kLdsBatch; u++) {
+            const int i = base + u * blockDim.x;
+            if (i < N) lds[i] = xv[u];
+        }
     }
     __syncthreads();
     fft_lds<-1>(lds, plan, twl);
@@ -666,7 +717,7 @@ __device__ __forceinline__ float wave_sum_f(float s)
     return s;
 }
 
-template <int NW = kAcqThreads / 64>  // waves per workgroup (the cross-wave loops unroll)
+template <int NW>  // waves per workgroup, = blockDim.x / 64 (the cross-wave loops unroll)
 __device__ __forceinline__ MaxIdx block_argmax(MaxIdx m, MaxIdx* red)
 {
     m = wave_argmax(m);
@@ -680,7 +731,7 @@ __device__ __forceinline__ MaxIdx block_argmax(MaxIdx m, MaxIdx* red)
     return r;
 }
 
-template <int NW = kAcqThreads / 64>  // waves per workgroup (the cross-wave loops unroll)
+template <int NW>  // waves per workgroup, = blockDim.x / 64 (the cross-wave loops unroll)
 __device__ __forceinline__ float block_sum(float s, float* red)
 {
     s = wave_sum_f(s);
@@ -706,7 +757,7 @@ __device__ __forceinline__ float wave_max_f(float s)
 }
 
 // Block maximum of values (no index): the second peak keeps only its value.
-template <int NW = kAcqThreads / 64>  // waves per workgroup (the cross-wave loops unroll)
+template <int NW>  // waves per workgroup, = blockDim.x / 64 (the cross-wave loops unroll)
 __device__ __forceinline__ float block_max(float s, float* red)
 {
     s = wave_max_f(s);
@@ -720,7 +771,7 @@ __device__ __forceinline__ float block_max(float s, float* red)
 }
 
 // Both at once (one barrier pair): the row maximum with its first index and the row sum.
-template <int NW = kAcqThreads / 64>  // waves per workgroup (the cross-wave loops unroll)
+template <int NW>  // waves per workgroup, = blockDim.x / 64 (the cross-wave loops unroll)
 __device__ __forceinline__ void block_argmax_sum(MaxIdx& m, float& s, MaxIdx* redm, float* reds)
 {
     m = wave_argmax(m);
@@ -758,7 +809,7 @@ __global__ __launch_bounds__(kAcqThreads) void acq_search_kernel(const float2* _
     const float2* x = X + static_cast<int64_t>(b) * N;
     const float2* c = codes_fft + static_cast<int64_t>(p) * N;
     const float2* twl = N <= kTwLdsMax ? stage_twiddles(lds + N, tw, N) : tw;
-    for (int i = threadIdx.x; i < N; i += blockDim.x) lds[i] = cmulf(x[i], c[i]);  // ×conj(code FFT)
+    lds_load_prod(lds, x, c, N, threadIdx.x, blockDim.x);  // ×conj(code FFT)
     __syncthreads();
     fft_lds<+1>(lds, plan, twl);
     // |Y|² in place (as float in the .x slot) + optional grid row (accumulated over dwells)
@@ -776,7 +827,7 @@ __global__ __launch_bounds__(kAcqThreads) void acq_search_kernel(const float2* _
         m = better(m, MaxIdx{mag, i});
         s += mag;
     }
-    block_argmax_sum(m, s, red_m, red_s);
+    block_argmax_sum<kAcqThreads / 64>(m, s, red_m, red_s);
     const MaxIdx best = m;
     const float sum = s;
     // second peak outside the circular window [best-spc, best+spc) (first_vs_second_peak_statistic :566-593)
@@ -788,7 +839,7 @@ __global__ __launch_bounds__(kAcqThreads) void acq_search_kernel(const float2* _
         const float v = in_win ? 0.0f : lds[rs.row_off + i].x;
         m2 = better(m2, MaxIdx{v, i});
     }
-    const MaxIdx second = block_argmax(m2, red_m);
+    const MaxIdx second = block_argmax<kAcqThreads / 64>(m2, red_m);
     if (threadIdx.x == 0) {
         RowStat r;
         r.max = best.v;
@@ -1069,13 +1120,21 @@ __global__ __launch_bounds__(kHugeColThreads) void acq_huge_cols_fwd_kernel(cons
     const int b = blockIdx.y;
     const int N = P * M;
     if (m >= M) return;
-    const float2* w = mult ? mult + static_cast<int64_t>(b) * N : nullptr;
     float2 v[P];
+    const int last = n_valid > 0 ? n_valid - 1 : 0;  // branch-free loads, zero padding past n_valid
 #pragma unroll
     for (int q = 0; q < P; q++) {
-        float2 x = (m + M * q < n_valid) ? load_if<FMT>(sig, m + M * q) : make_float2(0.0f, 0.0f);
-        if (w) x = cmulf(x, w[m + M * q]);  // volk_32fc_x2_multiply_32fc(in, wipeoff)
-        v[q] = x;
+        const int i = m + M * q;
+        const float2 x = load_if<FMT>(sig, i < n_valid ? i : last);
+        v[q] = i < n_valid ? x : make_float2(0.0f, 0.0f);
+    }
+    if (mult) {  // uniform: volk_32fc_x2_multiply_32fc(in, wipeoff)
+        const float2* w = mult + static_cast<int64_t>(b) * N;
+        float2 wv[P];
+#pragma unroll
+        for (int q = 0; q < P; q++) wv[q] = w[m + M * q];
+#pragma unroll
+        for (int q = 0; q < P; q++) v[q] = cmulf(v[q], wv[q]);
     }
     dft_reg<P, 1, -1>(v, twN, N);
     float2* out = T + static_cast<int64_t>(b) * N + m;
@@ -1096,7 +1155,7 @@ __global__ __launch_bounds__(kAcqThreads) void acq_huge_rows_kernel(const float2
     const int64_t row = static_cast<int64_t>(blockIdx.x) * M;
     const float2* a = A + blockIdx.y * a_sy + blockIdx.z * a_sz + row;
     const float2* bb = B ? B + blockIdx.y * b_sy + blockIdx.z * b_sz + row : nullptr;
-    for (int i = threadIdx.x; i < M; i += kAcqThreads) lds[i] = bb ? cmulf(a[i], bb[i]) : a[i];  // ×conj(code FFT)
+    lds_load_prod(lds, a, bb, M, threadIdx.x, kAcqThreads);  // ×conj(code FFT)
     __syncthreads();
     fft_lds<SIGN>(lds, plan, twM);
     float2* d = D + blockIdx.y * d_sy + blockIdx.z * d_sz + row;
@@ -1146,8 +1205,8 @@ __global__ __launch_bounds__(kHugeColThreads) void acq_huge_cols_inv_kernel(cons
             s += mag;
         }
     }
-    const MaxIdx bm = block_argmax(best, red_m);
-    const float bs = block_sum(s, red_s);
+    const MaxIdx bm = block_argmax<kHugeColThreads / 64>(best, red_m);
+    const float bs = block_sum<kHugeColThreads / 64>(s, red_s);
     if (threadIdx.x == 0) tiles[cell * gridDim.x + blockIdx.x] = TileStat{bm.v, bm.i, bs, 0};
 }
 
@@ -1165,7 +1224,7 @@ __global__ __launch_bounds__(kAcqThreads) void acq_huge_finalize_kernel(const fl
         m = better(m, MaxIdx{ts[i].max, ts[i].argmax});
         s += ts[i].sum;
     }
-    block_argmax_sum(m, s, red_m, red_s);
+    block_argmax_sum<kAcqThreads / 64>(m, s, red_m, red_s);
     const MaxIdx best = m;
     const float sum = s;
     int e1 = best.i - rs.spc, e2 = best.i + rs.spc;
@@ -1176,7 +1235,7 @@ __global__ __launch_bounds__(kAcqThreads) void acq_huge_finalize_kernel(const fl
         const bool in_win = (e1 < e2) ? (i >= e1 && i < e2) : (i >= e1 || i < e2);
         m2 = better(m2, MaxIdx{in_win ? 0.0f : g[i], i});
     }
-    const MaxIdx second = block_argmax(m2, red_m);
+    const MaxIdx second = block_argmax<kAcqThreads / 64>(m2, red_m);
     if (threadIdx.x == 0) rowstat[(static_cast<int64_t>(prn_offset) + blockIdx.y) * n_bins + blockIdx.x] = RowStat{best.v, best.i, sum, second.v};
 }
 

@@ -38,6 +38,24 @@ def run_one(out):
         res[tag + "_ms"] = np.array((time.perf_counter() - t0) / 20 * 1e3)
         acq.close()
         dev.free()
+    # Galileo E1 all-sky (huge layout, N = 100000), results only (the grid would be 512 MB)
+    fs, n = 25000000, 100000
+    sats = S.random_sky(6, seed=0x6E550007, system="GAL", prns=[2, 9, 13, 21, 26, 31])
+    sig = S.generate_if(fs, n, sats, seed=0x6E550007)
+    acq = engine.PcpsAcquisition(ctx, fs, n, 5000, 250, 0, False, max_prns=32, ms_per_code=4)
+    for k in range(32):
+        acq.set_local_code(C.galileo_e1_code_gen_complex_sampled("1B", False, k + 1, fs), k)
+    dev = ctx.upload(np.ascontiguousarray(sig))
+    r, _ = acq.run(dev, n_prns=32)
+    res["e1"] = np.frombuffer(b"".join(bytes(x) for x in r), np.uint8)
+    res["e1_grid"] = np.zeros(1, np.uint8)
+    ctx.sync()
+    t0 = time.perf_counter()
+    for _ in range(5):
+        acq.run(dev, n_prns=32)
+    res["e1_ms"] = np.array((time.perf_counter() - t0) / 5 * 1e3)
+    acq.close()
+    dev.free()
     ctx.close()
     np.savez(out, **res)
 
@@ -64,13 +82,16 @@ def main():
         outs.append(np.load(out))
     a, b = outs
     ok = True
-    for tag in ("c3", "c1"):
+    for tag in ("c3", "c1", "e1"):
         same = a[tag].tobytes() == b[tag].tobytes()
         gsame = a[tag + "_grid"].tobytes() == b[tag + "_grid"].tobytes()
         ra, rb = (np.frombuffer(x[tag].tobytes(), np.dtype(abi.AcqResult)) for x in (a, b))
         cells = all(np.array_equal(ra[f], rb[f]) for f in ("doppler_hz", "acq_delay_samples"))
         rel = float(np.max(np.abs(ra["test_statistic"] - rb["test_statistic"]) / np.abs(rb["test_statistic"])))
         ok &= cells if TOLERANT else (same and gsame)
+        bad = [k for k in range(len(ra)) if bytes(ra[k]) != bytes(rb[k])]
+        for k in bad[:6]:
+            print(f"  {tag} prn slot {k}: " + ", ".join(f"{f} {ra[f][k]} / {rb[f][k]}" for f in ("doppler_hz", "acq_delay_samples", "peak", "test_statistic")))
         print(f"{tag}: results identical {same}, grid identical {gsame}, peaks (Doppler, delay) identical {cells}, "
               f"test statistic max rel diff {rel:.2e}; sweep {float(a[tag + '_ms']):.3f} -> {float(b[tag + '_ms']):.3f} ms")
     sys.exit(0 if ok else 1)

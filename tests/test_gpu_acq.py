@@ -292,6 +292,38 @@ def test_huge_galileo_e1_25msps(ctx, cboc):
         assert min(abs(res[k].code_index - exp), n - abs(res[k].code_index - exp)) <= 2, (s.prn, res[k].code_index, exp)
 
 
+def test_huge_galileo_e1_all_sky_prn_batches(ctx):
+    """E1 all-sky as the bench runs it: 32 PRNs x 41 bins at N = 100000, so the inverse stage runs in
+    several PRN batches (≈256 MiB of row scratch each) with 4-wave column workgroups.  Two runs give
+    identical results, every statistic is finite, and two present PRNs and one absent PRN match the
+    oracle core exactly (a regression test for a cross-wave reduction that read past its workgroup's
+    waves)."""
+    fs, n, dmax, step = 25000000, 100000, 5000, 250
+    present_prns = [2, 9, 13, 21, 26, 31]
+    sats = signals.random_sky(6, seed=0x6E550007, system="GAL", prns=present_prns)
+    sig = signals.generate_if(fs, n, sats, seed=0x6E550007)
+    acq = engine.PcpsAcquisition(ctx, fs, n, dmax, step, 0, False, max_prns=32, ms_per_code=4)
+    lc = [codes.galileo_e1_code_gen_complex_sampled("1B", False, p, fs) for p in range(1, 33)]
+    for k in range(32):
+        acq.set_local_code(lc[k], k)
+    dev = ctx.upload(np.ascontiguousarray(sig))
+    res1, _ = acq.run(dev, n_prns=32)
+    res2, _ = acq.run(dev, n_prns=32)
+    acq.close()
+    dev.free()
+    assert b"".join(bytes(r) for r in res1) == b"".join(bytes(r) for r in res2)
+    stat = np.array([r.test_statistic for r in res1])
+    assert np.all(np.isfinite(stat)), stat
+    assert min(stat[p - 1] for p in present_prns) > max(stat[k] for k in range(32) if k + 1 not in present_prns)
+    spc, spcode = int(np.ceil(np.float32(fs) / np.float32(1023000.0))), float(np.float32(np.float32(fs) * np.float32(0.001)) * 4)
+    ex = ExactCount()
+    for p in (2, 26, 5):
+        ref, rgrid = O.pcps_acquisition_core(sig, lc[p - 1], fs, dmax, step, 0, False, samples_per_chip=spc, samples_per_code=spcode)
+        ex.check(res1[p - 1], ref, rgrid, p)
+        np.testing.assert_allclose(res1[p - 1].test_statistic, ref.test_statistic, rtol=2e-3)
+    assert ex.exact >= 2, ex.ties
+
+
 def test_huge_limits(ctx):
     from gnss_sim_receiver_amd import abi
     with pytest.raises(abi.GnssHipError):
