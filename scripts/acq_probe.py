@@ -1,5 +1,6 @@
 """Acquisition sweeps for profiling (rocprofv3): C3 (32 PRN x 40 bins x 25000, 25 Msps, BASELINE's
-signal) and the C1 shape (32 PRN x 40 bins x 4000, 4 Msps), `reps` each after a warm-up.
+signal), the C1 shape (32 PRN x 40 bins x 4000, 4 Msps) and the Galileo E1 all-sky sweep (32 PRN x
+41 bins x 100000, huge layout), `reps` each after a warm-up.
     python scripts/acq_probe.py [reps]"""
 import os
 import sys
@@ -11,10 +12,15 @@ import numpy as np  # noqa: E402
 from gnss_sim_receiver_amd import codes as C, engine, signals as S  # noqa: E402
 
 
-def sweep(ctx, fs, n, sig, reps):
-    acq = engine.PcpsAcquisition(ctx, fs, n, 5000, 250, 0, True, max_prns=32)
-    for k in range(32):
-        acq.set_local_code(C.gps_l1_ca_code_gen_complex_sampled(k + 1, fs), k)
+def sweep(ctx, fs, n, sig, reps, e1=False):
+    if e1:
+        acq = engine.PcpsAcquisition(ctx, fs, n, 5000, 250, 0, False, max_prns=32, ms_per_code=4)
+        for k in range(32):
+            acq.set_local_code(C.galileo_e1_code_gen_complex_sampled("1B", False, k + 1, fs), k)
+    else:
+        acq = engine.PcpsAcquisition(ctx, fs, n, 5000, 250, 0, True, max_prns=32)
+        for k in range(32):
+            acq.set_local_code(C.gps_l1_ca_code_gen_complex_sampled(k + 1, fs), k)
     dev = ctx.upload(np.ascontiguousarray(sig[:n]))
     res, _ = acq.run(dev, n_prns=32)
     t0 = time.perf_counter()
@@ -33,6 +39,9 @@ def main():
     dt3, r3 = sweep(ctx, 25000000, 25000, S.generate_if(25000000, 25000, c3, seed=0x6E550003), reps)
     sky = S.random_sky(32, seed=0x6E550002)
     dt1, r1 = sweep(ctx, 4000000, 4000, S.generate_if(4000000, 4000, sky, seed=0x6E550002), reps)
+    gal = S.random_sky(6, seed=0x6E550007, system="GAL", prns=[2, 9, 13, 21, 26, 31])
+    dte, _ = sweep(ctx, 25000000, 100000, S.generate_if(25000000, 100000, gal, seed=0x6E550007), max(1, reps // 4), e1=True)
+    print(f"E1 all-sky sweep {dte * 1e3:.3f} ms")
     present = sorted(s.prn for s in c3)
     top = sorted(range(32), key=lambda k: -r3[k].test_statistic)[:10]
     hits = len(set(k + 1 for k in top) & set(present))  # a sanity count only: parity is tests/test_gpu_acq.py
