@@ -1210,33 +1210,74 @@ __global__ __launch_bounds__(kHugeColThreads) void acq_huge_cols_inv_kernel(cons
     if (threadIdx.x == 0) tiles[cell * gridDim.x + blockIdx.x] = TileStat{bm.v, bm.i, bs, 0};
 }
 
-// Row statistics of cell (prn blockIdx.y, bin blockIdx.x) from its tiles and grid row.
+// Row statistics of cell (prn blockIdx.y, bin blockIdx.x) from its tiles and grid row.  Tile i
+// holds columns m ∈ [256·i, 256·i + 256) of every register point q, i.e. row indices
+// n = m + M·q − row_off.  The second peak (the largest |y|² outside the window around the peak,
+// first_vs_second_peak_statistic :566-593) takes the maximum of every tile that misses the window
+// from its tile statistic and rescans from the grid only the few tiles the window meets (the window
+// is 2·spc consecutive indices: one or two column runs), instead of the whole row.
+constexpr int kHugeFlagMax = 64;  // tiles met by the window that are rescanned together (more: full-row fallback)
+
+__device__ __forceinline__ bool interval_meets(int a0, int a1, int b0, int b1) { return a0 < b1 && b0 < a1; }
+
 __global__ __launch_bounds__(kAcqThreads) void acq_huge_finalize_kernel(const float* __restrict__ grid, const TileStat* __restrict__ tiles,
-    int n_tiles, int n_bins, int prn_offset, RowSpec rs, RowStat* __restrict__ rowstat)
+    int n_tiles, int n_bins, int prn_offset, RowSpec rs, int M, int P, RowStat* __restrict__ rowstat)
 {
     __shared__ MaxIdx red_m[kAcqThreads / 64];
     __shared__ float red_s[kAcqThreads / 64];
+    __shared__ int flag_list[kHugeFlagMax];
+    __shared__ int n_flag;
     const int64_t cell = static_cast<int64_t>(blockIdx.y) * n_bins + blockIdx.x;
     const TileStat* ts = tiles + cell * n_tiles;
+    if (threadIdx.x == 0) n_flag = 0;
     MaxIdx m{-1.0f, 0x7fffffff};
     float s = 0.0f;
     for (int i = threadIdx.x; i < n_tiles; i += kAcqThreads) {
         m = better(m, MaxIdx{ts[i].max, ts[i].argmax});
         s += ts[i].sum;
     }
-    block_argmax_sum<kAcqThreads / 64>(m, s, red_m, red_s);
+    block_argmax_sum<kAcqThreads / 64>(m, s, red_m, red_s);  // its barriers also publish n_flag = 0
     const MaxIdx best = m;
     const float sum = s;
     int e1 = best.i - rs.spc, e2 = best.i + rs.spc;
     if (e1 < 0) e1 += rs.win_mod; else if (e2 >= rs.win_mod) e2 -= rs.win_mod;
-    const float* g = grid + cell * rs.row_len;
-    MaxIdx m2{0.0f, 0x7fffffff};
-    for (int i = threadIdx.x; i < rs.row_len; i += kAcqThreads) {
-        const bool in_win = (e1 < e2) ? (i >= e1 && i < e2) : (i >= e1 || i < e2);
-        m2 = better(m2, MaxIdx{in_win ? 0.0f : g[i], i});
+    // the window as one or two row-index intervals
+    const int w0a = e1 < e2 ? e1 : e1, w0b = e1 < e2 ? e2 : rs.win_mod;
+    const int w1a = 0, w1b = e1 < e2 ? 0 : e2;
+    float v2 = 0.0f;  // max(0, …): the reference's second peak starts from 0
+    for (int i = threadIdx.x; i < n_tiles; i += kAcqThreads) {
+        const int lo = i * kHugeColThreads, hi = min(M, lo + kHugeColThreads);
+        bool meets = false;
+        for (int q = 0; q < P; q++) {
+            const int a0 = max(0, lo + M * q - rs.row_off), a1 = min(rs.row_len, hi + M * q - rs.row_off);
+            if (a0 < a1 && (interval_meets(a0, a1, w0a, w0b) || interval_meets(a0, a1, w1a, w1b))) meets = true;
+        }
+        if (meets) {
+            const int k = atomicAdd(&n_flag, 1);
+            if (k < kHugeFlagMax) flag_list[k] = i;
+        } else {
+            v2 = fmaxf(v2, ts[i].max);
+        }
     }
-    const MaxIdx second = block_argmax<kAcqThreads / 64>(m2, red_m);
-    if (threadIdx.x == 0) rowstat[(static_cast<int64_t>(prn_offset) + blockIdx.y) * n_bins + blockIdx.x] = RowStat{best.v, best.i, sum, second.v};
+    __syncthreads();
+    const float* g = grid + cell * rs.row_len;
+    auto in_win = [&](int i) { return (e1 < e2) ? (i >= e1 && i < e2) : (i >= e1 || i < e2); };
+    const int nf = n_flag;
+    if (nf <= kHugeFlagMax) {
+        for (int f = 0; f < nf; f++) {
+            const int lo = flag_list[f] * kHugeColThreads;
+            for (int j = threadIdx.x; j < kHugeColThreads * P; j += kAcqThreads) {
+                const int mm = lo + j % kHugeColThreads, q = j / kHugeColThreads;
+                const int n = mm + M * q - rs.row_off;
+                if (mm < M && n >= 0 && n < rs.row_len && !in_win(n)) v2 = fmaxf(v2, g[n]);
+            }
+        }
+    } else {  // more tiles met than listed: scan the whole row
+        for (int i = threadIdx.x; i < rs.row_len; i += kAcqThreads)
+            if (!in_win(i)) v2 = fmaxf(v2, g[i]);
+    }
+    const float second = block_max<kAcqThreads / 64>(v2, red_s);
+    if (threadIdx.x == 0) rowstat[(static_cast<int64_t>(prn_offset) + blockIdx.y) * n_bins + blockIdx.x] = RowStat{best.v, best.i, sum, second};
 }
 
 #define GNSSHIP_HUGE_P_LIST(X) X(4) X(5) X(8) X(10) X(16) X(20) X(25) X(32)
@@ -1309,7 +1350,7 @@ hipError_t launch_acq_search_huge(const float2* XT, const float2* codesT, int pr
     e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(acq_huge_finalize_kernel, dim3(n_bins, n_prns), dim3(kAcqThreads), 0, stream, grid, tiles, n_tiles, n_bins, prn_offset, rs,
-        rowstat);
+        M, P, rowstat);
     return hipGetLastError();
 }
 
