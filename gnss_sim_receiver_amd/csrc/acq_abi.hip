@@ -42,6 +42,12 @@ bool choose_acq_layout(int n, int force, FftPlan& plan, int& P, bool& huge)
 {
     P = 0;
     huge = false;
+    // The four-step with a compile-time plan in small workgroups beats the single-workgroup LDS
+    // transform at the C1 size (1 ms of GPS at 4 Msps: 4000 = 16 × 250).
+    if (force == 0 && n == 4000 && make_fft_plan(250, plan)) {
+        P = 16;
+        return true;
+    }
     if (force == 0 && make_fft_plan(n, plan)) return true;
     if (force != 2 && n >= 2 && n <= kMaxAcqBigN) {
         for (int p = 16; p <= 32; p++) {

@@ -1422,6 +1422,8 @@ hipError_t launch_acq_fft_big(const void* sig, int fmt, const float2* mult, int 
     const dim3 rgrid((rows_total + kBigRowWaves - 1) / kBigRowWaves);
     if (M == 1000)  // C3: N = 25000 (GPS 1 ms at 25 Msps), compile-time row plan
         hipLaunchKernelGGL((acq_fft_big_rows_kernel<1000>), rgrid, dim3(kBigRowWaves * 64), lds, stream, row_plan, P, tw, rowsT, rows_total, conj_out);
+    else if (M == 250)  // C1: N = 4000 (GPS 1 ms at 4 Msps) as 16 × 250
+        hipLaunchKernelGGL((acq_fft_big_rows_kernel<250>), rgrid, dim3(kBigRowWaves * 64), lds, stream, row_plan, P, tw, rowsT, rows_total, conj_out);
     else
         hipLaunchKernelGGL((acq_fft_big_rows_kernel<0>), rgrid, dim3(kBigRowWaves * 64), lds, stream, row_plan, P, tw, rowsT, rows_total, conj_out);
     return hipGetLastError();
@@ -1436,6 +1438,13 @@ hipError_t launch_acq_search_big(const float2* XT, const float2* codesT, int n_p
         constexpr int kB = col_split(1000);
         const size_t lds_c3 = lds + sizeof(float2) * static_cast<size_t>(kB * 25 + (1000 / kB) * 25);
         hipLaunchKernelGGL((acq_search_big_kernel<25, 1000>), dim3(n_bins, n_prns), dim3(kAcqThreads), lds_c3, stream, XT, codesT, row_plan, tw, n_bins,
+            rs, accumulate, rowstat, grid);
+        return hipGetLastError();
+    }
+    if (P == 16 && row_plan.n == 250) {  // C1: N = 4000 in 256-thread workgroups (several per CU)
+        constexpr int kNT = 256, kB = col_split(250);
+        const size_t lds_c1 = (static_cast<size_t>(kNT / 64) + 1) * sizeof(float2) * 250 + sizeof(float2) * static_cast<size_t>(kB * 16 + (250 / kB) * 16);
+        hipLaunchKernelGGL((acq_search_big_kernel<16, 250, kNT>), dim3(n_bins, n_prns), dim3(kNT), lds_c1, stream, XT, codesT, row_plan, tw, n_bins,
             rs, accumulate, rowstat, grid);
         return hipGetLastError();
     }
