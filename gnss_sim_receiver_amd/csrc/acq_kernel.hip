@@ -195,6 +195,53 @@ __device__ void fft_lds(float2* __restrict__ buf, const FftPlan& plan, const flo
     }
 }
 
+// fft_lds with the length known at compile time (ct_radix order: radix 10 where it divides, then
+// odd radices): constant index arithmetic, every pass's butterflies unrolled, fewer passes
+// (12500 = 10·10·5·5·5: five instead of six).  Twiddles tw[k·r·tstep] from the M-entry table.
+constexpr int ct_radix(int m);
+template <int MC, int NsC, int SIGN>
+__device__ __forceinline__ void fft_lds_ct(float2* __restrict__ buf, const float2* __restrict__ tw)
+{
+    if constexpr (NsC < MC) {
+        constexpr int R = ct_radix(MC / NsC);
+        constexpr int nb = MC / R;
+        constexpr int tstep = MC / (NsC * R);
+        constexpr int MAXB = (nb + kAcqThreads - 1) / kAcqThreads;
+        float2 v[MAXB][R];
+#pragma unroll
+        for (int c = 0; c < MAXB; c++) {
+            const int j = threadIdx.x + c * kAcqThreads;
+            if (j < nb) {
+                const int k = j % NsC;
+#pragma unroll
+                for (int r = 0; r < R; r++) {
+                    float2 x = buf[j + r * nb];
+                    if (r > 0 && NsC > 1) {
+                        float2 w = tw[k * r * tstep];
+                        if (SIGN > 0) w.y = -w.y;
+                        x = cmulf(x, w);
+                    }
+                    v[c][r] = x;
+                }
+                dft_small<R, SIGN>(v[c]);
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int c = 0; c < MAXB; c++) {
+            const int j = threadIdx.x + c * kAcqThreads;
+            if (j < nb) {
+                const int k = j % NsC;
+                const int base = (j / NsC) * NsC * R + k;
+#pragma unroll
+                for (int r = 0; r < R; r++) buf[base + r * NsC] = v[c][r];
+            }
+        }
+        __syncthreads();
+        fft_lds_ct<MC, NsC * R, SIGN>(buf, tw);
+    }
+}
+
 // Transforms of up to kTwLdsMax points read their twiddles from LDS: the N-entry table is staged
 // next to the data once per workgroup (every Stockham pass otherwise waits on L2 for its R − 1
 // twiddle loads, with only one or two butterflies per thread to hide them).
@@ -1145,7 +1192,7 @@ __global__ __launch_bounds__(kHugeColThreads) void acq_huge_cols_fwd_kernel(cons
 // One LDS-resident M-point transform per block: row blockIdx.x of cell (blockIdx.y, blockIdx.z).
 // src row = A + y·a_sy + z·a_sz + x·M (times B + z·b_sz + y·b_sy + x·M when B is given);
 // dst row = D + y·d_sy + z·d_sz + x·M.  conj_out stores the conjugate (the code spectrum).
-template <int SIGN>
+template <int SIGN, int MC = 0>
 __global__ __launch_bounds__(kAcqThreads) void acq_huge_rows_kernel(const float2* __restrict__ A, int64_t a_sy, int64_t a_sz,
     const float2* __restrict__ B, int64_t b_sy, int64_t b_sz, float2* __restrict__ D, int64_t d_sy, int64_t d_sz, FftPlan plan,
     const float2* __restrict__ twM, int conj_out)
@@ -1157,7 +1204,8 @@ __global__ __launch_bounds__(kAcqThreads) void acq_huge_rows_kernel(const float2
     const float2* bb = B ? B + blockIdx.y * b_sy + blockIdx.z * b_sz + row : nullptr;
     lds_load_prod(lds, a, bb, M, threadIdx.x, kAcqThreads);  // ×conj(code FFT)
     __syncthreads();
-    fft_lds<SIGN>(lds, plan, twM);
+    if constexpr (MC > 0) fft_lds_ct<MC, 1, SIGN>(lds, twM);
+    else fft_lds<SIGN>(lds, plan, twM);
     float2* d = D + blockIdx.y * d_sy + blockIdx.z * d_sz + row;
     for (int i = threadIdx.x; i < M; i += kAcqThreads) {
         float2 y = lds[i];
@@ -1318,8 +1366,12 @@ hipError_t launch_acq_fft_huge(const void* sig, int fmt, const float2* mult, int
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     const size_t lds = sizeof(float2) * static_cast<size_t>(M);
-    hipLaunchKernelGGL(acq_huge_rows_kernel<-1>, dim3(P, n_rows, 1), dim3(kAcqThreads), lds, stream, scratch, N, int64_t(0),
-        static_cast<const float2*>(nullptr), int64_t(0), int64_t(0), rowsT, N, int64_t(0), row_plan, twM, conj_out);
+    if (M == 12500)  // Galileo E1 at 25 Msps (N = 100000 = 8 × 12500), GPS/B1I at 50 Msps: compile-time plan
+        hipLaunchKernelGGL((acq_huge_rows_kernel<-1, 12500>), dim3(P, n_rows, 1), dim3(kAcqThreads), lds, stream, scratch, N, int64_t(0),
+            static_cast<const float2*>(nullptr), int64_t(0), int64_t(0), rowsT, N, int64_t(0), row_plan, twM, conj_out);
+    else
+        hipLaunchKernelGGL((acq_huge_rows_kernel<-1>), dim3(P, n_rows, 1), dim3(kAcqThreads), lds, stream, scratch, N, int64_t(0),
+            static_cast<const float2*>(nullptr), int64_t(0), int64_t(0), rowsT, N, int64_t(0), row_plan, twM, conj_out);
     return hipGetLastError();
 }
 
@@ -1331,8 +1383,12 @@ hipError_t launch_acq_search_huge(const float2* XT, const float2* codesT, int pr
     const int64_t N = static_cast<int64_t>(P) * M;
     const size_t lds = sizeof(float2) * static_cast<size_t>(M);
     // rows: blockIdx.y = bin (XT row set), blockIdx.z = prn (code spectrum), U cell = z·n_bins + y
-    hipLaunchKernelGGL(acq_huge_rows_kernel<+1>, dim3(P, n_bins, n_prns), dim3(kAcqThreads), lds, stream, XT, N, int64_t(0),
-        codesT + static_cast<int64_t>(prn_offset) * N, int64_t(0), N, U, N, N * n_bins, row_plan, twM, 0);
+    if (M == 12500)
+        hipLaunchKernelGGL((acq_huge_rows_kernel<+1, 12500>), dim3(P, n_bins, n_prns), dim3(kAcqThreads), lds, stream, XT, N, int64_t(0),
+            codesT + static_cast<int64_t>(prn_offset) * N, int64_t(0), N, U, N, N * n_bins, row_plan, twM, 0);
+    else
+        hipLaunchKernelGGL((acq_huge_rows_kernel<+1>), dim3(P, n_bins, n_prns), dim3(kAcqThreads), lds, stream, XT, N, int64_t(0),
+            codesT + static_cast<int64_t>(prn_offset) * N, int64_t(0), N, U, N, N * n_bins, row_plan, twM, 0);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     const int n_tiles = (M + kHugeColThreads - 1) / kHugeColThreads;
