@@ -15,14 +15,16 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np  # noqa: E402
 
 import bench  # noqa: E402
-from gnss_sim_receiver_amd import abi, engine  # noqa: E402
+from gnss_sim_receiver_amd import abi, engine, signals  # noqa: E402
 
 
 def main():
     os.environ.setdefault("GNSSHIP_LIB_PATH", os.path.join(os.path.dirname(os.path.abspath(__file__)), "libgnsship_prof.so"))
     lib = abi.load()
     lib.gnsship_debug_corr_profile.argtypes = [ctypes.c_void_p]
-    sats, block, n = bench.build_block(1.0)
+    sats = signals.random_sky(bench.N_SATS, seed=bench.SEED)  # the bench's open-loop block
+    n = bench.FS + 2 * bench.VL
+    block = np.ascontiguousarray(signals.generate_if(bench.FS, n, sats, seed=bench.SEED))
     ctx = engine.Context(0)
     jobs, codes = bench.receiver_jobs(sats, 0, 1.0)
     for cid, c in enumerate(codes):
