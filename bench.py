@@ -447,7 +447,13 @@ def receiver_jobs(sats, rank: int, seconds: float):
     return jobs, codes
 
 
-def open_loop_correlator(ctx, torch, device, steps=20):
+def job_flags(rot):
+    """Batch job flag for the rotator variant (GNSSHIP_JOB_ROTATOR_AVX when volk would dispatch AVX)."""
+    from gnss_sim_receiver_amd import abi
+    return abi.JOB_ROTATOR_AVX if rot == abi.ROTATOR_AVX else 0
+
+
+def open_loop_correlator(ctx, torch, device, steps=20, rot=0):
     """Round 1's headline, kept as an auxiliary line: 12 000 channel-epochs of one second with
     synthetic-truth NCOs (no loop filters) as one batched launch, three receivers in a ring."""
     from gnss_sim_receiver_amd import abi, engine, signals
@@ -459,6 +465,7 @@ def open_loop_correlator(ctx, torch, device, steps=20):
     for k in range(N_RING):
         jk, ck = receiver_jobs(sats, k, 1.0)
         jk["code_id"] += 32 * k
+        jk["flags"] = job_flags(rot)
         for cid, c in enumerate(ck):
             ctx.set_code(32 * k + cid, c)
         b = engine.CorrelatorBatch(ctx, len(jk))
@@ -494,7 +501,7 @@ def open_loop_correlator(ctx, torch, device, steps=20):
     jobs = N_CH * 1000
     byts = jobs * (8 * VL + 3 * 8)
     return {"config": "12 GPS L1 C/A channels x 1000 epochs (1 s, 4 Msps), synthetic-truth NCOs, one batched launch per "
-                      "receiver-second, 3 receivers in a ring (gnsship_batch_launch_pipelined2)",
+                      "receiver-second, 3 receivers in a ring (gnsship_batch_launch_pipelined2), rotator " + rotator_name(rot),
             "if_msamples_per_s": round(FS * steps / wall / 1e6, 1), "ms_per_launch": round(ms, 4),
             "split_ms_per_launch": split,
             "channel_msamples_per_s": round(jobs * VL / (ms * 1e-3) / 1e6, 1),
@@ -559,7 +566,7 @@ def acq_e1_bench(ctx, reps=5):
     return out
 
 
-def e1_open_loop(ctx, seconds=0.2, reps=10):
+def e1_open_loop(ctx, seconds=0.2, reps=10, rot=0):
     from gnss_sim_receiver_amd import abi, engine, signals as S
     fs, vl, nch = 25e6, 100000, 8
     sats = S.random_sky(nch, seed=SEED + 4, system="GAL", prns=[1, 5, 12, 19, 24, 30, 33, 36])
@@ -576,6 +583,7 @@ def e1_open_loop(ctx, seconds=0.2, reps=10):
         ctx.set_code(100 + 2 * k, s.code)
         ctx.set_code(100 + 2 * k + 1, s.code_data)
     jobs = np.concatenate(jobs)
+    jobs["flags"] = job_flags(rot)
     dev = ctx.upload(sig)
     ring = []
     for _ in range(3):
@@ -596,12 +604,12 @@ def e1_open_loop(ctx, seconds=0.2, reps=10):
     dev.free()
     if_msps = n_ep * vl / (ms * 1e-3) / 1e6
     return {"config": "C4 per-GPU share, open loop (truth NCOs): Galileo E1, 8 ch, 25 Msps, N=100000, 5 pilot taps + 1 data tap, "
-                      f"gr_complex, {seconds} s block, 3 batches in a ring",
+                      f"gr_complex, {seconds} s block, 3 batches in a ring, rotator " + rotator_name(rot),
             "ms_per_signal_second": round(ms / seconds, 4), "if_msamples_per_s": round(if_msps, 1),
             "realtime_factor": round(if_msps * 1e6 / fs, 1), "algorithmic_GBps": round(2 * nch * n_ep * vl * 8 / (ms * 1e-3) / 1e9, 1)}
 
 
-def c5_open_loop(ctx, seconds=0.2, reps=6):
+def c5_open_loop(ctx, seconds=0.2, reps=6, rot=0):
     from gnss_sim_receiver_amd import abi, engine, signals as S
     fs, f_if = 50e6, 7.161e6
     sys_conf = (("GPS", 12, 50000, [-0.25, 0.0, 0.25], 1000), ("GAL", 12, 200000, [-1.0, -0.5, 0.0, 0.5, 1.0], 250),
@@ -628,6 +636,7 @@ def c5_open_loop(ctx, seconds=0.2, reps=6):
             if k == 0:
                 present += sats[:2]
         receivers.append(np.concatenate(jobs))
+        receivers[-1]["flags"] = job_flags(rot)
     n = int(round(fs * seconds)) + 400000
     block = S.to_ibyte(S.generate_if(fs, n, present, seed=SEED + 5))
     dev = ctx.upload(block)
@@ -652,7 +661,7 @@ def c5_open_loop(ctx, seconds=0.2, reps=6):
     span_s = seconds - 2 * 0.004
     rt = span_s / (ms * 1e-3)
     return {"config": "C5 per-GPU share, open loop (truth NCOs): 12 GPS L1 C/A + 12 Galileo E1 (5+1 taps) + 8 BeiDou B1I, "
-                      f"50 Msps ibyte, {seconds} s block, 3 receivers in a ring",
+                      f"50 Msps ibyte, {seconds} s block, 3 receivers in a ring, rotator " + rotator_name(rot),
             "ms_per_block": round(ms, 4), "realtime_factor": round(rt, 1),
             "if_msamples_per_s": round(fs * span_s / (ms * 1e-3) / 1e6, 1),
             "channel_msamples_per_s": round(chan_samples / (ms * 1e-3) / 1e6, 1),
@@ -763,7 +772,7 @@ def main():
         result["closed_loop_e1_25msps_c4_share"] = closed_loop_aux(ctx, torch, device, "GAL", 25e6, 100000, 8, 0.4, h["rotator"], SEED + 12)
         if world == 1 and args.cpu_seconds > 0:
             result["cpu_baseline"] = cpu_baseline(h, args.cpu_seconds)
-        result["open_loop_correlator"] = open_loop_correlator(ctx, torch, device)
+        result["open_loop_correlator"] = open_loop_correlator(ctx, torch, device, rot=h["rotator"])
         from gnss_sim_receiver_amd import signals as S
         sky = S.random_sky(N_SATS, seed=SEED)
         blk = S.generate_if(FS, VL, sky, seed=SEED)
@@ -771,8 +780,8 @@ def main():
         result["acquisition_e1"] = acq_e1_bench(ctx)
         if world == 1:
             result["c1_receiver"] = c1_receiver(torch, device, cpu_seconds=1.0 if args.cpu_seconds > 0 else 0.0)
-        result["tracking_c4_e1_open_loop"] = e1_open_loop(ctx)
-        result["tracking_c5_hybrid_open_loop"] = c5_open_loop(ctx)
+        result["tracking_c4_e1_open_loop"] = e1_open_loop(ctx, rot=h["rotator"])
+        result["tracking_c5_hybrid_open_loop"] = c5_open_loop(ctx, rot=h["rotator"])
     del h
     if rank == 0:
         print(json.dumps(result), flush=True)

@@ -21,6 +21,69 @@ __device__ __forceinline__ int segment_block(int seg, int nblk, int n_segs = kAn
 // segments [seg_lo, seg_hi).  Block k stores the renormalised q_k and the chain's next three phasors
 // q_k·inc, q_k·inc², q_k·inc³ (engine.h Anchor).  A later segment resumes from the stored q of the
 // block before it: the chain after a renormalisation depends only on q.
+typedef float f2v __attribute__((ext_vector_type(2)));
+
+// The reference's complex<float> product a·b written out (re = ar·br − ai·bi, im = ar·bi + ai·br),
+// each product rounded separately (no FMA).
+__device__ __forceinline__ f2v avx_cmul(f2v a, f2v b) { return f2v{a.x, a.x} * b + f2v{a.y, a.y} * f2v{-b.y, b.x}; }
+
+// _mm256_complexnormalise_ps (volk_gnsssdr_avx_intrinsics.h:56-63): z / sqrt(re² + im²).
+__device__ __forceinline__ f2v avx_normalise(f2v z)
+{
+    const float m = __fsqrt_rn(__fadd_rn(__fmul_rn(z.x, z.x), __fmul_rn(z.y, z.y)));
+    return f2v{__fdiv_rn(z.x, m), __fdiv_rn(z.y, m)};
+}
+
+// Anchors of the AVX rotator variant (volk_gnsssdr_32fc_32f_rotator_dot_prod_32fc_xn_u_avx,
+// volk_gnsssdr_32fc_32f_rotator_dot_prod_32fc_xn.h:155-316):
+// 16 phasors z_l = phase·inc^l (generic chain), iteration m (samples 16m..16m+15) uses z_l and then
+// advances z_l ← z_l·dz with dz = normalise(inc^16 by four squarings), renormalising after the
+// update of iterations m ≡ 0 (mod 64).  Block k (samples 256k..) starts at iteration 16k; its anchor
+// holds z_0..z_3 there, so only lanes 0-3 are replayed: four independent chains of N/16 steps
+// instead of one of N.  Inside a block the correlation applies the lane factor E_{4t} as for the
+// generic variant (|dz| = 1: no magnitude term).  The N mod 16 tail (serial from normalise(z_0))
+// falls inside the last block's E_{4t} approximation.
+__device__ __forceinline__ void replay_anchors_avx(const DevJob& job, Anchor* __restrict__ out, int kb, int ke)
+{
+    const f2v inc = f2v{job.inc_re, job.inc_im};
+    f2v dz = inc;
+#pragma unroll
+    for (int q = 0; q < 4; q++) dz = avx_cmul(dz, dz);  // (:221-225)
+    dz = avx_normalise(dz);
+    f2v z[4];
+    if (kb == 0) {
+        z[0] = f2v{job.p0_re, job.p0_im};
+#pragma unroll
+        for (int l = 1; l < 4; l++) z[l] = avx_cmul(z[l - 1], inc);
+    } else {
+#pragma unroll
+        for (int l = 0; l < 4; l++) z[l] = f2v{out[kb - 1].p[2 * l], out[kb - 1].p[2 * l + 1]};
+    }
+    for (int k = (kb == 0 ? kb : kb - 1); k < ke; k++) {
+        if (k >= kb) {
+            Anchor A;
+#pragma unroll
+            for (int l = 0; l < 4; l++) {
+                A.p[2 * l] = z[l].x;
+                A.p[2 * l + 1] = z[l].y;
+            }
+            out[k] = A;
+            if (k == ke - 1) break;
+        }
+        // iterations 16k .. 16k+15: z ← z·dz, normalised after m ≡ 0 (mod 64) (:265-272)
+        const int m = 16 * k;
+#pragma unroll
+        for (int i = 0; i < 16; i++) {
+#pragma unroll
+            for (int l = 0; l < 4; l++) z[l] = avx_cmul(z[l], dz);
+            if (i == 0 && (m & 63) == 0) {
+#pragma unroll
+                for (int l = 0; l < 4; l++) z[l] = avx_normalise(z[l]);
+            }
+        }
+    }
+}
+
 __device__ __forceinline__ void replay_anchors(const DevJob& job, Anchor* __restrict__ anchors, int seg_lo, int seg_hi,
     int n_segs = kAnchorSegments)
 {
@@ -28,7 +91,10 @@ __device__ __forceinline__ void replay_anchors(const DevJob& job, Anchor* __rest
     const int kb = segment_block(seg_lo, nblk, n_segs), ke = segment_block(seg_hi, nblk, n_segs);
     if (kb >= ke) return;
     Anchor* out = anchors + job.anchor_offset;
-    typedef float f2v __attribute__((ext_vector_type(2)));
+    if (job.rot_avx) {
+        replay_anchors_avx(job, out, kb, ke);
+        return;
+    }
     // phase·inc = (pr·ir − pi·ii, pr·ii + pi·ir) as two packed products + one packed add, each
     // rounded separately like the reference's written-out complex product (no FMA).  The sign
     // sits in the constant: fl(pi·(−ii)) = −fl(pi·ii) and x + (−y) ≡ x − y, bit for bit.

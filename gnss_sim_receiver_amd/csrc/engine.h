@@ -44,6 +44,7 @@ struct DevJob {
     float rem_code;         // rem_code_phase_chips  (float, as passed by the reference)
     float code_step;        // code_phase_step_chips
     int32_t in_margin;      // 1: every chip index of the job lies in [−kCodeMargin, L + kCodeMargin)
+    int32_t rot_avx;        // 1: anchors from the AVX rotator recursion (GNSSHIP_JOB_ROTATOR_AVX), 0: generic
     float shifts[kMaxTaps];
 };
 

@@ -82,6 +82,9 @@ bool derive_job(const gnsship_corr_job& in, int code_len, DevJob& out)
     out.inc_im = inci;
     out.dtheta = std::atan2(static_cast<double>(inci), static_cast<double>(incr));
     out.log_mag_inc = static_cast<float>(std::log(std::hypot(static_cast<double>(incr), static_cast<double>(inci))));
+    // AVX variant: the phasors advance by the normalised dz = inc^16, so no magnitude drift inside a block
+    out.rot_avx = (in.flags & GNSSHIP_JOB_ROTATOR_AVX) ? 1 : 0;
+    if (out.rot_avx) out.log_mag_inc = 0.0f;
     out.rem_code = in.rem_code_phase_chips;
     out.code_step = in.code_phase_step_chips;
     for (int t = 0; t < kMaxTaps; t++) out.shifts[t] = (t < in.n_taps) ? in.shifts_chips[t] : 0.0f;
@@ -452,7 +455,7 @@ extern "C" int gnsship_batch_set_jobs(gnsship_batch* b, const gnsship_corr_job* 
         const gnsship_corr_job& in = jobs[j];
         if (in.code_id < 0 || in.code_id >= static_cast<int>(ctx->codes_host.size()) || !ctx->codes_host[in.code_id].ptr)
             return fail(ctx, GNSSHIP_E_INVAL, "gnsship_batch_set_jobs: job refers to an unset code id");
-        if (in.flags & ~1) return fail(ctx, GNSSHIP_E_INVAL, "gnsship_batch_set_jobs: unknown job flags");
+        if (in.flags & ~(GNSSHIP_JOB_HIGH_DYN | GNSSHIP_JOB_ROTATOR_AVX)) return fail(ctx, GNSSHIP_E_INVAL, "gnsship_batch_set_jobs: unknown job flags");
         if (in.flags & 1) {  // high-dynamics resampler/rotator: its own plan, an empty slot here
             HdJob h;
             if (!derive_hd_job(in, ctx->codes_host[in.code_id].ptr, ctx->codes_host[in.code_id].len, j, h))

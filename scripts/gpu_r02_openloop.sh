@@ -9,8 +9,11 @@ timeout -k 10 200 python3 -u -c "
 import json, torch, bench
 from gnss_sim_receiver_amd import engine
 ctx = engine.Context(0)
-for rep in range(3):
-    print(json.dumps(bench.open_loop_correlator(ctx, torch, 0, steps=60)), flush=True)
+for rot in (0, 1, 0, 1):
+    print(json.dumps(bench.open_loop_correlator(ctx, torch, 0, steps=60, rot=rot)), flush=True)
+for rot in (0, 1):
+    print(json.dumps(bench.e1_open_loop(ctx, rot=rot)), flush=True)
+    print(json.dumps(bench.c5_open_loop(ctx, rot=rot)), flush=True)
 " > $O/split.jsonl 2> $O/split.err || { echo "split failed"; tail -20 $O/split.err; exit 1; }
 cat $O/split.jsonl
 for mode in pipelined split; do

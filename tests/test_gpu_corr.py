@@ -263,3 +263,71 @@ def test_pipelined_ring_of_three_split_replay(ctx):
     for b in batches:
         b.close()
     dev.free()
+
+
+@pytest.mark.parametrize("fs,ntaps,system", [(4e6, 3, "GPS"), (25e6, 3, "GPS"), (25e6, 5, "GPS"), (50e6, 3, "BDS")])
+def test_batch_avx_rotator_vs_oracle(ctx, fs, ntaps, system):
+    """GNSSHIP_JOB_ROTATOR_AVX jobs (the variant volk_gnsssdr dispatches on AVX hosts,
+    volk_gnsssdr_32fc_32f_rotator_dot_prod_32fc_xn.h:155-316) against the oracle's AVX restatement:
+    N = 4000, 25000 (N mod 16 = 8: the serial tail), 50000; mixed with generic jobs in one batch."""
+    rng = np.random.default_rng(int(fs) + 7 * ntaps)
+    sats = signals.random_sky(6, seed=int(fs) % 7919, system=system)
+    vl = int(round(fs / 1000))
+    n_ep = 3
+    sig = signals.generate_if(fs, vl * (n_ep + 3), sats, seed=ntaps + 11)
+    shifts = {3: [-0.25, 0.0, 0.25], 5: [-0.5, -0.25, 0.0, 0.25, 0.5]}[ntaps]
+    jobs = np.concatenate([signals.truth_jobs(s, fs, n_ep, vl, shifts, k) for k, s in enumerate(sats)])
+    cl = [s.code for s in sats]
+    jobs["rem_carrier_phase_rad"] += rng.uniform(-0.3, 0.3, len(jobs)).astype(np.float32)
+    jobs["flags"][::3] = 0
+    jobs["flags"][1::3] = abi.JOB_ROTATOR_AVX
+    jobs["flags"][2::3] = abi.JOB_ROTATOR_AVX
+    out = engine.correlate_host(ctx, sig, jobs, cl)
+    ref = O.corr_batch(sig, jobs, cl, n_threads=8)
+    for j in range(len(jobs)):
+        t = jobs[j]["n_taps"]
+        e = rel_err(out[j, :t], ref[j, :t])
+        assert e <= TOL, (j, int(jobs[j]["flags"]), e)
+    # the two variants really differ in the oracle (the flag reaches it) by less than the tolerance
+    gen = jobs.copy()
+    gen["flags"] = 0
+    ref_gen = O.corr_batch(sig, gen, cl, n_threads=8)
+    avx = jobs["flags"] == abi.JOB_ROTATOR_AVX
+    assert not np.array_equal(ref[avx], ref_gen[avx])
+
+
+def test_pipelined_ring_avx_jobs_match_plain_launches(ctx):
+    """AVX-variant jobs through the pipelined ring (replay split at the middle block, resumed from the
+    stored four phasors) give exactly the plain launch results; odd block counts and one-block jobs."""
+    fs = 4e6
+    sats = signals.random_sky(6, seed=61)
+    sig = signals.generate_if(fs, 4000 * 30, sats, seed=62)
+    dev = ctx.upload(sig)
+    for k, s in enumerate(sats):
+        ctx.set_code(k, s.code)
+    ja = np.concatenate([signals.truth_jobs(s, fs, 10, 4000, [-0.25, 0.0, 0.25], k) for k, s in enumerate(sats[:2])])
+    jb = np.concatenate([signals.truth_jobs(s, fs, 8, 3001, [-0.5, 0.0, 0.5], k + 2, first_epoch=5) for k, s in enumerate(sats[2:4])])
+    jc = np.concatenate([signals.truth_jobs(s, fs, 6, 4000, [0.0], k + 4, first_epoch=3) for k, s in enumerate(sats[4:])])
+    jc["n_samples"][::3] = 200
+    jc["n_samples"][1::3] = 1300
+    for j in (ja, jb, jc):
+        j["flags"] = abi.JOB_ROTATOR_AVX
+    sets = [ja, jb, jc]
+    batches = [engine.CorrelatorBatch(ctx, len(j)) for j in sets]
+    refs = []
+    for b, j in zip(batches, sets):
+        b.set_jobs(j, len(sig))
+        b.launch_ptr(dev.ptr)
+        refs.append(b.results())
+    for rnd in range(7):
+        k = rnd % 3
+        batches[k].launch_pipelined(dev.ptr, next_batch=batches[(k + 1) % 3], next2=batches[(k + 2) % 3])
+        assert np.array_equal(batches[k].results(), refs[k]), rnd
+    for k, j in enumerate(sets):
+        ref = O.corr_batch(sig, j, [s.code for s in sats], n_threads=8)
+        for i in range(len(j)):
+            t = j[i]["n_taps"]
+            assert rel_err(refs[k][i, :t], ref[i, :t]) <= TOL, (k, i)
+    for b in batches:
+        b.close()
+    dev.free()
