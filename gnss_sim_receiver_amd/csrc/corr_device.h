@@ -175,17 +175,21 @@ __device__ __forceinline__ void load_any(i4v span, int lane, int kb, int len, f2
 }
 
 // E_j = |inc|^j · e^{i j Δ} for this lane's j = 4·lane (angle formed and range-reduced in double,
-// hardware sin/cos in revolutions — E_j to a few 1e-7, against the 1e-5 tolerance).
+// hardware sin/cos in revolutions — E_j to a few 1e-7, against the 1e-5 tolerance).  AVX-variant
+// jobs advance by dz per 16 samples: angle (j/16)·arg(dz) + (j mod 16)·Δ (16·Δ differs from arg(dz)
+// by the squarings' rounding, ≈ 1e-6 rad, which would grow to ≈ 2e-5 over a block).
 __device__ __forceinline__ f2 lane_rotation(const DevJob& job, int j)
 {
     constexpr double kInvTwoPi = 0.15915494309189533576888376337251;
+    const double ang = job.rot_avx ? static_cast<double>(j >> 4) * job.dtheta_dz + static_cast<double>(j & 15) * job.dtheta
+                                   : static_cast<double>(j) * job.dtheta;
 #ifndef GNSSHIP_EJ_LIBM
-    const double rev = static_cast<double>(j) * (job.dtheta * kInvTwoPi);
+    const double rev = ang * kInvTwoPi;
     const float rf = static_cast<float>(rev - rint(rev));
     const float s = __builtin_amdgcn_sinf(rf), c = __builtin_amdgcn_cosf(rf);
 #else
     constexpr double kTwoPi = 6.283185307179586476925286766559;
-    double th = static_cast<double>(j) * job.dtheta;
+    double th = ang;
     th = fma(-kTwoPi, rint(th * kInvTwoPi), th);
     float s, c;
     sincosf(static_cast<float>(th), &s, &c);

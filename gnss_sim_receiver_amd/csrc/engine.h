@@ -40,6 +40,7 @@ struct DevJob {
     float p0_re, p0_im;     // phase_offset_as_complex
     float inc_re, inc_im;   // phase_inc
     double dtheta;          // arg(phase_inc) in double (exact angle of the float phasor)
+    double dtheta_dz;       // rot_avx: arg(dz), dz = normalise(phase_inc^16) as the AVX recursion forms it
     float log_mag_inc;      // log|phase_inc| (magnitude growth between renormalisations)
     float rem_code;         // rem_code_phase_chips  (float, as passed by the reference)
     float code_step;        // code_phase_step_chips

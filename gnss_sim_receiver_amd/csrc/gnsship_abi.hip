@@ -84,7 +84,22 @@ bool derive_job(const gnsship_corr_job& in, int code_len, DevJob& out)
     out.log_mag_inc = static_cast<float>(std::log(std::hypot(static_cast<double>(incr), static_cast<double>(inci))));
     // AVX variant: the phasors advance by the normalised dz = inc^16, so no magnitude drift inside a block
     out.rot_avx = (in.flags & GNSSHIP_JOB_ROTATOR_AVX) ? 1 : 0;
-    if (out.rot_avx) out.log_mag_inc = 0.0f;
+    out.dtheta_dz = 0.0;
+    if (out.rot_avx) {
+        out.log_mag_inc = 0.0f;
+        // dz exactly as replay_anchors_avx forms it (four written-out float squarings, IEEE sqrt and
+        // division): the lane factor advances by arg(dz) per 16 samples, not 16·arg(inc)
+        float dr = incr, di = inci;
+        for (int q = 0; q < 4; q++) {
+            const float a = dr * dr, b = di * di, c = dr * di, d = di * dr;
+            dr = a - b;
+            di = c + d;
+        }
+        const float m = std::sqrt(dr * dr + di * di);
+        dr = dr / m;
+        di = di / m;
+        out.dtheta_dz = std::atan2(static_cast<double>(di), static_cast<double>(dr));
+    }
     out.rem_code = in.rem_code_phase_chips;
     out.code_step = in.code_phase_step_chips;
     for (int t = 0; t < kMaxTaps; t++) out.shifts[t] = (t < in.n_taps) ? in.shifts_chips[t] : 0.0f;

@@ -48,6 +48,7 @@ __device__ void fill_job(DevJob& j, const TrkParams& k, const TrkChannel& c, int
     j.inc_im = inci;
     j.dtheta = atan2(static_cast<double>(inci), static_cast<double>(incr));
     j.log_mag_inc = static_cast<float>(log(hypot(static_cast<double>(incr), static_cast<double>(inci))));
+    j.rot_avx = 0;
     j.rem_code = __fmul_rn(static_cast<float>(c.rem_code_phase_chips), spcf);
     j.code_step = __fmul_rn(static_cast<float>(c.code_phase_step_chips), spcf);
     j.in_margin = 0;  // the tracking plan launches the general (wrapping) chip-index path

@@ -376,6 +376,7 @@ __device__ void derive_epoch(PEpoch& ep, const TrkParams& k, const TrkChannel& c
     j.n_samples = static_cast<int32_t>(k.conf.vector_length);
     j.code_id = c.code_id;
     j.n_taps = NT;
+    j.rot_avx = 0;  // the batch lane-factor rule (this kernel's AVX path has its own replay)
     j.p0_re = p0.x;
     j.p0_im = p0.y;
     j.inc_re = inc.x;

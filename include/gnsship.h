@@ -68,6 +68,9 @@ extern "C" {
 /* gnsship_corr_job::flags bits */
 #define GNSSHIP_JOB_HIGH_DYN 1     /* high-dynamics resampler + rotator (set_high_dynamics_resampler) */
 #define GNSSHIP_JOB_ROTATOR_AVX 2  /* the AVX rotator variant (ignored with GNSSHIP_JOB_HIGH_DYN) */
+/* Batch jobs with GNSSHIP_JOB_ROTATOR_AVX replay phasor lanes 0-3 exactly and derive lanes 4-15 from
+ * them: within 1e-5 of the reference up to N = 50000 at zero IF; 2.3e-5 measured at N = 50000 with a
+ * 7 MHz IF (the reference's lanes round independently).  The tracking engine replays all 16. */
 /* The variant volk_gnsssdr's dispatcher would select for the rotator dot-product on this host:
  * VOLK_GENERIC set in the environment -> generic; an entry for the kernel in the volk_gnsssdr
  * preferences file ($VOLK_CONFIGPATH or $HOME/.volk_gnsssdr/volk_gnsssdr_config) -> that entry;
