@@ -84,7 +84,9 @@ JOB_HIGH_DYN, JOB_ROTATOR_AVX = 1, 2
 
 class TrkConf(ctypes.Structure):
     """gnsship_trk_conf — Dll_Pll_Conf (dll_pll_conf.h:33-80), same names/units; defaults as there
-    with the gnss_sdr_flags defaults for cn0_samples/cn0_min/max_*lock_fail/carrier_lock_th."""
+    with the gnss_sdr_flags defaults for cn0_samples/cn0_min/max_*lock_fail/carrier_lock_th.  The
+    rotator defaults to ROTATOR_AUTO in every binding (include/gnsship.h): the variant volk_gnsssdr
+    dispatches on this host.  if_hz (ABI 2): carrier IF fused into the correlator NCO."""
     _fields_ = [
         ("fs_in", ctypes.c_double), ("carrier_lock_th", ctypes.c_double),
         ("pll_bw_hz", ctypes.c_float), ("dll_bw_hz", ctypes.c_float), ("fll_bw_hz", ctypes.c_float),
@@ -102,6 +104,7 @@ class TrkConf(ctypes.Structure):
         ("early_late_space_narrow_chips", ctypes.c_float), ("very_early_late_space_narrow_chips", ctypes.c_float),
         ("enable_fll_pull_in", ctypes.c_int32), ("enable_fll_steady_state", ctypes.c_int32),
         ("high_dyn", ctypes.c_int32), ("smoother_length", ctypes.c_uint32), ("rotator", ctypes.c_int32),
+        ("reserved0", ctypes.c_int32), ("if_hz", ctypes.c_double),
     ]
 
     @classmethod
@@ -114,7 +117,7 @@ class TrkConf(ctypes.Structure):
                 max_code_lock_fail=50, max_carrier_lock_fail=5000, carrier_aiding=1, track_pilot=1, system=system,
                 extend_correlation_symbols=1, pll_bw_narrow_hz=5.0, dll_bw_narrow_hz=0.75, early_late_space_narrow_chips=0.15,
                 very_early_late_space_narrow_chips=0.5, enable_fll_pull_in=0, enable_fll_steady_state=0,
-                high_dyn=0, smoother_length=10, rotator=ROTATOR_GENERIC)
+                high_dyn=0, smoother_length=10, rotator=ROTATOR_AUTO, reserved0=0, if_hz=0.0)
         for k, v in kw.items():
             setattr(c, k, v)
         return c
@@ -162,6 +165,7 @@ _f = ctypes.c_float
 _SIGNATURES = {
     "gnsship_abi_version": ([], _i),
     "gnsship_rotator_dispatch": ([ctypes.POINTER(_i)], _i),
+    "gnsship_rotator_dispatch_detail": ([ctypes.c_char_p, _i], _i),
     "gnsship_device_count": ([ctypes.POINTER(_i)], _i),
     "gnsship_ctx_create": ([_i, _vpp], _i),
     "gnsship_ctx_destroy": ([_vp], _i),
@@ -215,6 +219,8 @@ _SIGNATURES = {
     "gnsship_trk_telemetry_event": ([_vp, _i, _i], _i),
     "gnsship_trk_run": ([_vp, _vp, _i, _i, ctypes.c_uint64, ctypes.c_int64, _i, _vp, ctypes.POINTER(_i)], _i),
     "gnsship_trk_run_dump": ([_vp, _vp, _i, _i, ctypes.c_uint64, ctypes.c_int64, _i, _vp, _vp, ctypes.POINTER(_i)], _i),
+    "gnsship_trk_launch": ([_vp, _vp, _i, ctypes.c_uint64, ctypes.c_int64, _i, _i, _i], _i),
+    "gnsship_trk_collect": ([_vp, _vp, _vp, ctypes.POINTER(_i)], _i),
     "gnsship_trk_channel_state": ([_vp, _i, ctypes.POINTER(_i), ctypes.POINTER(ctypes.c_uint64)], _i),
     "gnsship_trk_destroy": ([_vp], _i),
     "gnsship_comm_unique_id": ([_vp], _i),
@@ -237,6 +243,9 @@ def declared_symbols(header: str = HEADER_PATH) -> list:
 _LIB = None
 
 
+ABI_VERSION = 2  # GNSSHIP_ABI_VERSION of the header these bindings mirror
+
+
 def load() -> ctypes.CDLL:
     """Load libgnsship.so (raises if it was not built — no fallback)."""
     global _LIB
@@ -252,6 +261,8 @@ def load() -> ctypes.CDLL:
         fn = getattr(lib, name)  # AttributeError if the symbol is not exported
         fn.argtypes = argtypes
         fn.restype = restype
+    if lib.gnsship_abi_version() != ABI_VERSION:
+        raise RuntimeError(f"{path}: ABI version {lib.gnsship_abi_version()}, these bindings need {ABI_VERSION} (rebuild with `make`)")
     _LIB = lib
     return lib
 
@@ -272,7 +283,16 @@ def fptr(a: np.ndarray):
 
 def rotator_dispatch() -> int:
     """The volk_gnsssdr rotator variant the reference would run on this host (gnsship_rotator_dispatch):
-    ROTATOR_GENERIC or ROTATOR_AVX.  Host-only: no device needed."""
+    ROTATOR_GENERIC or ROTATOR_AVX.  Host-only: no device needed.  Raises for a preferences entry
+    naming a variant the engine does not reproduce (the message says which)."""
     v = ctypes.c_int(-1)
-    check(load().gnsship_rotator_dispatch(ctypes.byref(v)), "gnsship_rotator_dispatch")
+    rc = load().gnsship_rotator_dispatch(ctypes.byref(v))
+    if rc != OK:
+        raise GnssHipError(rc, f"gnsship_rotator_dispatch ({rotator_dispatch_detail()})")
     return v.value
+
+
+def rotator_dispatch_detail() -> str:
+    buf = ctypes.create_string_buffer(512)
+    load().gnsship_rotator_dispatch_detail(buf, 512)
+    return buf.value.decode(errors="replace")

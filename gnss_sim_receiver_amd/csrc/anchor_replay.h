@@ -1,6 +1,7 @@
 // anchor_replay.h — the reference rotator recursion replayed on the device (shared by the batched
 // correlator's anchor stage, corr_kernel.hip, and the tracking step kernel, trk_kernel.hip, which
-// replays its channels' next-epoch anchors right after deriving their NCO).
+// replays its channels' next-epoch anchors right after deriving their NCO).  Generic jobs: one
+// thread per job; AVX jobs: one thread per (job, phasor lane).
 #pragma once
 #include "engine.h"
 #include "nco_math.h"
@@ -35,66 +36,68 @@ __device__ __forceinline__ f2v avx_normalise(f2v z)
 }
 
 // Anchors of the AVX rotator variant (volk_gnsssdr_32fc_32f_rotator_dot_prod_32fc_xn_u_avx,
-// volk_gnsssdr_32fc_32f_rotator_dot_prod_32fc_xn.h:155-316):
-// 16 phasors z_l = phase·inc^l (generic chain), iteration m (samples 16m..16m+15) uses z_l and then
-// advances z_l ← z_l·dz with dz = normalise(inc^16 by four squarings), renormalising after the
-// update of iterations m ≡ 0 (mod 64).  Block k (samples 256k..) starts at iteration 16k; its anchor
-// holds z_0..z_3 there, so only lanes 0-3 are replayed: four independent chains of N/16 steps
-// instead of one of N.  Inside a block the correlation applies the lane factor E_{4t} as for the
-// generic variant (|dz| = 1: no magnitude term).  The N mod 16 tail (serial from normalise(z_0))
-// falls inside the last block's E_{4t} approximation.
-__device__ __forceinline__ void replay_anchors_avx(const DevJob& job, Anchor* __restrict__ out, int kb, int ke)
+// volk_gnsssdr_32fc_32f_rotator_dot_prod_32fc_xn.h:155-316), one thread per phasor lane l (engine.h
+// AVX layout): 16 phasors z_l = phase·inc^l (the generic chain, :204-208); iteration m (samples
+// 16m..16m+15) uses z_l and then advances z_l ← z_l·dz, normalising after the update of iterations
+// m ≡ 0 (mod 64) (:240-272).  Z[16t + l] = z_l at iteration 16t; segment s of n_segs covers tasks
+// [segment_block(s), segment_block(s + 1)) and a later segment resumes from the task before it.  The
+// last segment's lane 0 writes the serial tail: normalise(z_0) after the loop, then ·inc per sample
+// (:286-304).  Every product is the reference's float product (avx_cmul), bit for bit.
+__device__ __forceinline__ void replay_anchors_avx(const DevJob& job, f2v* __restrict__ Z, int lane, int seg_lo, int seg_hi, int n_segs)
 {
+    const int N = job.n_samples, M = N / kAvxLanes, T = avx_tasks_of(N);
+    const int kb = segment_block(seg_lo, T, n_segs), ke = segment_block(seg_hi, T, n_segs);
     const f2v inc = f2v{job.inc_re, job.inc_im};
-    f2v dz = inc;
-#pragma unroll
-    for (int q = 0; q < 4; q++) dz = avx_cmul(dz, dz);  // (:221-225)
-    dz = avx_normalise(dz);
-    f2v z[4];
+    const f2v dz = f2v{job.dz_re, job.dz_im};
+    auto step = [&](f2v z, int m) {
+        z = avx_cmul(z, dz);
+        return (m & 63) == 0 ? avx_normalise(z) : z;
+    };
+    f2v z;
     if (kb == 0) {
-        z[0] = f2v{job.p0_re, job.p0_im};
-#pragma unroll
-        for (int l = 1; l < 4; l++) z[l] = avx_cmul(z[l - 1], inc);
+        z = f2v{job.p0_re, job.p0_im};
+        for (int i = 0; i < kAvxLanes - 1; i++)
+            if (i < lane) z = avx_cmul(z, inc);
     } else {
-#pragma unroll
-        for (int l = 0; l < 4; l++) z[l] = f2v{out[kb - 1].p[2 * l], out[kb - 1].p[2 * l + 1]};
+        z = Z[(kb - 1) * kAvxLanes + lane];
+        const int m0 = (kb - 1) * kAvxTaskIters;
+        for (int i = 0; i < kAvxTaskIters && m0 + i < M; i++) z = step(z, m0 + i);
     }
-    for (int k = (kb == 0 ? kb : kb - 1); k < ke; k++) {
-        if (k >= kb) {
-            Anchor A;
+    for (int t = kb; t < ke; t++) {
+        Z[t * kAvxLanes + lane] = z;
+        if (t + 1 == ke && ke < T) break;  // the next segment resumes from here
+        const int m0 = t * kAvxTaskIters;
+        if (m0 + kAvxTaskIters <= M) {
+            z = step(z, m0);  // m0 ≡ 0 (mod 16): only the first update can normalise
 #pragma unroll
-            for (int l = 0; l < 4; l++) {
-                A.p[2 * l] = z[l].x;
-                A.p[2 * l + 1] = z[l].y;
-            }
-            out[k] = A;
-            if (k == ke - 1) break;
+            for (int i = 1; i < kAvxTaskIters; i++) z = avx_cmul(z, dz);
+        } else {
+            for (int i = 0; m0 + i < M; i++) z = step(z, m0 + i);
         }
-        // iterations 16k .. 16k+15: z ← z·dz, normalised after m ≡ 0 (mod 64) (:265-272)
-        const int m = 16 * k;
-#pragma unroll
-        for (int i = 0; i < 16; i++) {
-#pragma unroll
-            for (int l = 0; l < 4; l++) z[l] = avx_cmul(z[l], dz);
-            if (i == 0 && (m & 63) == 0) {
-#pragma unroll
-                for (int l = 0; l < 4; l++) z[l] = avx_normalise(z[l]);
-            }
+    }
+    if (ke == T && lane == 0) {  // the tail, from normalise(z_0) after the loop
+        f2v p = avx_normalise(z);
+        for (int j = 0; j < N - kAvxLanes * M; j++) {
+            Z[T * kAvxLanes + j] = p;
+            p = avx_cmul(p, inc);
         }
     }
 }
 
+// lane: this thread's phasor lane for AVX jobs (0..15, replay launched with kAvxLanes threads per
+// job); generic jobs run on lane 0 only.
 __device__ __forceinline__ void replay_anchors(const DevJob& job, Anchor* __restrict__ anchors, int seg_lo, int seg_hi,
-    int n_segs = kAnchorSegments)
+    int n_segs = kAnchorSegments, int lane = 0)
 {
+    if (job.rot_avx) {
+        replay_anchors_avx(job, reinterpret_cast<f2v*>(anchors + job.anchor_offset), lane, seg_lo, seg_hi, n_segs);
+        return;
+    }
+    if (lane != 0) return;
     const int nblk = (job.n_samples + kRenorm - 1) / kRenorm;
     const int kb = segment_block(seg_lo, nblk, n_segs), ke = segment_block(seg_hi, nblk, n_segs);
     if (kb >= ke) return;
     Anchor* out = anchors + job.anchor_offset;
-    if (job.rot_avx) {
-        replay_anchors_avx(job, out, kb, ke);
-        return;
-    }
     // phase·inc = (pr·ir − pi·ii, pr·ii + pi·ir) as two packed products + one packed add, each
     // rounded separately like the reference's written-out complex product (no FMA).  The sign
     // sits in the constant: fl(pi·(−ii)) = −fl(pi·ii) and x + (−y) ≡ x − y, bit for bit.

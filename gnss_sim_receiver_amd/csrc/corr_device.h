@@ -175,14 +175,12 @@ __device__ __forceinline__ void load_any(i4v span, int lane, int kb, int len, f2
 }
 
 // E_j = |inc|^j · e^{i j Δ} for this lane's j = 4·lane (angle formed and range-reduced in double,
-// hardware sin/cos in revolutions — E_j to a few 1e-7, against the 1e-5 tolerance).  AVX-variant
-// jobs advance by dz per 16 samples: angle (j/16)·arg(dz) + (j mod 16)·Δ (16·Δ differs from arg(dz)
-// by the squarings' rounding, ≈ 1e-6 rad, which would grow to ≈ 2e-5 over a block).
+// hardware sin/cos in revolutions — E_j to a few 1e-7, against the 1e-5 tolerance).  Generic
+// variant only (AVX-variant jobs continue every phasor exactly, corr_kernel.hip correlate_chunk_avx).
 __device__ __forceinline__ f2 lane_rotation(const DevJob& job, int j)
 {
     constexpr double kInvTwoPi = 0.15915494309189533576888376337251;
-    const double ang = job.rot_avx ? static_cast<double>(j >> 4) * job.dtheta_dz + static_cast<double>(j & 15) * job.dtheta
-                                   : static_cast<double>(j) * job.dtheta;
+    const double ang = static_cast<double>(j) * job.dtheta;
 #ifndef GNSSHIP_EJ_LIBM
     const double rev = ang * kInvTwoPi;
     const float rf = static_cast<float>(rev - rint(rev));
@@ -263,6 +261,34 @@ __device__ __forceinline__ void correlate_block(const DevJob& job, const ChunkDe
 #pragma unroll
         for (int t = 0; t < NT; t++) acc[t] = __builtin_elementwise_fma(tt, f2{cv[u][t], cv[u][t]}, acc[t]);
     }
+}
+
+// Complex product rounded exactly as the reference's written-out (ac − bd, ad + bc) (the AVX
+// rotator's _mm256_complexmul_ps and std::complex<float>): two packed products and one packed add,
+// no contraction (fl(x + fl(−y)) ≡ fl(x − y)).
+__device__ __forceinline__ f2 cmul_exact(f2 a, f2 b)
+{
+    const f2 t = f2{a.x, a.x} * b;
+    const f2 u = f2{a.y, a.y} * f2{-b.y, b.x};
+    return t + u;
+}
+
+// _mm256_complexnormalise_ps (volk_gnsssdr_avx_intrinsics.h:56-63): z / sqrt(re² + im²), IEEE sqrt
+// and division.
+__device__ __forceinline__ f2 normalise_avx(f2 z)
+{
+    const float m = __fsqrt_rn(__fadd_rn(__fmul_rn(z.x, z.x), __fmul_rn(z.y, z.y)));
+    return f2{__fdiv_rn(z.x, m), __fdiv_rn(z.y, m)};
+}
+
+// Chip index of tap shift `sh` at sample n: floor(step·(float)n + shift − rem), each operation
+// rounded in the reference's order (volk_gnsssdr_32f_xn_resampler_32f_xn.h:63-80); sn = step·(float)n.
+template <bool IN_MARGIN>
+__device__ __forceinline__ float code_at(const float* code, int L, float sn, float sh, float rem)
+{
+    int i = cvt_floor_i32(__fsub_rn(__fadd_rn(sn, sh), rem));
+    if constexpr (!IN_MARGIN) i = wrap_index(i, L);
+    return code[i];
 }
 
 // Sum over the 64 lanes of the wave (every lane gets it): DPP row sums, then the four rows.

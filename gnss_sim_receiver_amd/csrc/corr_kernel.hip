@@ -54,12 +54,15 @@ __device__ unsigned long long* g_corr_prof = nullptr;
     } while (0)
 #endif
 
-__global__ void corr_anchor_kernel(const DevJob* __restrict__ jobs, int n_jobs, Anchor* __restrict__ anchors, int seg_lo, int seg_hi, int n_segs)
+// lanes: threads per job (1, or kAvxLanes when the job set has AVX-variant jobs).
+__global__ void corr_anchor_kernel(const DevJob* __restrict__ jobs, int n_jobs, Anchor* __restrict__ anchors, int seg_lo, int seg_hi, int n_segs,
+    int lanes)
 {
-    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    const int g = blockIdx.x * blockDim.x + threadIdx.x;
+    const int j = lanes == 1 ? g : g / kAvxLanes, l = lanes == 1 ? 0 : g % kAvxLanes;
     if (j >= n_jobs) return;
     const DevJob job = jobs[j];
-    replay_anchors(job, anchors, seg_lo, seg_hi, n_segs);
+    replay_anchors(job, anchors, seg_lo, seg_hi, n_segs, l);
 }
 
 // Waves per SIMD the register allocation must allow: the 1- and 3-tap in-margin classes (GPS/B1I
@@ -68,10 +71,75 @@ __global__ void corr_anchor_kernel(const DevJob* __restrict__ jobs, int n_jobs, 
 #ifndef GNSSHIP_CORR_WAVES_EPL
 #define GNSSHIP_CORR_WAVES_EPL 8
 #endif
-template <int NT, bool IN_MARGIN>
+template <int NT, bool IN_MARGIN, bool AVX>
 constexpr int corr_waves_per_simd()
 {
-    return (NT <= 3 && IN_MARGIN) ? GNSSHIP_CORR_WAVES_EPL : kCorrWavesPerSimd;
+    return (NT <= 3 && IN_MARGIN && !AVX) ? GNSSHIP_CORR_WAVES_EPL : kCorrWavesPerSimd;
+}
+
+// AVX-variant chunk (engine.h AVX layout): the chunk's iterations [m0, m0 + 256) ∩ [0, M) are tasks of
+// 16; a wave takes groups of four tasks, lane = 16·(task in group) + phasor lane l, and continues
+// lane l's phasor from the task's anchor through the task's iterations with the reference's own
+// float products (z ← z·dz, normalised after the update of iterations ≡ 0 mod 64) — every phasor
+// bit-identical to u_avx's — correlating sample 16m + l at iteration m.  The N mod 16 tail (serial
+// from normalise(z_0), anchors after the tasks) goes to the lanes < tail of the chunk's first wave.
+// Sums stay in the sample frame (no lane factor).
+template <int FMT, int NT, bool IN_MARGIN>
+__device__ __forceinline__ void correlate_chunk_avx(const DevJob& job, const ChunkDesc& ch, i4v span, const f2* __restrict__ Z, const float (&shifts)[NT],
+    const float* __restrict__ code, int L, int lane, int part, int wpc, f2 (&acc)[NT])
+{
+    constexpr int SB = sample_bytes<FMT>();
+    const int M = job.n_samples / kAvxLanes, T = avx_tasks_of(job.n_samples);
+    const int m0 = ch.start / kAvxLanes;
+    const int it_end = min(m0 + kCorrChunk / kAvxLanes, M);
+    const int n_tasks = it_end > m0 ? (it_end - m0 + kAvxTaskIters - 1) / kAvxTaskIters : 0;
+    const int n_groups = (n_tasks + 3) / 4;
+    const int per = (n_groups + wpc - 1) / wpc;
+    const int g0 = min(part * per, n_groups), g1 = min(g0 + per, n_groups);
+    const f2 dz = f2{job.dz_re, job.dz_im};
+    const float step = job.code_step, rem = job.rem_code;
+    const int tl = lane >> 4, l = lane & (kAvxLanes - 1);
+    for (int g = g0; g < g1; g++) {
+        const int tc = 4 * g + tl;  // task within the chunk
+        const bool active = tc < n_tasks;
+        const int t = m0 / kAvxTaskIters + (active ? tc : 0);
+        const int m_lo = t * kAvxTaskIters;
+        const int cnt = active ? min(kAvxTaskIters, M - m_lo) : 0;
+        const int n0 = kAvxLanes * m_lo + l;  // job-relative sample of iteration m_lo
+        f2 x[kAvxTaskIters];
+#pragma unroll
+        for (int i = 0; i < kAvxTaskIters; i++) x[i] = load_sample<FMT>(span, (n0 - ch.start + kAvxLanes * i) * SB, 0);
+        f2 z = Z[t * kAvxLanes + l];
+        float fn = static_cast<float>(n0);  // (float)n, exact steps of 16 (n < 2^24)
+#pragma unroll
+        for (int i = 0; i < kAvxTaskIters; i++) {
+            const bool on = i < cnt;
+            const f2 r = on ? cmul_pk2(x[i], z) : f2{0.0f, 0.0f};
+            f2 zn = cmul_exact(z, dz);
+            if (i == 0 && (t & 3) == 0) zn = normalise_avx(zn);  // after iteration m_lo ≡ 0 (mod 64)
+            z = zn;
+            const float sn = __fmul_rn(step, on ? fn : static_cast<float>(n0));
+#pragma unroll
+            for (int q = 0; q < NT; q++) {
+                const float c = code_at<IN_MARGIN>(code, L, sn, shifts[q], rem);
+                acc[q] = __builtin_elementwise_fma(r, f2{c, c}, acc[q]);
+            }
+            fn += static_cast<float>(kAvxLanes);
+        }
+    }
+    const int tail = job.n_samples - kAvxLanes * M;
+    const int n_t = kAvxLanes * M;  // first tail sample
+    if (part == 0 && tail > 0 && n_t >= ch.start && n_t < ch.start + ch.len && lane < tail) {
+        const int n = n_t + lane;
+        const f2 xv = load_sample<FMT>(span, (n - ch.start) * SB, 0);
+        const f2 r = cmul_pk2(xv, Z[T * kAvxLanes + lane]);
+        const float sn = __fmul_rn(step, static_cast<float>(n));
+#pragma unroll
+        for (int q = 0; q < NT; q++) {
+            const float c = code_at<IN_MARGIN>(code, L, sn, shifts[q], rem);
+            acc[q] = __builtin_elementwise_fma(r, f2{c, c}, acc[q]);
+        }
+    }
 }
 
 // One launch per chunk class (tap-count template × in-margin flag), so each kernel is compiled
@@ -81,8 +149,8 @@ constexpr int corr_waves_per_simd()
 // channel).  The replica is staged in LDS once per workgroup; then wave w correlates chunk w of the
 // item on its own — 64 samples per lane, a block of four per step with the next block's samples in
 // flight — and reduces it within the wave (no further barrier).
-template <int FMT, int NT, bool IN_MARGIN>
-__global__ __launch_bounds__(kCorrThreads, (corr_waves_per_simd<NT, IN_MARGIN>())) void corr_batch_kernel(const void* __restrict__ samples,
+template <int FMT, int NT, bool IN_MARGIN, bool AVX>
+__global__ __launch_bounds__(kCorrThreads, (corr_waves_per_simd<NT, IN_MARGIN, AVX>())) void corr_batch_kernel(const void* __restrict__ samples,
     const DevJob* __restrict__ jobs, const ChunkDesc* __restrict__ chunks, const WorkItem* __restrict__ items, int n_items,
     const Anchor* __restrict__ anchors, float* __restrict__ partials, float* __restrict__ out, AnchorPrefetch pf)
 {
@@ -98,10 +166,11 @@ __global__ __launch_bounds__(kCorrThreads, (corr_waves_per_simd<NT, IN_MARGIN>()
         int ti = 0, base = 0;
         while (ti + 1 < kAnchorRingMax && static_cast<int>(blockIdx.x) >= base + pf.task[ti].n_blocks) base += pf.task[ti++].n_blocks;
         const ReplayTask& t = pf.task[ti];
-        const int j = (blockIdx.x - base) * kCorrThreads + threadIdx.x;
+        const int gi = (blockIdx.x - base) * kCorrThreads + threadIdx.x;
+        const int j = t.lanes == 1 ? gi : gi / kAvxLanes;
         if (j < t.n_jobs) {
             const DevJob pj = t.jobs[j];
-            replay_anchors(pj, t.anchors, t.seg_lo, t.seg_hi, t.n_segs);
+            replay_anchors(pj, t.anchors, t.seg_lo, t.seg_hi, t.n_segs, t.lanes == 1 ? 0 : gi % kAvxLanes);
         }
         GNSSHIP_PROF_STAMP(5);
         return;
@@ -157,7 +226,7 @@ __global__ __launch_bounds__(kCorrThreads, (corr_waves_per_simd<NT, IN_MARGIN>()
     const int kb0 = part * per < nblk_all ? part * per : nblk_all;
     const int kb1 = kb0 + per < nblk_all ? kb0 + per : nblk_all;  // this wave's blocks [kb0, kb1)
     f2 xa[kLaneSamples], xb[kLaneSamples];
-    if (kb0 < kb1) load_any<FMT>(span, lane, kb0, ch.len, xa);
+    if (!AVX && kb0 < kb1) load_any<FMT>(span, lane, kb0, ch.len, xa);
     __builtin_amdgcn_s_waitcnt(0);  // the replica's LDS-DMA (and the first block) landed
     __syncthreads();
     if (!active) return;  // only when wpc == 1: no barrier follows
@@ -182,6 +251,29 @@ __global__ __launch_bounds__(kCorrThreads, (corr_waves_per_simd<NT, IN_MARGIN>()
     f2 acc[NT];
 #pragma unroll
     for (int t = 0; t < NT; t++) acc[t] = f2{0.0f, 0.0f};
+    if constexpr (AVX) {
+        correlate_chunk_avx<FMT, NT, IN_MARGIN>(job, ch, span, reinterpret_cast<const f2*>(anchors + job.anchor_offset), shifts, code, L, lane, part, wpc,
+            acc);
+        float val = 0.0f;
+#pragma unroll
+        for (int t = 0; t < NT; t++) {
+            const float sr = wave_sum(acc[t].x), si = wave_sum(acc[t].y);
+            val = (lane == 2 * t) ? sr : val;
+            val = (lane == 2 * t + 1) ? si : val;
+        }
+        if (wpc > 1) {  // the chunk's waves combine in LDS, in part order (deterministic)
+            __shared__ float red_avx[kCorrThreads / kWave][2 * kMaxTaps];
+            if (lane < 2 * kMaxTaps) red_avx[wave][lane] = val;
+            __syncthreads();
+            if (part != 0) return;
+            float sum = 0.0f;
+            for (int w = 0; w < wpc; w++) sum += (lane < 2 * kMaxTaps) ? red_avx[wave + w][lane] : 0.0f;
+            val = sum;
+        }
+        float* dst = (job.n_chunks == 1) ? out + static_cast<int64_t>(ch.job) * 2 * kMaxTaps : partials + static_cast<int64_t>(it.first + cidx) * 2 * kMaxTaps;
+        if (lane < 2 * kMaxTaps) dst[lane] = (lane < 2 * job.n_taps && ch.len > 0) ? val : 0.0f;
+        return;
+    }
     Anchor A = anc(kb0);
     // ping-pong over blocks: block kb0 + 2i in xa, kb0 + 2i + 1 in xb
     for (int kb = kb0; kb < kb1; kb += 2) {
@@ -248,15 +340,17 @@ namespace gnsship {
 
 hipError_t launch_corr_batch(const void* samples, int fmt, const DevJob* jobs, int n_jobs, const ChunkDesc* chunks, const WorkItem* items,
     int n_items, const ChunkClass* classes, int max_code_len, bool any_multi_chunk, Anchor* anchors, float* partials, float* out,
-    hipStream_t stream, int stages, const AnchorPrefetch* prefetch)
+    hipStream_t stream, int stages, const AnchorPrefetch* prefetch, int replay_lanes)
 {
+    if (replay_lanes < 1) replay_lanes = 1;
     const int n_chunks = n_items;  // work items to launch (0: nothing to correlate)
     AnchorPrefetch pf{};
     if (prefetch && (stages & GNSSHIP_STAGE_CORRELATE)) {
         pf = *prefetch;
         int nb = 0;
         for (auto& t : pf.task) {
-            t.n_blocks = (t.n_jobs > 0 && t.seg_lo < t.seg_hi) ? (t.n_jobs + kCorrThreads - 1) / kCorrThreads : 0;
+            if (t.lanes < 1) t.lanes = 1;
+            t.n_blocks = (t.n_jobs > 0 && t.seg_lo < t.seg_hi) ? (t.n_jobs * t.lanes + kCorrThreads - 1) / kCorrThreads : 0;
             nb += t.n_blocks;
         }
         pf.n_blocks = (nb + 7) & ~7;
@@ -264,8 +358,8 @@ hipError_t launch_corr_batch(const void* samples, int fmt, const DevJob* jobs, i
     if (n_chunks <= 0) {
         for (const auto& t : pf.task) {
             if (t.n_blocks == 0) continue;
-            hipLaunchKernelGGL(corr_anchor_kernel, dim3((t.n_jobs + 63) / 64), dim3(64), 0, stream, t.jobs, t.n_jobs, t.anchors, t.seg_lo, t.seg_hi,
-                t.n_segs);
+            hipLaunchKernelGGL(corr_anchor_kernel, dim3((t.n_jobs * t.lanes + 63) / 64), dim3(64), 0, stream, t.jobs, t.n_jobs, t.anchors, t.seg_lo,
+                t.seg_hi, t.n_segs, t.lanes);
             hipError_t e = hipGetLastError();
             if (e != hipSuccess) return e;
         }
@@ -274,8 +368,9 @@ hipError_t launch_corr_batch(const void* samples, int fmt, const DevJob* jobs, i
     if (max_code_len < 1 || max_code_len > kMaxCodeLen) return hipErrorInvalidValue;
     hipError_t e = hipSuccess;
     if (stages & GNSSHIP_STAGE_ANCHORS) {
-        hipLaunchKernelGGL(corr_anchor_kernel, dim3((n_jobs + 63) / 64), dim3(64), 0, stream, jobs, n_jobs, anchors, 0, kAnchorSegments,
-            kAnchorSegments);
+        const int threads = n_jobs * replay_lanes;
+        hipLaunchKernelGGL(corr_anchor_kernel, dim3((threads + 63) / 64), dim3(64), 0, stream, jobs, n_jobs, anchors, 0, kAnchorSegments,
+            kAnchorSegments, replay_lanes);
         e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
@@ -286,18 +381,26 @@ hipError_t launch_corr_batch(const void* samples, int fmt, const DevJob* jobs, i
         if (cnt <= 0) continue;
         const WorkItem* ic = items + classes[c].start;
         dim3 grid(cnt + pf.n_blocks), block(kCorrThreads);
-#define GNSSHIP_LAUNCH_CORR(F, NTV, MV) \
-    hipLaunchKernelGGL((corr_batch_kernel<F, NTV, MV>), grid, block, lds, stream, samples, jobs, chunks, ic, cnt, anchors, partials, out, pf)
+#define GNSSHIP_LAUNCH_CORR(F, NTV, MV, AV) \
+    hipLaunchKernelGGL((corr_batch_kernel<F, NTV, MV, AV>), grid, block, lds, stream, samples, jobs, chunks, ic, cnt, anchors, partials, out, pf)
 #define GNSSHIP_LAUNCH_NT(F)                                                     \
     switch (c) {                                                                 \
-    case 0: GNSSHIP_LAUNCH_CORR(F, 1, false); break;                             \
-    case 1: GNSSHIP_LAUNCH_CORR(F, 1, true); break;                              \
-    case 2: GNSSHIP_LAUNCH_CORR(F, 3, false); break;                             \
-    case 3: GNSSHIP_LAUNCH_CORR(F, 3, true); break;                              \
-    case 4: GNSSHIP_LAUNCH_CORR(F, 5, false); break;                             \
-    case 5: GNSSHIP_LAUNCH_CORR(F, 5, true); break;                              \
-    case 6: GNSSHIP_LAUNCH_CORR(F, kMaxTaps, false); break;                      \
-    default: GNSSHIP_LAUNCH_CORR(F, kMaxTaps, true); break;                      \
+    case 0: GNSSHIP_LAUNCH_CORR(F, 1, false, false); break;                      \
+    case 1: GNSSHIP_LAUNCH_CORR(F, 1, true, false); break;                       \
+    case 2: GNSSHIP_LAUNCH_CORR(F, 3, false, false); break;                      \
+    case 3: GNSSHIP_LAUNCH_CORR(F, 3, true, false); break;                       \
+    case 4: GNSSHIP_LAUNCH_CORR(F, 5, false, false); break;                      \
+    case 5: GNSSHIP_LAUNCH_CORR(F, 5, true, false); break;                       \
+    case 6: GNSSHIP_LAUNCH_CORR(F, kMaxTaps, false, false); break;               \
+    case 7: GNSSHIP_LAUNCH_CORR(F, kMaxTaps, true, false); break;                \
+    case 8: GNSSHIP_LAUNCH_CORR(F, 1, false, true); break;                       \
+    case 9: GNSSHIP_LAUNCH_CORR(F, 1, true, true); break;                        \
+    case 10: GNSSHIP_LAUNCH_CORR(F, 3, false, true); break;                      \
+    case 11: GNSSHIP_LAUNCH_CORR(F, 3, true, true); break;                       \
+    case 12: GNSSHIP_LAUNCH_CORR(F, 5, false, true); break;                      \
+    case 13: GNSSHIP_LAUNCH_CORR(F, 5, true, true); break;                       \
+    case 14: GNSSHIP_LAUNCH_CORR(F, kMaxTaps, false, true); break;               \
+    default: GNSSHIP_LAUNCH_CORR(F, kMaxTaps, true, true); break;                \
     }
         switch (fmt) {
         case GNSSHIP_FMT_CF32: GNSSHIP_LAUNCH_NT(GNSSHIP_FMT_CF32); break;

@@ -40,7 +40,7 @@ struct DevJob {
     float p0_re, p0_im;     // phase_offset_as_complex
     float inc_re, inc_im;   // phase_inc
     double dtheta;          // arg(phase_inc) in double (exact angle of the float phasor)
-    double dtheta_dz;       // rot_avx: arg(dz), dz = normalise(phase_inc^16) as the AVX recursion forms it
+    float dz_re, dz_im;     // rot_avx: dz = normalise(phase_inc^16) exactly as the AVX recursion forms it
     float log_mag_inc;      // log|phase_inc| (magnitude growth between renormalisations)
     float rem_code;         // rem_code_phase_chips  (float, as passed by the reference)
     float code_step;        // code_phase_step_chips
@@ -60,6 +60,20 @@ constexpr int kCodeMargin = 32;
 constexpr int padded_code_quads(int len) { return (len + 2 * kCodeMargin + 3) / 4; }
 hipError_t upload_padded_code(const float* code, int len, float** chip0);  // allocates; *chip0 = chip 0
 hipError_t free_padded_code(const float* chip0);
+
+// AVX-variant jobs (rot_avx) keep their own anchor layout in the same buffer, in f2 (8-byte) units
+// from anchor_offset·4: Z[16t + l] = the phasor AVX lane l uses at iteration 16t (before its update;
+// task t = iterations [16t, 16t + 16) ∩ [0, N/16)), for every task, then the ≤ 15 phasors of the
+// serial N mod 16 tail at Z[16·T + j] (T tasks).  Every phasor is then continued bit-exactly by the
+// correlating lanes (corr_kernel.hip), so nothing is approximated.
+constexpr int kAvxLanes = 16;       // phasors of the u_avx rotator (…rotator_dot_prod_32fc_xn.h:199-213)
+constexpr int kAvxTaskIters = 16;   // iterations per anchored task
+__host__ __device__ constexpr int avx_tasks_of(int n_samples) { return (n_samples / kAvxLanes + kAvxTaskIters - 1) / kAvxTaskIters; }
+// Anchor entries (32 B each) of a job's layout: generic ceil(n/256), AVX 4·(tasks + 1).
+__host__ __device__ constexpr int anchor_entries(int n_samples, bool avx)
+{
+    return avx ? 4 * (avx_tasks_of(n_samples) + 1) : (n_samples + 255) / 256;
+}
 
 // Rotator anchor of one 256-sample block k of a job: the phasors the reference rotates samples
 // 256k + s by, s = 0..3 — p[0..1] = the renormalised q = a/|a| (the reference multiplies sample 256k
@@ -91,17 +105,17 @@ struct WorkItem {
 };
 
 // Launch the batched correlator: partials[chunk][2*kMaxTaps] then per-job reduction into out.
-// Chunks are grouped by class = 2·tap_class + in_margin, tap_class: 0 → 1 tap, 1 → ≤3, 2 → ≤5, 3 → ≤8;
-// each class is one kernel launch over work items [start, start + count).
-constexpr int kChunkClasses = 8;
+// Chunks are grouped by class = 8·avx + 2·tap_class + in_margin, tap_class: 0 → 1 tap, 1 → ≤3, 2 → ≤5,
+// 3 → ≤8; each class is one kernel launch over work items [start, start + count).
+constexpr int kChunkClasses = 16;
 struct ChunkClass {
     int32_t start;
     int32_t count;
 };
-inline int chunk_class(int n_taps, int in_margin)
+inline int chunk_class(int n_taps, int in_margin, int avx)
 {
     const int tc = n_taps <= 1 ? 0 : n_taps <= 3 ? 1 : n_taps <= 5 ? 2 : 3;
-    return 2 * tc + (in_margin ? 1 : 0);
+    return 8 * (avx ? 1 : 0) + 2 * tc + (in_margin ? 1 : 0);
 }
 
 // Anchor replay of another job set carried by a correlation launch (leading workgroups).
@@ -118,6 +132,7 @@ struct ReplayTask {
     int32_t seg_lo, seg_hi;  // segments [seg_lo, seg_hi) of n_segs equal block ranges
     int32_t n_segs;
     int32_t n_blocks;        // workgroups (set by launch_corr_batch)
+    int32_t lanes;           // threads per job: 1, or kAvxLanes when any job uses the AVX variant
 };
 struct AnchorPrefetch {
     ReplayTask task[kAnchorRingMax];
@@ -129,9 +144,11 @@ void attach_codes(std::vector<ChunkDesc>& chunks, const std::vector<struct DevJo
 
 // anchors: scratch of Σ ceil(n_j/256) Anchor entries, recomputed by every launch.  prefetch
 // (optional, with the CORRELATE stage): replay `prefetch->jobs`' anchors in the same launch.
+// replay_lanes: threads per job of the anchor stage (1, or kAvxLanes when any job is rot_avx).
 hipError_t launch_corr_batch(const void* samples, int fmt, const DevJob* jobs, int n_jobs, const ChunkDesc* chunks, const WorkItem* items,
     int n_items, const ChunkClass* classes, int max_code_len, bool any_multi_chunk, Anchor* anchors, float* partials, float* out,
-    hipStream_t stream, int stages = GNSSHIP_STAGE_ANCHORS | GNSSHIP_STAGE_CORRELATE, const AnchorPrefetch* prefetch = nullptr);
+    hipStream_t stream, int stages = GNSSHIP_STAGE_ANCHORS | GNSSHIP_STAGE_CORRELATE, const AnchorPrefetch* prefetch = nullptr,
+    int replay_lanes = 1);
 
 // Plan chunks (≤ kCorrChunk samples), rotator anchors and work items for a job list: chunks of one
 // job stay contiguous and in order; single-chunk jobs with equal code id (pair_by_code) share items

@@ -82,13 +82,13 @@ bool derive_job(const gnsship_corr_job& in, int code_len, DevJob& out)
     out.inc_im = inci;
     out.dtheta = std::atan2(static_cast<double>(inci), static_cast<double>(incr));
     out.log_mag_inc = static_cast<float>(std::log(std::hypot(static_cast<double>(incr), static_cast<double>(inci))));
-    // AVX variant: the phasors advance by the normalised dz = inc^16, so no magnitude drift inside a block
+    // AVX variant: dz = inc^16 by four written-out float squarings (dz *= dz, :221-225), then
+    // _mm256_complexnormalise_ps (IEEE sqrt and division); host and device form it identically
+    // (-ffp-contract=off), the replay and the correlation both read this value
     out.rot_avx = (in.flags & GNSSHIP_JOB_ROTATOR_AVX) ? 1 : 0;
-    out.dtheta_dz = 0.0;
+    out.dz_re = 1.0f;
+    out.dz_im = 0.0f;
     if (out.rot_avx) {
-        out.log_mag_inc = 0.0f;
-        // dz exactly as replay_anchors_avx forms it (four written-out float squarings, IEEE sqrt and
-        // division): the lane factor advances by arg(dz) per 16 samples, not 16·arg(inc)
         float dr = incr, di = inci;
         for (int q = 0; q < 4; q++) {
             const float a = dr * dr, b = di * di, c = dr * di, d = di * dr;
@@ -96,9 +96,8 @@ bool derive_job(const gnsship_corr_job& in, int code_len, DevJob& out)
             di = c + d;
         }
         const float m = std::sqrt(dr * dr + di * di);
-        dr = dr / m;
-        di = di / m;
-        out.dtheta_dz = std::atan2(static_cast<double>(di), static_cast<double>(dr));
+        out.dz_re = dr / m;
+        out.dz_im = di / m;
     }
     out.rem_code = in.rem_code_phase_chips;
     out.code_step = in.code_phase_step_chips;
@@ -131,7 +130,7 @@ int plan_chunks(std::vector<DevJob>& jobs, std::vector<ChunkDesc>& chunks, std::
     for (size_t j = 0; j < jobs.size(); j++) {
         const int n = jobs[j].n_samples;
         jobs[j].anchor_offset = static_cast<int32_t>(anchors);
-        anchors += (n + kRenorm - 1) / kRenorm;
+        anchors += anchor_entries(n > 0 ? n : 0, jobs[j].rot_avx != 0);
         jobs[j].n_chunks = n <= 0 ? 1 : (n + kCorrChunk - 1) / kCorrChunk;
         if (jobs[j].n_chunks > 1) any_multi = true;
     }
@@ -159,7 +158,7 @@ int plan_chunks(std::vector<DevJob>& jobs, std::vector<ChunkDesc>& chunks, std::
             js.clear();
         };
         for (size_t j = 0; j < jobs.size(); j++) {
-            if (chunk_class(jobs[j].n_taps, jobs[j].in_margin) != c) continue;
+            if (chunk_class(jobs[j].n_taps, jobs[j].in_margin, jobs[j].rot_avx) != c) continue;
             const int nch = jobs[j].n_chunks;
             if (nch == 1 && pair_by_code && chunks_per_item > 1) {
                 std::vector<int>& pend = open[jobs[j].code_id];
@@ -415,6 +414,7 @@ struct gnsship_batch {
     // the context stream by launches that carried this batch as `next` / `next2` (0..kAnchorSegments);
     // cleared by set_jobs.
     int anchor_segs = 0;
+    int replay_lanes = 1;  // kAvxLanes when any job uses the AVX rotator variant
     // high-dynamics jobs (flags bit 0): correlated by corr_hd_kernel.hip after the main classes; their
     // slots in the main plan are empty jobs
     HdPlan hd;
@@ -489,6 +489,9 @@ extern "C" int gnsship_batch_set_jobs(gnsship_batch* b, const gnsship_corr_job* 
         if (ctx->codes_host[in.code_id].len > max_len) max_len = ctx->codes_host[in.code_id].len;
     }
     b->max_code_len = max_len;
+    b->replay_lanes = 1;
+    for (const auto& dj : b->jobs_host)
+        if (dj.rot_avx) b->replay_lanes = kAvxLanes;
     int64_t n_anchors = 0;
     b->n_chunks = plan_chunks(b->jobs_host, b->chunks_host, b->items_host, b->any_multi, &n_anchors, b->classes, chunks_per_item_setting(), true);
     b->n_items = static_cast<int>(b->items_host.size());
@@ -543,7 +546,7 @@ extern "C" int gnsship_batch_launch_stages(gnsship_batch* b, const void* dev_sam
         // WAR: the previous correlation of this batch must have consumed the anchors
         HIP_TRY(ctx, hipStreamWaitEvent(b->aux, b->corr_done, 0));
         hipError_t e = launch_corr_batch(dev_samples, fmt, b->jobs_dev, b->n_jobs, b->chunks_dev, b->items_dev, b->n_items, b->classes,
-            b->max_code_len, b->any_multi, b->anchors_dev, b->partials_dev, b->out_dev, b->aux, GNSSHIP_STAGE_ANCHORS);
+            b->max_code_len, b->any_multi, b->anchors_dev, b->partials_dev, b->out_dev, b->aux, GNSSHIP_STAGE_ANCHORS, nullptr, b->replay_lanes);
         if (e != hipSuccess) return hip_fail(ctx, e, "launch_corr_batch(anchors)");
         HIP_TRY(ctx, hipEventRecord(b->anchors_ready, b->aux));
         HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, b->anchors_ready, 0));  // RAW: correlation (or caller) after replay
@@ -580,11 +583,13 @@ extern "C" int gnsship_batch_launch_pipelined2(gnsship_batch* b, const void* dev
     if (int rc = set_device(ctx)) return rc;
     AnchorPrefetch pf{};
     const bool p1 = next && next->n_jobs > 0, p2 = next2 && next2->n_jobs > 0;
-    if (p1) pf.task[0] = ReplayTask{next->jobs_dev, next->anchors_dev, next->n_jobs, next->anchor_segs == 1 ? 1 : 0, kAnchorSegments, 0};
-    if (p2) pf.task[1] = ReplayTask{next2->jobs_dev, next2->anchors_dev, next2->n_jobs, 0, 1, 0};
+    if (p1)
+        pf.task[0] = ReplayTask{next->jobs_dev, next->anchors_dev, next->n_jobs, next->anchor_segs == 1 ? 1 : 0, kAnchorSegments, kAnchorSegments, 0,
+            next->replay_lanes};
+    if (p2) pf.task[1] = ReplayTask{next2->jobs_dev, next2->anchors_dev, next2->n_jobs, 0, 1, kAnchorSegments, 0, next2->replay_lanes};
     if (b->n_jobs > 0 && b->anchor_segs < kAnchorSegments) {
         hipError_t e = launch_corr_batch(dev_samples, fmt, b->jobs_dev, b->n_jobs, b->chunks_dev, b->items_dev, b->n_items, b->classes,
-            b->max_code_len, b->any_multi, b->anchors_dev, b->partials_dev, b->out_dev, ctx->stream, GNSSHIP_STAGE_ANCHORS);
+            b->max_code_len, b->any_multi, b->anchors_dev, b->partials_dev, b->out_dev, ctx->stream, GNSSHIP_STAGE_ANCHORS, nullptr, b->replay_lanes);
         if (e != hipSuccess) return hip_fail(ctx, e, "launch_corr_batch(anchors)");
     }
     if (b->n_jobs > 0 || p1 || p2) {

@@ -71,6 +71,9 @@ struct gnsship_trk {
     HdPlan hd;
     TrkHist* hist_dev = nullptr;
     bool force_rounds = false;  // GNSSHIP_TRK_ROUNDS=1: the round-based loop even where the persistent one applies
+    // gnsship_trk_launch → gnsship_trk_collect: the enqueued run's rounds (−1: none pending)
+    int pending_rounds = -1;
+    bool pending_out = false, pending_dump = false;
 };
 
 namespace {
@@ -269,6 +272,13 @@ bool build_params(const gnsship_trk_conf& c, TrkParams& p)
     p.lock_init_samples = c.carrier_lock_test_smoother_samples <= 0 ? 1 : c.carrier_lock_test_smoother_samples;
     p.jobs_per_channel = p.track_pilot ? 2 : 1;
     p.chunks_per_job = (static_cast<int>(c.vector_length) + kCorrChunk - 1) / kCorrChunk;
+    // carrier IF fused into the correlator NCO (include/gnsship.h if_hz; gnsship_trk_create checked
+    // that if_hz and fs_in are whole Hz)
+    p.has_if = c.if_hz != 0.0 ? 1 : 0;
+    p.if_step_rad = p.has_if ? 6.2831853071796 * c.if_hz / c.fs_in : 0.0;
+    p.fs_int = static_cast<int64_t>(c.fs_in);
+    const int64_t ifi = static_cast<int64_t>(c.if_hz);
+    p.if_mod = p.fs_int > 0 ? ((ifi % p.fs_int) + p.fs_int) % p.fs_int : 0;
     return true;
 }
 
@@ -311,9 +321,12 @@ extern "C" int gnsship_trk_create(gnsship_ctx* ctx, const gnsship_trk_conf* conf
     if (max_channels < 1 || conf->fs_in <= 0.0 || conf->vector_length < 1 || conf->cn0_samples < 1 || conf->cn0_samples > kTrkMaxCn0Samples ||
         conf->pll_filter_order < 2 || conf->pll_filter_order > 3 || conf->dll_filter_order < 1 || conf->dll_filter_order > 3 ||
         (conf->high_dyn && conf->smoother_length > static_cast<uint32_t>(kTrkMaxSmoother)) || conf->rotator < GNSSHIP_ROTATOR_AUTO ||
-        conf->rotator > GNSSHIP_ROTATOR_AVX)
+        conf->rotator > GNSSHIP_ROTATOR_AVX || conf->reserved0 != 0)
         return fail(ctx, GNSSHIP_E_INVAL,
             "gnsship_trk_create: bad configuration (cn0_samples 1..64, pll order 2..3, dll order 1..3, smoother_length <= 64)");
+    if (conf->if_hz != 0.0 && (!std::isfinite(conf->if_hz) || conf->if_hz != std::floor(conf->if_hz) || conf->fs_in != std::floor(conf->fs_in) ||
+                                  std::fabs(conf->if_hz) >= conf->fs_in || conf->fs_in > 4.0e9))
+        return fail(ctx, GNSSHIP_E_INVAL, "gnsship_trk_create: if_hz must be a whole number of Hz below fs_in, with fs_in whole Hz");
     gnsship_trk* t = new (std::nothrow) gnsship_trk();
     if (!t) return GNSSHIP_E_NOMEM;
     t->ctx = ctx;
@@ -323,6 +336,10 @@ extern "C" int gnsship_trk_create(gnsship_ctx* ctx, const gnsship_trk_conf* conf
     }
     if (t->params.conf.rotator == GNSSHIP_ROTATOR_AUTO) gnsship_rotator_dispatch(&t->params.conf.rotator);
     if (t->params.conf.high_dyn) t->params.conf.rotator = GNSSHIP_ROTATOR_GENERIC;  // only generic high-dynamics variants exist
+    if (t->params.conf.rotator == GNSSHIP_ROTATOR_AVX && !trk_persist_supports(t->params)) {
+        delete t;
+        return fail(ctx, GNSSHIP_E_INVAL, "gnsship_trk_create: the AVX rotator runs in the persistent loop, which has no kernel for this tap layout");
+    }
     {
         const char* env = std::getenv("GNSSHIP_TRK_ROUNDS");  // A/B: force the round-based loop
         t->force_rounds = env && env[0] == '1';
@@ -450,6 +467,12 @@ extern "C" int gnsship_trk_start(gnsship_trk* t, int channel, const gnsship_trk_
     c.acc_carrier_phase_rad -= c.carrier_phase_step_rad * static_cast<double>(samples_offset);
     c.state = 2;
     c.nitems_read = a->first_sample + static_cast<uint64_t>(samples_offset);
+    if (p.has_if) {  // IF phase at nitems_read: (if_mod · n) mod fs exactly (both factors < fs ≤ 4e9 → split n)
+        const uint64_t fsu = static_cast<uint64_t>(p.fs_int);
+        const unsigned __int128 prod = static_cast<unsigned __int128>(static_cast<uint64_t>(p.if_mod)) * (c.nitems_read % fsu);
+        c.if_num = static_cast<int64_t>(prod % fsu);
+        c.if_cyc = static_cast<double>(c.if_num) / static_cast<double>(p.fs_int);
+    }
     if (int rc = set_device(ctx)) return rc;
     // the channel's chunks carry its code replica(s): only the code fields are rewritten (the
     // device owns the lengths)
@@ -519,16 +542,11 @@ extern "C" int gnsship_trk_run(gnsship_trk* t, const void* sig, int fmt, int sig
     return gnsship_trk_run_dump(t, sig, fmt, sig_on_device, buffer_first_sample, n_buffer_samples, max_rounds, out, nullptr, rounds_done);
 }
 
-extern "C" int gnsship_trk_run_dump(gnsship_trk* t, const void* sig, int fmt, int sig_on_device, uint64_t buffer_first_sample,
-    int64_t n_buffer_samples, int max_rounds, gnsship_trk_epoch* out, gnsship_trk_dump_record* dump, int* rounds_done)
+// Enqueue a run on the context stream (the body of gnsship_trk_run_dump up to the record copies).
+static int trk_enqueue(gnsship_trk* t, const void* src, int fmt, uint64_t buffer_first_sample, int64_t n_buffer_samples, int max_rounds, bool out,
+    bool dump)
 {
-    if (!t) return GNSSHIP_E_INVAL;
     gnsship_ctx* ctx = t->ctx;
-    if (!sig || n_buffer_samples < 0 || max_rounds < 0 || fmt_bytes(fmt) == 0) return fail(ctx, GNSSHIP_E_INVAL, "gnsship_trk_run: bad arguments");
-    if (rounds_done) *rounds_done = 0;
-    if (max_rounds == 0) return GNSSHIP_OK;
-    if (int rc = set_device(ctx)) return rc;
-    if (int rc = sync_code_table(ctx)) return rc;
     int max_len = 1;
     for (const auto& cd : ctx->codes_host)
         if (cd.ptr && cd.len > max_len) max_len = cd.len;
@@ -547,32 +565,23 @@ extern "C" int gnsship_trk_run_dump(gnsship_trk* t, const void* sig, int fmt, in
         HIP_TRY(ctx, hipMemcpyAsync(t->chunks_dev, t->chunks_host.data(), sizeof(ChunkDesc) * t->n_chunks, hipMemcpyHostToDevice, ctx->stream));
         t->attached_version = ctx->codes_version;
     }
-    const void* src = sig;
-    if (!sig_on_device) {
-        const size_t bytes = fmt_bytes(fmt) * static_cast<size_t>(n_buffer_samples);
-        if (t->stage_cap < bytes) {
-            if (t->stage_dev) HIP_TRY(ctx, hipFree(t->stage_dev));
-            t->stage_dev = nullptr;
-            HIP_TRY(ctx, hipMalloc(&t->stage_dev, bytes));
-            t->stage_cap = bytes;
-        }
-        HIP_TRY(ctx, hipMemcpyAsync(t->stage_dev, sig, bytes, hipMemcpyHostToDevice, ctx->stream));
-        src = t->stage_dev;
-    }
     const size_t nrec = static_cast<size_t>(max_rounds) * t->max_channels;
     if (dump && t->dump_cap < nrec) {
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
         if (t->dump_dev) HIP_TRY(ctx, hipFree(t->dump_dev));
         t->dump_dev = nullptr;
         HIP_TRY(ctx, hipMalloc(&t->dump_dev, sizeof(gnsship_trk_dump_record) * nrec));
         t->dump_cap = nrec;
     }
     if (out && t->rec_cap < nrec) {
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
         if (t->rec_dev) HIP_TRY(ctx, hipFree(t->rec_dev));
         t->rec_dev = nullptr;
         HIP_TRY(ctx, hipMalloc(&t->rec_dev, sizeof(gnsship_trk_epoch) * nrec));
         t->rec_cap = nrec;
     }
     if (t->ran_cap < static_cast<size_t>(max_rounds) + 1) {
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
         if (t->ran_dev) HIP_TRY(ctx, hipFree(t->ran_dev));
         t->ran_dev = nullptr;
         HIP_TRY(ctx, hipMalloc(&t->ran_dev, sizeof(int) * (max_rounds + 1)));
@@ -582,7 +591,8 @@ extern "C" int gnsship_trk_run_dump(gnsship_trk* t, const void* sig, int fmt, in
     const int nc = t->max_channels;
     const bool avx = t->params.conf.rotator == GNSSHIP_ROTATOR_AVX;
     const int code_cap = padded_code_quads(max_len) * 4;
-    const bool persist = !t->high_dyn && trk_persist_lds_bytes(t->params, code_cap, avx) <= kTrkPersistMaxLds && !(t->force_rounds && !avx);
+    const bool persist = !t->high_dyn && trk_persist_supports(t->params) && trk_persist_lds_bytes(t->params, code_cap, avx) <= kTrkPersistMaxLds &&
+                         !(t->force_rounds && !avx);
     if (avx && !persist) return fail(ctx, GNSSHIP_E_INVAL, "gnsship_trk_run: the AVX rotator needs the persistent loop (epoch too long for LDS)");
     if (persist) {
         // records of epochs a channel did not run stay zero (flags 0), as in the round-based loop
@@ -612,11 +622,25 @@ extern "C" int gnsship_trk_run_dump(gnsship_trk* t, const void* sig, int fmt, in
             t->anchors_dev, t->partials_dev, t->out_dev, ctx->stream, GNSSHIP_STAGE_CORRELATE);  // anchors: replayed by the step kernel
         if (e != hipSuccess) return hip_fail(ctx, e, "launch_corr_batch(tracking)");
     }
+    t->pending_rounds = max_rounds;
+    t->pending_out = out;
+    t->pending_dump = dump;
+    return GNSSHIP_OK;
+}
+
+// Wait for the enqueued run and copy its records (the tail of gnsship_trk_run_dump).
+static int trk_finish(gnsship_trk* t, gnsship_trk_epoch* out, gnsship_trk_dump_record* dump, int* rounds_done)
+{
+    gnsship_ctx* ctx = t->ctx;
+    const int max_rounds = t->pending_rounds;
+    const size_t nrec = static_cast<size_t>(max_rounds) * t->max_channels;
     std::vector<int> ran(max_rounds + 1);
     HIP_TRY(ctx, hipMemcpyAsync(ran.data(), t->ran_dev, sizeof(int) * (max_rounds + 1), hipMemcpyDeviceToHost, ctx->stream));
-    if (out) HIP_TRY(ctx, hipMemcpyAsync(out, t->rec_dev, sizeof(gnsship_trk_epoch) * nrec, hipMemcpyDeviceToHost, ctx->stream));
-    if (dump) HIP_TRY(ctx, hipMemcpyAsync(dump, t->dump_dev, sizeof(gnsship_trk_dump_record) * nrec, hipMemcpyDeviceToHost, ctx->stream));
+    if (out && t->pending_out) HIP_TRY(ctx, hipMemcpyAsync(out, t->rec_dev, sizeof(gnsship_trk_epoch) * nrec, hipMemcpyDeviceToHost, ctx->stream));
+    if (dump && t->pending_dump)
+        HIP_TRY(ctx, hipMemcpyAsync(dump, t->dump_dev, sizeof(gnsship_trk_dump_record) * nrec, hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    t->pending_rounds = -1;
     if (rounds_done) {
         int n = 0;
         for (int r = 0; r < max_rounds; r++)
@@ -624,4 +648,60 @@ extern "C" int gnsship_trk_run_dump(gnsship_trk* t, const void* sig, int fmt, in
         *rounds_done = n;
     }
     return GNSSHIP_OK;
+}
+
+extern "C" int gnsship_trk_run_dump(gnsship_trk* t, const void* sig, int fmt, int sig_on_device, uint64_t buffer_first_sample,
+    int64_t n_buffer_samples, int max_rounds, gnsship_trk_epoch* out, gnsship_trk_dump_record* dump, int* rounds_done)
+{
+    if (!t) return GNSSHIP_E_INVAL;
+    gnsship_ctx* ctx = t->ctx;
+    if (!sig || n_buffer_samples < 0 || max_rounds < 0 || fmt_bytes(fmt) == 0) return fail(ctx, GNSSHIP_E_INVAL, "gnsship_trk_run: bad arguments");
+    if (t->pending_rounds >= 0) return fail(ctx, GNSSHIP_E_STATE, "gnsship_trk_run: a gnsship_trk_launch is still pending (gnsship_trk_collect first)");
+    if (rounds_done) *rounds_done = 0;
+    if (max_rounds == 0) return GNSSHIP_OK;
+    if (int rc = set_device(ctx)) return rc;
+    if (int rc = sync_code_table(ctx)) return rc;
+    const void* src = sig;
+    if (!sig_on_device) {
+        const size_t bytes = fmt_bytes(fmt) * static_cast<size_t>(n_buffer_samples);
+        if (t->stage_cap < bytes) {
+            HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+            if (t->stage_dev) HIP_TRY(ctx, hipFree(t->stage_dev));
+            t->stage_dev = nullptr;
+            HIP_TRY(ctx, hipMalloc(&t->stage_dev, bytes));
+            t->stage_cap = bytes;
+        }
+        HIP_TRY(ctx, hipMemcpyAsync(t->stage_dev, sig, bytes, hipMemcpyHostToDevice, ctx->stream));
+        src = t->stage_dev;
+    }
+    if (int rc = trk_enqueue(t, src, fmt, buffer_first_sample, n_buffer_samples, max_rounds, out != nullptr, dump != nullptr)) {
+        t->pending_rounds = -1;
+        return rc;
+    }
+    return trk_finish(t, out, dump, rounds_done);
+}
+
+extern "C" int gnsship_trk_launch(gnsship_trk* t, const void* dev_sig, int fmt, uint64_t buffer_first_sample, int64_t n_buffer_samples,
+    int max_rounds, int want_records, int want_dump)
+{
+    if (!t) return GNSSHIP_E_INVAL;
+    gnsship_ctx* ctx = t->ctx;
+    if (!dev_sig || n_buffer_samples < 0 || max_rounds < 1 || fmt_bytes(fmt) == 0)
+        return fail(ctx, GNSSHIP_E_INVAL, "gnsship_trk_launch: bad arguments (device buffer, max_rounds >= 1)");
+    if (t->pending_rounds >= 0) return fail(ctx, GNSSHIP_E_STATE, "gnsship_trk_launch: the previous launch was not collected");
+    if (int rc = set_device(ctx)) return rc;
+    if (int rc = sync_code_table(ctx)) return rc;
+    if (int rc = trk_enqueue(t, dev_sig, fmt, buffer_first_sample, n_buffer_samples, max_rounds, want_records != 0, want_dump != 0)) {
+        t->pending_rounds = -1;
+        return rc;
+    }
+    return GNSSHIP_OK;
+}
+
+extern "C" int gnsship_trk_collect(gnsship_trk* t, gnsship_trk_epoch* out, gnsship_trk_dump_record* dump, int* rounds_done)
+{
+    if (!t) return GNSSHIP_E_INVAL;
+    if (t->pending_rounds < 0) return fail(t->ctx, GNSSHIP_E_STATE, "gnsship_trk_collect: nothing launched");
+    if (int rc = set_device(t->ctx)) return rc;
+    return trk_finish(t, out, dump, rounds_done);
 }

@@ -51,6 +51,12 @@ struct TrkParams {
     // job layout
     int32_t jobs_per_channel;  // 1, or 2 with the E1 data prompt
     int32_t chunks_per_job;
+    // carrier IF fused into the correlator NCO (gnsship_trk_conf::if_hz): 2π·if_hz/fs, and the IF phase
+    // per sample as the exact fraction if_mod / fs_int of a cycle (0 ≤ if_mod < fs_int)
+    int32_t has_if;
+    int32_t pad_if;
+    double if_step_rad;
+    int64_t if_mod, fs_int;
 };
 
 struct Smoother {
@@ -92,6 +98,9 @@ struct TrkChannel {
     // high_dyn (:1205-1255): the smoothed NCO rates and the ring state of TrkHist
     double carrier_phase_rate_step_rad, code_phase_rate_step_chips;
     int32_t hist_head, hist_count;
+    // IF phase at nitems_read: if_num / fs_int cycles exactly (if_cyc = that quotient in double)
+    int64_t if_num;
+    double if_cyc;
 };
 
 // high_dyn: d_carr_ph_history and d_code_ph_history of one channel (boost::circular_buffer of
@@ -118,6 +127,13 @@ hipError_t launch_trk_step(const TrkParams* params, TrkChannel* chans, int n_cha
 // buffer within one launch (standard correlator only; not high_dyn).  code_cap_floats: LDS floats per
 // code replica (padded_code_quads(max code length) · 4).  LDS bytes of the dynamic region:
 size_t trk_persist_lds_bytes(const TrkParams& p, int code_cap_floats, bool avx);
+// Tap layouts the persistent kernel is instantiated for (3 or 5 taps, the E1 data prompt with 5);
+// others run the round-based loop (generic rotator only).
+inline bool trk_persist_supports(const TrkParams& p)
+{
+    const bool data = p.jobs_per_channel > 1;
+    return (p.n_taps == 3 && !data) || (p.n_taps == 5 && !data) || (p.n_taps == 5 && data);
+}
 constexpr size_t kTrkPersistMaxLds = 150 * 1024;  // of the 160 KiB per CU, beside the static state
 hipError_t launch_trk_persist(const TrkParams* params_dev, const TrkParams& params, TrkChannel* chans, int n_chans, const CodeDesc* codes,
     int n_codes, int code_cap_floats, const void* samples, int fmt, uint64_t buf_first, int64_t buf_len, int max_rounds, gnsship_trk_epoch* rec,

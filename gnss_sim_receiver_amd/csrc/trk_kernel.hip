@@ -34,8 +34,8 @@ namespace {
 __device__ void fill_job(DevJob& j, const TrkParams& k, const TrkChannel& c, int64_t offset, int code_id, int n_taps, const float* shifts)
 {
     const float spcf = static_cast<float>(k.code_samples_per_chip);
-    const float rem_carr = c.rem_carr_phase_rad;
-    const float step = static_cast<float>(c.carrier_phase_step_rad);
+    const float rem_carr = corr_rem_carr(k, c);
+    const float step = corr_phase_step(k, c);
     const float p0r = cos_f32_rn(rem_carr), p0i = -sin_f32_rn(rem_carr);
     const float incr = cos_f32_rn(-step), inci = sin_f32_rn(-step);
     j.sample_offset = offset;
@@ -60,8 +60,8 @@ __device__ void fill_job(DevJob& j, const TrkParams& k, const TrkChannel& c, int
 __device__ void fill_hd_job(HdJob& j, const TrkParams& k, const TrkChannel& c, int64_t offset, int n_taps, const float* shifts)
 {
     const float spcf = static_cast<float>(k.code_samples_per_chip);
-    const float rem_carr = c.rem_carr_phase_rad;
-    const float step = static_cast<float>(c.carrier_phase_step_rad);
+    const float rem_carr = corr_rem_carr(k, c);
+    const float step = corr_phase_step(k, c);
     const float rate = static_cast<float>(c.carrier_phase_rate_step_rad);
     j.sample_offset = offset;
     j.n_samples = static_cast<int32_t>(k.conf.vector_length);

@@ -637,8 +637,10 @@ __device__ void epoch_post(const TrkParams& k, TrkChannel& c, const float* taps,
     if (k.sync[c.geo].extend > 1) c.state = 3;  // next coherent integration cycle
 }
 
+__device__ __forceinline__ void advance_if(const TrkParams& k, TrkChannel& c, int32_t consumed);
+
 // The record's loop outputs and consume_each (:2061); false when the channel stopped (loss of lock).
-__device__ bool epoch_finish(TrkChannel& c, gnsship_trk_epoch& rec)
+__device__ bool epoch_finish(const TrkParams& k, TrkChannel& c, gnsship_trk_epoch& rec)
 {
     if (c.pll_180) rec.flags |= 4;
     rec.code_phase_samples = c.rem_code_phase_samples;
@@ -652,7 +654,28 @@ __device__ bool epoch_finish(TrkChannel& c, gnsship_trk_epoch& rec)
     rec.prn_length_samples = c.current_prn_length_samples;
     if (rec.flags & 2) return false;
     c.nitems_read = c.epoch_start + static_cast<uint64_t>(c.current_prn_length_samples);  // consume_each (:2061)
+    advance_if(k, c, c.current_prn_length_samples);
     return true;
+}
+
+// The IF phase follows the consumed samples (gnsship_trk_conf::if_hz): if_num += if_mod·len (mod fs).
+__device__ __forceinline__ void advance_if(const TrkParams& k, TrkChannel& c, int32_t consumed)
+{
+    if (!k.has_if) return;
+    c.if_num = (c.if_num + k.if_mod * static_cast<int64_t>(consumed)) % k.fs_int;
+    c.if_cyc = static_cast<double>(c.if_num) / static_cast<double>(k.fs_int);
+}
+
+// do_correlation_step's carrier arguments with the IF fused in (include/gnsship.h if_hz): the
+// correlator wipes off IF + Doppler, the loop keeps the IF-free quantities.
+__device__ __forceinline__ float corr_rem_carr(const TrkParams& k, const TrkChannel& c)
+{
+    if (!k.has_if) return c.rem_carr_phase_rad;
+    return static_cast<float>(fmod(static_cast<double>(c.rem_carr_phase_rad) + kTwoPi * c.if_cyc, kTwoPi));
+}
+__device__ __forceinline__ float corr_phase_step(const TrkParams& k, const TrkChannel& c)
+{
+    return static_cast<float>(c.carrier_phase_step_rad + k.if_step_rad);  // + 0.0 without IF: exact
 }
 
 // The phases in the reference's order on one lane (the round-based step kernel).
@@ -666,7 +689,7 @@ __device__ bool epoch_update(const TrkParams& k, TrkChannel& c, const float* tap
         if (locked) epoch_loop(k, c, h);
         epoch_post(k, c, taps, pdata, rec, locked, dump);
     }
-    return epoch_finish(c, rec);
+    return epoch_finish(k, c, rec);
 }
 
 }  // namespace

@@ -65,7 +65,6 @@ namespace {
 
 constexpr int kPThreads = 256;
 constexpr int kPWaves = kPThreads / kWave;
-constexpr int kAvxLanes = 16;  // phasors of the AVX rotator (volk_gnsssdr_32fc_32f_rotator_dot_prod_32fc_xn.h:199-213)
 constexpr int kAvxSeg = 64;    // its renormalisation period in 16-sample iterations (:265-272)
 
 // The epoch being correlated (LDS): the reference's call arguments as a DevJob plus the AVX step.
@@ -82,23 +81,6 @@ struct PEpoch {
     gnsship_trk_epoch rec;
     gnsship_trk_dump_record dump;
 };
-
-// Complex product rounded exactly as the reference's written-out (ac − bd, ad + bc): two packed
-// products and one packed add, no contraction (fl(x + fl(−y)) ≡ fl(x − y)).
-__device__ __forceinline__ f2 cmul_exact(f2 a, f2 b)
-{
-    const f2 t = f2{a.x, a.x} * b;
-    const f2 u = f2{a.y, a.y} * f2{-b.y, b.x};
-    return t + u;
-}
-
-// _mm256_complexnormalise_ps (volk_gnsssdr_avx_intrinsics.h:56-63): z / sqrt(re² + im²), IEEE sqrt
-// and division.
-__device__ __forceinline__ f2 normalise_avx(f2 z)
-{
-    const float m = __fsqrt_rn(__fadd_rn(__fmul_rn(z.x, z.x), __fmul_rn(z.y, z.y)));
-    return f2{__fdiv_rn(z.x, m), __fdiv_rn(z.y, m)};
-}
 
 // The publishing wave's LDS operations complete in program order, so a counter stored after the
 // data it announces lands after it: a relaxed store behind a wavefront-scope fence (which only
@@ -264,16 +246,6 @@ __device__ void consume_generic(PEpoch& ep, const Anchor* A, i4v span, int N, co
         for (int t = 0; t < NT; t++) acc[t] += ap[t];
         if constexpr (DATA) acc[NT] += ad[0];
     }
-}
-
-// Chip index of tap shift `sh` at sample n: floor(step·(float)n + shift − rem), each operation
-// rounded in the reference's order (volk_gnsssdr_32f_xn_resampler_32f_xn.h:63-80).
-template <bool IN_MARGIN>
-__device__ __forceinline__ float code_at(const float* code, int L, float sn, float sh, float rem)
-{
-    int i = cvt_floor_i32(__fsub_rn(__fadd_rn(sn, sh), rem));
-    if constexpr (!IN_MARGIN) i = wrap_index(i, L);
-    return code[i];
 }
 
 // AVX: wave step g = tasks 4g..4g+3 × the 16 phasors (64 lanes: lane = 16·(t − 4g) + l), each lane
@@ -470,7 +442,7 @@ __global__ __launch_bounds__(kPThreads, persist_waves_per_simd<THRU>()) void trk
 #endif
             // the epoch's two phasors (cpu_multicorrelator_real_codes.cc:115,123), lane 0: rem_carr,
             // lane 1: −step, each as the once-rounded double cos/sin (nco_math.h)
-            const float a = lane == 0 ? sc.rem_carr_phase_rad : -static_cast<float>(sc.carrier_phase_step_rad);
+            const float a = lane == 0 ? corr_rem_carr(k, sc) : -corr_phase_step(k, sc);
             double sd, cd;
             sincos(static_cast<double>(a), &sd, &cd);
             const float sf = static_cast<float>(sd), cf = static_cast<float>(cd);
@@ -571,7 +543,7 @@ __global__ __launch_bounds__(kPThreads, persist_waves_per_simd<THRU>()) void trk
                 if (locked) store_regs(lr, sc);
                 epoch_post(k, sc, taps, pdata, ep.rec, locked, dr);
             }
-            epoch_finish(sc, ep.rec);
+            epoch_finish(k, sc, ep.rec);
             const size_t slot = static_cast<size_t>(e) * n_chans + ch;
             if (rec) rec[slot] = ep.rec;
             if (dump && (ep.rec.flags & 16)) dump[slot] = ep.dump;

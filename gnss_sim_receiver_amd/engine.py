@@ -527,6 +527,24 @@ class DllPllVemlTracking:
                                                 None, None, ctypes.byref(done)), "gnsship_trk_run_dump", self.ctx.h)
         return done.value
 
+    def launch_ptr(self, dev_ptr: int, fmt: int, buffer_first_sample: int, n_buffer_samples: int, max_rounds: int,
+                   records: bool = False, dump: bool = False):
+        """gnsship_trk_launch: enqueue the run on this engine's context stream and return at once
+        (engines on other contexts of the same device run concurrently); :meth:`collect` waits."""
+        check(self.ctx.lib.gnsship_trk_launch(self.h, ctypes.c_void_p(dev_ptr), fmt, buffer_first_sample, n_buffer_samples, max_rounds,
+                                              int(records), int(dump)), "gnsship_trk_launch", self.ctx.h)
+        self._pending = (max_rounds, records, dump)
+
+    def collect(self):
+        """gnsship_trk_collect for the last launch_ptr: (records or None, rounds_done[, dump])."""
+        max_rounds, records, dump = self._pending
+        out = np.zeros((max_rounds, self.max_channels), abi.TRK_EPOCH_DTYPE) if records else None
+        dmp = np.zeros((max_rounds, self.max_channels), abi.TRK_DUMP_DTYPE) if dump else None
+        done = ctypes.c_int()
+        check(self.ctx.lib.gnsship_trk_collect(self.h, out.ctypes.data if records else None, dmp.ctypes.data if dump else None,
+                                               ctypes.byref(done)), "gnsship_trk_collect", self.ctx.h)
+        return (out, done.value, dmp) if dump else (out, done.value)
+
     def states(self) -> np.ndarray:
         """Tracking state (0 idle/lost, 2, 3, 4) of every channel."""
         return np.array([self.channel_state(ch)[0] for ch in range(self.max_channels)], np.int32)

@@ -38,7 +38,9 @@
 extern "C" {
 #endif
 
-#define GNSSHIP_ABI_VERSION 1
+/* 2: gnsship_trk_conf gained `rotator` and `if_hz` (a caller built against version 1 passes a shorter
+ * struct — bindings compare gnsship_abi_version() with the header they were built from at load time). */
+#define GNSSHIP_ABI_VERSION 2
 
 /* ---- status codes (reference: bool-always-true + LOG/throw; here explicit) ---- */
 #define GNSSHIP_OK 0
@@ -60,22 +62,30 @@ extern "C" {
  * (volk_gnsssdr_rank_archs.c): the generic C kernel (:66-98; VOLK_GENERIC set, or no AVX) or the
  * u_avx/a_avx kernel (:155-316; any AVX host without a volk_gnsssdr_config override): 16 phasors
  * advanced by normalise(inc^16), renormalised every 64 iterations.  The two differ by up to 1e-2
- * relative at 50 Msps with a 7 MHz IF, so the engine reproduces either one exactly (phasors
- * bit-identical), selected per job / per tracking engine. */
+ * relative at 50 Msps with a 7 MHz IF, so the engine reproduces either one, selected per job / per
+ * tracking engine.  Generic: the phasor at every renormalisation point is bit-identical, inside a
+ * 256-sample block the engine applies the exact lane rotation (the reference's own ≤255-step rounding
+ * walk, ~1e-6, is the only difference).  AVX: all 16 phasor lanes are replayed and continued with the
+ * reference's float products, so every phasor is bit-identical (batch jobs and tracking engines).
+ * Default in every binding (Python TrkConf.defaults, the C++ mirror's Dll_Pll_Conf, tools/gnsship_rx):
+ * GNSSHIP_ROTATOR_AUTO, i.e. what the reference itself would run on this host. */
 #define GNSSHIP_ROTATOR_GENERIC 0
 #define GNSSHIP_ROTATOR_AVX 1
 #define GNSSHIP_ROTATOR_AUTO (-1) /* what volk_gnsssdr dispatches on this host (gnsship_rotator_dispatch) */
 /* gnsship_corr_job::flags bits */
 #define GNSSHIP_JOB_HIGH_DYN 1     /* high-dynamics resampler + rotator (set_high_dynamics_resampler) */
 #define GNSSHIP_JOB_ROTATOR_AVX 2  /* the AVX rotator variant (ignored with GNSSHIP_JOB_HIGH_DYN) */
-/* Batch jobs with GNSSHIP_JOB_ROTATOR_AVX replay phasor lanes 0-3 exactly and derive lanes 4-15 from
- * them: within 1e-5 of the reference up to N = 50000 at zero IF; 2.3e-5 measured at N = 50000 with a
- * 7 MHz IF (the reference's lanes round independently).  The tracking engine replays all 16. */
 /* The variant volk_gnsssdr's dispatcher would select for the rotator dot-product on this host:
  * VOLK_GENERIC set in the environment -> generic; an entry for the kernel in the volk_gnsssdr
- * preferences file ($VOLK_CONFIGPATH or $HOME/.volk_gnsssdr/volk_gnsssdr_config) -> that entry;
- * otherwise the AVX variant when the CPU has AVX.  *variant = GNSSHIP_ROTATOR_GENERIC / _AVX. */
+ * preferences file ($VOLK_CONFIGPATH or $HOME/.volk_gnsssdr/volk_gnsssdr_config) -> that entry
+ * (its aligned and unaligned names are taken as the same variant: a_avx / u_avx and generic are
+ * reproduced; any other entry, e.g. generic_reload, returns GNSSHIP_E_INVAL naming it in
+ * gnsship_rotator_dispatch_detail); otherwise the AVX variant when the CPU has AVX.
+ * *variant = GNSSHIP_ROTATOR_GENERIC / _AVX. */
 int gnsship_rotator_dispatch(int* variant);
+/* What the last gnsship_rotator_dispatch call on this thread matched (the environment, the
+ * preferences file and its entry, or the CPU), as text. */
+int gnsship_rotator_dispatch_detail(char* buf, int cap);
 
 typedef struct gnsship_ctx gnsship_ctx;
 typedef struct gnsship_corr gnsship_corr;
@@ -330,6 +340,17 @@ typedef struct gnsship_trk_conf { /* Dll_Pll_Conf (dll_pll_conf.h:33-80), same n
     uint32_t smoother_length;        /* rate smoother length, 1..64 (0 is raised to 1, dll_pll_conf.cc:118-123) */
     int32_t rotator;                 /* GNSSHIP_ROTATOR_*: which volk_gnsssdr rotator variant the correlations
                                         reproduce (0 = generic; high_dyn has only the generic variant) */
+    int32_t reserved0;               /* 0 */
+    /* ABI 2.  Carrier IF of this engine's signal in the IF buffer [Hz] (e.g. +7.161e6 for GPS L1 / Galileo
+     * E1 and −7.161e6 for BeiDou B1I in a 1568.259 MHz-centred front end).  The reference removes it
+     * ahead of the channels (InputFilter.IF → freq_xlating_fir_filter, conf/gnss-sdr_BDS_B3I_GPS_L1_CA_
+     * ibyte.conf:45-92; GNSSFlowgraph connects the filtered output to every channel); here it is fused
+     * into the correlator's carrier NCO: phase_step = (float)(carrier_phase_step_rad + 2π·if_hz/fs) and
+     * rem_carrier_phase = (float)fmod(rem_carr_phase_rad + 2π·frac(if_hz·n/fs), 2π) at the epoch's first
+     * absolute sample n (frac(if_hz·n/fs) carried per channel in double, exact for integer if_hz and
+     * fs).  The loop, its Doppler, carrier phase and all outputs stay IF-free, as in the reference.
+     * 0 = the buffer is at baseband. */
+    double if_hz;
 } gnsship_trk_conf;
 
 typedef struct gnsship_trk_start_args { /* Gnss_Synchro fields start_tracking reads (:647-649) */
@@ -403,6 +424,15 @@ typedef struct gnsship_trk_dump_record {
  * records of the epochs flagged 16. */
 int gnsship_trk_run_dump(gnsship_trk* t, const void* sig, int fmt, int sig_on_device, uint64_t buffer_first_sample, int64_t n_buffer_samples,
     int max_rounds, gnsship_trk_epoch* out, gnsship_trk_dump_record* dump, int* rounds_done);
+/* Asynchronous form: enqueue the run on the context stream and return (dev_sig: a device buffer that
+ * stays valid until gnsship_trk_collect); records / dump records are kept on the device when
+ * requested.  Engines on different contexts of one device then run concurrently from one host
+ * thread (e.g. a hybrid receiver's GPS, Galileo and BeiDou engines over one IF block).  Every launch
+ * is followed by exactly one gnsship_trk_collect, which waits for it and copies the records
+ * (out / dump as in gnsship_trk_run_dump, NULL to skip). */
+int gnsship_trk_launch(gnsship_trk* t, const void* dev_sig, int fmt, uint64_t buffer_first_sample, int64_t n_buffer_samples, int max_rounds,
+    int want_records, int want_dump);
+int gnsship_trk_collect(gnsship_trk* t, gnsship_trk_epoch* out, gnsship_trk_dump_record* dump, int* rounds_done);
 int gnsship_trk_channel_state(gnsship_trk* t, int channel, int* state, uint64_t* next_sample);
 int gnsship_trk_destroy(gnsship_trk* t);
 

@@ -50,6 +50,10 @@ public:
 private:
     explicit Device(int device)
     {
+        // the library must implement the structs this header was compiled against (gnsship.h ABI notes)
+        if (gnsship_abi_version() != GNSSHIP_ABI_VERSION)
+            throw std::runtime_error("gnsship: libgnsship ABI " + std::to_string(gnsship_abi_version()) + ", header " +
+                                     std::to_string(GNSSHIP_ABI_VERSION));
         if (gnsship_ctx_create(device, &ctx_) != GNSSHIP_OK) throw std::runtime_error("gnsship: no HIP device " + std::to_string(device));
     }
     gnsship_ctx* ctx_ = nullptr;
@@ -600,6 +604,9 @@ struct Dll_Pll_Conf {
     // Not a Dll_Pll_Conf member: the reference's correlations follow the volk_gnsssdr rotator variant
     // its dispatcher picks on the host (volk_gnsssdr_rank_archs.c); AUTO makes the same choice.
     int32_t rotator{GNSSHIP_ROTATOR_AUTO};
+    // Not a Dll_Pll_Conf member either: InputFilter<i>.IF of the signal's conditioner (the reference removes
+    // it ahead of the channels; here the correlator NCO wipes it off, gnsship.h if_hz).
+    double if_hz{0.0};
 };
 
 // Mirror of dll_pll_veml_tracking (gnuradio_blocks/dll_pll_veml_tracking.cc) for many channels on one
@@ -645,6 +652,7 @@ public:
         c.high_dyn = conf.high_dyn ? 1 : 0;
         c.smoother_length = conf.smoother_length;
         c.rotator = conf.rotator;
+        c.if_hz = conf.if_hz;
         c.system = conf.system == 'E' ? GNSSHIP_SYS_GAL_E1 : conf.system == 'C' ? GNSSHIP_SYS_BDS_B1I : GNSSHIP_SYS_GPS_L1CA;
         code_base_ = 1024 + 2 * max_channels * next_engine_id();
         std::lock_guard<std::mutex> lk(dev_->mutex());

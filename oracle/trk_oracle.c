@@ -348,6 +348,13 @@ typedef struct {
                                  orc_rotator_dot_prod_acc64) */
     int32_t cr_trig;          /* test-only: phasors from double cos/sin rounded to float (the device loop's
                                  nco_math.h) instead of glibc cosf/sinf */
+    int32_t pad_if;
+    /* Carrier IF of the signal in the buffer [Hz], whole Hz (with a whole-Hz fs_in).  The reference removes
+     * it ahead of the channels (InputFilter.IF, freq_xlating_fir_filter; conf/gnss-sdr_BDS_B3I_GPS_L1_CA_
+     * ibyte.conf:45-92) so its tracking sees the IF-free signal; this restatement (like the engine, see
+     * include/gnsship.h if_hz) folds it into the correlation arguments instead: carr_step + 2π·if/fs, and
+     * rem_carr + 2π·frac(if·n/fs) at the epoch's first absolute sample n.  The loop itself is unchanged. */
+    double if_hz;
 } orc_trk_conf;
 
 #define TRK_MAX_SMOOTHER 64
@@ -380,7 +387,16 @@ typedef struct {
     double hist_carr[2 * TRK_MAX_SMOOTHER], hist_code[2 * TRK_MAX_SMOOTHER], hist_samples[2 * TRK_MAX_SMOOTHER];
     int hist_head, hist_count;
     uint32_t prn; /* Gnss_Synchro::PRN (dump records) */
+    int64_t if_num; /* IF phase at nitems_read = if_num / fs cycles, exactly */
 } orc_trk_channel;
+
+/* (if·n) mod fs for whole-Hz if and fs, exact (if reduced into [0, fs) first). */
+static int64_t orc_if_num(const orc_trk_conf* k, uint64_t n)
+{
+    const int64_t fs = (int64_t)k->fs_in;
+    const int64_t ifm = (((int64_t)k->if_hz % fs) + fs) % fs;
+    return (int64_t)(((unsigned __int128)(uint64_t)ifm * (n % (uint64_t)fs)) % (uint64_t)fs);
+}
 
 /* The tracking dump record log_data writes field by field (dll_pll_veml_tracking.cc:1376-1466;
  * read back by tracking_dump_reader.cc:26-47): 96 bytes, no padding. */
@@ -478,6 +494,7 @@ void orc_trk_start(const orc_trk_conf* k, orc_trk_channel* c, double acq_delay_s
     orc_sm_reset(&c->cn0_sm);
     orc_sm_reset(&c->lock_sm);
     c->nitems_read = first_sample + (uint64_t)samples_offset;
+    c->if_num = k->if_hz != 0.0 ? orc_if_num(k, c->nitems_read) : 0;
 }
 
 /* do_correlation_step arguments (:1037-1062) for the next epoch: the float values passed to
@@ -488,6 +505,11 @@ void orc_trk_correlation_args(const orc_trk_conf* k, const orc_trk_channel* c, f
     const float spcf = (float)k->code_samples_per_chip;
     out[0] = c->rem_carr_phase_rad;
     out[1] = (float)c->carrier_phase_step_rad;
+    if (k->if_hz != 0.0) { /* the IF folded into the carrier arguments (orc_trk_conf::if_hz) */
+        const double fs = (double)(int64_t)k->fs_in;
+        out[0] = (float)fmod((double)c->rem_carr_phase_rad + TRK_TWO_PI * ((double)c->if_num / fs), TRK_TWO_PI);
+        out[1] = (float)(c->carrier_phase_step_rad + TRK_TWO_PI * k->if_hz / k->fs_in);
+    }
     out[2] = (float)c->carrier_phase_rate_step_rad;
     out[3] = (float)c->rem_code_phase_chips * spcf;
     out[4] = (float)c->code_phase_step_chips * spcf;
@@ -867,6 +889,10 @@ int orc_trk_epoch_update(const orc_trk_conf* k, orc_trk_channel* c, const float*
     rec->prn_length_samples = c->current_prn_length_samples;
     if (loss) return 0;
     c->nitems_read += (uint64_t)c->current_prn_length_samples; /* consume_each (:2061) */
+    if (k->if_hz != 0.0) {
+        const int64_t fs = (int64_t)k->fs_in;
+        c->if_num = (c->if_num + ((((int64_t)k->if_hz % fs) + fs) % fs) * (int64_t)c->current_prn_length_samples) % fs;
+    }
     return 1;
 }
 

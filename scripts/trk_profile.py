@@ -16,7 +16,7 @@ def main():
     sats = signals.random_sky(32, seed=1)
     x = signals.generate_if(fs, vl * (rounds + 8), sats, seed=1)
     ctx = engine.Context(0)
-    trk = engine.DllPllVemlTracking(ctx, abi.TrkConf.defaults(abi.SYS_GPS_L1CA, fs, vl), n_ch)
+    trk = engine.DllPllVemlTracking(ctx, abi.TrkConf.defaults(abi.SYS_GPS_L1CA, fs, vl, rotator=abi.ROTATOR_GENERIC), n_ch)
     for i, s in enumerate(sats):
         ctx.set_code(i, s.code)
     for ch in range(n_ch):

@@ -296,9 +296,27 @@ def test_batch_avx_rotator_vs_oracle(ctx, fs, ntaps, system):
     assert not np.array_equal(ref[avx], ref_gen[avx])
 
 
+@pytest.mark.parametrize("n", [7, 15, 16, 17, 255, 1023, 4096, 4104, 8200, 12345])
+def test_batch_avx_rotator_lengths(ctx, n):
+    """AVX-variant edge lengths: no whole iteration (N < 16: all tail), one iteration, tasks ending
+    mid-chunk, the N mod 16 tail alone in a new 4096-sample chunk (4104 = 256·16 + 8), several chunks;
+    50 Msps with a 7 MHz IF (large phase steps) beside a zero-IF job."""
+    fs = 50e6
+    sats = signals.random_sky(2, seed=n, system="GPS")
+    sats[0].f_if_hz = 7.161e6
+    sig = signals.generate_if(fs, 3 * 50000 + n + 64, sats, seed=n + 1)  # epochs start at code-period boundaries (≤ 2 ms)
+    jobs = np.concatenate([signals.truth_jobs(s, fs, 2, n, [-0.25, 0.0, 0.25], k, first_epoch=0) for k, s in enumerate(sats)])
+    jobs["flags"] = abi.JOB_ROTATOR_AVX
+    cl = [s.code for s in sats]
+    out = engine.correlate_host(ctx, sig, jobs, cl)
+    ref = O.corr_batch(sig, jobs, cl, n_threads=4)
+    for j in range(len(jobs)):
+        assert rel_err(out[j, :3], ref[j, :3]) <= TOL, (n, j, rel_err(out[j, :3], ref[j, :3]))
+
+
 def test_pipelined_ring_avx_jobs_match_plain_launches(ctx):
-    """AVX-variant jobs through the pipelined ring (replay split at the middle block, resumed from the
-    stored four phasors) give exactly the plain launch results; odd block counts and one-block jobs."""
+    """AVX-variant jobs through the pipelined ring (replay split at the middle task, resumed from the
+    stored 16 phasors) give exactly the plain launch results; odd task counts and one-task jobs."""
     fs = 4e6
     sats = signals.random_sky(6, seed=61)
     sig = signals.generate_if(fs, 4000 * 30, sats, seed=62)

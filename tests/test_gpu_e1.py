@@ -14,7 +14,7 @@ relative to max(|ref|, ‖x‖₂) (‖x‖₂ only matters for a tap at the noi
 import numpy as np
 import pytest
 
-from gnss_sim_receiver_amd import engine, signals
+from gnss_sim_receiver_amd import abi, engine, signals
 from oracle import oracle as O
 
 pytestmark = pytest.mark.gpu
@@ -82,12 +82,14 @@ def test_c5_e1_ibyte_50msps(ctx):
     check(out, as_float, jobs, cl)
 
 
-def test_c5_hybrid_batch_one_launch(ctx):
+@pytest.mark.parametrize("flags", [0, abi.JOB_ROTATOR_AVX])
+def test_c5_hybrid_batch_one_launch(ctx, flags):
     """configs[4]'s per-GPU mix in ONE batched launch from the 50 Msps ibyte block: GPS L1 C/A
     E/P/L (N = 50000) and Galileo E1 5 VEML pilot taps + data prompt (N = 200000) at IF +7.161 MHz,
     BeiDou B1I E/P/L (N = 50000, 2046-chip code) at −7.161 MHz (the 1568.259 MHz centre, SURVEY §8d
     C5).  Each job against the oracle on the same int8 samples (converted without scaling, as
-    IbyteToComplex, ibyte_to_complex.cc:39)."""
+    IbyteToComplex, ibyte_to_complex.cc:39), for the generic and the AVX rotator variant (the AVX
+    batch path continues all 16 phasor lanes bit-exactly)."""
     fs, f_if = 50e6, 7.161e6
     gps = signals.random_sky(3, seed=551, system="GPS", cn0=48.0, prns=[3, 11, 27])
     gal = signals.random_sky(2, seed=552, system="GAL", cn0=48.0, prns=[4, 19])
@@ -109,9 +111,41 @@ def test_c5_hybrid_batch_one_launch(ctx):
     jobs = np.concatenate(jobs + [ej])
     rng = np.random.default_rng(5)
     jobs["rem_carrier_phase_rad"] += rng.uniform(-0.3, 0.3, len(jobs)).astype(np.float32)
+    jobs["flags"] = flags
     out = engine.correlate_host(ctx, raw, jobs, cl)
     worst = check(out, as_float, jobs, cl)
     assert worst <= TOL
     # the locked prompts carry the signal (GPS / B1I prompt >> early/late noise)
     epl = out[jobs["n_taps"] == 3]
     assert np.median(np.abs(epl[:, 1]) / np.abs(epl[:, 0])) > 1.2  # ACF(0.25 chip) = 0.75 of the prompt
+
+
+def test_c5_share_32_channels_one_launch_avx(ctx):
+    """The whole per-GPU share of configs[4] (256 channels / 8 GPUs = 12 GPS + 12 E1 (5 + 1 taps) + 8
+    B1I) in one batched launch, 4 GPS / B1I epochs and one E1 epoch per channel, AVX rotator variant,
+    50 Msps ibyte with ±7.161 MHz IF — every job against the oracle."""
+    fs, f_if = 50e6, 7.161e6
+    gps = signals.random_sky(12, seed=561, system="GPS", cn0=47.0)
+    gal = signals.random_sky(12, seed=562, system="GAL", cn0=47.0, prns=list(range(1, 13)))
+    bds = signals.random_sky(8, seed=563, system="BDS", cn0=47.0, prns=list(range(6, 14)))
+    for s in gps + gal:
+        s.f_if_hz = f_if
+    for s in bds:
+        s.f_if_hz = -f_if
+    x = signals.generate_if_device(fs, 200000 * 3, gps + gal + bds, seed=57, device="cpu").numpy()
+    raw = signals.to_ibyte(x)
+    as_float = raw.astype(np.float32).view(np.complex64)
+    jobs, cl = [], []
+    for s in gps + bds:
+        cl.append(s.code)
+        jobs.append(signals.truth_jobs(s, fs, 4, 50000, [-0.25, 0.0, 0.25], len(cl) - 1))
+    ej, ecl = e1_jobs(gal, fs, 1, 200000)
+    ej["code_id"] += len(cl)
+    cl += ecl
+    jobs = np.concatenate(jobs + [ej])
+    jobs["flags"] = abi.JOB_ROTATOR_AVX
+    rng = np.random.default_rng(6)
+    jobs["rem_carrier_phase_rad"] += rng.uniform(-0.3, 0.3, len(jobs)).astype(np.float32)
+    assert len(jobs) == 4 * 20 + 24
+    out = engine.correlate_host(ctx, raw, jobs, cl)
+    assert check(out, as_float, jobs, cl) <= TOL

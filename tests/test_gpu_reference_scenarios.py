@@ -101,7 +101,7 @@ def test_pull_in_acquisition_to_tracking(ctx):
     res, _ = acq.run(x[stamp:stamp + N], n_prns=len(prns))
     thr = threshold(0.01, acq.n_bins, N)
     k = T.conf("GPS", FS, N, pull_in_time_s=0)
-    c = abi.TrkConf.defaults(abi.SYS_GPS_L1CA, FS, N, pull_in_time_s=0)
+    c = abi.TrkConf.defaults(abi.SYS_GPS_L1CA, FS, N, pull_in_time_s=0, rotator=abi.ROTATOR_GENERIC)
     trk = engine.DllPllVemlTracking(ctx, c, len(prns))
     first = 6 * N  # tracking starts two code periods after the acquisition's dwell
     for ch, (s, r) in enumerate(zip(sats, res)):

@@ -30,6 +30,8 @@ def dev_conf(k, system):
     c = abi.TrkConf.defaults(SYS[system], k.fs_in, k.vector_length)
     for f in SHARED:
         setattr(c, f, getattr(k, f))
+    c.rotator = abi.ROTATOR_AVX if k.rotator_avx else abi.ROTATOR_GENERIC  # the oracle's variant, not the host's
+    c.if_hz = k.if_hz
     if system == "GAL":
         c.track_pilot = k.track_pilot
     return c

@@ -29,15 +29,16 @@ SYNC_PATTERNS = {"GPS": dict(bits="1000101100110"), "GAL": dict(secondary=T.E1C_
                  "BDS_GEO": dict(bits="111000100100110", symbols_per_bit=2)}
 
 
-def sync(system, fs, epochs, prn=9, dop=1210.0, delay_chips=100.3, seed=5, cn0=50.0, rate_hz_s=0.0, **conf_kw):
+def sync(system, fs, epochs, prn=9, dop=1210.0, delay_chips=100.3, seed=5, cn0=50.0, rate_hz_s=0.0, f_if_hz=0.0, **conf_kw):
     """A signal carrying the pattern the block synchronises on (GPS navigation bits with the
     10001011 preamble, CS25 on the E1-C pilot, the B1I NH code), acquisition stamped one second
     before tracking starts so that pull_in_time_s = 0 ends the pull-in at once.  x[0] is absolute
-    sample `first` = fs.  rate_hz_s: Doppler ramp (the acquisition reports the Doppler at `first`)."""
+    sample `first` = fs.  rate_hz_s: Doppler ramp (the acquisition reports the Doppler at `first`).
+    f_if_hz: the signal sits at this IF in the buffer (C5's front end), the loop's conf carries it."""
     geo = system == "BDS" and T.is_bds_geo(prn)
     sat = signals.Satellite(prn=prn, doppler_hz=dop, code_delay_chips=delay_chips, cn0_dbhz=cn0, system=system, carrier_phase_rad=1.0,
-                            doppler_rate_hz_s=rate_hz_s, **SYNC_PATTERNS["BDS_GEO" if geo else system])
-    kw = dict(pull_in_time_s=0)
+                            doppler_rate_hz_s=rate_hz_s, f_if_hz=f_if_hz, **SYNC_PATTERNS["BDS_GEO" if geo else system])
+    kw = dict(pull_in_time_s=0, if_hz=f_if_hz)
     kw.update(conf_kw)
     k = T.conf(system, fs, int(round(fs * T.SYSTEMS[system][2])), prn=prn, **kw)
     first = int(fs)
