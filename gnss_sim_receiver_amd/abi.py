@@ -149,6 +149,14 @@ TRK_DUMP_DTYPE = np.dtype([
 assert TRK_DUMP_DTYPE.itemsize == 96
 TRK_FLAG_DUMP = 16
 
+# gnsship_trk_corr_trace: one channel-epoch's do_correlation_step arguments and outputs
+TRK_TRACE_DTYPE = np.dtype([
+    ("sample_counter", "<u8"), ("n_samples", "<i4"), ("n_taps", "<i4"), ("rem_carrier_phase_rad", "<f4"), ("phase_step_rad", "<f4"),
+    ("rem_code_phase_samples", "<f4"), ("code_phase_step_samples", "<f4"), ("shifts", "<f4", (5,)), ("taps", "<f4", (10,)),
+    ("data_prompt", "<f4", (2,)), ("pad", "<i4"),
+])
+assert TRK_TRACE_DTYPE.itemsize == 104
+
 
 class GnssHipError(RuntimeError):
     def __init__(self, code: int, what: str):
@@ -221,6 +229,8 @@ _SIGNATURES = {
     "gnsship_trk_run_dump": ([_vp, _vp, _i, _i, ctypes.c_uint64, ctypes.c_int64, _i, _vp, _vp, ctypes.POINTER(_i)], _i),
     "gnsship_trk_launch": ([_vp, _vp, _i, ctypes.c_uint64, ctypes.c_int64, _i, _i, _i], _i),
     "gnsship_trk_collect": ([_vp, _vp, _vp, ctypes.POINTER(_i)], _i),
+    "gnsship_trk_set_trace": ([_vp, _i], _i),
+    "gnsship_trk_trace_records": ([_vp, _vp, _i], _i),
     "gnsship_trk_channel_state": ([_vp, _i, ctypes.POINTER(_i), ctypes.POINTER(ctypes.c_uint64)], _i),
     "gnsship_trk_destroy": ([_vp], _i),
     "gnsship_comm_unique_id": ([_vp], _i),

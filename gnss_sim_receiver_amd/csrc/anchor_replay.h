@@ -31,7 +31,7 @@ __device__ __forceinline__ f2v avx_cmul(f2v a, f2v b) { return f2v{a.x, a.x} * b
 // _mm256_complexnormalise_ps (volk_gnsssdr_avx_intrinsics.h:56-63): z / sqrt(re² + im²).
 __device__ __forceinline__ f2v avx_normalise(f2v z)
 {
-    const float m = __fsqrt_rn(__fadd_rn(__fmul_rn(z.x, z.x), __fmul_rn(z.y, z.y)));
+    const float m = sqrt_rn_f32(__fadd_rn(__fmul_rn(z.x, z.x), __fmul_rn(z.y, z.y)));
     return f2v{__fdiv_rn(z.x, m), __fdiv_rn(z.y, m)};
 }
 

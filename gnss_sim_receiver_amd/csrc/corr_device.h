@@ -273,11 +273,54 @@ __device__ __forceinline__ f2 cmul_exact(f2 a, f2 b)
     return t + u;
 }
 
+// The same product on a serial chain with q wave-uniform (q in an SGPR pair): six single-rate VALU
+// ops (4 cycles each for a lone wave) instead of three packed ones, whose dependent issue costs
+// several times more on gfx950 — the AVX phasor replay is a chain of these.
+// One asm block per STEPS products: the hazard recognizer pads every inline-asm boundary with an
+// s_nop, so a chain written one product per statement would pay one per product.  Within a step
+// the products read re, re, im, im and the sums come last (re − bd, ad + bc: the reference's order).
+#define GNSSHIP_CMUL_STEP                  \
+    "v_mul_f32 %2, %6, %0\n\t"             \
+    "v_mul_f32 %4, %7, %0\n\t"             \
+    "v_mul_f32 %3, %7, %1\n\t"             \
+    "v_mul_f32 %5, %6, %1\n\t"             \
+    "v_sub_f32 %0, %2, %3\n\t"             \
+    "v_add_f32 %1, %4, %5\n\t"
+template <int STEPS>
+__device__ __forceinline__ f2 cmul_chain_s(f2 a, f2 q)
+{
+    static_assert(STEPS >= 1 && STEPS <= 4, "cmul_chain_s: 1-4 steps per block");
+    float re = a.x, im = a.y, ac, bd, ad, bc;
+    if constexpr (STEPS == 1)
+        asm(GNSSHIP_CMUL_STEP : "+v"(re), "+v"(im), "=&v"(ac), "=&v"(bd), "=&v"(ad), "=&v"(bc) : "s"(q.x), "s"(q.y));
+    else if constexpr (STEPS == 2)
+        asm(GNSSHIP_CMUL_STEP GNSSHIP_CMUL_STEP : "+v"(re), "+v"(im), "=&v"(ac), "=&v"(bd), "=&v"(ad), "=&v"(bc) : "s"(q.x), "s"(q.y));
+    else if constexpr (STEPS == 3)
+        asm(GNSSHIP_CMUL_STEP GNSSHIP_CMUL_STEP GNSSHIP_CMUL_STEP
+            : "+v"(re), "+v"(im), "=&v"(ac), "=&v"(bd), "=&v"(ad), "=&v"(bc)
+            : "s"(q.x), "s"(q.y));
+    else
+        asm(GNSSHIP_CMUL_STEP GNSSHIP_CMUL_STEP GNSSHIP_CMUL_STEP GNSSHIP_CMUL_STEP
+            : "+v"(re), "+v"(im), "=&v"(ac), "=&v"(bd), "=&v"(ad), "=&v"(bc)
+            : "s"(q.x), "s"(q.y));
+    return f2{re, im};
+}
+#undef GNSSHIP_CMUL_STEP
+__device__ __forceinline__ f2 cmul_exact_s(f2 a, f2 q) { return cmul_chain_s<1>(a, q); }
+// z·q^n for n ≥ 0 as n successive exact products.
+template <int N>
+__device__ __forceinline__ f2 cmul_pow_s(f2 z, f2 q)
+{
+    if constexpr (N >= 4) return cmul_pow_s<N - 4>(cmul_chain_s<4>(z, q), q);
+    else if constexpr (N > 0) return cmul_chain_s<N>(z, q);
+    else return z;
+}
+
 // _mm256_complexnormalise_ps (volk_gnsssdr_avx_intrinsics.h:56-63): z / sqrt(re² + im²), IEEE sqrt
 // and division.
 __device__ __forceinline__ f2 normalise_avx(f2 z)
 {
-    const float m = __fsqrt_rn(__fadd_rn(__fmul_rn(z.x, z.x), __fmul_rn(z.y, z.y)));
+    const float m = sqrt_rn_f32(__fadd_rn(__fmul_rn(z.x, z.x), __fmul_rn(z.y, z.y)));
     return f2{__fdiv_rn(z.x, m), __fdiv_rn(z.y, m)};
 }
 

@@ -26,6 +26,7 @@ int chunks_per_item_setting();
 
 using namespace gnsship;
 static_assert(sizeof(gnsship_trk_epoch) == 96, "gnsship_trk_epoch layout");
+static_assert(sizeof(gnsship_trk_corr_trace) == 104, "gnsship_trk_corr_trace layout");
 static_assert(sizeof(gnsship_trk_dump_record) == 96 && offsetof(gnsship_trk_dump_record, PRN_start_sample_count) == 28 &&
                   offsetof(gnsship_trk_dump_record, aux2) == 84 && offsetof(gnsship_trk_dump_record, PRN) == 92,
     "gnsship_trk_dump_record = the log_data file record");
@@ -74,6 +75,11 @@ struct gnsship_trk {
     // gnsship_trk_launch → gnsship_trk_collect: the enqueued run's rounds (−1: none pending)
     int pending_rounds = -1;
     bool pending_out = false, pending_dump = false;
+    // gnsship_trk_set_trace: per channel-epoch correlation trace of the last run
+    bool trace_on = false;
+    gnsship_trk_corr_trace* trace_dev = nullptr;
+    size_t trace_cap = 0;
+    size_t trace_n = 0;  // records of the last run (max_rounds × max_channels)
 };
 
 namespace {
@@ -296,7 +302,7 @@ hipError_t upload_hd_code(gnsship_trk* t, int job, const CodeDesc& cd)
 void release(gnsship_trk* t)
 {
     void* ptrs[] = {t->params_dev, t->chans_dev, t->jobs_dev, t->chunks_dev, t->items_dev, t->anchors_dev, t->partials_dev, t->out_dev, t->rec_dev,
-        t->ran_dev, t->stage_dev, t->hist_dev, t->dump_dev};
+        t->ran_dev, t->stage_dev, t->hist_dev, t->dump_dev, t->trace_dev};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     hd_plan_free(t->hd);
@@ -594,13 +600,32 @@ static int trk_enqueue(gnsship_trk* t, const void* src, int fmt, uint64_t buffer
     const bool persist = !t->high_dyn && trk_persist_supports(t->params) && trk_persist_lds_bytes(t->params, code_cap, avx) <= kTrkPersistMaxLds &&
                          !(t->force_rounds && !avx);
     if (avx && !persist) return fail(ctx, GNSSHIP_E_INVAL, "gnsship_trk_run: the AVX rotator needs the persistent loop (epoch too long for LDS)");
+    gnsship_trk_corr_trace* trace = nullptr;
+    t->trace_n = 0;
+    if (t->trace_on && persist) {
+        if (t->trace_cap < nrec) {
+            HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+            if (t->trace_dev) HIP_TRY(ctx, hipFree(t->trace_dev));
+            t->trace_dev = nullptr;
+            HIP_TRY(ctx, hipMalloc(&t->trace_dev, sizeof(gnsship_trk_corr_trace) * nrec));
+            t->trace_cap = nrec;
+        }
+        HIP_TRY(ctx, hipMemsetAsync(t->trace_dev, 0, sizeof(gnsship_trk_corr_trace) * nrec, ctx->stream));
+        trace = t->trace_dev;
+        t->trace_n = nrec;
+    }
     if (persist) {
         // records of epochs a channel did not run stay zero (flags 0), as in the round-based loop
         if (out) HIP_TRY(ctx, hipMemsetAsync(t->rec_dev, 0, sizeof(gnsship_trk_epoch) * nrec, ctx->stream));
         if (dump) HIP_TRY(ctx, hipMemsetAsync(t->dump_dev, 0, sizeof(gnsship_trk_dump_record) * nrec, ctx->stream));
-        hipError_t e = launch_trk_persist(t->params_dev, t->params, t->chans_dev, nc, ctx->codes_dev, static_cast<int>(ctx->codes_host.size()),
-            code_cap, src, fmt, buffer_first_sample, n_buffer_samples, max_rounds, out ? t->rec_dev : nullptr, dump ? t->dump_dev : nullptr,
-            t->ran_dev, avx, ctx->stream);
+        const int n_codes = static_cast<int>(ctx->codes_host.size());
+        hipError_t e;
+        if (avx && trk_fast_supported(t->params, code_cap, nc))
+            e = launch_trk_fast(t->params_dev, t->params, t->chans_dev, nc, ctx->codes_dev, n_codes, code_cap, src, fmt, buffer_first_sample,
+                n_buffer_samples, max_rounds, out ? t->rec_dev : nullptr, dump ? t->dump_dev : nullptr, trace, t->ran_dev, ctx->stream);
+        else
+            e = launch_trk_persist(t->params_dev, t->params, t->chans_dev, nc, ctx->codes_dev, n_codes, code_cap, src, fmt, buffer_first_sample,
+                n_buffer_samples, max_rounds, out ? t->rec_dev : nullptr, dump ? t->dump_dev : nullptr, trace, t->ran_dev, avx, ctx->stream);
         if (e != hipSuccess) return hip_fail(ctx, e, "launch_trk_persist");
     }
     for (int r = 0; r <= max_rounds && !persist; r++) {
@@ -704,4 +729,24 @@ extern "C" int gnsship_trk_collect(gnsship_trk* t, gnsship_trk_epoch* out, gnssh
     if (t->pending_rounds < 0) return fail(t->ctx, GNSSHIP_E_STATE, "gnsship_trk_collect: nothing launched");
     if (int rc = set_device(t->ctx)) return rc;
     return trk_finish(t, out, dump, rounds_done);
+}
+
+extern "C" int gnsship_trk_set_trace(gnsship_trk* t, int enable)
+{
+    if (!t) return GNSSHIP_E_INVAL;
+    t->trace_on = enable != 0;
+    return GNSSHIP_OK;
+}
+
+extern "C" int gnsship_trk_trace_records(gnsship_trk* t, gnsship_trk_corr_trace* out, int max_records)
+{
+    if (!t) return GNSSHIP_E_INVAL;
+    gnsship_ctx* ctx = t->ctx;
+    if (!out || max_records < 0) return fail(ctx, GNSSHIP_E_INVAL, "gnsship_trk_trace_records: bad arguments");
+    if (t->trace_n == 0) return fail(ctx, GNSSHIP_E_STATE, "gnsship_trk_trace_records: no traced run (gnsship_trk_set_trace, persistent loop)");
+    if (static_cast<size_t>(max_records) < t->trace_n) return fail(ctx, GNSSHIP_E_INVAL, "gnsship_trk_trace_records: buffer smaller than the run");
+    if (int rc = set_device(ctx)) return rc;
+    HIP_TRY(ctx, hipMemcpyAsync(out, t->trace_dev, sizeof(gnsship_trk_corr_trace) * t->trace_n, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    return GNSSHIP_OK;
 }

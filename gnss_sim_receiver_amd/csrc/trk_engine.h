@@ -137,6 +137,12 @@ inline bool trk_persist_supports(const TrkParams& p)
 constexpr size_t kTrkPersistMaxLds = 150 * 1024;  // of the 160 KiB per CU, beside the static state
 hipError_t launch_trk_persist(const TrkParams* params_dev, const TrkParams& params, TrkChannel* chans, int n_chans, const CodeDesc* codes,
     int n_codes, int code_cap_floats, const void* samples, int fmt, uint64_t buf_first, int64_t buf_len, int max_rounds, gnsship_trk_epoch* rec,
-    gnsship_trk_dump_record* dump, int* ran_count, bool avx, hipStream_t stream);
+    gnsship_trk_dump_record* dump, gnsship_trk_corr_trace* trace, int* ran_count, bool avx, hipStream_t stream);
+// The latency-optimised persistent loop for the AVX rotator (trk_fast.hip): register-resident loop
+// state, flagless phasor slots, lock detectors beside the loop update.
+bool trk_fast_supported(const TrkParams& p, int code_cap_floats, int n_chans);
+hipError_t launch_trk_fast(const TrkParams* params_dev, const TrkParams& params, TrkChannel* chans, int n_chans, const CodeDesc* codes, int n_codes,
+    int code_cap_floats, const void* samples, int fmt, uint64_t buf_first, int64_t buf_len, int max_rounds, gnsship_trk_epoch* rec,
+    gnsship_trk_dump_record* dump, gnsship_trk_corr_trace* trace, int* ran_count, hipStream_t stream);
 
 }  // namespace gnsship

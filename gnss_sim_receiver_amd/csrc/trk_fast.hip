@@ -1,0 +1,758 @@
+// trk_fast.hip — the closed DLL/PLL loop with the AVX rotator variant (the one volk_gnsssdr
+// dispatches on AVX hosts), one workgroup per channel for a whole run, organised around the epoch's
+// serial critical path.
+//
+// dll_pll_veml_tracking::general_work (dll_pll_veml_tracking.cc:1728-2094) is a strictly serial
+// chain per channel: epoch k's correlations (do_correlation_step :1037-1062 →
+// Cpu_Multicorrelator_Real_Codes, volk_gnsssdr_32fc_32f_rotator_dot_prod_32fc_xn u_avx :155-316)
+// feed its loop update (cn0_and_tracking_lock_status :972-1029, run_dll_pll :1065-1152,
+// update_tracking_vars :1189-1260), which sets epoch k+1's NCO.  The rate at which one channel
+// advances is 1 / (epoch latency), so this kernel shortens the chain itself:
+//
+//  * wave 0 is the control wave.  The channel's loop state lives in its registers for the whole
+//    run (RChan, trk_loop.h) — no LDS round trip per member; it derives the epoch's correlator
+//    arguments (cos/sin of the NCO phase and step in parallel lanes), then replays the 16 AVX phasor
+//    lanes (z ← z·dz, the reference's float products) and stores each lane's phasor at every task
+//    start (G iterations, 4 for GPS at 4 Msps) with a plain LDS store — no fence, no flag: the
+//    phasor slot itself is the signal (all-ones NaN = not yet written; a phasor is never NaN);
+//  * waves 1-3 correlate: groups of four tasks, lane (task, l) polls its slot, re-arms it for the
+//    next epoch, and continues lane l's chain over the task's iterations with the same float
+//    products — every phasor bit-identical to u_avx's — correlating sample 16m + l at iteration
+//    m; groups are dealt statically (wave w takes groups w − 1 mod 3), so sums are reproducible;
+//  * after the barrier, wave 0 sums the per-wave tap sums in wave order and runs the loop update
+//    on its registers while wave 1 runs the lock detectors (lock_status) on the LDS copy of their
+//    members; wave 0 runs run_dll_pll + update_tracking_vars speculatively and keeps them only when
+//    the lock test (published by wave 1) passes, as the reference runs them only then.
+//
+// Epochs too long for the LDS task slots, the generic rotator and high_dyn stay on trk_persist.hip
+// / the round-based loop.
+#include <cstdlib>
+
+#include "corr_device.h"
+#include "trk_engine.h"
+
+#ifdef GNSSHIP_CORR_PROFILE
+namespace gnsship {
+namespace {
+constexpr int kFProfEpochs = 64;
+constexpr int kFProfSlots = 32;
+__device__ unsigned long long* g_trkf_prof = nullptr;
+__shared__ int g_fprof_epoch;
+__device__ __forceinline__ void trkf_prof_stamp(int e, int k)
+{
+    if (g_trkf_prof && e < kFProfEpochs && (threadIdx.x & 63) == 0)
+        g_trkf_prof[(static_cast<size_t>(blockIdx.x) * kFProfEpochs + e) * kFProfSlots + k] = wall_clock64();
+}
+}  // namespace
+}  // namespace gnsship
+namespace gnsship {
+__device__ __forceinline__ void trkf_prof_clock(int e, int k)
+{
+    if (g_trkf_prof && e < kFProfEpochs && (threadIdx.x & 63) == 0)
+        g_trkf_prof[(static_cast<size_t>(blockIdx.x) * kFProfEpochs + e) * kFProfSlots + k] = clock64();
+}
+}  // namespace gnsship
+namespace gnsship {
+__device__ __forceinline__ void trkf_prof_hwid(int k)  // HW_ID (wave slot, SIMD, CU, SE) of the stamping wave
+{
+    if (g_trkf_prof && (threadIdx.x & 63) == 0)
+        g_trkf_prof[static_cast<size_t>(blockIdx.x) * kFProfEpochs * kFProfSlots + k] = static_cast<uint32_t>(__builtin_amdgcn_s_getreg(4 | (31 << 11)));
+}
+}  // namespace gnsship
+#define GNSSHIP_FSTAMP(e, k) gnsship::trkf_prof_stamp((e), (k))
+#define GNSSHIP_FCLK(e, k) gnsship::trkf_prof_clock((e), (k))
+#define GNSSHIP_FHWID(k) gnsship::trkf_prof_hwid((k))
+#define GNSSHIP_TRK_LOOP_STAMP(k) gnsship::trkf_prof_stamp(gnsship::g_fprof_epoch, (k))
+#else
+#define GNSSHIP_FSTAMP(e, k) \
+    do {                     \
+    } while (0)
+#define GNSSHIP_FCLK(e, k) \
+    do {                   \
+    } while (0)
+#define GNSSHIP_FHWID(k) \
+    do {                 \
+    } while (0)
+#endif
+
+#include "trk_loop.h"
+
+#pragma clang fp contract(off)
+
+namespace gnsship {
+namespace {
+
+constexpr int kFThreads = 256;
+constexpr int kFWaves = kFThreads / kWave;
+constexpr uint64_t kSlotEmpty = ~0ull;  // an unwritten phasor slot (NaN, NaN)
+
+// The epoch's correlation as the consumers need it (LDS, written by wave 0 before the barrier).
+struct FJob {
+    int64_t off;  // first sample of the epoch in the IF buffer
+    float rem_code, code_step;  // do_correlation_step's rem_code_phase_chips·spc, code_phase_step_chips·spc
+    float shifts[5];
+    float dz_re, dz_im;  // normalise(inc^16)
+    float rem_carr, step;  // the carrier arguments (IF folded in), for the trace
+    int32_t runnable, in_margin, M, S, tail, pad;
+};
+
+struct FShared {
+    FJob job;
+    float red[4 * kFWaves][2 * (kMaxTaps + 1)];  // per 16-lane row
+    float taps[2 * kMaxTaps + 2];  // the epoch's tap sums (+ the data prompt at 2·kMaxTaps), as epoch_pre reads them
+    gnsship_trk_dump_record drec;  // log_data's record of the epoch
+    double coh;       // the coherent time lock_status is called with (0: no lock test this epoch)
+    int32_t pre_seq;  // e + 1 once wave 0 published this epoch's prompt / pull-in / coh
+    int32_t lock_seq; // e + 1 once wave 1 published the lock outcome
+    int32_t locked;
+    int32_t pad;
+};
+
+// The job as wave-uniform values (scalar registers): read from LDS it would otherwise be per-lane,
+// and a per-lane buffer resource turns every sample load into a waterfall loop.
+__device__ __forceinline__ float unif(float v) { return __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, v))); }
+__device__ __forceinline__ FJob uniform_job(const FJob& s)
+{
+    FJob j;
+    const uint64_t off = static_cast<uint64_t>(s.off);
+    j.off = static_cast<int64_t>((static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(off >> 32)))) << 32) |
+                                 static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(off & 0xffffffffu))));
+    j.rem_code = unif(s.rem_code);
+    j.code_step = unif(s.code_step);
+    for (int t = 0; t < 5; t++) j.shifts[t] = unif(s.shifts[t]);
+    j.dz_re = unif(s.dz_re);
+    j.dz_im = unif(s.dz_im);
+    j.rem_carr = unif(s.rem_carr);
+    j.step = unif(s.step);
+    j.runnable = __builtin_amdgcn_readfirstlane(s.runnable);
+    j.in_margin = __builtin_amdgcn_readfirstlane(s.in_margin);
+    j.M = __builtin_amdgcn_readfirstlane(s.M);
+    j.S = __builtin_amdgcn_readfirstlane(s.S);
+    j.tail = __builtin_amdgcn_readfirstlane(s.tail);
+    j.pad = 0;
+    return j;
+}
+
+__device__ __forceinline__ void store_slot(uint64_t* p, f2 z) { __hip_atomic_store(p, __builtin_bit_cast(uint64_t, z), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
+__device__ __forceinline__ uint64_t load_slot(const uint64_t* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
+
+__device__ __forceinline__ void publish_seq(int32_t* p, int v)
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void wait_seq(int32_t* p, int need)
+{
+    while (__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < need) __builtin_amdgcn_s_sleep(0);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+// ---- wave 0: the AVX phasor replay ---------------------------------------------------------------
+// Chain l (< 16) starts at z_l = phase·inc^l at iteration 0 (:204-208).  Task t = iterations
+// [G·t, G·t + G) ∩ [0, M); its slot gets z_l at iteration G·t.  After iteration m's update the chains
+// normalise when m ≡ 0 (mod 64) (:265-272) — for G | 64 only a task's first iteration can be one.
+// The last task is continued by its consumer lanes; the replay goes on only for the N mod 16 tail.
+//
+// Two lanes per chain (lane 2l holds re, 2l + 1 im): one product z·dz is a plain multiply by dz.re,
+// a DPP multiply of the partner lane's component by ∓dz.im and one add — re' = fl(fl(re·c) +
+// fl(im·(−d))) ≡ fl(ac − bd), im' = fl(fl(im·c) + fl(re·d)) ≡ fl(ad + bc): the reference's
+// products bit for bit, in three single-rate VALU ops instead of six (measured 15.7 vs 30 shader
+// cycles per iteration on one wave, scripts/replay_bench.hip).  A DPP read needs two wait states
+// after the VALU write of its source: the step's plain multiply and one s_nop.  Each lane stores its
+// 32-bit half of the slot (the consumer polls until both halves are written).
+#define GNSSHIP_PSTEP(X, Y)                                                                   \
+    "v_mul_f32 %[t], %[c], " X "\n\t"                                                      \
+    "s_nop 0\n\t"                                                                           \
+    "v_mul_f32_dpp %[u], " X ", %[k2] quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t" \
+    "v_add_f32 " Y ", %[t], %[u]\n\t"
+
+// N iterations (1-4) in one asm block (the hazard recognizer pads each block boundary with one
+// s_nop); STORE: the block's input (the task start) goes to its slot half at `lds_off` (a byte offset
+// in LDS), after the first product has read it and long before it is overwritten.
+#define GNSSHIP_PSTEP_ASM(BODY)                                                                              \
+    do {                                                                                                   \
+        if constexpr (STORE)                                                                               \
+            asm volatile(BODY : [x] "+v"(x), [t] "=&v"(t), [u] "=&v"(u), [w] "=&v"(w), [v] "=&v"(v)        \
+                         : [c] "s"(c), [k2] "v"(k2), [p] "v"(lds_off)                                       \
+                         : "memory");                                                                      \
+        else                                                                                               \
+            asm volatile(BODY : [x] "+v"(x), [t] "=&v"(t), [u] "=&v"(u), [w] "=&v"(w), [v] "=&v"(v)        \
+                         : [c] "s"(c), [k2] "v"(k2), [p] "v"(lds_off));                                     \
+    } while (0)
+#define GNSSHIP_ST "ds_write_b32 %[p], %[x]\n\t"
+template <int N, bool STORE>
+__device__ __forceinline__ float pstep(float x, float c, float k2, uint32_t lds_off)
+{
+    static_assert(N >= 1 && N <= 4, "1-4 iterations per block");
+    float t, u, w, v;
+    if constexpr (N == 1) {
+        if constexpr (STORE)
+            GNSSHIP_PSTEP_ASM(GNSSHIP_PSTEP("%[x]", "%[w]") GNSSHIP_ST "v_mov_b32 %[x], %[w]\n\t");
+        else
+            GNSSHIP_PSTEP_ASM(GNSSHIP_PSTEP("%[x]", "%[x]"));
+    } else if constexpr (N == 2) {
+        if constexpr (STORE)
+            GNSSHIP_PSTEP_ASM(GNSSHIP_PSTEP("%[x]", "%[w]") GNSSHIP_ST GNSSHIP_PSTEP("%[w]", "%[x]"));
+        else
+            GNSSHIP_PSTEP_ASM(GNSSHIP_PSTEP("%[x]", "%[w]") GNSSHIP_PSTEP("%[w]", "%[x]"));
+    } else if constexpr (N == 3) {
+        if constexpr (STORE)
+            GNSSHIP_PSTEP_ASM(GNSSHIP_PSTEP("%[x]", "%[w]") GNSSHIP_ST GNSSHIP_PSTEP("%[w]", "%[v]") GNSSHIP_PSTEP("%[v]", "%[x]"));
+        else
+            GNSSHIP_PSTEP_ASM(GNSSHIP_PSTEP("%[x]", "%[w]") GNSSHIP_PSTEP("%[w]", "%[v]") GNSSHIP_PSTEP("%[v]", "%[x]"));
+    } else {
+        if constexpr (STORE)
+            GNSSHIP_PSTEP_ASM(GNSSHIP_PSTEP("%[x]", "%[w]") GNSSHIP_ST GNSSHIP_PSTEP("%[w]", "%[v]") GNSSHIP_PSTEP("%[v]", "%[w]")
+                    GNSSHIP_PSTEP("%[w]", "%[x]"));
+        else
+            GNSSHIP_PSTEP_ASM(GNSSHIP_PSTEP("%[x]", "%[w]") GNSSHIP_PSTEP("%[w]", "%[v]") GNSSHIP_PSTEP("%[v]", "%[w]") GNSSHIP_PSTEP("%[w]", "%[x]"));
+    }
+    return x;
+}
+#undef GNSSHIP_ST
+#undef GNSSHIP_PSTEP_ASM
+// x·dz^N: N ≥ 0 iterations
+template <int N>
+__device__ __forceinline__ float ppow(float x, float c, float k2)
+{
+    if constexpr (N >= 4) return ppow<N - 4>(pstep<4, false>(x, c, k2, 0), c, k2);
+    else if constexpr (N > 0) return pstep<N, false>(x, c, k2, 0);
+    else return x;
+}
+#undef GNSSHIP_PSTEP
+
+// _mm256_complexnormalise_ps on the lane pair: both lanes form fl(re² + im²) (the partner's square
+// by DPP), then x / sqrt(·) — normalise_avx's operations.
+__device__ __forceinline__ float pnormalise(float x)
+{
+    const float s = __fmul_rn(x, x);
+    const float o = __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, s), 0xB1, 0xF, 0xF, false));
+    return __fdiv_rn(x, sqrt_rn_f32(__fadd_rn(s, o)));
+}
+
+// Lanes 0-31.  `x` = this lane's component of z_l, k2 = (lane odd ? dz.im : −dz.im), c = dz.re
+// (uniform).  Returns the component of z_l after the last task's start (or at M with a tail).
+template <int G>
+__device__ __forceinline__ float fast_replay(float x, float c, float k2, int M, int S, int tail, uint64_t* __restrict__ Zs, int lane)
+{
+    static_assert(G % 4 == 0 && G >= 4 && G <= 64, "task length");
+    constexpr int kTB = 64 / G;  // tasks per 64-iteration block
+    if (S <= 0) return x;
+    const int full = (S - 1) / kTB;  // whole blocks before the last task
+    // the flat address of an LDS location carries its LDS offset in the low 32 bits
+    uint32_t off = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(Zs)) + 4u * static_cast<uint32_t>(lane);
+    constexpr uint32_t kSlotRow = kAvxLanes * sizeof(uint64_t);
+    uint32_t* half = reinterpret_cast<uint32_t*>(Zs) + lane;
+#pragma unroll 1
+    for (int b = 0; b < full; b++) {
+#pragma unroll
+        for (int q = 0; q < kTB; q++) {
+            if (q == 0)  // the block's first iteration normalises
+                x = ppow<G - 1>(pnormalise(pstep<1, true>(x, c, k2, off)), c, k2);
+            else
+                x = ppow<G - 4>(pstep<4, true>(x, c, k2, off), c, k2);
+            off += kSlotRow;
+            half += 2 * kAvxLanes;
+        }
+    }
+#pragma unroll 1
+    for (int t = full * kTB; t < S - 1; t++) {
+        x = pstep<1, true>(x, c, k2, off);
+        if (t == full * kTB) x = pnormalise(x);
+        x = ppow<G - 1>(x, c, k2);
+        off += kSlotRow;
+        half += 2 * kAvxLanes;
+    }
+    __hip_atomic_store(half, __builtin_bit_cast(uint32_t, x), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);  // the last task: its consumers continue
+    if (tail > 0) {  // z_l(M) for the tail (chain 0's is what the reference keeps)
+        for (int m = G * (S - 1); m < M; m++) {
+            x = pstep<1, false>(x, c, k2, 0);
+            if ((m & 63) == 0) x = pnormalise(x);
+        }
+    }
+    return x;
+}
+
+// ---- waves 1-3: the correlation -------------------------------------------------------------------
+template <int FMT, int NT, bool DATA, bool IN_MARGIN, int G>
+__device__ __forceinline__ void fast_consume(const FJob& job, i4v span, const float* __restrict__ code0, const float* __restrict__ code1, int L,
+    uint64_t* __restrict__ Zs, int lane, int wave, f2 (&acc)[NT + 1])
+{
+    constexpr int SB = sample_bytes<FMT>();
+    constexpr int kB = G < 8 ? G : 8;  // iterations whose samples are in flight together
+    const int M = job.M, S = job.S;
+    const int n_groups = (S + 3) / 4;
+    const f2 dz = f2{job.dz_re, job.dz_im};
+    const float step = job.code_step, rem = job.rem_code;
+    float shifts[NT];
+#pragma unroll
+    for (int q = 0; q < NT; q++) shifts[q] = job.shifts[q];
+    const int tl = lane >> 4, l = lane & (kAvxLanes - 1);
+    // the first kB samples of a group's lanes: issued one group ahead (the wave's next group), so a
+    // wave that trails the replay does not pay a memory round trip per group
+    auto first_samples = [&](int g, f2 (&x)[kB]) {
+        const int t = 4 * g + tl;
+        const int n0 = kAvxLanes * G * (t < S ? t : 0) + l;
+#pragma unroll
+        for (int u = 0; u < kB; u++) x[u] = load_sample<FMT>(span, (n0 + kAvxLanes * u) * SB, 0);
+    };
+    f2 xa[kB], xb[kB], xn[kB];
+    if (wave - 1 < n_groups) first_samples(wave - 1, xa);
+    for (int g = wave - 1; g < n_groups; g += kFWaves - 1) {
+        const int t = 4 * g + tl;
+        const bool active = t < S;
+        const int m_lo = G * (active ? t : 0);
+        const int cnt = active ? min(G, M - m_lo) : 0;
+        const int n0 = kAvxLanes * m_lo + l;
+        const bool more = g + kFWaves - 1 < n_groups;
+        if (more) first_samples(g + kFWaves - 1, xn);  // in flight while polling and correlating this group
+        uint64_t* slot = Zs + (active ? t : 0) * kAvxLanes + l;
+        uint64_t v = kSlotEmpty;
+        if (active) {
+            // written when neither 32-bit half is the sentinel any more (two replay lanes write it)
+            while (static_cast<uint32_t>(v = load_slot(slot)) == ~0u || static_cast<uint32_t>(v >> 32) == ~0u) __builtin_amdgcn_s_sleep(0);
+            store_slot(slot, __builtin_bit_cast(f2, kSlotEmpty));  // re-armed for the next epoch
+        }
+        f2 z = active ? __builtin_bit_cast(f2, v) : f2{0.0f, 0.0f};
+        const bool renorm = ((G * t) & 63) == 0;
+        float fn = static_cast<float>(n0);  // (float)n, exact steps of 16 (n < 2^24)
+#pragma unroll 1
+        for (int i0 = 0; i0 < G; i0 += kB) {
+            if (i0 + kB < G) {
+#pragma unroll
+                for (int u = 0; u < kB; u++) xb[u] = load_sample<FMT>(span, (n0 + kAvxLanes * (i0 + kB + u)) * SB, 0);
+            }
+#pragma unroll
+            for (int u = 0; u < kB; u++) {
+                const int i = i0 + u;
+                const bool on = i < cnt;
+                const f2 r = on ? cmul_pk2(xa[u], z) : f2{0.0f, 0.0f};
+                f2 zn = cmul_exact_s(z, dz);
+                if (i == 0 && renorm) zn = normalise_avx(zn);
+                z = zn;
+                const float sn = __fmul_rn(step, on ? fn : static_cast<float>(n0));
+#pragma unroll
+                for (int q = 0; q < NT; q++) {
+                    const float c = code_at<IN_MARGIN>(code0, L, sn, shifts[q], rem);
+                    acc[q] = __builtin_elementwise_fma(r, f2{c, c}, acc[q]);
+                }
+                if constexpr (DATA) {
+                    const float c = code_at<IN_MARGIN>(code1, L, sn, 0.0f, rem);
+                    acc[NT] = __builtin_elementwise_fma(r, f2{c, c}, acc[NT]);
+                }
+                fn += static_cast<float>(kAvxLanes);
+            }
+            if (i0 + kB < G) {
+#pragma unroll
+                for (int u = 0; u < kB; u++) xa[u] = xb[u];
+            }
+        }
+        if (more) {
+#pragma unroll
+            for (int u = 0; u < kB; u++) xa[u] = xn[u];
+        }
+    }
+}
+
+// The N mod 16 tail (:286-304) on wave 0: lane j < tail correlates sample 16M + j with T[j].
+template <int FMT, int NT, bool DATA, bool IN_MARGIN>
+__device__ __forceinline__ void fast_tail(const FJob& job, i4v span, const float* __restrict__ code0, const float* __restrict__ code1, int L, const f2* T, int lane,
+    f2 (&acc)[NT + 1])
+{
+    constexpr int SB = sample_bytes<FMT>();
+    if (lane >= job.tail) return;
+    const int n = kAvxLanes * job.M + lane;
+    const f2 x = load_sample<FMT>(span, n * SB, 0);
+    const f2 r = cmul_pk2(x, T[lane]);
+    const float sn = __fmul_rn(job.code_step, static_cast<float>(n));
+#pragma unroll
+    for (int q = 0; q < NT; q++) {
+        const float c = code_at<IN_MARGIN>(code0, L, sn, job.shifts[q], job.rem_code);
+        acc[q] = __builtin_elementwise_fma(r, f2{c, c}, acc[q]);
+    }
+    if constexpr (DATA) {
+        const float c = code_at<IN_MARGIN>(code1, L, sn, 0.0f, job.rem_code);
+        acc[NT] = __builtin_elementwise_fma(r, f2{c, c}, acc[NT]);
+    }
+}
+
+__device__ void stage_code_f(float* dst, const CodeDesc& cd)
+{
+    const int nq = padded_code_quads(cd.len);
+    const float4* src = reinterpret_cast<const float4*>(cd.ptr - kCodeMargin);
+    float4* d4 = reinterpret_cast<float4*>(dst);
+    for (int q = threadIdx.x; q < nq; q += kFThreads) d4[q] = src[q];
+}
+
+// THRU (more channels than CUs): two workgroups per CU (≤ 256 VGPRs — the control wave keeps the
+// channel in registers); otherwise one.  Two waves on a SIMD each keep their own issue cadence.
+template <bool THRU>
+constexpr int fast_waves_per_simd() { return THRU ? 2 : 1; }
+
+template <int FMT, int NT, bool DATA, int G, bool THRU>
+__global__ __launch_bounds__(kFThreads, fast_waves_per_simd<THRU>()) void trk_fast_kernel(const TrkParams* __restrict__ pk, TrkChannel* __restrict__ chans,
+    const CodeDesc* __restrict__ codes, int n_codes, const void* __restrict__ samples, uint64_t buf_first, int64_t buf_len, int max_rounds,
+    int n_chans, int code_cap_floats, int slot_cap, gnsship_trk_epoch* __restrict__ rec, gnsship_trk_dump_record* __restrict__ dump,
+    gnsship_trk_corr_trace* __restrict__ trace, int* __restrict__ ran_count)
+{
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    __shared__ TrkChannel sc;
+    __shared__ FShared sh;
+    __shared__ int32_t skip;
+    __shared__ f2 tailz[kAvxLanes];
+    const int ch = blockIdx.x;
+    const int tid = threadIdx.x, lane = tid & (kWave - 1), wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const TrkParams& k = *pk;
+    {
+        const int* src = reinterpret_cast<const int*>(chans + ch);
+        int* dst = reinterpret_cast<int*>(&sc);
+        for (int i = tid; i < static_cast<int>(sizeof(TrkChannel) / 4); i += kFThreads) dst[i] = src[i];
+    }
+    float* code0 = lds;
+    float* code1 = lds + code_cap_floats;
+    uint64_t* Zs = reinterpret_cast<uint64_t*>(lds + (DATA ? 2 : 1) * code_cap_floats);
+    for (int i = tid; i < slot_cap * kAvxLanes; i += kFThreads) Zs[i] = kSlotEmpty;
+    __syncthreads();
+    if (tid == 0) {
+        const bool tracking = sc.state == 2 || sc.state == 3 || sc.state == 4;
+        const bool codes_ok = sc.code_id >= 0 && sc.code_id < n_codes && codes[sc.code_id].ptr && codes[sc.code_id].len > 0 &&
+                              padded_code_quads(codes[sc.code_id].len) * 4 <= code_cap_floats &&
+                              (!DATA || (sc.data_code_id >= 0 && sc.data_code_id < n_codes && codes[sc.data_code_id].ptr &&
+                                            codes[sc.data_code_id].len == codes[sc.code_id].len));
+        skip = (tracking && codes_ok) ? 0 : 1;
+        sh.pre_seq = 0;
+        sh.lock_seq = 0;
+    }
+    __syncthreads();
+    if (skip) return;  // idle channel: its state is untouched
+    GNSSHIP_FHWID(20 + wave);  // epoch 0's slots 20-23 (the epoch loop stamps 0-15)
+    stage_code_f(code0, codes[sc.code_id]);
+    if constexpr (DATA) stage_code_f(code1, codes[sc.data_code_id]);
+    const int L = codes[sc.code_id].len;
+    const float* c0 = code0 + kCodeMargin;
+    const float* c1 = code1 + kCodeMargin;
+    const int N = static_cast<int>(k.conf.vector_length);
+    const int M = N / kAvxLanes;
+    const int S = (M + G - 1) / G;
+    const int tail = N - kAvxLanes * M;
+    constexpr int kOut = NT + (DATA ? 1 : 0);
+    RChan rc;
+    if (wave == 0) rchan_load(sc, &sc, rc);
+    int e_done = 0;
+    for (int e = 0; e < max_rounds; e++) {
+        // ---- derive (wave 0): do_correlation_step's arguments for the epoch at nitems_read ----
+        f2 zinit = f2{0.0f, 0.0f}, dz = f2{1.0f, 0.0f}, inc = f2{1.0f, 0.0f};
+        if (wave == 0) {
+            GNSSHIP_FSTAMP(e, 0);
+#ifdef GNSSHIP_CORR_PROFILE
+            if (lane == 0) g_fprof_epoch = e;
+#endif
+            const uint64_t vl = k.conf.vector_length;
+            const bool runnable = (rc.state == 2 || rc.state == 3 || rc.state == 4) && rc.nitems_read >= buf_first &&
+                                  rc.nitems_read + vl <= buf_first + static_cast<uint64_t>(buf_len);
+            // (cos rem, −sin rem) and (cos −step, sin −step) (cpu_multicorrelator_real_codes.cc:115,123):
+            // lane 0 the phase, lane 1 the step, each the once-rounded double cos/sin (nco_math.h)
+            const float rem_carr = corr_rem_carr(k, rc), stepf = corr_phase_step(k, rc);
+            const float a = lane == 0 ? rem_carr : -stepf;
+            double sd, cd;
+            sincos(static_cast<double>(a), &sd, &cd);
+            const int sfi = __builtin_bit_cast(int, static_cast<float>(sd)), cfi = __builtin_bit_cast(int, static_cast<float>(cd));
+            const f2 p0 = f2{__builtin_bit_cast(float, __builtin_amdgcn_readlane(cfi, 0)), -__builtin_bit_cast(float, __builtin_amdgcn_readlane(sfi, 0))};
+            inc = f2{__builtin_bit_cast(float, __builtin_amdgcn_readlane(cfi, 1)), __builtin_bit_cast(float, __builtin_amdgcn_readlane(sfi, 1))};
+            // dz = normalise(inc^16) by four squarings (:215-225)
+            f2 d = inc;
+#pragma unroll
+            for (int q = 0; q < 4; q++) d = cmul_exact(d, d);
+            dz = normalise_avx(d);
+            // z_l = phase·inc^l, the generic chain (:204-208), for the replay's lane pairs
+            f2 z = p0;
+#pragma unroll
+            for (int i = 0; i < kAvxLanes - 1; i++) {
+                const f2 zi = cmul_exact(z, inc);
+                z = i < (lane >> 1) ? zi : z;  // lanes 2l, 2l + 1: chain l
+            }
+            zinit = z;
+            if (runnable) rc.epoch_start = rc.nitems_read;
+            if (lane == 0) {
+                FJob& j = sh.job;
+                j.runnable = runnable ? 1 : 0;
+                if (runnable) {
+                    const float spcf = static_cast<float>(k.code_samples_per_chip);
+                    const float* shv = uni(rc.narrow) ? k.shifts_n : k.shifts;
+                    j.off = static_cast<int64_t>(rc.nitems_read - buf_first);
+                    j.rem_code = __fmul_rn(static_cast<float>(rc.rem_code_phase_chips), spcf);
+                    j.code_step = __fmul_rn(static_cast<float>(rc.code_phase_step_chips), spcf);
+                    float smin = 0.0f, smax = 0.0f;
+                    for (int t = 0; t < 5; t++) {
+                        j.shifts[t] = t < NT ? shv[t] : 0.0f;
+                        smin = fminf(smin, j.shifts[t]);
+                        smax = fmaxf(smax, j.shifts[t]);
+                    }
+                    const double span = static_cast<double>(j.code_step) * static_cast<double>(N > 0 ? N - 1 : 0);
+                    const double lo = fmin(0.0, span) + smin - j.rem_code - 2.0;
+                    const double hi = fmax(0.0, span) + smax - j.rem_code + 2.0;
+                    j.in_margin = (isfinite(lo) && isfinite(hi) && lo >= -kCodeMargin && hi < static_cast<double>(L + kCodeMargin)) ? 1 : 0;
+                    j.dz_re = dz.x;
+                    j.dz_im = dz.y;
+                    j.rem_carr = rem_carr;
+                    j.step = stepf;
+                    j.M = M;
+                    j.S = S;
+                    j.tail = tail;
+                }
+            }
+            GNSSHIP_FSTAMP(e, 1);
+            GNSSHIP_FCLK(e, 12);
+        }
+        __syncthreads();  // B: the job is published (and, in the first epoch, the code replicas staged)
+        if (!sh.job.runnable) break;
+        const FJob job = uniform_job(sh.job);
+        const i4v span = sample_span<FMT>(samples, job.off, N);
+        f2 acc[NT + 1];
+#pragma unroll
+        for (int t = 0; t <= NT; t++) acc[t] = f2{0.0f, 0.0f};
+        if (wave == 0) {
+            float xl = (lane & 1) ? zinit.y : zinit.x;
+            if (lane < 2 * kAvxLanes) xl = fast_replay<G>(xl, job.dz_re, (lane & 1) ? job.dz_im : -job.dz_im, M, S, tail, Zs, lane);
+            if (tail > 0) {
+                const f2 zl = f2{__builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, xl), 0)),
+                    __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, xl), 1))};  // the serial tail from normalise(z_0) after the loop (:286-304), on this wave
+                if (lane == 0) {
+                    f2 p = normalise_avx(zl);
+                    for (int j = 0; j < tail; j++) {
+                        tailz[j] = p;
+                        p = cmul_exact(p, inc);
+                    }
+                }
+                if (job.in_margin)
+                    fast_tail<FMT, NT, DATA, true>(job, span, c0, c1, L, tailz, lane, acc);
+                else
+                    fast_tail<FMT, NT, DATA, false>(job, span, c0, c1, L, tailz, lane, acc);
+            }
+            GNSSHIP_FSTAMP(e, 2);
+            GNSSHIP_FCLK(e, 13);
+#ifdef GNSSHIP_FAST_SERIAL  // diagnostic only: the consumers start after the whole replay
+            __syncthreads();
+#endif
+        } else {
+#ifdef GNSSHIP_FAST_SERIAL
+            __syncthreads();
+#endif
+            if (job.in_margin)
+                fast_consume<FMT, NT, DATA, true, G>(job, span, c0, c1, L, Zs, lane, wave, acc);
+            else
+                fast_consume<FMT, NT, DATA, false, G>(job, span, c0, c1, L, Zs, lane, wave, acc);
+            GNSSHIP_FSTAMP(e, 2 + wave);  // 3, 4, 5: each correlating wave done
+        }
+        // DPP row sums only (no cross-row shuffle through LDS): the first lane of each 16-lane row
+        // stores its row's sums; wave 0 adds the rows after the barrier
+        {
+            f2 rs[kOut];
+#pragma unroll
+            for (int t = 0; t < kOut; t++) rs[t] = f2{row_sum(acc[t].x), row_sum(acc[t].y)};
+            if ((lane & 15) == 0) {
+                f2* dst = reinterpret_cast<f2*>(sh.red[4 * wave + (lane >> 4)]);
+#pragma unroll
+                for (int t = 0; t < kOut; t++) dst[t] = rs[t];
+            }
+        }
+        __syncthreads();  // C: every row's tap sums are in LDS
+        if (wave == 0) {
+            GNSSHIP_FSTAMP(e, 6);
+            GNSSHIP_FCLK(e, 14);
+            // tap sums over the rows in row order (lane v sums value v; wave 0's rows hold only the
+            // N mod 16 tail); the data prompt at 2·kMaxTaps
+            float* taps = sh.taps;
+            if (lane < 2 * kOut) {
+                const int t = lane >> 1, c = lane & 1;
+                float sum = 0.0f;
+                if (job.tail > 0) {
+#pragma unroll
+                    for (int w = 0; w < 4; w++) sum += sh.red[w][lane];
+                }
+#pragma unroll
+                for (int w = 4; w < 4 * kFWaves; w++) sum += sh.red[w][lane];
+                taps[((DATA && t == NT) ? 2 * kMaxTaps : 2 * t) + c] = sum;
+            }
+            GNSSHIP_FSTAMP(e, 16);
+            const float* pdata = DATA ? taps + 2 * kMaxTaps : taps;
+            gnsship_trk_epoch r{};
+            r.flags = 8;
+            gnsship_trk_dump_record* dr = dump ? &sh.drec : nullptr;
+            const double coh = epoch_pre(k, rc, taps, pdata, r, nullptr, dr);
+            GNSSHIP_FSTAMP(e, 17);
+            // hand the prompt to the lock detectors (wave 1; coh 0: no lock test this epoch)
+            if (lane == 0) {
+                sc.p[0] = rc.p[0];
+                sc.p[1] = rc.p[1];
+                sc.pull_in = rc.pull_in;
+                sh.coh = coh;
+                publish_seq(&sh.pre_seq, e + 1);
+            }
+            GNSSHIP_FSTAMP(e, 18);
+            if (coh > 0.0) {  // the loop runs speculatively beside the lock test
+                // what the record shows if the test fails (the channel then stops: nothing else of the
+                // loop's output is ever read)
+                const double k_rcs = rc.rem_code_phase_samples, k_acc = rc.acc_carrier_phase_rad, k_dop = rc.carrier_doppler_hz;
+                const double k_cf = rc.code_freq_chips, k_rcc = rc.rem_code_phase_chips;
+                const float k_rem = rc.rem_carr_phase_rad;
+                const int32_t k_len = rc.current_prn_length_samples;
+                epoch_loop(k, rc, nullptr);
+                wait_seq(&sh.lock_seq, e + 1);
+                GNSSHIP_FSTAMP(e, 19);
+                const bool locked = sh.locked != 0;
+                if (!locked) {  // the reference runs the loop only on a passed lock test
+                    rc.rem_code_phase_samples = k_rcs;
+                    rc.acc_carrier_phase_rad = k_acc;
+                    rc.carrier_doppler_hz = k_dop;
+                    rc.code_freq_chips = k_cf;
+                    rc.rem_code_phase_chips = k_rcc;
+                    rc.rem_carr_phase_rad = k_rem;
+                    rc.current_prn_length_samples = k_len;
+                }
+                epoch_post(k, rc, taps, pdata, r, locked, dr);
+            }
+            GNSSHIP_FSTAMP(e, 24);
+            epoch_finish(k, rc, r);
+            GNSSHIP_FSTAMP(e, 25);
+            if (lane == 0) {
+                const size_t slot = static_cast<size_t>(e) * n_chans + ch;
+                if (rec) rec[slot] = r;
+                if (dump && (r.flags & 16)) dump[slot] = sh.drec;
+                if (trace) {
+                    gnsship_trk_corr_trace tr{};
+                    tr.sample_counter = rc.epoch_start;
+                    tr.n_samples = N;
+                    tr.n_taps = NT;
+                    tr.rem_carrier_phase_rad = job.rem_carr;
+                    tr.phase_step_rad = job.step;
+                    tr.rem_code_phase_samples = job.rem_code;
+                    tr.code_phase_step_samples = job.code_step;
+                    for (int t = 0; t < 5; t++) tr.shifts[t] = job.shifts[t];
+                    for (int t = 0; t < 10; t++) tr.taps[t] = t < 2 * NT ? taps[t] : 0.0f;
+                    tr.data_prompt[0] = DATA ? pdata[0] : 0.0f;
+                    tr.data_prompt[1] = DATA ? pdata[1] : 0.0f;
+                    trace[slot] = tr;
+                }
+            }
+            e_done = e + 1;
+            GNSSHIP_FSTAMP(e, 7);
+            GNSSHIP_FCLK(e, 15);
+        } else if (wave == 1) {
+            // cn0_and_tracking_lock_status (:972-1029) on the LDS copy of its members, beside the loop update
+            wait_seq(&sh.pre_seq, e + 1);
+            const double coh = sh.coh;
+            if (lane == 0) {
+                GNSSHIP_TRK_LOOP_STAMP(8);
+                sh.locked = (coh > 0.0 && !lock_status(k, sc, coh)) ? 0 : 1;
+                GNSSHIP_TRK_LOOP_STAMP(26);
+                publish_seq(&sh.lock_seq, e + 1);
+            }
+        }
+        // the next derive reads nothing the other waves write, and they wait at B for it
+    }
+    if (wave == 0 && lane == 0) {
+        rchan_store(rc, sc);
+        sc.ran = 0;
+        if (e_done > 0) atomicAdd(ran_count + e_done - 1, 1);  // rounds_done = the longest channel's epochs
+    }
+    __syncthreads();
+    {
+        const int* src = reinterpret_cast<const int*>(&sc);
+        int* dst = reinterpret_cast<int*>(chans + ch);
+        for (int i = tid; i < static_cast<int>(sizeof(TrkChannel) / 4); i += kFThreads) dst[i] = src[i];
+    }
+}
+
+}  // namespace
+
+#ifdef GNSSHIP_CORR_PROFILE
+}  // namespace gnsship
+extern "C" int gnsship_debug_trk_fast_profile(void* dev_buf)
+{
+    return hipMemcpyToSymbol(HIP_SYMBOL(gnsship::g_trkf_prof), &dev_buf, sizeof(void*)) == hipSuccess ? 0 : -3;
+}
+namespace gnsship {
+#endif
+
+// Task length G (iterations per phasor slot) and the LDS bytes of the dynamic region (codes + slots):
+// the shortest task whose slots fit the budget (4 iterations keeps the epoch's tail short; longer
+// epochs take longer tasks).  0 when even 64-iteration tasks do not fit.
+static size_t fast_lds(const TrkParams& p, int code_cap_floats, int n_chans, int* g_out, int* slots_out)
+{
+    const int N = static_cast<int>(p.conf.vector_length);
+    const int M = N / kAvxLanes;
+    const size_t codes = static_cast<size_t>(p.jobs_per_channel > 1 ? 2 : 1) * code_cap_floats * sizeof(float);
+    // more channels than CUs: two workgroups per CU share its LDS
+    const size_t budget = n_chans > 256 ? 72 * 1024 : kTrkPersistMaxLds;
+    for (int G = 4; G <= 64; G *= 2) {
+        const int S = (M + G - 1) / G;
+        const size_t bytes = codes + static_cast<size_t>(S > 0 ? S : 1) * kAvxLanes * sizeof(uint64_t);
+        if (bytes <= budget) {
+            if (g_out) *g_out = G;
+            if (slots_out) *slots_out = S > 0 ? S : 1;
+            return bytes;
+        }
+    }
+    return 0;
+}
+
+bool trk_fast_supported(const TrkParams& p, int code_cap_floats, int n_chans)
+{
+    if (!trk_persist_supports(p) || p.conf.rotator != GNSSHIP_ROTATOR_AVX || p.conf.high_dyn) return false;
+    if (const char* env = std::getenv("GNSSHIP_TRK_FAST")) {  // A/B against trk_persist.hip
+        if (env[0] == '0') return false;
+    }
+    return fast_lds(p, code_cap_floats, n_chans, nullptr, nullptr) > 0;
+}
+
+hipError_t launch_trk_fast(const TrkParams* params_dev, const TrkParams& params, TrkChannel* chans, int n_chans, const CodeDesc* codes, int n_codes,
+    int code_cap_floats, const void* samples, int fmt, uint64_t buf_first, int64_t buf_len, int max_rounds, gnsship_trk_epoch* rec,
+    gnsship_trk_dump_record* dump, gnsship_trk_corr_trace* trace, int* ran_count, hipStream_t stream)
+{
+    int G = 0, slots = 0;
+    const size_t lds = fast_lds(params, code_cap_floats, n_chans, &G, &slots);
+    if (lds == 0) return hipErrorInvalidValue;
+    const bool data = params.jobs_per_channel > 1;
+    bool thru = n_chans > 256;
+    if (const char* env = std::getenv("GNSSHIP_TRK_THRU")) thru = env[0] == '1';
+    const int nt = params.n_taps;
+    dim3 grid(n_chans), block(kFThreads);
+#define GNSSHIP_FAST(F, NTV, DV, GV)                                                                                                              \
+    do {                                                                                                                                        \
+        auto kfn = thru ? trk_fast_kernel<F, NTV, DV, GV, true> : trk_fast_kernel<F, NTV, DV, GV, false>;                                        \
+        hipError_t e0 = hipFuncSetAttribute(reinterpret_cast<const void*>(kfn), hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)); \
+        if (e0 != hipSuccess) return e0;                                                                                                        \
+        hipLaunchKernelGGL(kfn, grid, block, lds, stream, params_dev, chans, codes, n_codes, samples, buf_first, buf_len, max_rounds, n_chans,   \
+            code_cap_floats, slots, rec, dump, trace, ran_count);                                                                               \
+    } while (0)
+#define GNSSHIP_FAST_G(F, NTV, DV)                          \
+    do {                                                    \
+        switch (G) {                                        \
+        case 4: GNSSHIP_FAST(F, NTV, DV, 4); break;         \
+        case 8: GNSSHIP_FAST(F, NTV, DV, 8); break;         \
+        case 16: GNSSHIP_FAST(F, NTV, DV, 16); break;       \
+        case 32: GNSSHIP_FAST(F, NTV, DV, 32); break;       \
+        default: GNSSHIP_FAST(F, NTV, DV, 64); break;       \
+        }                                                   \
+    } while (0)
+#define GNSSHIP_FAST_F(F)                                   \
+    do {                                                    \
+        if (nt == 3 && !data) GNSSHIP_FAST_G(F, 3, false);  \
+        else if (nt == 5 && !data) GNSSHIP_FAST_G(F, 5, false); \
+        else if (nt == 5 && data) GNSSHIP_FAST_G(F, 5, true); \
+        else return hipErrorInvalidValue;                   \
+    } while (0)
+    switch (fmt) {
+    case GNSSHIP_FMT_CF32: GNSSHIP_FAST_F(GNSSHIP_FMT_CF32); break;
+    case GNSSHIP_FMT_CI16: GNSSHIP_FAST_F(GNSSHIP_FMT_CI16); break;
+    case GNSSHIP_FMT_CI8: GNSSHIP_FAST_F(GNSSHIP_FMT_CI8); break;
+    default: return hipErrorInvalidValue;
+    }
+#undef GNSSHIP_FAST_F
+#undef GNSSHIP_FAST_G
+#undef GNSSHIP_FAST
+    return hipGetLastError();
+}
+
+}  // namespace gnsship

@@ -81,7 +81,7 @@ __device__ float cn0_m2m4(const float* prompt, int length, float coh_integration
     psig = __fmul_rn(psig, psig);
     m_2 = __fdiv_rn(m_2, n);
     m_4 = __fdiv_rn(m_4, n);
-    aux = sqrtf(__fsub_rn(__fmul_rn(__fmul_rn(2.0f, m_2), m_2), m_4));
+    aux = sqrt_rn_f32(__fsub_rn(__fmul_rn(__fmul_rn(2.0f, m_2), m_2), m_4));
     const float snr = isnan(aux) ? __fdiv_rn(psig, __fsub_rn(m_2, psig)) : __fdiv_rn(aux, __fsub_rn(m_2, aux));
     return __fsub_rn(__fmul_rn(10.0f, log10f(snr)), __fmul_rn(10.0f, log10f(coh_integration_time_s)));
 }
@@ -145,8 +145,169 @@ struct LoopRegs {
     LoopSet q;
 };
 
+// A channel held in registers for a whole run (the fast persistent kernel, trk_fast.hip): every
+// scalar member of TrkChannel the loop touches, the Tracking_loop_filter rings in logical order (as
+// LoopRegs), and a pointer to the channel's memory copy (LDS) for what stays there — the sign
+// history, and the lock-detector members (prompt buffer, CN0 / lock-test smoothers and fail
+// counters), which another wave updates beside the loop update (lock_status).
+struct RChan {
+    int32_t state, geo, narrow, ext_count, cloop, pull_in, pll_180, acc_phase_init, sign_count;
+    uint32_t prn;
+    uint64_t acq_sample_stamp, nitems_read, epoch_start;
+    double carrier_doppler_hz, carrier_phase_step_rad, code_freq_chips, code_phase_step_chips;
+    double rem_code_phase_chips, rem_code_phase_samples, acc_carrier_phase_rad;
+    double carr_phase_error_hz, carr_error_filt_hz, code_error_chips, code_error_filt_chips, K_blk_samples;
+    double carrier_phase_rate_step_rad, code_phase_rate_step_chips;
+    float rem_carr_phase_rad;
+    int32_t current_prn_length_samples;
+    float spc;
+    float ve[2], e[2], p[2], l[2], vl[2], p_data[2], p_old[2];
+    int32_t current_symbol, current_data_symbol;
+    float lfi[4], lfo[4];
+    int32_t lf_idx;
+    float fp_w, fp_x;
+    int32_t hist_head, hist_count;  // high_dyn rings are not on this path (kept for the shared templates)
+    int64_t if_num;
+    double if_cyc;
+    TrkChannel* m;  // the memory copy: sign_bits and the lock-detector members
+};
+
 __device__ __forceinline__ const LoopSet& loopset(const TrkParams& k, const TrkChannel& c) { return k.ls[c.narrow ? 1 + c.geo : 0]; }
 __device__ __forceinline__ const LoopSet& loopset(const TrkParams&, const LoopRegs& c) { return c.q; }
+// RChan lives in a whole wave's registers with the same value in every lane: indices into the
+// parameter block go through readfirstlane so that the compiler reads it with scalar loads instead
+// of one vector load per lane on the critical path.
+__device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ const LoopSet& loopset(const TrkParams& k, const RChan& c) { return k.ls[uni(c.narrow ? 1 + c.geo : 0)]; }
+__device__ __forceinline__ const SymSync& syncset(const TrkParams& k, const TrkChannel& c) { return k.sync[c.geo]; }
+__device__ __forceinline__ const SymSync& syncset(const TrkParams& k, const RChan& c) { return k.sync[uni(c.geo)]; }
+__device__ __forceinline__ const SymSync& syncset(const TrkParams& k, const LoopRegs& c) { return k.sync[c.geo]; }
+
+// The members cn0_and_tracking_lock_status owns (prompt buffer, smoothers, fail counters, CN0 and
+// lock test) and the sign history live in memory for both channel forms.
+__device__ __forceinline__ TrkChannel& mem(TrkChannel& c) { return c; }
+__device__ __forceinline__ const TrkChannel& mem(const TrkChannel& c) { return c; }
+__device__ __forceinline__ TrkChannel& mem(RChan& c) { return *c.m; }
+__device__ __forceinline__ const TrkChannel& mem(const RChan& c) { return *c.m; }
+
+__device__ __forceinline__ void rchan_load(const TrkChannel& c, TrkChannel* mcopy, RChan& r)
+{
+    r.state = c.state;
+    r.geo = c.geo;
+    r.narrow = c.narrow;
+    r.ext_count = c.ext_count;
+    r.cloop = c.cloop;
+    r.pull_in = c.pull_in;
+    r.pll_180 = c.pll_180;
+    r.acc_phase_init = c.acc_phase_init;
+    r.sign_count = c.sign_count;
+    r.prn = c.prn;
+    r.acq_sample_stamp = c.acq_sample_stamp;
+    r.nitems_read = c.nitems_read;
+    r.epoch_start = c.epoch_start;
+    r.carrier_doppler_hz = c.carrier_doppler_hz;
+    r.carrier_phase_step_rad = c.carrier_phase_step_rad;
+    r.code_freq_chips = c.code_freq_chips;
+    r.code_phase_step_chips = c.code_phase_step_chips;
+    r.rem_code_phase_chips = c.rem_code_phase_chips;
+    r.rem_code_phase_samples = c.rem_code_phase_samples;
+    r.acc_carrier_phase_rad = c.acc_carrier_phase_rad;
+    r.carr_phase_error_hz = c.carr_phase_error_hz;
+    r.carr_error_filt_hz = c.carr_error_filt_hz;
+    r.code_error_chips = c.code_error_chips;
+    r.code_error_filt_chips = c.code_error_filt_chips;
+    r.K_blk_samples = c.K_blk_samples;
+    r.carrier_phase_rate_step_rad = c.carrier_phase_rate_step_rad;
+    r.code_phase_rate_step_chips = c.code_phase_rate_step_chips;
+    r.rem_carr_phase_rad = c.rem_carr_phase_rad;
+    r.current_prn_length_samples = c.current_prn_length_samples;
+    r.spc = c.spc;
+#pragma unroll
+    for (int i = 0; i < 2; i++) {
+        r.ve[i] = c.ve[i];
+        r.e[i] = c.e[i];
+        r.p[i] = c.p[i];
+        r.l[i] = c.l[i];
+        r.vl[i] = c.vl[i];
+        r.p_data[i] = c.p_data[i];
+        r.p_old[i] = c.p_old[i];
+    }
+    r.current_symbol = c.current_symbol;
+    r.current_data_symbol = c.current_data_symbol;
+    r.lf_idx = c.lf_idx;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        r.lfi[i] = c.lf_inputs[(c.lf_idx + i) & 3];
+        r.lfo[i] = c.lf_outputs[(c.lf_idx + i) & 3];
+    }
+    r.fp_w = c.fp_w;
+    r.fp_x = c.fp_x;
+    r.hist_head = c.hist_head;
+    r.hist_count = c.hist_count;
+    r.if_num = c.if_num;
+    r.if_cyc = c.if_cyc;
+    r.m = mcopy;
+}
+
+// The register members back into the memory copy (the lock-detector members and sign bits are
+// there already).
+__device__ __forceinline__ void rchan_store(const RChan& r, TrkChannel& c)
+{
+    c.state = r.state;
+    c.geo = r.geo;
+    c.narrow = r.narrow;
+    c.ext_count = r.ext_count;
+    c.cloop = r.cloop;
+    c.pull_in = r.pull_in;
+    c.pll_180 = r.pll_180;
+    c.acc_phase_init = r.acc_phase_init;
+    c.sign_count = r.sign_count;
+    c.prn = r.prn;
+    c.acq_sample_stamp = r.acq_sample_stamp;
+    c.nitems_read = r.nitems_read;
+    c.epoch_start = r.epoch_start;
+    c.carrier_doppler_hz = r.carrier_doppler_hz;
+    c.carrier_phase_step_rad = r.carrier_phase_step_rad;
+    c.code_freq_chips = r.code_freq_chips;
+    c.code_phase_step_chips = r.code_phase_step_chips;
+    c.rem_code_phase_chips = r.rem_code_phase_chips;
+    c.rem_code_phase_samples = r.rem_code_phase_samples;
+    c.acc_carrier_phase_rad = r.acc_carrier_phase_rad;
+    c.carr_phase_error_hz = r.carr_phase_error_hz;
+    c.carr_error_filt_hz = r.carr_error_filt_hz;
+    c.code_error_chips = r.code_error_chips;
+    c.code_error_filt_chips = r.code_error_filt_chips;
+    c.K_blk_samples = r.K_blk_samples;
+    c.carrier_phase_rate_step_rad = r.carrier_phase_rate_step_rad;
+    c.code_phase_rate_step_chips = r.code_phase_rate_step_chips;
+    c.rem_carr_phase_rad = r.rem_carr_phase_rad;
+    c.current_prn_length_samples = r.current_prn_length_samples;
+    c.spc = r.spc;
+#pragma unroll
+    for (int i = 0; i < 2; i++) {
+        c.ve[i] = r.ve[i];
+        c.e[i] = r.e[i];
+        c.p[i] = r.p[i];
+        c.l[i] = r.l[i];
+        c.vl[i] = r.vl[i];
+        c.p_data[i] = r.p_data[i];
+        c.p_old[i] = r.p_old[i];
+    }
+    c.current_symbol = r.current_symbol;
+    c.current_data_symbol = r.current_data_symbol;
+    c.lf_idx = r.lf_idx;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        c.lf_inputs[(r.lf_idx + i) & 3] = r.lfi[i];
+        c.lf_outputs[(r.lf_idx + i) & 3] = r.lfo[i];
+    }
+    c.fp_w = r.fp_w;
+    c.fp_x = r.fp_x;
+    c.hist_head = r.hist_head;
+    c.hist_count = r.hist_count;
+    c.if_num = r.if_num;
+    c.if_cyc = r.if_cyc;
+}
 
 __device__ __forceinline__ void load_regs(const TrkParams& k, const TrkChannel& c, LoopRegs& r)
 {
@@ -234,9 +395,10 @@ __device__ float loop_filter_apply(const TrkParams& k, TrkChannel& c, float x)
 // Tracking_loop_filter::apply (tracking_loop_filter.cc:58-84) on the logical-order rings: the same
 // products in the same order (outputs[(idx+ii)%4] ≡ lfo[ii] before the insert, inputs[(idx'+ii)%4] ≡
 // lfi[ii] after it).
-__device__ float loop_filter_apply(const TrkParams&, LoopRegs& c, float x)
+template <class C>
+__device__ float loop_filter_apply(const TrkParams& k, C& c, float x)
 {
-    const LoopSet& q = c.q;
+    const LoopSet& q = loopset(k, c);
     float result = 0.0f;
 #pragma unroll
     for (int ii = 0; ii < 3; ii++)
@@ -281,10 +443,10 @@ __device__ void run_dll_pll(const TrkParams& k, C& c)
         disc = static_cast<double>(atan2f(c.p[1], c.p[0]));  // gr::fast_atan2f restated as atan2f
     c.carr_phase_error_hz = disc / kTwoPi;
     // d_current_correlation_time_s: the code period, or extend × code period once extended
-    const float T = c.narrow ? k.sync[c.geo].T_ext : static_cast<float>(k.code_period);
+    const float T = c.narrow ? syncset(k, c).T_ext : static_cast<float>(k.code_period);
     if ((c.pull_in && k.conf.enable_fll_pull_in) || k.conf.enable_fll_steady_state) {  // :1080-1097
         // d_current_correlation_time_s is a double: the code period, or (float)extend·(float)period
-        const double Td = c.narrow ? static_cast<double>(k.sync[c.geo].T_ext) : k.code_period;
+        const double Td = c.narrow ? static_cast<double>(syncset(k, c).T_ext) : k.code_period;
         const double fe = fll_diff_atan(c.p_old, c.p, 0.0, Td) / kTwoPi;
         c.p_old[0] = c.p[0];
         c.p_old[1] = c.p[1];
@@ -295,10 +457,10 @@ __device__ void run_dll_pll(const TrkParams& k, C& c)
     }
     c.carrier_doppler_hz = c.carr_error_filt_hz;
     if (k.veml) {
-        const double early = static_cast<double>(sqrtf(__fadd_rn(__fadd_rn(__fadd_rn(__fmul_rn(c.ve[0], c.ve[0]), __fmul_rn(c.ve[1], c.ve[1])),
+        const double early = static_cast<double>(sqrt_rn_f32(__fadd_rn(__fadd_rn(__fadd_rn(__fmul_rn(c.ve[0], c.ve[0]), __fmul_rn(c.ve[1], c.ve[1])),
                                                                           __fmul_rn(c.e[0], c.e[0])),
             __fmul_rn(c.e[1], c.e[1]))));
-        const double late = static_cast<double>(sqrtf(__fadd_rn(__fadd_rn(__fadd_rn(__fmul_rn(c.l[0], c.l[0]), __fmul_rn(c.l[1], c.l[1])),
+        const double late = static_cast<double>(sqrt_rn_f32(__fadd_rn(__fadd_rn(__fadd_rn(__fmul_rn(c.l[0], c.l[0]), __fmul_rn(c.l[1], c.l[1])),
                                                                          __fmul_rn(c.vl[0], c.vl[0])),
             __fmul_rn(c.vl[1], c.vl[1]))));
         const double s = early + late;
@@ -377,39 +539,44 @@ __device__ void update_tracking_vars(const TrkParams& k, C& c, TrkHist* h)
 
 __device__ __forceinline__ int bit_at(const uint32_t* bits, int i) { return (bits[i >> 5] >> (i & 31)) & 1; }
 
-__device__ void push_sign(const TrkParams& k, TrkChannel& c, float prompt_re)
+template <class C>
+__device__ void push_sign(const TrkParams& k, C& c, float prompt_re)
 {
-    const int cap = k.sync[c.geo].secondary_len;
+    const int cap = syncset(k, c).secondary_len;
     const uint32_t neg = prompt_re < 0.0f ? 1u : 0u;
+    uint32_t* bits = mem(c).sign_bits;
     if (c.sign_count == cap) {  // boost::circular_buffer::push_back on a full buffer drops the oldest
         for (int w = 0; w < kTrkMaxSecondary / 32; w++) {
-            const uint32_t carry = (w + 1 < kTrkMaxSecondary / 32) ? (c.sign_bits[w + 1] & 1u) : 0u;
-            c.sign_bits[w] = (c.sign_bits[w] >> 1) | (carry << 31);
+            const uint32_t carry = (w + 1 < kTrkMaxSecondary / 32) ? (bits[w + 1] & 1u) : 0u;
+            bits[w] = (bits[w] >> 1) | (carry << 31);
         }
         const int i = cap - 1;
-        c.sign_bits[i >> 5] = (c.sign_bits[i >> 5] & ~(1u << (i & 31))) | (neg << (i & 31));
+        bits[i >> 5] = (bits[i >> 5] & ~(1u << (i & 31))) | (neg << (i & 31));
     } else {
         const int i = c.sign_count++;
-        c.sign_bits[i >> 5] = (c.sign_bits[i >> 5] & ~(1u << (i & 31))) | (neg << (i & 31));
+        bits[i >> 5] = (bits[i >> 5] & ~(1u << (i & 31))) | (neg << (i & 31));
     }
 }
 
-__device__ bool acquire_secondary(const TrkParams& k, TrkChannel& c)
+template <class C>
+__device__ bool acquire_secondary(const TrkParams& k, C& c)
 {
     int corr = 0;
-    for (int i = 0; i < k.sync[c.geo].secondary_len; i++) {
-        const int neg = bit_at(c.sign_bits, i);
-        const int one = bit_at(k.sync[c.geo].secondary_bits, i);
+    const uint32_t* bits = mem(c).sign_bits;
+    for (int i = 0; i < syncset(k, c).secondary_len; i++) {
+        const int neg = bit_at(bits, i);
+        const int one = bit_at(syncset(k, c).secondary_bits, i);
         corr += (neg ^ one) ? 1 : -1;  // +1 for (real < 0, '0') and (real ≥ 0, '1')
     }
-    if (abs(corr) == k.sync[c.geo].secondary_len) {
+    if (abs(corr) == syncset(k, c).secondary_len) {
         c.pll_180 = corr < 0 ? 1 : 0;
         return true;
     }
     return false;
 }
 
-__device__ void clear_tracking_vars(TrkChannel& c)
+template <class C>
+__device__ void clear_tracking_vars(C& c)
 {
     c.p_data[0] = c.p_data[1] = 0.0f;
     c.p_old[0] = c.p_old[1] = 0.0f;
@@ -432,14 +599,16 @@ __device__ __forceinline__ void cadd(float* acc, const float* v, float sgn)
     acc[1] = __fadd_rn(acc[1], __fmul_rn(sgn, v[1]));
 }
 
-__device__ void zero_accu(TrkChannel& c)
+template <class C>
+__device__ void zero_accu(C& c)
 {
     c.ve[0] = c.ve[1] = c.e[0] = c.e[1] = c.p[0] = c.p[1] = 0.0f;
     c.l[0] = c.l[1] = c.vl[0] = c.vl[1] = 0.0f;
 }
 
 // log_data (:1376-1466) at epoch start nir, after update_tracking_vars.
-__device__ void log_data(const TrkParams& k, const TrkChannel& c, const float* taps, const float* pdata, uint64_t nir, gnsship_trk_dump_record* d)
+template <class C>
+__device__ void log_data(const TrkParams& k, const C& c, const float* taps, const float* pdata, uint64_t nir, gnsship_trk_dump_record* d)
 {
     if (!d) return;
     const int eo = k.veml ? 2 : 0;
@@ -462,8 +631,8 @@ __device__ void log_data(const TrkParams& k, const TrkChannel& c, const float* t
     d->carr_error_filt_hz = static_cast<float>(c.carr_error_filt_hz);
     d->code_error_chips = static_cast<float>(c.code_error_chips);
     d->code_error_filt_chips = static_cast<float>(c.code_error_filt_chips);
-    d->CN0_SNV_dB_Hz = c.cn0_db_hz;
-    d->carrier_lock_test = c.carrier_lock_test;
+    d->CN0_SNV_dB_Hz = mem(c).cn0_db_hz;
+    d->carrier_lock_test = mem(c).carrier_lock_test;
     d->aux1 = static_cast<float>(c.rem_code_phase_samples);
     d->aux2 = static_cast<double>(nir + static_cast<uint64_t>(c.current_prn_length_samples));
     d->PRN = c.prn;
@@ -487,7 +656,8 @@ __device__ __forceinline__ bool seconds_exceed(uint64_t elapsed, uint32_t limit_
     return elapsed >= (static_cast<uint64_t>(limit_s) + 1u) * fs_int;
 }
 
-__device__ double epoch_pre(const TrkParams& k, TrkChannel& c, const float* taps, const float* pdata, gnsship_trk_epoch& rec, TrkHist* h,
+template <class C>
+__device__ double epoch_pre(const TrkParams& k, C& c, const float* taps, const float* pdata, gnsship_trk_epoch& rec, TrkHist* h,
     gnsship_trk_dump_record* dump)
 {
     const uint64_t nir = c.epoch_start;
@@ -495,8 +665,8 @@ __device__ double epoch_pre(const TrkParams& k, TrkChannel& c, const float* taps
     rec.sample_counter = nir;
     if (c.pull_in && seconds_exceed(nir - c.acq_sample_stamp, k.conf.pull_in_time_s, fs_int)) {
         c.pull_in = 0;
-        c.carrier_fail = 0;
-        c.code_fail = 0;
+        mem(c).carrier_fail = 0;
+        mem(c).code_fail = 0;
     }
     const int eo = k.veml ? 2 : 0;
     const int st = c.state;
@@ -517,14 +687,14 @@ __device__ double epoch_pre(const TrkParams& k, TrkChannel& c, const float* taps
         c.spc = k.conf.early_late_space_chips;
         rec.prompt_i = static_cast<double>(c.p[0]);  // diagnostic: the epoch's prompt (no symbol flag in state 2)
         rec.prompt_q = static_cast<double>(c.p[1]);
-        if (seconds_exceed(nir - c.acq_sample_stamp, k.conf.bit_synchronization_time_limit_s, fs_int)) c.carrier_fail = 300000;
+        if (seconds_exceed(nir - c.acq_sample_stamp, k.conf.bit_synchronization_time_limit_s, fs_int)) mem(c).carrier_fail = 300000;
         return k.code_period;
     }
     // save_correlation_results
     float sgn = 1.0f;
-    if (k.sync[c.geo].secondary) {
-        sgn = bit_at(k.sync[c.geo].secondary_bits, c.current_symbol) ? -1.0f : 1.0f;
-        c.current_symbol = (c.current_symbol + 1) % k.sync[c.geo].secondary_len;
+    if (syncset(k, c).secondary) {
+        sgn = bit_at(syncset(k, c).secondary_bits, c.current_symbol) ? -1.0f : 1.0f;
+        c.current_symbol = (c.current_symbol + 1) % syncset(k, c).secondary_len;
     }
     if (k.veml) {
         cadd(c.ve, taps, sgn);
@@ -534,13 +704,13 @@ __device__ double epoch_pre(const TrkParams& k, TrkChannel& c, const float* taps
     cadd(c.p, taps + eo + 2, sgn);
     cadd(c.l, taps + eo + 4, sgn);
     const float* src = k.track_pilot ? pdata : taps + eo + 2;
-    if (k.sync[c.geo].symbols_per_bit > 1) {
-        if (k.sync[c.geo].data_secondary_len > 0) {
-            cadd(c.p_data, src, bit_at(k.sync[c.geo].data_secondary_bits, c.current_data_symbol) ? -1.0f : 1.0f);
-            c.current_data_symbol = (c.current_data_symbol + 1) % k.sync[c.geo].data_secondary_len;
+    if (syncset(k, c).symbols_per_bit > 1) {
+        if (syncset(k, c).data_secondary_len > 0) {
+            cadd(c.p_data, src, bit_at(syncset(k, c).data_secondary_bits, c.current_data_symbol) ? -1.0f : 1.0f);
+            c.current_data_symbol = (c.current_data_symbol + 1) % syncset(k, c).data_secondary_len;
         } else {
             cadd(c.p_data, src, 1.0f);
-            c.current_data_symbol = (c.current_data_symbol + 1) % k.sync[c.geo].symbols_per_bit;
+            c.current_data_symbol = (c.current_data_symbol + 1) % syncset(k, c).symbols_per_bit;
         }
     } else {
         c.p_data[0] = src[0];
@@ -558,13 +728,13 @@ __device__ double epoch_pre(const TrkParams& k, TrkChannel& c, const float* taps
             c.p_data[0] = c.p_data[1] = 0.0f;
         }
         c.ext_count++;
-        if (c.ext_count == k.sync[c.geo].extend - 1) {
+        if (c.ext_count == syncset(k, c).extend - 1) {
             c.ext_count = 0;
             c.state = 4;
         }
         return 0.0;
     }
-    return k.code_period * static_cast<double>(k.sync[c.geo].extend);
+    return k.code_period * static_cast<double>(syncset(k, c).extend);
 }
 
 template <class C>
@@ -579,7 +749,8 @@ __device__ __forceinline__ void epoch_loop(const TrkParams& k, C& c, TrkHist* h)
 
 // After epoch_pre returned a coherent time: the rest of state 2 / 4 given the lock outcome (epoch_loop
 // has run iff locked).
-__device__ void epoch_post(const TrkParams& k, TrkChannel& c, const float* taps, const float* pdata, gnsship_trk_epoch& rec, bool locked,
+template <class C>
+__device__ void epoch_post(const TrkParams& k, C& c, const float* taps, const float* pdata, gnsship_trk_epoch& rec, bool locked,
     gnsship_trk_dump_record* dump)
 {
     const uint64_t nir = c.epoch_start;
@@ -596,9 +767,9 @@ __device__ void epoch_post(const TrkParams& k, TrkChannel& c, const float* taps,
         GNSSHIP_TRK_LOOP_STAMP(12);
         rec.flags |= 16;
         if (!c.pull_in) {
-            if (k.sync[c.geo].secondary || k.sync[c.geo].symbols_per_bit > 1) {
+            if (syncset(k, c).secondary || syncset(k, c).symbols_per_bit > 1) {
                 push_sign(k, c, taps[eo + 2]);
-                if (c.sign_count == k.sync[c.geo].secondary_len) next_state = acquire_secondary(k, c);
+                if (c.sign_count == syncset(k, c).secondary_len) next_state = acquire_secondary(k, c);
             } else {
                 next_state = true;
             }
@@ -609,7 +780,7 @@ __device__ void epoch_post(const TrkParams& k, TrkChannel& c, const float* taps,
             c.sign_count = 0;
             c.current_symbol = 0;
             c.current_data_symbol = 0;
-            if (k.sync[c.geo].extend > 1) {  // extended integration (:1890-1926): narrow loops and taps, state 3
+            if (syncset(k, c).extend > 1) {  // extended integration (:1890-1926): narrow loops and taps, state 3
                 c.ext_count = 0;
                 c.narrow = 1;
                 c.spc = k.spc_n;
@@ -634,20 +805,22 @@ __device__ void epoch_post(const TrkParams& k, TrkChannel& c, const float* taps,
         c.p_data[0] = c.p_data[1] = 0.0f;
     }
     zero_accu(c);
-    if (k.sync[c.geo].extend > 1) c.state = 3;  // next coherent integration cycle
+    if (syncset(k, c).extend > 1) c.state = 3;  // next coherent integration cycle
 }
 
-__device__ __forceinline__ void advance_if(const TrkParams& k, TrkChannel& c, int32_t consumed);
+template <class C>
+__device__ __forceinline__ void advance_if(const TrkParams& k, C& c, int32_t consumed);
 
 // The record's loop outputs and consume_each (:2061); false when the channel stopped (loss of lock).
-__device__ bool epoch_finish(const TrkParams& k, TrkChannel& c, gnsship_trk_epoch& rec)
+template <class C>
+__device__ bool epoch_finish(const TrkParams& k, C& c, gnsship_trk_epoch& rec)
 {
     if (c.pll_180) rec.flags |= 4;
     rec.code_phase_samples = c.rem_code_phase_samples;
     rec.carrier_phase_rads = c.acc_carrier_phase_rad;
     rec.carrier_doppler_hz = c.carrier_doppler_hz;
-    rec.cn0_db_hz = static_cast<double>(c.cn0_db_hz);
-    rec.carrier_lock_test = c.carrier_lock_test;
+    rec.cn0_db_hz = static_cast<double>(mem(c).cn0_db_hz);
+    rec.carrier_lock_test = mem(c).carrier_lock_test;
     rec.code_freq_chips = c.code_freq_chips;
     rec.rem_code_phase_chips = c.rem_code_phase_chips;
     rec.rem_carr_phase_rad = c.rem_carr_phase_rad;
@@ -659,7 +832,8 @@ __device__ bool epoch_finish(const TrkParams& k, TrkChannel& c, gnsship_trk_epoc
 }
 
 // The IF phase follows the consumed samples (gnsship_trk_conf::if_hz): if_num += if_mod·len (mod fs).
-__device__ __forceinline__ void advance_if(const TrkParams& k, TrkChannel& c, int32_t consumed)
+template <class C>
+__device__ __forceinline__ void advance_if(const TrkParams& k, C& c, int32_t consumed)
 {
     if (!k.has_if) return;
     c.if_num = (c.if_num + k.if_mod * static_cast<int64_t>(consumed)) % k.fs_int;
@@ -668,12 +842,14 @@ __device__ __forceinline__ void advance_if(const TrkParams& k, TrkChannel& c, in
 
 // do_correlation_step's carrier arguments with the IF fused in (include/gnsship.h if_hz): the
 // correlator wipes off IF + Doppler, the loop keeps the IF-free quantities.
-__device__ __forceinline__ float corr_rem_carr(const TrkParams& k, const TrkChannel& c)
+template <class C>
+__device__ __forceinline__ float corr_rem_carr(const TrkParams& k, const C& c)
 {
     if (!k.has_if) return c.rem_carr_phase_rad;
     return static_cast<float>(fmod(static_cast<double>(c.rem_carr_phase_rad) + kTwoPi * c.if_cyc, kTwoPi));
 }
-__device__ __forceinline__ float corr_phase_step(const TrkParams& k, const TrkChannel& c)
+template <class C>
+__device__ __forceinline__ float corr_phase_step(const TrkParams& k, const C& c)
 {
     return static_cast<float>(c.carrier_phase_step_rad + k.if_step_rad);  // + 0.0 without IF: exact
 }

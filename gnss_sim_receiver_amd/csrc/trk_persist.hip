@@ -76,6 +76,7 @@ struct PEpoch {
     int32_t published;   // anchors ready: generic blocks, or AVX segments (S + 1 = all, tail included)
     int32_t locked;      // lock_status outcome (wave 1) for the loop update (wave 0)
     double coh;          // epoch_pre's coherent integration time (0: no lock test this epoch)
+    float trace_rem_carr, trace_step;  // the carrier arguments as passed (IF folded in)
     float red[kPWaves][2 * (kMaxTaps + 1)];
     float taps[2 * kMaxTaps + 2];  // the epoch's tap sums (+ the data prompt), as epoch_update reads them
     gnsship_trk_epoch rec;
@@ -397,7 +398,7 @@ template <int FMT, int NT, bool DATA, bool AVX, bool THRU>
 __global__ __launch_bounds__(kPThreads, persist_waves_per_simd<THRU>()) void trk_persist_kernel(const TrkParams* __restrict__ pk, TrkChannel* __restrict__ chans,
     const CodeDesc* __restrict__ codes, int n_codes, const void* __restrict__ samples, uint64_t buf_first, int64_t buf_len, int max_rounds,
     int n_chans, int code_cap_floats, int avx_g, gnsship_trk_epoch* __restrict__ rec, gnsship_trk_dump_record* __restrict__ dump,
-    int* __restrict__ ran_count)
+    gnsship_trk_corr_trace* __restrict__ trace, int* __restrict__ ran_count)
 {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     __shared__ TrkChannel sc;
@@ -443,6 +444,10 @@ __global__ __launch_bounds__(kPThreads, persist_waves_per_simd<THRU>()) void trk
             // the epoch's two phasors (cpu_multicorrelator_real_codes.cc:115,123), lane 0: rem_carr,
             // lane 1: −step, each as the once-rounded double cos/sin (nco_math.h)
             const float a = lane == 0 ? corr_rem_carr(k, sc) : -corr_phase_step(k, sc);
+            if (lane == 0) {
+                ep.trace_rem_carr = corr_rem_carr(k, sc);
+                ep.trace_step = corr_phase_step(k, sc);
+            }
             double sd, cd;
             sincos(static_cast<double>(a), &sd, &cd);
             const float sf = static_cast<float>(sd), cf = static_cast<float>(cd);
@@ -463,7 +468,12 @@ __global__ __launch_bounds__(kPThreads, persist_waves_per_simd<THRU>()) void trk
         }
         __syncthreads();  // also: the code replicas are staged (first epoch)
         if (!ep.runnable) break;
-        const i4v span = sample_span<FMT>(samples, ep.job.sample_offset, N);
+        // the epoch's first sample as a wave-uniform value: read from LDS it is per-lane, and a per-lane
+        // buffer resource turns every sample load into a waterfall loop
+        const uint64_t off64 = static_cast<uint64_t>(ep.job.sample_offset);
+        const int64_t off_u = static_cast<int64_t>((static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(off64 >> 32)))) << 32) |
+                                                   static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(off64 & 0xffffffffu))));
+        const i4v span = sample_span<FMT>(samples, off_u, N);
         f2 acc[NT + 1];
 #pragma unroll
         for (int t = 0; t <= NT; t++) acc[t] = f2{0.0f, 0.0f};
@@ -547,6 +557,21 @@ __global__ __launch_bounds__(kPThreads, persist_waves_per_simd<THRU>()) void trk
             const size_t slot = static_cast<size_t>(e) * n_chans + ch;
             if (rec) rec[slot] = ep.rec;
             if (dump && (ep.rec.flags & 16)) dump[slot] = ep.dump;
+            if (trace) {
+                gnsship_trk_corr_trace tr{};
+                tr.sample_counter = sc.epoch_start;
+                tr.n_samples = N;
+                tr.n_taps = NT;
+                tr.rem_carrier_phase_rad = ep.trace_rem_carr;
+                tr.phase_step_rad = ep.trace_step;
+                tr.rem_code_phase_samples = ep.job.rem_code;
+                tr.code_phase_step_samples = ep.job.code_step;
+                for (int t = 0; t < 5; t++) tr.shifts[t] = ep.job.shifts[t];
+                for (int t = 0; t < 10; t++) tr.taps[t] = t < 2 * NT ? taps[t] : 0.0f;
+                tr.data_prompt[0] = DATA ? pdata[0] : 0.0f;
+                tr.data_prompt[1] = DATA ? pdata[1] : 0.0f;
+                trace[slot] = tr;
+            }
             atomicAdd(ran_count + e, 1);
             GNSSHIP_TRK_STAMP(e, 6);
         }
@@ -595,7 +620,7 @@ size_t trk_persist_lds_bytes(const TrkParams& p, int code_cap_floats, bool avx) 
 
 hipError_t launch_trk_persist(const TrkParams* params_dev, const TrkParams& params, TrkChannel* chans, int n_chans, const CodeDesc* codes,
     int n_codes, int code_cap_floats, const void* samples, int fmt, uint64_t buf_first, int64_t buf_len, int max_rounds, gnsship_trk_epoch* rec,
-    gnsship_trk_dump_record* dump, int* ran_count, bool avx, hipStream_t stream)
+    gnsship_trk_dump_record* dump, gnsship_trk_corr_trace* trace, int* ran_count, bool avx, hipStream_t stream)
 {
     int avx_g = 0;
     const size_t lds = persist_lds(params, code_cap_floats, avx, &avx_g);
@@ -611,7 +636,7 @@ hipError_t launch_trk_persist(const TrkParams* params_dev, const TrkParams& para
         hipError_t e0 = hipFuncSetAttribute(reinterpret_cast<const void*>(kfn), hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)); \
         if (e0 != hipSuccess) return e0;                                                                                                       \
         hipLaunchKernelGGL(kfn, grid, block, lds, stream, params_dev, chans, codes, n_codes, samples, buf_first, buf_len, max_rounds, n_chans,  \
-            code_cap_floats, avx_g, rec, dump, ran_count);                                                                                            \
+            code_cap_floats, avx_g, rec, dump, trace, ran_count);                                                                                     \
     } while (0)
 #define GNSSHIP_PERSIST_F(F)                                                      \
     do {                                                                          \

@@ -545,6 +545,16 @@ class DllPllVemlTracking:
                                                ctypes.byref(done)), "gnsship_trk_collect", self.ctx.h)
         return (out, done.value, dmp) if dump else (out, done.value)
 
+    def set_trace(self, enable: bool = True):
+        """gnsship_trk_set_trace: record every channel-epoch's correlator arguments and outputs."""
+        check(self.ctx.lib.gnsship_trk_set_trace(self.h, int(enable)), "gnsship_trk_set_trace", self.ctx.h)
+
+    def trace(self, max_rounds: int) -> np.ndarray:
+        """The last run's trace, [max_rounds, max_channels] TRK_TRACE_DTYPE (max_rounds of that run)."""
+        out = np.zeros((max_rounds, self.max_channels), abi.TRK_TRACE_DTYPE)
+        check(self.ctx.lib.gnsship_trk_trace_records(self.h, out.ctypes.data, out.size), "gnsship_trk_trace_records", self.ctx.h)
+        return out
+
     def states(self) -> np.ndarray:
         """Tracking state (0 idle/lost, 2, 3, 4) of every channel."""
         return np.array([self.channel_state(ch)[0] for ch in range(self.max_channels)], np.int32)

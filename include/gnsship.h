@@ -434,6 +434,26 @@ int gnsship_trk_launch(gnsship_trk* t, const void* dev_sig, int fmt, uint64_t bu
     int want_records, int want_dump);
 int gnsship_trk_collect(gnsship_trk* t, gnsship_trk_epoch* out, gnsship_trk_dump_record* dump, int* rounds_done);
 int gnsship_trk_channel_state(gnsship_trk* t, int channel, int* state, uint64_t* next_sample);
+/* Correlation trace: each channel-epoch's do_correlation_step call (dll_pll_veml_tracking.cc:1037-1062)
+ * as the engine ran it — the float arguments of Carrier_wipeoff_multicorrelator_resampler
+ * (cpu_multicorrelator_real_codes.cc:103-126, the carrier ones with the IF folded in) and the
+ * correlator outputs — so that a caller can re-run exactly those correlations on the reference's
+ * CPU correlator and compare them tap by tap.  Off by default (a debugging aid: 104 bytes per
+ * channel-epoch written to HBM). */
+typedef struct gnsship_trk_corr_trace {
+    uint64_t sample_counter;               /* absolute first sample of the epoch (nitems_read) */
+    int32_t n_samples;                     /* vector_length */
+    int32_t n_taps;
+    float rem_carrier_phase_rad, phase_step_rad;
+    float rem_code_phase_samples, code_phase_step_samples;  /* rem_code_phase_chips·spc, code_phase_step_chips·spc */
+    float shifts[5];                       /* local code shifts in code samples (narrow taps once narrowed) */
+    float taps[10];                        /* complex output per tap */
+    float data_prompt[2];                  /* the data correlator's prompt (track_pilot), else 0 */
+    int32_t pad;
+} gnsship_trk_corr_trace; /* 104 bytes */
+int gnsship_trk_set_trace(gnsship_trk* t, int enable);
+/* The last run's trace: max_rounds × max_channels records (the run's max_rounds), zero where no epoch ran. */
+int gnsship_trk_trace_records(gnsship_trk* t, gnsship_trk_corr_trace* out, int max_records);
 int gnsship_trk_destroy(gnsship_trk* t);
 
 /* ------------------------------------------------------------------------------------------ */

@@ -622,7 +622,7 @@ static void* orc_batch_worker(void* p)
     for (int j = a->j0; j < a->j1; j++) {
         const orc_job* jb = &a->jobs[j];
         orc_multicorrelator_impl(a->out + (size_t)j * 2 * ORC_MAX_TAPS, a->samples + 2 * jb->sample_offset, a->codes[jb->code_id],
-            a->code_lengths[jb->code_id], jb->shifts_chips, jb->n_taps, jb->flags & 3, jb->rem_carrier_phase_rad, jb->phase_step_rad,
+            a->code_lengths[jb->code_id], jb->shifts_chips, jb->n_taps, jb->flags & 7, jb->rem_carrier_phase_rad, jb->phase_step_rad,
             jb->phase_rate_step_rad, jb->rem_code_phase_chips, jb->code_phase_step_chips, jb->code_phase_rate_step_chips, jb->n_samples,
             scratch, a->accum_f64);
     }

@@ -1,0 +1,89 @@
+"""Epoch phase timeline of the fast AVX persistent tracking kernel (trk_fast.hip), C2 workload.
+
+    make prof && python scripts/trk_fast_profile.py [channels]
+
+Stamps (wall_clock64, 100 MHz) per channel-epoch, lane 0 of the stamping wave: 0 epoch start (wave 0),
+1 job derived, 2 replay done (wave 0), 3/4/5 correlating waves 1/2/3 done, 6 tap sums read (wave 0,
+after the barrier), 7 loop update + records done; 8 lock_status start (wave 1), 9 run_dll_pll start,
+10 its end, 11 update_tracking_vars end (wave 0).  The channels bit-synchronise first (state 4, as in
+bench.py)."""
+import ctypes
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+os.environ.setdefault("GNSSHIP_LIB_PATH", os.path.join(os.path.dirname(os.path.abspath(__file__)), "libgnsship_prof.so"))
+import numpy as np  # noqa: E402
+
+from gnss_sim_receiver_amd import abi, engine, signals  # noqa: E402
+
+EP = 64
+SLOTS = 32
+
+
+def main():
+    n_ch = int(sys.argv[1]) if len(sys.argv) > 1 else 12
+    fs, vl = 4e6, 4000
+    lib = abi.load()
+    lib.gnsship_debug_trk_fast_profile.argtypes = [ctypes.c_void_p]
+    ctx = engine.Context(0)
+    sats = signals.random_sky(32, seed=0x6E550002)
+    first = int(11 * fs)
+    for s in sats:
+        s.bits = "1000101100110"
+    pre = 500
+    block = signals.generate_if(fs, (pre + EP + 4) * vl, sats, seed=1, start=first - 2 * vl)
+    trk = engine.DllPllVemlTracking(ctx, abi.TrkConf.defaults(abi.SYS_GPS_L1CA, fs, vl, rotator=abi.ROTATOR_AVX), n_ch)
+    for i, s in enumerate(sats):
+        ctx.set_code(300 + i, s.code)
+    for ch in range(n_ch):
+        s = sats[ch % 32]
+        trk.start(ch, 300 + ch % 32, signals.acq_delay_samples(s, fs, 0, first), s.doppler_hz, 0, first)
+    dev = ctx.upload(block)
+    trk.run(dev, first - 2 * vl, pre, n_buffer_samples=len(block), records=False)
+    prof = engine.DeviceBuffer(ctx, n_ch * EP * SLOTS * 8)
+    prof.upload(np.zeros(n_ch * EP * SLOTS, np.uint64))
+    lib.gnsship_debug_trk_fast_profile(ctypes.c_void_p(prof.ptr))
+    ctx.event_record(0)
+    trk.run(dev, first - 2 * vl, EP, n_buffer_samples=len(block), records=False)
+    ctx.event_record(1)
+    ms = ctx.event_elapsed_ms(0, 1)
+    lib.gnsship_debug_trk_fast_profile(ctypes.c_void_p(0))
+    print("states:", sorted(set(trk.channel_state(ch)[0] for ch in range(n_ch))), f"launch {ms:.3f} ms for {EP} epochs")
+    t = np.zeros(n_ch * EP * SLOTS, np.uint64)
+    prof.download(t)
+    t = t.reshape(n_ch, EP, SLOTS).astype(np.int64)
+    us = lambda v: v / 100.0  # noqa: E731
+    nxt = np.concatenate([t[:, 1:, 0:1], np.zeros((n_ch, 1, 1), np.int64)], axis=1)
+    t = np.concatenate([t, nxt], axis=2)  # slot 32 = next epoch start
+    v = t[:, 1:-1, :]
+    print(f"{n_ch} channels: epoch period {us(np.median(np.diff(t[:, :, 0], axis=1))):.2f} us (median)")
+    rows = [("derive", 0, 1), ("derive -> replay done", 1, 2), ("derive -> wave1 corr done", 1, 3), ("derive -> wave2 corr done", 1, 4),
+            ("derive -> wave3 corr done", 1, 5), ("replay done -> sums read", 2, 6), ("sums read -> loop done", 6, 7),
+            ("  sums read -> run_dll_pll", 6, 9), ("  run_dll_pll", 9, 10), ("  update_tracking_vars", 10, 11),
+            ("  tracking_vars -> loop done", 11, 7), ("  lock_status start (wave 1) after sums", 6, 8), ("loop done -> next epoch", 7, 32),
+            ("  sums read -> tap sums", 6, 16), ("  tap sums -> epoch_pre done", 16, 17), ("  epoch_pre -> published", 17, 18),
+            ("  published -> run_dll_pll", 18, 9), ("  lock_status (wave 1)", 8, 26), ("  tracking_vars -> lock seen", 11, 19),
+            ("  lock seen -> epoch_post done", 19, 24), ("  epoch_finish", 24, 25), ("  epoch_finish -> loop done (records)", 25, 7)]
+    for nm, a, b in rows:
+        ok = (v[:, :, a] > 0) & (v[:, :, b] > 0)
+        if not ok.any():
+            continue
+        d = us(v[:, :, b] - v[:, :, a])[ok]
+        print(f"  {nm:40s} median {np.median(d):7.2f} us  p90 {np.percentile(d, 90):7.2f}  (n={ok.sum()})")
+    for nm, a, b, wa, wb in [("replay", 12, 13, 1, 2), ("loop update", 14, 15, 6, 7)]:
+        ok = (v[:, :, a] > 0) & (v[:, :, b] > 0) & (v[:, :, wa] > 0) & (v[:, :, wb] > 0)
+        if not ok.any():
+            continue
+        cyc = (v[:, :, b] - v[:, :, a])[ok].astype(np.float64)
+        wall = us(v[:, :, wb] - v[:, :, wa])[ok]
+        print(f"  {nm:40s} median {np.median(cyc):8.0f} shader cycles, clock {np.median(cyc / wall) / 1e3:.2f} GHz")
+    for ch in range(min(n_ch, 4)):
+        ids = [int(t[ch, 0, 20 + w]) for w in range(4)]
+        print(f"  channel {ch} HW_ID per wave: " + ", ".join(f"w{w} simd {(h >> 4) & 3} slot {h & 15} cu {(h >> 8) & 15} se {(h >> 13) & 7}" for w, h in enumerate(ids)))
+    trk.close()
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()
