@@ -45,9 +45,10 @@ clean:
 
 # C++ mirror-class test (links the product library and, as the checker, the oracle source)
 MIRROR_TEST := tests/cpp/mirror_test
-$(MIRROR_TEST): tests/cpp/mirror_test.cpp include/gnsship_cpp.hpp include/gnsship.h oracle/gnss_oracle.c $(LIB)
+$(MIRROR_TEST): tests/cpp/mirror_test.cpp include/gnsship_cpp.hpp include/gnsship.h oracle/gnss_oracle.c oracle/avx_port.c $(LIB)
 	gcc -O2 -fPIC -ffp-contract=off -std=gnu11 -c oracle/gnss_oracle.c -o build/gnss_oracle_test.o
-	g++ -O2 -std=c++17 -Iinclude tests/cpp/mirror_test.cpp build/gnss_oracle_test.o -o $@ -L$(PKG) -lgnsship -Wl,-rpath,'$$ORIGIN/../../$(PKG)' -lpthread -lm
+	gcc -O2 -fPIC -ffp-contract=off -std=gnu11 -c oracle/avx_port.c -o build/avx_port_test.o
+	g++ -O2 -std=c++17 -Iinclude tests/cpp/mirror_test.cpp build/gnss_oracle_test.o build/avx_port_test.o -o $@ -L$(PKG) -lgnsship -Wl,-rpath,'$$ORIGIN/../../$(PKG)' -lpthread -lm
 all: $(MIRROR_TEST)
 
 # Profiling variant (workgroup phase timestamps in corr_batch_kernel; scripts/corr_wg_profile.py)

@@ -24,8 +24,8 @@
 //    members; wave 0 runs run_dll_pll + update_tracking_vars speculatively and keeps them only when
 //    the lock test (published by wave 1) passes, as the reference runs them only then.
 //
-// Epochs too long for the LDS task slots, the generic rotator and high_dyn stay on trk_persist.hip
-// / the round-based loop.
+// Epochs too long for the LDS task slots, the generic rotator, high_dyn and runs of more channels
+// than CUs stay on trk_persist.hip / the round-based loop.
 #include <cstdlib>
 
 #include "corr_device.h"
@@ -255,13 +255,16 @@ __device__ __forceinline__ float fast_replay(float x, float c, float k2, int M, 
             half += 2 * kAvxLanes;
         }
     }
-#pragma unroll 1
-    for (int t = full * kTB; t < S - 1; t++) {
-        x = pstep<1, true>(x, c, k2, off);
-        if (t == full * kTB) x = pnormalise(x);
-        x = ppow<G - 1>(x, c, k2);
+    if (full * kTB < S - 1) {  // a partial block: its first task normalises, the rest do not
+        x = ppow<G - 1>(pnormalise(pstep<1, true>(x, c, k2, off)), c, k2);
         off += kSlotRow;
         half += 2 * kAvxLanes;
+#pragma unroll 1
+        for (int t = full * kTB + 1; t < S - 1; t++) {
+            x = ppow<G - 4>(pstep<4, true>(x, c, k2, off), c, k2);
+            off += kSlotRow;
+            half += 2 * kAvxLanes;
+        }
     }
     __hip_atomic_store(half, __builtin_bit_cast(uint32_t, x), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);  // the last task: its consumers continue
     if (tail > 0) {  // z_l(M) for the tail (chain 0's is what the reference keeps)
@@ -512,6 +515,7 @@ __global__ __launch_bounds__(kFThreads, fast_waves_per_simd<THRU>()) void trk_fa
 #pragma unroll
         for (int t = 0; t <= NT; t++) acc[t] = f2{0.0f, 0.0f};
         if (wave == 0) {
+            GNSSHIP_FCLK(e, 28);
             float xl = (lane & 1) ? zinit.y : zinit.x;
             if (lane < 2 * kAvxLanes) xl = fast_replay<G>(xl, job.dz_re, (lane & 1) ? job.dz_im : -job.dz_im, M, S, tail, Zs, lane);
             if (tail > 0) {
@@ -538,10 +542,16 @@ __global__ __launch_bounds__(kFThreads, fast_waves_per_simd<THRU>()) void trk_fa
 #ifdef GNSSHIP_FAST_SERIAL
             __syncthreads();
 #endif
+#ifdef GNSSHIP_FAST_NOCONSUME  // diagnostic only: the correlating waves idle (wrong sums)
+            if (false) {
+#endif
             if (job.in_margin)
                 fast_consume<FMT, NT, DATA, true, G>(job, span, c0, c1, L, Zs, lane, wave, acc);
             else
                 fast_consume<FMT, NT, DATA, false, G>(job, span, c0, c1, L, Zs, lane, wave, acc);
+#ifdef GNSSHIP_FAST_NOCONSUME
+            }
+#endif
             GNSSHIP_FSTAMP(e, 2 + wave);  // 3, 4, 5: each correlating wave done
         }
         // DPP row sums only (no cross-row shuffle through LDS): the first lane of each 16-lane row
@@ -702,7 +712,12 @@ bool trk_fast_supported(const TrkParams& p, int code_cap_floats, int n_chans)
     if (!trk_persist_supports(p) || p.conf.rotator != GNSSHIP_ROTATOR_AVX || p.conf.high_dyn) return false;
     if (const char* env = std::getenv("GNSSHIP_TRK_FAST")) {  // A/B against trk_persist.hip
         if (env[0] == '0') return false;
+        if (env[0] == '1') return fast_lds(p, code_cap_floats, n_chans, nullptr, nullptr) > 0;
     }
+    // More channels than CUs: channel-epochs per second, not epoch latency, is what counts, and
+    // trk_persist.hip's four equal correlating waves sustain more of them (measured at 65536
+    // channels: 76.6 M vs 64.8 M channel-epochs/s)
+    if (n_chans > 256) return false;
     return fast_lds(p, code_cap_floats, n_chans, nullptr, nullptr) > 0;
 }
 

@@ -67,16 +67,30 @@ __device__ float smooth(Smoother& s, float raw, float alpha, float one_minus_alp
     return v;
 }
 
-__device__ float cn0_m2m4(const float* prompt, int length, float coh_integration_time_s)
+// The three running sums over the prompt buffer in index order.  N > 0: the length as a constant
+// (the buffer read in one batch of LDS loads instead of a load round trip per entry).
+template <int N>
+__device__ __forceinline__ void m2m4_sums(const float* prompt, int length, float& psig, float& m_2, float& m_4)
 {
-    float psig = 0.0f, m_2 = 0.0f, m_4 = 0.0f, aux;
-    const float n = static_cast<float>(length);
-    for (int i = 0; i < length; i++) {
+    float aux;
+    const int n = N > 0 ? N : length;
+#pragma unroll
+    for (int i = 0; i < (N > 0 ? N : n); i++) {
         psig = __fadd_rn(psig, fabsf(prompt[2 * i]));
         aux = __fadd_rn(__fmul_rn(prompt[2 * i + 1], prompt[2 * i + 1]), __fmul_rn(prompt[2 * i], prompt[2 * i]));
         m_2 = __fadd_rn(m_2, aux);
         m_4 = __fadd_rn(m_4, __fmul_rn(aux, aux));
     }
+}
+
+__device__ float cn0_m2m4(const float* prompt, int length, float coh_integration_time_s)
+{
+    float psig = 0.0f, m_2 = 0.0f, m_4 = 0.0f, aux;
+    const float n = static_cast<float>(length);
+    if (length == 20)  // every system's default (cn0_samples)
+        m2m4_sums<20>(prompt, length, psig, m_2, m_4);
+    else
+        m2m4_sums<0>(prompt, length, psig, m_2, m_4);
     psig = __fdiv_rn(psig, n);
     psig = __fmul_rn(psig, psig);
     m_2 = __fdiv_rn(m_2, n);

@@ -539,6 +539,20 @@ int orc_multicorrelator_real_codes(float* corr_out, const float* sig_in, const f
         code_phase_rate_step_chips, signal_length_samples, scratch, 0);
 }
 
+/* The AVX restatement (oracle/avx_port.c) for the timed CPU baseline: bit-identical to the scalar
+ * restatement, selected by orc_set_simd(1) (off by default; tests pin the two against each other). */
+int orc_simd_available(void);
+void orc_rotator_dot_prod_avx_vec(float* result, const float* in_common, float inc_re, float inc_im, float* phase,
+    const float* in_a, int num_a_vectors, unsigned int num_points);
+void orc_resampler_avx(float* out, const float* local_code, float rem_code_phase_chips, float code_phase_step_chips,
+    const float* shifts_chips, unsigned int code_length_chips, int num_out_vectors, unsigned int num_points);
+static int g_simd = 0;
+int orc_set_simd(int on)
+{
+    g_simd = (on && orc_simd_available()) ? 1 : 0;
+    return g_simd;
+}
+
 /* flags: bit0 high-dynamics resampler/rotator, bit1 the AVX rotator variant (the job flags of
  * gnsship_corr_job; high_dyn has only generic variants, so bit1 is ignored with bit0). */
 static int orc_multicorrelator_impl(float* corr_out, const float* sig_in, const float* local_code, int code_length_chips,
@@ -565,6 +579,9 @@ static int orc_multicorrelator_impl(float* corr_out, const float* sig_in, const 
     if (high_dyn)
         orc_high_dynamics_resampler_generic(codes, local_code, rem_code_phase_chips, code_phase_step_chips, code_phase_rate_step_chips,
             shifts_chips, (unsigned)code_length_chips, n_correlators, (unsigned)signal_length_samples);
+    else if (g_simd && (flags & 2))
+        orc_resampler_avx(codes, local_code, rem_code_phase_chips, code_phase_step_chips, shifts_chips, (unsigned)code_length_chips,
+            n_correlators, (unsigned)signal_length_samples);
     else
         orc_resampler_generic(codes, local_code, rem_code_phase_chips, code_phase_step_chips, shifts_chips, (unsigned)code_length_chips,
             n_correlators, (unsigned)signal_length_samples);
@@ -580,6 +597,8 @@ static int orc_multicorrelator_impl(float* corr_out, const float* sig_in, const 
         const float rr = cosf(-phase_rate_step_rad), ri = sinf(-phase_rate_step_rad);
         orc_high_dynamic_rotator_dot_prod_impl(corr_out, sig_in, inc_re, inc_im, rr, ri, phase, codes, n_correlators,
             (unsigned)signal_length_samples, accum_f64);
+    } else if ((flags & 2) && g_simd && !accum_f64) {
+        orc_rotator_dot_prod_avx_vec(corr_out, sig_in, inc_re, inc_im, phase, codes, n_correlators, (unsigned)signal_length_samples);
     } else if (flags & 2) {
         orc_rotator_dot_prod_avx_impl(corr_out, sig_in, inc_re, inc_im, phase, codes, n_correlators, (unsigned)signal_length_samples,
             accum_f64);

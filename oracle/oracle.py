@@ -116,6 +116,9 @@ def lib(fast: bool = False) -> ctypes.CDLL:
     L.orc_firdes_low_pass.argtypes = [ctypes.c_double] * 4 + [_f32p]
     L.orc_firdes_low_pass.restype = ctypes.c_int
     L.orc_fir_decimate.argtypes = [_f32p, ctypes.c_int64, _f32p, _f32p, ctypes.c_int, ctypes.c_int, _f32p]
+    L.orc_set_simd.argtypes = [ctypes.c_int]
+    L.orc_set_simd.restype = ctypes.c_int
+    L.orc_simd_available.restype = ctypes.c_int
     _LIBS[name] = L
     return L
 
@@ -179,6 +182,13 @@ def multicorrelator(sig, code, shifts, rem_carr, carr_step, rem_code, code_step,
     if rc:
         raise ValueError("oracle multicorrelator rejected arguments")
     return out.view(np.complex64)
+
+
+def set_simd(on: bool, fast: bool = False) -> bool:
+    """The AVX restatement of the AVX rotator + resampler (oracle/avx_port.c, bit-identical to the scalar
+    one) for jobs with the AVX flag: on for the timed CPU baseline.  Returns whether it is active
+    (False when this CPU lacks AVX2)."""
+    return bool(lib(fast).orc_set_simd(int(on)))
 
 
 def corr_batch(samples: np.ndarray, jobs: np.ndarray, codes: list, n_threads: int = 1, fast: bool = False,

@@ -71,6 +71,9 @@ def main():
             continue
         d = us(v[:, :, b] - v[:, :, a])[ok]
         print(f"  {nm:40s} median {np.median(d):7.2f} us  p90 {np.percentile(d, 90):7.2f}  (n={ok.sum()})")
+    ok = (v[:, :, 28] > 0) & (v[:, :, 13] > 0)
+    if ok.any():
+        print(f"  {'replay only (after barrier B + job)':40s} median {np.median((v[:, :, 13] - v[:, :, 28])[ok]):8.0f} shader cycles")
     for nm, a, b, wa, wb in [("replay", 12, 13, 1, 2), ("loop update", 14, 15, 6, 7)]:
         ok = (v[:, :, a] > 0) & (v[:, :, b] > 0) & (v[:, :, wa] > 0) & (v[:, :, wb] > 0)
         if not ok.any():
