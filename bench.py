@@ -524,15 +524,16 @@ def c1_receiver(torch, device, seconds=10.0, cpu_seconds=1.0):
 # ---------------------------------------------------------------------------------------------------
 # CPU baseline: the oracle's closed loop, one thread per channel (ctypes releases the GIL)
 def cpu_baseline(h, budget_s):
+    """The oracle's closed loop on the host: 12 threads, one per channel of the workload, over a
+    bounded sample of the same file.  For the AVX variant two figures: the AVX restatement
+    (oracle/avx_port.c — the arithmetic the reference's u_avx kernel runs on such a host; `value`)
+    and the scalar restatement of the same loop (`scalar_port`), each timed over part of the budget."""
     from oracle import trk as T
     from gnss_sim_receiver_amd import signals
     import platform
     from oracle import oracle as O
     O.build()
     rot = h["rotator"]
-    # the reference's AVX correlator form on this host (oracle/avx_port.c, bit-identical to the scalar
-    # restatement) for the AVX variant; the generic variant stays scalar, as volk's generic kernel
-    simd = O.set_simd(rot == 1, fast=True)
     # bounded sample of the same file (host copy of the first 0.6 s after the pre-roll start)
     n_s = int(0.6 * FS)
     x = h["x"][: n_s + 4 * VL].cpu().numpy()
@@ -540,31 +541,35 @@ def cpu_baseline(h, budget_s):
     threads = min(N_CH, len(os.sched_getaffinity(0)))  # one thread per channel of the workload
     k = T.conf("GPS", FS, VL, rotator_avx=1 if rot == 1 else 0)
     sats = h["sats"]
-    work = [(c % N_CH) for c in range(threads)]
-    done_epochs = [0] * threads
-    stop = [False]
 
-    def worker(t):
-        s = sats[work[t]]
-        delay = signals.acq_delay_samples(s, FS, 0, first)
-        while not stop[0]:
-            ch = T.Channel(k, s.code, delay, s.doppler_hz, 0, first, fast=True)
-            rec = ch.run(x, base_abs, 500)
-            done_epochs[t] += len(rec)
-            if len(rec) == 0:
-                break
+    def timed(simd_on, seconds):
+        simd = O.set_simd(simd_on, fast=True)
+        done_epochs = [0] * threads
+        stop = [False]
 
-    ths = [threading.Thread(target=worker, args=(t,)) for t in range(threads)]
-    t0 = time.perf_counter()
-    for th in ths:
-        th.start()
-    time.sleep(budget_s)
-    stop[0] = True
-    for th in ths:
-        th.join()
-    dt = time.perf_counter() - t0
-    O.set_simd(False, fast=True)
-    ep = sum(done_epochs)
+        def worker(t):
+            s = sats[t % N_CH]
+            delay = signals.acq_delay_samples(s, FS, 0, first)
+            while not stop[0]:
+                ch = T.Channel(k, s.code, delay, s.doppler_hz, 0, first, fast=True)
+                rec = ch.run(x, base_abs, 500)
+                done_epochs[t] += len(rec)
+                if len(rec) == 0:
+                    break
+
+        ths = [threading.Thread(target=worker, args=(t,)) for t in range(threads)]
+        t0 = time.perf_counter()
+        for th in ths:
+            th.start()
+        time.sleep(seconds)
+        stop[0] = True
+        for th in ths:
+            th.join()
+        dt = time.perf_counter() - t0
+        O.set_simd(False, fast=True)
+        return simd, sum(done_epochs), dt
+
+    simd, ep, dt = timed(rot == 1, budget_s * (0.6 if rot == 1 else 1.0))
     model = "unknown"
     try:
         with open("/proc/cpuinfo") as f:
@@ -575,17 +580,24 @@ def cpu_baseline(h, budget_s):
     except OSError:
         pass
     chan_sps = ep * VL / dt
-    return {"value": round(chan_sps / N_CH / 1e6, 2), "unit": "Msamples/s",
-            "cores": threads, "kind": "port",
-            "sample": f"{ep} channel-epochs of the closed loop (oracle/trk_oracle.c, rotator {rot}, -O3 -march=native, correlator "
-                      f"{'AVX restatement oracle/avx_port.c' if simd else 'scalar restatement'}) on 0.6 s of the same file, {threads} threads "
-                      f"(one channel each) for {dt:.1f} s; value = channel-samples/s ÷ {N_CH} channels, i.e. the IF rate at which this "
-                      f"host would keep {N_CH} channels",
-            "channel_msamples_per_s": round(chan_sps / 1e6, 2),
-            "channel_msamples_per_s_per_core": round(chan_sps / threads / 1e6, 1),
-            "cpu_model": model, "machine": platform.machine(),
-            "reference_avx_note": "SURVEY §6 measured the reference's own AVX correlator at 268 M channel-samples/s per core in "
-                                  "the survey container; the AVX restatement runs the same 16-lane u_avx arithmetic"}
+    out = {"value": round(chan_sps / N_CH / 1e6, 2), "unit": "Msamples/s",
+           "cores": threads, "kind": "port",
+           "sample": f"{ep} channel-epochs of the closed loop (oracle/trk_oracle.c, rotator {rot}, -O3 -march=native, correlator "
+                     f"{'AVX restatement oracle/avx_port.c' if simd else 'scalar restatement'}) on 0.6 s of the same file, {threads} threads "
+                     f"(one channel each) for {dt:.1f} s; value = channel-samples/s ÷ {N_CH} channels, i.e. the IF rate at which this "
+                     f"host would keep {N_CH} channels",
+           "channel_msamples_per_s": round(chan_sps / 1e6, 2),
+           "channel_msamples_per_s_per_core": round(chan_sps / threads / 1e6, 1),
+           "cpu_model": model, "machine": platform.machine(),
+           "reference_avx_note": "SURVEY §6 measured the reference's own AVX correlator at 268 M channel-samples/s per core in "
+                                 "the survey container; the AVX restatement runs the same 16-lane u_avx arithmetic"}
+    if simd:
+        _, ep2, dt2 = timed(False, budget_s * 0.4)
+        cs2 = ep2 * VL / dt2
+        out["scalar_port"] = {"value": round(cs2 / N_CH / 1e6, 2), "unit": "Msamples/s", "cores": threads,
+                              "channel_msamples_per_s_per_core": round(cs2 / threads / 1e6, 1),
+                              "sample": f"{ep2} channel-epochs, same loop with the scalar correlator restatement, {dt2:.1f} s"}
+    return out
 
 
 def cpu_acq_c3(budget_s=8.0):

@@ -90,7 +90,7 @@ struct gnsship_acq {
     float2* twM = nullptr;       // huge: M twiddles exp(-2πi t/M) of the row transform
     float2* T = nullptr;         // huge: forward column-stage scratch, n_bins × N
     float2* U = nullptr;         // huge: inverse row-stage scratch, prn_batch × n_bins × N
-    float* grid_scratch = nullptr; // huge without a kept grid: prn_batch × n_bins × N
+    float* grid_scratch = nullptr; // unused: the huge search keeps no |y|² rows without a kept grid
     TileStat* tiles = nullptr;   // huge: prn_batch × n_bins × huge_tiles(M)
     int prn_batch = 0;
     int n_bins = 0;
@@ -172,7 +172,6 @@ static int acq_upload_wipeoffs(gnsship_acq* a, int nb, const std::vector<float>&
             const size_t tiles = static_cast<size_t>(a->prn_batch) * nb * huge_tiles(a->plan.n);
             HIP_TRY(ctx, hipMalloc(&a->T, sizeof(float2) * static_cast<size_t>(nb) * N));
             HIP_TRY(ctx, hipMalloc(&a->U, cell * a->prn_batch));
-            HIP_TRY(ctx, hipMalloc(&a->grid_scratch, sizeof(float) * static_cast<size_t>(nb) * N * a->prn_batch));
             HIP_TRY(ctx, hipMalloc(&a->tiles, sizeof(TileStat) * tiles));
         }
     }
@@ -367,7 +366,8 @@ extern "C" int gnsship_acq_run(gnsship_acq* a, const void* sig, int fmt, int sig
         HIP_TRY(ctx, launch_acq_fft_huge(src, fmt, a->wipe, a->n_bins, a->P, a->plan, a->tw, a->twM, a->T, a->X, 0, a->consumed, ctx->stream));
         for (int p0 = 0; p0 < n_prns; p0 += a->prn_batch) {
             const int np = std::min(a->prn_batch, n_prns - p0);
-            float* g = keep_grid ? a->grid_dev + static_cast<size_t>(p0) * a->n_bins * rs.row_len : a->grid_scratch;
+            // without a kept grid the |y|² rows never reach HBM (tile statistics + finalize's recomputation)
+            float* g = keep_grid ? a->grid_dev + static_cast<size_t>(p0) * a->n_bins * rs.row_len : nullptr;
             HIP_TRY(ctx, launch_acq_search_huge(a->X, a->codes_fft, p0, np, a->n_bins, a->P, a->plan, a->tw, a->twM, a->U, g,
                              keep_grid ? accumulate : 0, a->tiles, rs, a->rowstat, ctx->stream));
         }

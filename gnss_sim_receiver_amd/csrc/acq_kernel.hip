@@ -242,6 +242,76 @@ __device__ __forceinline__ void fft_lds_ct(float2* __restrict__ buf, const float
     }
 }
 
+// fft_lds_ct with the twiddles from a QUARTER table in LDS (tq[u] = exp(−2πi u/M), u < M/4): the
+// M-entry table no longer fits beside an M-point row (12500 × 8 B each), and read from global
+// memory its loads sat in every pass's vmcnt queue.  tw[t] for t = q·M/4 + u
+// is tq[u]·(−j)^q — exact, the same float values as the full table (whose entries are rounded from
+// the same double cos/sin up to the quarter-turn symmetry).
+template <int MC, int NsC, int SIGN>
+__device__ __forceinline__ void fft_lds_ct_q(float2* __restrict__ buf, const float2* __restrict__ tq, int tid)
+{
+    static_assert(MC % 4 == 0, "quarter twiddle table");
+    if constexpr (NsC < MC) {
+        constexpr int R = ct_radix(MC / NsC);
+        constexpr int nb = MC / R;
+        constexpr int tstep = MC / (NsC * R);
+        constexpr int Q = MC / 4;
+        constexpr int MAXB = (nb + kAcqThreads - 1) / kAcqThreads;
+        float2 v[MAXB][R];
+#pragma unroll
+        for (int c = 0; c < MAXB; c++) {
+            const int j = tid + c * kAcqThreads;
+            if (j < nb) {
+                const int k = j % NsC;
+                if constexpr (NsC > 1 && (NsC - 1) * tstep < Q) {
+                    // W^{k·r·tstep} = (W^{k·tstep})^r: one table read (k·tstep < M/4, no quarter turn),
+                    // the other powers as a balanced product tree (≤ 4 products deep)
+                    float2 w[R];
+                    w[1] = tq[k * tstep];
+                    if (SIGN > 0) w[1].y = -w[1].y;
+#pragma unroll
+                    for (int r = 2; r < R; r++) w[r] = cmulf(w[r / 2], w[r - r / 2]);
+                    v[c][0] = buf[j];
+#pragma unroll
+                    for (int r = 1; r < R; r++) v[c][r] = cmulf(buf[j + r * nb], w[r]);
+                } else {
+#pragma unroll
+                for (int r = 0; r < R; r++) {
+                    float2 x = buf[j + r * nb];
+                    if (r > 0 && NsC > 1) {
+                        const int t = k * r * tstep;  // < MC
+                        const int q = t / Q, u = t - q * Q;
+                        const float2 w0 = tq[u];
+                        float wx = (q & 1) ? w0.y : w0.x, wy = (q & 1) ? -w0.x : w0.y;
+                        if (q & 2) {
+                            wx = -wx;
+                            wy = -wy;
+                        }
+                        if (SIGN > 0) wy = -wy;
+                        x = cmulf(x, make_float2(wx, wy));
+                    }
+                    v[c][r] = x;
+                }
+                }
+                dft_small<R, SIGN>(v[c]);
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int c = 0; c < MAXB; c++) {
+            const int j = tid + c * kAcqThreads;
+            if (j < nb) {
+                const int k = j % NsC;
+                const int base = (j / NsC) * NsC * R + k;
+#pragma unroll
+                for (int r = 0; r < R; r++) buf[base + r * NsC] = v[c][r];
+            }
+        }
+        __syncthreads();
+        fft_lds_ct_q<MC, NsC * R, SIGN>(buf, tq, tid);
+    }
+}
+
 // Transforms of up to kTwLdsMax points read their twiddles from LDS: the N-entry table is staged
 // next to the data once per workgroup (every Stockham pass otherwise waits on L2 for its R − 1
 // twiddle loads, with only one or two butterflies per thread to hide them).
@@ -1158,6 +1228,7 @@ __global__ __launch_bounds__(64) void acq_decide_kernel(const RowStat* __restric
 //             ±samples_per_chip (pcps_acquisition.cc:496-597).
 // ---------------------------------------------------------------------------------------------
 constexpr int kHugeColThreads = 256;
+#define GNSSHIP_HUGE_P_LIST(X) X(4) X(5) X(8) X(10) X(16) X(20) X(25) X(32)
 
 template <int FMT, int P>
 __global__ __launch_bounds__(kHugeColThreads) void acq_huge_cols_fwd_kernel(const void* __restrict__ sig, const float2* __restrict__ mult,
@@ -1202,9 +1273,12 @@ __global__ __launch_bounds__(kAcqThreads) void acq_huge_rows_kernel(const float2
     const int64_t row = static_cast<int64_t>(blockIdx.x) * M;
     const float2* a = A + blockIdx.y * a_sy + blockIdx.z * a_sz + row;
     const float2* bb = B ? B + blockIdx.y * b_sy + blockIdx.z * b_sz + row : nullptr;
+    if constexpr (MC > 0) {  // the quarter twiddle table beside the row (M + M/4 entries of LDS)
+        for (int i = threadIdx.x; i < MC / 4; i += kAcqThreads) lds[MC + i] = twM[i];
+    }
     lds_load_prod(lds, a, bb, M, threadIdx.x, kAcqThreads);  // ×conj(code FFT)
     __syncthreads();
-    if constexpr (MC > 0) fft_lds_ct<MC, 1, SIGN>(lds, twM);
+    if constexpr (MC > 0) fft_lds_ct_q<MC, 1, SIGN>(lds, lds + MC, threadIdx.x);
     else fft_lds<SIGN>(lds, plan, twM);
     float2* d = D + blockIdx.y * d_sy + blockIdx.z * d_sz + row;
     for (int i = threadIdx.x; i < M; i += kAcqThreads) {
@@ -1214,8 +1288,83 @@ __global__ __launch_bounds__(kAcqThreads) void acq_huge_rows_kernel(const float2
     }
 }
 
-// Inverse column stage + |y|² for cell (prn blockIdx.z, bin blockIdx.y): grid row
-// g = grid + (z·n_bins + y)·N (accumulated over dwells when `accumulate`), tile statistics.
+// Column m of the inverse column stage for one cell: v[q] = y[m + M·q] (the same instructions in
+// the column kernel and in the finalize kernel's recomputation, so the |y|² agree bit for bit).
+template <int P>
+__device__ __forceinline__ void huge_col_inv(const float2* __restrict__ u, int m, int M, const float2* __restrict__ twN, float2 (&v)[P])
+{
+    const int N = P * M;
+#pragma unroll
+    for (int kq = 0; kq < P; kq++) {
+        float2 x = u[kq * M];
+        if (kq) {
+            float2 w = twN[m * kq];  // W_N^{−m·kq}
+            w.y = -w.y;
+            x = cmulf(x, w);
+        }
+        v[kq] = x;
+    }
+    dft_reg<P, 1, +1>(v, twN, N);
+}
+
+// The compile-time-length rows of the search (inverse) stage as a persistent pipeline: block b
+// transforms rows b, b + grid, …; the next row's XT and code-spectrum loads (13 + 13 per thread) are
+// issued before the current row's transform and land during it, so with one workgroup per CU (the
+// 12500-point row and its quarter twiddle table fill 125 KB of LDS) the row reads no longer stall
+// each transform.  Row index r = x + P·(y + ny·z) as acq_huge_rows_kernel's (x, y, z) blocks.
+template <int SIGN, int MC>
+__global__ __launch_bounds__(kAcqThreads) void acq_huge_rows_pipe_kernel(const float2* __restrict__ A, int64_t a_sy, int64_t a_sz,
+    const float2* __restrict__ B, int64_t b_sy, int64_t b_sz, float2* __restrict__ D, int64_t d_sy, int64_t d_sz, const float2* __restrict__ twM,
+    int P, int ny, int nz)
+{
+    extern __shared__ __attribute__((aligned(16))) float2 lds[];
+    constexpr int PER = (MC + kAcqThreads - 1) / kAcqThreads;
+    const int total = P * ny * nz;
+    const int tid = threadIdx.x;
+    for (int i = tid; i < MC / 4; i += kAcqThreads) lds[MC + i] = twM[i];
+    constexpr int PF = PER;  // prefetched: all of each thread's PER XT samples
+    float2 av[PF];  // the next row's XT samples (the code spectrum rows, 8 per PRN, stay cache-resident)
+    auto issue = [&](int r) {
+        const int x = r % P, yz = r / P, y = yz % ny, z = yz / ny;
+        const float2* a = A + y * a_sy + z * a_sz + static_cast<int64_t>(x) * MC;
+#pragma unroll
+        for (int u = 0; u < PF; u++) av[u] = a[min(tid + u * kAcqThreads, MC - 1)];
+    };
+    int r = blockIdx.x;
+    if (r < total) issue(r);
+    for (; r < total; r += gridDim.x) {
+        {
+            const int x = r % P, yz = r / P, y = yz % ny, z = yz / ny;
+            const float2* a = A + y * a_sy + z * a_sz + static_cast<int64_t>(x) * MC;
+            const float2* b = B + y * b_sy + z * b_sz + static_cast<int64_t>(x) * MC;
+            float2 bv[PER], ar[PER - PF + 1];
+#pragma unroll
+            for (int u = PF; u < PER; u++) ar[u - PF] = a[min(tid + u * kAcqThreads, MC - 1)];
+#pragma unroll
+            for (int u = 0; u < PER; u++) bv[u] = b[min(tid + u * kAcqThreads, MC - 1)];
+#pragma unroll
+            for (int u = 0; u < PER; u++) {
+                const int i = tid + u * kAcqThreads;
+                if (i < MC) lds[i] = cmulf(u < PF ? av[u] : ar[u - PF], bv[u]);  // XT ⊙ conj(code FFT)
+            }
+        }
+        __syncthreads();
+        if (r + static_cast<int>(gridDim.x) < total) issue(r + gridDim.x);  // in flight during this transform
+        // the transform's index arithmetic is loop-invariant; recomputed per row (an opaque thread id)
+        // rather than hoisted into registers that would spill
+        int tid_r = tid;
+        asm volatile("" : "+v"(tid_r));
+        fft_lds_ct_q<MC, 1, SIGN>(lds, lds + MC, tid_r);
+        const int x = r % P, yz = r / P, y = yz % ny, z = yz / ny;
+        float2* d = D + y * d_sy + z * d_sz + static_cast<int64_t>(x) * MC;
+        for (int i = tid; i < MC; i += kAcqThreads) d[i] = lds[i];
+        __syncthreads();  // the row is read out before the next one is written
+    }
+}
+
+// Inverse column stage + |y|² for cell (prn blockIdx.z, bin blockIdx.y): tile statistics, and the
+// grid row g = grid + (z·n_bins + y)·N (accumulated over dwells when `accumulate`) only when a grid
+// is kept — without one the |y|² never reach HBM (finalize recomputes the few columns it rescans).
 template <int P>
 __global__ __launch_bounds__(kHugeColThreads) void acq_huge_cols_inv_kernel(const float2* __restrict__ U, int M, int n_bins,
     const float2* __restrict__ twN, float* __restrict__ grid, int accumulate, TileStat* __restrict__ tiles, RowSpec rs)
@@ -1228,27 +1377,18 @@ __global__ __launch_bounds__(kHugeColThreads) void acq_huge_cols_inv_kernel(cons
     MaxIdx best{-1.0f, 0x7fffffff};
     float s = 0.0f;
     if (m < M) {
-        const float2* u = U + cell * N + m;
         float2 v[P];
-#pragma unroll
-        for (int kq = 0; kq < P; kq++) {
-            float2 x = u[kq * M];
-            if (kq) {
-                float2 w = twN[m * kq];  // W_N^{−m·kq}
-                w.y = -w.y;
-                x = cmulf(x, w);
-            }
-            v[kq] = x;
-        }
-        dft_reg<P, 1, +1>(v, twN, N);
-        float* g = grid + cell * rs.row_len;
+        huge_col_inv<P>(U + cell * N + m, m, M, twN, v);
+        float* g = grid ? grid + cell * rs.row_len : nullptr;
 #pragma unroll
         for (int q = 0; q < P; q++) {
             const int n = m + M * q - rs.row_off;  // index in the row
             if (n < 0 || n >= rs.row_len) continue;
             float mag = __fadd_rn(__fmul_rn(v[q].x, v[q].x), __fmul_rn(v[q].y, v[q].y));  // volk_32fc_magnitude_squared_32f
-            if (accumulate) mag = __fadd_rn(g[n], mag);                                      // volk_32f_x2_add_32f
-            g[n] = mag;
+            if (g) {
+                if (accumulate) mag = __fadd_rn(g[n], mag);  // volk_32f_x2_add_32f
+                g[n] = mag;
+            }
             best = better(best, MaxIdx{mag, n});
             s += mag;
         }
@@ -1268,8 +1408,34 @@ constexpr int kHugeFlagMax = 64;  // tiles met by the window that are rescanned 
 
 __device__ __forceinline__ bool interval_meets(int a0, int a1, int b0, int b1) { return a0 < b1 && b0 < a1; }
 
+// |y|² of row index n's column tile recomputed from U (grid-free mode): thread t of the block takes
+// column lo + t % 256 and register point q = t / 256 … the whole tile's P·256 values, each thread
+// folding the ones outside the window into v2.
+template <int P>
+__device__ __forceinline__ float huge_tile_max_outside(const float2* __restrict__ Ucell, int lo, int M, const float2* __restrict__ twN, RowSpec rs,
+    int e1, int e2)
+{
+    float v2 = 0.0f;
+    for (int c = threadIdx.x; c < kHugeColThreads; c += kAcqThreads) {
+        const int mm = lo + c;
+        if (mm >= M) continue;
+        float2 v[P];
+        huge_col_inv<P>(Ucell + mm, mm, M, twN, v);
+#pragma unroll
+        for (int q = 0; q < P; q++) {
+            const int n = mm + M * q - rs.row_off;
+            if (n < 0 || n >= rs.row_len) continue;
+            const bool in_win = (e1 < e2) ? (n >= e1 && n < e2) : (n >= e1 || n < e2);
+            const float mag = __fadd_rn(__fmul_rn(v[q].x, v[q].x), __fmul_rn(v[q].y, v[q].y));
+            if (!in_win) v2 = fmaxf(v2, mag);
+        }
+    }
+    return v2;
+}
+
 __global__ __launch_bounds__(kAcqThreads) void acq_huge_finalize_kernel(const float* __restrict__ grid, const TileStat* __restrict__ tiles,
-    int n_tiles, int n_bins, int prn_offset, RowSpec rs, int M, int P, RowStat* __restrict__ rowstat)
+    int n_tiles, int n_bins, int prn_offset, RowSpec rs, int M, int P, RowStat* __restrict__ rowstat, const float2* __restrict__ U,
+    const float2* __restrict__ twN)
 {
     __shared__ MaxIdx red_m[kAcqThreads / 64];
     __shared__ float red_s[kAcqThreads / 64];
@@ -1308,9 +1474,25 @@ __global__ __launch_bounds__(kAcqThreads) void acq_huge_finalize_kernel(const fl
         }
     }
     __syncthreads();
-    const float* g = grid + cell * rs.row_len;
     auto in_win = [&](int i) { return (e1 < e2) ? (i >= e1 && i < e2) : (i >= e1 || i < e2); };
     const int nf = n_flag;
+    if (!grid) {  // grid-free: the met tiles (or, past kHugeFlagMax of them, every tile) recomputed from U
+        const float2* Ucell = U + cell * static_cast<int64_t>(P) * M;
+        const int cnt = nf <= kHugeFlagMax ? nf : n_tiles;
+        for (int f = 0; f < cnt; f++) {
+            const int lo = (nf <= kHugeFlagMax ? flag_list[f] : f) * kHugeColThreads;
+            float t = 0.0f;
+#define GNSSHIP_P_CASE(p) \
+    case p: t = huge_tile_max_outside<p>(Ucell, lo, M, twN, rs, e1, e2); break;
+            switch (P) { GNSSHIP_HUGE_P_LIST(GNSSHIP_P_CASE) default: break; }
+#undef GNSSHIP_P_CASE
+            v2 = fmaxf(v2, t);
+        }
+        const float second = block_max<kAcqThreads / 64>(v2, red_s);
+        if (threadIdx.x == 0) rowstat[(static_cast<int64_t>(prn_offset) + blockIdx.y) * n_bins + blockIdx.x] = RowStat{best.v, best.i, sum, second};
+        return;
+    }
+    const float* g = grid + cell * rs.row_len;
     if (nf <= kHugeFlagMax) {
         for (int f = 0; f < nf; f++) {
             const int lo = flag_list[f] * kHugeColThreads;
@@ -1328,7 +1510,6 @@ __global__ __launch_bounds__(kAcqThreads) void acq_huge_finalize_kernel(const fl
     if (threadIdx.x == 0) rowstat[(static_cast<int64_t>(prn_offset) + blockIdx.y) * n_bins + blockIdx.x] = RowStat{best.v, best.i, sum, second};
 }
 
-#define GNSSHIP_HUGE_P_LIST(X) X(4) X(5) X(8) X(10) X(16) X(20) X(25) X(32)
 
 bool huge_p_supported(int P)
 {
@@ -1366,8 +1547,9 @@ hipError_t launch_acq_fft_huge(const void* sig, int fmt, const float2* mult, int
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     const size_t lds = sizeof(float2) * static_cast<size_t>(M);
+    const size_t lds_q = sizeof(float2) * static_cast<size_t>(M + M / 4);  // + the quarter twiddle table
     if (M == 12500)  // Galileo E1 at 25 Msps (N = 100000 = 8 × 12500), GPS/B1I at 50 Msps: compile-time plan
-        hipLaunchKernelGGL((acq_huge_rows_kernel<-1, 12500>), dim3(P, n_rows, 1), dim3(kAcqThreads), lds, stream, scratch, N, int64_t(0),
+        hipLaunchKernelGGL((acq_huge_rows_kernel<-1, 12500>), dim3(P, n_rows, 1), dim3(kAcqThreads), lds_q, stream, scratch, N, int64_t(0),
             static_cast<const float2*>(nullptr), int64_t(0), int64_t(0), rowsT, N, int64_t(0), row_plan, twM, conj_out);
     else
         hipLaunchKernelGGL((acq_huge_rows_kernel<-1>), dim3(P, n_rows, 1), dim3(kAcqThreads), lds, stream, scratch, N, int64_t(0),
@@ -1382,10 +1564,18 @@ hipError_t launch_acq_search_huge(const float2* XT, const float2* codesT, int pr
     const int M = row_plan.n;
     const int64_t N = static_cast<int64_t>(P) * M;
     const size_t lds = sizeof(float2) * static_cast<size_t>(M);
+    const size_t lds_q = sizeof(float2) * static_cast<size_t>(M + M / 4);
     // rows: blockIdx.y = bin (XT row set), blockIdx.z = prn (code spectrum), U cell = z·n_bins + y
-    if (M == 12500)
-        hipLaunchKernelGGL((acq_huge_rows_kernel<+1, 12500>), dim3(P, n_bins, n_prns), dim3(kAcqThreads), lds, stream, XT, N, int64_t(0),
-            codesT + static_cast<int64_t>(prn_offset) * N, int64_t(0), N, U, N, N * n_bins, row_plan, twM, 0);
+    if (M == 12500) {
+        // persistent: one workgroup per CU (125 KB of LDS each), rows pipelined through it
+        int n_cu = 256;
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) n_cu = 256;
+        const int total = P * n_bins * n_prns;
+        const int blocks = total < n_cu ? total : n_cu;
+        hipLaunchKernelGGL((acq_huge_rows_pipe_kernel<+1, 12500>), dim3(blocks), dim3(kAcqThreads), lds_q, stream, XT, N, int64_t(0),
+            codesT + static_cast<int64_t>(prn_offset) * N, int64_t(0), N, U, N, N * n_bins, twM, P, n_bins, n_prns);
+    }
     else
         hipLaunchKernelGGL((acq_huge_rows_kernel<+1>), dim3(P, n_bins, n_prns), dim3(kAcqThreads), lds, stream, XT, N, int64_t(0),
             codesT + static_cast<int64_t>(prn_offset) * N, int64_t(0), N, U, N, N * n_bins, row_plan, twM, 0);
@@ -1406,7 +1596,7 @@ hipError_t launch_acq_search_huge(const float2* XT, const float2* codesT, int pr
     e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(acq_huge_finalize_kernel, dim3(n_bins, n_prns), dim3(kAcqThreads), 0, stream, grid, tiles, n_tiles, n_bins, prn_offset, rs,
-        M, P, rowstat);
+        M, P, rowstat, U, twN);
     return hipGetLastError();
 }
 

@@ -10,19 +10,22 @@
 // advances is 1 / (epoch latency), so this kernel shortens the chain itself:
 //
 //  * wave 0 is the control wave.  The channel's loop state lives in its registers for the whole
-//    run (RChan, trk_loop.h) — no LDS round trip per member; it derives the epoch's correlator
-//    arguments (cos/sin of the NCO phase and step in parallel lanes), then replays the 16 AVX phasor
-//    lanes (z ← z·dz, the reference's float products) and stores each lane's phasor at every task
-//    start (G iterations, 4 for GPS at 4 Msps) with a plain LDS store — no fence, no flag: the
-//    phasor slot itself is the signal (all-ones NaN = not yet written; a phasor is never NaN);
-//  * waves 1-3 correlate: groups of four tasks, lane (task, l) polls its slot, re-arms it for the
-//    next epoch, and continues lane l's chain over the task's iterations with the same float
+//    run (RChan, trk_loop.h) — no LDS round trip per member.  After the correlation it sums the
+//    taps, runs the loop update, and as soon as epoch_post has settled the next epoch's NCO it
+//    publishes that epoch's correlator arguments (the seed) before writing this epoch's records;
+//  * wave 1 is the phasor wave: from the seed it derives cos/sin of the NCO phase and step (double,
+//    once rounded, in two lanes), dz = normalise(inc^16) and the 16 AVX lane starts, then replays
+//    the 16 phasor chains (z ← z·dz, the reference's float products, two lanes per chain with a DPP
+//    partner product) and stores each chain's phasor at every task start (G iterations, 4 for GPS
+//    at 4 Msps) with a plain LDS store — no fence, no flag: the phasor slot itself is the signal
+//    (all-ones NaN = not yet written; a phasor is never NaN);
+//  * waves 0, 2 and 3 correlate: groups of four tasks, lane (task, l) polls its slot, re-arms it for
+//    the next epoch, and continues chain l over the task's iterations with the same float
 //    products — every phasor bit-identical to u_avx's — correlating sample 16m + l at iteration
-//    m; groups are dealt statically (wave w takes groups w − 1 mod 3), so sums are reproducible;
-//  * after the barrier, wave 0 sums the per-wave tap sums in wave order and runs the loop update
-//    on its registers while wave 1 runs the lock detectors (lock_status) on the LDS copy of their
-//    members; wave 0 runs run_dll_pll + update_tracking_vars speculatively and keeps them only when
-//    the lock test (published by wave 1) passes, as the reference runs them only then.
+//    m; groups are dealt statically (group sets 1, 2, 3), so sums are reproducible; wave 2 also
+//    runs the lock detectors (lock_status) on the LDS copy of their members while wave 0 runs
+//    run_dll_pll + update_tracking_vars speculatively, kept only when the lock test passes, as the
+//    reference runs them only then.
 //
 // Epochs too long for the LDS task slots, the generic rotator, high_dyn and runs of more channels
 // than CUs stay on trk_persist.hip / the round-based loop.
@@ -102,6 +105,8 @@ struct FShared {
     float taps[2 * kMaxTaps + 2];  // the epoch's tap sums (+ the data prompt at 2·kMaxTaps), as epoch_pre reads them
     gnsship_trk_dump_record drec;  // log_data's record of the epoch
     double coh;       // the coherent time lock_status is called with (0: no lock test this epoch)
+    int32_t seed_seq; // e + 1 once wave 0 published epoch e's NCO arguments (sh.job without dz)
+    int32_t job_seq;  // e + 1 once wave 1 completed epoch e's job (dz) — the correlating waves start
     int32_t pre_seq;  // e + 1 once wave 0 published this epoch's prompt / pull-in / coh
     int32_t lock_seq; // e + 1 once wave 1 published the lock outcome
     int32_t locked;
@@ -423,6 +428,8 @@ __global__ __launch_bounds__(kFThreads, fast_waves_per_simd<THRU>()) void trk_fa
                               (!DATA || (sc.data_code_id >= 0 && sc.data_code_id < n_codes && codes[sc.data_code_id].ptr &&
                                             codes[sc.data_code_id].len == codes[sc.code_id].len));
         skip = (tracking && codes_ok) ? 0 : 1;
+        sh.seed_seq = 0;
+        sh.job_seq = 0;
         sh.pre_seq = 0;
         sh.lock_seq = 0;
     }
@@ -431,6 +438,7 @@ __global__ __launch_bounds__(kFThreads, fast_waves_per_simd<THRU>()) void trk_fa
     GNSSHIP_FHWID(20 + wave);  // epoch 0's slots 20-23 (the epoch loop stamps 0-15)
     stage_code_f(code0, codes[sc.code_id]);
     if constexpr (DATA) stage_code_f(code1, codes[sc.data_code_id]);
+    __syncthreads();  // the code replicas are staged before any wave correlates
     const int L = codes[sc.code_id].len;
     const float* c0 = code0 + kCodeMargin;
     const float* c1 = code1 + kCodeMargin;
@@ -441,86 +449,106 @@ __global__ __launch_bounds__(kFThreads, fast_waves_per_simd<THRU>()) void trk_fa
     constexpr int kOut = NT + (DATA ? 1 : 0);
     RChan rc;
     if (wave == 0) rchan_load(sc, &sc, rc);
+    // Wave roles (one channel per workgroup, its epochs a serial chain):
+    //   wave 0 — the control wave: the loop update on its register-resident channel (RChan), the
+    //            epoch records, and one third of the correlation;
+    //   wave 1 — the phasor wave: derives the epoch's phasors (cos/sin of the NCO phase and step,
+    //            dz, the 16 lane starts) and replays them into the task slots, plus the N mod 16 tail;
+    //   waves 2, 3 — the other two thirds of the correlation; wave 2 also runs the lock detectors.
+    // Wave 0 hands the next epoch's NCO arguments (the seed) to wave 1 as soon as epoch_post has
+    // settled them, so the derive and the first tasks of epoch e + 1 overlap epoch e's record writes.
+    const int cw = wave == 0 ? 1 : wave;  // correlating waves 0, 2, 3 take group sets 1, 2, 3
+    uint64_t seed_start = 0;              // wave 0: the epoch start the seed was made for
+    // wave 0: do_correlation_step's arguments for the epoch at nitems_read (all but the phasors)
+    auto make_seed = [&](int e) {
+        const uint64_t vl = k.conf.vector_length;
+        const bool runnable = e < max_rounds && (rc.state == 2 || rc.state == 3 || rc.state == 4) && rc.nitems_read >= buf_first &&
+                              rc.nitems_read + vl <= buf_first + static_cast<uint64_t>(buf_len);
+        const float rem_carr = corr_rem_carr(k, rc), stepf = corr_phase_step(k, rc);
+        if (runnable) rc.epoch_start = rc.nitems_read;
+        seed_start = rc.epoch_start;
+        if (lane == 0) {
+            FJob& j = sh.job;
+            j.runnable = runnable ? 1 : 0;
+            if (runnable) {
+                const float spcf = static_cast<float>(k.code_samples_per_chip);
+                const float* shv = uni(rc.narrow) ? k.shifts_n : k.shifts;
+                j.off = static_cast<int64_t>(rc.nitems_read - buf_first);
+                j.rem_code = __fmul_rn(static_cast<float>(rc.rem_code_phase_chips), spcf);
+                j.code_step = __fmul_rn(static_cast<float>(rc.code_phase_step_chips), spcf);
+                float smin = 0.0f, smax = 0.0f;
+                for (int t = 0; t < 5; t++) {
+                    j.shifts[t] = t < NT ? shv[t] : 0.0f;
+                    smin = fminf(smin, j.shifts[t]);
+                    smax = fmaxf(smax, j.shifts[t]);
+                }
+                const double span = static_cast<double>(j.code_step) * static_cast<double>(N > 0 ? N - 1 : 0);
+                const double lo = fmin(0.0, span) + smin - j.rem_code - 2.0;
+                const double hi = fmax(0.0, span) + smax - j.rem_code + 2.0;
+                j.in_margin = (isfinite(lo) && isfinite(hi) && lo >= -kCodeMargin && hi < static_cast<double>(L + kCodeMargin)) ? 1 : 0;
+                j.rem_carr = rem_carr;
+                j.step = stepf;
+                j.M = M;
+                j.S = S;
+                j.tail = tail;
+            }
+            publish_seq(&sh.seed_seq, e + 1);
+        }
+    };
+    if (wave == 0) make_seed(0);
     int e_done = 0;
-    for (int e = 0; e < max_rounds; e++) {
-        // ---- derive (wave 0): do_correlation_step's arguments for the epoch at nitems_read ----
-        f2 zinit = f2{0.0f, 0.0f}, dz = f2{1.0f, 0.0f}, inc = f2{1.0f, 0.0f};
-        if (wave == 0) {
+    for (int e = 0;; e++) {
+        f2 acc[NT + 1];
+#pragma unroll
+        for (int t = 0; t <= NT; t++) acc[t] = f2{0.0f, 0.0f};
+        FJob job;
+        if (wave == 1) {
+            // ---- derive: the phasors of the seeded epoch ----
+            wait_seq(&sh.seed_seq, e + 1);
             GNSSHIP_FSTAMP(e, 0);
 #ifdef GNSSHIP_CORR_PROFILE
             if (lane == 0) g_fprof_epoch = e;
 #endif
-            const uint64_t vl = k.conf.vector_length;
-            const bool runnable = (rc.state == 2 || rc.state == 3 || rc.state == 4) && rc.nitems_read >= buf_first &&
-                                  rc.nitems_read + vl <= buf_first + static_cast<uint64_t>(buf_len);
-            // (cos rem, −sin rem) and (cos −step, sin −step) (cpu_multicorrelator_real_codes.cc:115,123):
-            // lane 0 the phase, lane 1 the step, each the once-rounded double cos/sin (nco_math.h)
-            const float rem_carr = corr_rem_carr(k, rc), stepf = corr_phase_step(k, rc);
-            const float a = lane == 0 ? rem_carr : -stepf;
-            double sd, cd;
-            sincos(static_cast<double>(a), &sd, &cd);
-            const int sfi = __builtin_bit_cast(int, static_cast<float>(sd)), cfi = __builtin_bit_cast(int, static_cast<float>(cd));
-            const f2 p0 = f2{__builtin_bit_cast(float, __builtin_amdgcn_readlane(cfi, 0)), -__builtin_bit_cast(float, __builtin_amdgcn_readlane(sfi, 0))};
-            inc = f2{__builtin_bit_cast(float, __builtin_amdgcn_readlane(cfi, 1)), __builtin_bit_cast(float, __builtin_amdgcn_readlane(sfi, 1))};
-            // dz = normalise(inc^16) by four squarings (:215-225)
-            f2 d = inc;
+            const FJob sd = uniform_job(sh.job);
+            f2 zinit = f2{0.0f, 0.0f}, inc = f2{1.0f, 0.0f};
+            if (sd.runnable) {
+                // (cos rem, −sin rem) and (cos −step, sin −step) (cpu_multicorrelator_real_codes.cc:115,123):
+                // lane 0 the phase, lane 1 the step, each the once-rounded double cos/sin (nco_math.h)
+                const float a = lane == 0 ? sd.rem_carr : -sd.step;
+                double sdn, cdn;
+                sincos(static_cast<double>(a), &sdn, &cdn);
+                const int sfi = __builtin_bit_cast(int, static_cast<float>(sdn)), cfi = __builtin_bit_cast(int, static_cast<float>(cdn));
+                const f2 p0 = f2{__builtin_bit_cast(float, __builtin_amdgcn_readlane(cfi, 0)), -__builtin_bit_cast(float, __builtin_amdgcn_readlane(sfi, 0))};
+                inc = f2{__builtin_bit_cast(float, __builtin_amdgcn_readlane(cfi, 1)), __builtin_bit_cast(float, __builtin_amdgcn_readlane(sfi, 1))};
+                // dz = normalise(inc^16) by four squarings (:215-225)
+                f2 d = inc;
 #pragma unroll
-            for (int q = 0; q < 4; q++) d = cmul_exact(d, d);
-            dz = normalise_avx(d);
-            // z_l = phase·inc^l, the generic chain (:204-208), for the replay's lane pairs
-            f2 z = p0;
+                for (int q = 0; q < 4; q++) d = cmul_exact(d, d);
+                const f2 dz = normalise_avx(d);
+                // z_l = phase·inc^l, the generic chain (:204-208), for the replay's lane pairs
+                f2 z = p0;
 #pragma unroll
-            for (int i = 0; i < kAvxLanes - 1; i++) {
-                const f2 zi = cmul_exact(z, inc);
-                z = i < (lane >> 1) ? zi : z;  // lanes 2l, 2l + 1: chain l
-            }
-            zinit = z;
-            if (runnable) rc.epoch_start = rc.nitems_read;
-            if (lane == 0) {
-                FJob& j = sh.job;
-                j.runnable = runnable ? 1 : 0;
-                if (runnable) {
-                    const float spcf = static_cast<float>(k.code_samples_per_chip);
-                    const float* shv = uni(rc.narrow) ? k.shifts_n : k.shifts;
-                    j.off = static_cast<int64_t>(rc.nitems_read - buf_first);
-                    j.rem_code = __fmul_rn(static_cast<float>(rc.rem_code_phase_chips), spcf);
-                    j.code_step = __fmul_rn(static_cast<float>(rc.code_phase_step_chips), spcf);
-                    float smin = 0.0f, smax = 0.0f;
-                    for (int t = 0; t < 5; t++) {
-                        j.shifts[t] = t < NT ? shv[t] : 0.0f;
-                        smin = fminf(smin, j.shifts[t]);
-                        smax = fmaxf(smax, j.shifts[t]);
-                    }
-                    const double span = static_cast<double>(j.code_step) * static_cast<double>(N > 0 ? N - 1 : 0);
-                    const double lo = fmin(0.0, span) + smin - j.rem_code - 2.0;
-                    const double hi = fmax(0.0, span) + smax - j.rem_code + 2.0;
-                    j.in_margin = (isfinite(lo) && isfinite(hi) && lo >= -kCodeMargin && hi < static_cast<double>(L + kCodeMargin)) ? 1 : 0;
-                    j.dz_re = dz.x;
-                    j.dz_im = dz.y;
-                    j.rem_carr = rem_carr;
-                    j.step = stepf;
-                    j.M = M;
-                    j.S = S;
-                    j.tail = tail;
+                for (int i = 0; i < kAvxLanes - 1; i++) {
+                    const f2 zi = cmul_exact(z, inc);
+                    z = i < (lane >> 1) ? zi : z;  // lanes 2l, 2l + 1: chain l
+                }
+                zinit = z;
+                if (lane == 0) {
+                    sh.job.dz_re = dz.x;
+                    sh.job.dz_im = dz.y;
                 }
             }
+            if (lane == 0) publish_seq(&sh.job_seq, e + 1);
             GNSSHIP_FSTAMP(e, 1);
             GNSSHIP_FCLK(e, 12);
-        }
-        __syncthreads();  // B: the job is published (and, in the first epoch, the code replicas staged)
-        if (!sh.job.runnable) break;
-        const FJob job = uniform_job(sh.job);
-        const i4v span = sample_span<FMT>(samples, job.off, N);
-        f2 acc[NT + 1];
-#pragma unroll
-        for (int t = 0; t <= NT; t++) acc[t] = f2{0.0f, 0.0f};
-        if (wave == 0) {
-            GNSSHIP_FCLK(e, 28);
+            if (!sd.runnable) break;
+            job = uniform_job(sh.job);
+            const i4v span = sample_span<FMT>(samples, job.off, N);
             float xl = (lane & 1) ? zinit.y : zinit.x;
             if (lane < 2 * kAvxLanes) xl = fast_replay<G>(xl, job.dz_re, (lane & 1) ? job.dz_im : -job.dz_im, M, S, tail, Zs, lane);
-            if (tail > 0) {
+            if (tail > 0) {  // the serial tail from normalise(z_0) after the loop (:286-304)
                 const f2 zl = f2{__builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, xl), 0)),
-                    __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, xl), 1))};  // the serial tail from normalise(z_0) after the loop (:286-304), on this wave
+                    __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, xl), 1))};
                 if (lane == 0) {
                     f2 p = normalise_avx(zl);
                     for (int j = 0; j < tail; j++) {
@@ -535,24 +563,16 @@ __global__ __launch_bounds__(kFThreads, fast_waves_per_simd<THRU>()) void trk_fa
             }
             GNSSHIP_FSTAMP(e, 2);
             GNSSHIP_FCLK(e, 13);
-#ifdef GNSSHIP_FAST_SERIAL  // diagnostic only: the consumers start after the whole replay
-            __syncthreads();
-#endif
         } else {
-#ifdef GNSSHIP_FAST_SERIAL
-            __syncthreads();
-#endif
-#ifdef GNSSHIP_FAST_NOCONSUME  // diagnostic only: the correlating waves idle (wrong sums)
-            if (false) {
-#endif
+            wait_seq(&sh.job_seq, e + 1);
+            job = uniform_job(sh.job);
+            if (!job.runnable) break;
+            const i4v span = sample_span<FMT>(samples, job.off, N);
             if (job.in_margin)
-                fast_consume<FMT, NT, DATA, true, G>(job, span, c0, c1, L, Zs, lane, wave, acc);
+                fast_consume<FMT, NT, DATA, true, G>(job, span, c0, c1, L, Zs, lane, cw, acc);
             else
-                fast_consume<FMT, NT, DATA, false, G>(job, span, c0, c1, L, Zs, lane, wave, acc);
-#ifdef GNSSHIP_FAST_NOCONSUME
-            }
-#endif
-            GNSSHIP_FSTAMP(e, 2 + wave);  // 3, 4, 5: each correlating wave done
+                fast_consume<FMT, NT, DATA, false, G>(job, span, c0, c1, L, Zs, lane, cw, acc);
+            GNSSHIP_FSTAMP(e, 2 + cw);  // 3, 4, 5: each correlating wave done
         }
         // DPP row sums only (no cross-row shuffle through LDS): the first lane of each 16-lane row
         // stores its row's sums; wave 0 adds the rows after the barrier
@@ -570,18 +590,15 @@ __global__ __launch_bounds__(kFThreads, fast_waves_per_simd<THRU>()) void trk_fa
         if (wave == 0) {
             GNSSHIP_FSTAMP(e, 6);
             GNSSHIP_FCLK(e, 14);
-            // tap sums over the rows in row order (lane v sums value v; wave 0's rows hold only the
+            // tap sums over the rows in row order (lane v sums value v; wave 1's rows hold only the
             // N mod 16 tail); the data prompt at 2·kMaxTaps
             float* taps = sh.taps;
             if (lane < 2 * kOut) {
                 const int t = lane >> 1, c = lane & 1;
                 float sum = 0.0f;
-                if (job.tail > 0) {
 #pragma unroll
-                    for (int w = 0; w < 4; w++) sum += sh.red[w][lane];
-                }
-#pragma unroll
-                for (int w = 4; w < 4 * kFWaves; w++) sum += sh.red[w][lane];
+                for (int w = 0; w < 4 * kFWaves; w++)
+                    if (w / 4 != 1 || job.tail > 0) sum += sh.red[w][lane];
                 taps[((DATA && t == NT) ? 2 * kMaxTaps : 2 * t) + c] = sum;
             }
             GNSSHIP_FSTAMP(e, 16);
@@ -591,7 +608,7 @@ __global__ __launch_bounds__(kFThreads, fast_waves_per_simd<THRU>()) void trk_fa
             gnsship_trk_dump_record* dr = dump ? &sh.drec : nullptr;
             const double coh = epoch_pre(k, rc, taps, pdata, r, nullptr, dr);
             GNSSHIP_FSTAMP(e, 17);
-            // hand the prompt to the lock detectors (wave 1; coh 0: no lock test this epoch)
+            // hand the prompt to the lock detectors (wave 2; coh 0: no lock test this epoch)
             if (lane == 0) {
                 sc.p[0] = rc.p[0];
                 sc.p[1] = rc.p[1];
@@ -623,7 +640,9 @@ __global__ __launch_bounds__(kFThreads, fast_waves_per_simd<THRU>()) void trk_fa
                 epoch_post(k, rc, taps, pdata, r, locked, dr);
             }
             GNSSHIP_FSTAMP(e, 24);
+            const uint64_t es = rc.epoch_start;
             epoch_finish(k, rc, r);
+            make_seed(e + 1);  // wave 1 derives the next epoch while the records go out
             GNSSHIP_FSTAMP(e, 25);
             if (lane == 0) {
                 const size_t slot = static_cast<size_t>(e) * n_chans + ch;
@@ -631,7 +650,7 @@ __global__ __launch_bounds__(kFThreads, fast_waves_per_simd<THRU>()) void trk_fa
                 if (dump && (r.flags & 16)) dump[slot] = sh.drec;
                 if (trace) {
                     gnsship_trk_corr_trace tr{};
-                    tr.sample_counter = rc.epoch_start;
+                    tr.sample_counter = es;
                     tr.n_samples = N;
                     tr.n_taps = NT;
                     tr.rem_carrier_phase_rad = job.rem_carr;
@@ -648,7 +667,7 @@ __global__ __launch_bounds__(kFThreads, fast_waves_per_simd<THRU>()) void trk_fa
             e_done = e + 1;
             GNSSHIP_FSTAMP(e, 7);
             GNSSHIP_FCLK(e, 15);
-        } else if (wave == 1) {
+        } else if (wave == 2) {
             // cn0_and_tracking_lock_status (:972-1029) on the LDS copy of its members, beside the loop update
             wait_seq(&sh.pre_seq, e + 1);
             const double coh = sh.coh;
@@ -659,7 +678,6 @@ __global__ __launch_bounds__(kFThreads, fast_waves_per_simd<THRU>()) void trk_fa
                 publish_seq(&sh.lock_seq, e + 1);
             }
         }
-        // the next derive reads nothing the other waves write, and they wait at B for it
     }
     if (wave == 0 && lane == 0) {
         rchan_store(rc, sc);

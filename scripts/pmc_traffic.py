@@ -16,11 +16,15 @@ import sys
 
 root = sys.argv[1]
 kname = sys.argv[2] if len(sys.argv) > 2 else "corr_batch_kernel"
+last_only = len(sys.argv) > 3 and sys.argv[3] == "last"  # only each pass's last dispatch of the kernel (the timed launch)
 vals = {}
 for f in glob.glob(os.path.join(root, "p*", "*counter_collection.csv")) + glob.glob(os.path.join(root, "p*", "*", "*counter_collection.csv")):
-    for row in csv.DictReader(open(f)):
-        if kname not in row["Kernel_Name"]:
-            continue
+    rows = [r for r in csv.DictReader(open(f)) if kname in r["Kernel_Name"]]
+    if last_only and rows:
+        key = lambda r: int(r.get("Dispatch_Id") or r.get("Correlation_Id") or 0)  # noqa: E731
+        top = max(key(r) for r in rows)
+        rows = [r for r in rows if key(r) == top]
+    for row in rows:
         disp = (f, row.get("Dispatch_Id") or row.get("Correlation_Id") or "")
         vals.setdefault(row["Counter_Name"], {}).setdefault(disp, 0.0)
         vals[row["Counter_Name"]][disp] += float(row["Counter_Value"])
