@@ -88,6 +88,7 @@ struct gnsship_acq {
     int P = 0;                   // four-step / huge register points; spectra are then stored transposed
     bool huge = false;           // huge layout (separate column and row kernels)
     float2* twM = nullptr;       // huge: M twiddles exp(-2πi t/M) of the row transform
+    float2* twC = nullptr;       // huge: the column twiddles in column layout, twC[kq·M + m] = exp(-2πi m·kq/N)
     float2* T = nullptr;         // huge: forward column-stage scratch, n_bins × N
     float2* U = nullptr;         // huge: inverse row-stage scratch, prn_batch × n_bins × N
     float* grid_scratch = nullptr; // unused: the huge search keeps no |y|² rows without a kept grid
@@ -142,7 +143,7 @@ extern "C" int gnsship_acq_destroy(gnsship_acq* a)
     (void)hipSetDevice(a->ctx->device);
     (void)hipStreamSynchronize(a->ctx->stream);
     acq_free_grid_buffers(a);
-    void* ptrs[] = {a->tw, a->twM, a->codes_fft, a->res_dev, a->sig_dev};
+    void* ptrs[] = {a->tw, a->twM, a->twC, a->codes_fft, a->res_dev, a->sig_dev};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     delete a;
@@ -165,9 +166,13 @@ static int acq_upload_wipeoffs(gnsship_acq* a, int nb, const std::vector<float>&
         HIP_TRY(ctx, hipMalloc(&a->rowstat, sizeof(RowStat) * static_cast<size_t>(nb) * a->conf.max_prns));
         a->n_bins = nb;
         if (a->huge) {
-            // PRNs searched per round: the inverse row-stage scratch held to ~256 MiB
+            // PRNs searched per round: the inverse row-stage scratch U held to ~128 MiB, so that the
+            // row stage's writes are still in the 256 MB MALL when the column stage reads them
+            // (GNSSHIP_ACQ_U_MIB overrides, for measurement)
             const size_t cell = static_cast<size_t>(nb) * N * sizeof(float2);
-            int pb = static_cast<int>((size_t(256) << 20) / cell);
+            size_t u_mib = 128;
+            if (const char* env = std::getenv("GNSSHIP_ACQ_U_MIB")) u_mib = static_cast<size_t>(std::max(1, std::atoi(env)));
+            int pb = static_cast<int>((u_mib << 20) / cell);
             a->prn_batch = pb < 1 ? 1 : (pb > a->conf.max_prns ? a->conf.max_prns : pb);
             const size_t tiles = static_cast<size_t>(a->prn_batch) * nb * huge_tiles(a->plan.n);
             HIP_TRY(ctx, hipMalloc(&a->T, sizeof(float2) * static_cast<size_t>(nb) * N));
@@ -275,6 +280,13 @@ extern "C" int gnsship_acq_create(gnsship_ctx* ctx, const gnsship_acq_conf* conf
         }
         e = hipMalloc(&a->twM, sizeof(float2) * M);
         if (e == hipSuccess) e = hipMemcpy(a->twM, twm.data(), sizeof(float2) * M, hipMemcpyHostToDevice);
+        // the N-table re-laid out for the column stages: thread m reads twC[kq·M + m] (consecutive
+        // threads, consecutive entries) instead of tw[m·kq] (stride kq); the same values
+        std::vector<float2> twc(static_cast<size_t>(N));
+        for (int kq = 0; kq < P; kq++)
+            for (int m = 0; m < M; m++) twc[static_cast<size_t>(kq) * M + m] = tw[static_cast<size_t>(m) * kq];
+        if (e == hipSuccess) e = hipMalloc(&a->twC, sizeof(float2) * N);
+        if (e == hipSuccess) e = hipMemcpy(a->twC, twc.data(), sizeof(float2) * N, hipMemcpyHostToDevice);
     }
     if (e == hipSuccess) e = hipMalloc(&a->res_dev, sizeof(gnsship_acq_result) * conf->max_prns);
     if (e == hipSuccess) e = hipMalloc(&a->sig_dev, sizeof(float2) * static_cast<size_t>(N));
@@ -322,7 +334,7 @@ extern "C" int gnsship_acq_set_local_code(gnsship_acq* a, int prn_slot, const fl
     HIP_TRY(ctx, hipMemcpyAsync(a->sig_dev, buf.data(), sizeof(float2) * N, hipMemcpyHostToDevice, ctx->stream));
     float2* dst = a->codes_fft + static_cast<size_t>(prn_slot) * N;
     if (a->huge)
-        HIP_TRY(ctx, launch_acq_fft_huge(a->sig_dev, GNSSHIP_FMT_CF32, nullptr, 1, a->P, a->plan, a->tw, a->twM, a->T, dst, 1, N, ctx->stream));
+        HIP_TRY(ctx, launch_acq_fft_huge(a->sig_dev, GNSSHIP_FMT_CF32, nullptr, 1, a->P, a->plan, a->twC, a->twM, a->T, dst, 1, N, ctx->stream));
     else if (a->P)
         HIP_TRY(ctx, launch_acq_fft_big(a->sig_dev, GNSSHIP_FMT_CF32, nullptr, 1, a->P, a->plan, a->tw, dst, 1, N, ctx->stream));
     else
@@ -363,12 +375,12 @@ extern "C" int gnsship_acq_run(gnsship_acq* a, const void* sig, int fmt, int sig
     const int accumulate = (a->conf.max_dwells > 1 && a->dwell_count > 0) ? 1 : 0;
     a->dwell_count++;
     if (a->huge) {
-        HIP_TRY(ctx, launch_acq_fft_huge(src, fmt, a->wipe, a->n_bins, a->P, a->plan, a->tw, a->twM, a->T, a->X, 0, a->consumed, ctx->stream));
+        HIP_TRY(ctx, launch_acq_fft_huge(src, fmt, a->wipe, a->n_bins, a->P, a->plan, a->twC, a->twM, a->T, a->X, 0, a->consumed, ctx->stream));
         for (int p0 = 0; p0 < n_prns; p0 += a->prn_batch) {
             const int np = std::min(a->prn_batch, n_prns - p0);
             // without a kept grid the |y|² rows never reach HBM (tile statistics + finalize's recomputation)
             float* g = keep_grid ? a->grid_dev + static_cast<size_t>(p0) * a->n_bins * rs.row_len : nullptr;
-            HIP_TRY(ctx, launch_acq_search_huge(a->X, a->codes_fft, p0, np, a->n_bins, a->P, a->plan, a->tw, a->twM, a->U, g,
+            HIP_TRY(ctx, launch_acq_search_huge(a->X, a->codes_fft, p0, np, a->n_bins, a->P, a->plan, a->twC, a->twM, a->U, g,
                              keep_grid ? accumulate : 0, a->tiles, rs, a->rowstat, ctx->stream));
         }
     } else if (a->P) {

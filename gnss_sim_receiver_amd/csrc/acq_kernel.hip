@@ -1257,7 +1257,7 @@ __global__ __launch_bounds__(kHugeColThreads) void acq_huge_cols_fwd_kernel(cons
     dft_reg<P, 1, -1>(v, twN, N);
     float2* out = T + static_cast<int64_t>(b) * N + m;
 #pragma unroll
-    for (int kq = 0; kq < P; kq++) out[kq * M] = kq ? cmulf(v[kq], twN[m * kq]) : v[kq];  // W_N^{m·kq}, m·kq < N
+    for (int kq = 0; kq < P; kq++) out[kq * M] = kq ? cmulf(v[kq], twN[kq * M + m]) : v[kq];  // W_N^{m·kq} (column layout, coalesced)
 }
 
 // One LDS-resident M-point transform per block: row blockIdx.x of cell (blockIdx.y, blockIdx.z).
@@ -1298,7 +1298,7 @@ __device__ __forceinline__ void huge_col_inv(const float2* __restrict__ u, int m
     for (int kq = 0; kq < P; kq++) {
         float2 x = u[kq * M];
         if (kq) {
-            float2 w = twN[m * kq];  // W_N^{−m·kq}
+            float2 w = twN[kq * M + m];  // W_N^{−m·kq}: the column-layout table twC[kq·M + m] = W_N^{m·kq} (coalesced)
             w.y = -w.y;
             x = cmulf(x, w);
         }
