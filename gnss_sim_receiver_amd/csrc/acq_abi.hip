@@ -92,8 +92,11 @@ struct gnsship_acq {
     float2* T = nullptr;         // huge: forward column-stage scratch, n_bins × N
     float2* U = nullptr;         // huge: inverse row-stage scratch, prn_batch × n_bins × N
     float* grid_scratch = nullptr; // unused: the huge search keeps no |y|² rows without a kept grid
-    TileStat* tiles = nullptr;   // huge: prn_batch × n_bins × huge_tiles(M)
+    TileStat* tiles = nullptr;   // huge: lanes × prn_batch × n_bins × huge_tiles(M)
     int prn_batch = 0;
+    int lanes = 1;               // huge: PRN batches in flight together (U and tiles per lane)
+    hipStream_t lane_stream = nullptr;  // huge, lanes = 2: the second batch lane
+    hipEvent_t ev_fwd = nullptr, ev_lane = nullptr;
     int n_bins = 0;
     int dwell_count = 0;
     float2* tw = nullptr;        // N twiddles exp(-2πi t/N)
@@ -146,6 +149,9 @@ extern "C" int gnsship_acq_destroy(gnsship_acq* a)
     void* ptrs[] = {a->tw, a->twM, a->twC, a->codes_fft, a->res_dev, a->sig_dev};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
+    if (a->lane_stream) (void)hipStreamDestroy(a->lane_stream);
+    if (a->ev_fwd) (void)hipEventDestroy(a->ev_fwd);
+    if (a->ev_lane) (void)hipEventDestroy(a->ev_lane);
     delete a;
     return GNSSHIP_OK;
 }
@@ -172,12 +178,23 @@ static int acq_upload_wipeoffs(gnsship_acq* a, int nb, const std::vector<float>&
             const size_t cell = static_cast<size_t>(nb) * N * sizeof(float2);
             size_t u_mib = 128;
             if (const char* env = std::getenv("GNSSHIP_ACQ_U_MIB")) u_mib = static_cast<size_t>(std::max(1, std::atoi(env)));
-            int pb = static_cast<int>((u_mib << 20) / cell);
+            // Two batch lanes (GNSSHIP_ACQ_LANES=1: one): batch i runs on lane i mod 2 with its own U and
+            // tiles, so one batch's column stage and finalize overlap the next batch's row stage (the
+            // persistent row kernel's drain and the finalize's small grid no longer idle the chip);
+            // the two lanes share the U budget.
+            a->lanes = 2;
+            if (const char* env = std::getenv("GNSSHIP_ACQ_LANES")) a->lanes = std::atoi(env) == 1 ? 1 : 2;
+            int pb = static_cast<int>((u_mib << 20) / (cell * a->lanes));
             a->prn_batch = pb < 1 ? 1 : (pb > a->conf.max_prns ? a->conf.max_prns : pb);
             const size_t tiles = static_cast<size_t>(a->prn_batch) * nb * huge_tiles(a->plan.n);
             HIP_TRY(ctx, hipMalloc(&a->T, sizeof(float2) * static_cast<size_t>(nb) * N));
-            HIP_TRY(ctx, hipMalloc(&a->U, cell * a->prn_batch));
-            HIP_TRY(ctx, hipMalloc(&a->tiles, sizeof(TileStat) * tiles));
+            HIP_TRY(ctx, hipMalloc(&a->U, cell * a->prn_batch * a->lanes));
+            HIP_TRY(ctx, hipMalloc(&a->tiles, sizeof(TileStat) * tiles * a->lanes));
+            if (a->lanes == 2 && !a->lane_stream) {
+                HIP_TRY(ctx, hipStreamCreateWithFlags(&a->lane_stream, hipStreamNonBlocking));
+                HIP_TRY(ctx, hipEventCreateWithFlags(&a->ev_fwd, hipEventDisableTiming));
+                HIP_TRY(ctx, hipEventCreateWithFlags(&a->ev_lane, hipEventDisableTiming));
+            }
         }
     }
     std::vector<float2> host(static_cast<size_t>(nb) * N);
@@ -376,12 +393,24 @@ extern "C" int gnsship_acq_run(gnsship_acq* a, const void* sig, int fmt, int sig
     a->dwell_count++;
     if (a->huge) {
         HIP_TRY(ctx, launch_acq_fft_huge(src, fmt, a->wipe, a->n_bins, a->P, a->plan, a->twC, a->twM, a->T, a->X, 0, a->consumed, ctx->stream));
-        for (int p0 = 0; p0 < n_prns; p0 += a->prn_batch) {
+        const bool two = a->lanes == 2 && n_prns > a->prn_batch;
+        if (two) {
+            HIP_TRY(ctx, hipEventRecord(a->ev_fwd, ctx->stream));
+            HIP_TRY(ctx, hipStreamWaitEvent(a->lane_stream, a->ev_fwd, 0));  // lane 1 reads the forward spectra
+        }
+        const size_t u_lane = static_cast<size_t>(a->prn_batch) * a->n_bins * a->conf.fft_size;
+        const size_t t_lane = static_cast<size_t>(a->prn_batch) * a->n_bins * huge_tiles(a->plan.n);
+        for (int p0 = 0, i = 0; p0 < n_prns; p0 += a->prn_batch, i++) {
             const int np = std::min(a->prn_batch, n_prns - p0);
+            const int lane = two ? (i & 1) : 0;  // batches i and i + 2 share a lane's U and tiles, in stream order
             // without a kept grid the |y|² rows never reach HBM (tile statistics + finalize's recomputation)
             float* g = keep_grid ? a->grid_dev + static_cast<size_t>(p0) * a->n_bins * rs.row_len : nullptr;
-            HIP_TRY(ctx, launch_acq_search_huge(a->X, a->codes_fft, p0, np, a->n_bins, a->P, a->plan, a->twC, a->twM, a->U, g,
-                             keep_grid ? accumulate : 0, a->tiles, rs, a->rowstat, ctx->stream));
+            HIP_TRY(ctx, launch_acq_search_huge(a->X, a->codes_fft, p0, np, a->n_bins, a->P, a->plan, a->twC, a->twM, a->U + lane * u_lane, g,
+                             keep_grid ? accumulate : 0, a->tiles + lane * t_lane, rs, a->rowstat, lane ? a->lane_stream : ctx->stream));
+        }
+        if (two) {  // the decision reads every batch's row statistics
+            HIP_TRY(ctx, hipEventRecord(a->ev_lane, a->lane_stream));
+            HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, a->ev_lane, 0));
         }
     } else if (a->P) {
         HIP_TRY(ctx, launch_acq_fft_big(src, fmt, a->wipe, a->n_bins, a->P, a->plan, a->tw, a->X, 0, a->consumed, ctx->stream));

@@ -11,12 +11,14 @@
 //
 //  * wave 0 is the control wave.  The channel's loop state lives in its registers for the whole
 //    run (RChan, trk_loop.h) — no LDS round trip per member.  After the correlation it sums the
-//    taps, runs the loop update, and as soon as epoch_post has settled the next epoch's NCO it
-//    publishes that epoch's correlator arguments (the seed) before writing this epoch's records;
+//    taps and runs the loop update; in state 4 it publishes the next epoch's correlator arguments
+//    (the seed) as soon as update_tracking_vars has set them — before the lock test's outcome, which
+//    a failed test cancels (the channel stops) — and only then finishes this epoch and writes its
+//    records (other states: after epoch_post);
 //  * wave 1 is the phasor wave: from the seed it derives cos/sin of the NCO phase and step (double,
 //    once rounded, in two lanes), dz = normalise(inc^16) and the 16 AVX lane starts, then replays
 //    the 16 phasor chains (z ← z·dz, the reference's float products, two lanes per chain with a DPP
-//    partner product) and stores each chain's phasor at every task start (G iterations, 4 for GPS
+//    partner product) and stores each chain's phasor at every task start (G iterations, 8 for GPS
 //    at 4 Msps) with a plain LDS store — no fence, no flag: the phasor slot itself is the signal
 //    (all-ones NaN = not yet written; a phasor is never NaN);
 //  * waves 0, 2 and 3 correlate: groups of four tasks, lane (task, l) polls its slot, re-arms it for
@@ -410,6 +412,7 @@ __global__ __launch_bounds__(kFThreads, fast_waves_per_simd<THRU>()) void trk_fa
     __shared__ f2 tailz[kAvxLanes];
     const int ch = blockIdx.x;
     const int tid = threadIdx.x, lane = tid & (kWave - 1), wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    // (an LDS copy of the parameters measured slower: 8.20 vs 8.00 us per C2 epoch, profiling build)
     const TrkParams& k = *pk;
     {
         const int* src = reinterpret_cast<const int*>(chans + ch);
@@ -459,29 +462,44 @@ __global__ __launch_bounds__(kFThreads, fast_waves_per_simd<THRU>()) void trk_fa
     // settled them, so the derive and the first tasks of epoch e + 1 overlap epoch e's record writes.
     const int cw = wave == 0 ? 1 : wave;  // correlating waves 0, 2, 3 take group sets 1, 2, 3
     uint64_t seed_start = 0;              // wave 0: the epoch start the seed was made for
+    // wave 0: the seed's per-run constants, read once (inside the epoch loop each TrkParams member is a
+    // dependent scalar load on the chain)
+    const uint64_t vl = k.conf.vector_length;
+    const float spcf = static_cast<float>(k.code_samples_per_chip);
+    const int32_t has_if = k.has_if;
+    const double if_step = k.if_step_rad;
+    float shv_w[5], shv_n[5];
+    float smin_w = 0.0f, smax_w = 0.0f, smin_n = 0.0f, smax_n = 0.0f;
+#pragma unroll
+    for (int t = 0; t < 5; t++) {
+        shv_w[t] = t < NT ? k.shifts[t] : 0.0f;
+        shv_n[t] = t < NT ? k.shifts_n[t] : 0.0f;
+        smin_w = fminf(smin_w, shv_w[t]);
+        smax_w = fmaxf(smax_w, shv_w[t]);
+        smin_n = fminf(smin_n, shv_n[t]);
+        smax_n = fmaxf(smax_n, shv_n[t]);
+    }
     // wave 0: do_correlation_step's arguments for the epoch at nitems_read (all but the phasors)
     auto make_seed = [&](int e) {
-        const uint64_t vl = k.conf.vector_length;
         const bool runnable = e < max_rounds && (rc.state == 2 || rc.state == 3 || rc.state == 4) && rc.nitems_read >= buf_first &&
                               rc.nitems_read + vl <= buf_first + static_cast<uint64_t>(buf_len);
-        const float rem_carr = corr_rem_carr(k, rc), stepf = corr_phase_step(k, rc);
+        // corr_rem_carr / corr_phase_step (trk_loop.h) on the hoisted IF constants
+        const float rem_carr = has_if ? static_cast<float>(fmod(static_cast<double>(rc.rem_carr_phase_rad) + kTwoPi * rc.if_cyc, kTwoPi))
+                                      : rc.rem_carr_phase_rad;
+        const float stepf = static_cast<float>(rc.carrier_phase_step_rad + if_step);
         if (runnable) rc.epoch_start = rc.nitems_read;
         seed_start = rc.epoch_start;
         if (lane == 0) {
             FJob& j = sh.job;
             j.runnable = runnable ? 1 : 0;
             if (runnable) {
-                const float spcf = static_cast<float>(k.code_samples_per_chip);
-                const float* shv = uni(rc.narrow) ? k.shifts_n : k.shifts;
+                const bool nw = uni(rc.narrow) != 0;
                 j.off = static_cast<int64_t>(rc.nitems_read - buf_first);
                 j.rem_code = __fmul_rn(static_cast<float>(rc.rem_code_phase_chips), spcf);
                 j.code_step = __fmul_rn(static_cast<float>(rc.code_phase_step_chips), spcf);
-                float smin = 0.0f, smax = 0.0f;
-                for (int t = 0; t < 5; t++) {
-                    j.shifts[t] = t < NT ? shv[t] : 0.0f;
-                    smin = fminf(smin, j.shifts[t]);
-                    smax = fmaxf(smax, j.shifts[t]);
-                }
+#pragma unroll
+                for (int t = 0; t < 5; t++) j.shifts[t] = nw ? shv_n[t] : shv_w[t];
+                const float smin = nw ? smin_n : smin_w, smax = nw ? smax_n : smax_w;
                 const double span = static_cast<double>(j.code_step) * static_cast<double>(N > 0 ? N - 1 : 0);
                 const double lo = fmin(0.0, span) + smin - j.rem_code - 2.0;
                 const double hi = fmax(0.0, span) + smax - j.rem_code + 2.0;
@@ -497,6 +515,7 @@ __global__ __launch_bounds__(kFThreads, fast_waves_per_simd<THRU>()) void trk_fa
     };
     if (wave == 0) make_seed(0);
     int e_done = 0;
+    bool cancel = false;  // wave 0: the current epoch was seeded before a lock test that failed
     for (int e = 0;; e++) {
         f2 acc[NT + 1];
 #pragma unroll
@@ -590,15 +609,30 @@ __global__ __launch_bounds__(kFThreads, fast_waves_per_simd<THRU>()) void trk_fa
         if (wave == 0) {
             GNSSHIP_FSTAMP(e, 6);
             GNSSHIP_FCLK(e, 14);
+            if (cancel) {
+                // the epoch seeded speculatively before the last lock test failed: the channel stopped
+                // there (state 0), so nothing of this epoch is kept — no lock test, no record — and
+                // the seed for the next one says "not runnable", which ends every wave's loop
+                cancel = false;
+                if (lane == 0) {
+                    sh.coh = 0.0;
+                    publish_seq(&sh.pre_seq, e + 1);
+                }
+                make_seed(e + 1);
+                continue;
+            }
             // tap sums over the rows in row order (lane v sums value v; wave 1's rows hold only the
-            // N mod 16 tail); the data prompt at 2·kMaxTaps
+            // N mod 16 tail), the 16 row values loaded together first; the data prompt at 2·kMaxTaps
             float* taps = sh.taps;
             if (lane < 2 * kOut) {
                 const int t = lane >> 1, c = lane & 1;
+                float v[4 * kFWaves];
+#pragma unroll
+                for (int w = 0; w < 4 * kFWaves; w++) v[w] = sh.red[w][lane];
                 float sum = 0.0f;
 #pragma unroll
                 for (int w = 0; w < 4 * kFWaves; w++)
-                    if (w / 4 != 1 || job.tail > 0) sum += sh.red[w][lane];
+                    if (w / 4 != 1 || job.tail > 0) sum += v[w];
                 taps[((DATA && t == NT) ? 2 * kMaxTaps : 2 * t) + c] = sum;
             }
             GNSSHIP_FSTAMP(e, 16);
@@ -606,6 +640,7 @@ __global__ __launch_bounds__(kFThreads, fast_waves_per_simd<THRU>()) void trk_fa
             gnsship_trk_epoch r{};
             r.flags = 8;
             gnsship_trk_dump_record* dr = dump ? &sh.drec : nullptr;
+            const uint64_t es = rc.epoch_start;  // this epoch's first sample
             const double coh = epoch_pre(k, rc, taps, pdata, r, nullptr, dr);
             GNSSHIP_FSTAMP(e, 17);
             // hand the prompt to the lock detectors (wave 2; coh 0: no lock test this epoch)
@@ -617,6 +652,7 @@ __global__ __launch_bounds__(kFThreads, fast_waves_per_simd<THRU>()) void trk_fa
                 publish_seq(&sh.pre_seq, e + 1);
             }
             GNSSHIP_FSTAMP(e, 18);
+            bool seeded = false;
             if (coh > 0.0) {  // the loop runs speculatively beside the lock test
                 // what the record shows if the test fails (the channel then stops: nothing else of the
                 // loop's output is ever read)
@@ -625,6 +661,19 @@ __global__ __launch_bounds__(kFThreads, fast_waves_per_simd<THRU>()) void trk_fa
                 const float k_rem = rc.rem_carr_phase_rad;
                 const int32_t k_len = rc.current_prn_length_samples;
                 epoch_loop(k, rc, nullptr);
+                // State 4: epoch_post cannot change what the next epoch's correlation needs (the
+                // channel stays runnable — 4, or 3 for extended integration — on the same taps), so
+                // the next epoch is seeded now, before the lock test's outcome, and wave 1 derives
+                // it while this epoch finishes.  A failed test (the channel stops) cancels it.
+                const uint64_t k_nir = rc.nitems_read;
+                const int64_t k_ifn = rc.if_num;
+                const double k_ifc = rc.if_cyc;
+                if (rc.state == 4) {
+                    epoch_consume(k, rc);
+                    make_seed(e + 1);
+                    rc.epoch_start = es;  // epoch_post and the record still describe this epoch
+                    seeded = true;
+                }
                 wait_seq(&sh.lock_seq, e + 1);
                 GNSSHIP_FSTAMP(e, 19);
                 const bool locked = sh.locked != 0;
@@ -636,13 +685,19 @@ __global__ __launch_bounds__(kFThreads, fast_waves_per_simd<THRU>()) void trk_fa
                     rc.rem_code_phase_chips = k_rcc;
                     rc.rem_carr_phase_rad = k_rem;
                     rc.current_prn_length_samples = k_len;
+                    rc.nitems_read = k_nir;
+                    rc.if_num = k_ifn;
+                    rc.if_cyc = k_ifc;
+                    cancel = seeded;
                 }
                 epoch_post(k, rc, taps, pdata, r, locked, dr);
             }
             GNSSHIP_FSTAMP(e, 24);
-            const uint64_t es = rc.epoch_start;
-            epoch_finish(k, rc, r);
-            make_seed(e + 1);  // wave 1 derives the next epoch while the records go out
+            epoch_finish(k, rc, r, !seeded);  // (a stopped channel consumes nothing either way)
+            if (!seeded)
+                make_seed(e + 1);  // wave 1 derives the next epoch while the records go out
+            else if (!cancel)
+                rc.epoch_start = seed_start;  // the next epoch, as make_seed left it
             GNSSHIP_FSTAMP(e, 25);
             if (lane == 0) {
                 const size_t slot = static_cast<size_t>(e) * n_chans + ch;
@@ -704,8 +759,11 @@ namespace gnsship {
 #endif
 
 // Task length G (iterations per phasor slot) and the LDS bytes of the dynamic region (codes + slots):
-// the shortest task whose slots fit the budget (4 iterations keeps the epoch's tail short; longer
-// epochs take longer tasks).  0 when even 64-iteration tasks do not fit.
+// the shortest task of at least kFastMinG iterations whose slots fit the budget (longer epochs take
+// longer tasks).  8 rather than 4: half the slot stores and asm-block boundaries on the replay chain
+// for four more iterations on the last task (C2, profiling build: 8.24 -> 8.00 us per epoch).  0 when
+// even 64-iteration tasks do not fit.
+constexpr int kFastMinG = 8;
 static size_t fast_lds(const TrkParams& p, int code_cap_floats, int n_chans, int* g_out, int* slots_out)
 {
     const int N = static_cast<int>(p.conf.vector_length);
@@ -713,7 +771,7 @@ static size_t fast_lds(const TrkParams& p, int code_cap_floats, int n_chans, int
     const size_t codes = static_cast<size_t>(p.jobs_per_channel > 1 ? 2 : 1) * code_cap_floats * sizeof(float);
     // more channels than CUs: two workgroups per CU share its LDS
     const size_t budget = n_chans > 256 ? 72 * 1024 : kTrkPersistMaxLds;
-    for (int G = 4; G <= 64; G *= 2) {
+    for (int G = kFastMinG; G <= 64; G *= 2) {
         const int S = (M + G - 1) / G;
         const size_t bytes = codes + static_cast<size_t>(S > 0 ? S : 1) * kAvxLanes * sizeof(uint64_t);
         if (bytes <= budget) {
@@ -744,8 +802,17 @@ hipError_t launch_trk_fast(const TrkParams* params_dev, const TrkParams& params,
     gnsship_trk_dump_record* dump, gnsship_trk_corr_trace* trace, int* ran_count, hipStream_t stream)
 {
     int G = 0, slots = 0;
-    const size_t lds = fast_lds(params, code_cap_floats, n_chans, &G, &slots);
+    size_t lds = fast_lds(params, code_cap_floats, n_chans, &G, &slots);
     if (lds == 0) return hipErrorInvalidValue;
+    if (const char* env = std::getenv("GNSSHIP_TRK_FAST_G")) {  // measurement: a longer task than the shortest that fits
+        const int g = std::atoi(env);
+        if (g > G && g <= 64 && (g & (g - 1)) == 0) {
+            const int M = static_cast<int>(params.conf.vector_length) / kAvxLanes;
+            G = g;
+            slots = std::max(1, (M + G - 1) / G);
+            lds = static_cast<size_t>(params.jobs_per_channel > 1 ? 2 : 1) * code_cap_floats * sizeof(float) + static_cast<size_t>(slots) * kAvxLanes * sizeof(uint64_t);
+        }
+    }
     const bool data = params.jobs_per_channel > 1;
     bool thru = n_chans > 256;
     if (const char* env = std::getenv("GNSSHIP_TRK_THRU")) thru = env[0] == '1';

@@ -117,7 +117,7 @@ __device__ bool lock_status(const TrkParams& k, TrkChannel& c, double coh_integr
         c.cn0_counter++;
         return true;
     }
-    const int slot = c.cn0_counter % ns;
+    const int slot = ns == 20 ? c.cn0_counter % 20 : c.cn0_counter % ns;  // the default as a constant divisor
     c.prompt_buf[2 * slot] = c.p[0];
     c.prompt_buf[2 * slot + 1] = c.p[1];
     c.cn0_counter++;
@@ -670,6 +670,14 @@ __device__ __forceinline__ bool seconds_exceed(uint64_t elapsed, uint32_t limit_
     return elapsed >= (static_cast<uint64_t>(limit_s) + 1u) * fs_int;
 }
 
+// (i + 1) % n for a counter kept in [0, n) — the reference's modulo without an integer division
+// (any other value still takes the division, so the result is (i + 1) % n for every i ≥ 0)
+__device__ __forceinline__ int next_mod(int i, int n)
+{
+    const int v = i + 1;
+    return v < n ? v : (v == n ? 0 : v % n);
+}
+
 template <class C>
 __device__ double epoch_pre(const TrkParams& k, C& c, const float* taps, const float* pdata, gnsship_trk_epoch& rec, TrkHist* h,
     gnsship_trk_dump_record* dump)
@@ -708,7 +716,7 @@ __device__ double epoch_pre(const TrkParams& k, C& c, const float* taps, const f
     float sgn = 1.0f;
     if (syncset(k, c).secondary) {
         sgn = bit_at(syncset(k, c).secondary_bits, c.current_symbol) ? -1.0f : 1.0f;
-        c.current_symbol = (c.current_symbol + 1) % syncset(k, c).secondary_len;
+        c.current_symbol = next_mod(c.current_symbol, syncset(k, c).secondary_len);
     }
     if (k.veml) {
         cadd(c.ve, taps, sgn);
@@ -721,10 +729,10 @@ __device__ double epoch_pre(const TrkParams& k, C& c, const float* taps, const f
     if (syncset(k, c).symbols_per_bit > 1) {
         if (syncset(k, c).data_secondary_len > 0) {
             cadd(c.p_data, src, bit_at(syncset(k, c).data_secondary_bits, c.current_data_symbol) ? -1.0f : 1.0f);
-            c.current_data_symbol = (c.current_data_symbol + 1) % syncset(k, c).data_secondary_len;
+            c.current_data_symbol = next_mod(c.current_data_symbol, syncset(k, c).data_secondary_len);
         } else {
             cadd(c.p_data, src, 1.0f);
-            c.current_data_symbol = (c.current_data_symbol + 1) % syncset(k, c).symbols_per_bit;
+            c.current_data_symbol = next_mod(c.current_data_symbol, syncset(k, c).symbols_per_bit);
         }
     } else {
         c.p_data[0] = src[0];
@@ -825,9 +833,18 @@ __device__ void epoch_post(const TrkParams& k, C& c, const float* taps, const fl
 template <class C>
 __device__ __forceinline__ void advance_if(const TrkParams& k, C& c, int32_t consumed);
 
-// The record's loop outputs and consume_each (:2061); false when the channel stopped (loss of lock).
+// consume_each (:2061) and the IF phase of the consumed samples.
 template <class C>
-__device__ bool epoch_finish(const TrkParams& k, C& c, gnsship_trk_epoch& rec)
+__device__ __forceinline__ void epoch_consume(const TrkParams& k, C& c)
+{
+    c.nitems_read = c.epoch_start + static_cast<uint64_t>(c.current_prn_length_samples);
+    advance_if(k, c, c.current_prn_length_samples);
+}
+
+// The record's loop outputs and consume_each (:2061); false when the channel stopped (loss of lock).
+// consume = false: the caller has already run epoch_consume (the fast kernel's early seed).
+template <class C>
+__device__ bool epoch_finish(const TrkParams& k, C& c, gnsship_trk_epoch& rec, bool consume = true)
 {
     if (c.pll_180) rec.flags |= 4;
     rec.code_phase_samples = c.rem_code_phase_samples;
@@ -840,8 +857,7 @@ __device__ bool epoch_finish(const TrkParams& k, C& c, gnsship_trk_epoch& rec)
     rec.rem_carr_phase_rad = c.rem_carr_phase_rad;
     rec.prn_length_samples = c.current_prn_length_samples;
     if (rec.flags & 2) return false;
-    c.nitems_read = c.epoch_start + static_cast<uint64_t>(c.current_prn_length_samples);  // consume_each (:2061)
-    advance_if(k, c, c.current_prn_length_samples);
+    if (consume) epoch_consume(k, c);
     return true;
 }
 

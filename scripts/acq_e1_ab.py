@@ -1,7 +1,8 @@
 """A/B of the Galileo E1 all-sky search (32 PRN x 40 bins, N = 100000 at 25 Msps, the huge layout)
 between two builds, each in its own process (GNSSHIP_LIB_PATH): per-PRN Doppler / code index /
 statistic and the sweep time.
-    python scripts/acq_e1_ab.py scripts/libgnsship_base.so gnss_sim_receiver_amd/libgnsship.so"""
+    python scripts/acq_e1_ab.py scripts/libgnsship_base.so gnss_sim_receiver_amd/libgnsship.so
+Either side may carry environment settings after a colon: lib.so:GNSSHIP_ACQ_LANES=1,OTHER=2."""
 import json
 import os
 import subprocess
@@ -40,8 +41,10 @@ def main():
         run_one()
         return
     outs = []
-    for lib in sys.argv[1:3]:
+    for spec in sys.argv[1:3]:
+        lib, _, extra = spec.partition(":")
         env = dict(os.environ, GNSSHIP_LIB_PATH=os.path.abspath(lib))
+        env.update(kv.split("=", 1) for kv in extra.split(",") if kv)
         p = subprocess.run([sys.executable, os.path.abspath(__file__), "--one"], env=env, capture_output=True, text=True, timeout=300)
         line = [x for x in p.stdout.splitlines() if x.startswith("RESULT ")]
         if not line:

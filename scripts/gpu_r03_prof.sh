@@ -5,6 +5,9 @@ set -o pipefail
 R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/r03prof
 mkdir -p $O/pmc
+cd $R && timeout -k 10 200 python -u -m pytest tests/test_gpu_receiver.py -m gpu -q --timeout 150 --timeout-method thread > $O/rx_tests.log 2>&1; echo "rx tests rc=$?"; tail -2 $O/rx_tests.log
+timeout -k 10 120 python3 scripts/trk_fast_profile.py 12 > $O/fast_phases.txt 2>&1 || { echo "phase profile failed"; tail $O/fast_phases.txt; exit 1; }
+cat $O/fast_phases.txt
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 $R/bench.py --steps 10 --warmup 2 --no-aux --cpu-seconds 0 > $O/prof_bench.json 2> $O/prof_stderr.txt || { echo "rocprof failed"; tail $O/prof_stderr.txt; exit 1; }
 cat $O/prof_bench.json

@@ -38,20 +38,27 @@ pytestmark = pytest.mark.gpu
 TOL = 1e-5
 
 
-def compare_if(dev, ref, label):
-    """test_gpu_trk.compare with the IF loop's Doppler / carrier-phase bounds (module docstring)."""
+def compare_if(dev, ref, label, kick_frac=0.0, kick_scale=1.0):
+    """test_gpu_trk.compare with the IF loop's Doppler / carrier-phase bounds (module docstring).
+    kick_frac > 0 (long runs): up to that fraction of the epochs may exceed a bound, by at most
+    kick_scale × the bound — the one-epoch discriminator kicks that the loops' ~1e-7 correlation
+    sum differences occasionally cause (test_gpu_headline_pin.py), which the PLL then carries for a
+    few epochs; epoch boundaries, states and flags stay exact either way."""
     d = dev[(dev["flags"] & 8) == 8]
     assert len(d) == len(ref), (label, len(d), len(ref))
     for f in ("sample_counter", "state", "prn_length_samples"):
         assert np.array_equal(d[f], ref[f]), (label, f, np.nonzero(d[f] != ref[f])[0][:5])
     assert np.array_equal(d["flags"] & 7, ref["flags"] & 7), label
-    np.testing.assert_allclose(d["carrier_doppler_hz"], ref["carrier_doppler_hz"], rtol=0, atol=0.25, err_msg=label)
-    # the DLL sees the same phase-step kicks: 5e-2 Hz (5e-8 relative)
-    np.testing.assert_allclose(d["code_freq_chips"], ref["code_freq_chips"], rtol=0, atol=5e-2, err_msg=label)
-    # the code NCO integrates that frequency difference: 5e-2 Hz over a 4 ms E1 epoch is 2e-4 chips
-    np.testing.assert_allclose(d["rem_code_phase_chips"], ref["rem_code_phase_chips"], rtol=0, atol=2e-4, err_msg=label)
-    np.testing.assert_allclose(d["cn0_db_hz"], ref["cn0_db_hz"], rtol=0, atol=5e-2, err_msg=label)
-    np.testing.assert_allclose(d["carrier_phase_rads"], ref["carrier_phase_rads"], rtol=0, atol=5e-2, err_msg=label)
+    # Doppler 0.25 Hz; the DLL sees the same phase-step kicks: code frequency 5e-2 Hz (5e-8
+    # relative); the code NCO integrates that frequency difference: 5e-2 Hz over a 4 ms E1 epoch is
+    # 2e-4 chips; CN0 5e-2 dB; accumulated carrier phase 5e-2 rad
+    for f, tol in (("carrier_doppler_hz", 0.25), ("code_freq_chips", 5e-2), ("rem_code_phase_chips", 2e-4), ("cn0_db_hz", 5e-2),
+                   ("carrier_phase_rads", 5e-2)):
+        err = np.abs(d[f] - ref[f])
+        if kick_frac > 0.0:
+            assert np.mean(err > tol) <= kick_frac and err.max() <= kick_scale * tol, (label, f, float(np.mean(err > tol)), float(err.max()))
+        else:
+            np.testing.assert_allclose(d[f], ref[f], rtol=0, atol=tol, err_msg=f"{label} {f}")
 
 
 def check_trace(tr, xf, first, codes, data_code=None):
