@@ -399,6 +399,15 @@ __device__ void stage_code_f(float* dst, const CodeDesc& cd)
 template <bool THRU>
 constexpr int fast_waves_per_simd() { return THRU ? 2 : 1; }
 
+template <bool THRU>
+__device__ __forceinline__ const auto& loop_params(const TrkParams& k, const KFast& kf)
+{
+    if constexpr (THRU)
+        return k;
+    else
+        return kf;
+}
+
 template <int FMT, int NT, bool DATA, int G, bool THRU>
 __global__ __launch_bounds__(kFThreads, fast_waves_per_simd<THRU>()) void trk_fast_kernel(const TrkParams* __restrict__ pk, TrkChannel* __restrict__ chans,
     const CodeDesc* __restrict__ codes, int n_codes, const void* __restrict__ samples, uint64_t buf_first, int64_t buf_len, int max_rounds,
@@ -452,6 +461,10 @@ __global__ __launch_bounds__(kFThreads, fast_waves_per_simd<THRU>()) void trk_fa
     constexpr int kOut = NT + (DATA ? 1 : 0);
     RChan rc;
     if (wave == 0) rchan_load(sc, &sc, rc);
+    // wave 0's loop parameters in registers for the run (two workgroups per CU have no registers to
+    // spare: they keep reading TrkParams)
+    const KFast kf = make_kfast(k, sc.geo);
+    const auto& kp = loop_params<THRU>(k, kf);
     // Wave roles (one channel per workgroup, its epochs a serial chain):
     //   wave 0 — the control wave: the loop update on its register-resident channel (RChan), the
     //            epoch records, and one third of the correlation;
@@ -641,7 +654,7 @@ __global__ __launch_bounds__(kFThreads, fast_waves_per_simd<THRU>()) void trk_fa
             r.flags = 8;
             gnsship_trk_dump_record* dr = dump ? &sh.drec : nullptr;
             const uint64_t es = rc.epoch_start;  // this epoch's first sample
-            const double coh = epoch_pre(k, rc, taps, pdata, r, nullptr, dr);
+            const double coh = epoch_pre(kp, rc, taps, pdata, r, nullptr, dr);
             GNSSHIP_FSTAMP(e, 17);
             // hand the prompt to the lock detectors (wave 2; coh 0: no lock test this epoch)
             if (lane == 0) {
@@ -660,7 +673,7 @@ __global__ __launch_bounds__(kFThreads, fast_waves_per_simd<THRU>()) void trk_fa
                 const double k_cf = rc.code_freq_chips, k_rcc = rc.rem_code_phase_chips;
                 const float k_rem = rc.rem_carr_phase_rad;
                 const int32_t k_len = rc.current_prn_length_samples;
-                epoch_loop(k, rc, nullptr);
+                epoch_loop(kp, rc, nullptr);
                 // State 4: epoch_post cannot change what the next epoch's correlation needs (the
                 // channel stays runnable — 4, or 3 for extended integration — on the same taps), so
                 // the next epoch is seeded now, before the lock test's outcome, and wave 1 derives
@@ -669,7 +682,7 @@ __global__ __launch_bounds__(kFThreads, fast_waves_per_simd<THRU>()) void trk_fa
                 const int64_t k_ifn = rc.if_num;
                 const double k_ifc = rc.if_cyc;
                 if (rc.state == 4) {
-                    epoch_consume(k, rc);
+                    epoch_consume(kp, rc);
                     make_seed(e + 1);
                     rc.epoch_start = es;  // epoch_post and the record still describe this epoch
                     seeded = true;
@@ -690,10 +703,10 @@ __global__ __launch_bounds__(kFThreads, fast_waves_per_simd<THRU>()) void trk_fa
                     rc.if_cyc = k_ifc;
                     cancel = seeded;
                 }
-                epoch_post(k, rc, taps, pdata, r, locked, dr);
+                epoch_post(kp, rc, taps, pdata, r, locked, dr);
             }
             GNSSHIP_FSTAMP(e, 24);
-            epoch_finish(k, rc, r, !seeded);  // (a stopped channel consumes nothing either way)
+            epoch_finish(kp, rc, r, !seeded);  // (a stopped channel consumes nothing either way)
             if (!seeded)
                 make_seed(e + 1);  // wave 1 derives the next epoch while the records go out
             else if (!cancel)

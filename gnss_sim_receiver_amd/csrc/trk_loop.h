@@ -197,6 +197,67 @@ __device__ __forceinline__ const SymSync& syncset(const TrkParams& k, const TrkC
 __device__ __forceinline__ const SymSync& syncset(const TrkParams& k, const RChan& c) { return k.sync[uni(c.geo)]; }
 __device__ __forceinline__ const SymSync& syncset(const TrkParams& k, const LoopRegs& c) { return k.sync[c.geo]; }
 
+// The parameters one channel's loop reads, as register values for a whole run (the fast kernel's
+// control wave): inside the epoch loop every TrkParams member is otherwise a dependent scalar load on
+// the epoch's critical chain.  The member names are TrkParams's, so the loop templates read either;
+// the channel's symbol-sync profile and its wide / narrow loop sets are selected once (a channel's
+// geo profile is fixed from start_tracking on), the secondary-code bit tables stay in memory.
+struct KFastConf {
+    double fs_in;
+    uint32_t pull_in_time_s, bit_synchronization_time_limit_s, smoother_length;
+    int32_t enable_fll_pull_in, enable_fll_steady_state, carrier_aiding;
+    float slope, y_intercept, early_late_space_chips;
+};
+struct SyncView {
+    int32_t symbols_per_bit, secondary, secondary_len, data_secondary_len, extend;
+    float T_ext;
+    const uint32_t* secondary_bits;
+    const uint32_t* data_secondary_bits;
+};
+struct KFast {
+    KFastConf conf;
+    double code_chip_rate, carrier_freq, code_period, if_step_rad;
+    int64_t if_mod, fs_int;
+    int32_t code_length_chips, veml, track_pilot, fp_order, has_if;
+    float spc_n;
+    LoopSet ls_w, ls_n;  // the wide set and this channel's narrow set (k.ls[0], k.ls[1 + geo])
+    SyncView sv;         // k.sync[geo]
+};
+__device__ __forceinline__ KFast make_kfast(const TrkParams& k, int geo)
+{
+    KFast f;
+    f.conf.fs_in = k.conf.fs_in;
+    f.conf.pull_in_time_s = k.conf.pull_in_time_s;
+    f.conf.bit_synchronization_time_limit_s = k.conf.bit_synchronization_time_limit_s;
+    f.conf.smoother_length = k.conf.smoother_length;
+    f.conf.enable_fll_pull_in = k.conf.enable_fll_pull_in;
+    f.conf.enable_fll_steady_state = k.conf.enable_fll_steady_state;
+    f.conf.carrier_aiding = k.conf.carrier_aiding;
+    f.conf.slope = k.conf.slope;
+    f.conf.y_intercept = k.conf.y_intercept;
+    f.conf.early_late_space_chips = k.conf.early_late_space_chips;
+    f.code_chip_rate = k.code_chip_rate;
+    f.carrier_freq = k.carrier_freq;
+    f.code_period = k.code_period;
+    f.if_step_rad = k.if_step_rad;
+    f.if_mod = k.if_mod;
+    f.fs_int = k.fs_int;
+    f.code_length_chips = k.code_length_chips;
+    f.veml = k.veml;
+    f.track_pilot = k.track_pilot;
+    f.fp_order = k.fp_order;
+    f.has_if = k.has_if;
+    f.spc_n = k.spc_n;
+    const int g = uni(geo);
+    f.ls_w = k.ls[0];
+    f.ls_n = k.ls[1 + g];
+    const SymSync& s = k.sync[g];
+    f.sv = SyncView{s.symbols_per_bit, s.secondary, s.secondary_len, s.data_secondary_len, s.extend, s.T_ext, s.secondary_bits, s.data_secondary_bits};
+    return f;
+}
+__device__ __forceinline__ LoopSet loopset(const KFast& k, const RChan& c) { return uni(c.narrow) ? k.ls_n : k.ls_w; }
+__device__ __forceinline__ const SyncView& syncset(const KFast& k, const RChan&) { return k.sv; }
+
 // The members cn0_and_tracking_lock_status owns (prompt buffer, smoothers, fail counters, CN0 and
 // lock test) and the sign history live in memory for both channel forms.
 __device__ __forceinline__ TrkChannel& mem(TrkChannel& c) { return c; }
@@ -409,8 +470,8 @@ __device__ float loop_filter_apply(const TrkParams& k, TrkChannel& c, float x)
 // Tracking_loop_filter::apply (tracking_loop_filter.cc:58-84) on the logical-order rings: the same
 // products in the same order (outputs[(idx+ii)%4] ≡ lfo[ii] before the insert, inputs[(idx'+ii)%4] ≡
 // lfi[ii] after it).
-template <class C>
-__device__ float loop_filter_apply(const TrkParams& k, C& c, float x)
+template <class K, class C>
+__device__ float loop_filter_apply(const K& k, C& c, float x)
 {
     const LoopSet& q = loopset(k, c);
     float result = 0.0f;
@@ -430,8 +491,8 @@ __device__ float loop_filter_apply(const TrkParams& k, C& c, float x)
     return result;
 }
 
-template <class C>
-__device__ float carrier_filter(const TrkParams& k, C& c, float fll, float pll, float T)
+template <class K, class C>
+__device__ float carrier_filter(const K& k, C& c, float fll, float pll, float T)
 {
     const LoopSet& q = loopset(k, c);
     if (k.fp_order == 3) {
@@ -447,8 +508,8 @@ __device__ float carrier_filter(const TrkParams& k, C& c, float fll, float pll, 
     return e;
 }
 
-template <class C>
-__device__ void run_dll_pll(const TrkParams& k, C& c)
+template <class K, class C>
+__device__ void run_dll_pll(const K& k, C& c)
 {
     double disc;
     if (c.cloop)
@@ -512,8 +573,8 @@ __device__ double smoothed_rate(const TrkChannel& c, const TrkHist& h, const dou
     return (cp2 - cp1) / samples;
 }
 
-template <class C>
-__device__ void update_tracking_vars(const TrkParams& k, C& c, TrkHist* h)
+template <class K, class C>
+__device__ void update_tracking_vars(const K& k, C& c, TrkHist* h)
 {
     const double fs = k.conf.fs_in;
     const double T_chip = 1.0 / c.code_freq_chips;
@@ -553,8 +614,8 @@ __device__ void update_tracking_vars(const TrkParams& k, C& c, TrkHist* h)
 
 __device__ __forceinline__ int bit_at(const uint32_t* bits, int i) { return (bits[i >> 5] >> (i & 31)) & 1; }
 
-template <class C>
-__device__ void push_sign(const TrkParams& k, C& c, float prompt_re)
+template <class K, class C>
+__device__ void push_sign(const K& k, C& c, float prompt_re)
 {
     const int cap = syncset(k, c).secondary_len;
     const uint32_t neg = prompt_re < 0.0f ? 1u : 0u;
@@ -572,8 +633,8 @@ __device__ void push_sign(const TrkParams& k, C& c, float prompt_re)
     }
 }
 
-template <class C>
-__device__ bool acquire_secondary(const TrkParams& k, C& c)
+template <class K, class C>
+__device__ bool acquire_secondary(const K& k, C& c)
 {
     int corr = 0;
     const uint32_t* bits = mem(c).sign_bits;
@@ -621,8 +682,8 @@ __device__ void zero_accu(C& c)
 }
 
 // log_data (:1376-1466) at epoch start nir, after update_tracking_vars.
-template <class C>
-__device__ void log_data(const TrkParams& k, const C& c, const float* taps, const float* pdata, uint64_t nir, gnsship_trk_dump_record* d)
+template <class K, class C>
+__device__ void log_data(const K& k, const C& c, const float* taps, const float* pdata, uint64_t nir, gnsship_trk_dump_record* d)
 {
     if (!d) return;
     const int eo = k.veml ? 2 : 0;
@@ -678,8 +739,8 @@ __device__ __forceinline__ int next_mod(int i, int n)
     return v < n ? v : (v == n ? 0 : v % n);
 }
 
-template <class C>
-__device__ double epoch_pre(const TrkParams& k, C& c, const float* taps, const float* pdata, gnsship_trk_epoch& rec, TrkHist* h,
+template <class K, class C>
+__device__ double epoch_pre(const K& k, C& c, const float* taps, const float* pdata, gnsship_trk_epoch& rec, TrkHist* h,
     gnsship_trk_dump_record* dump)
 {
     const uint64_t nir = c.epoch_start;
@@ -759,8 +820,8 @@ __device__ double epoch_pre(const TrkParams& k, C& c, const float* taps, const f
     return k.code_period * static_cast<double>(syncset(k, c).extend);
 }
 
-template <class C>
-__device__ __forceinline__ void epoch_loop(const TrkParams& k, C& c, TrkHist* h)
+template <class K, class C>
+__device__ __forceinline__ void epoch_loop(const K& k, C& c, TrkHist* h)
 {
     GNSSHIP_TRK_LOOP_STAMP(9);
     run_dll_pll(k, c);
@@ -771,8 +832,8 @@ __device__ __forceinline__ void epoch_loop(const TrkParams& k, C& c, TrkHist* h)
 
 // After epoch_pre returned a coherent time: the rest of state 2 / 4 given the lock outcome (epoch_loop
 // has run iff locked).
-template <class C>
-__device__ void epoch_post(const TrkParams& k, C& c, const float* taps, const float* pdata, gnsship_trk_epoch& rec, bool locked,
+template <class K, class C>
+__device__ void epoch_post(const K& k, C& c, const float* taps, const float* pdata, gnsship_trk_epoch& rec, bool locked,
     gnsship_trk_dump_record* dump)
 {
     const uint64_t nir = c.epoch_start;
@@ -830,12 +891,12 @@ __device__ void epoch_post(const TrkParams& k, C& c, const float* taps, const fl
     if (syncset(k, c).extend > 1) c.state = 3;  // next coherent integration cycle
 }
 
-template <class C>
-__device__ __forceinline__ void advance_if(const TrkParams& k, C& c, int32_t consumed);
+template <class K, class C>
+__device__ __forceinline__ void advance_if(const K& k, C& c, int32_t consumed);
 
 // consume_each (:2061) and the IF phase of the consumed samples.
-template <class C>
-__device__ __forceinline__ void epoch_consume(const TrkParams& k, C& c)
+template <class K, class C>
+__device__ __forceinline__ void epoch_consume(const K& k, C& c)
 {
     c.nitems_read = c.epoch_start + static_cast<uint64_t>(c.current_prn_length_samples);
     advance_if(k, c, c.current_prn_length_samples);
@@ -843,8 +904,8 @@ __device__ __forceinline__ void epoch_consume(const TrkParams& k, C& c)
 
 // The record's loop outputs and consume_each (:2061); false when the channel stopped (loss of lock).
 // consume = false: the caller has already run epoch_consume (the fast kernel's early seed).
-template <class C>
-__device__ bool epoch_finish(const TrkParams& k, C& c, gnsship_trk_epoch& rec, bool consume = true)
+template <class K, class C>
+__device__ bool epoch_finish(const K& k, C& c, gnsship_trk_epoch& rec, bool consume = true)
 {
     if (c.pll_180) rec.flags |= 4;
     rec.code_phase_samples = c.rem_code_phase_samples;
@@ -862,8 +923,8 @@ __device__ bool epoch_finish(const TrkParams& k, C& c, gnsship_trk_epoch& rec, b
 }
 
 // The IF phase follows the consumed samples (gnsship_trk_conf::if_hz): if_num += if_mod·len (mod fs).
-template <class C>
-__device__ __forceinline__ void advance_if(const TrkParams& k, C& c, int32_t consumed)
+template <class K, class C>
+__device__ __forceinline__ void advance_if(const K& k, C& c, int32_t consumed)
 {
     if (!k.has_if) return;
     c.if_num = (c.if_num + k.if_mod * static_cast<int64_t>(consumed)) % k.fs_int;
@@ -872,14 +933,14 @@ __device__ __forceinline__ void advance_if(const TrkParams& k, C& c, int32_t con
 
 // do_correlation_step's carrier arguments with the IF fused in (include/gnsship.h if_hz): the
 // correlator wipes off IF + Doppler, the loop keeps the IF-free quantities.
-template <class C>
-__device__ __forceinline__ float corr_rem_carr(const TrkParams& k, const C& c)
+template <class K, class C>
+__device__ __forceinline__ float corr_rem_carr(const K& k, const C& c)
 {
     if (!k.has_if) return c.rem_carr_phase_rad;
     return static_cast<float>(fmod(static_cast<double>(c.rem_carr_phase_rad) + kTwoPi * c.if_cyc, kTwoPi));
 }
-template <class C>
-__device__ __forceinline__ float corr_phase_step(const TrkParams& k, const C& c)
+template <class K, class C>
+__device__ __forceinline__ float corr_phase_step(const K& k, const C& c)
 {
     return static_cast<float>(c.carrier_phase_step_rad + k.if_step_rad);  // + 0.0 without IF: exact
 }

@@ -91,7 +91,7 @@ __device__ __forceinline__ float replay2(float x, float c, float k2, int S, uint
 }
 
 template <bool STORE, bool NORM>
-__global__ void k2(float* out, unsigned long long* cyc, float dzr, float dzi, int S)
+__global__ void k2(float* out, unsigned long long* cyc, float dzr, float dzi, int S, int busy = 0, int prio = 0)
 {
     __shared__ uint64_t Zs[64 * 16 * 4];
     __shared__ int done;
@@ -100,13 +100,25 @@ __global__ void k2(float* out, unsigned long long* cyc, float dzr, float dzi, in
     __syncthreads();
     if (threadIdx.x >= 64) {  // pollers (launched with 256 threads): spin on LDS until wave 0 is done
         uint64_t acc = 0;
+        float f0 = threadIdx.x * 1e-3f, f1 = f0 + 1.0f, f2v = f0 + 2.0f, f3 = f0 + 3.0f;
         while (__hip_atomic_load(&done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0) {
-            acc += __hip_atomic_load(Zs + (threadIdx.x & 255), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            if (POLL_SLEEP >= 0) __builtin_amdgcn_s_sleep(POLL_SLEEP > 0 ? POLL_SLEEP : 0);
+            if (busy) {  // VALU-bound neighbours (the correlating waves' load): independent FMA chains
+#pragma unroll
+                for (int i = 0; i < 64; i++) {
+                    f0 = __builtin_fmaf(f0, 0.999f, 1e-3f);
+                    f1 = __builtin_fmaf(f1, 0.999f, 1e-3f);
+                    f2v = __builtin_fmaf(f2v, 0.999f, 1e-3f);
+                    f3 = __builtin_fmaf(f3, 0.999f, 1e-3f);
+                }
+            } else {
+                acc += __hip_atomic_load(Zs + (threadIdx.x & 255), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                if (POLL_SLEEP >= 0) __builtin_amdgcn_s_sleep(POLL_SLEEP > 0 ? POLL_SLEEP : 0);
+            }
         }
-        out[threadIdx.x] = static_cast<float>(acc);
+        out[threadIdx.x] = static_cast<float>(acc) + f0 + f1 + f2v + f3;
         return;
     }
+    if (prio) __builtin_amdgcn_s_setprio(3);
     float x = (lane & 1) ? (lane >> 1) * 1e-3f : 1.0f - (lane >> 1) * 1e-3f;
     const float c = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, dzr)));
     const float k2v = (lane & 1) ? dzi : -dzi;
@@ -140,7 +152,7 @@ int main()
     unsigned long long* cyc;
     if (hipMalloc(&out, 256 * sizeof(float)) != hipSuccess || hipMalloc(&cyc, sizeof(unsigned long long)) != hipSuccess) return 1;
     const int S = 63;  // C2: 4000 samples, 250 iterations, 4-iteration tasks
-    for (int v = 0; v < 10; v++) {
+    for (int v = 0; v < 13; v++) {
         unsigned long long best = ~0ull;
         for (int rep = 0; rep < 5; rep++) {
             switch (v) {
@@ -153,14 +165,18 @@ int main()
             case 6: hipLaunchKernelGGL((k2<true, false>), 1, 64, 0, 0, out, cyc, 0.99f, 0.14f, S); break;
             case 7: hipLaunchKernelGGL((k2<false, false>), 1, 64, 0, 0, out, cyc, 0.99f, 0.14f, S); break;
             case 8: hipLaunchKernelGGL((k2<true, true>), 1, 256, 0, 0, out, cyc, 0.99f, 0.14f, S); break;
-            default: hipLaunchKernelGGL((k2<false, false>), 1, 256, 0, 0, out, cyc, 0.99f, 0.14f, S); break;
+            case 9: hipLaunchKernelGGL((k2<false, false>), 1, 256, 0, 0, out, cyc, 0.99f, 0.14f, S, 0, 0); break;
+            case 10: hipLaunchKernelGGL((k2<true, true>), 1, 256, 0, 0, out, cyc, 0.99f, 0.14f, S, 1, 0); break;
+            case 11: hipLaunchKernelGGL((k2<true, true>), 1, 256, 0, 0, out, cyc, 0.99f, 0.14f, S, 1, 1); break;
+            default: hipLaunchKernelGGL((k2<true, true>), 1, 256, 0, 0, out, cyc, 0.99f, 0.14f, S, 0, 1); break;
             }
             unsigned long long c = 0;
             if (hipMemcpy(&c, cyc, sizeof(c), hipMemcpyDeviceToHost) != hipSuccess) return 2;
             if (c < best) best = c;
         }
         printf("%s stores %d normalise %d: %llu cycles for 250 iterations (%.1f / iteration)\n",
-            v < 4 ? "1-lane" : v < 8 ? "2-lane DPP" : "2-lane DPP + 3 polling waves", v == 8 || (v < 8 && (v & 1) == 0), v == 8 || (v < 8 && (v & 3) < 2),
+            v < 4 ? "1-lane" : v < 8 ? "2-lane DPP" : v < 10 ? "2-lane DPP + 3 polling waves" : v == 10 ? "2-lane DPP + 3 VALU-busy waves" : v == 11 ? "2-lane DPP + 3 VALU-busy waves, setprio 3" : "2-lane DPP + 3 polling waves, setprio 3",
+            v == 8 || v >= 10 || (v < 8 && (v & 1) == 0), v == 8 || v >= 10 || (v < 8 && (v & 3) < 2),
             best, best / 250.0);
     }
     return 0;

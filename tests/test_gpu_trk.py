@@ -37,7 +37,7 @@ def dev_conf(k, system):
     return c
 
 
-def compare(dev, ref, label=""):
+def compare(dev, ref, label="", cn0_tol=5e-3):
     d = dev[(dev["flags"] & 8) == 8]
     assert len(d) == len(ref), (label, len(d), len(ref))
     for f in ("sample_counter", "state", "prn_length_samples"):
@@ -46,7 +46,7 @@ def compare(dev, ref, label=""):
     np.testing.assert_allclose(d["carrier_doppler_hz"], ref["carrier_doppler_hz"], rtol=0, atol=2e-3, err_msg=label)
     np.testing.assert_allclose(d["code_freq_chips"], ref["code_freq_chips"], rtol=0, atol=2e-3, err_msg=label)
     np.testing.assert_allclose(d["rem_code_phase_chips"], ref["rem_code_phase_chips"], rtol=0, atol=1e-5, err_msg=label)
-    np.testing.assert_allclose(d["cn0_db_hz"], ref["cn0_db_hz"], rtol=0, atol=5e-3, err_msg=label)
+    np.testing.assert_allclose(d["cn0_db_hz"], ref["cn0_db_hz"], rtol=0, atol=cn0_tol, err_msg=label)
     np.testing.assert_allclose(d["carrier_phase_rads"], ref["carrier_phase_rads"], rtol=0, atol=1e-2, err_msg=label)
     pd = d["prompt_i"] + 1j * d["prompt_q"]
     pr = ref["prompt_i"] + 1j * ref["prompt_q"]
