@@ -548,7 +548,7 @@ __global__ __launch_bounds__(kFThreads, fast_waves_per_simd<THRU>()) void trk_fa
                 // lane 0 the phase, lane 1 the step, each the once-rounded double cos/sin (nco_math.h)
                 const float a = lane == 0 ? sd.rem_carr : -sd.step;
                 double sdn, cdn;
-                sincos(static_cast<double>(a), &sdn, &cdn);
+                sincos_f64_small(static_cast<double>(a), &sdn, &cdn);
                 const int sfi = __builtin_bit_cast(int, static_cast<float>(sdn)), cfi = __builtin_bit_cast(int, static_cast<float>(cdn));
                 const f2 p0 = f2{__builtin_bit_cast(float, __builtin_amdgcn_readlane(cfi, 0)), -__builtin_bit_cast(float, __builtin_amdgcn_readlane(sfi, 0))};
                 inc = f2{__builtin_bit_cast(float, __builtin_amdgcn_readlane(cfi, 1)), __builtin_bit_cast(float, __builtin_amdgcn_readlane(sfi, 1))};

@@ -154,10 +154,17 @@ def test_c4_share_8_e1_channels_closed_loop_matches_oracle(ctx):
     the data prompt, N = 100000 at 25 Msps, AVX rotator) on one engine, eight satellites in one
     signal, 90 epochs each (synchronised to the CS25 pilot code, state 4), every channel against the
     oracle loop on the same signal (long-integration oracle: double sums, once-rounded trig, as
-    run_pair)."""
+    run_pair).  Two checks: the correlator contract on the device's own arguments (every traced
+    channel-epoch re-run on the oracle correlator, taps and data prompt within 1e-5), and the loop
+    against the oracle loop — epoch boundaries, states and flags exact, observables at
+    test_gpu_c5_closed_loop.compare_if's bounds with bounded kicks: over 720 channel-epochs of eight
+    channels the two loops' NCOs (~1e-7 chip apart from their correlation sum orders) occasionally put
+    one of an epoch's 100000 samples on the other side of a chip edge (measured: PRN 19, epoch 4, a
+    1e-3 prompt step), which the loop then carries for a few tens of epochs."""
     import concurrent.futures as cf
 
     from gnss_sim_receiver_amd import signals
+    from test_gpu_c5_closed_loop import compare_if, trace_errors
 
     fs, epochs = 25e6, 90
     prns = [1, 5, 12, 19, 24, 30, 33, 36]
@@ -175,7 +182,9 @@ def test_c4_share_8_e1_channels_closed_loop_matches_oracle(ctx):
         ctx.set_code(61 + 2 * ch, s.code_data)
         starts.append((S.acq_delay_for(s, fs, "GAL", 0, first) + 0.2, s.doppler_hz + 15.0))
         trk.start(ch, 60 + 2 * ch, starts[-1][0], starts[-1][1], 0, first, data_code_id=61 + 2 * ch, prn=s.prn)
+    trk.set_trace(True)
     rec, rounds = trk.run(x, first, epochs)
+    tr = trk.trace(epochs)
     trk.close()
 
     def oracle(ch):
@@ -186,8 +195,6 @@ def test_c4_share_8_e1_channels_closed_loop_matches_oracle(ctx):
         refs = list(ex.map(oracle, range(len(sats))))
     for ch, ref in enumerate(refs):
         assert ref["state"][-1] == 4, (ch, np.bincount(ref["state"]))
-        # CN0 at 0.1 dB: at 50 dB-Hz over 4 ms the m2m4 estimator's m2 − |P|-power difference is a
-        # small residue of two large sums (lock_detectors.cc:90-112), so the ~1e-7 relative prompt
-        # differences of the two correlation orders come out ~1e-3 relative in CN0 (measured 0.049 dB
-        # on PRN 19 with seven other satellites in the signal); every other bound is compare()'s
-        compare(rec[:, ch], ref, f"C4 share channel {ch} (PRN {sats[ch].prn})", cn0_tol=0.1)
+        label = f"C4 share channel {ch} (PRN {sats[ch].prn})"
+        assert trace_errors(tr[:, ch], x, first, sats[ch].code, sats[ch].code_data, True) <= 1e-5, label
+        compare_if(rec[:, ch], ref, label, kick_frac=0.5, kick_scale=8.0)
