@@ -620,13 +620,14 @@ static int trk_enqueue(gnsship_trk* t, const void* src, int fmt, uint64_t buffer
         if (dump) HIP_TRY(ctx, hipMemsetAsync(t->dump_dev, 0, sizeof(gnsship_trk_dump_record) * nrec, ctx->stream));
         const int n_codes = static_cast<int>(ctx->codes_host.size());
         hipError_t e;
-        if (avx && trk_fast_supported(t->params, code_cap, nc))
+        const bool fast = avx && trk_fast_supported(t->params, code_cap, nc);
+        if (fast)
             e = launch_trk_fast(t->params_dev, t->params, t->chans_dev, nc, ctx->codes_dev, n_codes, code_cap, src, fmt, buffer_first_sample,
                 n_buffer_samples, max_rounds, out ? t->rec_dev : nullptr, dump ? t->dump_dev : nullptr, trace, t->ran_dev, ctx->stream);
         else
             e = launch_trk_persist(t->params_dev, t->params, t->chans_dev, nc, ctx->codes_dev, n_codes, code_cap, src, fmt, buffer_first_sample,
                 n_buffer_samples, max_rounds, out ? t->rec_dev : nullptr, dump ? t->dump_dev : nullptr, trace, t->ran_dev, avx, ctx->stream);
-        if (e != hipSuccess) return hip_fail(ctx, e, "launch_trk_persist");
+        if (e != hipSuccess) return hip_fail(ctx, e, fast ? "launch_trk_fast" : "launch_trk_persist");
     }
     for (int r = 0; r <= max_rounds && !persist; r++) {
         const int consume = r > 0 ? 1 : 0, emit = r < max_rounds ? 1 : 0;

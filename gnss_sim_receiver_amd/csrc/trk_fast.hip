@@ -1,6 +1,6 @@
 // trk_fast.hip — the closed DLL/PLL loop with the AVX rotator variant (the one volk_gnsssdr
 // dispatches on AVX hosts), one workgroup per channel for a whole run, organised around the epoch's
-// serial critical path.
+// serial critical path and bit-exact to the reference's correlator.
 //
 // dll_pll_veml_tracking::general_work (dll_pll_veml_tracking.cc:1728-2094) is a strictly serial
 // chain per channel: epoch k's correlations (do_correlation_step :1037-1062 →
@@ -9,28 +9,32 @@
 // update_tracking_vars :1189-1260), which sets epoch k+1's NCO.  The rate at which one channel
 // advances is 1 / (epoch latency), so this kernel shortens the chain itself:
 //
-//  * wave 0 is the control wave.  The channel's loop state lives in its registers for the whole
-//    run (RChan, trk_loop.h) — no LDS round trip per member.  After the correlation it sums the
-//    taps and runs the loop update; in state 4 it publishes the next epoch's correlator arguments
-//    (the seed) as soon as update_tracking_vars has set them — before the lock test's outcome, which
-//    a failed test cancels (the channel stops) — and only then finishes this epoch and writes its
-//    records (other states: after epoch_post);
-//  * wave 1 is the phasor wave: from the seed it derives cos/sin of the NCO phase and step (double,
-//    once rounded, in two lanes), dz = normalise(inc^16) and the 16 AVX lane starts, then replays
+//  * wave 1 is the phasor wave: from the seed it derives glibc's cos/sin of the NCO phase and step
+//    (glibc_sincosf.h, two lanes), dz = normalise(inc^16) and the 16 AVX lane starts, then replays
 //    the 16 phasor chains (z ← z·dz, the reference's float products, two lanes per chain with a DPP
 //    partner product) and stores each chain's phasor at every task start (G iterations, 8 for GPS
 //    at 4 Msps) with a plain LDS store — no fence, no flag: the phasor slot itself is the signal
-//    (all-ones NaN = not yet written; a phasor is never NaN);
-//  * waves 0, 2 and 3 correlate: groups of four tasks, lane (task, l) polls its slot, re-arms it for
-//    the next epoch, and continues chain l over the task's iterations with the same float
-//    products — every phasor bit-identical to u_avx's — correlating sample 16m + l at iteration
-//    m; groups are dealt statically (group sets 1, 2, 3), so sums are reproducible; wave 2 also
-//    runs the lock detectors (lock_status) on the LDS copy of their members while wave 0 runs
-//    run_dll_pll + update_tracking_vars speculatively, kept only when the lock test passes, as the
-//    reference runs them only then.
+//    (all-ones NaN = not yet written; a phasor is never NaN); then the N mod 16 tail's products;
+//  * waves 2 and 3 are the producers: groups of four tasks, lane (task, l) polls its slot, re-arms
+//    it, and continues chain l over the task's iterations with the same float products — every
+//    phasor bit-identical to u_avx's — forming at iteration m the sample product
+//    a = x[16m + l]·z_l(m) (_mm256_complexmul_ps rounding) and per tap the product a·code[tap]
+//    (_mm256_mul_ps), which it stores to an LDS product ring; a group's flag is set once its
+//    products have landed.  Wave 2 also runs the lock detectors (lock_status) beside wave 0's
+//    speculative loop update, kept only when the lock test passes, as the reference runs it;
+//  * wave 0 is the control wave and the accumulator.  Lane (l, r) keeps u_avx's accumulator of
+//    chain l for taps r and r + 4 and adds the products in iteration order (dotProdVal += c,
+//    :257-260) as the groups land, then combines the 16 chains exactly as u_avx does —
+//    ((d_k + d_{k+4}) + d_{k+8}) + d_{k+12}, then the four lanes serially from 0 (:279-291) — and
+//    the serial N mod 16 tail (:298-308): every tap bit-identical to the reference's.  The channel's
+//    loop state lives in its registers for the whole run (RChan, trk_loop.h); in state 4 it
+//    publishes the next epoch's correlator arguments (the seed) as soon as update_tracking_vars has
+//    set them — before the lock test's outcome, which a failed test cancels (the channel stops) —
+//    and only then finishes this epoch and writes its records (other states: after epoch_post).
 //
-// Epochs too long for the LDS task slots, the generic rotator, high_dyn and runs of more channels
-// than CUs stay on trk_persist.hip / the round-based loop.
+// Epochs too long for the LDS rings, the generic rotator, high_dyn and runs of more channels than
+// CUs stay on trk_persist.hip / the round-based loop.
+#include <algorithm>
 #include <cstdlib>
 
 #include "corr_device.h"
@@ -89,9 +93,10 @@ namespace {
 
 constexpr int kFThreads = 256;
 constexpr int kFWaves = kFThreads / kWave;
+constexpr int kFProducers = kFWaves - 2;  // waves 2.. form and store the products
 constexpr uint64_t kSlotEmpty = ~0ull;  // an unwritten phasor slot (NaN, NaN)
 
-// The epoch's correlation as the consumers need it (LDS, written by wave 0 before the barrier).
+// The epoch's correlation as the producers need it (LDS: the seed from wave 0, dz from wave 1).
 struct FJob {
     int64_t off;  // first sample of the epoch in the IF buffer
     float rem_code, code_step;  // do_correlation_step's rem_code_phase_chips·spc, code_phase_step_chips·spc
@@ -103,16 +108,18 @@ struct FJob {
 
 struct FShared {
     FJob job;
-    float red[4 * kFWaves][2 * (kMaxTaps + 1)];  // per 16-lane row
     float taps[2 * kMaxTaps + 2];  // the epoch's tap sums (+ the data prompt at 2·kMaxTaps), as epoch_pre reads them
     gnsship_trk_dump_record drec;  // log_data's record of the epoch
     double coh;       // the coherent time lock_status is called with (0: no lock test this epoch)
     int32_t seed_seq; // e + 1 once wave 0 published epoch e's NCO arguments (sh.job without dz)
-    int32_t job_seq;  // e + 1 once wave 1 completed epoch e's job (dz) — the correlating waves start
+    int32_t job_seq;  // e + 1 once wave 1 completed epoch e's job (dz) — the producers start
     int32_t pre_seq;  // e + 1 once wave 0 published this epoch's prompt / pull-in / coh
-    int32_t lock_seq; // e + 1 once wave 1 published the lock outcome
+    int32_t lock_seq; // e + 1 once wave 2 published the lock outcome
     int32_t locked;
+    int32_t tail_seq;   // e + 1 once wave 1 stored epoch e's N mod 16 tail products
+    int32_t acc_groups; // product groups the accumulator has consumed (counted over the run)
     int32_t pad;
+    f2 tailp[kAvxLanes][kMaxTaps + 1];  // the tail's products (sample 16M + j, tap), wave 1 → wave 0
 };
 
 // The job as wave-uniform values (scalar registers): read from LDS it would otherwise be per-lane,
@@ -154,7 +161,26 @@ __device__ __forceinline__ void wait_seq(int32_t* p, int need)
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
-// ---- wave 0: the AVX phasor replay ---------------------------------------------------------------
+// Product-ring flags: a producer's stores are complete (lgkmcnt) before its flag store; a reader
+// that saw the flag issues its loads after it (the loads follow the polling loop in program order,
+// and one wave's LDS operations are performed in order).
+__device__ __forceinline__ void lds_release_store(int32_t* p, int v)
+{
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_wait_eq(const int32_t* p, int v)
+{
+    while (__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != v) __builtin_amdgcn_s_sleep(0);
+    asm volatile("" ::: "memory");
+}
+__device__ __forceinline__ void lds_wait_ge(const int32_t* p, int v)
+{
+    while (__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < v) __builtin_amdgcn_s_sleep(0);
+    asm volatile("" ::: "memory");
+}
+
+// ---- wave 1: the AVX phasor replay ---------------------------------------------------------------
 // Chain l (< 16) starts at z_l = phase·inc^l at iteration 0 (:204-208).  Task t = iterations
 // [G·t, G·t + G) ∩ [0, M); its slot gets z_l at iteration G·t.  After iteration m's update the chains
 // normalise when m ≡ 0 (mod 64) (:265-272) — for G | 64 only a task's first iteration can be one.
@@ -239,41 +265,69 @@ __device__ __forceinline__ float pnormalise(float x)
 
 // Lanes 0-31.  `x` = this lane's component of z_l, k2 = (lane odd ? dz.im : −dz.im), c = dz.re
 // (uniform).  Returns the component of z_l after the last task's start (or at M with a tail).
-template <int G>
-__device__ __forceinline__ float fast_replay(float x, float c, float k2, int M, int S, int tail, uint64_t* __restrict__ Zs, int lane)
+// The slots form a ring of `rs` tasks (rs = S: one slot per task of the epoch, no ring).  In the
+// ring (SRING) a slot still holds task t − rs until its producer re-armed it; the replay reads the
+// state of the slot it writes next one task ahead and waits only if that slot is still taken.
+template <int G, bool SRING>
+__device__ __forceinline__ float fast_replay(float x, float c, float k2, int M, int S, int tail, uint64_t* __restrict__ Zs, int rs, int lane)
 {
     static_assert(G % 4 == 0 && G >= 4 && G <= 64, "task length");
     constexpr int kTB = 64 / G;  // tasks per 64-iteration block
     if (S <= 0) return x;
-    const int full = (S - 1) / kTB;  // whole blocks before the last task
     // the flat address of an LDS location carries its LDS offset in the low 32 bits
-    uint32_t off = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(Zs)) + 4u * static_cast<uint32_t>(lane);
+    const uint32_t base = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(Zs)) + 4u * static_cast<uint32_t>(lane);
+    uint32_t off = base;
     constexpr uint32_t kSlotRow = kAvxLanes * sizeof(uint64_t);
-    uint32_t* half = reinterpret_cast<uint32_t*>(Zs) + lane;
+    uint32_t* const half0 = reinterpret_cast<uint32_t*>(Zs) + lane;
+    int ts = 0;  // ring slot of the task
+    if constexpr (!SRING) {
+        const int full = (S - 1) / kTB;  // whole blocks before the last task
 #pragma unroll 1
-    for (int b = 0; b < full; b++) {
+        for (int b = 0; b < full; b++) {
 #pragma unroll
-        for (int q = 0; q < kTB; q++) {
-            if (q == 0)  // the block's first iteration normalises
+            for (int q = 0; q < kTB; q++) {
+                if (q == 0)  // the block's first iteration normalises
+                    x = ppow<G - 1>(pnormalise(pstep<1, true>(x, c, k2, off)), c, k2);
+                else
+                    x = ppow<G - 4>(pstep<4, true>(x, c, k2, off), c, k2);
+                off += kSlotRow;
+            }
+        }
+        if (full * kTB < S - 1) {  // a partial block: its first task normalises, the rest do not
+            x = ppow<G - 1>(pnormalise(pstep<1, true>(x, c, k2, off)), c, k2);
+            off += kSlotRow;
+#pragma unroll 1
+            for (int t = full * kTB + 1; t < S - 1; t++) {
+                x = ppow<G - 4>(pstep<4, true>(x, c, k2, off), c, k2);
+                off += kSlotRow;
+            }
+        }
+        ts = S - 1;
+    } else {
+        uint32_t next_state = ~0u;  // the slot's state read one task ahead
+#pragma unroll 1
+        for (int t = 0; t < S - 1; t++) {
+            if (t >= rs) {
+                uint32_t v = next_state;
+                while (v != ~0u) {
+                    __builtin_amdgcn_s_sleep(0);
+                    v = __hip_atomic_load(half0 + 2 * kAvxLanes * ts, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                }
+            }
+            const int tn = ts + 1 == rs ? 0 : ts + 1;
+            if (t + 1 >= rs) next_state = __hip_atomic_load(half0 + 2 * kAvxLanes * tn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (t % kTB == 0)
                 x = ppow<G - 1>(pnormalise(pstep<1, true>(x, c, k2, off)), c, k2);
             else
                 x = ppow<G - 4>(pstep<4, true>(x, c, k2, off), c, k2);
-            off += kSlotRow;
-            half += 2 * kAvxLanes;
+            ts = tn;
+            off = base + static_cast<uint32_t>(ts) * kSlotRow;
         }
+        if (S - 1 >= rs)
+            while (__hip_atomic_load(half0 + 2 * kAvxLanes * ts, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != ~0u) __builtin_amdgcn_s_sleep(0);
     }
-    if (full * kTB < S - 1) {  // a partial block: its first task normalises, the rest do not
-        x = ppow<G - 1>(pnormalise(pstep<1, true>(x, c, k2, off)), c, k2);
-        off += kSlotRow;
-        half += 2 * kAvxLanes;
-#pragma unroll 1
-        for (int t = full * kTB + 1; t < S - 1; t++) {
-            x = ppow<G - 4>(pstep<4, true>(x, c, k2, off), c, k2);
-            off += kSlotRow;
-            half += 2 * kAvxLanes;
-        }
-    }
-    __hip_atomic_store(half, __builtin_bit_cast(uint32_t, x), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);  // the last task: its consumers continue
+    // the last task: its producers continue it
+    __hip_atomic_store(half0 + 2 * kAvxLanes * ts, __builtin_bit_cast(uint32_t, x), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     if (tail > 0) {  // z_l(M) for the tail (chain 0's is what the reference keeps)
         for (int m = G * (S - 1); m < M; m++) {
             x = pstep<1, false>(x, c, k2, 0);
@@ -283,12 +337,16 @@ __device__ __forceinline__ float fast_replay(float x, float c, float k2, int M, 
     return x;
 }
 
-// ---- waves 1-3: the correlation -------------------------------------------------------------------
+// ---- waves 2-3: the products ----------------------------------------------------------------------
+// Product ring: `rg` groups of 4·G iterations; iteration m of group g lives at ring iteration
+// (g mod rg)·4G + (m − 4gG), element ((ring iteration · NTT) + tap) · 16 + chain.  Group tags count
+// over the run (gbase = epoch · n_groups), so no flag is ever re-armed.
 template <int FMT, int NT, bool DATA, bool IN_MARGIN, int G>
-__device__ __forceinline__ void fast_consume(const FJob& job, i4v span, const float* __restrict__ code0, const float* __restrict__ code1, int L,
-    uint64_t* __restrict__ Zs, int lane, int wave, f2 (&acc)[NT + 1])
+__device__ __forceinline__ void fast_produce(const FJob& job, i4v span, const float* __restrict__ code0, const float* __restrict__ code1, int L,
+    uint64_t* __restrict__ Zs, int rs, f2* __restrict__ P, int rg, int32_t* ready, const int32_t* acc_groups, int gbase, int lane, int pw, int pe)
 {
     constexpr int SB = sample_bytes<FMT>();
+    constexpr int NTT = NT + (DATA ? 1 : 0);
     constexpr int kB = G < 8 ? G : 8;  // iterations whose samples are in flight together
     const int M = job.M, S = job.S;
     const int n_groups = (S + 3) / 4;
@@ -298,8 +356,6 @@ __device__ __forceinline__ void fast_consume(const FJob& job, i4v span, const fl
 #pragma unroll
     for (int q = 0; q < NT; q++) shifts[q] = job.shifts[q];
     const int tl = lane >> 4, l = lane & (kAvxLanes - 1);
-    // the first kB samples of a group's lanes: issued one group ahead (the wave's next group), so a
-    // wave that trails the replay does not pay a memory round trip per group
     auto first_samples = [&](int g, f2 (&x)[kB]) {
         const int t = 4 * g + tl;
         const int n0 = kAvxLanes * G * (t < S ? t : 0) + l;
@@ -307,25 +363,33 @@ __device__ __forceinline__ void fast_consume(const FJob& job, i4v span, const fl
         for (int u = 0; u < kB; u++) x[u] = load_sample<FMT>(span, (n0 + kAvxLanes * u) * SB, 0);
     };
     f2 xa[kB], xb[kB], xn[kB];
-    if (wave - 1 < n_groups) first_samples(wave - 1, xa);
-    for (int g = wave - 1; g < n_groups; g += kFWaves - 1) {
+    if (pw < n_groups) first_samples(pw, xa);
+    int rslot = pw % rg;
+    const int rstep = kFProducers % rg;
+    for (int g = pw; g < n_groups; g += kFProducers) {
         const int t = 4 * g + tl;
         const bool active = t < S;
         const int m_lo = G * (active ? t : 0);
         const int cnt = active ? min(G, M - m_lo) : 0;
         const int n0 = kAvxLanes * m_lo + l;
-        const bool more = g + kFWaves - 1 < n_groups;
-        if (more) first_samples(g + kFWaves - 1, xn);  // in flight while polling and correlating this group
-        uint64_t* slot = Zs + (active ? t : 0) * kAvxLanes + l;
+        const bool more = g + kFProducers < n_groups;
+        if (more) first_samples(g + kFProducers, xn);  // in flight while polling and forming this group
+        // the ring group is free once the accumulator consumed its previous occupant
+        if (g >= rg) lds_wait_ge(acc_groups, gbase + g - rg + 1);
+        const int ts = active ? t % rs : 0;
+        uint64_t* slot = Zs + ts * kAvxLanes + l;
         uint64_t v = kSlotEmpty;
         if (active) {
             // written when neither 32-bit half is the sentinel any more (two replay lanes write it)
             while (static_cast<uint32_t>(v = load_slot(slot)) == ~0u || static_cast<uint32_t>(v >> 32) == ~0u) __builtin_amdgcn_s_sleep(0);
-            store_slot(slot, __builtin_bit_cast(f2, kSlotEmpty));  // re-armed for the next epoch
+            store_slot(slot, __builtin_bit_cast(f2, kSlotEmpty));  // re-armed for the next lap / epoch
         }
+        if (g == pw && pw == 0) GNSSHIP_FSTAMP(pe, 30);
+        if (g + kFProducers >= n_groups && pw == 1) GNSSHIP_FSTAMP(pe, 31);
         f2 z = active ? __builtin_bit_cast(f2, v) : f2{0.0f, 0.0f};
         const bool renorm = ((G * t) & 63) == 0;
         float fn = static_cast<float>(n0);  // (float)n, exact steps of 16 (n < 2^24)
+        f2* dst = P + (static_cast<size_t>(rslot * 4 * G + tl * G) * NTT) * kAvxLanes + l;
 #pragma unroll 1
         for (int i0 = 0; i0 < G; i0 += kB) {
             if (i0 + kB < G) {
@@ -336,19 +400,22 @@ __device__ __forceinline__ void fast_consume(const FJob& job, i4v span, const fl
             for (int u = 0; u < kB; u++) {
                 const int i = i0 + u;
                 const bool on = i < cnt;
-                const f2 r = on ? cmul_pk2(xa[u], z) : f2{0.0f, 0.0f};
+                // x·z_l (_mm256_complexmul_ps: ac − bd, ad + bc, each product rounded), then the
+                // chain's own update z·dz
+                const f2 a = on ? cmul_exact(xa[u], z) : f2{0.0f, 0.0f};
                 f2 zn = cmul_exact_s(z, dz);
                 if (i == 0 && renorm) zn = normalise_avx(zn);
                 z = zn;
                 const float sn = __fmul_rn(step, on ? fn : static_cast<float>(n0));
+                f2* d = dst + static_cast<size_t>(i) * NTT * kAvxLanes;
 #pragma unroll
                 for (int q = 0; q < NT; q++) {
                     const float c = code_at<IN_MARGIN>(code0, L, sn, shifts[q], rem);
-                    acc[q] = __builtin_elementwise_fma(r, f2{c, c}, acc[q]);
+                    d[q * kAvxLanes] = a * f2{c, c};  // _mm256_mul_ps (the sum is the accumulator's)
                 }
                 if constexpr (DATA) {
                     const float c = code_at<IN_MARGIN>(code1, L, sn, 0.0f, rem);
-                    acc[NT] = __builtin_elementwise_fma(r, f2{c, c}, acc[NT]);
+                    d[NT * kAvxLanes] = a * f2{c, c};
                 }
                 fn += static_cast<float>(kAvxLanes);
             }
@@ -357,32 +424,100 @@ __device__ __forceinline__ void fast_consume(const FJob& job, i4v span, const fl
                 for (int u = 0; u < kB; u++) xa[u] = xb[u];
             }
         }
+        if (lane == 0) lds_release_store(ready + rslot, gbase + g + 1);
         if (more) {
 #pragma unroll
             for (int u = 0; u < kB; u++) xa[u] = xn[u];
         }
+        rslot += rstep;
+        if (rslot >= rg) rslot -= rg;
     }
 }
 
-// The N mod 16 tail (:286-304) on wave 0: lane j < tail correlates sample 16M + j with T[j].
+// ---- wave 0: the accumulation in u_avx's order ----------------------------------------------------
+// Lane (l, r): chain l's accumulators of tap r (a0) and tap r + 4 (a1), both components.  Every
+// product is added in iteration order, exactly dotProdVal_{l/4}[tap] += c (:257-260).
+template <int NTT, int G>
+__device__ __forceinline__ void fast_accumulate(const f2* __restrict__ P, int rg, const int32_t* ready, int32_t* acc_groups, int gbase, int M, int S, int lane,
+    f2& a0, f2& a1, int pe)
+{
+    const int l = lane & (kAvxLanes - 1), r = lane >> 4;
+    const int r0 = r < NTT ? r : 0;                      // lanes without a tap read tap 0 (discarded)
+    const int r1 = (NTT > 4 && r + 4 < NTT) ? r + 4 : 0;
+    const int n_groups = (S + 3) / 4;
+    a0 = f2{0.0f, 0.0f};
+    a1 = f2{0.0f, 0.0f};
+    int rslot = 0;
+    for (int g = 0; g < n_groups; g++) {
+        lds_wait_eq(ready + rslot, gbase + g + 1);
+        if (g == 0) GNSSHIP_FSTAMP(pe, 28);
+        if (g == n_groups - 1) GNSSHIP_FSTAMP(pe, 29);
+        const int cnt = min(4 * G, M - 4 * G * g);
+        const f2* src0 = P + (static_cast<size_t>(rslot * 4 * G) * NTT + r0) * kAvxLanes + l;
+        const f2* src1 = P + (static_cast<size_t>(rslot * 4 * G) * NTT + r1) * kAvxLanes + l;
+        if (cnt == 4 * G) {
+            constexpr int kU = 8;  // loads in flight ahead of the dependent adds
+#pragma unroll
+            for (int j0 = 0; j0 < 4 * G; j0 += kU) {
+                f2 v0[kU], v1[kU];
+#pragma unroll
+                for (int u = 0; u < kU; u++) {
+                    v0[u] = src0[(j0 + u) * NTT * kAvxLanes];
+                    if constexpr (NTT > 4) v1[u] = src1[(j0 + u) * NTT * kAvxLanes];
+                }
+#pragma unroll
+                for (int u = 0; u < kU; u++) {
+                    a0 = a0 + v0[u];
+                    if constexpr (NTT > 4) a1 = a1 + v1[u];
+                }
+            }
+        } else {
+#pragma unroll 1
+            for (int j = 0; j < cnt; j++) {
+                a0 = a0 + src0[j * NTT * kAvxLanes];
+                if constexpr (NTT > 4) a1 = a1 + src1[j * NTT * kAvxLanes];
+            }
+        }
+        asm volatile("" ::: "memory");  // the group's loads are issued (and used) before it is released
+        if (lane == 0) lds_release_store(acc_groups, gbase + g + 1);
+        rslot = rslot + 1 == rg ? 0 : rslot + 1;
+    }
+}
+
+// u_avx's final combination of the 16 chains (:279-291), valid at lane 0 of each 16-lane row:
+// ((d_k + d_{k+4}) + d_{k+8}) + d_{k+12} for k = 0..3, then (((0 + s_0) + s_1) + s_2) + s_3.
+__device__ __forceinline__ float avx_chain_sum(float d)
+{
+    float s = d + dpp_mov<0x12C>(d);  // row_ror:12 — lane k reads lane k + 4
+    s = s + dpp_mov<0x128>(d);        // row_ror:8  — lane k + 8
+    s = s + dpp_mov<0x124>(d);        // row_ror:4  — lane k + 12
+    float r = 0.0f + s;
+    r = r + dpp_mov<0x101>(s);  // row_shl:1 — lane 0 reads lane 1
+    r = r + dpp_mov<0x102>(s);  // row_shl:2
+    r = r + dpp_mov<0x103>(s);  // row_shl:3
+    return r;
+}
+
+// The N mod 16 tail (:298-308) on wave 1: lane j < tail forms sample 16M + j's products with the
+// serial phasor T[j] (the accumulator adds them in order after the chain combination).
 template <int FMT, int NT, bool DATA, bool IN_MARGIN>
-__device__ __forceinline__ void fast_tail(const FJob& job, i4v span, const float* __restrict__ code0, const float* __restrict__ code1, int L, const f2* T, int lane,
-    f2 (&acc)[NT + 1])
+__device__ __forceinline__ void fast_tail_products(const FJob& job, i4v span, const float* __restrict__ code0, const float* __restrict__ code1, int L,
+    const f2* T, int lane, f2 (*tp)[kMaxTaps + 1])
 {
     constexpr int SB = sample_bytes<FMT>();
     if (lane >= job.tail) return;
     const int n = kAvxLanes * job.M + lane;
     const f2 x = load_sample<FMT>(span, n * SB, 0);
-    const f2 r = cmul_pk2(x, T[lane]);
+    const f2 wo = cmul_exact(x, T[lane]);  // wo = in_common[n] · _phase
     const float sn = __fmul_rn(job.code_step, static_cast<float>(n));
 #pragma unroll
     for (int q = 0; q < NT; q++) {
         const float c = code_at<IN_MARGIN>(code0, L, sn, job.shifts[q], job.rem_code);
-        acc[q] = __builtin_elementwise_fma(r, f2{c, c}, acc[q]);
+        tp[lane][q] = wo * f2{c, c};
     }
     if constexpr (DATA) {
         const float c = code_at<IN_MARGIN>(code1, L, sn, 0.0f, job.rem_code);
-        acc[NT] = __builtin_elementwise_fma(r, f2{c, c}, acc[NT]);
+        tp[lane][NT] = wo * f2{c, c};
     }
 }
 
@@ -408,12 +543,13 @@ __device__ __forceinline__ const auto& loop_params(const TrkParams& k, const KFa
         return kf;
 }
 
-template <int FMT, int NT, bool DATA, int G, bool THRU>
+template <int FMT, int NT, bool DATA, int G, bool THRU, bool SRING>
 __global__ __launch_bounds__(kFThreads, fast_waves_per_simd<THRU>()) void trk_fast_kernel(const TrkParams* __restrict__ pk, TrkChannel* __restrict__ chans,
     const CodeDesc* __restrict__ codes, int n_codes, const void* __restrict__ samples, uint64_t buf_first, int64_t buf_len, int max_rounds,
-    int n_chans, int code_cap_floats, int slot_cap, gnsship_trk_epoch* __restrict__ rec, gnsship_trk_dump_record* __restrict__ dump,
+    int n_chans, int code_cap_floats, int rs, int rg, gnsship_trk_epoch* __restrict__ rec, gnsship_trk_dump_record* __restrict__ dump,
     gnsship_trk_corr_trace* __restrict__ trace, int* __restrict__ ran_count)
 {
+    constexpr int NTT = NT + (DATA ? 1 : 0);
     extern __shared__ __attribute__((aligned(16))) float lds[];
     __shared__ TrkChannel sc;
     __shared__ FShared sh;
@@ -428,10 +564,14 @@ __global__ __launch_bounds__(kFThreads, fast_waves_per_simd<THRU>()) void trk_fa
         int* dst = reinterpret_cast<int*>(&sc);
         for (int i = tid; i < static_cast<int>(sizeof(TrkChannel) / 4); i += kFThreads) dst[i] = src[i];
     }
+    // dynamic LDS: code replica(s) | phasor slots (rs tasks) | product ring (rg groups) | ring flags
     float* code0 = lds;
     float* code1 = lds + code_cap_floats;
     uint64_t* Zs = reinterpret_cast<uint64_t*>(lds + (DATA ? 2 : 1) * code_cap_floats);
-    for (int i = tid; i < slot_cap * kAvxLanes; i += kFThreads) Zs[i] = kSlotEmpty;
+    f2* P = reinterpret_cast<f2*>(Zs + static_cast<size_t>(rs) * kAvxLanes);
+    int32_t* ready = reinterpret_cast<int32_t*>(P + static_cast<size_t>(rg) * 4 * G * NTT * kAvxLanes);
+    for (int i = tid; i < rs * kAvxLanes; i += kFThreads) Zs[i] = kSlotEmpty;
+    for (int i = tid; i < rg; i += kFThreads) ready[i] = 0;
     __syncthreads();
     if (tid == 0) {
         const bool tracking = sc.state == 2 || sc.state == 3 || sc.state == 4;
@@ -444,6 +584,8 @@ __global__ __launch_bounds__(kFThreads, fast_waves_per_simd<THRU>()) void trk_fa
         sh.job_seq = 0;
         sh.pre_seq = 0;
         sh.lock_seq = 0;
+        sh.tail_seq = 0;
+        sh.acc_groups = 0;
     }
     __syncthreads();
     if (skip) return;  // idle channel: its state is untouched
@@ -458,7 +600,7 @@ __global__ __launch_bounds__(kFThreads, fast_waves_per_simd<THRU>()) void trk_fa
     const int M = N / kAvxLanes;
     const int S = (M + G - 1) / G;
     const int tail = N - kAvxLanes * M;
-    constexpr int kOut = NT + (DATA ? 1 : 0);
+    const int n_groups = (S + 3) / 4;
     RChan rc;
     if (wave == 0) rchan_load(sc, &sc, rc);
     // wave 0's loop parameters in registers for the run (two workgroups per CU have no registers to
@@ -466,14 +608,13 @@ __global__ __launch_bounds__(kFThreads, fast_waves_per_simd<THRU>()) void trk_fa
     const KFast kf = make_kfast(k, sc.geo);
     const auto& kp = loop_params<THRU>(k, kf);
     // Wave roles (one channel per workgroup, its epochs a serial chain):
-    //   wave 0 — the control wave: the loop update on its register-resident channel (RChan), the
-    //            epoch records, and one third of the correlation;
+    //   wave 0 — the control wave: the accumulation in u_avx order, the loop update on its
+    //            register-resident channel (RChan) and the epoch records;
     //   wave 1 — the phasor wave: derives the epoch's phasors (cos/sin of the NCO phase and step,
     //            dz, the 16 lane starts) and replays them into the task slots, plus the N mod 16 tail;
-    //   waves 2, 3 — the other two thirds of the correlation; wave 2 also runs the lock detectors.
+    //   waves 2, 3 — the producers of the products; wave 2 also runs the lock detectors.
     // Wave 0 hands the next epoch's NCO arguments (the seed) to wave 1 as soon as epoch_post has
     // settled them, so the derive and the first tasks of epoch e + 1 overlap epoch e's record writes.
-    const int cw = wave == 0 ? 1 : wave;  // correlating waves 0, 2, 3 take group sets 1, 2, 3
     uint64_t seed_start = 0;              // wave 0: the epoch start the seed was made for
     // wave 0: the seed's per-run constants, read once (inside the epoch loop each TrkParams member is a
     // dependent scalar load on the chain)
@@ -530,9 +671,7 @@ __global__ __launch_bounds__(kFThreads, fast_waves_per_simd<THRU>()) void trk_fa
     int e_done = 0;
     bool cancel = false;  // wave 0: the current epoch was seeded before a lock test that failed
     for (int e = 0;; e++) {
-        f2 acc[NT + 1];
-#pragma unroll
-        for (int t = 0; t <= NT; t++) acc[t] = f2{0.0f, 0.0f};
+        const int gbase = e * n_groups;  // the epoch's first product-group tag - 1
         FJob job;
         if (wave == 1) {
             // ---- derive: the phasors of the seeded epoch ----
@@ -545,11 +684,11 @@ __global__ __launch_bounds__(kFThreads, fast_waves_per_simd<THRU>()) void trk_fa
             f2 zinit = f2{0.0f, 0.0f}, inc = f2{1.0f, 0.0f};
             if (sd.runnable) {
                 // (cos rem, −sin rem) and (cos −step, sin −step) (cpu_multicorrelator_real_codes.cc:115,123):
-                // lane 0 the phase, lane 1 the step, each the once-rounded double cos/sin (nco_math.h)
+                // lane 0 the phase, lane 1 the step, each glibc's cosf / sinf (glibc_sincosf.h)
                 const float a = lane == 0 ? sd.rem_carr : -sd.step;
-                double sdn, cdn;
-                sincos_f64_small(static_cast<double>(a), &sdn, &cdn);
-                const int sfi = __builtin_bit_cast(int, static_cast<float>(sdn)), cfi = __builtin_bit_cast(int, static_cast<float>(cdn));
+                float sfn, cfn;
+                glibc_sincosf(a, &sfn, &cfn);
+                const int sfi = __builtin_bit_cast(int, sfn), cfi = __builtin_bit_cast(int, cfn);
                 const f2 p0 = f2{__builtin_bit_cast(float, __builtin_amdgcn_readlane(cfi, 0)), -__builtin_bit_cast(float, __builtin_amdgcn_readlane(sfi, 0))};
                 inc = f2{__builtin_bit_cast(float, __builtin_amdgcn_readlane(cfi, 1)), __builtin_bit_cast(float, __builtin_amdgcn_readlane(sfi, 1))};
                 // dz = normalise(inc^16) by four squarings (:215-225)
@@ -575,10 +714,10 @@ __global__ __launch_bounds__(kFThreads, fast_waves_per_simd<THRU>()) void trk_fa
             GNSSHIP_FCLK(e, 12);
             if (!sd.runnable) break;
             job = uniform_job(sh.job);
-            const i4v span = sample_span<FMT>(samples, job.off, N);
             float xl = (lane & 1) ? zinit.y : zinit.x;
-            if (lane < 2 * kAvxLanes) xl = fast_replay<G>(xl, job.dz_re, (lane & 1) ? job.dz_im : -job.dz_im, M, S, tail, Zs, lane);
-            if (tail > 0) {  // the serial tail from normalise(z_0) after the loop (:286-304)
+            if (lane < 2 * kAvxLanes) xl = fast_replay<G, SRING>(xl, job.dz_re, (lane & 1) ? job.dz_im : -job.dz_im, M, S, tail, Zs, rs, lane);
+            if (tail > 0) {  // the serial tail from normalise(z_0) after the loop (:294-308)
+                const i4v span = sample_span<FMT>(samples, job.off, N);
                 const f2 zl = f2{__builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, xl), 0)),
                     __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, xl), 1))};
                 if (lane == 0) {
@@ -589,65 +728,85 @@ __global__ __launch_bounds__(kFThreads, fast_waves_per_simd<THRU>()) void trk_fa
                     }
                 }
                 if (job.in_margin)
-                    fast_tail<FMT, NT, DATA, true>(job, span, c0, c1, L, tailz, lane, acc);
+                    fast_tail_products<FMT, NT, DATA, true>(job, span, c0, c1, L, tailz, lane, sh.tailp);
                 else
-                    fast_tail<FMT, NT, DATA, false>(job, span, c0, c1, L, tailz, lane, acc);
+                    fast_tail_products<FMT, NT, DATA, false>(job, span, c0, c1, L, tailz, lane, sh.tailp);
+                if (lane == 0) publish_seq(&sh.tail_seq, e + 1);
             }
             GNSSHIP_FSTAMP(e, 2);
             GNSSHIP_FCLK(e, 13);
-        } else {
-            wait_seq(&sh.job_seq, e + 1);
-            job = uniform_job(sh.job);
-            if (!job.runnable) break;
+            continue;
+        }
+        wait_seq(&sh.job_seq, e + 1);
+        job = uniform_job(sh.job);
+        if (!job.runnable) break;
+        if (wave >= 2) {
             const i4v span = sample_span<FMT>(samples, job.off, N);
             if (job.in_margin)
-                fast_consume<FMT, NT, DATA, true, G>(job, span, c0, c1, L, Zs, lane, cw, acc);
+                fast_produce<FMT, NT, DATA, true, G>(job, span, c0, c1, L, Zs, rs, P, rg, ready, &sh.acc_groups, gbase, lane, wave - 2, e);
             else
-                fast_consume<FMT, NT, DATA, false, G>(job, span, c0, c1, L, Zs, lane, cw, acc);
-            GNSSHIP_FSTAMP(e, 2 + cw);  // 3, 4, 5: each correlating wave done
-        }
-        // DPP row sums only (no cross-row shuffle through LDS): the first lane of each 16-lane row
-        // stores its row's sums; wave 0 adds the rows after the barrier
-        {
-            f2 rs[kOut];
-#pragma unroll
-            for (int t = 0; t < kOut; t++) rs[t] = f2{row_sum(acc[t].x), row_sum(acc[t].y)};
-            if ((lane & 15) == 0) {
-                f2* dst = reinterpret_cast<f2*>(sh.red[4 * wave + (lane >> 4)]);
-#pragma unroll
-                for (int t = 0; t < kOut; t++) dst[t] = rs[t];
-            }
-        }
-        __syncthreads();  // C: every row's tap sums are in LDS
-        if (wave == 0) {
-            GNSSHIP_FSTAMP(e, 6);
-            GNSSHIP_FCLK(e, 14);
-            if (cancel) {
-                // the epoch seeded speculatively before the last lock test failed: the channel stopped
-                // there (state 0), so nothing of this epoch is kept — no lock test, no record — and
-                // the seed for the next one says "not runnable", which ends every wave's loop
-                cancel = false;
+                fast_produce<FMT, NT, DATA, false, G>(job, span, c0, c1, L, Zs, rs, P, rg, ready, &sh.acc_groups, gbase, lane, wave - 2, e);
+            GNSSHIP_FSTAMP(e, 1 + wave);  // 3, 4: each producer done
+            if (wave == 2) {
+                // cn0_and_tracking_lock_status (:972-1029) on the LDS copy of its members, beside the loop update
+                wait_seq(&sh.pre_seq, e + 1);
+                const double coh = sh.coh;
                 if (lane == 0) {
-                    sh.coh = 0.0;
-                    publish_seq(&sh.pre_seq, e + 1);
+                    GNSSHIP_TRK_LOOP_STAMP(8);
+                    sh.locked = (coh > 0.0 && !lock_status(k, sc, coh)) ? 0 : 1;
+                    GNSSHIP_TRK_LOOP_STAMP(26);
+                    publish_seq(&sh.lock_seq, e + 1);
                 }
-                make_seed(e + 1);
-                continue;
             }
-            // tap sums over the rows in row order (lane v sums value v; wave 1's rows hold only the
-            // N mod 16 tail), the 16 row values loaded together first; the data prompt at 2·kMaxTaps
-            float* taps = sh.taps;
-            if (lane < 2 * kOut) {
-                const int t = lane >> 1, c = lane & 1;
-                float v[4 * kFWaves];
-#pragma unroll
-                for (int w = 0; w < 4 * kFWaves; w++) v[w] = sh.red[w][lane];
-                float sum = 0.0f;
-#pragma unroll
-                for (int w = 0; w < 4 * kFWaves; w++)
-                    if (w / 4 != 1 || job.tail > 0) sum += v[w];
-                taps[((DATA && t == NT) ? 2 * kMaxTaps : 2 * t) + c] = sum;
+            continue;
+        }
+        // ---- wave 0: the epoch's taps in u_avx's order ----
+        {
+            f2 a0, a1;
+            GNSSHIP_FSTAMP(e, 27);
+            fast_accumulate<NTT, G>(P, rg, ready, &sh.acc_groups, gbase, M, S, lane, a0, a1, e);
+            GNSSHIP_FSTAMP(e, 5);
+            f2 t0 = f2{avx_chain_sum(a0.x), avx_chain_sum(a0.y)};
+            f2 t1 = f2{0.0f, 0.0f};
+            if constexpr (NTT > 4) t1 = f2{avx_chain_sum(a1.x), avx_chain_sum(a1.y)};
+            const int r = lane >> 4;
+            if (job.tail > 0) {  // the serial tail, sample by sample (:298-308)
+                wait_seq(&sh.tail_seq, e + 1);
+                for (int j = 0; j < job.tail; j++) {
+                    t0 = t0 + sh.tailp[j][r < NTT ? r : 0];
+                    if constexpr (NTT > 4) t1 = t1 + sh.tailp[j][r + 4 < NTT ? r + 4 : 0];
+                }
             }
+            if ((lane & 15) == 0) {
+                if (r < NTT) {
+                    const int o = (DATA && r == NT) ? 2 * kMaxTaps : 2 * r;
+                    sh.taps[o] = t0.x;
+                    sh.taps[o + 1] = t0.y;
+                }
+                if (NTT > 4 && r + 4 < NTT) {
+                    const int o = (DATA && r + 4 == NT) ? 2 * kMaxTaps : 2 * (r + 4);
+                    sh.taps[o] = t1.x;
+                    sh.taps[o + 1] = t1.y;
+                }
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        }
+        GNSSHIP_FSTAMP(e, 6);
+        GNSSHIP_FCLK(e, 14);
+        if (cancel) {
+            // the epoch seeded speculatively before the last lock test failed: the channel stopped
+            // there (state 0), so nothing of this epoch is kept — no lock test, no record — and
+            // the seed for the next one says "not runnable", which ends every wave's loop
+            cancel = false;
+            if (lane == 0) {
+                sh.coh = 0.0;
+                publish_seq(&sh.pre_seq, e + 1);
+            }
+            make_seed(e + 1);
+            continue;
+        }
+        {
+            const float* taps = sh.taps;
             GNSSHIP_FSTAMP(e, 16);
             const float* pdata = DATA ? taps + 2 * kMaxTaps : taps;
             gnsship_trk_epoch r{};
@@ -735,16 +894,6 @@ __global__ __launch_bounds__(kFThreads, fast_waves_per_simd<THRU>()) void trk_fa
             e_done = e + 1;
             GNSSHIP_FSTAMP(e, 7);
             GNSSHIP_FCLK(e, 15);
-        } else if (wave == 2) {
-            // cn0_and_tracking_lock_status (:972-1029) on the LDS copy of its members, beside the loop update
-            wait_seq(&sh.pre_seq, e + 1);
-            const double coh = sh.coh;
-            if (lane == 0) {
-                GNSSHIP_TRK_LOOP_STAMP(8);
-                sh.locked = (coh > 0.0 && !lock_status(k, sc, coh)) ? 0 : 1;
-                GNSSHIP_TRK_LOOP_STAMP(26);
-                publish_seq(&sh.lock_seq, e + 1);
-            }
         }
     }
     if (wave == 0 && lane == 0) {
@@ -771,90 +920,106 @@ extern "C" int gnsship_debug_trk_fast_profile(void* dev_buf)
 namespace gnsship {
 #endif
 
-// Task length G (iterations per phasor slot) and the LDS bytes of the dynamic region (codes + slots):
-// the shortest task of at least kFastMinG iterations whose slots fit the budget (longer epochs take
-// longer tasks).  8 rather than 4: half the slot stores and asm-block boundaries on the replay chain
-// for four more iterations on the last task (C2, profiling build: 8.24 -> 8.00 us per epoch).  0 when
-// even 64-iteration tasks do not fit.
-constexpr int kFastMinG = 8;
-static size_t fast_lds(const TrkParams& p, int code_cap_floats, int n_chans, int* g_out, int* slots_out)
+// The LDS plan of a run: task length G (iterations per phasor slot), the phasor-slot ring (rs tasks;
+// rs = S: one slot per task of the epoch) and the product ring (rg groups of 4 tasks; rg = n_groups:
+// the whole epoch).  G = 8 (half the slot stores and asm-block boundaries of G = 4 on the replay
+// chain, C2 profiling build: 8.24 -> 8.00 us per epoch); the whole epoch's slots and products when
+// they fit, otherwise a product ring of as many groups as fit (at least 2), with the slots in a ring
+// of 16 groups when the whole epoch's slots leave too little room.  `bytes` 0: no plan fits.
+struct FastPlan {
+    size_t bytes = 0;
+    int G = 8, rs = 0, rg = 0;
+};
+constexpr int kFastG = 8;
+constexpr int kFastSlotRingGroups = 16;
+static FastPlan fast_plan(const TrkParams& p, int code_cap_floats, int n_chans)
 {
+    FastPlan f;
     const int N = static_cast<int>(p.conf.vector_length);
     const int M = N / kAvxLanes;
+    const int G = kFastG;
+    const int S = std::max(1, (M + G - 1) / G);
+    const int n_groups = (S + 3) / 4;
+    const int ntt = p.n_taps + (p.jobs_per_channel > 1 ? 1 : 0);
     const size_t codes = static_cast<size_t>(p.jobs_per_channel > 1 ? 2 : 1) * code_cap_floats * sizeof(float);
+    const size_t slot_b = kAvxLanes * sizeof(uint64_t);
+    const size_t group_b = static_cast<size_t>(4 * G) * ntt * kAvxLanes * 2 * sizeof(float) + sizeof(int32_t);
     // more channels than CUs: two workgroups per CU share its LDS
-    const size_t budget = n_chans > 256 ? 72 * 1024 : kTrkPersistMaxLds;
-    for (int G = kFastMinG; G <= 64; G *= 2) {
-        const int S = (M + G - 1) / G;
-        const size_t bytes = codes + static_cast<size_t>(S > 0 ? S : 1) * kAvxLanes * sizeof(uint64_t);
-        if (bytes <= budget) {
-            if (g_out) *g_out = G;
-            if (slots_out) *slots_out = S > 0 ? S : 1;
-            return bytes;
+    size_t budget = n_chans > 256 ? 72 * 1024 : kTrkPersistMaxLds;
+    if (const char* env = std::getenv("GNSSHIP_TRK_FAST_LDS"))  // tests: a smaller budget forces the rings
+        budget = std::min(budget, static_cast<size_t>(std::atol(env)) * 1024);
+    auto fit = [&](int rs) -> int {  // product groups that fit beside `rs` slots (0: fewer than 2)
+        const size_t used = codes + static_cast<size_t>(rs) * slot_b;
+        if (used >= budget) return 0;
+        const int rg = static_cast<int>(std::min<size_t>((budget - used) / group_b, static_cast<size_t>(n_groups)));
+        return rg >= std::min(2, n_groups) ? rg : 0;
+    };
+    int rs = S, rg = fit(S);
+    // the slot ring must hold at least 4 tasks per product group (a producer passed the ring's
+    // back-pressure before it polls a slot, so the slot's previous lap is consumed)
+    if (rg < n_groups && S > 4 * kFastSlotRingGroups) {
+        const int rg2 = std::min(fit(4 * kFastSlotRingGroups), kFastSlotRingGroups);
+        if (rg2 > rg) {
+            rs = 4 * kFastSlotRingGroups;
+            rg = rg2;
         }
     }
-    return 0;
+    if (rg == 0) return f;
+    f.G = G;
+    f.rs = rs;
+    f.rg = rg;
+    f.bytes = codes + static_cast<size_t>(rs) * slot_b + static_cast<size_t>(rg) * group_b;
+    return f;
 }
 
 bool trk_fast_supported(const TrkParams& p, int code_cap_floats, int n_chans)
 {
     if (!trk_persist_supports(p) || p.conf.rotator != GNSSHIP_ROTATOR_AVX || p.conf.high_dyn) return false;
+    if (p.n_taps + (p.jobs_per_channel > 1 ? 1 : 0) > 2 * 4) return false;  // the accumulator's two taps per lane row
     if (const char* env = std::getenv("GNSSHIP_TRK_FAST")) {  // A/B against trk_persist.hip
         if (env[0] == '0') return false;
-        if (env[0] == '1') return fast_lds(p, code_cap_floats, n_chans, nullptr, nullptr) > 0;
+        if (env[0] == '1') return fast_plan(p, code_cap_floats, n_chans).bytes > 0;
     }
     // More channels than CUs: channel-epochs per second, not epoch latency, is what counts, and
     // trk_persist.hip's four equal correlating waves sustain more of them (measured at 65536
     // channels: 76.6 M vs 64.8 M channel-epochs/s)
     if (n_chans > 256) return false;
-    return fast_lds(p, code_cap_floats, n_chans, nullptr, nullptr) > 0;
+    return fast_plan(p, code_cap_floats, n_chans).bytes > 0;
 }
 
 hipError_t launch_trk_fast(const TrkParams* params_dev, const TrkParams& params, TrkChannel* chans, int n_chans, const CodeDesc* codes, int n_codes,
     int code_cap_floats, const void* samples, int fmt, uint64_t buf_first, int64_t buf_len, int max_rounds, gnsship_trk_epoch* rec,
     gnsship_trk_dump_record* dump, gnsship_trk_corr_trace* trace, int* ran_count, hipStream_t stream)
 {
-    int G = 0, slots = 0;
-    size_t lds = fast_lds(params, code_cap_floats, n_chans, &G, &slots);
-    if (lds == 0) return hipErrorInvalidValue;
-    if (const char* env = std::getenv("GNSSHIP_TRK_FAST_G")) {  // measurement: a longer task than the shortest that fits
-        const int g = std::atoi(env);
-        if (g > G && g <= 64 && (g & (g - 1)) == 0) {
-            const int M = static_cast<int>(params.conf.vector_length) / kAvxLanes;
-            G = g;
-            slots = std::max(1, (M + G - 1) / G);
-            lds = static_cast<size_t>(params.jobs_per_channel > 1 ? 2 : 1) * code_cap_floats * sizeof(float) + static_cast<size_t>(slots) * kAvxLanes * sizeof(uint64_t);
-        }
-    }
+    const FastPlan f = fast_plan(params, code_cap_floats, n_chans);
+    if (f.bytes == 0) return hipErrorInvalidValue;
+    const int N = static_cast<int>(params.conf.vector_length);
+    const int S = std::max(1, (N / kAvxLanes + f.G - 1) / f.G);
+    const bool sring = f.rs < S;
     const bool data = params.jobs_per_channel > 1;
     bool thru = n_chans > 256;
     if (const char* env = std::getenv("GNSSHIP_TRK_THRU")) thru = env[0] == '1';
     const int nt = params.n_taps;
     dim3 grid(n_chans), block(kFThreads);
-#define GNSSHIP_FAST(F, NTV, DV, GV)                                                                                                              \
-    do {                                                                                                                                        \
-        auto kfn = thru ? trk_fast_kernel<F, NTV, DV, GV, true> : trk_fast_kernel<F, NTV, DV, GV, false>;                                        \
-        hipError_t e0 = hipFuncSetAttribute(reinterpret_cast<const void*>(kfn), hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)); \
-        if (e0 != hipSuccess) return e0;                                                                                                        \
-        hipLaunchKernelGGL(kfn, grid, block, lds, stream, params_dev, chans, codes, n_codes, samples, buf_first, buf_len, max_rounds, n_chans,   \
-            code_cap_floats, slots, rec, dump, trace, ran_count);                                                                               \
+#define GNSSHIP_FAST(F, NTV, DV, SR)                                                                                                               \
+    do {                                                                                                                                         \
+        auto kfn = thru ? trk_fast_kernel<F, NTV, DV, kFastG, true, SR> : trk_fast_kernel<F, NTV, DV, kFastG, false, SR>;                        \
+        hipError_t e0 = hipFuncSetAttribute(reinterpret_cast<const void*>(kfn), hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(f.bytes)); \
+        if (e0 != hipSuccess) return e0;                                                                                                         \
+        hipLaunchKernelGGL(kfn, grid, block, f.bytes, stream, params_dev, chans, codes, n_codes, samples, buf_first, buf_len, max_rounds, n_chans, \
+            code_cap_floats, f.rs, f.rg, rec, dump, trace, ran_count);                                                                           \
     } while (0)
-#define GNSSHIP_FAST_G(F, NTV, DV)                          \
-    do {                                                    \
-        switch (G) {                                        \
-        case 4: GNSSHIP_FAST(F, NTV, DV, 4); break;         \
-        case 8: GNSSHIP_FAST(F, NTV, DV, 8); break;         \
-        case 16: GNSSHIP_FAST(F, NTV, DV, 16); break;       \
-        case 32: GNSSHIP_FAST(F, NTV, DV, 32); break;       \
-        default: GNSSHIP_FAST(F, NTV, DV, 64); break;       \
-        }                                                   \
+#define GNSSHIP_FAST_R(F, NTV, DV)                        \
+    do {                                                  \
+        if (sring) GNSSHIP_FAST(F, NTV, DV, true);        \
+        else GNSSHIP_FAST(F, NTV, DV, false);             \
     } while (0)
-#define GNSSHIP_FAST_F(F)                                   \
-    do {                                                    \
-        if (nt == 3 && !data) GNSSHIP_FAST_G(F, 3, false);  \
-        else if (nt == 5 && !data) GNSSHIP_FAST_G(F, 5, false); \
-        else if (nt == 5 && data) GNSSHIP_FAST_G(F, 5, true); \
-        else return hipErrorInvalidValue;                   \
+#define GNSSHIP_FAST_F(F)                                    \
+    do {                                                     \
+        if (nt == 3 && !data) GNSSHIP_FAST_R(F, 3, false);   \
+        else if (nt == 5 && !data) GNSSHIP_FAST_R(F, 5, false); \
+        else if (nt == 5 && data) GNSSHIP_FAST_R(F, 5, true); \
+        else return hipErrorInvalidValue;                    \
     } while (0)
     switch (fmt) {
     case GNSSHIP_FMT_CF32: GNSSHIP_FAST_F(GNSSHIP_FMT_CF32); break;
@@ -863,7 +1028,7 @@ hipError_t launch_trk_fast(const TrkParams* params_dev, const TrkParams& params,
     default: return hipErrorInvalidValue;
     }
 #undef GNSSHIP_FAST_F
-#undef GNSSHIP_FAST_G
+#undef GNSSHIP_FAST_R
 #undef GNSSHIP_FAST
     return hipGetLastError();
 }

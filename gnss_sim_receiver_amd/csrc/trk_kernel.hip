@@ -17,9 +17,8 @@
 //   cn0_and_tracking_lock_status :972-1029, run_dll_pll :1065-1152, update_tracking_vars
 //   :1189-1260, save_correlation_results :1262-1350, acquire_secondary :925-970,
 //   general_work states 2 (:1789-1932) and 4 (:1971-2028).
-// The job derivation repeats derive_job (gnsship_abi.hip) on the device: the phasors are the
-// double-precision cos/sin rounded to float (nco_math.h), glibc's cosf/sinf in ~99 % of epochs and
-// one ulp away otherwise.
+// The job derivation repeats derive_job (gnsship_abi.hip) on the device, the phasors with glibc's
+// cosf / sinf restated (glibc_sincosf.h), as the host path calls them.
 #include <cmath>
 
 #include "anchor_replay.h"
@@ -36,8 +35,11 @@ __device__ void fill_job(DevJob& j, const TrkParams& k, const TrkChannel& c, int
     const float spcf = static_cast<float>(k.code_samples_per_chip);
     const float rem_carr = corr_rem_carr(k, c);
     const float step = corr_phase_step(k, c);
-    const float p0r = cos_f32_rn(rem_carr), p0i = -sin_f32_rn(rem_carr);
-    const float incr = cos_f32_rn(-step), inci = sin_f32_rn(-step);
+    float sr, cr, si, ci;
+    glibc_sincosf(rem_carr, &sr, &cr);
+    glibc_sincosf(-step, &si, &ci);
+    const float p0r = cr, p0i = -sr;
+    const float incr = ci, inci = si;
     j.sample_offset = offset;
     j.n_samples = static_cast<int32_t>(k.conf.vector_length);
     j.code_id = code_id;
@@ -66,10 +68,13 @@ __device__ void fill_hd_job(HdJob& j, const TrkParams& k, const TrkChannel& c, i
     j.sample_offset = offset;
     j.n_samples = static_cast<int32_t>(k.conf.vector_length);
     j.n_taps = n_taps;
-    j.p0_re = cos_f32_rn(rem_carr);
-    j.p0_im = -sin_f32_rn(rem_carr);
-    j.inc_re = cos_f32_rn(-step);
-    j.inc_im = sin_f32_rn(-step);
+    float sr, cr, si, ci;
+    glibc_sincosf(rem_carr, &sr, &cr);
+    glibc_sincosf(-step, &si, &ci);
+    j.p0_re = cr;
+    j.p0_im = -sr;
+    j.inc_re = ci;
+    j.inc_im = si;
     j.dtheta = atan2(static_cast<double>(j.inc_im), static_cast<double>(j.inc_re));
     j.log_mag_inc = static_cast<float>(log(hypot(static_cast<double>(j.inc_re), static_cast<double>(j.inc_im))));
     j.rate_arg = atan2f(sinf(-rate), cosf(-rate));

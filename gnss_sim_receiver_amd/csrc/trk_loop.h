@@ -35,7 +35,7 @@ constexpr double kHalfPi = kGnssPi / 2.0;
 // fll_diff_atan + phase_unwrap (tracking_discriminators.cc:27-41, 68-76)
 __device__ double fll_diff_atan(const float* s1, const float* s2, double t1, double t2)
 {
-    double d = static_cast<double>(__fsub_rn(atanf(__fdiv_rn(s2[1], s2[0])), atanf(__fdiv_rn(s1[1], s1[0]))));
+    double d = static_cast<double>(__fsub_rn(glibc_atanf(__fdiv_rn(s2[1], s2[0])), glibc_atanf(__fdiv_rn(s1[1], s1[0]))));
     if (isnan(d)) d = 0.0;
     if (d >= kHalfPi)
         d -= kGnssPi;
@@ -513,9 +513,9 @@ __device__ void run_dll_pll(const K& k, C& c)
 {
     double disc;
     if (c.cloop)
-        disc = (c.p[0] != 0.0f) ? static_cast<double>(atanf(__fdiv_rn(c.p[1], c.p[0]))) : 0.0;
+        disc = (c.p[0] != 0.0f) ? static_cast<double>(glibc_atanf(__fdiv_rn(c.p[1], c.p[0]))) : 0.0;
     else
-        disc = static_cast<double>(atan2f(c.p[1], c.p[0]));  // gr::fast_atan2f restated as atan2f
+        disc = static_cast<double>(glibc_atan2f(c.p[1], c.p[0]));  // gr::fast_atan2f restated as atan2f (glibc_atanf.h)
     c.carr_phase_error_hz = disc / kTwoPi;
     // d_current_correlation_time_s: the code period, or extend × code period once extended
     const float T = c.narrow ? syncset(k, c).T_ext : static_cast<float>(k.code_period);
@@ -541,8 +541,8 @@ __device__ void run_dll_pll(const K& k, C& c)
         const double s = early + late;
         c.code_error_chips = (s == 0.0) ? 0.0 : (early - late) / s;
     } else {
-        const double pe = static_cast<double>(hypotf(c.e[0], c.e[1]));
-        const double pl = static_cast<double>(hypotf(c.l[0], c.l[1]));
+        const double pe = static_cast<double>(hypotf_glibc(c.e[0], c.e[1]));
+        const double pl = static_cast<double>(hypotf_glibc(c.l[0], c.l[1]));
         const double s = pe + pl;
         const float slope = k.conf.slope;
         const float norm = __fdiv_rn(__fsub_rn(k.conf.y_intercept, __fmul_rn(slope, c.spc)), slope);
@@ -689,11 +689,11 @@ __device__ void log_data(const K& k, const C& c, const float* taps, const float*
     const int eo = k.veml ? 2 : 0;
     const float* prompt = k.track_pilot ? pdata : taps + eo + 2;
     const double fs = k.conf.fs_in;
-    d->abs_VE = k.veml ? hypotf(c.ve[0], c.ve[1]) : 0.0f;
-    d->abs_E = hypotf(c.e[0], c.e[1]);
-    d->abs_P = hypotf(c.p[0], c.p[1]);
-    d->abs_L = hypotf(c.l[0], c.l[1]);
-    d->abs_VL = k.veml ? hypotf(c.vl[0], c.vl[1]) : 0.0f;
+    d->abs_VE = k.veml ? hypotf_glibc(c.ve[0], c.ve[1]) : 0.0f;
+    d->abs_E = hypotf_glibc(c.e[0], c.e[1]);
+    d->abs_P = hypotf_glibc(c.p[0], c.p[1]);
+    d->abs_L = hypotf_glibc(c.l[0], c.l[1]);
+    d->abs_VL = k.veml ? hypotf_glibc(c.vl[0], c.vl[1]) : 0.0f;
     d->prompt_I = prompt[0];
     d->prompt_Q = prompt[1];
     d->PRN_start_sample_count = nir + static_cast<uint64_t>(c.current_prn_length_samples);

@@ -442,15 +442,14 @@ __global__ __launch_bounds__(kPThreads, persist_waves_per_simd<THRU>()) void trk
             if (lane == 0) g_prof_epoch = e;
 #endif
             // the epoch's two phasors (cpu_multicorrelator_real_codes.cc:115,123), lane 0: rem_carr,
-            // lane 1: −step, each as the once-rounded double cos/sin (nco_math.h)
+            // lane 1: −step, each glibc's cosf / sinf (glibc_sincosf.h)
             const float a = lane == 0 ? corr_rem_carr(k, sc) : -corr_phase_step(k, sc);
             if (lane == 0) {
                 ep.trace_rem_carr = corr_rem_carr(k, sc);
                 ep.trace_step = corr_phase_step(k, sc);
             }
-            double sd, cd;
-            sincos(static_cast<double>(a), &sd, &cd);
-            const float sf = static_cast<float>(sd), cf = static_cast<float>(cd);
+            float sf, cf;
+            glibc_sincosf(a, &sf, &cf);
             const f2 p0 = f2{__shfl(cf, 0, kWave), -__shfl(sf, 0, kWave)};
             const f2 inc = f2{__shfl(cf, 1, kWave), __shfl(sf, 1, kWave)};
             if (lane == 0) {

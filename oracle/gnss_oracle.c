@@ -527,8 +527,7 @@ int orc_multicorrelator_real_codes_ex(float* corr_out, const float* sig_in, cons
         code_phase_rate_step_chips, signal_length_samples, scratch, accum_f64);
 }
 
-/* flags as gnsship_corr_job::flags: bit0 high_dyn, bit1 AVX rotator variant; bit2 (test-only):
- * phasors from double cos/sin rounded to float instead of glibc cosf/sinf. */
+/* flags as gnsship_corr_job::flags: bit0 high_dyn, bit1 AVX rotator variant. */
 int orc_multicorrelator_real_codes(float* corr_out, const float* sig_in, const float* local_code, int code_length_chips,
     const float* shifts_chips, int n_correlators, int flags, float rem_carrier_phase_in_rad, float phase_step_rad,
     float phase_rate_step_rad, float rem_code_phase_chips, float code_phase_step_chips, float code_phase_rate_step_chips,
@@ -587,12 +586,6 @@ static int orc_multicorrelator_impl(float* corr_out, const float* sig_in, const 
             n_correlators, (unsigned)signal_length_samples);
     float phase[2] = {cosf(rem_carrier_phase_in_rad), -sinf(rem_carrier_phase_in_rad)};
     float inc_re = cosf(-phase_step_rad), inc_im = sinf(-phase_step_rad);
-    if (flags & 4) { /* test-only: the double-rounded-once trig of the device loop (nco_math.h) */
-        phase[0] = (float)cos((double)rem_carrier_phase_in_rad);
-        phase[1] = -(float)sin((double)rem_carrier_phase_in_rad);
-        inc_re = (float)cos((double)-phase_step_rad);
-        inc_im = (float)sin((double)-phase_step_rad);
-    }
     if (high_dyn) {
         const float rr = cosf(-phase_rate_step_rad), ri = sinf(-phase_rate_step_rad);
         orc_high_dynamic_rotator_dot_prod_impl(corr_out, sig_in, inc_re, inc_im, rr, ri, phase, codes, n_correlators,

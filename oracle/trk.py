@@ -36,7 +36,7 @@ class OrcTrkConf(ctypes.Structure):
         ("early_late_space_narrow_chips", ctypes.c_float), ("very_early_late_space_narrow_chips", ctypes.c_float),
         ("enable_fll_pull_in", ctypes.c_int32), ("enable_fll_steady_state", ctypes.c_int32),
         ("high_dyn", ctypes.c_int32), ("smoother_length", ctypes.c_uint32), ("rotator_avx", ctypes.c_int32),
-        ("accum_f64", ctypes.c_int32), ("cr_trig", ctypes.c_int32), ("pad_if", ctypes.c_int32), ("if_hz", ctypes.c_double),
+        ("accum_f64", ctypes.c_int32), ("pad_trig", ctypes.c_int32), ("pad_if", ctypes.c_int32), ("if_hz", ctypes.c_double),
     ]
 
 

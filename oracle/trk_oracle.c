@@ -346,8 +346,7 @@ typedef struct {
                                  dispatches on an AVX host, volk_gnsssdr_rank_archs.c), 0: generic */
     int32_t accum_f64;        /* test-only: the same float products summed in double (long epochs, see
                                  orc_rotator_dot_prod_acc64) */
-    int32_t cr_trig;          /* test-only: phasors from double cos/sin rounded to float (the device loop's
-                                 nco_math.h) instead of glibc cosf/sinf */
+    int32_t pad_trig;         /* unused (layout) */
     int32_t pad_if;
     /* Carrier IF of the signal in the buffer [Hz], whole Hz (with a whole-Hz fs_in).  The reference removes
      * it ahead of the channels (InputFilter.IF, freq_xlating_fir_filter; conf/gnss-sdr_BDS_B3I_GPS_L1_CA_
@@ -921,7 +920,7 @@ int orc_trk_run(const orc_trk_conf* k, orc_trk_channel* c, const float* samples,
 {
     const int vl = (int)k->vector_length;
     float* scratch = (float*)malloc((size_t)5 * (size_t)vl * sizeof(float));
-    const int cflags = (k->high_dyn ? 1 : 0) | (k->rotator_avx ? 2 : 0) | (k->cr_trig ? 4 : 0); /* gnsship_corr_job flags (+ test bit) */
+    const int cflags = (k->high_dyn ? 1 : 0) | (k->rotator_avx ? 2 : 0); /* gnsship_corr_job flags */
     int e = 0;
     for (; e < max_epochs; e++) {
         if (c->state != 2 && c->state != 3 && c->state != 4) break;

@@ -21,7 +21,7 @@ def main():
     system = sys.argv[1] if len(sys.argv) > 1 else "GAL"
     avx = int(sys.argv[2]) if len(sys.argv) > 2 else 1
     epochs = 60 if system == "GAL" else 100
-    sat, k, x, stamp, first, delay, dop = S.sync(system, C.FS, epochs, f_if_hz=C.IF_OF[system], rotator_avx=avx, accum_f64=1, cr_trig=1, cn0=48.0)
+    sat, k, x, stamp, first, delay, dop = S.sync(system, C.FS, epochs, f_if_hz=C.IF_OF[system], rotator_avx=avx, accum_f64=1, cn0=48.0)
     raw = signals.to_ibyte(x)
     xf = raw.astype(np.float32).view(np.complex64)
     ctx = engine.Context(0)

@@ -2,11 +2,11 @@
 
     make prof && python scripts/trk_fast_profile.py [channels]
 
-Stamps (wall_clock64, 100 MHz) per channel-epoch, lane 0 of the stamping wave: 0 epoch start (wave 0),
-1 job derived, 2 replay done (wave 0), 3/4/5 correlating waves 1/2/3 done, 6 tap sums read (wave 0,
-after the barrier), 7 loop update + records done; 8 lock_status start (wave 1), 9 run_dll_pll start,
-10 its end, 11 update_tracking_vars end (wave 0).  The channels bit-synchronise first (state 4, as in
-bench.py)."""
+Stamps (wall_clock64, 100 MHz) per channel-epoch, lane 0 of the stamping wave: 0 derive start (wave 1),
+1 job published, 2 replay + tail done (wave 1), 3/4 producer waves 2/3 done, 5 accumulation done
+(wave 0), 6 taps combined and stored, 7 loop update + records done; 8 lock_status start (wave 2),
+9 run_dll_pll start, 10 its end, 11 update_tracking_vars end (wave 0).  The channels bit-synchronise
+first (state 4, as in bench.py)."""
 import ctypes
 import os
 import sys
@@ -58,13 +58,16 @@ def main():
     t = np.concatenate([t, nxt], axis=2)  # slot 32 = next epoch start
     v = t[:, 1:-1, :]
     print(f"{n_ch} channels: epoch period {us(np.median(np.diff(t[:, :, 0], axis=1))):.2f} us (median)")
-    rows = [("derive", 0, 1), ("derive -> replay done", 1, 2), ("derive -> wave1 corr done", 1, 3), ("derive -> wave2 corr done", 1, 4),
-            ("derive -> wave3 corr done", 1, 5), ("replay done -> sums read", 2, 6), ("sums read -> loop done", 6, 7),
-            ("  sums read -> run_dll_pll", 6, 9), ("  run_dll_pll", 9, 10), ("  update_tracking_vars", 10, 11),
-            ("  tracking_vars -> loop done", 11, 7), ("  lock_status start (wave 1) after sums", 6, 8), ("loop done -> next epoch", 7, 32),
-            ("  sums read -> tap sums", 6, 16), ("  tap sums -> epoch_pre done", 16, 17), ("  epoch_pre -> published", 17, 18),
-            ("  published -> run_dll_pll", 18, 9), ("  lock_status (wave 1)", 8, 26), ("  tracking_vars -> lock seen", 11, 19),
-            ("  lock seen -> epoch_post done", 19, 24), ("  epoch_finish", 24, 25), ("  epoch_finish -> loop done (records)", 25, 7)]
+    rows = [("derive", 0, 1), ("derive -> replay done", 1, 2), ("derive -> producer 2 done", 1, 3), ("derive -> producer 3 done", 1, 4),
+            ("derive -> accumulation done", 1, 5), ("replay done -> accumulation done", 2, 5), ("accumulation -> taps stored", 5, 6),
+            ("taps stored -> loop done", 6, 7), ("  taps -> run_dll_pll", 6, 9), ("  run_dll_pll", 9, 10), ("  update_tracking_vars", 10, 11),
+            ("  tracking_vars -> loop done", 11, 7), ("loop done -> next derive", 7, 32), ("  taps -> epoch_pre done", 16, 17),
+            ("  epoch_pre -> published", 17, 18), ("  published -> run_dll_pll", 18, 9), ("  lock_status (wave 2)", 8, 26),
+            ("  tracking_vars -> lock seen", 11, 19), ("  lock seen -> epoch_post done", 19, 24), ("  epoch_finish", 24, 25),
+            ("  epoch_finish -> loop done (records)", 25, 7), ("seed (tracking_vars) -> next derive start", 11, 32),
+            ("derive -> wave 0 starts accumulating", 1, 27), ("derive -> group 0 seen by wave 0", 1, 28), ("derive -> last group seen by wave 0", 1, 29),
+            ("derive -> producer 2 has group 0's slots", 1, 30), ("derive -> producer 3 has its last group's slots", 1, 31),
+            ("last group seen -> accumulation done", 29, 5)]
     for nm, a, b in rows:
         ok = (v[:, :, a] > 0) & (v[:, :, b] > 0)
         if not ok.any():

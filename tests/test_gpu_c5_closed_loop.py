@@ -6,22 +6,19 @@ NCO (gnsship_trk_conf::if_hz) and the oracle loop (oracle/trk_oracle.c, orc_trk_
 the same term, so every epoch of dll_pll_veml_tracking::general_work (:1728-2094) is compared.
 
 The int8 samples go to the device as they are (converted in the loads, no scaling, as IbyteToComplex,
-ibyte_to_complex.cc:39) and to the oracle converted to float.  Tolerances: test_gpu_trk.compare
-(exact epoch boundaries / states / flags, Doppler ≤ 2e-3 Hz, …).  E1 at N = 200000 is checked
-against the oracle's double-accumulated sums with once-rounded trig (test_gpu_trk_persist.run_pair's
-reasoning for N ≥ 1e5).
+ibyte_to_complex.cc:39) and to the oracle converted to float.
 
-With the IF in the NCO the phase step is ≈ 0.9 rad per sample, and one ulp of the float arguments the
-reference passes (phase_step_rad = (float)d_carrier_phase_step_rad, and phase_inc from cosf/sinf of it)
-turns the carrier phase by ≈ 3e-3 rad over 50000 samples.  So (1) the oracle takes the device's trig
-rounding (cr_trig: once-rounded double cos/sin; glibc's cosf/sinf are not correctly rounded) and sums
-its float products in double (accum_f64), and (2) two loops whose states differ by the ~1e-5 Hz that
-their correlation sums' rounding leaves occasionally round the float step one ulp apart, which the
-loop sees as a ≈ 3e-3 rad prompt phase step: Doppler and carrier phase are compared at 0.25 Hz /
-0.05 rad, the code frequency at 5e-2 Hz and the code phase at 2e-4 chips (the DLL filter sees the
-same phase-step kicks) here (epoch boundaries, states and flags stay exact), and the correlator itself is pinned at
-the contract's 1e-5 on the device's own arguments: every traced epoch (gnsship_trk_set_trace) re-run
-on the oracle correlator.
+With the IF in the NCO the phase step is ≈ 0.9 rad per sample, and one ulp of phase_inc turns the
+carrier by ≈ 3e-3 rad over 50000 samples: the phasors must be glibc's cosf / sinf exactly, which the
+engine reproduces (glibc_sincosf.h).  The AVX engine (trk_fast.hip) then equals the oracle: every
+traced epoch's taps equal the oracle correlator's on the same arguments, and every record field
+equals the oracle loop's (test_gpu_trk.compare_exact).  The generic-rotator engine (trk_persist.hip)
+sums in a tree; it is held to the correlator contract (1e-5 on its own arguments, against the
+oracle's double-accumulated sums at N ≥ 5e4, where the reference's serial float sum is itself ~1e-5
+from the exact sum of its products: measured 1.09e-5 between the tree and the serial sum on B1I) and, for the loop, to compare_if's bounds: two loops
+whose correlation sums differ by ~1e-7 now and then round the float step one ulp apart, a ≈ 3e-3 rad
+prompt phase step, so Doppler and carrier phase are compared at 0.25 Hz / 0.05 rad, the code
+frequency at 5e-2 Hz and the code phase at 2e-4 chips (epoch boundaries, states and flags exact).
 """
 import concurrent.futures as cf
 
@@ -32,7 +29,7 @@ from gnss_sim_receiver_amd import abi, engine, signals
 from oracle import trk as T
 
 import trk_scenarios as S
-from test_gpu_trk import dev_conf
+from test_gpu_trk import compare_exact, dev_conf
 
 pytestmark = pytest.mark.gpu
 TOL = 1e-5
@@ -88,8 +85,8 @@ def trace_errors(tr, xf, first, code, data_code, rotator_avx):
     tr = tr[tr["n_samples"] > 0]
     jobs = check_trace(tr, xf, first, [code])
     jobs["code_id"] = 0
-    jobs["flags"] = (A.JOB_ROTATOR_AVX if rotator_avx else 0) | 4  # 4: the oracle's once-rounded trig (cr_trig)
-    long_n = int(jobs["n_samples"][0]) >= 100000
+    jobs["flags"] = A.JOB_ROTATOR_AVX if rotator_avx else 0
+    long_n = int(jobs["n_samples"][0]) >= 50000
     ref = O.corr_batch(xf, jobs, [code], n_threads=8, accum_f64=long_n)
     worst = 0.0
     for j in range(len(jobs)):
@@ -110,6 +107,33 @@ def trace_errors(tr, xf, first, code, data_code, rotator_avx):
             scale = max(abs(dref[j, 0]), float(np.linalg.norm(xf[o:o + n].astype(np.complex128))) if long_n else 0.0)
             worst = max(worst, abs(got[j] - dref[j, 0]) / max(scale, 1e-30))
     return worst
+
+
+def trace_exact(tr, xf, first, code, data_code, label=""):
+    """Each traced channel-epoch of the AVX engine re-run on the oracle's u_avx correlator with the
+    device's own arguments: every tap (and the data prompt) equal, bit for bit."""
+    from gnss_sim_receiver_amd import abi as A
+    from oracle import oracle as O
+    tr = tr[tr["n_samples"] > 0]
+    jobs = check_trace(tr, xf, first, [code])
+    jobs["code_id"] = 0
+    jobs["flags"] = A.JOB_ROTATOR_AVX
+    ref = O.corr_batch(xf, jobs, [code], n_threads=8).astype(np.complex64)
+    t = int(jobs["n_taps"][0])
+    got = (tr["taps"][:, 0:2 * t:2] + 1j * tr["taps"][:, 1:2 * t:2]).astype(np.complex64)
+    bad = np.nonzero(np.any(got != ref[:, :t], axis=1))[0]
+    assert len(bad) == 0, (label, "taps differ in", len(bad), "of", len(jobs), "epochs; first", int(bad[0]), got[bad[0]], ref[bad[0], :t])
+    if data_code is not None:
+        dj = jobs.copy()
+        dj["n_taps"] = 1
+        dj["shifts_chips"] = 0.0
+        dref = O.corr_batch(xf, dj, [data_code], n_threads=8).astype(np.complex64)[:, 0]
+        dgot = (tr["data_prompt"][:, 0] + 1j * tr["data_prompt"][:, 1]).astype(np.complex64)
+        bad = np.nonzero(dgot != dref)[0]
+        assert len(bad) == 0, (label, "data prompt differs in", len(bad), "epochs; first", int(bad[0]), dgot[bad[0]], dref[bad[0]])
+    return len(jobs)
+
+
 FS = 50e6
 F_IF = 7.161e6
 IF_OF = {"GPS": F_IF, "GAL": F_IF, "BDS": -F_IF}
@@ -119,9 +143,8 @@ IF_OF = {"GPS": F_IF, "GAL": F_IF, "BDS": -F_IF}
 @pytest.mark.parametrize("system,epochs", [("GPS", 300), ("GAL", 60), ("BDS", 300)])
 def test_c5_channel_closed_loop_ibyte_if(ctx, system, epochs, avx):
     """One channel per system at 50 Msps, ibyte, IF fused into the NCO, both rotator variants."""
-    long_n = 1 if system == "GAL" else 0
     sat, k, x, stamp, first, delay, dop = S.sync(system, FS, epochs, f_if_hz=IF_OF[system], rotator_avx=1 if avx else 0,
-                                                 accum_f64=1, cr_trig=1, cn0=48.0)
+                                                 accum_f64=0 if avx else 1, cn0=48.0)
     raw = signals.to_ibyte(x)
     xf = raw.astype(np.float32).view(np.complex64)
     c = dev_conf(k, system)
@@ -137,9 +160,12 @@ def test_c5_channel_closed_loop_ibyte_if(ctx, system, epochs, avx):
     trk.close()
     ref = T.track(k, xf, sat.code, delay, dop, stamp, first, epochs, data_code=sat.code_data, buffer_first=first, prn=sat.prn)
     assert len(ref) == epochs and ref["state"][-1] in (3, 4), np.bincount(ref["state"])
-    compare_if(rec[:, 0], ref, f"C5 {system} avx={avx}")
-    # the correlations on the device's own arguments, every epoch, at the 1e-5 contract
-    assert trace_errors(tr, xf, first, sat.code, sat.code_data, avx) <= TOL
+    if avx:  # bit-exact: the taps on the device's own arguments, then the loop
+        trace_exact(tr, xf, first, sat.code, sat.code_data, f"C5 {system}")
+        compare_exact(rec[:, 0], ref, f"C5 {system} avx")
+    else:  # the correlations on the device's own arguments at the 1e-5 contract, the loop at compare_if
+        assert trace_errors(tr, xf, first, sat.code, sat.code_data, avx) <= TOL
+        compare_if(rec[:, 0], ref, f"C5 {system} generic")
     # the IF is wiped off: the loop holds the signal's Doppler (± the narrow-loop walk), not Doppler + IF
     assert np.all(np.abs(ref[-20:]["carrier_doppler_hz"] - sat.doppler_hz) < 200.0)
 
@@ -170,8 +196,8 @@ def c5_share_sky():
 def test_c5_share_engines_concurrent_match_oracle(ctx):
     """C5's per-GPU share in closed loop: three tracking engines (GPS N = 50000, E1 5 VEML + data prompt
     N = 200000, B1I N = 50000), each on its own context (stream) of the one GPU, launched together
-    over the same 50 Msps ibyte block (gnsship_trk_launch / _collect) — every channel against the
-    oracle loop, every epoch."""
+    over the same 50 Msps ibyte block (gnsship_trk_launch / _collect) — every channel's records equal
+    to the oracle loop's, every epoch."""
     sky = c5_share_sky()
     seconds = 0.3
     first = int(FS)
@@ -187,7 +213,7 @@ def test_c5_share_engines_concurrent_match_oracle(ctx):
     for system, sats in sky.items():
         cx = ctxs[system]
         vl = int(round(FS * T.SYSTEMS[system][2]))
-        k = T.conf(system, FS, vl, pull_in_time_s=0, if_hz=IF_OF[system], rotator_avx=1, accum_f64=1, cr_trig=1)
+        k = T.conf(system, FS, vl, pull_in_time_s=0, if_hz=IF_OF[system], rotator_avx=1)
         confs[system] = k
         trk = engine.DllPllVemlTracking(cx, dev_conf(k, system), len(sats))
         for ch, s in enumerate(sats):
@@ -215,7 +241,7 @@ def test_c5_share_engines_concurrent_match_oracle(ctx):
     states = {}
     for (system, ch), ref in refs.items():
         rec, done = got[system]
-        compare_if(rec[:, ch], ref, f"{system} ch{ch}")
+        compare_exact(rec[:, ch], ref, f"{system} ch{ch}")
         states.setdefault(system, []).append(int(ref["state"][-1]))
     # GPS and B1I synchronise within the block (preamble / NH code), E1 on CS25 after 25 epochs
     assert all(st in (3, 4) for st in states["GAL"]) and all(st in (3, 4) for st in states["BDS"]), states

@@ -5,19 +5,13 @@ u_avx, :155-316 — what volk dispatches on an x86 host with AVX), the bench's s
 the first sample (the 10 s pull-in over), run for 1100 epochs so that every channel spends ≥ 500
 epochs in state 4 (bit-synchronised, dll_pll_veml_tracking.cc:1971-2028).
 
-Two checks on the same run (the persistent fast kernel, trk_fast.hip):
-  * the correlator (the contract): every traced channel-epoch (gnsship_trk_set_trace: the arguments
-    the device correlated with and its tap sums) re-run on oracle.corr_batch with the same
-    arguments, taps within 1e-5 relative error;
-  * the loop: every channel's epoch records against the oracle loop (oracle/trk_oracle.c, the same
-    AVX correlator): epoch boundaries, states, flags and PRN lengths exact, the loop observables at
-    test_gpu_c5_closed_loop.compare_if's bounds.  At 45 dB-Hz over 1100 epochs the two loops'
-    correlation sums (tree vs serial float order, ~1e-7 apart) occasionally straddle the
-    two-quadrant atan's ±π/2 cut when the prompt's I is near 0, a one-epoch discriminator kick of
-    up to a few tenths of a Hz that the 35 Hz PLL then carries for a few epochs (measured: 15 % of
-    epochs of one channel beyond 2e-3 Hz, max 0.17 Hz; with 8-iteration tasks, whose different sum
-    order moves the kicks, one epoch of 1100 at 0.28 Hz), so the Doppler is held to 0.25 Hz here,
-    not 2e-3, on all but 1 % of the epochs, and to 1 Hz on those.
+Two checks on the same run (the persistent fast kernel, trk_fast.hip), both bit-exact:
+  * the correlator: every traced channel-epoch (gnsship_trk_set_trace: the arguments the device
+    correlated with and its tap sums) re-run on oracle.corr_batch (the u_avx restatement) with the
+    same arguments — every tap equal;
+  * the loop: every channel's epoch records equal the oracle loop's (oracle/trk_oracle.c, the same
+    AVX correlator, glibc trig and discriminators) — test_gpu_trk.compare_exact (CN0 to 1e-4 dB: the
+    device's log10f).
 """
 import concurrent.futures as cf
 
@@ -28,8 +22,8 @@ from gnss_sim_receiver_amd import abi, engine, signals
 from oracle import oracle as O
 from oracle import trk as T
 
-from test_gpu_trk import dev_conf
-from test_gpu_c5_closed_loop import compare_if
+from test_gpu_trk import compare_exact, dev_conf
+from test_gpu_c5_closed_loop import trace_exact
 
 pytestmark = pytest.mark.gpu
 
@@ -74,25 +68,9 @@ def test_headline_c2_avx_500_state4_epochs_match_oracle(ctx):
     for ch in range(N_CH):
         ref = refs[ch]
         assert np.count_nonzero(ref["state"] == 4) >= 500, (ch, np.bincount(ref["state"]))
-        compare_if(rec[:, ch], ref, f"C2 channel {ch}", kick_frac=0.01, kick_scale=4.0)
-    # the correlator on the device's own arguments, every channel-epoch
-    t = tr.reshape(-1)
-    t = t[t["n_samples"] > 0]
-    assert len(t) >= N_CH * 1000
-    jobs = np.zeros(len(t), abi.JOB_DTYPE)
-    jobs["sample_offset"] = t["sample_counter"].astype(np.int64) - lo
-    jobs["n_samples"] = t["n_samples"]
-    jobs["n_taps"] = t["n_taps"]
-    jobs["rem_carrier_phase_rad"] = t["rem_carrier_phase_rad"]
-    jobs["phase_step_rad"] = t["phase_step_rad"]
-    jobs["rem_code_phase_chips"] = t["rem_code_phase_samples"]
-    jobs["code_phase_step_chips"] = t["code_phase_step_samples"]
-    jobs["shifts_chips"][:, :5] = t["shifts"]
-    jobs["flags"] = abi.JOB_ROTATOR_AVX | 4  # 4: the oracle's once-rounded trig (cr_trig), as the device's
-    # code id: the channel of each trace row (rows are [epoch, channel] flattened, idle rows dropped)
-    ch_of = np.broadcast_to(np.arange(N_CH), tr.shape).reshape(-1)[tr.reshape(-1)["n_samples"] > 0]
-    jobs["code_id"] = ch_of
-    ref = O.corr_batch(x, jobs, [sats[ch].code for ch in range(N_CH)], n_threads=8)
-    got = t["taps"][:, 0:6:2] + 1j * t["taps"][:, 1:6:2]
-    worst = max(rel_err(got[j], ref[j, :3]) for j in range(len(jobs)))
-    assert worst <= TOL, worst
+        compare_exact(rec[:, ch], ref, f"C2 channel {ch}")
+    # the correlator on the device's own arguments, every channel-epoch, tap for tap
+    n = 0
+    for ch in range(N_CH):
+        n += trace_exact(tr[:, ch], x, lo, sats[ch].code, None, f"C2 channel {ch}")
+    assert n >= N_CH * 1000

@@ -3,8 +3,11 @@ loop (oracle/trk_oracle.c), for both volk_gnsssdr rotator variants the reference
 (generic, and u_avx/a_avx: volk_gnsssdr_32fc_32f_rotator_dot_prod_32fc_xn.h:155-316), and at the
 north_star's 25 Msps rates (GPS L1 C/A N = 25000, Galileo E1 N = 100000 — C3/C4's sampling rate).
 
-Tolerances are test_gpu_trk.compare's: exact epoch boundaries / states / flags, Doppler and code
-frequency ≤ 2e-3, remnant code phase ≤ 1e-5 chip, CN0 ≤ 5e-3 dB, prompt ≤ 1e-4 relative.
+The AVX variant runs trk_fast.hip, which reproduces u_avx's products and accumulation order, glibc's
+phasor trig and the discriminators' libm: its records equal the oracle loop's (test_gpu_trk.compare_exact,
+CN0 to 1e-4 dB).  The generic variant (trk_persist.hip, tree sums) is held to test_gpu_trk.compare's
+tolerances: exact epoch boundaries / states / flags, Doppler and code frequency ≤ 2e-3, remnant code
+phase ≤ 1e-5 chip, CN0 ≤ 5e-3 dB, prompt ≤ 1e-4 relative.
 """
 import os
 
@@ -15,24 +18,21 @@ from gnss_sim_receiver_amd import abi, engine
 from oracle import trk as T
 
 import trk_scenarios as S
-from test_gpu_trk import compare, dev_conf
+from test_gpu_trk import compare, compare_exact, dev_conf
 
 pytestmark = pytest.mark.gpu
 
 
 def run_pair(ctx, system, fs, epochs, avx, n_ch=2, **kw):
-    """One channel (index 1) synchronising to state 4 on the device and in the oracle.  At
-    N ≥ 1e5 the oracle sums its float products in double (accum_f64): the reference's serial float
-    sum is itself ~1e-5 off the exact sum there (DESIGN.md §4 'Long integrations'), and the loop
-    turns that into ~0.07 Hz of Doppler walk, so the device (tree sums) is held to the loop on the
-    exact sums of the same products.  Likewise a one-ulp difference in phase_inc (glibc's sinf is
-    not correctly rounded, and differs between its FMA and non-FMA builds) turns the phase by
-    N·6e-8 rad over a 1e5-sample epoch, so at N ≥ 1e5 the oracle's phasors come from the same
-    once-rounded double cos/sin as the device's (cr_trig); test_oracle_trk.py bounds the loop's
-    distance between the two trig choices."""
+    """One channel (index 1) synchronising to state 4 on the device and in the oracle.  Generic
+    rotator at N ≥ 1e5: the oracle sums its float products in double (accum_f64): the reference's
+    serial float sum is itself ~1e-5 off the exact sum there (DESIGN.md §4 'Long integrations'), and
+    the loop turns that into ~0.07 Hz of Doppler walk, so the device's tree sums are held to the loop
+    on the exact sums of the same products.  The AVX engine sums in the reference's own order and is
+    compared with the plain oracle."""
     vl = int(round(fs * T.SYSTEMS[system][2]))
-    long_n = 1 if vl >= 100000 else 0
-    sat, k, x, stamp, first, delay, dop = S.sync(system, fs, epochs, rotator_avx=1 if avx else 0, accum_f64=long_n, cr_trig=long_n, **kw)
+    long_n = 1 if (vl >= 100000 and not avx) else 0
+    sat, k, x, stamp, first, delay, dop = S.sync(system, fs, epochs, rotator_avx=1 if avx else 0, accum_f64=long_n, **kw)
     c = dev_conf(k, system)
     c.rotator = abi.ROTATOR_AVX if avx else abi.ROTATOR_GENERIC
     trk = engine.DllPllVemlTracking(ctx, c, n_ch)
@@ -50,7 +50,7 @@ def run_pair(ctx, system, fs, epochs, avx, n_ch=2, **kw):
 def test_avx_rotator_loop_matches_oracle(ctx, system, fs, epochs):
     rec, rounds, ref = run_pair(ctx, system, fs, epochs, avx=True)
     assert ref["state"][-1] == 4
-    compare(rec[:, 1], ref, f"{system} avx")
+    compare_exact(rec[:, 1], ref, f"{system} avx")
     assert not np.any(rec[:, 0]["flags"])  # the idle channel never ran
 
 
@@ -61,13 +61,40 @@ def test_closed_loop_25msps_matches_oracle(ctx, system, epochs, avx):
     N = 100000 with the data prompt (configs[3]'s per-channel epoch, dll_pll_veml_tracking.cc:1728-2094)."""
     rec, rounds, ref = run_pair(ctx, system, 25e6, epochs, avx=avx)
     assert ref["state"][-1] == 4
-    compare(rec[:, 1], ref, f"{system} 25 Msps avx={avx}")
+    (compare_exact if avx else compare)(rec[:, 1], ref, f"{system} 25 Msps avx={avx}")
 
 
 def test_galileo_e1_50msps_avx_matches_oracle(ctx):
-    """E1 at 50 Msps (configs[4]'s N = 200000) with the AVX rotator: 12500-step phasor chains."""
+    """E1 at 50 Msps (configs[4]'s N = 200000) with the AVX rotator: 12500-step phasor chains, the
+    phasor slots and the products in LDS rings (trk_fast.hip fast_plan)."""
     rec, rounds, ref = run_pair(ctx, "GAL", 50e6, 40, avx=True)
-    compare(rec[:, 1], ref, "GAL 50 Msps avx")
+    compare_exact(rec[:, 1], ref, "GAL 50 Msps avx")
+
+
+@pytest.mark.parametrize("lds_kib", [36, 64])
+def test_fast_kernel_rings_match_oracle(ctx, lds_kib, monkeypatch):
+    """The same GPS 4 Msps loop with the LDS budget cut (GNSSHIP_TRK_FAST_LDS) so that the product
+    ring holds only a few of the epoch's eight groups (36 KiB: 2 groups, 64 KiB: 4, with
+    back-pressure on the producers) — still equal to the oracle."""
+    monkeypatch.setenv("GNSSHIP_TRK_FAST_LDS", str(lds_kib))
+    own = engine.Context(0)  # only GPS codes: the LDS replica is sized by the context's longest code
+    try:
+        rec, rounds, ref = run_pair(own, "GPS", 4e6, 300, avx=True)
+    finally:
+        own.close()
+    compare_exact(rec[:, 1], ref, f"GPS rings {lds_kib} KiB")
+
+
+def test_fast_kernel_slot_ring_matches_oracle(ctx, monkeypatch):
+    """GPS at 25 Msps (196 tasks per epoch) with a budget that forces the phasor slots into their
+    64-task ring and the products into a 2-group ring."""
+    monkeypatch.setenv("GNSSHIP_TRK_FAST_LDS", "40")
+    own = engine.Context(0)
+    try:
+        rec, rounds, ref = run_pair(own, "GPS", 25e6, 120, avx=True)
+    finally:
+        own.close()
+    compare_exact(rec[:, 1], ref, "GPS 25 Msps slot ring")
 
 
 def test_persistent_loop_matches_round_based_loop(ctx):
@@ -136,7 +163,8 @@ def test_telemetry_fault_forces_loss_of_lock(ctx, avx):
     ref_ch = T.Channel(k, sat.code, delay, dop, stamp, first)
     r1, _ = trk.run(x, first, 120)
     o1 = ref_ch.run(x, first, 120)
-    compare(r1[:, 0], o1, "before")
+    cmp = compare_exact if avx else compare
+    cmp(r1[:, 0], o1, "before")
     trk.telemetry_event(0, 2)  # not a fault: ignored
     trk.telemetry_event(0, 1)
     ref_ch.telemetry_fault()
@@ -144,7 +172,7 @@ def test_telemetry_fault_forces_loss_of_lock(ctx, avx):
     o2 = ref_ch.run(x, first, 20)
     d = r2[:, 0][(r2[:, 0]["flags"] & 8) == 8]
     assert len(d) == len(o2) == 1 and (d["flags"][0] & 2) and (o2["flags"][0] & 2)
-    compare(r2[:, 0], o2, "fault epoch")
+    cmp(r2[:, 0], o2, "fault epoch")
     assert trk.channel_state(0)[0] == 0
     trk.close()
 
@@ -153,24 +181,18 @@ def test_c4_share_8_e1_channels_closed_loop_matches_oracle(ctx):
     """configs[3] (C4)'s per-GPU share in closed loop: 8 Galileo E1 B/C channels (5 VEML pilot taps +
     the data prompt, N = 100000 at 25 Msps, AVX rotator) on one engine, eight satellites in one
     signal, 90 epochs each (synchronised to the CS25 pilot code, state 4), every channel against the
-    oracle loop on the same signal (long-integration oracle: double sums, once-rounded trig, as
-    run_pair).  Two checks: the correlator contract on the device's own arguments (every traced
-    channel-epoch re-run on the oracle correlator, taps and data prompt within 1e-5), and the loop
-    against the oracle loop — epoch boundaries, states and flags exact, observables at
-    test_gpu_c5_closed_loop.compare_if's bounds with bounded kicks: over 720 channel-epochs of eight
-    channels the two loops' NCOs (~1e-7 chip apart from their correlation sum orders) occasionally put
-    one of an epoch's 100000 samples on the other side of a chip edge (measured: PRN 19, epoch 4, a
-    1e-3 prompt step), which the loop then carries for a few tens of epochs."""
+    plain oracle loop on the same signal: every traced channel-epoch's taps and data prompt equal the
+    oracle correlator's on the device's own arguments, and the records equal the oracle loop's."""
     import concurrent.futures as cf
 
     from gnss_sim_receiver_amd import signals
-    from test_gpu_c5_closed_loop import compare_if, trace_errors
+    from test_gpu_c5_closed_loop import trace_exact
 
     fs, epochs = 25e6, 90
     prns = [1, 5, 12, 19, 24, 30, 33, 36]
     sats = [signals.Satellite(prn=p, doppler_hz=-3000.0 + 800.0 * i, code_delay_chips=150.3 + 417.0 * i, cn0_dbhz=50.0, system="GAL",
                               carrier_phase_rad=0.3 * i, **S.SYNC_PATTERNS["GAL"]) for i, p in enumerate(prns)]
-    k = T.conf("GAL", fs, int(round(fs * T.SYSTEMS["GAL"][2])), pull_in_time_s=0, rotator_avx=1, accum_f64=1, cr_trig=1)
+    k = T.conf("GAL", fs, int(round(fs * T.SYSTEMS["GAL"][2])), pull_in_time_s=0, rotator_avx=1)
     first = int(fs)
     x = signals.generate_if(fs, int(round(fs)) // 4 + k.vector_length * (epochs + 3), sats, seed=0x6E550004, start=first)
     c = dev_conf(k, "GAL")
@@ -196,5 +218,5 @@ def test_c4_share_8_e1_channels_closed_loop_matches_oracle(ctx):
     for ch, ref in enumerate(refs):
         assert ref["state"][-1] == 4, (ch, np.bincount(ref["state"]))
         label = f"C4 share channel {ch} (PRN {sats[ch].prn})"
-        assert trace_errors(tr[:, ch], x, first, sats[ch].code, sats[ch].code_data, True) <= 1e-5, label
-        compare_if(rec[:, ch], ref, label, kick_frac=0.5, kick_scale=8.0)
+        trace_exact(tr[:, ch], x, first, sats[ch].code, sats[ch].code_data, label)
+        compare_exact(rec[:, ch], ref, label)
