@@ -21,6 +21,9 @@ all: $(LIB) oracle
 # gfx950 (a packed f32 op issues in 4 cycles, a scalar one in 2) and costs register-pair moves
 # and VGPRs (C3 search kernel: 128 VGPRs + scratch packed, 84 unpacked).  Same IEEE ops either way.
 $(OBJDIR)/acq_kernel.o build/prof_obj/acq_kernel.o: HIPFLAGS += -fno-slp-vectorize
+# The tracking engine's serial accumulations (trk_fast.hip) likewise: a dependent packed add issues
+# several times slower than single-rate adds.
+$(OBJDIR)/trk_fast.o build/prof_obj/trk_fast.o: HIPFLAGS += -fno-slp-vectorize
 
 $(OBJDIR)/%.o: $(CSRC)/%.hip $(HDRS)
 	@mkdir -p $(OBJDIR)

@@ -179,28 +179,39 @@ def headline(ctx, torch, args, rank, world, device, barrier):
                 first=first, records=n_rec)
 
 
-def sweep(ctx, h, rot, counts, rounds=100):
-    """Tracked channels sustained: channels c -> satellite c mod 32 on the same file, `rounds`
-    epochs each from the steady-state point of the headline run."""
+def sweep(ctx, h, rot, counts, rounds=1000):
+    """Tracked channels sustained: channels c -> satellite c mod 32 on the same file, each point run
+    for `rounds` epochs (1 s of signal) from the steady-state point of the headline run, every
+    channel-epoch's record (the Gnss_Synchro the reference emits, dll_pll_veml_tracking.cc:2063-2091)
+    copied to the host inside the timed region."""
+    from gnss_sim_receiver_amd import abi
     out = []
     t_abs = h["first"]
     pre = 450  # epochs: every channel bit-synchronised (state 4) before the timed epochs
     for n in counts:
         rx = Receiver(ctx, "GPS", FS, VL, h["sats"], n, t_abs, rot, code_base=2000)
         n_samp = rounds * VL + 4 * VL
-        rx.run(h["base"][0] + (t_abs - h["base"][1]) * 8, 0, t_abs, (pre + 2) * VL)
+        # untimed: the pre-roll, with records on and the timed run's round count, so the device record
+        # buffer is sized here; the host record array is allocated and touched here too
+        rx.trk.launch_ptr(h["base"][0] + (t_abs - h["base"][1]) * 8, 0, t_abs, (pre + 2) * VL, rounds + 4, records=True)
+        rx.trk.collect()
+        host = np.empty((rounds + 4, n), abi.TRK_EPOCH_DTYPE)
+        host.view(np.uint8).fill(0)
         lo = t_abs + pre * VL
         ctx.event_record(2)
         t0 = time.perf_counter()
-        done = rx.run(h["base"][0] + (lo - h["base"][1]) * 8, 0, lo, n_samp)
+        rx.trk.launch_ptr(h["base"][0] + (lo - h["base"][1]) * 8, 0, lo, n_samp, rounds + 4, records=True)
+        rec, done = rx.trk.collect(out=host)
         dt = time.perf_counter() - t0
         ctx.event_record(3)
         k_ms = ctx.event_elapsed_ms(2, 3)
+        n_rec = int(np.count_nonzero(rec[:done]["flags"] & 8))
         idx = np.linspace(0, n - 1, min(n, 64)).astype(int)
         tracking = float(np.mean([rx.trk.channel_state(int(c))[0] in (2, 3, 4) for c in idx]))
         rx.close()
-        cps = n * done / dt
-        out.append({"channels": n, "epochs": done, "us_per_epoch_round": round(dt / done * 1e6, 2),
+        del rec, host
+        cps = n_rec / dt
+        out.append({"channels": n, "epochs": done, "epoch_records": n_rec, "record_bytes": n_rec * 96, "us_per_epoch_round": round(dt / done * 1e6, 2),
                     "kernel_us_per_round": round(k_ms * 1e3 / done, 2), "channel_epochs_per_s": round(cps, 0),
                     "realtime_factor": round(done * 1e-3 / dt, 2), "tracking_fraction_sampled": round(tracking, 3)})
     return out
@@ -210,7 +221,7 @@ def closed_loop_aux(ctx, torch, device, system, fs, vl, n_ch, seconds, rot, seed
     """Closed loop at another rate / signal: n_ch channels, 0.5 s pre-roll (synchronisation), then `seconds` timed."""
     from gnss_sim_receiver_amd import signals
     if system == "GAL":
-        prns = [1, 5, 12, 19, 24, 30, 33, 36, 2, 8, 11, 26][:n_ch]
+        prns = [1, 5, 12, 19, 24, 30, 33, 36, 2, 8, 11, 26][:n_ch] if n_ch <= 12 else (list(range(1, 37)) * 2)[:n_ch]
         sats = signals.random_sky(n_ch, seed=seed, system="GAL", prns=prns)
         for s in sats:
             s.secondary = "0011100000001010110110010"
@@ -244,16 +255,23 @@ def closed_loop_aux(ctx, torch, device, system, fs, vl, n_ch, seconds, rot, seed
             "channels_in_state_4": int(np.sum(st == 4))}
 
 
-def closed_loop_c5_share(torch, device, rot, seconds=0.2, pre_s=0.6):
+def closed_loop_c5_share(torch, device, rot, seconds=0.2, pre_s=0.6, full=False):
     """configs[4]'s per-GPU share in closed loop: 12 GPS L1 C/A + 12 Galileo E1 (5 VEML pilot taps +
     data prompt) + 8 BeiDou B1I channels, three tracking engines each on its own context (stream),
     launched together over one 50 Msps ibyte block whose IF is centred 7.161 MHz from L1/E1 (−7.161
     MHz for B1I), the IF removed in the tracking NCO (gnsship_trk_conf::if_hz).  0.6 s pre-roll
-    (bit / secondary-code synchronisation), then `seconds` timed: launch all three, collect all three."""
+    (bit / secondary-code synchronisation), then `seconds` timed: launch all three, collect all three.
+    full=True: the whole of configs[4] on this one GPU — 96 GPS + 96 E1 + 64 B1I channels, every
+    channel its own signal (PRNs re-used with their own Doppler, delay and phase, as SURVEY §8d C4
+    does beyond PRN 36)."""
     from gnss_sim_receiver_amd import abi, engine, signals as S
     fs, f_if = 50e6, 7.161e6
-    prn_sets = (("GPS", range(1, 13), 0.001, 50000), ("GAL", [1, 2, 3, 4, 5, 7, 8, 9, 11, 12, 13, 15], 0.004, 200000),
-                ("BDS", range(6, 14), 0.001, 50000))
+    if full:
+        prn_sets = (("GPS", (list(range(1, 33)) * 3)[:96], 0.001, 50000), ("GAL", (list(range(1, 37)) * 3)[:96], 0.004, 200000),
+                    ("BDS", (list(range(6, 59)) * 2)[:64], 0.001, 50000))
+    else:
+        prn_sets = (("GPS", range(1, 13), 0.001, 50000), ("GAL", [1, 2, 3, 4, 5, 7, 8, 9, 11, 12, 13, 15], 0.004, 200000),
+                    ("BDS", range(6, 14), 0.001, 50000))
     rng = np.random.default_rng(0x6E550005)
     sky = {}
     for system, prns, _, _ in prn_sets:
@@ -313,7 +331,9 @@ def closed_loop_c5_share(torch, device, rot, seconds=0.2, pre_s=0.6):
     del raw
     sig_s = min(epochs["GPS"] * 0.001, epochs["GAL"] * 0.004, epochs["BDS"] * 0.001)
     chan_samples = sum(recs[k] * vl for k, _, _, vl in prn_sets)
-    return {"config": "C5 per-GPU share, closed loop: 12 GPS L1 C/A + 12 Galileo E1 (5 VEML + data prompt) + 8 BeiDou B1I, 50 Msps ibyte, "
+    counts = "96 GPS L1 C/A + 96 Galileo E1 (5 VEML + data prompt) + 64 BeiDou B1I (configs[4] whole, one GPU)" if full else \
+        "C5 per-GPU share, 12 GPS L1 C/A + 12 Galileo E1 (5 VEML + data prompt) + 8 BeiDou B1I"
+    return {"config": counts + ", closed loop, 50 Msps ibyte, "
                       "IF +-7.161 MHz in the tracking NCO, three engines on three streams launched together, rotator " + rotator_name(rot),
             "signal_s": round(sig_s, 3), "wall_ms": round(dt * 1e3, 3), "realtime_factor": round(sig_s / dt, 1),
             "if_msamples_per_s": round(sig_s * fs / dt / 1e6, 1), "channel_msamples_per_s": round(chan_samples / dt / 1e6, 1),
@@ -525,22 +545,29 @@ def c1_receiver(torch, device, seconds=10.0, cpu_seconds=1.0):
 # CPU baseline: the oracle's closed loop, one thread per channel (ctypes releases the GIL)
 def cpu_baseline(h, budget_s):
     """The oracle's closed loop on the host: 12 threads, one per channel of the workload, over a
-    bounded sample of the same file.  For the AVX variant two figures: the AVX restatement
-    (oracle/avx_port.c — the arithmetic the reference's u_avx kernel runs on such a host; `value`)
-    and the scalar restatement of the same loop (`scalar_port`), each timed over part of the budget."""
+    bounded sample of the same file.  Like the GPU leg, only steady-state epochs are timed: each
+    thread first runs its channel through start_tracking and the pre-roll (bit synchronisation,
+    state 4) untimed, snapshots the channel (the oracle's channel state is one plain C struct), then
+    replays the next 500 epochs of the file from that snapshot again and again while the clock runs —
+    no start_tracking, pull-in or state-2 epochs inside the timed region.  For the AVX variant two
+    figures: the AVX restatement (oracle/avx_port.c — the arithmetic the reference's u_avx kernel runs
+    on such a host; `value`) and the scalar restatement of the same loop (`scalar_port`)."""
+    import ctypes
     from oracle import trk as T
     from gnss_sim_receiver_amd import signals
     import platform
     from oracle import oracle as O
     O.build()
     rot = h["rotator"]
-    # bounded sample of the same file (host copy of the first 0.6 s after the pre-roll start)
-    n_s = int(0.6 * FS)
+    pre_ep, run_ep = int(round(PRE_ROLL_S * 1000)), 500
+    # bounded sample of the same file: the pre-roll plus 500 steady-state epochs (host copy)
+    n_s = (pre_ep + run_ep + 4) * VL
     x = h["x"][: n_s + 4 * VL].cpu().numpy()
     first, base_abs = h["first"], h["base"][1]
     threads = min(N_CH, len(os.sched_getaffinity(0)))  # one thread per channel of the workload
     k = T.conf("GPS", FS, VL, rotator_avx=1 if rot == 1 else 0)
     sats = h["sats"]
+    states = [None] * threads
 
     def timed(simd_on, seconds):
         simd = O.set_simd(simd_on, fast=True)
@@ -549,18 +576,23 @@ def cpu_baseline(h, budget_s):
 
         def worker(t):
             s = sats[t % N_CH]
-            delay = signals.acq_delay_samples(s, FS, 0, first)
+            ch = T.Channel(k, s.code, signals.acq_delay_samples(s, FS, 0, first), s.doppler_hz, 0, first, fast=True)
+            ch.run(x, base_abs, pre_ep)  # untimed: pull-in over, bit synchronisation
+            states[t] = ch.state
+            snap = ctypes.create_string_buffer(ch.buf.raw, len(ch.buf))
             while not stop[0]:
-                ch = T.Channel(k, s.code, delay, s.doppler_hz, 0, first, fast=True)
-                rec = ch.run(x, base_abs, 500)
+                ctypes.memmove(ch.buf, snap, len(ch.buf))  # back to the steady-state snapshot
+                rec = ch.run(x, base_abs, run_ep)
                 done_epochs[t] += len(rec)
                 if len(rec) == 0:
                     break
 
         ths = [threading.Thread(target=worker, args=(t,)) for t in range(threads)]
-        t0 = time.perf_counter()
         for th in ths:
             th.start()
+        while any(st is None for st in states):  # the pre-rolls run before the clock starts
+            time.sleep(0.01)
+        t0 = time.perf_counter()
         time.sleep(seconds)
         stop[0] = True
         for th in ths:
@@ -582,16 +614,19 @@ def cpu_baseline(h, budget_s):
     chan_sps = ep * VL / dt
     out = {"value": round(chan_sps / N_CH / 1e6, 2), "unit": "Msamples/s",
            "cores": threads, "kind": "port",
-           "sample": f"{ep} channel-epochs of the closed loop (oracle/trk_oracle.c, rotator {rot}, -O3 -march=native, correlator "
-                     f"{'AVX restatement oracle/avx_port.c' if simd else 'scalar restatement'}) on 0.6 s of the same file, {threads} threads "
-                     f"(one channel each) for {dt:.1f} s; value = channel-samples/s ÷ {N_CH} channels, i.e. the IF rate at which this "
-                     f"host would keep {N_CH} channels",
+           "sample": f"{ep} steady-state channel-epochs of the closed loop (oracle/trk_oracle.c, rotator {rot}, -O3 -march=native, "
+                     f"correlator {'AVX restatement oracle/avx_port.c' if simd else 'scalar restatement'}): {threads} threads (one channel "
+                     f"each) replay the {run_ep} epochs after the {pre_ep}-epoch untimed pre-roll from a state-{states[0]} snapshot for "
+                     f"{dt:.1f} s (no start_tracking / pull-in / state-2 epochs timed); value = channel-samples/s ÷ {N_CH} channels, "
+                     f"i.e. the IF rate at which this host would keep {N_CH} channels",
+           "states_after_preroll": [int(v) for v in states],
            "channel_msamples_per_s": round(chan_sps / 1e6, 2),
            "channel_msamples_per_s_per_core": round(chan_sps / threads / 1e6, 1),
            "cpu_model": model, "machine": platform.machine(),
            "reference_avx_note": "SURVEY §6 measured the reference's own AVX correlator at 268 M channel-samples/s per core in "
                                  "the survey container; the AVX restatement runs the same 16-lane u_avx arithmetic"}
     if simd:
+        states[:] = [None] * threads
         _, ep2, dt2 = timed(False, budget_s * 0.4)
         cs2 = ep2 * VL / dt2
         out["scalar_port"] = {"value": round(cs2 / N_CH / 1e6, 2), "unit": "Msamples/s", "cores": threads,
@@ -980,8 +1015,9 @@ def main():
         rt = [r["channels"] for r in sw if r["realtime_factor"] >= 1.0]
         result["tracked_channels_sustained"] = max(rt) if rt else 0
         result["channel_sweep"] = sw
-        result["tracked_channels_note"] = ("the largest channel count of the sweep measured at >= real time (1000 epochs per channel-second); "
-                                           "channels beyond two workgroups per CU run in successive generations of the persistent kernel")
+        result["tracked_channels_note"] = ("the largest channel count of the sweep measured at >= real time: 1 s of signal (1000 epochs) per "
+                                           "point, every channel-epoch record copied to the host inside the timed run; channels beyond the "
+                                           "resident workgroups run in successive generations of the persistent kernel")
         if h["rotator"] != 0:
             g = Receiver(ctx, "GPS", FS, VL, [h["sats"][i] for i in range(N_CH)], N_CH, h["first"], 0, code_base=800)
             pre = int(round(PRE_ROLL_S * FS))
@@ -994,6 +1030,9 @@ def main():
         result["closed_loop_gps_25msps"] = guarded(closed_loop_aux, ctx, torch, device, "GPS", 25e6, 25000, N_CH, 0.3, h["rotator"], SEED + 11)
         result["closed_loop_e1_25msps_c4_share"] = guarded(closed_loop_aux, ctx, torch, device, "GAL", 25e6, 100000, 8, 0.4, h["rotator"], SEED + 12)
         result["closed_loop_c5_share"] = guarded(closed_loop_c5_share, torch, device, h["rotator"])
+        # the BASELINE channel counts of C4 and C5 whole, on this one GPU (the 8-GPU split divides them)
+        result["closed_loop_c4_full_64_e1"] = guarded(closed_loop_aux, ctx, torch, device, "GAL", 25e6, 100000, 64, 0.4, h["rotator"], SEED + 14)
+        result["closed_loop_c5_full_256"] = guarded(closed_loop_c5_share, torch, device, h["rotator"], full=True)
         if world == 1 and args.cpu_seconds > 0:
             result["cpu_baseline"] = guarded(cpu_baseline, h, args.cpu_seconds)
         result["open_loop_correlator"] = guarded(open_loop_correlator, ctx, torch, device, rot=h["rotator"])

@@ -111,6 +111,17 @@ struct gnsship_acq {
     std::vector<char> code_set;
     int consumed = 0;            // d_consumed_samples: input samples used, the rest zero-padded
     Step2Spec step2{};           // make_2_steps: step-two grid active
+    // The sweep's launches (forward transform, search, decision) as one hipGraph, re-captured when
+    // any launch argument changes: a C3 sweep is four short kernels, and the launch gaps between
+    // them cost ~15 % of its time when launched one by one.  GNSSHIP_ACQ_GRAPH=0: plain launches.
+    hipGraphExec_t graph = nullptr;
+    struct GraphKey {
+        const void* src;
+        int fmt, n_prns, accumulate, keep_grid, dwell;
+        const float* grid;
+        Step2Spec step2;
+    } graph_key{};
+    bool graph_broken = false;   // a capture failed once: plain launches from then on
     RowSpec rows() const
     {
         const int N = conf.fft_size;
@@ -119,8 +130,15 @@ struct gnsship_acq {
     }
 };
 
+static void acq_graph_reset(gnsship_acq* a)
+{
+    if (a->graph) (void)hipGraphExecDestroy(a->graph);
+    a->graph = nullptr;
+}
+
 static void acq_free_grid_buffers(gnsship_acq* a)
 {
+    acq_graph_reset(a);
     void* hp[] = {a->T, a->U, a->grid_scratch, a->tiles};
     for (void* p : hp)
         if (p) (void)hipFree(p);
@@ -146,6 +164,7 @@ extern "C" int gnsship_acq_destroy(gnsship_acq* a)
     (void)hipSetDevice(a->ctx->device);
     (void)hipStreamSynchronize(a->ctx->stream);
     acq_free_grid_buffers(a);
+    acq_graph_reset(a);
     void* ptrs[] = {a->tw, a->twM, a->twC, a->codes_fft, a->res_dev, a->sig_dev};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
@@ -229,6 +248,7 @@ extern "C" int gnsship_acq_set_grid(gnsship_acq* a, int doppler_max, int doppler
     a->conf.doppler_step = doppler_step;
     a->conf.doppler_center = doppler_center;
     a->step2 = Step2Spec{};
+    acq_graph_reset(a);
     return GNSSHIP_OK;
 }
 
@@ -249,6 +269,7 @@ extern "C" int gnsship_acq_set_grid_step2(gnsship_acq* a, float doppler_center_s
     }
     if (int rc = acq_upload_wipeoffs(a, num_doppler_bins_step2, f)) return rc;
     a->step2 = Step2Spec{1, doppler_center_step_two, doppler_step2, step_one_input_power};
+    acq_graph_reset(a);
     return GNSSHIP_OK;
 }
 
@@ -391,39 +412,72 @@ extern "C" int gnsship_acq_run(gnsship_acq* a, const void* sig, int fmt, int sig
     if (a->dwell_count >= a->conf.max_dwells) a->dwell_count = 0;
     const int accumulate = (a->conf.max_dwells > 1 && a->dwell_count > 0) ? 1 : 0;
     a->dwell_count++;
-    if (a->huge) {
-        HIP_TRY(ctx, launch_acq_fft_huge(src, fmt, a->wipe, a->n_bins, a->P, a->plan, a->twC, a->twM, a->T, a->X, 0, a->consumed, ctx->stream));
-        const bool two = a->lanes == 2 && n_prns > a->prn_batch;
-        if (two) {
-            HIP_TRY(ctx, hipEventRecord(a->ev_fwd, ctx->stream));
-            HIP_TRY(ctx, hipStreamWaitEvent(a->lane_stream, a->ev_fwd, 0));  // lane 1 reads the forward spectra
+    auto enqueue = [&]() -> int {
+        if (a->huge) {
+            HIP_TRY(ctx, launch_acq_fft_huge(src, fmt, a->wipe, a->n_bins, a->P, a->plan, a->twC, a->twM, a->T, a->X, 0, a->consumed, ctx->stream));
+            const bool two = a->lanes == 2 && n_prns > a->prn_batch;
+            if (two) {
+                HIP_TRY(ctx, hipEventRecord(a->ev_fwd, ctx->stream));
+                HIP_TRY(ctx, hipStreamWaitEvent(a->lane_stream, a->ev_fwd, 0));  // lane 1 reads the forward spectra
+            }
+            const size_t u_lane = static_cast<size_t>(a->prn_batch) * a->n_bins * a->conf.fft_size;
+            const size_t t_lane = static_cast<size_t>(a->prn_batch) * a->n_bins * huge_tiles(a->plan.n);
+            for (int p0 = 0, i = 0; p0 < n_prns; p0 += a->prn_batch, i++) {
+                const int np = std::min(a->prn_batch, n_prns - p0);
+                const int lane = two ? (i & 1) : 0;  // batches i and i + 2 share a lane's U and tiles, in stream order
+                // without a kept grid the |y|² rows never reach HBM (tile statistics + finalize's recomputation)
+                float* g = keep_grid ? a->grid_dev + static_cast<size_t>(p0) * a->n_bins * rs.row_len : nullptr;
+                HIP_TRY(ctx, launch_acq_search_huge(a->X, a->codes_fft, p0, np, a->n_bins, a->P, a->plan, a->twC, a->twM, a->U + lane * u_lane, g,
+                                 keep_grid ? accumulate : 0, a->tiles + lane * t_lane, rs, a->rowstat, lane ? a->lane_stream : ctx->stream));
+            }
+            if (two) {  // the decision reads every batch's row statistics
+                HIP_TRY(ctx, hipEventRecord(a->ev_lane, a->lane_stream));
+                HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, a->ev_lane, 0));
+            }
+        } else if (a->P) {
+            HIP_TRY(ctx, launch_acq_fft_big(src, fmt, a->wipe, a->n_bins, a->P, a->plan, a->tw, a->X, 0, a->consumed, ctx->stream));
+            HIP_TRY(ctx, launch_acq_search_big(a->X, a->codes_fft, n_prns, a->n_bins, a->P, a->plan, a->tw, rs, accumulate,
+                             a->rowstat, keep_grid ? a->grid_dev : nullptr, ctx->stream));
+        } else {
+            HIP_TRY(ctx, launch_acq_fft_rows(src, fmt, a->wipe, a->n_bins, a->plan, a->tw, a->X, 0, a->consumed, ctx->stream));
+            HIP_TRY(ctx, launch_acq_search(a->X, a->codes_fft, n_prns, a->n_bins, a->plan, a->tw, rs, accumulate,
+                             a->rowstat, keep_grid ? a->grid_dev : nullptr, ctx->stream));
         }
-        const size_t u_lane = static_cast<size_t>(a->prn_batch) * a->n_bins * a->conf.fft_size;
-        const size_t t_lane = static_cast<size_t>(a->prn_batch) * a->n_bins * huge_tiles(a->plan.n);
-        for (int p0 = 0, i = 0; p0 < n_prns; p0 += a->prn_batch, i++) {
-            const int np = std::min(a->prn_batch, n_prns - p0);
-            const int lane = two ? (i & 1) : 0;  // batches i and i + 2 share a lane's U and tiles, in stream order
-            // without a kept grid the |y|² rows never reach HBM (tile statistics + finalize's recomputation)
-            float* g = keep_grid ? a->grid_dev + static_cast<size_t>(p0) * a->n_bins * rs.row_len : nullptr;
-            HIP_TRY(ctx, launch_acq_search_huge(a->X, a->codes_fft, p0, np, a->n_bins, a->P, a->plan, a->twC, a->twM, a->U + lane * u_lane, g,
-                             keep_grid ? accumulate : 0, a->tiles + lane * t_lane, rs, a->rowstat, lane ? a->lane_stream : ctx->stream));
+        HIP_TRY(ctx, launch_acq_decide(a->rowstat, n_prns, a->n_bins, rs.row_len, a->conf.doppler_max, a->conf.doppler_step, a->conf.doppler_center,
+                         a->dwell_count, a->conf.use_cfar, a->conf.samples_per_code, a->conf.resampler_ratio > 0.0f ? a->conf.resampler_ratio : 1.0f,
+                         a->conf.resampler_latency_samples, a->step2, a->res_dev, ctx->stream));
+        return GNSSHIP_OK;
+    };
+    static const bool graphs_on = [] {
+        const char* env = std::getenv("GNSSHIP_ACQ_GRAPH");
+        return !(env && env[0] == '0');
+    }();
+    if (graphs_on && !a->graph_broken) {
+        const gnsship_acq::GraphKey key{src, fmt, n_prns, accumulate, keep_grid ? 1 : 0, a->dwell_count, keep_grid ? a->grid_dev : nullptr, a->step2};
+        const bool same = a->graph && std::memcmp(&key, &a->graph_key, sizeof(key)) == 0;
+        if (!same) {
+            acq_graph_reset(a);
+            hipGraph_t g = nullptr;
+            int rc = GNSSHIP_OK;
+            if (hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeThreadLocal) == hipSuccess) {
+                rc = enqueue();
+                const hipError_t e = hipStreamEndCapture(ctx->stream, &g);
+                if (rc == GNSSHIP_OK && e == hipSuccess && g && hipGraphInstantiate(&a->graph, g, nullptr, nullptr, 0) == hipSuccess)
+                    a->graph_key = key;
+                else
+                    a->graph = nullptr;
+                if (g) (void)hipGraphDestroy(g);
+            }
+            (void)hipGetLastError();
+            if (!a->graph) {  // capture unavailable: launch directly, now and from now on
+                a->graph_broken = true;
+                if (int rc2 = enqueue()) return rc2;
+            }
         }
-        if (two) {  // the decision reads every batch's row statistics
-            HIP_TRY(ctx, hipEventRecord(a->ev_lane, a->lane_stream));
-            HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, a->ev_lane, 0));
-        }
-    } else if (a->P) {
-        HIP_TRY(ctx, launch_acq_fft_big(src, fmt, a->wipe, a->n_bins, a->P, a->plan, a->tw, a->X, 0, a->consumed, ctx->stream));
-        HIP_TRY(ctx, launch_acq_search_big(a->X, a->codes_fft, n_prns, a->n_bins, a->P, a->plan, a->tw, rs, accumulate,
-                         a->rowstat, keep_grid ? a->grid_dev : nullptr, ctx->stream));
-    } else {
-        HIP_TRY(ctx, launch_acq_fft_rows(src, fmt, a->wipe, a->n_bins, a->plan, a->tw, a->X, 0, a->consumed, ctx->stream));
-        HIP_TRY(ctx, launch_acq_search(a->X, a->codes_fft, n_prns, a->n_bins, a->plan, a->tw, rs, accumulate,
-                         a->rowstat, keep_grid ? a->grid_dev : nullptr, ctx->stream));
+        if (a->graph) HIP_TRY(ctx, hipGraphLaunch(a->graph, ctx->stream));
+    } else if (int rc = enqueue()) {
+        return rc;
     }
-    HIP_TRY(ctx, launch_acq_decide(a->rowstat, n_prns, a->n_bins, rs.row_len, a->conf.doppler_max, a->conf.doppler_step, a->conf.doppler_center,
-                     a->dwell_count, a->conf.use_cfar, a->conf.samples_per_code, a->conf.resampler_ratio > 0.0f ? a->conf.resampler_ratio : 1.0f,
-                     a->conf.resampler_latency_samples, a->step2, a->res_dev, ctx->stream));
     HIP_TRY(ctx, hipMemcpyAsync(results, a->res_dev, sizeof(gnsship_acq_result) * n_prns, hipMemcpyDeviceToHost, ctx->stream));
     if (grid)
         HIP_TRY(ctx, hipMemcpyAsync(grid, a->grid_dev, sizeof(float) * static_cast<size_t>(n_prns) * a->n_bins * rs.row_len, hipMemcpyDeviceToHost,

@@ -88,6 +88,18 @@ __device__ __forceinline__ f2 cmul_pk2(f2 x, f2 p)
     return r;
 }
 
+// x·z rounded exactly as _mm256_complexmul_ps / the written-out (ac − bd, ad + bc): every product
+// rounded, then one add and one subtract — three packed ops, the swizzles in op_sel / neg modifiers:
+//   t = (xr·zr, xr·zi);  u = (xi·zi, xi·zr);  x·z = (t.lo − u.lo, t.hi + u.hi)
+__device__ __forceinline__ f2 cmul_exact_pk(f2 x, f2 z)
+{
+    f2 t, u, r;
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]" : "=v"(t) : "v"(x), "v"(z));
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel:[1,1] op_sel_hi:[1,0]" : "=v"(u) : "v"(x), "v"(z));
+    asm("v_pk_add_f32 %0, %1, %2 neg_lo:[0,1]" : "=v"(r) : "v"(t), "v"(u));
+    return r;
+}
+
 // x·q with q wave-uniform (an anchor from the chunk's scalar block): q stays in its SGPR pair.
 __device__ __forceinline__ f2 cmul_pk2_s(f2 x, f2 q)
 {
@@ -271,6 +283,15 @@ __device__ __forceinline__ f2 cmul_exact(f2 a, f2 b)
     const f2 t = f2{a.x, a.x} * b;
     const f2 u = f2{a.y, a.y} * f2{-b.y, b.x};
     return t + u;
+}
+
+// The same product in single-rate scalar ops (6 VALU, two deep): for short dependent chains, where a
+// dependent packed op issues several times slower on gfx950.
+__device__ __forceinline__ f2 cmul_exact_sc(f2 a, f2 b)
+{
+    const float re = __fsub_rn(__fmul_rn(a.x, b.x), __fmul_rn(a.y, b.y));
+    const float im = __fadd_rn(__fmul_rn(a.x, b.y), __fmul_rn(a.y, b.x));
+    return f2{re, im};
 }
 
 // The same product on a serial chain with q wave-uniform (q in an SGPR pair): six single-rate VALU

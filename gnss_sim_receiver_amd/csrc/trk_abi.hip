@@ -7,6 +7,7 @@
 // device (trk_kernel.hip) between fixed-plan correlator launches.
 #include <cmath>
 #include <cstddef>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <new>
@@ -340,7 +341,17 @@ extern "C" int gnsship_trk_create(gnsship_ctx* ctx, const gnsship_trk_conf* conf
         delete t;
         return fail(ctx, GNSSHIP_E_INVAL, "gnsship_trk_create: unknown system");
     }
-    if (t->params.conf.rotator == GNSSHIP_ROTATOR_AUTO) gnsship_rotator_dispatch(&t->params.conf.rotator);
+    if (t->params.conf.rotator == GNSSHIP_ROTATOR_AUTO) {
+        // a preference entry the engine does not reproduce (generic_reload, another variant name) is
+        // an error, not a silent fall-back to the nearest variant
+        if (gnsship_rotator_dispatch(&t->params.conf.rotator) != GNSSHIP_OK) {
+            char detail[256] = {0}, msg[320];
+            gnsship_rotator_dispatch_detail(detail, sizeof(detail));
+            std::snprintf(msg, sizeof(msg), "gnsship_trk_create: rotator dispatch: %s", detail);
+            delete t;
+            return fail(ctx, GNSSHIP_E_INVAL, msg);
+        }
+    }
     if (t->params.conf.high_dyn) t->params.conf.rotator = GNSSHIP_ROTATOR_GENERIC;  // only generic high-dynamics variants exist
     if (t->params.conf.rotator == GNSSHIP_ROTATOR_AVX && !trk_persist_supports(t->params)) {
         delete t;
@@ -662,9 +673,13 @@ static int trk_finish(gnsship_trk* t, gnsship_trk_epoch* out, gnsship_trk_dump_r
     const size_t nrec = static_cast<size_t>(max_rounds) * t->max_channels;
     std::vector<int> ran(max_rounds + 1);
     HIP_TRY(ctx, hipMemcpyAsync(ran.data(), t->ran_dev, sizeof(int) * (max_rounds + 1), hipMemcpyDeviceToHost, ctx->stream));
-    if (out && t->pending_out) HIP_TRY(ctx, hipMemcpyAsync(out, t->rec_dev, sizeof(gnsship_trk_epoch) * nrec, hipMemcpyDeviceToHost, ctx->stream));
-    if (dump && t->pending_dump)
-        HIP_TRY(ctx, hipMemcpyAsync(dump, t->dump_dev, sizeof(gnsship_trk_dump_record) * nrec, hipMemcpyDeviceToHost, ctx->stream));
+    if ((out && !t->pending_out) || (dump && !t->pending_dump)) {  // the launch did not keep them: nothing to copy
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+        t->pending_rounds = -1;
+        return fail(ctx, GNSSHIP_E_INVAL, "gnsship_trk_collect: records / dump requested that the launch did not keep (want_records / want_dump)");
+    }
+    if (out) HIP_TRY(ctx, hipMemcpyAsync(out, t->rec_dev, sizeof(gnsship_trk_epoch) * nrec, hipMemcpyDeviceToHost, ctx->stream));
+    if (dump) HIP_TRY(ctx, hipMemcpyAsync(dump, t->dump_dev, sizeof(gnsship_trk_dump_record) * nrec, hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     t->pending_rounds = -1;
     if (rounds_done) {

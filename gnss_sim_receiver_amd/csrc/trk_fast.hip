@@ -44,7 +44,7 @@
 namespace gnsship {
 namespace {
 constexpr int kFProfEpochs = 64;
-constexpr int kFProfSlots = 32;
+constexpr int kFProfSlots = 48;
 __device__ unsigned long long* g_trkf_prof = nullptr;
 __shared__ int g_fprof_epoch;
 __device__ __forceinline__ void trkf_prof_stamp(int e, int k)
@@ -91,9 +91,16 @@ __device__ __forceinline__ void trkf_prof_hwid(int k)  // HW_ID (wave slot, SIMD
 namespace gnsship {
 namespace {
 
-constexpr int kFThreads = 256;
-constexpr int kFWaves = kFThreads / kWave;
-constexpr int kFProducers = kFWaves - 2;  // waves 2.. form and store the products
+#ifndef GNSSHIP_FAST_WAVES
+#define GNSSHIP_FAST_WAVES 6
+#endif
+constexpr int kFWaves = GNSSHIP_FAST_WAVES;
+constexpr int kFThreads = kFWaves * kWave;
+constexpr int kFProducers = kFWaves - 2;  // every wave but the control and phasor waves forms products
+// Wave roles (fast_roles): the control wave and the phasor wave each get a SIMD of their own — the
+// phasor chain is the epoch's critical path and the control wave's loop update is the next — and the
+// producers share the other SIMDs (two producer waves on a SIMD interleave their issue).
+constexpr int kRoleControl = 0, kRoleReplay = 1, kRoleProducer = 2;
 constexpr uint64_t kSlotEmpty = ~0ull;  // an unwritten phasor slot (NaN, NaN)
 
 // The epoch's correlation as the producers need it (LDS: the seed from wave 0, dz from wave 1).
@@ -337,13 +344,68 @@ __device__ __forceinline__ float fast_replay(float x, float c, float k2, int M, 
     return x;
 }
 
-// ---- waves 2-3: the products ----------------------------------------------------------------------
-// Product ring: `rg` groups of 4·G iterations; iteration m of group g lives at ring iteration
-// (g mod rg)·4G + (m − 4gG), element ((ring iteration · NTT) + tap) · 16 + chain.  Group tags count
-// over the run (gbase = epoch · n_groups), so no flag is ever re-armed.
+// Producer phase A, before the group's phasor slots are ready: the code value of every tap at
+// every sample of this lane's task (the resampler, volk_gnsssdr_32f_xn_resampler_32f_xn.h:63-80) into
+// the ring group's code table — it depends only on the code NCO, so it runs ahead of the replay.
+template <int NT, bool DATA, bool IN_MARGIN, int G, bool FULL>
+__device__ __forceinline__ void group_codes(const float* __restrict__ code0, const float* __restrict__ code1, int L, int n0, int cnt, float step,
+    float rem, const float (&shifts)[NT], float* __restrict__ cdst)
+{
+    constexpr int NTT = NT + (DATA ? 1 : 0);
+    float fn = static_cast<float>(n0);  // (float)n, exact steps of 16 (n < 2^24)
+    const float fn0 = fn;
+#pragma unroll
+    for (int i = 0; i < G; i++) {
+        const bool on = FULL || i < cnt;
+        const float sn = __fmul_rn(step, on ? fn : fn0);
+        float* d = cdst + static_cast<size_t>(i) * NTT * kAvxLanes;
+#pragma unroll
+        for (int q = 0; q < NT; q++) d[q * kAvxLanes] = code_at<IN_MARGIN>(code0, L, sn, shifts[q], rem);
+        if constexpr (DATA) d[NT * kAvxLanes] = code_at<IN_MARGIN>(code1, L, sn, 0.0f, rem);
+        fn += static_cast<float>(kAvxLanes);
+    }
+}
+
+// Producer phase B, once the slot holds z_l at the task start: per iteration the sample product
+// a = x·z_l (_mm256_complexmul_ps rounding) into the ring group, and the chain's own update z·dz
+// (renormalised after the task's first iteration when that is ≡ 0 mod 64, :265-272).
+// FULL: every lane's task has all G iterations, so nothing is masked.
+template <int FMT, int G, bool FULL>
+__device__ __forceinline__ void group_phasors(i4v span, f2 z, f2 dz, bool renorm, int n0, int cnt, f2* __restrict__ adst, f2 (&xa)[G < 8 ? G : 8],
+    f2 (&xb)[G < 8 ? G : 8])
+{
+    constexpr int SB = sample_bytes<FMT>();
+    constexpr int kB = G < 8 ? G : 8;
+#pragma unroll 1
+    for (int i0 = 0; i0 < G; i0 += kB) {
+        if (i0 + kB < G) {
+#pragma unroll
+            for (int u = 0; u < kB; u++) xb[u] = load_sample<FMT>(span, (n0 + kAvxLanes * (i0 + kB + u)) * SB, 0);
+        }
+#pragma unroll
+        for (int u = 0; u < kB; u++) {
+            const int i = i0 + u;
+            const bool on = FULL || i < cnt;
+            adst[static_cast<size_t>(i) * kAvxLanes] = on ? cmul_exact_pk(xa[u], z) : f2{0.0f, 0.0f};
+            f2 zn = cmul_exact_s(z, dz);
+            if (i == 0 && renorm) zn = normalise_avx(zn);
+            z = zn;
+        }
+        if (i0 + kB < G) {
+#pragma unroll
+            for (int u = 0; u < kB; u++) xa[u] = xb[u];
+        }
+    }
+}
+
+// ---- producer waves -------------------------------------------------------------------------------
+// Ring group r (of rg) holds one group of 4 tasks = 4G iterations: the sample products
+// Pa[(r·4G + j)·16 + l] and the code values Pc[((r·4G + j)·NTT + tap)·16 + l] of iteration j of the
+// group, chain l.  Group tags count over the run (gbase = epoch · n_groups): no flag is re-armed.
 template <int FMT, int NT, bool DATA, bool IN_MARGIN, int G>
 __device__ __forceinline__ void fast_produce(const FJob& job, i4v span, const float* __restrict__ code0, const float* __restrict__ code1, int L,
-    uint64_t* __restrict__ Zs, int rs, f2* __restrict__ P, int rg, int32_t* ready, const int32_t* acc_groups, int gbase, int lane, int pw, int pe)
+    uint64_t* __restrict__ Zs, int rs, f2* __restrict__ Pa, float* __restrict__ Pc, int rg, int32_t* ready, const int32_t* acc_groups, int gbase, int lane,
+    int pw, int pe)
 {
     constexpr int SB = sample_bytes<FMT>();
     constexpr int NTT = NT + (DATA ? 1 : 0);
@@ -362,8 +424,7 @@ __device__ __forceinline__ void fast_produce(const FJob& job, i4v span, const fl
 #pragma unroll
         for (int u = 0; u < kB; u++) x[u] = load_sample<FMT>(span, (n0 + kAvxLanes * u) * SB, 0);
     };
-    f2 xa[kB], xb[kB], xn[kB];
-    if (pw < n_groups) first_samples(pw, xa);
+    f2 xa[kB], xb[kB];
     int rslot = pw % rg;
     const int rstep = kFProducers % rg;
     for (int g = pw; g < n_groups; g += kFProducers) {
@@ -372,10 +433,16 @@ __device__ __forceinline__ void fast_produce(const FJob& job, i4v span, const fl
         const int m_lo = G * (active ? t : 0);
         const int cnt = active ? min(G, M - m_lo) : 0;
         const int n0 = kAvxLanes * m_lo + l;
-        const bool more = g + kFProducers < n_groups;
-        if (more) first_samples(g + kFProducers, xn);  // in flight while polling and forming this group
+        const bool full = 4 * g + 4 <= S && G * (4 * g + 4) <= M;  // every task of the group whole
+        first_samples(g, xa);  // in flight during phase A and the slot poll
         // the ring group is free once the accumulator consumed its previous occupant
         if (g >= rg) lds_wait_ge(acc_groups, gbase + g - rg + 1);
+        const size_t j0 = static_cast<size_t>(rslot * 4 * G + tl * G);
+        float* cdst = Pc + j0 * NTT * kAvxLanes + l;
+        if (full)
+            group_codes<NT, DATA, IN_MARGIN, G, true>(code0, code1, L, n0, G, step, rem, shifts, cdst);
+        else
+            group_codes<NT, DATA, IN_MARGIN, G, false>(code0, code1, L, n0, cnt, step, rem, shifts, cdst);
         const int ts = active ? t % rs : 0;
         uint64_t* slot = Zs + ts * kAvxLanes + l;
         uint64_t v = kSlotEmpty;
@@ -386,102 +453,86 @@ __device__ __forceinline__ void fast_produce(const FJob& job, i4v span, const fl
         }
         if (g == pw && pw == 0) GNSSHIP_FSTAMP(pe, 30);
         if (g + kFProducers >= n_groups && pw == 1) GNSSHIP_FSTAMP(pe, 31);
-        f2 z = active ? __builtin_bit_cast(f2, v) : f2{0.0f, 0.0f};
+        const f2 z = active ? __builtin_bit_cast(f2, v) : f2{0.0f, 0.0f};
         const bool renorm = ((G * t) & 63) == 0;
-        float fn = static_cast<float>(n0);  // (float)n, exact steps of 16 (n < 2^24)
-        f2* dst = P + (static_cast<size_t>(rslot * 4 * G + tl * G) * NTT) * kAvxLanes + l;
-#pragma unroll 1
-        for (int i0 = 0; i0 < G; i0 += kB) {
-            if (i0 + kB < G) {
-#pragma unroll
-                for (int u = 0; u < kB; u++) xb[u] = load_sample<FMT>(span, (n0 + kAvxLanes * (i0 + kB + u)) * SB, 0);
-            }
-#pragma unroll
-            for (int u = 0; u < kB; u++) {
-                const int i = i0 + u;
-                const bool on = i < cnt;
-                // x·z_l (_mm256_complexmul_ps: ac − bd, ad + bc, each product rounded), then the
-                // chain's own update z·dz
-                const f2 a = on ? cmul_exact(xa[u], z) : f2{0.0f, 0.0f};
-                f2 zn = cmul_exact_s(z, dz);
-                if (i == 0 && renorm) zn = normalise_avx(zn);
-                z = zn;
-                const float sn = __fmul_rn(step, on ? fn : static_cast<float>(n0));
-                f2* d = dst + static_cast<size_t>(i) * NTT * kAvxLanes;
-#pragma unroll
-                for (int q = 0; q < NT; q++) {
-                    const float c = code_at<IN_MARGIN>(code0, L, sn, shifts[q], rem);
-                    d[q * kAvxLanes] = a * f2{c, c};  // _mm256_mul_ps (the sum is the accumulator's)
-                }
-                if constexpr (DATA) {
-                    const float c = code_at<IN_MARGIN>(code1, L, sn, 0.0f, rem);
-                    d[NT * kAvxLanes] = a * f2{c, c};
-                }
-                fn += static_cast<float>(kAvxLanes);
-            }
-            if (i0 + kB < G) {
-#pragma unroll
-                for (int u = 0; u < kB; u++) xa[u] = xb[u];
-            }
-        }
+        f2* adst = Pa + j0 * kAvxLanes + l;
+        if (full)
+            group_phasors<FMT, G, true>(span, z, dz, renorm, n0, G, adst, xa, xb);
+        else
+            group_phasors<FMT, G, false>(span, z, dz, renorm, n0, cnt, adst, xa, xb);
         if (lane == 0) lds_release_store(ready + rslot, gbase + g + 1);
-        if (more) {
-#pragma unroll
-            for (int u = 0; u < kB; u++) xa[u] = xn[u];
-        }
         rslot += rstep;
         if (rslot >= rg) rslot -= rg;
     }
 }
 
-// ---- wave 0: the accumulation in u_avx's order ----------------------------------------------------
+// ---- control wave: the accumulation in u_avx's order ----------------------------------------------
 // Lane (l, r): chain l's accumulators of tap r (a0) and tap r + 4 (a1), both components.  Every
-// product is added in iteration order, exactly dotProdVal_{l/4}[tap] += c (:257-260).
+// product a·code is formed and added in iteration order, exactly c = _mm256_mul_ps(a, b);
+// dotProdVal_{l/4}[tap] += c (:252-260).  Scalar single-rate VALU ops (this file is built without SLP
+// packing): a dependent v_pk_add_f32 chain issues several times slower on gfx950 than two
+// interleaved v_add_f32 chains (measured: ≈ 56 vs ≈ 10 cycles per iteration of the accumulator).
 template <int NTT, int G>
-__device__ __forceinline__ void fast_accumulate(const f2* __restrict__ P, int rg, const int32_t* ready, int32_t* acc_groups, int gbase, int M, int S, int lane,
-    f2& a0, f2& a1, int pe)
+__device__ __forceinline__ void fast_accumulate(const f2* __restrict__ Pa, const float* __restrict__ Pc, int rg, const int32_t* ready, int32_t* acc_groups,
+    int gbase, int M, int S, int lane, f2& a0, f2& a1, int pe)
 {
     const int l = lane & (kAvxLanes - 1), r = lane >> 4;
     const int r0 = r < NTT ? r : 0;                      // lanes without a tap read tap 0 (discarded)
     const int r1 = (NTT > 4 && r + 4 < NTT) ? r + 4 : 0;
     const int n_groups = (S + 3) / 4;
-    a0 = f2{0.0f, 0.0f};
-    a1 = f2{0.0f, 0.0f};
+    float s0r = 0.0f, s0i = 0.0f, s1r = 0.0f, s1i = 0.0f;
     int rslot = 0;
     for (int g = 0; g < n_groups; g++) {
         lds_wait_eq(ready + rslot, gbase + g + 1);
         if (g == 0) GNSSHIP_FSTAMP(pe, 28);
         if (g == n_groups - 1) GNSSHIP_FSTAMP(pe, 29);
         const int cnt = min(4 * G, M - 4 * G * g);
-        const f2* src0 = P + (static_cast<size_t>(rslot * 4 * G) * NTT + r0) * kAvxLanes + l;
-        const f2* src1 = P + (static_cast<size_t>(rslot * 4 * G) * NTT + r1) * kAvxLanes + l;
+        const size_t j0 = static_cast<size_t>(rslot * 4 * G);
+        const f2* pa = Pa + j0 * kAvxLanes + l;
+        const float* pc0 = Pc + (j0 * NTT + r0) * kAvxLanes + l;
+        const float* pc1 = Pc + (j0 * NTT + r1) * kAvxLanes + l;
         if (cnt == 4 * G) {
             constexpr int kU = 8;  // loads in flight ahead of the dependent adds
 #pragma unroll
-            for (int j0 = 0; j0 < 4 * G; j0 += kU) {
-                f2 v0[kU], v1[kU];
+            for (int j = 0; j < 4 * G; j += kU) {
+                f2 va[kU];
+                float c0[kU], c1[kU];
 #pragma unroll
                 for (int u = 0; u < kU; u++) {
-                    v0[u] = src0[(j0 + u) * NTT * kAvxLanes];
-                    if constexpr (NTT > 4) v1[u] = src1[(j0 + u) * NTT * kAvxLanes];
+                    va[u] = pa[(j + u) * kAvxLanes];
+                    c0[u] = pc0[(j + u) * NTT * kAvxLanes];
+                    if constexpr (NTT > 4) c1[u] = pc1[(j + u) * NTT * kAvxLanes];
                 }
 #pragma unroll
                 for (int u = 0; u < kU; u++) {
-                    a0 = a0 + v0[u];
-                    if constexpr (NTT > 4) a1 = a1 + v1[u];
+                    s0r = __fadd_rn(s0r, __fmul_rn(va[u].x, c0[u]));
+                    s0i = __fadd_rn(s0i, __fmul_rn(va[u].y, c0[u]));
+                    if constexpr (NTT > 4) {
+                        s1r = __fadd_rn(s1r, __fmul_rn(va[u].x, c1[u]));
+                        s1i = __fadd_rn(s1i, __fmul_rn(va[u].y, c1[u]));
+                    }
                 }
             }
         } else {
 #pragma unroll 1
             for (int j = 0; j < cnt; j++) {
-                a0 = a0 + src0[j * NTT * kAvxLanes];
-                if constexpr (NTT > 4) a1 = a1 + src1[j * NTT * kAvxLanes];
+                const f2 va = pa[j * kAvxLanes];
+                const float c0 = pc0[j * NTT * kAvxLanes];
+                s0r = __fadd_rn(s0r, __fmul_rn(va.x, c0));
+                s0i = __fadd_rn(s0i, __fmul_rn(va.y, c0));
+                if constexpr (NTT > 4) {
+                    const float c1 = pc1[j * NTT * kAvxLanes];
+                    s1r = __fadd_rn(s1r, __fmul_rn(va.x, c1));
+                    s1i = __fadd_rn(s1i, __fmul_rn(va.y, c1));
+                }
             }
         }
         asm volatile("" ::: "memory");  // the group's loads are issued (and used) before it is released
         if (lane == 0) lds_release_store(acc_groups, gbase + g + 1);
         rslot = rslot + 1 == rg ? 0 : rslot + 1;
     }
+    a0 = f2{s0r, s0i};
+    a1 = f2{s1r, s1i};
 }
 
 // u_avx's final combination of the 16 chains (:279-291), valid at lane 0 of each 16-lane row:
@@ -564,15 +615,46 @@ __global__ __launch_bounds__(kFThreads, fast_waves_per_simd<THRU>()) void trk_fa
         int* dst = reinterpret_cast<int*>(&sc);
         for (int i = tid; i < static_cast<int>(sizeof(TrkChannel) / 4); i += kFThreads) dst[i] = src[i];
     }
-    // dynamic LDS: code replica(s) | phasor slots (rs tasks) | product ring (rg groups) | ring flags
+    // dynamic LDS: code replica(s) | phasor slots (rs tasks) | ring: sample products (rg groups) |
+    // ring: code values | ring flags
     float* code0 = lds;
     float* code1 = lds + code_cap_floats;
     uint64_t* Zs = reinterpret_cast<uint64_t*>(lds + (DATA ? 2 : 1) * code_cap_floats);
-    f2* P = reinterpret_cast<f2*>(Zs + static_cast<size_t>(rs) * kAvxLanes);
-    int32_t* ready = reinterpret_cast<int32_t*>(P + static_cast<size_t>(rg) * 4 * G * NTT * kAvxLanes);
+    f2* Pa = reinterpret_cast<f2*>(Zs + static_cast<size_t>(rs) * kAvxLanes);
+    float* Pc = reinterpret_cast<float*>(Pa + static_cast<size_t>(rg) * 4 * G * kAvxLanes);
+    int32_t* ready = reinterpret_cast<int32_t*>(Pc + static_cast<size_t>(rg) * 4 * G * NTT * kAvxLanes);
     for (int i = tid; i < rs * kAvxLanes; i += kFThreads) Zs[i] = kSlotEmpty;
     for (int i = tid; i < rg; i += kFThreads) ready[i] = 0;
+    __shared__ int32_t simd_of[kFWaves];
+    if (lane == 0) simd_of[wave] = static_cast<int32_t>((__builtin_amdgcn_s_getreg(4 | (31 << 11)) >> 4) & 3);  // HW_ID.SIMD_ID
     __syncthreads();
+    // the role of each wave: the first two waves alone on their SIMD take the phasor and control
+    // roles (in that order), the others produce; without two such SIMDs, waves 1 and 0 do
+    int role = kRoleProducer, pw = 0;
+    {
+        int cnt[4] = {0, 0, 0, 0};
+        for (int w = 0; w < kFWaves; w++) cnt[simd_of[w] & 3]++;
+        int rep = -1, ctl = -1;
+        for (int w = 0; w < kFWaves; w++)
+            if (cnt[simd_of[w] & 3] == 1) {
+                if (rep < 0) rep = w;
+                else if (ctl < 0) ctl = w;
+            }
+        if (rep < 0 || ctl < 0) {
+            rep = 1;
+            ctl = 0;
+        }
+        int np = 0;
+        for (int w = 0; w < kFWaves; w++) {
+            if (w == wave) {
+                role = w == rep ? kRoleReplay : w == ctl ? kRoleControl : kRoleProducer;
+                pw = np;
+            }
+            if (w != rep && w != ctl) np++;
+        }
+        role = __builtin_amdgcn_readfirstlane(role);
+        pw = __builtin_amdgcn_readfirstlane(pw);
+    }
     if (tid == 0) {
         const bool tracking = sc.state == 2 || sc.state == 3 || sc.state == 4;
         const bool codes_ok = sc.code_id >= 0 && sc.code_id < n_codes && codes[sc.code_id].ptr && codes[sc.code_id].len > 0 &&
@@ -589,7 +671,7 @@ __global__ __launch_bounds__(kFThreads, fast_waves_per_simd<THRU>()) void trk_fa
     }
     __syncthreads();
     if (skip) return;  // idle channel: its state is untouched
-    GNSSHIP_FHWID(20 + wave);  // epoch 0's slots 20-23 (the epoch loop stamps 0-15)
+    if (wave < 4) GNSSHIP_FHWID(20 + wave);  // epoch 0's slots 20-23 (the epoch loop stamps 0-15)
     stage_code_f(code0, codes[sc.code_id]);
     if constexpr (DATA) stage_code_f(code1, codes[sc.data_code_id]);
     __syncthreads();  // the code replicas are staged before any wave correlates
@@ -602,17 +684,18 @@ __global__ __launch_bounds__(kFThreads, fast_waves_per_simd<THRU>()) void trk_fa
     const int tail = N - kAvxLanes * M;
     const int n_groups = (S + 3) / 4;
     RChan rc;
-    if (wave == 0) rchan_load(sc, &sc, rc);
+    if (role == kRoleControl) rchan_load(sc, &sc, rc);
     // wave 0's loop parameters in registers for the run (two workgroups per CU have no registers to
     // spare: they keep reading TrkParams)
     const KFast kf = make_kfast(k, sc.geo);
     const auto& kp = loop_params<THRU>(k, kf);
     // Wave roles (one channel per workgroup, its epochs a serial chain):
-    //   wave 0 — the control wave: the accumulation in u_avx order, the loop update on its
-    //            register-resident channel (RChan) and the epoch records;
-    //   wave 1 — the phasor wave: derives the epoch's phasors (cos/sin of the NCO phase and step,
-    //            dz, the 16 lane starts) and replays them into the task slots, plus the N mod 16 tail;
-    //   waves 2, 3 — the producers of the products; wave 2 also runs the lock detectors.
+    //   control  — the accumulation in u_avx order, the loop update on its register-resident
+    //              channel (RChan) and the epoch records;
+    //   phasor   — derives the epoch's phasors (cos/sin of the NCO phase and step, dz, the 16 lane
+    //              starts) and replays them into the task slots, plus the N mod 16 tail;
+    //   producers — the products of the groups pw, pw + kFProducers, ...; producer 0 also runs the
+    //              lock detectors.
     // Wave 0 hands the next epoch's NCO arguments (the seed) to wave 1 as soon as epoch_post has
     // settled them, so the derive and the first tasks of epoch e + 1 overlap epoch e's record writes.
     uint64_t seed_start = 0;              // wave 0: the epoch start the seed was made for
@@ -667,13 +750,13 @@ __global__ __launch_bounds__(kFThreads, fast_waves_per_simd<THRU>()) void trk_fa
             publish_seq(&sh.seed_seq, e + 1);
         }
     };
-    if (wave == 0) make_seed(0);
+    if (role == kRoleControl) make_seed(0);
     int e_done = 0;
     bool cancel = false;  // wave 0: the current epoch was seeded before a lock test that failed
     for (int e = 0;; e++) {
         const int gbase = e * n_groups;  // the epoch's first product-group tag - 1
         FJob job;
-        if (wave == 1) {
+        if (role == kRoleReplay) {
             // ---- derive: the phasors of the seeded epoch ----
             wait_seq(&sh.seed_seq, e + 1);
             GNSSHIP_FSTAMP(e, 0);
@@ -691,19 +774,20 @@ __global__ __launch_bounds__(kFThreads, fast_waves_per_simd<THRU>()) void trk_fa
                 const int sfi = __builtin_bit_cast(int, sfn), cfi = __builtin_bit_cast(int, cfn);
                 const f2 p0 = f2{__builtin_bit_cast(float, __builtin_amdgcn_readlane(cfi, 0)), -__builtin_bit_cast(float, __builtin_amdgcn_readlane(sfi, 0))};
                 inc = f2{__builtin_bit_cast(float, __builtin_amdgcn_readlane(cfi, 1)), __builtin_bit_cast(float, __builtin_amdgcn_readlane(sfi, 1))};
-                // dz = normalise(inc^16) by four squarings (:215-225)
-                f2 d = inc;
-#pragma unroll
-                for (int q = 0; q < 4; q++) d = cmul_exact(d, d);
-                const f2 dz = normalise_avx(d);
-                // z_l = phase·inc^l, the generic chain (:204-208), for the replay's lane pairs
-                f2 z = p0;
+                GNSSHIP_FSTAMP(e, 35);
+                // z_l = phase·inc^l, the generic chain (:204-208), for the replay's lane pairs, and
+                // dz = normalise(inc^16) by four squarings (:215-225): two independent chains of
+                // scalar exact products (a dependent packed product issues several times slower)
+                f2 w = p0, z = p0, d = inc;
 #pragma unroll
                 for (int i = 0; i < kAvxLanes - 1; i++) {
-                    const f2 zi = cmul_exact(z, inc);
-                    z = i < (lane >> 1) ? zi : z;  // lanes 2l, 2l + 1: chain l
+                    w = cmul_exact_sc(w, inc);
+                    if (i < 4) d = cmul_exact_sc(d, d);
+                    z = i + 1 == (lane >> 1) ? w : z;  // lanes 2l, 2l + 1: chain l (off the chain)
                 }
+                const f2 dz = normalise_avx(d);
                 zinit = z;
+                GNSSHIP_FSTAMP(e, 36);
                 if (lane == 0) {
                     sh.job.dz_re = dz.x;
                     sh.job.dz_im = dz.y;
@@ -740,14 +824,14 @@ __global__ __launch_bounds__(kFThreads, fast_waves_per_simd<THRU>()) void trk_fa
         wait_seq(&sh.job_seq, e + 1);
         job = uniform_job(sh.job);
         if (!job.runnable) break;
-        if (wave >= 2) {
+        if (role == kRoleProducer) {
             const i4v span = sample_span<FMT>(samples, job.off, N);
             if (job.in_margin)
-                fast_produce<FMT, NT, DATA, true, G>(job, span, c0, c1, L, Zs, rs, P, rg, ready, &sh.acc_groups, gbase, lane, wave - 2, e);
+                fast_produce<FMT, NT, DATA, true, G>(job, span, c0, c1, L, Zs, rs, Pa, Pc, rg, ready, &sh.acc_groups, gbase, lane, pw, e);
             else
-                fast_produce<FMT, NT, DATA, false, G>(job, span, c0, c1, L, Zs, rs, P, rg, ready, &sh.acc_groups, gbase, lane, wave - 2, e);
-            GNSSHIP_FSTAMP(e, 1 + wave);  // 3, 4: each producer done
-            if (wave == 2) {
+                fast_produce<FMT, NT, DATA, false, G>(job, span, c0, c1, L, Zs, rs, Pa, Pc, rg, ready, &sh.acc_groups, gbase, lane, pw, e);
+            if (pw < 2) GNSSHIP_FSTAMP(e, 3 + pw);  // 3, 4: producers 0 and 1 done
+            if (pw == 0) {
                 // cn0_and_tracking_lock_status (:972-1029) on the LDS copy of its members, beside the loop update
                 wait_seq(&sh.pre_seq, e + 1);
                 const double coh = sh.coh;
@@ -764,7 +848,7 @@ __global__ __launch_bounds__(kFThreads, fast_waves_per_simd<THRU>()) void trk_fa
         {
             f2 a0, a1;
             GNSSHIP_FSTAMP(e, 27);
-            fast_accumulate<NTT, G>(P, rg, ready, &sh.acc_groups, gbase, M, S, lane, a0, a1, e);
+            fast_accumulate<NTT, G>(Pa, Pc, rg, ready, &sh.acc_groups, gbase, M, S, lane, a0, a1, e);
             GNSSHIP_FSTAMP(e, 5);
             f2 t0 = f2{avx_chain_sum(a0.x), avx_chain_sum(a0.y)};
             f2 t1 = f2{0.0f, 0.0f};
@@ -843,6 +927,7 @@ __global__ __launch_bounds__(kFThreads, fast_waves_per_simd<THRU>()) void trk_fa
                 if (rc.state == 4) {
                     epoch_consume(kp, rc);
                     make_seed(e + 1);
+                    GNSSHIP_FSTAMP(e, 33);
                     rc.epoch_start = es;  // epoch_post and the record still describe this epoch
                     seeded = true;
                 }
@@ -896,7 +981,7 @@ __global__ __launch_bounds__(kFThreads, fast_waves_per_simd<THRU>()) void trk_fa
             GNSSHIP_FCLK(e, 15);
         }
     }
-    if (wave == 0 && lane == 0) {
+    if (role == kRoleControl && lane == 0) {
         rchan_store(rc, sc);
         sc.ran = 0;
         if (e_done > 0) atomicAdd(ran_count + e_done - 1, 1);  // rounds_done = the longest channel's epochs
@@ -926,6 +1011,19 @@ namespace gnsship {
 // chain, C2 profiling build: 8.24 -> 8.00 us per epoch); the whole epoch's slots and products when
 // they fit, otherwise a product ring of as many groups as fit (at least 2), with the slots in a ring
 // of 16 groups when the whole epoch's slots leave too little room.  `bytes` 0: no plan fits.
+// Compute units of the current device (the "more channels than CUs" switch), queried once per device.
+static int device_cus()
+{
+    static int cache[64] = {0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+    if (cache[dev] == 0) {
+        int n = 0;
+        cache[dev] = (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0) ? n : 256;
+    }
+    return cache[dev];
+}
+
 struct FastPlan {
     size_t bytes = 0;
     int G = 8, rs = 0, rg = 0;
@@ -943,9 +1041,9 @@ static FastPlan fast_plan(const TrkParams& p, int code_cap_floats, int n_chans)
     const int ntt = p.n_taps + (p.jobs_per_channel > 1 ? 1 : 0);
     const size_t codes = static_cast<size_t>(p.jobs_per_channel > 1 ? 2 : 1) * code_cap_floats * sizeof(float);
     const size_t slot_b = kAvxLanes * sizeof(uint64_t);
-    const size_t group_b = static_cast<size_t>(4 * G) * ntt * kAvxLanes * 2 * sizeof(float) + sizeof(int32_t);
+    const size_t group_b = static_cast<size_t>(4 * G) * kAvxLanes * (2 + ntt) * sizeof(float) + sizeof(int32_t);  // products, codes, flag
     // more channels than CUs: two workgroups per CU share its LDS
-    size_t budget = n_chans > 256 ? 72 * 1024 : kTrkPersistMaxLds;
+    size_t budget = n_chans > device_cus() ? 72 * 1024 : kTrkPersistMaxLds;
     if (const char* env = std::getenv("GNSSHIP_TRK_FAST_LDS"))  // tests: a smaller budget forces the rings
         budget = std::min(budget, static_cast<size_t>(std::atol(env)) * 1024);
     auto fit = [&](int rs) -> int {  // product groups that fit beside `rs` slots (0: fewer than 2)
@@ -983,7 +1081,7 @@ bool trk_fast_supported(const TrkParams& p, int code_cap_floats, int n_chans)
     // More channels than CUs: channel-epochs per second, not epoch latency, is what counts, and
     // trk_persist.hip's four equal correlating waves sustain more of them (measured at 65536
     // channels: 76.6 M vs 64.8 M channel-epochs/s)
-    if (n_chans > 256) return false;
+    if (n_chans > device_cus()) return false;
     return fast_plan(p, code_cap_floats, n_chans).bytes > 0;
 }
 
@@ -997,7 +1095,7 @@ hipError_t launch_trk_fast(const TrkParams* params_dev, const TrkParams& params,
     const int S = std::max(1, (N / kAvxLanes + f.G - 1) / f.G);
     const bool sring = f.rs < S;
     const bool data = params.jobs_per_channel > 1;
-    bool thru = n_chans > 256;
+    bool thru = n_chans > device_cus();
     if (const char* env = std::getenv("GNSSHIP_TRK_THRU")) thru = env[0] == '1';
     const int nt = params.n_taps;
     dim3 grid(n_chans), block(kFThreads);

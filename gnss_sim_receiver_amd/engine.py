@@ -535,10 +535,15 @@ class DllPllVemlTracking:
                                               int(records), int(dump)), "gnsship_trk_launch", self.ctx.h)
         self._pending = (max_rounds, records, dump)
 
-    def collect(self):
-        """gnsship_trk_collect for the last launch_ptr: (records or None, rounds_done[, dump])."""
+    def collect(self, out: np.ndarray = None):
+        """gnsship_trk_collect for the last launch_ptr: (records or None, rounds_done[, dump]).
+        out: a caller's (max_rounds, max_channels) TRK_EPOCH_DTYPE array to fill (reused buffers)."""
         max_rounds, records, dump = self._pending
-        out = np.zeros((max_rounds, self.max_channels), abi.TRK_EPOCH_DTYPE) if records else None
+        if out is not None:
+            if not records or out.dtype != abi.TRK_EPOCH_DTYPE or out.shape != (max_rounds, self.max_channels) or not out.flags.c_contiguous:
+                raise ValueError("collect(out=): a C-contiguous (max_rounds, max_channels) TRK_EPOCH_DTYPE array, records launched")
+        else:
+            out = np.zeros((max_rounds, self.max_channels), abi.TRK_EPOCH_DTYPE) if records else None
         dmp = np.zeros((max_rounds, self.max_channels), abi.TRK_DUMP_DTYPE) if dump else None
         done = ctypes.c_int()
         check(self.ctx.lib.gnsship_trk_collect(self.h, out.ctypes.data if records else None, dmp.ctypes.data if dump else None,

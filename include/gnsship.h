@@ -429,7 +429,8 @@ int gnsship_trk_run_dump(gnsship_trk* t, const void* sig, int fmt, int sig_on_de
  * requested.  Engines on different contexts of one device then run concurrently from one host
  * thread (e.g. a hybrid receiver's GPS, Galileo and BeiDou engines over one IF block).  Every launch
  * is followed by exactly one gnsship_trk_collect, which waits for it and copies the records
- * (out / dump as in gnsship_trk_run_dump, NULL to skip). */
+ * (out / dump as in gnsship_trk_run_dump, NULL to skip; a non-NULL out / dump that the launch did not
+ * keep — want_records / want_dump 0 — is GNSSHIP_E_INVAL, the buffer untouched, the launch finished). */
 int gnsship_trk_launch(gnsship_trk* t, const void* dev_sig, int fmt, uint64_t buffer_first_sample, int64_t n_buffer_samples, int max_rounds,
     int want_records, int want_dump);
 int gnsship_trk_collect(gnsship_trk* t, gnsship_trk_epoch* out, gnsship_trk_dump_record* dump, int* rounds_done);

@@ -249,3 +249,91 @@ def test_c5_share_engines_concurrent_match_oracle(ctx):
         trks[system].close()
         dev[system].free()
         ctxs[system].close()
+
+
+def if_on_device(fs, n, sats, seed, start):
+    """The IF model (signals.generate_if_device) evaluated on the GPU with torch, returned to the host:
+    hundreds of satellites at 50 Msps take minutes on the host."""
+    import torch
+    x = signals.generate_if_device(fs, n, sats, seed=seed, start=start, device="cuda")
+    out = x.cpu().numpy()
+    del x
+    torch.cuda.empty_cache()
+    return out
+
+
+def c5_full_sky():
+    """configs[4] whole: 96 GPS + 96 Galileo E1 + 64 BeiDou B1I MEO channels, every channel its own
+    signal (PRNs re-used with their own Doppler, delay and phase beyond each system's PRN count)."""
+    rng = np.random.default_rng(0x6E550006)
+    sky = {}
+    for system, prns in (("GPS", (list(range(1, 33)) * 3)[:96]), ("GAL", (list(range(1, 37)) * 3)[:96]), ("BDS", (list(range(6, 59)) * 2)[:64])):
+        sky[system] = [signals.Satellite(prn=int(p), doppler_hz=float(rng.uniform(-4000, 4000)), code_delay_chips=float(rng.uniform(0, 1000)),
+                                         cn0_dbhz=47.0, system=system, carrier_phase_rad=float(rng.uniform(0, 6.28)), f_if_hz=IF_OF[system],
+                                         **S.SYNC_PATTERNS[system]) for p in prns]
+    return sky
+
+
+def test_c5_full_256_channels_one_gpu(ctx):
+    """configs[4] at its BASELINE channel count on one GPU (the 8-GPU split divides exactly this): three
+    engines — 96 GPS (N = 50000), 96 E1 (5 VEML + data prompt, N = 200000), 64 B1I (N = 50000) — on three
+    streams over one 50 Msps ibyte block with the IF in the NCO, launched together.  A sampled subset of
+    channels of every system is checked bit for bit against the oracle (traced taps on the device's own
+    arguments, and every record against the oracle loop); every channel's state is checked."""
+    import concurrent.futures as cf
+    sky = c5_full_sky()
+    seconds = 0.3
+    first = int(FS)
+    n = int(seconds * FS) + 4 * 200000
+    allsats = sky["GPS"] + sky["GAL"] + sky["BDS"]
+    x = if_on_device(FS, n, allsats, seed=0x6E550006, start=first)
+    raw = signals.to_ibyte(x)
+    xf = raw.astype(np.float32).view(np.complex64)
+    del x
+    ctxs = {s: engine.Context(0) for s in ("GPS", "GAL", "BDS")}
+    dev, trks, confs = {}, {}, {}
+    start = {}
+    for system, sats in sky.items():
+        cx = ctxs[system]
+        vl = int(round(FS * T.SYSTEMS[system][2]))
+        k = T.conf(system, FS, vl, pull_in_time_s=0, if_hz=IF_OF[system], rotator_avx=1)
+        confs[system] = k
+        trk = engine.DllPllVemlTracking(cx, dev_conf(k, system), len(sats))
+        for ch, s in enumerate(sats):
+            cx.set_code(2 * ch, s.code)
+            if s.code_data is not None:
+                cx.set_code(2 * ch + 1, s.code_data)
+            start[(system, ch)] = (S.acq_delay_for(s, FS, system, 0, first) + 0.2, s.doppler_hz + 15.0)
+            trk.start(ch, 2 * ch, *start[(system, ch)], 0, first, data_code_id=2 * ch + 1, prn=s.prn)
+        trk.set_trace(True)
+        dev[system] = cx.upload(raw)
+        trks[system] = trk
+    rounds = {"GPS": int(seconds * 1000), "GAL": int(seconds * 250), "BDS": int(seconds * 1000)}
+    for system, trk in trks.items():
+        trk.launch_ptr(dev[system].ptr, abi.FMT_CI8, first, len(raw), rounds[system], records=True)
+    got = {system: trk.collect() for system, trk in trks.items()}
+    traces = {system: trk.trace(rounds[system]) for system, trk in trks.items()}
+    states = {system: trk.states() for system, trk in trks.items()}
+    for system in trks:
+        trks[system].close()
+        dev[system].free()
+        ctxs[system].close()
+    sample = [("GPS", c) for c in (0, 31, 50, 95)] + [("GAL", c) for c in (0, 35, 61, 95)] + [("BDS", c) for c in (0, 29, 63)]
+
+    def oracle(args):
+        system, ch = args
+        s = sky[system][ch]
+        return T.track(confs[system], xf, s.code, *start[(system, ch)], 0, first, rounds[system], data_code=s.code_data, buffer_first=first,
+                       prn=s.prn)
+
+    with cf.ThreadPoolExecutor(8) as ex:
+        refs = dict(zip(sample, ex.map(oracle, sample)))
+    for (system, ch), ref in refs.items():
+        label = f"C5 full {system} ch{ch}"
+        s = sky[system][ch]
+        trace_exact(traces[system][:, ch], xf, first, s.code, s.code_data, label)
+        compare_exact(got[system][0][:, ch], ref, label)
+    for system, st in states.items():  # every channel still tracking; E1 and B1I synchronised (secondary / NH code)
+        assert np.all(st >= 2), (system, np.bincount(st))
+        if system != "GPS":
+            assert np.mean(np.isin(st, (3, 4))) >= 0.9, (system, np.bincount(st))

@@ -308,3 +308,30 @@ def test_idle_channel_with_empty_code_slot():
         assert not np.any(rec[:, 0]["flags"]) and not np.any(rec[:, 1]["flags"])
         compare(rec[:, 2], T.track(k, x, sat.code, delay, dop, stamp, first, 30), "idle")
         trk.close()
+
+
+def test_auto_rotator_with_unreproduced_preference_fails_create(tmp_path):
+    """ROTATOR_AUTO (every binding's default) under a volk_gnsssdr preference entry the engine does
+    not reproduce (generic_reload): gnsship_trk_create fails with E_INVAL and the dispatcher's detail,
+    instead of running another rotator silently.  A child process, so the preference file
+    is the one the library reads."""
+    import os
+    import subprocess
+    import sys
+    cfg = tmp_path / "cfg" / "volk_gnsssdr"
+    cfg.mkdir(parents=True)
+    (cfg / "volk_gnsssdr_config").write_text("volk_gnsssdr_32fc_32f_rotator_dot_prod_32fc_xn generic_reload generic_reload\n")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = ("import sys; sys.path.insert(0, %r)\n"
+            "from gnss_sim_receiver_amd import abi, engine\n"
+            "ctx = engine.Context(0)\n"
+            "c = abi.TrkConf.defaults(abi.SYS_GPS_L1CA, 4e6, 4000)\n"
+            "assert c.rotator == abi.ROTATOR_AUTO\n"
+            "try:\n    engine.DllPllVemlTracking(ctx, c, 1)\n    print('CREATED')\n"
+            "except abi.GnssHipError as e:\n    print('ERR', e)\n") % root
+    env = {k: v for k, v in os.environ.items() if k not in ("VOLK_GENERIC",)}
+    env["VOLK_CONFIGPATH"] = str(tmp_path / "cfg")
+    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    last = out.stdout.strip().splitlines()[-1]
+    assert last.startswith("ERR") and "E_INVAL" in last and "generic_reload" in last, last

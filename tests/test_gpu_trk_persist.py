@@ -220,3 +220,50 @@ def test_c4_share_8_e1_channels_closed_loop_matches_oracle(ctx):
         label = f"C4 share channel {ch} (PRN {sats[ch].prn})"
         trace_exact(tr[:, ch], x, first, sats[ch].code, sats[ch].code_data, label)
         compare_exact(rec[:, ch], ref, label)
+
+
+def test_c4_full_64_e1_channels_one_engine(ctx):
+    """configs[3] (C4) at its BASELINE channel count on one GPU: 64 Galileo E1 B/C channels (PRNs 1-36,
+    then PRNs re-used with their own Doppler / delay / phase) on one engine at 25 Msps,
+    90 epochs.  Eight sampled channels bit for bit against the oracle (traced taps and records); all
+    64 synchronised to the CS25 pilot code (state 4)."""
+    import concurrent.futures as cf
+
+    from gnss_sim_receiver_amd import signals
+    from test_gpu_c5_closed_loop import if_on_device, trace_exact
+
+    fs, epochs = 25e6, 90
+    rng = np.random.default_rng(0x6E550007)
+    prns = (list(range(1, 37)) * 2)[:64]
+    sats = [signals.Satellite(prn=p, doppler_hz=float(rng.uniform(-4000, 4000)), code_delay_chips=float(rng.uniform(0, 4000)), cn0_dbhz=48.0,
+                              system="GAL", carrier_phase_rad=float(rng.uniform(0, 6.28)), **S.SYNC_PATTERNS["GAL"]) for p in prns]
+    k = T.conf("GAL", fs, int(round(fs * T.SYSTEMS["GAL"][2])), pull_in_time_s=0, rotator_avx=1)
+    first = int(fs)
+    x = if_on_device(fs, int(round(fs)) // 4 + k.vector_length * (epochs + 3), sats, seed=0x6E550007, start=first)
+    c = dev_conf(k, "GAL")
+    c.rotator = abi.ROTATOR_AVX
+    trk = engine.DllPllVemlTracking(ctx, c, len(sats))
+    starts = []
+    for ch, s in enumerate(sats):
+        ctx.set_code(400 + 2 * ch, s.code)
+        ctx.set_code(401 + 2 * ch, s.code_data)
+        starts.append((S.acq_delay_for(s, fs, "GAL", 0, first) + 0.2, s.doppler_hz + 15.0))
+        trk.start(ch, 400 + 2 * ch, starts[-1][0], starts[-1][1], 0, first, data_code_id=401 + 2 * ch, prn=s.prn)
+    trk.set_trace(True)
+    rec, rounds = trk.run(x, first, epochs)
+    tr = trk.trace(epochs)
+    st = trk.states()
+    trk.close()
+    assert np.all(st == 4), np.bincount(st)
+    sample = [0, 9, 18, 27, 36, 45, 54, 63]
+
+    def oracle(ch):
+        s = sats[ch]
+        return T.track(k, x, s.code, starts[ch][0], starts[ch][1], 0, first, epochs, data_code=s.code_data, buffer_first=first, prn=s.prn)
+
+    with cf.ThreadPoolExecutor(8) as ex:
+        refs = list(ex.map(oracle, sample))
+    for ch, ref in zip(sample, refs):
+        label = f"C4 full channel {ch} (PRN {sats[ch].prn})"
+        trace_exact(tr[:, ch], x, first, sats[ch].code, sats[ch].code_data, label)
+        compare_exact(rec[:, ch], ref, label)
