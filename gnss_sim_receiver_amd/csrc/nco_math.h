@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include "glibc_atanf.h"
+#include "glibc_logf.h"
 #include "glibc_sincosf.h"
 
 namespace gnsship {

@@ -101,6 +101,10 @@ constexpr int kFProducers = kFWaves - 2;  // every wave but the control and phas
 // phasor chain is the epoch's critical path and the control wave's loop update is the next — and the
 // producers share the other SIMDs (two producer waves on a SIMD interleave their issue).
 constexpr int kRoleControl = 0, kRoleReplay = 1, kRoleProducer = 2;
+// Polling waves back off this many s_sleep units (≈ 64 cycles each) between LDS polls.
+#ifndef GNSSHIP_POLL_SLEEP
+#define GNSSHIP_POLL_SLEEP 0
+#endif
 constexpr uint64_t kSlotEmpty = ~0ull;  // an unwritten phasor slot (NaN, NaN)
 
 // The epoch's correlation as the producers need it (LDS: the seed from wave 0, dz from wave 1).
@@ -164,7 +168,7 @@ __device__ __forceinline__ void publish_seq(int32_t* p, int v)
 }
 __device__ __forceinline__ void wait_seq(int32_t* p, int need)
 {
-    while (__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < need) __builtin_amdgcn_s_sleep(0);
+    while (__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < need) __builtin_amdgcn_s_sleep(GNSSHIP_POLL_SLEEP);
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
@@ -178,12 +182,12 @@ __device__ __forceinline__ void lds_release_store(int32_t* p, int v)
 }
 __device__ __forceinline__ void lds_wait_eq(const int32_t* p, int v)
 {
-    while (__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != v) __builtin_amdgcn_s_sleep(0);
+    while (__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != v) __builtin_amdgcn_s_sleep(GNSSHIP_POLL_SLEEP);
     asm volatile("" ::: "memory");
 }
 __device__ __forceinline__ void lds_wait_ge(const int32_t* p, int v)
 {
-    while (__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < v) __builtin_amdgcn_s_sleep(0);
+    while (__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < v) __builtin_amdgcn_s_sleep(GNSSHIP_POLL_SLEEP);
     asm volatile("" ::: "memory");
 }
 
@@ -317,7 +321,7 @@ __device__ __forceinline__ float fast_replay(float x, float c, float k2, int M, 
             if (t >= rs) {
                 uint32_t v = next_state;
                 while (v != ~0u) {
-                    __builtin_amdgcn_s_sleep(0);
+                    __builtin_amdgcn_s_sleep(GNSSHIP_POLL_SLEEP);
                     v = __hip_atomic_load(half0 + 2 * kAvxLanes * ts, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 }
             }
@@ -331,7 +335,7 @@ __device__ __forceinline__ float fast_replay(float x, float c, float k2, int M, 
             off = base + static_cast<uint32_t>(ts) * kSlotRow;
         }
         if (S - 1 >= rs)
-            while (__hip_atomic_load(half0 + 2 * kAvxLanes * ts, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != ~0u) __builtin_amdgcn_s_sleep(0);
+            while (__hip_atomic_load(half0 + 2 * kAvxLanes * ts, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != ~0u) __builtin_amdgcn_s_sleep(GNSSHIP_POLL_SLEEP);
     }
     // the last task: its producers continue it
     __hip_atomic_store(half0 + 2 * kAvxLanes * ts, __builtin_bit_cast(uint32_t, x), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -448,7 +452,7 @@ __device__ __forceinline__ void fast_produce(const FJob& job, i4v span, const fl
         uint64_t v = kSlotEmpty;
         if (active) {
             // written when neither 32-bit half is the sentinel any more (two replay lanes write it)
-            while (static_cast<uint32_t>(v = load_slot(slot)) == ~0u || static_cast<uint32_t>(v >> 32) == ~0u) __builtin_amdgcn_s_sleep(0);
+            while (static_cast<uint32_t>(v = load_slot(slot)) == ~0u || static_cast<uint32_t>(v >> 32) == ~0u) __builtin_amdgcn_s_sleep(GNSSHIP_POLL_SLEEP);
             store_slot(slot, __builtin_bit_cast(f2, kSlotEmpty));  // re-armed for the next lap / epoch
         }
         if (g == pw && pw == 0) GNSSHIP_FSTAMP(pe, 30);

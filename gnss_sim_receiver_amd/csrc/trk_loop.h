@@ -97,7 +97,8 @@ __device__ float cn0_m2m4(const float* prompt, int length, float coh_integration
     m_4 = __fdiv_rn(m_4, n);
     aux = sqrt_rn_f32(__fsub_rn(__fmul_rn(__fmul_rn(2.0f, m_2), m_2), m_4));
     const float snr = isnan(aux) ? __fdiv_rn(psig, __fsub_rn(m_2, psig)) : __fdiv_rn(aux, __fsub_rn(m_2, aux));
-    return __fsub_rn(__fmul_rn(10.0f, log10f(snr)), __fmul_rn(10.0f, log10f(coh_integration_time_s)));
+    // glibc's log10f (glibc_logf.h): the CN0 the reference computes, to the bit
+    return __fsub_rn(__fmul_rn(10.0f, glibc_log10f(snr)), __fmul_rn(10.0f, glibc_log10f(coh_integration_time_s)));
 }
 
 __device__ float carrier_lock_detector(const float* prompt)  // called with length 1 (:989)
@@ -517,6 +518,7 @@ __device__ void run_dll_pll(const K& k, C& c)
     else
         disc = static_cast<double>(glibc_atan2f(c.p[1], c.p[0]));  // gr::fast_atan2f restated as atan2f (glibc_atanf.h)
     c.carr_phase_error_hz = disc / kTwoPi;
+    GNSSHIP_TRK_LOOP_STAMP(37);
     // d_current_correlation_time_s: the code period, or extend × code period once extended
     const float T = c.narrow ? syncset(k, c).T_ext : static_cast<float>(k.code_period);
     if ((c.pull_in && k.conf.enable_fll_pull_in) || k.conf.enable_fll_steady_state) {  // :1080-1097
@@ -531,6 +533,7 @@ __device__ void run_dll_pll(const K& k, C& c)
         c.carr_error_filt_hz = carrier_filter(k, c, 0.0f, static_cast<float>(c.carr_phase_error_hz), T);
     }
     c.carrier_doppler_hz = c.carr_error_filt_hz;
+    GNSSHIP_TRK_LOOP_STAMP(38);
     if (k.veml) {
         const double early = static_cast<double>(sqrt_rn_f32(__fadd_rn(__fadd_rn(__fadd_rn(__fmul_rn(c.ve[0], c.ve[0]), __fmul_rn(c.ve[1], c.ve[1])),
                                                                           __fmul_rn(c.e[0], c.e[0])),
@@ -548,7 +551,9 @@ __device__ void run_dll_pll(const K& k, C& c)
         const float norm = __fdiv_rn(__fsub_rn(k.conf.y_intercept, __fmul_rn(slope, c.spc)), slope);
         c.code_error_chips = (s == 0.0) ? 0.0 : static_cast<double>(norm) * (pe - pl) / s;
     }
+    GNSSHIP_TRK_LOOP_STAMP(39);
     c.code_error_filt_chips = loop_filter_apply(k, c, static_cast<float>(c.code_error_chips));
+    GNSSHIP_TRK_LOOP_STAMP(40);
     c.code_freq_chips = k.code_chip_rate - c.code_error_filt_chips;
     if (k.conf.carrier_aiding) c.code_freq_chips += c.carrier_doppler_hz * k.code_chip_rate / k.carrier_freq;
 }

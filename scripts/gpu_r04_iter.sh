@@ -4,7 +4,7 @@ R=$GRAFT_REPO_ROOT
 cd $R
 O=$R/gpurun_out/r04iter
 mkdir -p $O
-timeout -k 10 300 python -u -m pytest tests/test_gpu_headline_pin.py tests/test_gpu_trk_persist.py -m gpu -q -x --timeout 200 --timeout-method thread ${PYTEST_K:-} > $O/tests.log 2>&1
+timeout -k 10 600 python -u -m pytest tests/test_gpu_headline_pin.py tests/test_gpu_trk_persist.py tests/test_gpu_c5_closed_loop.py tests/test_gpu_trk.py -m gpu -q --timeout 280 --timeout-method thread ${PYTEST_K:-} > $O/tests.log 2>&1
 rc=$?; echo "tests rc=$rc"; grep -E "^FAILED|^ERROR|passed|failed|Error" $O/tests.log | tail -12
 [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit 1
 timeout -k 10 120 python3 scripts/trk_fast_profile.py 12 > $O/fast_phases.txt 2>&1 || { echo "phase profile failed"; tail $O/fast_phases.txt; exit 1; }
@@ -13,3 +13,5 @@ timeout -k 10 300 python -u bench.py --no-aux --cpu-seconds 0 > $O/bench.json 2>
 python3 -c "import json;d=json.load(open('$O/bench.json'));print('value',d['value'],'us/epoch',d['us_per_epoch'])"
 GNSSHIP_LIB_PATH=$R/scripts/libgnsship_prof4.so timeout -k 10 120 python3 scripts/trk_fast_profile.py 12 > $O/fast_phases4.txt 2>&1 || { echo "phase profile 4 failed"; tail $O/fast_phases4.txt; exit 1; }
 echo "---- 4 waves"; head -30 $O/fast_phases4.txt
+GNSSHIP_LIB_PATH=$R/scripts/libgnsship_prof_s2.so timeout -k 10 120 python3 scripts/trk_fast_profile.py 12 > $O/fast_phases_s2.txt 2>&1 || { echo "phase profile s2 failed"; tail $O/fast_phases_s2.txt; exit 1; }
+echo "---- poll sleep 2"; head -45 $O/fast_phases_s2.txt | grep -v HW_ID

@@ -64,7 +64,7 @@ def main():
             ("  tracking_vars -> loop done", 11, 7), ("loop done -> next derive", 7, 48), ("  taps -> epoch_pre done", 16, 17),
             ("  epoch_pre -> published", 17, 18), ("  published -> run_dll_pll", 18, 9), ("  lock_status (wave 2)", 8, 26),
             ("  tracking_vars -> lock seen", 11, 19), ("  lock seen -> epoch_post done", 19, 24), ("  epoch_finish", 24, 25),
-            ("  epoch_finish -> loop done (records)", 25, 7), ("seed (tracking_vars) -> next derive start", 11, 48), ("  tracking_vars -> seed published", 11, 33), ("  seed published -> next derive start", 33, 48), ("derive: sincos", 0, 35), ("derive: chains", 35, 36), ("derive: dz + publish", 36, 1),
+            ("  epoch_finish -> loop done (records)", 25, 7), ("seed (tracking_vars) -> next derive start", 11, 48), ("  tracking_vars -> seed published", 11, 33), ("  seed published -> next derive start", 33, 48), ("derive: sincos", 0, 35), ("derive: chains", 35, 36), ("derive: dz + publish", 36, 1), ("  run_dll_pll: PLL discriminator", 9, 37), ("  run_dll_pll: carrier filter", 37, 38), ("  run_dll_pll: DLL discriminator", 38, 39), ("  run_dll_pll: code loop filter", 39, 40), ("  run_dll_pll: code freq", 40, 10),
             ("derive -> wave 0 starts accumulating", 1, 27), ("derive -> group 0 seen by wave 0", 1, 28), ("derive -> last group seen by wave 0", 1, 29),
             ("derive -> producer 2 has group 0's slots", 1, 30), ("derive -> producer 3 has its last group's slots", 1, 31),
             ("last group seen -> accumulation done", 29, 5)]

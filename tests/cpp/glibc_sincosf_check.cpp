@@ -10,10 +10,12 @@
 //   glibc_sincosf_check fma                        1 if the CPU has FMA (glibc then runs its FMA build)
 //   FN=atan (environment): the same modes for atanf, and atan2f(x, 1 / x), atan2f(x, −x), atan2f(−x, y)
 //                                                  with y the next random draw
+//   FN=log: the same modes for logf and log10f (glibc_logf.h)
 // Prints "checked N mismatches M" (and the first few mismatching arguments); exit 0 iff M == 0.
 #define GNSSHIP_HD
 #include "../../gnss_sim_receiver_amd/csrc/glibc_sincosf.h"
 #include "../../gnss_sim_receiver_amd/csrc/glibc_atanf.h"
+#include "../../gnss_sim_receiver_amd/csrc/glibc_logf.h"
 
 #include <cmath>
 #include <cstdio>
@@ -35,7 +37,17 @@ std::atomic<int> g_printed{0};
 
 bool same(float a, float b) { return std::memcmp(&a, &b, 4) == 0 || (std::isnan(a) && std::isnan(b)); }
 
-bool g_atan = false;
+bool g_atan = false, g_log = false;
+
+void check_log(float x)
+{
+    const float a = gnsship::glibc_logf(x), ha = ::logf(x);
+    const float b = gnsship::glibc_log10f(x), hb = ::log10f(x);
+    if (!same(a, ha) || !same(b, hb)) {
+        g_bad++;
+        if (g_printed++ < 8) std::printf("mismatch x=%a: logf %a/%a log10f %a/%a\n", x, a, ha, b, hb);
+    }
+}
 
 void check_atan(float x, float y)
 {
@@ -51,6 +63,10 @@ void check_atan(float x, float y)
 
 void check_one(float x)
 {
+    if (g_log) {
+        check_log(x);
+        return;
+    }
     if (g_atan) {
         const uint32_t h = __builtin_bit_cast(uint32_t, x) * 2654435761u;
         check_atan(x, __builtin_bit_cast(float, (h & 0x807fffffu) | (__builtin_bit_cast(uint32_t, x) & 0x7f800000u) ^ ((h >> 8) & 0x07800000u)));
@@ -85,7 +101,10 @@ void parallel(uint64_t n, F f)
 int main(int argc, char** argv)
 {
     if (argc < 2) return 2;
-    if (const char* f = std::getenv("FN")) g_atan = !std::strcmp(f, "atan");
+    if (const char* f = std::getenv("FN")) {
+        g_atan = !std::strcmp(f, "atan");
+        g_log = !std::strcmp(f, "log");
+    }
     const char* mode = argv[1];
     uint64_t n = 0;
     if (!std::strcmp(mode, "fma")) {

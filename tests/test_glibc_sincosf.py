@@ -1,8 +1,8 @@
-"""The device's libm restatements (gnss_sim_receiver_amd/csrc/glibc_sincosf.h, glibc_atanf.h) against
+"""The device's libm restatements (gnss_sim_receiver_amd/csrc/glibc_sincosf.h, glibc_atanf.h, glibc_logf.h) against
 this host's own glibc, bit for bit: the tracking engines' carrier phasors are the reference's
 (cos rem, −sin rem) and exp(−j·step) (cpu_multicorrelator_real_codes.cc:115,123 → glibc cosf / sinf /
-cexpf → __sincosf), and the loop's discriminators its atanf / atan2f (tracking_discriminators.cc:
-68-104).  The headers are compiled for the host (tests/cpp/glibc_sincosf_check.cpp, -ffp-contract=off,
+cexpf → __sincosf), the loop's discriminators its atanf / atan2f (tracking_discriminators.cc:
+68-104), and the CN0 estimate its log10f (lock_detectors.cc:119, log10f → the ifunc'd FMA logf).  The headers are compiled for the host (tests/cpp/glibc_sincosf_check.cpp, -ffp-contract=off,
 as the device objects are built) and compared with sinf / cosf / sincosf / atanf / atan2f on:
   * every float in [0.5, 1) (8.4 M: the C5 steps' binade) and in [2^-8, 2^-7) (the C2 steps' binade),
   * 5 M uniform in ±7 rad (rem_carr after fmod(·, 2π), IF folded in),
@@ -10,8 +10,8 @@ as the device objects are built) and compared with sinf / cosf / sincosf / atanf
   * 5 M random bit patterns (the whole float line: the large-argument reduction, tiny and special values);
 ≥ 20 M arguments in all.  glibc picks its FMA build of sinf/cosf on FMA hosts (every AVX2 server,
 the GPU box's EPYC included); the restatement is that build, so the test requires FMA.
-(One-off exhaustive runs here: every float with |x| < 120 for sin/cos — 2.25e9 arguments — and every
-float for atanf, 0 mismatches)"""
+(One-off exhaustive runs here: every float with |x| < 120 for sin/cos — 2.25e9 arguments — every float
+for atanf / atan2f and every positive float for logf / log10f, 0 mismatches)"""
 import math
 import os
 import subprocess
@@ -65,4 +65,12 @@ def test_atanf_atan2f_match_host_glibc(checker):
     n += run(checker, "uniform", 5_000_000, 11, -4.0, 4.0, fn="atan")
     n += run(checker, "random", 5_000_000, 12, fn="atan")
     n += run(checker, "range", f32_bits(0.4375), f32_bits(2.4375), fn="atan")
+    assert n >= 10_000_000
+
+
+def test_logf_log10f_match_host_glibc(checker):
+    n = 0
+    n += run(checker, "uniform", 5_000_000, 21, 1e-3, 1e6, fn="log")  # SNR and coherent-time arguments
+    n += run(checker, "random", 5_000_000, 22, fn="log")
+    n += run(checker, "range", f32_bits(0.5), f32_bits(2.0), fn="log")
     assert n >= 10_000_000

@@ -10,8 +10,7 @@ Two checks on the same run (the persistent fast kernel, trk_fast.hip), both bit-
     correlated with and its tap sums) re-run on oracle.corr_batch (the u_avx restatement) with the
     same arguments — every tap equal;
   * the loop: every channel's epoch records equal the oracle loop's (oracle/trk_oracle.c, the same
-    AVX correlator, glibc trig and discriminators) — test_gpu_trk.compare_exact (CN0 to 1e-4 dB: the
-    device's log10f).
+    AVX correlator, glibc trig, discriminators and CN0 log10f) — test_gpu_trk.compare_exact.
 """
 import concurrent.futures as cf
 
@@ -19,7 +18,6 @@ import numpy as np
 import pytest
 
 from gnss_sim_receiver_amd import abi, engine, signals
-from oracle import oracle as O
 from oracle import trk as T
 
 from test_gpu_trk import compare_exact, dev_conf
@@ -30,13 +28,6 @@ pytestmark = pytest.mark.gpu
 FS, VL, N_CH = 4e6, 4000, 12
 SEED = 0x6E550002
 EPOCHS = 1100
-TOL = 1e-5
-
-
-def rel_err(got, ref):
-    return float(np.max(np.abs(got - ref) / np.maximum(np.abs(ref), 1e-30)))
-
-
 def test_headline_c2_avx_500_state4_epochs_match_oracle(ctx):
     sats = signals.random_sky(32, seed=SEED)
     for s in sats:

@@ -5,7 +5,7 @@ acquisition (Channels.in_acquisition = 1, conf/gnss-sdr_GPS_L1_gr_complex.conf: 
 250 Hz, pll 40 / dll 4, order 3).  Checked: the same control-event sequence (acquisition start,
 negative, positive, stream positions, PRN per channel), bit-identical acquisition outcomes of the
 positive acquisitions, tracking records (the AVX engine, trk_fast.hip, is bit-exact to the oracle loop:
-every record field equal, CN0 to 1e-4 dB — test_gpu_trk.compare_exact), the per-channel tracking dump
+every record field equal — test_gpu_trk.compare_exact), the per-channel tracking dump
 files (tracking_dump_reader.cc:26-47 layout), ishort input, and re-acquisition after a loss of lock
 (the signal of one satellite switched off mid-file)."""
 import os
@@ -78,7 +78,6 @@ def compare(events, recs, rx, dump_prefix, values_until=None):
             a, b = mine[f][sel], ref_c[f][sel]
             same = (a == b) | (np.isnan(a) & np.isnan(b)) if a.dtype.kind == "f" else a == b
             assert np.all(same), (c, f, int(np.count_nonzero(~same)), int(np.nonzero(~same)[0][0]))
-        np.testing.assert_allclose(mine["cn0_db_hz"][sel], ref_c["cn0_db_hz"][sel], rtol=0, atol=1e-4, err_msg=f"ch{c} cn0")
         dumped = np.fromfile(f"{dump_prefix}{c}.dat", abi.TRK_DUMP_DTYPE)
         assert len(dumped) == int(np.sum((mine["flags"] & 16) != 0))
         np.testing.assert_array_equal(dumped["PRN_start_sample_count"], mine["sample_counter"][(mine["flags"] & 16) != 0]

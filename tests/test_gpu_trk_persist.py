@@ -4,8 +4,7 @@ loop (oracle/trk_oracle.c), for both volk_gnsssdr rotator variants the reference
 north_star's 25 Msps rates (GPS L1 C/A N = 25000, Galileo E1 N = 100000 — C3/C4's sampling rate).
 
 The AVX variant runs trk_fast.hip, which reproduces u_avx's products and accumulation order, glibc's
-phasor trig and the discriminators' libm: its records equal the oracle loop's (test_gpu_trk.compare_exact,
-CN0 to 1e-4 dB).  The generic variant (trk_persist.hip, tree sums) is held to test_gpu_trk.compare's
+phasor trig and the loop's libm calls: its records equal the oracle loop's (test_gpu_trk.compare_exact).  The generic variant (trk_persist.hip, tree sums) is held to test_gpu_trk.compare's
 tolerances: exact epoch boundaries / states / flags, Doppler and code frequency ≤ 2e-3, remnant code
 phase ≤ 1e-5 chip, CN0 ≤ 5e-3 dB, prompt ≤ 1e-4 relative.
 """
