@@ -286,6 +286,8 @@ bool build_params(const gnsship_trk_conf& c, TrkParams& p)
     p.fs_int = static_cast<int64_t>(c.fs_in);
     const int64_t ifi = static_cast<int64_t>(c.if_hz);
     p.if_mod = p.fs_int > 0 ? ((ifi % p.fs_int) + p.fs_int) % p.fs_int : 0;
+    p.inv_fs = 1.0 / c.fs_in;
+    p.inv_carrier_freq = 1.0 / p.carrier_freq;
     return true;
 }
 

@@ -57,6 +57,8 @@ struct TrkParams {
     int32_t pad_if;
     double if_step_rad;
     int64_t if_mod, fs_int;
+    // RN(1/fs_in) and RN(1/carrier_freq): the loop's quotients by them as exact FMA sequences (exact_div.h)
+    double inv_fs, inv_carrier_freq;
 };
 
 struct Smoother {

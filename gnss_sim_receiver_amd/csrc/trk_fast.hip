@@ -44,7 +44,7 @@
 namespace gnsship {
 namespace {
 constexpr int kFProfEpochs = 64;
-constexpr int kFProfSlots = 48;
+constexpr int kFProfSlots = 64;
 __device__ unsigned long long* g_trkf_prof = nullptr;
 __shared__ int g_fprof_epoch;
 __device__ __forceinline__ void trkf_prof_stamp(int e, int k)
@@ -349,37 +349,37 @@ __device__ __forceinline__ float fast_replay(float x, float c, float k2, int M, 
 }
 
 // Producer phase A, before the group's phasor slots are ready: the code value of every tap at
-// every sample of this lane's task (the resampler, volk_gnsssdr_32f_xn_resampler_32f_xn.h:63-80) into
-// the ring group's code table — it depends only on the code NCO, so it runs ahead of the replay.
+// every sample of this lane's task (the resampler, volk_gnsssdr_32f_xn_resampler_32f_xn.h:63-80), in
+// registers — it depends only on the code NCO, so it runs ahead of the replay.
 template <int NT, bool DATA, bool IN_MARGIN, int G, bool FULL>
 __device__ __forceinline__ void group_codes(const float* __restrict__ code0, const float* __restrict__ code1, int L, int n0, int cnt, float step,
-    float rem, const float (&shifts)[NT], float* __restrict__ cdst)
+    float rem, const float (&shifts)[NT], float (&cv)[G][NT + (DATA ? 1 : 0)])
 {
-    constexpr int NTT = NT + (DATA ? 1 : 0);
     float fn = static_cast<float>(n0);  // (float)n, exact steps of 16 (n < 2^24)
     const float fn0 = fn;
 #pragma unroll
     for (int i = 0; i < G; i++) {
         const bool on = FULL || i < cnt;
         const float sn = __fmul_rn(step, on ? fn : fn0);
-        float* d = cdst + static_cast<size_t>(i) * NTT * kAvxLanes;
 #pragma unroll
-        for (int q = 0; q < NT; q++) d[q * kAvxLanes] = code_at<IN_MARGIN>(code0, L, sn, shifts[q], rem);
-        if constexpr (DATA) d[NT * kAvxLanes] = code_at<IN_MARGIN>(code1, L, sn, 0.0f, rem);
+        for (int q = 0; q < NT; q++) cv[i][q] = code_at<IN_MARGIN>(code0, L, sn, shifts[q], rem);
+        if constexpr (DATA) cv[i][NT] = code_at<IN_MARGIN>(code1, L, sn, 0.0f, rem);
         fn += static_cast<float>(kAvxLanes);
     }
 }
 
 // Producer phase B, once the slot holds z_l at the task start: per iteration the sample product
-// a = x·z_l (_mm256_complexmul_ps rounding) into the ring group, and the chain's own update z·dz
-// (renormalised after the task's first iteration when that is ≡ 0 mod 64, :265-272).
-// FULL: every lane's task has all G iterations, so nothing is masked.
-template <int FMT, int G, bool FULL>
-__device__ __forceinline__ void group_phasors(i4v span, f2 z, f2 dz, bool renorm, int n0, int cnt, f2* __restrict__ adst, f2 (&xa)[G < 8 ? G : 8],
-    f2 (&xb)[G < 8 ? G : 8])
+// a = x·z_l (_mm256_complexmul_ps rounding) and its products with the taps' code values,
+// c = _mm256_mul_ps(a, code) (:252-258), into the ring group — the accumulator only adds them — and
+// the chain's own update z·dz (renormalised after the task's first iteration when that is ≡ 0 mod 64,
+// :265-272).  FULL: every lane's task has all G iterations, so nothing is masked.
+template <int FMT, int NTT, int G, bool FULL>
+__device__ __forceinline__ void group_phasors(i4v span, f2 z, f2 dz, bool renorm, int n0, int cnt, float* __restrict__ pdst, const float (&cv)[G][NTT],
+    f2 (&xa)[G < 8 ? G : 8], f2 (&xb)[G < 8 ? G : 8])
 {
     constexpr int SB = sample_bytes<FMT>();
     constexpr int kB = G < 8 ? G : 8;
+    constexpr int IS = 2 * NTT * kAvxLanes;  // one iteration's products (floats)
 #pragma unroll 1
     for (int i0 = 0; i0 < G; i0 += kB) {
         if (i0 + kB < G) {
@@ -390,7 +390,15 @@ __device__ __forceinline__ void group_phasors(i4v span, f2 z, f2 dz, bool renorm
         for (int u = 0; u < kB; u++) {
             const int i = i0 + u;
             const bool on = FULL || i < cnt;
-            adst[static_cast<size_t>(i) * kAvxLanes] = on ? cmul_exact_pk(xa[u], z) : f2{0.0f, 0.0f};
+            const f2 a = cmul_exact_pk(xa[u], z);
+            float* d = pdst + static_cast<size_t>(i) * IS;
+            // an iteration past the epoch's last holds −0, which the accumulator adds unconditionally:
+            // x + (−0) = x for every x, so its sums are the reference's
+#pragma unroll
+            for (int q = 0; q < NTT; q++) {
+                d[(2 * q) * kAvxLanes] = on ? __fmul_rn(a.x, cv[i][q]) : -0.0f;
+                d[(2 * q + 1) * kAvxLanes] = on ? __fmul_rn(a.y, cv[i][q]) : -0.0f;
+            }
             f2 zn = cmul_exact_s(z, dz);
             if (i == 0 && renorm) zn = normalise_avx(zn);
             z = zn;
@@ -402,17 +410,27 @@ __device__ __forceinline__ void group_phasors(i4v span, f2 z, f2 dz, bool renorm
     }
 }
 
+// The product ring's layout (floats): group r, task t (of 4), iteration i (of G), product slot s
+// (2·tap + component), chain l at  r·group_floats + t·task_floats + i·2·NTT·16 + s·16 + l.  Each task
+// is padded by 16 floats so the four tasks a producer wave writes at once fall in different banks.
+template <int NTT, int G>
+struct ProdLayout {
+    static constexpr int kIter = 2 * NTT * kAvxLanes;
+    static constexpr int kTask = G * kIter + kAvxLanes;
+    static constexpr int kGroup = 4 * kTask;
+};
+
 // ---- producer waves -------------------------------------------------------------------------------
-// Ring group r (of rg) holds one group of 4 tasks = 4G iterations: the sample products
-// Pa[(r·4G + j)·16 + l] and the code values Pc[((r·4G + j)·NTT + tap)·16 + l] of iteration j of the
-// group, chain l.  Group tags count over the run (gbase = epoch · n_groups): no flag is re-armed.
+// Ring group r (of rg) holds one group of 4 tasks = 4G iterations: the products of iteration j of the
+// group, chain l, every tap and component (ProdLayout).  Group tags count over the run
+// (gbase = epoch · n_groups): no flag is re-armed.
 template <int FMT, int NT, bool DATA, bool IN_MARGIN, int G>
 __device__ __forceinline__ void fast_produce(const FJob& job, i4v span, const float* __restrict__ code0, const float* __restrict__ code1, int L,
-    uint64_t* __restrict__ Zs, int rs, f2* __restrict__ Pa, float* __restrict__ Pc, int rg, int32_t* ready, const int32_t* acc_groups, int gbase, int lane,
-    int pw, int pe)
+    uint64_t* __restrict__ Zs, int rs, float* __restrict__ Pp, int rg, int32_t* ready, const int32_t* acc_groups, int gbase, int lane, int pw, int pe)
 {
     constexpr int SB = sample_bytes<FMT>();
     constexpr int NTT = NT + (DATA ? 1 : 0);
+    using PL = ProdLayout<NTT, G>;
     constexpr int kB = G < 8 ? G : 8;  // iterations whose samples are in flight together
     const int M = job.M, S = job.S;
     const int n_groups = (S + 3) / 4;
@@ -429,6 +447,7 @@ __device__ __forceinline__ void fast_produce(const FJob& job, i4v span, const fl
         for (int u = 0; u < kB; u++) x[u] = load_sample<FMT>(span, (n0 + kAvxLanes * u) * SB, 0);
     };
     f2 xa[kB], xb[kB];
+    float cv[G][NTT];
     int rslot = pw % rg;
     const int rstep = kFProducers % rg;
     for (int g = pw; g < n_groups; g += kFProducers) {
@@ -439,14 +458,10 @@ __device__ __forceinline__ void fast_produce(const FJob& job, i4v span, const fl
         const int n0 = kAvxLanes * m_lo + l;
         const bool full = 4 * g + 4 <= S && G * (4 * g + 4) <= M;  // every task of the group whole
         first_samples(g, xa);  // in flight during phase A and the slot poll
-        // the ring group is free once the accumulator consumed its previous occupant
-        if (g >= rg) lds_wait_ge(acc_groups, gbase + g - rg + 1);
-        const size_t j0 = static_cast<size_t>(rslot * 4 * G + tl * G);
-        float* cdst = Pc + j0 * NTT * kAvxLanes + l;
         if (full)
-            group_codes<NT, DATA, IN_MARGIN, G, true>(code0, code1, L, n0, G, step, rem, shifts, cdst);
+            group_codes<NT, DATA, IN_MARGIN, G, true>(code0, code1, L, n0, G, step, rem, shifts, cv);
         else
-            group_codes<NT, DATA, IN_MARGIN, G, false>(code0, code1, L, n0, cnt, step, rem, shifts, cdst);
+            group_codes<NT, DATA, IN_MARGIN, G, false>(code0, code1, L, n0, cnt, step, rem, shifts, cv);
         const int ts = active ? t % rs : 0;
         uint64_t* slot = Zs + ts * kAvxLanes + l;
         uint64_t v = kSlotEmpty;
@@ -457,86 +472,72 @@ __device__ __forceinline__ void fast_produce(const FJob& job, i4v span, const fl
         }
         if (g == pw && pw == 0) GNSSHIP_FSTAMP(pe, 30);
         if (g + kFProducers >= n_groups && pw == 1) GNSSHIP_FSTAMP(pe, 31);
+        // the ring group is free once the accumulator consumed its previous occupant
+        if (g >= rg) lds_wait_ge(acc_groups, gbase + g - rg + 1);
         const f2 z = active ? __builtin_bit_cast(f2, v) : f2{0.0f, 0.0f};
         const bool renorm = ((G * t) & 63) == 0;
-        f2* adst = Pa + j0 * kAvxLanes + l;
+        float* pdst = Pp + static_cast<size_t>(rslot) * PL::kGroup + tl * PL::kTask + l;
         if (full)
-            group_phasors<FMT, G, true>(span, z, dz, renorm, n0, G, adst, xa, xb);
+            group_phasors<FMT, NTT, G, true>(span, z, dz, renorm, n0, G, pdst, cv, xa, xb);
         else
-            group_phasors<FMT, G, false>(span, z, dz, renorm, n0, cnt, adst, xa, xb);
+            group_phasors<FMT, NTT, G, false>(span, z, dz, renorm, n0, cnt, pdst, cv, xa, xb);
         if (lane == 0) lds_release_store(ready + rslot, gbase + g + 1);
+        if (g < 8) GNSSHIP_FSTAMP(pe, 48 + g);
         rslot += rstep;
         if (rslot >= rg) rslot -= rg;
     }
 }
 
 // ---- control wave: the accumulation in u_avx's order ----------------------------------------------
-// Lane (l, r): chain l's accumulators of tap r (a0) and tap r + 4 (a1), both components.  Every
-// product a·code is formed and added in iteration order, exactly c = _mm256_mul_ps(a, b);
-// dotProdVal_{l/4}[tap] += c (:252-260).  Scalar single-rate VALU ops (this file is built without SLP
-// packing): a dependent v_pk_add_f32 chain issues several times slower on gfx950 than two
-// interleaved v_add_f32 chains (measured: ≈ 56 vs ≈ 10 cycles per iteration of the accumulator).
+// Lane (l, r): chain l's accumulators of product slots r, r + 4, r + 8, r + 12 (slot s = 2·tap +
+// component) — each c = _mm256_mul_ps(a, code) the producers formed is added in iteration order,
+// dotProdVal_{l/4}[tap] += c (:252-260), one v_add_f32 per slot and iteration, the slots' chains
+// interleaved.
+template <int NTT>
+constexpr int acc_slots() { return (2 * NTT + 3) / 4; }
+
 template <int NTT, int G>
-__device__ __forceinline__ void fast_accumulate(const f2* __restrict__ Pa, const float* __restrict__ Pc, int rg, const int32_t* ready, int32_t* acc_groups,
-    int gbase, int M, int S, int lane, f2& a0, f2& a1, int pe)
+__device__ __forceinline__ void fast_accumulate(const float* __restrict__ Pp, int rg, const int32_t* ready, int32_t* acc_groups, int gbase, int M, int S,
+    int lane, float (&acc)[acc_slots<NTT>()], int pe)
 {
+    using PL = ProdLayout<NTT, G>;
+    constexpr int NS = acc_slots<NTT>();
     const int l = lane & (kAvxLanes - 1), r = lane >> 4;
-    const int r0 = r < NTT ? r : 0;                      // lanes without a tap read tap 0 (discarded)
-    const int r1 = (NTT > 4 && r + 4 < NTT) ? r + 4 : 0;
     const int n_groups = (S + 3) / 4;
-    float s0r = 0.0f, s0i = 0.0f, s1r = 0.0f, s1i = 0.0f;
+    int off[NS];  // lane offsets of the slots (a slot past the last reads the last: discarded)
+#pragma unroll
+    for (int k = 0; k < NS; k++) {
+        acc[k] = 0.0f;
+        off[k] = min(r + 4 * k, 2 * NTT - 1) * kAvxLanes + l;
+    }
     int rslot = 0;
     for (int g = 0; g < n_groups; g++) {
         lds_wait_eq(ready + rslot, gbase + g + 1);
         if (g == 0) GNSSHIP_FSTAMP(pe, 28);
         if (g == n_groups - 1) GNSSHIP_FSTAMP(pe, 29);
-        const int cnt = min(4 * G, M - 4 * G * g);
-        const size_t j0 = static_cast<size_t>(rslot * 4 * G);
-        const f2* pa = Pa + j0 * kAvxLanes + l;
-        const float* pc0 = Pc + (j0 * NTT + r0) * kAvxLanes + l;
-        const float* pc1 = Pc + (j0 * NTT + r1) * kAvxLanes + l;
-        if (cnt == 4 * G) {
-            constexpr int kU = 8;  // loads in flight ahead of the dependent adds
+        if (g < 8) GNSSHIP_FSTAMP(pe, 56 + g);
+        // every group is added whole: a partial group's iterations past the epoch's end hold −0
+        const float* src = Pp + static_cast<size_t>(rslot) * PL::kGroup;
 #pragma unroll
-            for (int j = 0; j < 4 * G; j += kU) {
-                f2 va[kU];
-                float c0[kU], c1[kU];
+        for (int t = 0; t < 4; t++) {
+            constexpr int kU = G < 8 ? G : 8;  // iterations whose loads are in flight together
 #pragma unroll
-                for (int u = 0; u < kU; u++) {
-                    va[u] = pa[(j + u) * kAvxLanes];
-                    c0[u] = pc0[(j + u) * NTT * kAvxLanes];
-                    if constexpr (NTT > 4) c1[u] = pc1[(j + u) * NTT * kAvxLanes];
-                }
+            for (int i0 = 0; i0 < G; i0 += kU) {
+                float v[kU][NS];
 #pragma unroll
-                for (int u = 0; u < kU; u++) {
-                    s0r = __fadd_rn(s0r, __fmul_rn(va[u].x, c0[u]));
-                    s0i = __fadd_rn(s0i, __fmul_rn(va[u].y, c0[u]));
-                    if constexpr (NTT > 4) {
-                        s1r = __fadd_rn(s1r, __fmul_rn(va[u].x, c1[u]));
-                        s1i = __fadd_rn(s1i, __fmul_rn(va[u].y, c1[u]));
-                    }
-                }
-            }
-        } else {
-#pragma unroll 1
-            for (int j = 0; j < cnt; j++) {
-                const f2 va = pa[j * kAvxLanes];
-                const float c0 = pc0[j * NTT * kAvxLanes];
-                s0r = __fadd_rn(s0r, __fmul_rn(va.x, c0));
-                s0i = __fadd_rn(s0i, __fmul_rn(va.y, c0));
-                if constexpr (NTT > 4) {
-                    const float c1 = pc1[j * NTT * kAvxLanes];
-                    s1r = __fadd_rn(s1r, __fmul_rn(va.x, c1));
-                    s1i = __fadd_rn(s1i, __fmul_rn(va.y, c1));
-                }
+                for (int u = 0; u < kU; u++)
+#pragma unroll
+                    for (int k = 0; k < NS; k++) v[u][k] = src[off[k] + t * PL::kTask + (i0 + u) * PL::kIter];
+#pragma unroll
+                for (int u = 0; u < kU; u++)
+#pragma unroll
+                    for (int k = 0; k < NS; k++) acc[k] = __fadd_rn(acc[k], v[u][k]);
             }
         }
         asm volatile("" ::: "memory");  // the group's loads are issued (and used) before it is released
         if (lane == 0) lds_release_store(acc_groups, gbase + g + 1);
         rslot = rslot + 1 == rg ? 0 : rslot + 1;
     }
-    a0 = f2{s0r, s0i};
-    a1 = f2{s1r, s1i};
 }
 
 // u_avx's final combination of the 16 chains (:279-291), valid at lane 0 of each 16-lane row:
@@ -624,9 +625,8 @@ __global__ __launch_bounds__(kFThreads, fast_waves_per_simd<THRU>()) void trk_fa
     float* code0 = lds;
     float* code1 = lds + code_cap_floats;
     uint64_t* Zs = reinterpret_cast<uint64_t*>(lds + (DATA ? 2 : 1) * code_cap_floats);
-    f2* Pa = reinterpret_cast<f2*>(Zs + static_cast<size_t>(rs) * kAvxLanes);
-    float* Pc = reinterpret_cast<float*>(Pa + static_cast<size_t>(rg) * 4 * G * kAvxLanes);
-    int32_t* ready = reinterpret_cast<int32_t*>(Pc + static_cast<size_t>(rg) * 4 * G * NTT * kAvxLanes);
+    float* Pp = reinterpret_cast<float*>(Zs + static_cast<size_t>(rs) * kAvxLanes);
+    int32_t* ready = reinterpret_cast<int32_t*>(Pp + static_cast<size_t>(rg) * ProdLayout<NTT, G>::kGroup);
     for (int i = tid; i < rs * kAvxLanes; i += kFThreads) Zs[i] = kSlotEmpty;
     for (int i = tid; i < rg; i += kFThreads) ready[i] = 0;
     __shared__ int32_t simd_of[kFWaves];
@@ -676,6 +676,11 @@ __global__ __launch_bounds__(kFThreads, fast_waves_per_simd<THRU>()) void trk_fa
     __syncthreads();
     if (skip) return;  // idle channel: its state is untouched
     if (wave < 4) GNSSHIP_FHWID(20 + wave);  // epoch 0's slots 20-23 (the epoch loop stamps 0-15)
+#ifdef GNSSHIP_CORR_PROFILE
+    if (g_trkf_prof && lane == 0)  // epoch 2's slots 41-46: HW_ID | role << 32 of every wave
+        g_trkf_prof[(static_cast<size_t>(blockIdx.x) * kFProfEpochs + 2) * kFProfSlots + 41 + wave] =
+            static_cast<uint32_t>(__builtin_amdgcn_s_getreg(4 | (31 << 11))) | (static_cast<unsigned long long>(role) << 32);
+#endif
     stage_code_f(code0, codes[sc.code_id]);
     if constexpr (DATA) stage_code_f(code1, codes[sc.data_code_id]);
     __syncthreads();  // the code replicas are staged before any wave correlates
@@ -725,7 +730,7 @@ __global__ __launch_bounds__(kFThreads, fast_waves_per_simd<THRU>()) void trk_fa
         const bool runnable = e < max_rounds && (rc.state == 2 || rc.state == 3 || rc.state == 4) && rc.nitems_read >= buf_first &&
                               rc.nitems_read + vl <= buf_first + static_cast<uint64_t>(buf_len);
         // corr_rem_carr / corr_phase_step (trk_loop.h) on the hoisted IF constants
-        const float rem_carr = has_if ? static_cast<float>(fmod(static_cast<double>(rc.rem_carr_phase_rad) + kTwoPi * rc.if_cyc, kTwoPi))
+        const float rem_carr = has_if ? static_cast<float>(fmod_2pi(static_cast<double>(rc.rem_carr_phase_rad) + kTwoPi * rc.if_cyc))
                                       : rc.rem_carr_phase_rad;
         const float stepf = static_cast<float>(rc.carrier_phase_step_rad + if_step);
         if (runnable) rc.epoch_start = rc.nitems_read;
@@ -831,9 +836,9 @@ __global__ __launch_bounds__(kFThreads, fast_waves_per_simd<THRU>()) void trk_fa
         if (role == kRoleProducer) {
             const i4v span = sample_span<FMT>(samples, job.off, N);
             if (job.in_margin)
-                fast_produce<FMT, NT, DATA, true, G>(job, span, c0, c1, L, Zs, rs, Pa, Pc, rg, ready, &sh.acc_groups, gbase, lane, pw, e);
+                fast_produce<FMT, NT, DATA, true, G>(job, span, c0, c1, L, Zs, rs, Pp, rg, ready, &sh.acc_groups, gbase, lane, pw, e);
             else
-                fast_produce<FMT, NT, DATA, false, G>(job, span, c0, c1, L, Zs, rs, Pa, Pc, rg, ready, &sh.acc_groups, gbase, lane, pw, e);
+                fast_produce<FMT, NT, DATA, false, G>(job, span, c0, c1, L, Zs, rs, Pp, rg, ready, &sh.acc_groups, gbase, lane, pw, e);
             if (pw < 2) GNSSHIP_FSTAMP(e, 3 + pw);  // 3, 4: producers 0 and 1 done
             if (pw == 0) {
                 // cn0_and_tracking_lock_status (:972-1029) on the LDS copy of its members, beside the loop update
@@ -850,31 +855,34 @@ __global__ __launch_bounds__(kFThreads, fast_waves_per_simd<THRU>()) void trk_fa
         }
         // ---- wave 0: the epoch's taps in u_avx's order ----
         {
-            f2 a0, a1;
+            constexpr int NS = acc_slots<NTT>();
+            float acc[NS];
             GNSSHIP_FSTAMP(e, 27);
-            fast_accumulate<NTT, G>(Pa, Pc, rg, ready, &sh.acc_groups, gbase, M, S, lane, a0, a1, e);
+            fast_accumulate<NTT, G>(Pp, rg, ready, &sh.acc_groups, gbase, M, S, lane, acc, e);
             GNSSHIP_FSTAMP(e, 5);
-            f2 t0 = f2{avx_chain_sum(a0.x), avx_chain_sum(a0.y)};
-            f2 t1 = f2{0.0f, 0.0f};
-            if constexpr (NTT > 4) t1 = f2{avx_chain_sum(a1.x), avx_chain_sum(a1.y)};
             const int r = lane >> 4;
+#pragma unroll
+            for (int kk = 0; kk < NS; kk++) acc[kk] = avx_chain_sum(acc[kk]);
             if (job.tail > 0) {  // the serial tail, sample by sample (:298-308)
                 wait_seq(&sh.tail_seq, e + 1);
                 for (int j = 0; j < job.tail; j++) {
-                    t0 = t0 + sh.tailp[j][r < NTT ? r : 0];
-                    if constexpr (NTT > 4) t1 = t1 + sh.tailp[j][r + 4 < NTT ? r + 4 : 0];
+#pragma unroll
+                    for (int kk = 0; kk < NS; kk++) {
+                        const int sl = min(r + 4 * kk, 2 * NTT - 1);
+                        const f2 tv = sh.tailp[j][sl >> 1];
+                        acc[kk] = acc[kk] + ((sl & 1) ? tv.y : tv.x);
+                    }
                 }
             }
             if ((lane & 15) == 0) {
-                if (r < NTT) {
-                    const int o = (DATA && r == NT) ? 2 * kMaxTaps : 2 * r;
-                    sh.taps[o] = t0.x;
-                    sh.taps[o + 1] = t0.y;
-                }
-                if (NTT > 4 && r + 4 < NTT) {
-                    const int o = (DATA && r + 4 == NT) ? 2 * kMaxTaps : 2 * (r + 4);
-                    sh.taps[o] = t1.x;
-                    sh.taps[o + 1] = t1.y;
+#pragma unroll
+                for (int kk = 0; kk < NS; kk++) {
+                    const int sl = r + 4 * kk;  // slot 2·tap + component
+                    if (sl < 2 * NTT) {
+                        const int tap = sl >> 1;
+                        const int o = (DATA && tap == NT) ? 2 * kMaxTaps : 2 * tap;
+                        sh.taps[o + (sl & 1)] = acc[kk];
+                    }
                 }
             }
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1045,7 +1053,9 @@ static FastPlan fast_plan(const TrkParams& p, int code_cap_floats, int n_chans)
     const int ntt = p.n_taps + (p.jobs_per_channel > 1 ? 1 : 0);
     const size_t codes = static_cast<size_t>(p.jobs_per_channel > 1 ? 2 : 1) * code_cap_floats * sizeof(float);
     const size_t slot_b = kAvxLanes * sizeof(uint64_t);
-    const size_t group_b = static_cast<size_t>(4 * G) * kAvxLanes * (2 + ntt) * sizeof(float) + sizeof(int32_t);  // products, codes, flag
+    // a group's products (ProdLayout: 4 tasks of G iterations × 2·ntt slots × 16 chains, each task
+    // padded by 16 floats) and its flag
+    const size_t group_b = static_cast<size_t>(4) * (G * 2 * ntt * kAvxLanes + kAvxLanes) * sizeof(float) + sizeof(int32_t);
     // more channels than CUs: two workgroups per CU share its LDS
     size_t budget = n_chans > device_cus() ? 72 * 1024 : kTrkPersistMaxLds;
     if (const char* env = std::getenv("GNSSHIP_TRK_FAST_LDS"))  // tests: a smaller budget forces the rings

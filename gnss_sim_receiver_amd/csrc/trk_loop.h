@@ -16,6 +16,7 @@
 #include <cmath>
 #include <type_traits>
 
+#include "exact_div.h"
 #include "trk_engine.h"
 
 // Phase hook for the profiling build of the persistent kernel (trk_persist.hip); empty otherwise.
@@ -30,6 +31,14 @@ namespace {
 // MATH_CONSTANTS.h:47-49: the reference's pi is the GNSS value 3.1415926535898
 constexpr double kGnssPi = 3.1415926535898;
 constexpr double kTwoPi = 2.0 * kGnssPi;
+constexpr double kInvTwoPi = 1.0 / kTwoPi;
+// x / TWO_PI, fmod(x, TWO_PI), x / fs_in and x / carrier_freq, each the IEEE result (exact_div.h)
+__device__ __forceinline__ double div_2pi(double x) { return div_by(x, kTwoPi, kInvTwoPi); }
+__device__ __forceinline__ double fmod_2pi(double x) { return fmod_by(x, kTwoPi, kInvTwoPi); }
+template <class K>
+__device__ __forceinline__ double div_fs(const K& k, double x) { return div_by(x, k.conf.fs_in, k.inv_fs); }
+template <class K>
+__device__ __forceinline__ double div_carrier(const K& k, double x) { return div_by(x, k.carrier_freq, k.inv_carrier_freq); }
 constexpr double kHalfPi = kGnssPi / 2.0;
 
 // fll_diff_atan + phase_unwrap (tracking_discriminators.cc:27-41, 68-76)
@@ -219,6 +228,7 @@ struct KFast {
     KFastConf conf;
     double code_chip_rate, carrier_freq, code_period, if_step_rad;
     int64_t if_mod, fs_int;
+    double inv_fs, inv_carrier_freq;
     int32_t code_length_chips, veml, track_pilot, fp_order, has_if;
     float spc_n;
     LoopSet ls_w, ls_n;  // the wide set and this channel's narrow set (k.ls[0], k.ls[1 + geo])
@@ -243,6 +253,8 @@ __device__ __forceinline__ KFast make_kfast(const TrkParams& k, int geo)
     f.if_step_rad = k.if_step_rad;
     f.if_mod = k.if_mod;
     f.fs_int = k.fs_int;
+    f.inv_fs = k.inv_fs;
+    f.inv_carrier_freq = k.inv_carrier_freq;
     f.code_length_chips = k.code_length_chips;
     f.veml = k.veml;
     f.track_pilot = k.track_pilot;
@@ -517,14 +529,14 @@ __device__ void run_dll_pll(const K& k, C& c)
         disc = (c.p[0] != 0.0f) ? static_cast<double>(glibc_atanf(__fdiv_rn(c.p[1], c.p[0]))) : 0.0;
     else
         disc = static_cast<double>(glibc_atan2f(c.p[1], c.p[0]));  // gr::fast_atan2f restated as atan2f (glibc_atanf.h)
-    c.carr_phase_error_hz = disc / kTwoPi;
+    c.carr_phase_error_hz = div_2pi(disc);
     GNSSHIP_TRK_LOOP_STAMP(37);
     // d_current_correlation_time_s: the code period, or extend × code period once extended
     const float T = c.narrow ? syncset(k, c).T_ext : static_cast<float>(k.code_period);
     if ((c.pull_in && k.conf.enable_fll_pull_in) || k.conf.enable_fll_steady_state) {  // :1080-1097
         // d_current_correlation_time_s is a double: the code period, or (float)extend·(float)period
         const double Td = c.narrow ? static_cast<double>(syncset(k, c).T_ext) : k.code_period;
-        const double fe = fll_diff_atan(c.p_old, c.p, 0.0, Td) / kTwoPi;
+        const double fe = div_2pi(fll_diff_atan(c.p_old, c.p, 0.0, Td));
         c.p_old[0] = c.p[0];
         c.p_old[1] = c.p[1];
         const float pll = (c.pull_in && k.conf.enable_fll_pull_in) ? 0.0f : static_cast<float>(c.carr_phase_error_hz);
@@ -555,7 +567,7 @@ __device__ void run_dll_pll(const K& k, C& c)
     c.code_error_filt_chips = loop_filter_apply(k, c, static_cast<float>(c.code_error_chips));
     GNSSHIP_TRK_LOOP_STAMP(40);
     c.code_freq_chips = k.code_chip_rate - c.code_error_filt_chips;
-    if (k.conf.carrier_aiding) c.code_freq_chips += c.carrier_doppler_hz * k.code_chip_rate / k.carrier_freq;
+    if (k.conf.carrier_aiding) c.code_freq_chips += div_carrier(k, c.carrier_doppler_hz * k.code_chip_rate);
 }
 
 // high_dyn rate estimate (:1208-1221, :1241-1254): mean step of the newest smoother_length entries
@@ -587,9 +599,9 @@ __device__ void update_tracking_vars(const K& k, C& c, TrkHist* h)
     const double T_prn_samples = T_prn * fs;
     c.K_blk_samples = T_prn_samples + c.rem_code_phase_samples;
     c.current_prn_length_samples = static_cast<int32_t>(floor(c.K_blk_samples));
-    c.carrier_phase_step_rad = kTwoPi * c.carrier_doppler_hz / fs;
+    c.carrier_phase_step_rad = div_fs(k, kTwoPi * c.carrier_doppler_hz);
     const double n = static_cast<double>(c.current_prn_length_samples);
-    c.code_phase_step_chips = c.code_freq_chips / fs;
+    c.code_phase_step_chips = div_fs(k, c.code_freq_chips);
     if constexpr (std::is_same<C, TrkChannel>::value) if (h) {  // high_dyn: push_back on the ring (full: drop the oldest), rates once it is full
         const int L = static_cast<int>(k.conf.smoother_length), cap = 2 * L;
         int slot;
@@ -611,10 +623,10 @@ __device__ void update_tracking_vars(const K& k, C& c, TrkHist* h)
     }
     const double adv = c.carrier_phase_step_rad * n + 0.5 * c.carrier_phase_rate_step_rad * n * n;
     c.rem_carr_phase_rad = __fadd_rn(c.rem_carr_phase_rad, static_cast<float>(adv));
-    c.rem_carr_phase_rad = static_cast<float>(fmod(static_cast<double>(c.rem_carr_phase_rad), kTwoPi));
+    c.rem_carr_phase_rad = static_cast<float>(fmod_2pi(static_cast<double>(c.rem_carr_phase_rad)));
     c.acc_carrier_phase_rad -= adv;
     c.rem_code_phase_samples = c.K_blk_samples - n;
-    c.rem_code_phase_chips = c.code_freq_chips * c.rem_code_phase_samples / fs;
+    c.rem_code_phase_chips = div_fs(k, c.code_freq_chips * c.rem_code_phase_samples);
 }
 
 __device__ __forceinline__ int bit_at(const uint32_t* bits, int i) { return (bits[i >> 5] >> (i & 31)) & 1; }
@@ -942,7 +954,7 @@ template <class K, class C>
 __device__ __forceinline__ float corr_rem_carr(const K& k, const C& c)
 {
     if (!k.has_if) return c.rem_carr_phase_rad;
-    return static_cast<float>(fmod(static_cast<double>(c.rem_carr_phase_rad) + kTwoPi * c.if_cyc, kTwoPi));
+    return static_cast<float>(fmod_2pi(static_cast<double>(c.rem_carr_phase_rad) + kTwoPi * c.if_cyc));
 }
 template <class K, class C>
 __device__ __forceinline__ float corr_phase_step(const K& k, const C& c)

@@ -11,7 +11,3 @@ timeout -k 10 120 python3 scripts/trk_fast_profile.py 12 > $O/fast_phases.txt 2>
 cat $O/fast_phases.txt
 timeout -k 10 300 python -u bench.py --no-aux --cpu-seconds 0 > $O/bench.json 2> $O/bench.err || { echo "bench failed"; tail -20 $O/bench.err; exit 1; }
 python3 -c "import json;d=json.load(open('$O/bench.json'));print('value',d['value'],'us/epoch',d['us_per_epoch'])"
-GNSSHIP_LIB_PATH=$R/scripts/libgnsship_prof4.so timeout -k 10 120 python3 scripts/trk_fast_profile.py 12 > $O/fast_phases4.txt 2>&1 || { echo "phase profile 4 failed"; tail $O/fast_phases4.txt; exit 1; }
-echo "---- 4 waves"; head -30 $O/fast_phases4.txt
-GNSSHIP_LIB_PATH=$R/scripts/libgnsship_prof_s2.so timeout -k 10 120 python3 scripts/trk_fast_profile.py 12 > $O/fast_phases_s2.txt 2>&1 || { echo "phase profile s2 failed"; tail $O/fast_phases_s2.txt; exit 1; }
-echo "---- poll sleep 2"; head -45 $O/fast_phases_s2.txt | grep -v HW_ID

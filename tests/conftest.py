@@ -25,6 +25,12 @@ def built():
 
 @pytest.fixture(scope="session")
 def ctx(built):
+    # torch's HIP runtime (its own libamdhip64) is initialised before libgnsship's, as bench.py does:
+    # initialised second it finds no device, and the tests that generate long IF records on the GPU
+    # (test_gpu_c5_closed_loop.if_on_device) need it
+    import torch
+    if torch.cuda.is_available():
+        torch.cuda.init()
     from gnss_sim_receiver_amd import engine
     c = engine.Context(0)
     yield c
