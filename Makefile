@@ -9,9 +9,11 @@ HDRS := $(wildcard $(CSRC)/*.h) include/gnsship.h
 # -ffp-contract=off: no implicit fusion anywhere (the HIP header intrinsics __fmul_rn/__fadd_rn
 # carry contract flags and were fused into v_fma_f32 otherwise, breaking the bit-exact chip index);
 # fused multiply-adds are written explicitly where wanted.
-HIPFLAGS := --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 -ffp-contract=off -Iinclude -I$(CSRC) -Wall -Wno-unused-result
+EXTRA ?=
+HIPFLAGS := --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 -ffp-contract=off -Iinclude -I$(CSRC) -Wall -Wno-unused-result $(EXTRA)
 LIB := $(PKG)/libgnsship.so
 OBJDIR := build/obj
+PROF_OBJDIR := build/prof_obj
 
 OBJS := $(patsubst $(CSRC)/%.hip,$(OBJDIR)/%.o,$(HIP_SRCS)) $(patsubst $(CSRC)/%.cpp,$(OBJDIR)/%.cpp.o,$(CPP_SRCS))
 
@@ -20,10 +22,10 @@ all: $(LIB) oracle
 # The acquisition FFTs are plain f32 VALU work: SLP packing into v_pk_add/mul_f32 buys no rate on
 # gfx950 (a packed f32 op issues in 4 cycles, a scalar one in 2) and costs register-pair moves
 # and VGPRs (C3 search kernel: 128 VGPRs + scratch packed, 84 unpacked).  Same IEEE ops either way.
-$(OBJDIR)/acq_kernel.o build/prof_obj/acq_kernel.o: HIPFLAGS += -fno-slp-vectorize
+$(OBJDIR)/acq_kernel.o $(PROF_OBJDIR)/acq_kernel.o: HIPFLAGS += -fno-slp-vectorize
 # The tracking engine's serial accumulations (trk_fast.hip) likewise: a dependent packed add issues
 # several times slower than single-rate adds.
-$(OBJDIR)/trk_fast.o build/prof_obj/trk_fast.o: HIPFLAGS += -fno-slp-vectorize
+$(OBJDIR)/trk_fast.o $(PROF_OBJDIR)/trk_fast.o: HIPFLAGS += -fno-slp-vectorize
 
 $(OBJDIR)/%.o: $(CSRC)/%.hip $(HDRS)
 	@mkdir -p $(OBJDIR)
@@ -56,12 +58,12 @@ all: $(MIRROR_TEST)
 
 # Profiling variant (workgroup phase timestamps in corr_batch_kernel; scripts/corr_wg_profile.py)
 PROF_LIB := scripts/libgnsship_prof.so
-PROF_OBJS := $(patsubst $(CSRC)/%.hip,build/prof_obj/%.o,$(HIP_SRCS)) $(patsubst $(CSRC)/%.cpp,build/prof_obj/%.cpp.o,$(CPP_SRCS))
-build/prof_obj/%.o: $(CSRC)/%.hip $(HDRS)
-	@mkdir -p build/prof_obj
+PROF_OBJS := $(patsubst $(CSRC)/%.hip,$(PROF_OBJDIR)/%.o,$(HIP_SRCS)) $(patsubst $(CSRC)/%.cpp,$(PROF_OBJDIR)/%.cpp.o,$(CPP_SRCS))
+$(PROF_OBJDIR)/%.o: $(CSRC)/%.hip $(HDRS)
+	@mkdir -p $(PROF_OBJDIR)
 	$(HIPCC) $(HIPFLAGS) -DGNSSHIP_CORR_PROFILE -c $< -o $@
-build/prof_obj/%.cpp.o: $(CSRC)/%.cpp $(HDRS)
-	@mkdir -p build/prof_obj
+$(PROF_OBJDIR)/%.cpp.o: $(CSRC)/%.cpp $(HDRS)
+	@mkdir -p $(PROF_OBJDIR)
 	$(HIPCC) $(HIPFLAGS) -x c++ -c $< -o $@
 $(PROF_LIB): $(PROF_OBJS)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(PROF_OBJS) -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib

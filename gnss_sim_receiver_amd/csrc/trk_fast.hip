@@ -43,29 +43,32 @@
 #ifdef GNSSHIP_CORR_PROFILE
 namespace gnsship {
 namespace {
-constexpr int kFProfEpochs = 64;
-constexpr int kFProfSlots = 64;
+constexpr int kFProfEpochs = 16;  // profiled epochs kFProfFirst .. kFProfFirst + 15, stamped into LDS
+constexpr int kFProfFirst = 8;
+constexpr int kFProfSlots = 80;
 __device__ unsigned long long* g_trkf_prof = nullptr;
 __shared__ int g_fprof_epoch;
+// stamps go to LDS and out to g_trkf_prof when the kernel ends: a global store per stamp would put
+// its write acknowledgement (≈ 0.8 µs) into the next vmcnt wait of the stamping wave
+__shared__ unsigned long long g_fprof_lds[kFProfEpochs * kFProfSlots];
 __device__ __forceinline__ void trkf_prof_stamp(int e, int k)
 {
-    if (g_trkf_prof && e < kFProfEpochs && (threadIdx.x & 63) == 0)
-        g_trkf_prof[(static_cast<size_t>(blockIdx.x) * kFProfEpochs + e) * kFProfSlots + k] = wall_clock64();
+    const int r = e - kFProfFirst;
+    if (g_trkf_prof && r >= 0 && r < kFProfEpochs && (threadIdx.x & 63) == 0) g_fprof_lds[r * kFProfSlots + k] = wall_clock64();
 }
 }  // namespace
 }  // namespace gnsship
 namespace gnsship {
 __device__ __forceinline__ void trkf_prof_clock(int e, int k)
 {
-    if (g_trkf_prof && e < kFProfEpochs && (threadIdx.x & 63) == 0)
-        g_trkf_prof[(static_cast<size_t>(blockIdx.x) * kFProfEpochs + e) * kFProfSlots + k] = clock64();
+    const int r = e - kFProfFirst;
+    if (g_trkf_prof && r >= 0 && r < kFProfEpochs && (threadIdx.x & 63) == 0) g_fprof_lds[r * kFProfSlots + k] = clock64();
 }
 }  // namespace gnsship
 namespace gnsship {
-__device__ __forceinline__ void trkf_prof_hwid(int k)  // HW_ID (wave slot, SIMD, CU, SE) of the stamping wave
+__device__ __forceinline__ void trkf_prof_hwid(int k)  // HW_ID (wave slot, SIMD, CU, SE) of the stamping wave (row 0)
 {
-    if (g_trkf_prof && (threadIdx.x & 63) == 0)
-        g_trkf_prof[static_cast<size_t>(blockIdx.x) * kFProfEpochs * kFProfSlots + k] = static_cast<uint32_t>(__builtin_amdgcn_s_getreg(4 | (31 << 11)));
+    if (g_trkf_prof && (threadIdx.x & 63) == 0) g_fprof_lds[k] = static_cast<uint32_t>(__builtin_amdgcn_s_getreg(4 | (31 << 11)));
 }
 }  // namespace gnsship
 #define GNSSHIP_FSTAMP(e, k) gnsship::trkf_prof_stamp((e), (k))
@@ -102,6 +105,9 @@ constexpr int kFProducers = kFWaves - 2;  // every wave but the control and phas
 // producers share the other SIMDs (two producer waves on a SIMD interleave their issue).
 constexpr int kRoleControl = 0, kRoleReplay = 1, kRoleProducer = 2;
 // Polling waves back off this many s_sleep units (≈ 64 cycles each) between LDS polls.
+#ifndef GNSSHIP_ACC_BATCH  // iterations per accumulator load batch
+#define GNSSHIP_ACC_BATCH 8
+#endif
 #ifndef GNSSHIP_POLL_SLEEP
 #define GNSSHIP_POLL_SLEEP 0
 #endif
@@ -117,6 +123,15 @@ struct FJob {
     int32_t runnable, in_margin, M, S, tail, pad;
 };
 
+// What the loop hands the derive wave once its carrier filter ran (state 4): the next epoch's
+// carrier step, and the inputs of its remainder phase if the epoch length stays n_pred samples.
+struct SpecArgs {
+    double step_d, rate;
+    int64_t if_num;
+    float rem_prev;
+    int32_t n_pred;
+};
+
 struct FShared {
     FJob job;
     float taps[2 * kMaxTaps + 2];  // the epoch's tap sums (+ the data prompt at 2·kMaxTaps), as epoch_pre reads them
@@ -129,7 +144,8 @@ struct FShared {
     int32_t locked;
     int32_t tail_seq;   // e + 1 once wave 1 stored epoch e's N mod 16 tail products
     int32_t acc_groups; // product groups the accumulator has consumed (counted over the run)
-    int32_t pad;
+    int32_t step_seq;   // e + 1 once wave 0 published epoch e's early loop values (state 4, SpecArgs)
+    SpecArgs spec;      // those values
     f2 tailp[kAvxLanes][kMaxTaps + 1];  // the tail's products (sample 16M + j, tap), wave 1 → wave 0
 };
 
@@ -348,6 +364,46 @@ __device__ __forceinline__ float fast_replay(float x, float c, float k2, int M, 
     return x;
 }
 
+// fast_replay (whole-epoch slots) started before the epoch's seed, on the predicted phasors: at every
+// task the seed's arrival is polled (the load issued at the task's start, read at its end) and
+// `check` is run once it is there — it returns 1 (the prediction holds: the job is published and the
+// producers consume the slots as they come) or 2 (it does not: the replay stops here).  `status`
+// (0 / 1 / 2) is wave-uniform.
+template <int G, class Check>
+__device__ __forceinline__ float fast_replay_spec(float x, float c, float k2, int M, int S, int tail, uint64_t* __restrict__ Zs, int lane,
+    const int32_t* seed_seq, int need, int& status, Check&& check)
+{
+    static_assert(G % 4 == 0 && G >= 4 && G <= 64, "task length");
+    constexpr int kTB = 64 / G;
+    if (S <= 0) return x;
+    const uint32_t base = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(Zs)) + 4u * static_cast<uint32_t>(lane);
+    uint32_t off = base;
+    constexpr uint32_t kSlotRow = kAvxLanes * sizeof(uint64_t);
+    uint32_t* const half0 = reinterpret_cast<uint32_t*>(Zs) + lane;
+#pragma unroll 1
+    for (int t = 0; t < S - 1; t++) {
+        int v = 0;
+        if (status == 0) v = __hip_atomic_load(seed_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (t % kTB == 0)
+            x = ppow<G - 1>(pnormalise(pstep<1, true>(x, c, k2, off)), c, k2);
+        else
+            x = ppow<G - 4>(pstep<4, true>(x, c, k2, off), c, k2);
+        off += kSlotRow;
+        if (status == 0 && __builtin_amdgcn_readfirstlane(v) >= need) {
+            status = __builtin_amdgcn_readfirstlane(check());
+            if (status == 2) return x;
+        }
+    }
+    __hip_atomic_store(half0 + 2 * kAvxLanes * (S - 1), __builtin_bit_cast(uint32_t, x), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (tail > 0) {
+        for (int m = G * (S - 1); m < M; m++) {
+            x = pstep<1, false>(x, c, k2, 0);
+            if ((m & 63) == 0) x = pnormalise(x);
+        }
+    }
+    return x;
+}
+
 // Producer phase A, before the group's phasor slots are ready: the code value of every tap at
 // every sample of this lane's task (the resampler, volk_gnsssdr_32f_xn_resampler_32f_xn.h:63-80), in
 // registers — it depends only on the code NCO, so it runs ahead of the replay.
@@ -516,26 +572,41 @@ __device__ __forceinline__ void fast_accumulate(const float* __restrict__ Pp, in
         if (g == 0) GNSSHIP_FSTAMP(pe, 28);
         if (g == n_groups - 1) GNSSHIP_FSTAMP(pe, 29);
         if (g < 8) GNSSHIP_FSTAMP(pe, 56 + g);
-        // every group is added whole: a partial group's iterations past the epoch's end hold −0
+        // every group is added whole: a partial group's iterations past the epoch's end hold −0.
+        // Batches of kU iterations, the next batch's loads issued before the current one's adds.
         const float* src = Pp + static_cast<size_t>(rslot) * PL::kGroup;
+        constexpr int kJ = 4 * G;
+        constexpr int kU = GNSSHIP_ACC_BATCH < kJ ? GNSSHIP_ACC_BATCH : kJ;
+        static_assert(kJ % kU == 0, "accumulator batch");
+        auto at = [&](int j, int k) { return src[off[k] + (j / G) * PL::kTask + (j % G) * PL::kIter]; };
+        float cur[kU][NS];
 #pragma unroll
-        for (int t = 0; t < 4; t++) {
-            constexpr int kU = G < 8 ? G : 8;  // iterations whose loads are in flight together
+        for (int u = 0; u < kU; u++)
 #pragma unroll
-            for (int i0 = 0; i0 < G; i0 += kU) {
-                float v[kU][NS];
+            for (int k = 0; k < NS; k++) cur[u][k] = at(u, k);
+#pragma unroll
+        for (int j0 = 0; j0 < kJ; j0 += kU) {
+            float nxt[kU][NS];
+            if (j0 + kU < kJ) {
 #pragma unroll
                 for (int u = 0; u < kU; u++)
 #pragma unroll
-                    for (int k = 0; k < NS; k++) v[u][k] = src[off[k] + t * PL::kTask + (i0 + u) * PL::kIter];
+                    for (int k = 0; k < NS; k++) nxt[u][k] = at(j0 + kU + u, k);
+            }
+#pragma unroll
+            for (int u = 0; u < kU; u++)
+#pragma unroll
+                for (int k = 0; k < NS; k++) acc[k] = __fadd_rn(acc[k], cur[u][k]);
+            if (j0 + kU < kJ) {
 #pragma unroll
                 for (int u = 0; u < kU; u++)
 #pragma unroll
-                    for (int k = 0; k < NS; k++) acc[k] = __fadd_rn(acc[k], v[u][k]);
+                    for (int k = 0; k < NS; k++) cur[u][k] = nxt[u][k];
             }
         }
         asm volatile("" ::: "memory");  // the group's loads are issued (and used) before it is released
         if (lane == 0) lds_release_store(acc_groups, gbase + g + 1);
+        if (g < 8) GNSSHIP_FSTAMP(pe, 64 + g);
         rslot = rslot + 1 == rg ? 0 : rslot + 1;
     }
 }
@@ -599,6 +670,42 @@ __device__ __forceinline__ const auto& loop_params(const TrkParams& k, const KFa
         return kf;
 }
 
+// The carrier step's phasor inc = (cos −step, sin −step) (cpu_multicorrelator_real_codes.cc:123, glibc
+// cosf / sinf) and the AVX rotator's dz = normalise(inc^16) by four squarings (:215-225).
+__device__ __forceinline__ void derive_step(float step, f2& inc, f2& dz)
+{
+    float s, c;
+    glibc_sincosf(-step, &s, &c);
+    inc = f2{c, s};
+    f2 d = inc;
+#pragma unroll
+    for (int i = 0; i < 4; i++) d = cmul_exact_sc(d, d);
+    dz = normalise_avx(d);
+}
+
+// a wave-uniform 64-bit value as scalar registers
+__device__ __forceinline__ uint64_t uni64(uint64_t v)
+{
+    const uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(v)), hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(v >> 32));
+    return (static_cast<uint64_t>(hi) << 32) | lo;
+}
+
+// z_l = phase·inc^l, the generic chain (:204-208) from phase = (cos rem, −sin rem) (glibc cosf / sinf,
+// cpu_multicorrelator_real_codes.cc:115), for the replay's lane pairs (lanes 2l, 2l + 1: chain l).
+__device__ __forceinline__ f2 derive_chains(float rem, f2 inc, int lane)
+{
+    float sfn, cfn;
+    glibc_sincosf(rem, &sfn, &cfn);
+    const f2 p0 = f2{cfn, -sfn};
+    f2 w = p0, z = p0;
+#pragma unroll
+    for (int i = 0; i < kAvxLanes - 1; i++) {
+        w = cmul_exact_sc(w, inc);
+        z = i + 1 == (lane >> 1) ? w : z;
+    }
+    return z;
+}
+
 template <int FMT, int NT, bool DATA, int G, bool THRU, bool SRING>
 __global__ __launch_bounds__(kFThreads, fast_waves_per_simd<THRU>()) void trk_fast_kernel(const TrkParams* __restrict__ pk, TrkChannel* __restrict__ chans,
     const CodeDesc* __restrict__ codes, int n_codes, const void* __restrict__ samples, uint64_t buf_first, int64_t buf_len, int max_rounds,
@@ -631,6 +738,9 @@ __global__ __launch_bounds__(kFThreads, fast_waves_per_simd<THRU>()) void trk_fa
     for (int i = tid; i < rg; i += kFThreads) ready[i] = 0;
     __shared__ int32_t simd_of[kFWaves];
     if (lane == 0) simd_of[wave] = static_cast<int32_t>((__builtin_amdgcn_s_getreg(4 | (31 << 11)) >> 4) & 3);  // HW_ID.SIMD_ID
+#ifdef GNSSHIP_CORR_PROFILE
+    for (int i = tid; i < kFProfEpochs * kFProfSlots; i += kFThreads) g_fprof_lds[i] = 0;
+#endif
     __syncthreads();
     // the role of each wave: the first two waves alone on their SIMD take the phasor and control
     // roles (in that order), the others produce; without two such SIMDs, waves 1 and 0 do
@@ -672,14 +782,14 @@ __global__ __launch_bounds__(kFThreads, fast_waves_per_simd<THRU>()) void trk_fa
         sh.lock_seq = 0;
         sh.tail_seq = 0;
         sh.acc_groups = 0;
+        sh.step_seq = 0;
     }
     __syncthreads();
     if (skip) return;  // idle channel: its state is untouched
     if (wave < 4) GNSSHIP_FHWID(20 + wave);  // epoch 0's slots 20-23 (the epoch loop stamps 0-15)
 #ifdef GNSSHIP_CORR_PROFILE
-    if (g_trkf_prof && lane == 0)  // epoch 2's slots 41-46: HW_ID | role << 32 of every wave
-        g_trkf_prof[(static_cast<size_t>(blockIdx.x) * kFProfEpochs + 2) * kFProfSlots + 41 + wave] =
-            static_cast<uint32_t>(__builtin_amdgcn_s_getreg(4 | (31 << 11))) | (static_cast<unsigned long long>(role) << 32);
+    if (g_trkf_prof && lane == 0)  // row 0's slots 72-77: HW_ID | role << 32 of every wave
+        g_fprof_lds[72 + wave] = static_cast<uint32_t>(__builtin_amdgcn_s_getreg(4 | (31 << 11))) | (static_cast<unsigned long long>(role) << 32);
 #endif
     stage_code_f(code0, codes[sc.code_id]);
     if constexpr (DATA) stage_code_f(code1, codes[sc.data_code_id]);
@@ -696,7 +806,19 @@ __global__ __launch_bounds__(kFThreads, fast_waves_per_simd<THRU>()) void trk_fa
     if (role == kRoleControl) rchan_load(sc, &sc, rc);
     // wave 0's loop parameters in registers for the run (two workgroups per CU have no registers to
     // spare: they keep reading TrkParams)
-    const KFast kf = make_kfast(k, sc.geo);
+    KFast kf = make_kfast(k, sc.geo);
+    // the sign patterns epoch_pre reads every epoch (bit_at), in LDS: a global load there is a
+    // dependent memory round trip on the loop's chain
+    __shared__ uint32_t sec_bits[kTrkMaxSecondary / 32], dsec_bits[kTrkMaxSecondary / 32];
+    if constexpr (!THRU) {
+        if (tid < kTrkMaxSecondary / 32) {
+            sec_bits[tid] = kf.sv.secondary_bits[tid];
+            dsec_bits[tid] = kf.sv.data_secondary_bits[tid];
+        }
+        kf.sv.secondary_bits = sec_bits;
+        kf.sv.data_secondary_bits = dsec_bits;
+        __syncthreads();
+    }
     const auto& kp = loop_params<THRU>(k, kf);
     // Wave roles (one channel per workgroup, its epochs a serial chain):
     //   control  — the accumulation in u_avx order, the loop update on its register-resident
@@ -762,235 +884,309 @@ __global__ __launch_bounds__(kFThreads, fast_waves_per_simd<THRU>()) void trk_fa
     if (role == kRoleControl) make_seed(0);
     int e_done = 0;
     bool cancel = false;  // wave 0: the current epoch was seeded before a lock test that failed
-    for (int e = 0;; e++) {
-        const int gbase = e * n_groups;  // the epoch's first product-group tag - 1
-        FJob job;
-        if (role == kRoleReplay) {
-            // ---- derive: the phasors of the seeded epoch ----
-            wait_seq(&sh.seed_seq, e + 1);
-            GNSSHIP_FSTAMP(e, 0);
-#ifdef GNSSHIP_CORR_PROFILE
-            if (lane == 0) g_fprof_epoch = e;
-#endif
-            const FJob sd = uniform_job(sh.job);
-            f2 zinit = f2{0.0f, 0.0f}, inc = f2{1.0f, 0.0f};
-            if (sd.runnable) {
-                // (cos rem, −sin rem) and (cos −step, sin −step) (cpu_multicorrelator_real_codes.cc:115,123):
-                // lane 0 the phase, lane 1 the step, each glibc's cosf / sinf (glibc_sincosf.h)
-                const float a = lane == 0 ? sd.rem_carr : -sd.step;
-                float sfn, cfn;
-                glibc_sincosf(a, &sfn, &cfn);
-                const int sfi = __builtin_bit_cast(int, sfn), cfi = __builtin_bit_cast(int, cfn);
-                const f2 p0 = f2{__builtin_bit_cast(float, __builtin_amdgcn_readlane(cfi, 0)), -__builtin_bit_cast(float, __builtin_amdgcn_readlane(sfi, 0))};
-                inc = f2{__builtin_bit_cast(float, __builtin_amdgcn_readlane(cfi, 1)), __builtin_bit_cast(float, __builtin_amdgcn_readlane(sfi, 1))};
-                GNSSHIP_FSTAMP(e, 35);
-                // z_l = phase·inc^l, the generic chain (:204-208), for the replay's lane pairs, and
-                // dz = normalise(inc^16) by four squarings (:215-225): two independent chains of
-                // scalar exact products (a dependent packed product issues several times slower)
-                f2 w = p0, z = p0, d = inc;
-#pragma unroll
-                for (int i = 0; i < kAvxLanes - 1; i++) {
-                    w = cmul_exact_sc(w, inc);
-                    if (i < 4) d = cmul_exact_sc(d, d);
-                    z = i + 1 == (lane >> 1) ? w : z;  // lanes 2l, 2l + 1: chain l (off the chain)
+    // One epoch loop per role: the roles never share a control-flow path, so the waits the compiler
+    // places for one role's memory operations are not charged to another (a merged loop made the
+    // control wave wait for the producers' sample loads it never issued).
+    if (role == kRoleReplay) {
+        for (int e = 0;; e++) {
+            FJob job;
+                // ---- derive: the phasors of the seeded epoch ----
+                // In state 4 the loop publishes its early values (SpecArgs) once the carrier filter ran,
+                // before the DLL, update_tracking_vars and the seed.  With whole-epoch slots the next
+                // epoch's phasors are then derived from them — the step exactly, the remainder phase for
+                // an unchanged epoch length — and replayed speculatively; the seed, when it comes, confirms
+                // both floats (the job is published mid-replay) or the slots are cleared and the epoch is
+                // derived again from the seed.  With the slot ring only the step's part is done early.
+                bool spec = false;
+                SpecArgs sp{};
+                while (__hip_atomic_load(&sh.seed_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < e + 1) {
+                    if (__hip_atomic_load(&sh.step_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= e + 1) {
+                        sp.step_d = __builtin_bit_cast(double, uni64(__builtin_bit_cast(uint64_t, sh.spec.step_d)));
+                        sp.rate = __builtin_bit_cast(double, uni64(__builtin_bit_cast(uint64_t, sh.spec.rate)));
+                        sp.if_num = static_cast<int64_t>(uni64(static_cast<uint64_t>(sh.spec.if_num)));
+                        sp.rem_prev = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, sh.spec.rem_prev)));
+                        sp.n_pred = __builtin_amdgcn_readfirstlane(sh.spec.n_pred);
+                        spec = true;
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(GNSSHIP_POLL_SLEEP);
                 }
-                const f2 dz = normalise_avx(d);
-                zinit = z;
-                GNSSHIP_FSTAMP(e, 36);
-                if (lane == 0) {
-                    sh.job.dz_re = dz.x;
-                    sh.job.dz_im = dz.y;
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                GNSSHIP_FSTAMP(e, 0);
+    #ifdef GNSSHIP_CORR_PROFILE
+                if (lane == 0) g_fprof_epoch = e;
+    #endif
+                f2 zinit = f2{0.0f, 0.0f}, inc = f2{1.0f, 0.0f}, dz = f2{1.0f, 0.0f};
+                float step_pre = 0.0f;
+                bool published = false;
+                float xl = 0.0f;
+                if (spec) {
+                    step_pre = static_cast<float>(sp.step_d + if_step);  // make_seed's j.step
+                    derive_step(step_pre, inc, dz);
                 }
-            }
-            if (lane == 0) publish_seq(&sh.job_seq, e + 1);
-            GNSSHIP_FSTAMP(e, 1);
-            GNSSHIP_FCLK(e, 12);
-            if (!sd.runnable) break;
-            job = uniform_job(sh.job);
-            float xl = (lane & 1) ? zinit.y : zinit.x;
-            if (lane < 2 * kAvxLanes) xl = fast_replay<G, SRING>(xl, job.dz_re, (lane & 1) ? job.dz_im : -job.dz_im, M, S, tail, Zs, rs, lane);
-            if (tail > 0) {  // the serial tail from normalise(z_0) after the loop (:294-308)
+                if (!SRING && spec) {
+                    // make_seed's j.rem_carr after update_tracking_vars and epoch_consume, for n = n_pred
+                    float rem_pred = carr_rem_next(sp.rem_prev, carr_advance(sp.step_d, sp.rate, static_cast<double>(sp.n_pred)));
+                    if (has_if) {
+                        const int64_t ifn = (sp.if_num + kp.if_mod * static_cast<int64_t>(sp.n_pred)) % kp.fs_int;
+                        const double ifc = static_cast<double>(ifn) / static_cast<double>(kp.fs_int);
+                        rem_pred = static_cast<float>(fmod_2pi(static_cast<double>(rem_pred) + kTwoPi * ifc));
+                    }
+                    zinit = derive_chains(rem_pred, inc, lane);
+                    GNSSHIP_FSTAMP(e, 35);
+                    auto check = [&]() -> int {
+                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                        const FJob sd = uniform_job(sh.job);
+                        if (sd.runnable && __builtin_bit_cast(uint32_t, sd.step) == __builtin_bit_cast(uint32_t, step_pre) &&
+                            __builtin_bit_cast(uint32_t, sd.rem_carr) == __builtin_bit_cast(uint32_t, rem_pred)) {
+                            if (lane == 0) {
+                                sh.job.dz_re = dz.x;
+                                sh.job.dz_im = dz.y;
+                                publish_seq(&sh.job_seq, e + 1);
+                            }
+                            return 1;
+                        }
+                        return 2;
+                    };
+                    int status = 0;
+                    xl = (lane & 1) ? zinit.y : zinit.x;
+                    if (lane < 2 * kAvxLanes) xl = fast_replay_spec<G>(xl, dz.x, (lane & 1) ? dz.y : -dz.y, M, S, tail, Zs, lane, &sh.seed_seq, e + 1, status, check);
+                    status = __builtin_amdgcn_readfirstlane(status);
+                    if (status == 0) {
+                        wait_seq(&sh.seed_seq, e + 1);
+                        status = check();
+                    }
+                    if (status == 1) {
+                        published = true;
+                    } else {  // mispredicted (or the end of the run): the slots are cleared before the job goes out
+                        for (int i = lane; i < S * kAvxLanes; i += kWave) Zs[i] = kSlotEmpty;
+                    }
+                    GNSSHIP_FSTAMP(e, 36);
+                }
+                if (!published) {
+                    wait_seq(&sh.seed_seq, e + 1);
+                    const FJob sd = uniform_job(sh.job);
+                    if (sd.runnable) {
+                        // (cos rem, −sin rem) and (cos −step, sin −step) (cpu_multicorrelator_real_codes.cc:115,123),
+                        // each glibc's cosf / sinf (glibc_sincosf.h)
+                        if (!(spec && __builtin_bit_cast(uint32_t, sd.step) == __builtin_bit_cast(uint32_t, step_pre))) derive_step(sd.step, inc, dz);
+                        zinit = derive_chains(sd.rem_carr, inc, lane);
+                        if (lane == 0) {
+                            sh.job.dz_re = dz.x;
+                            sh.job.dz_im = dz.y;
+                        }
+                    }
+                    if (lane == 0) publish_seq(&sh.job_seq, e + 1);
+                    if (!sd.runnable) break;
+                }
+                GNSSHIP_FSTAMP(e, 1);
+                GNSSHIP_FCLK(e, 12);
+                job = uniform_job(sh.job);
+                if (!published) {
+                    xl = (lane & 1) ? zinit.y : zinit.x;
+                    if (lane < 2 * kAvxLanes) xl = fast_replay<G, SRING>(xl, job.dz_re, (lane & 1) ? job.dz_im : -job.dz_im, M, S, tail, Zs, rs, lane);
+                }
+                if (tail > 0) {  // the serial tail from normalise(z_0) after the loop (:294-308)
+                    const i4v span = sample_span<FMT>(samples, job.off, N);
+                    const f2 zl = f2{__builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, xl), 0)),
+                        __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, xl), 1))};
+                    if (lane == 0) {
+                        f2 p = normalise_avx(zl);
+                        for (int j = 0; j < tail; j++) {
+                            tailz[j] = p;
+                            p = cmul_exact(p, inc);
+                        }
+                    }
+                    if (job.in_margin)
+                        fast_tail_products<FMT, NT, DATA, true>(job, span, c0, c1, L, tailz, lane, sh.tailp);
+                    else
+                        fast_tail_products<FMT, NT, DATA, false>(job, span, c0, c1, L, tailz, lane, sh.tailp);
+                    if (lane == 0) publish_seq(&sh.tail_seq, e + 1);
+                }
+                GNSSHIP_FSTAMP(e, 2);
+                GNSSHIP_FCLK(e, 13);
+        }
+    } else if (role == kRoleProducer) {
+        for (int e = 0;; e++) {
+            const int gbase = e * n_groups;  // the epoch's first product-group tag - 1
+            wait_seq(&sh.job_seq, e + 1);
+            const FJob job = uniform_job(sh.job);
+            if (!job.runnable) break;
                 const i4v span = sample_span<FMT>(samples, job.off, N);
-                const f2 zl = f2{__builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, xl), 0)),
-                    __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, xl), 1))};
-                if (lane == 0) {
-                    f2 p = normalise_avx(zl);
-                    for (int j = 0; j < tail; j++) {
-                        tailz[j] = p;
-                        p = cmul_exact(p, inc);
-                    }
-                }
                 if (job.in_margin)
-                    fast_tail_products<FMT, NT, DATA, true>(job, span, c0, c1, L, tailz, lane, sh.tailp);
+                    fast_produce<FMT, NT, DATA, true, G>(job, span, c0, c1, L, Zs, rs, Pp, rg, ready, &sh.acc_groups, gbase, lane, pw, e);
                 else
-                    fast_tail_products<FMT, NT, DATA, false>(job, span, c0, c1, L, tailz, lane, sh.tailp);
-                if (lane == 0) publish_seq(&sh.tail_seq, e + 1);
-            }
-            GNSSHIP_FSTAMP(e, 2);
-            GNSSHIP_FCLK(e, 13);
-            continue;
-        }
-        wait_seq(&sh.job_seq, e + 1);
-        job = uniform_job(sh.job);
-        if (!job.runnable) break;
-        if (role == kRoleProducer) {
-            const i4v span = sample_span<FMT>(samples, job.off, N);
-            if (job.in_margin)
-                fast_produce<FMT, NT, DATA, true, G>(job, span, c0, c1, L, Zs, rs, Pp, rg, ready, &sh.acc_groups, gbase, lane, pw, e);
-            else
-                fast_produce<FMT, NT, DATA, false, G>(job, span, c0, c1, L, Zs, rs, Pp, rg, ready, &sh.acc_groups, gbase, lane, pw, e);
-            if (pw < 2) GNSSHIP_FSTAMP(e, 3 + pw);  // 3, 4: producers 0 and 1 done
-            if (pw == 0) {
-                // cn0_and_tracking_lock_status (:972-1029) on the LDS copy of its members, beside the loop update
-                wait_seq(&sh.pre_seq, e + 1);
-                const double coh = sh.coh;
-                if (lane == 0) {
-                    GNSSHIP_TRK_LOOP_STAMP(8);
-                    sh.locked = (coh > 0.0 && !lock_status(k, sc, coh)) ? 0 : 1;
-                    GNSSHIP_TRK_LOOP_STAMP(26);
-                    publish_seq(&sh.lock_seq, e + 1);
+                    fast_produce<FMT, NT, DATA, false, G>(job, span, c0, c1, L, Zs, rs, Pp, rg, ready, &sh.acc_groups, gbase, lane, pw, e);
+                if (pw < 2) GNSSHIP_FSTAMP(e, 3 + pw);  // 3, 4: producers 0 and 1 done
+                if (pw == 0) {
+                    // cn0_and_tracking_lock_status (:972-1029) on the LDS copy of its members, beside the loop update
+                    wait_seq(&sh.pre_seq, e + 1);
+                    const double coh = sh.coh;
+                    if (lane == 0) {
+                        GNSSHIP_TRK_LOOP_STAMP(8);
+                        sh.locked = (coh > 0.0 && !lock_status(k, sc, coh)) ? 0 : 1;
+                        GNSSHIP_TRK_LOOP_STAMP(26);
+                        publish_seq(&sh.lock_seq, e + 1);
+                    }
                 }
-            }
-            continue;
         }
-        // ---- wave 0: the epoch's taps in u_avx's order ----
-        {
-            constexpr int NS = acc_slots<NTT>();
-            float acc[NS];
-            GNSSHIP_FSTAMP(e, 27);
-            fast_accumulate<NTT, G>(Pp, rg, ready, &sh.acc_groups, gbase, M, S, lane, acc, e);
-            GNSSHIP_FSTAMP(e, 5);
-            const int r = lane >> 4;
-#pragma unroll
-            for (int kk = 0; kk < NS; kk++) acc[kk] = avx_chain_sum(acc[kk]);
-            if (job.tail > 0) {  // the serial tail, sample by sample (:298-308)
-                wait_seq(&sh.tail_seq, e + 1);
-                for (int j = 0; j < job.tail; j++) {
-#pragma unroll
+    } else {
+        for (int e = 0;; e++) {
+            const int gbase = e * n_groups;  // the epoch's first product-group tag - 1
+            wait_seq(&sh.job_seq, e + 1);
+            const FJob job = uniform_job(sh.job);
+            if (!job.runnable) break;
+            // ---- wave 0: the epoch's taps in u_avx's order ----
+            {
+                constexpr int NS = acc_slots<NTT>();
+                float acc[NS];
+                GNSSHIP_FSTAMP(e, 27);
+                fast_accumulate<NTT, G>(Pp, rg, ready, &sh.acc_groups, gbase, M, S, lane, acc, e);
+                GNSSHIP_FSTAMP(e, 5);
+                const int r = lane >> 4;
+    #pragma unroll
+                for (int kk = 0; kk < NS; kk++) acc[kk] = avx_chain_sum(acc[kk]);
+                if (job.tail > 0) {  // the serial tail, sample by sample (:298-308)
+                    wait_seq(&sh.tail_seq, e + 1);
+                    for (int j = 0; j < job.tail; j++) {
+    #pragma unroll
+                        for (int kk = 0; kk < NS; kk++) {
+                            const int sl = min(r + 4 * kk, 2 * NTT - 1);
+                            const f2 tv = sh.tailp[j][sl >> 1];
+                            acc[kk] = acc[kk] + ((sl & 1) ? tv.y : tv.x);
+                        }
+                    }
+                }
+                if ((lane & 15) == 0) {
+    #pragma unroll
                     for (int kk = 0; kk < NS; kk++) {
-                        const int sl = min(r + 4 * kk, 2 * NTT - 1);
-                        const f2 tv = sh.tailp[j][sl >> 1];
-                        acc[kk] = acc[kk] + ((sl & 1) ? tv.y : tv.x);
+                        const int sl = r + 4 * kk;  // slot 2·tap + component
+                        if (sl < 2 * NTT) {
+                            const int tap = sl >> 1;
+                            const int o = (DATA && tap == NT) ? 2 * kMaxTaps : 2 * tap;
+                            sh.taps[o + (sl & 1)] = acc[kk];
+                        }
                     }
                 }
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             }
-            if ((lane & 15) == 0) {
-#pragma unroll
-                for (int kk = 0; kk < NS; kk++) {
-                    const int sl = r + 4 * kk;  // slot 2·tap + component
-                    if (sl < 2 * NTT) {
-                        const int tap = sl >> 1;
-                        const int o = (DATA && tap == NT) ? 2 * kMaxTaps : 2 * tap;
-                        sh.taps[o + (sl & 1)] = acc[kk];
+            GNSSHIP_FSTAMP(e, 6);
+            GNSSHIP_FCLK(e, 14);
+            if (cancel) {
+                // the epoch seeded speculatively before the last lock test failed: the channel stopped
+                // there (state 0), so nothing of this epoch is kept — no lock test, no record — and
+                // the seed for the next one says "not runnable", which ends every wave's loop
+                cancel = false;
+                if (lane == 0) {
+                    sh.coh = 0.0;
+                    publish_seq(&sh.pre_seq, e + 1);
+                }
+                make_seed(e + 1);
+                continue;
+            }
+            {
+                const float* taps = sh.taps;
+                GNSSHIP_FSTAMP(e, 16);
+                const float* pdata = DATA ? taps + 2 * kMaxTaps : taps;
+                gnsship_trk_epoch r{};
+                r.flags = 8;
+                gnsship_trk_dump_record* dr = dump ? &sh.drec : nullptr;
+                const uint64_t es = rc.epoch_start;  // this epoch's first sample
+                const double coh = epoch_pre(kp, rc, taps, pdata, r, nullptr, dr);
+                GNSSHIP_FSTAMP(e, 17);
+                // hand the prompt to the lock detectors (wave 2; coh 0: no lock test this epoch)
+                if (lane == 0) {
+                    sc.p[0] = rc.p[0];
+                    sc.p[1] = rc.p[1];
+                    sc.pull_in = rc.pull_in;
+                    sh.coh = coh;
+                    publish_seq(&sh.pre_seq, e + 1);
+                }
+                GNSSHIP_FSTAMP(e, 18);
+                bool seeded = false;
+                if (coh > 0.0) {  // the loop runs speculatively beside the lock test
+                    // what the record shows if the test fails (the channel then stops: nothing else of the
+                    // loop's output is ever read)
+                    const double k_rcs = rc.rem_code_phase_samples, k_acc = rc.acc_carrier_phase_rad, k_dop = rc.carrier_doppler_hz;
+                    const double k_cf = rc.code_freq_chips, k_rcc = rc.rem_code_phase_chips;
+                    const float k_rem = rc.rem_carr_phase_rad;
+                    const int32_t k_len = rc.current_prn_length_samples;
+                    // state 4: the next epoch's carrier step to wave 1 once the carrier filter ran (the seed
+                    // repeats it; wave 1 checks they agree)
+                    auto early_step = [&](double dop) {
+                        if (rc.state == 4 && lane == 0) {
+                            sh.spec.step_d = div_fs(kp, kTwoPi * dop);  // update_tracking_vars' carrier_phase_step_rad
+                            sh.spec.rate = rc.carrier_phase_rate_step_rad;
+                            sh.spec.if_num = rc.if_num;
+                            sh.spec.rem_prev = rc.rem_carr_phase_rad;
+                            sh.spec.n_pred = rc.current_prn_length_samples;
+                            publish_seq(&sh.step_seq, e + 2);
+                        }
+                    };
+                    epoch_loop(kp, rc, nullptr, early_step);
+                    // State 4: epoch_post cannot change what the next epoch's correlation needs (the
+                    // channel stays runnable — 4, or 3 for extended integration — on the same taps), so
+                    // the next epoch is seeded now, before the lock test's outcome, and wave 1 derives
+                    // it while this epoch finishes.  A failed test (the channel stops) cancels it.
+                    const uint64_t k_nir = rc.nitems_read;
+                    const int64_t k_ifn = rc.if_num;
+                    const double k_ifc = rc.if_cyc;
+                    if (rc.state == 4) {
+                        epoch_consume(kp, rc);
+                        make_seed(e + 1);
+                        GNSSHIP_FSTAMP(e, 33);
+                        rc.epoch_start = es;  // epoch_post and the record still describe this epoch
+                        seeded = true;
+                    }
+                    wait_seq(&sh.lock_seq, e + 1);
+                    GNSSHIP_FSTAMP(e, 19);
+                    const bool locked = sh.locked != 0;
+                    if (!locked) {  // the reference runs the loop only on a passed lock test
+                        rc.rem_code_phase_samples = k_rcs;
+                        rc.acc_carrier_phase_rad = k_acc;
+                        rc.carrier_doppler_hz = k_dop;
+                        rc.code_freq_chips = k_cf;
+                        rc.rem_code_phase_chips = k_rcc;
+                        rc.rem_carr_phase_rad = k_rem;
+                        rc.current_prn_length_samples = k_len;
+                        rc.nitems_read = k_nir;
+                        rc.if_num = k_ifn;
+                        rc.if_cyc = k_ifc;
+                        cancel = seeded;
+                    }
+                    epoch_post(kp, rc, taps, pdata, r, locked, dr);
+                }
+                GNSSHIP_FSTAMP(e, 24);
+                epoch_finish(kp, rc, r, !seeded);  // (a stopped channel consumes nothing either way)
+                if (!seeded)
+                    make_seed(e + 1);  // wave 1 derives the next epoch while the records go out
+                else if (!cancel)
+                    rc.epoch_start = seed_start;  // the next epoch, as make_seed left it
+                GNSSHIP_FSTAMP(e, 25);
+                if (lane == 0) {
+                    const size_t slot = static_cast<size_t>(e) * n_chans + ch;
+                    if (rec) rec[slot] = r;
+                    if (dump && (r.flags & 16)) dump[slot] = sh.drec;
+                    if (trace) {
+                        gnsship_trk_corr_trace tr{};
+                        tr.sample_counter = es;
+                        tr.n_samples = N;
+                        tr.n_taps = NT;
+                        tr.rem_carrier_phase_rad = job.rem_carr;
+                        tr.phase_step_rad = job.step;
+                        tr.rem_code_phase_samples = job.rem_code;
+                        tr.code_phase_step_samples = job.code_step;
+                        for (int t = 0; t < 5; t++) tr.shifts[t] = job.shifts[t];
+                        for (int t = 0; t < 10; t++) tr.taps[t] = t < 2 * NT ? taps[t] : 0.0f;
+                        tr.data_prompt[0] = DATA ? pdata[0] : 0.0f;
+                        tr.data_prompt[1] = DATA ? pdata[1] : 0.0f;
+                        trace[slot] = tr;
                     }
                 }
+                e_done = e + 1;
+                GNSSHIP_FSTAMP(e, 7);
+                GNSSHIP_FCLK(e, 15);
             }
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        }
-        GNSSHIP_FSTAMP(e, 6);
-        GNSSHIP_FCLK(e, 14);
-        if (cancel) {
-            // the epoch seeded speculatively before the last lock test failed: the channel stopped
-            // there (state 0), so nothing of this epoch is kept — no lock test, no record — and
-            // the seed for the next one says "not runnable", which ends every wave's loop
-            cancel = false;
-            if (lane == 0) {
-                sh.coh = 0.0;
-                publish_seq(&sh.pre_seq, e + 1);
-            }
-            make_seed(e + 1);
-            continue;
-        }
-        {
-            const float* taps = sh.taps;
-            GNSSHIP_FSTAMP(e, 16);
-            const float* pdata = DATA ? taps + 2 * kMaxTaps : taps;
-            gnsship_trk_epoch r{};
-            r.flags = 8;
-            gnsship_trk_dump_record* dr = dump ? &sh.drec : nullptr;
-            const uint64_t es = rc.epoch_start;  // this epoch's first sample
-            const double coh = epoch_pre(kp, rc, taps, pdata, r, nullptr, dr);
-            GNSSHIP_FSTAMP(e, 17);
-            // hand the prompt to the lock detectors (wave 2; coh 0: no lock test this epoch)
-            if (lane == 0) {
-                sc.p[0] = rc.p[0];
-                sc.p[1] = rc.p[1];
-                sc.pull_in = rc.pull_in;
-                sh.coh = coh;
-                publish_seq(&sh.pre_seq, e + 1);
-            }
-            GNSSHIP_FSTAMP(e, 18);
-            bool seeded = false;
-            if (coh > 0.0) {  // the loop runs speculatively beside the lock test
-                // what the record shows if the test fails (the channel then stops: nothing else of the
-                // loop's output is ever read)
-                const double k_rcs = rc.rem_code_phase_samples, k_acc = rc.acc_carrier_phase_rad, k_dop = rc.carrier_doppler_hz;
-                const double k_cf = rc.code_freq_chips, k_rcc = rc.rem_code_phase_chips;
-                const float k_rem = rc.rem_carr_phase_rad;
-                const int32_t k_len = rc.current_prn_length_samples;
-                epoch_loop(kp, rc, nullptr);
-                // State 4: epoch_post cannot change what the next epoch's correlation needs (the
-                // channel stays runnable — 4, or 3 for extended integration — on the same taps), so
-                // the next epoch is seeded now, before the lock test's outcome, and wave 1 derives
-                // it while this epoch finishes.  A failed test (the channel stops) cancels it.
-                const uint64_t k_nir = rc.nitems_read;
-                const int64_t k_ifn = rc.if_num;
-                const double k_ifc = rc.if_cyc;
-                if (rc.state == 4) {
-                    epoch_consume(kp, rc);
-                    make_seed(e + 1);
-                    GNSSHIP_FSTAMP(e, 33);
-                    rc.epoch_start = es;  // epoch_post and the record still describe this epoch
-                    seeded = true;
-                }
-                wait_seq(&sh.lock_seq, e + 1);
-                GNSSHIP_FSTAMP(e, 19);
-                const bool locked = sh.locked != 0;
-                if (!locked) {  // the reference runs the loop only on a passed lock test
-                    rc.rem_code_phase_samples = k_rcs;
-                    rc.acc_carrier_phase_rad = k_acc;
-                    rc.carrier_doppler_hz = k_dop;
-                    rc.code_freq_chips = k_cf;
-                    rc.rem_code_phase_chips = k_rcc;
-                    rc.rem_carr_phase_rad = k_rem;
-                    rc.current_prn_length_samples = k_len;
-                    rc.nitems_read = k_nir;
-                    rc.if_num = k_ifn;
-                    rc.if_cyc = k_ifc;
-                    cancel = seeded;
-                }
-                epoch_post(kp, rc, taps, pdata, r, locked, dr);
-            }
-            GNSSHIP_FSTAMP(e, 24);
-            epoch_finish(kp, rc, r, !seeded);  // (a stopped channel consumes nothing either way)
-            if (!seeded)
-                make_seed(e + 1);  // wave 1 derives the next epoch while the records go out
-            else if (!cancel)
-                rc.epoch_start = seed_start;  // the next epoch, as make_seed left it
-            GNSSHIP_FSTAMP(e, 25);
-            if (lane == 0) {
-                const size_t slot = static_cast<size_t>(e) * n_chans + ch;
-                if (rec) rec[slot] = r;
-                if (dump && (r.flags & 16)) dump[slot] = sh.drec;
-                if (trace) {
-                    gnsship_trk_corr_trace tr{};
-                    tr.sample_counter = es;
-                    tr.n_samples = N;
-                    tr.n_taps = NT;
-                    tr.rem_carrier_phase_rad = job.rem_carr;
-                    tr.phase_step_rad = job.step;
-                    tr.rem_code_phase_samples = job.rem_code;
-                    tr.code_phase_step_samples = job.code_step;
-                    for (int t = 0; t < 5; t++) tr.shifts[t] = job.shifts[t];
-                    for (int t = 0; t < 10; t++) tr.taps[t] = t < 2 * NT ? taps[t] : 0.0f;
-                    tr.data_prompt[0] = DATA ? pdata[0] : 0.0f;
-                    tr.data_prompt[1] = DATA ? pdata[1] : 0.0f;
-                    trace[slot] = tr;
-                }
-            }
-            e_done = e + 1;
-            GNSSHIP_FSTAMP(e, 7);
-            GNSSHIP_FCLK(e, 15);
         }
     }
     if (role == kRoleControl && lane == 0) {
@@ -999,6 +1195,10 @@ __global__ __launch_bounds__(kFThreads, fast_waves_per_simd<THRU>()) void trk_fa
         if (e_done > 0) atomicAdd(ran_count + e_done - 1, 1);  // rounds_done = the longest channel's epochs
     }
     __syncthreads();
+#ifdef GNSSHIP_CORR_PROFILE
+    if (g_trkf_prof)
+        for (int i = tid; i < kFProfEpochs * kFProfSlots; i += kFThreads) g_trkf_prof[static_cast<size_t>(blockIdx.x) * kFProfEpochs * kFProfSlots + i] = g_fprof_lds[i];
+#endif
     {
         const int* src = reinterpret_cast<const int*>(&sc);
         int* dst = reinterpret_cast<int*>(chans + ch);

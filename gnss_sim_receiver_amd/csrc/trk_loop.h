@@ -521,8 +521,14 @@ __device__ float carrier_filter(const K& k, C& c, float fll, float pll, float T)
     return e;
 }
 
-template <class K, class C>
-__device__ void run_dll_pll(const K& k, C& c)
+// run_dll_pll's hook after the carrier filter set the Doppler (the fast kernel hands the next epoch's
+// carrier step to its derive wave there); the default does nothing
+struct NoDopplerHook {
+    __device__ void operator()(double) const {}
+};
+
+template <class K, class C, class H = NoDopplerHook>
+__device__ void run_dll_pll(const K& k, C& c, const H& on_doppler = H{})
 {
     double disc;
     if (c.cloop)
@@ -545,6 +551,7 @@ __device__ void run_dll_pll(const K& k, C& c)
         c.carr_error_filt_hz = carrier_filter(k, c, 0.0f, static_cast<float>(c.carr_phase_error_hz), T);
     }
     c.carrier_doppler_hz = c.carr_error_filt_hz;
+    on_doppler(c.carrier_doppler_hz);
     GNSSHIP_TRK_LOOP_STAMP(38);
     if (k.veml) {
         const double early = static_cast<double>(sqrt_rn_f32(__fadd_rn(__fadd_rn(__fadd_rn(__fmul_rn(c.ve[0], c.ve[0]), __fmul_rn(c.ve[1], c.ve[1])),
@@ -590,6 +597,14 @@ __device__ double smoothed_rate(const TrkChannel& c, const TrkHist& h, const dou
     return (cp2 - cp1) / samples;
 }
 
+// update_tracking_vars' carrier advance over the epoch's n samples and the new remainder phase
+// (:1235-1245); the fast kernel's derive wave evaluates the same functions ahead of the loop.
+__device__ __forceinline__ double carr_advance(double step, double rate, double n) { return step * n + 0.5 * rate * n * n; }
+__device__ __forceinline__ float carr_rem_next(float rem, double adv)
+{
+    return static_cast<float>(fmod_2pi(static_cast<double>(__fadd_rn(rem, static_cast<float>(adv)))));
+}
+
 template <class K, class C>
 __device__ void update_tracking_vars(const K& k, C& c, TrkHist* h)
 {
@@ -621,9 +636,8 @@ __device__ void update_tracking_vars(const K& k, C& c, TrkHist* h)
             c.code_phase_rate_step_chips = smoothed_rate(c, *h, h->code, L);
         }
     }
-    const double adv = c.carrier_phase_step_rad * n + 0.5 * c.carrier_phase_rate_step_rad * n * n;
-    c.rem_carr_phase_rad = __fadd_rn(c.rem_carr_phase_rad, static_cast<float>(adv));
-    c.rem_carr_phase_rad = static_cast<float>(fmod_2pi(static_cast<double>(c.rem_carr_phase_rad)));
+    const double adv = carr_advance(c.carrier_phase_step_rad, c.carrier_phase_rate_step_rad, n);
+    c.rem_carr_phase_rad = carr_rem_next(c.rem_carr_phase_rad, adv);
     c.acc_carrier_phase_rad -= adv;
     c.rem_code_phase_samples = c.K_blk_samples - n;
     c.rem_code_phase_chips = div_fs(k, c.code_freq_chips * c.rem_code_phase_samples);
@@ -837,11 +851,11 @@ __device__ double epoch_pre(const K& k, C& c, const float* taps, const float* pd
     return k.code_period * static_cast<double>(syncset(k, c).extend);
 }
 
-template <class K, class C>
-__device__ __forceinline__ void epoch_loop(const K& k, C& c, TrkHist* h)
+template <class K, class C, class H = NoDopplerHook>
+__device__ __forceinline__ void epoch_loop(const K& k, C& c, TrkHist* h, const H& on_doppler = H{})
 {
     GNSSHIP_TRK_LOOP_STAMP(9);
-    run_dll_pll(k, c);
+    run_dll_pll(k, c, on_doppler);
     GNSSHIP_TRK_LOOP_STAMP(10);
     update_tracking_vars(k, c, h);
     GNSSHIP_TRK_LOOP_STAMP(11);

@@ -1,13 +1,20 @@
-# A/B variants of the correlator (scripts/libgnsship_<tag>.so), selected with GNSSHIP_LIB_PATH.
-#   bash scripts/build_variants.sh "w8:-DGNSSHIP_CORR_WAVES_EPL=8" "w6:-DGNSSHIP_CORR_WAVES_EPL=6"
+#!/bin/bash
+# A/B builds of the fast tracking kernel: scripts/libgnsship_<name>.so = the product library with
+# trk_fast.hip compiled under extra flags (the other objects are build/obj's).  Usage:
+#   bash scripts/build_variants.sh name1 "-DX=1" name2 "-DY=2 -DZ=3" ...   [PROF=1: profiling builds]
 set -e
 cd "$(dirname "$0")/.."
 make -s -j8 gnss_sim_receiver_amd/libgnsship.so
-OBJS=$(ls build/obj/*.o | grep -v corr_kernel)
-for spec in "$@"; do
-  tag=${spec%%:*}; flags=${spec#*:}
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -ffp-contract=off -Iinclude -Ignss_sim_receiver_amd/csrc $flags \
-    -c ${CORR_SRC:-gnss_sim_receiver_amd/csrc/corr_kernel.hip} -o build/corr_$tag.o
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o scripts/libgnsship_$tag.so $OBJS build/corr_$tag.o
-  echo "built scripts/libgnsship_$tag.so"
+BASE="--offload-arch=gfx950 -O3 -fPIC -std=c++17 -ffp-contract=off -Iinclude -Ignss_sim_receiver_amd/csrc -Wall -Wno-unused-result -fno-slp-vectorize"
+OBJS=$(ls build/obj/*.o | grep -v "/trk_fast.o$")
+if [ "${PROF:-0}" = 1 ]; then
+  make -s -j8 prof
+  OBJS=$(ls build/prof_obj/*.o | grep -v "/trk_fast.o$")
+  BASE="$BASE -DGNSSHIP_CORR_PROFILE"
+fi
+while [ $# -ge 2 ]; do
+  name=$1; flags=$2; shift 2
+  mkdir -p build/var_$name
+  /opt/rocm/bin/hipcc $BASE $flags -c gnss_sim_receiver_amd/csrc/trk_fast.hip -o build/var_$name/trk_fast.o &
 done
+wait

@@ -11,3 +11,11 @@ timeout -k 10 120 python3 scripts/trk_fast_profile.py 12 > $O/fast_phases.txt 2>
 cat $O/fast_phases.txt
 timeout -k 10 300 python -u bench.py --no-aux --cpu-seconds 0 > $O/bench.json 2> $O/bench.err || { echo "bench failed"; tail -20 $O/bench.err; exit 1; }
 python3 -c "import json;d=json.load(open('$O/bench.json'));print('value',d['value'],'us/epoch',d['us_per_epoch'])"
+for V in ${VARIANTS:-}; do
+  GNSSHIP_LIB_PATH=$R/scripts/libgnsship_$V.so timeout -k 10 300 python -u bench.py --no-aux --cpu-seconds 0 > $O/bench_$V.json 2> $O/bench_$V.err || { echo "bench $V failed"; tail -20 $O/bench_$V.err; exit 1; }
+  python3 -c "import json;d=json.load(open('$O/bench_$V.json'));print('variant $V value',d['value'],'us/epoch',d['us_per_epoch'])"
+done
+for PV in ${PVARIANTS:-}; do
+  GNSSHIP_LIB_PATH=$R/scripts/libgnsship_$PV.so timeout -k 10 120 python3 scripts/trk_fast_profile.py 12 > $O/fast_phases_$PV.txt 2>&1 || { echo "profile $PV failed"; tail $O/fast_phases_$PV.txt; exit 1; }
+  echo "---- profile $PV"; grep -E "epoch period|group . seen|group . ready" $O/fast_phases_$PV.txt
+done

@@ -1,0 +1,8 @@
+#!/bin/bash
+# Links the objects scripts/build_variants.sh compiled: scripts/libgnsship_<name>.so
+set -e
+cd "$(dirname "$0")/.."
+for name in "$@"; do
+  if [ "${PROF:-0}" = 1 ]; then OBJS=$(ls build/prof_obj/*.o | grep -v "/trk_fast.o$"); else OBJS=$(ls build/obj/*.o | grep -v "/trk_fast.o$"); fi
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o scripts/libgnsship_$name.so $OBJS build/var_$name/trk_fast.o -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
+done

@@ -17,8 +17,9 @@ import numpy as np  # noqa: E402
 
 from gnss_sim_receiver_amd import abi, engine, signals  # noqa: E402
 
-EP = 64
-SLOTS = 64
+EP = 16  # epochs 8-23 of the profiled launch (trk_fast.hip kFProfFirst)
+RUN = 64  # epochs in the profiled launch
+SLOTS = 80
 
 
 def main():
@@ -32,7 +33,7 @@ def main():
     for s in sats:
         s.bits = "1000101100110"
     pre = 500
-    block = signals.generate_if(fs, (pre + EP + 4) * vl, sats, seed=1, start=first - 2 * vl)
+    block = signals.generate_if(fs, (pre + RUN + 4) * vl, sats, seed=1, start=first - 2 * vl)
     trk = engine.DllPllVemlTracking(ctx, abi.TrkConf.defaults(abi.SYS_GPS_L1CA, fs, vl, rotator=abi.ROTATOR_AVX), n_ch)
     for i, s in enumerate(sats):
         ctx.set_code(300 + i, s.code)
@@ -45,26 +46,26 @@ def main():
     prof.upload(np.zeros(n_ch * EP * SLOTS, np.uint64))
     lib.gnsship_debug_trk_fast_profile(ctypes.c_void_p(prof.ptr))
     ctx.event_record(0)
-    trk.run(dev, first - 2 * vl, EP, n_buffer_samples=len(block), records=False)
+    trk.run(dev, first - 2 * vl, RUN, n_buffer_samples=len(block), records=False)
     ctx.event_record(1)
     ms = ctx.event_elapsed_ms(0, 1)
     lib.gnsship_debug_trk_fast_profile(ctypes.c_void_p(0))
-    print("states:", sorted(set(trk.channel_state(ch)[0] for ch in range(n_ch))), f"launch {ms:.3f} ms for {EP} epochs")
+    print("states:", sorted(set(trk.channel_state(ch)[0] for ch in range(n_ch))), f"launch {ms:.3f} ms for {RUN} epochs")
     t = np.zeros(n_ch * EP * SLOTS, np.uint64)
     prof.download(t)
     t = t.reshape(n_ch, EP, SLOTS).astype(np.int64)
     us = lambda v: v / 100.0  # noqa: E731
     nxt = np.concatenate([t[:, 1:, 0:1], np.zeros((n_ch, 1, 1), np.int64)], axis=1)
-    t = np.concatenate([t, nxt], axis=2)  # slot 64 = next epoch start
+    t = np.concatenate([t, nxt], axis=2)  # slot 80 = next epoch start
     v = t[:, 1:-1, :]
     print(f"{n_ch} channels: epoch period {us(np.median(np.diff(t[:, :, 0], axis=1))):.2f} us (median)")
     rows = [("derive", 0, 1), ("derive -> replay done", 1, 2), ("derive -> producer 2 done", 1, 3), ("derive -> producer 3 done", 1, 4),
             ("derive -> accumulation done", 1, 5), ("replay done -> accumulation done", 2, 5), ("accumulation -> taps stored", 5, 6),
             ("taps stored -> loop done", 6, 7), ("  taps -> run_dll_pll", 6, 9), ("  run_dll_pll", 9, 10), ("  update_tracking_vars", 10, 11),
-            ("  tracking_vars -> loop done", 11, 7), ("loop done -> next derive", 7, 64), ("  taps -> epoch_pre done", 16, 17),
+            ("  tracking_vars -> loop done", 11, 7), ("loop done -> next derive", 7, 80), ("  taps -> epoch_pre done", 16, 17),
             ("  epoch_pre -> published", 17, 18), ("  published -> run_dll_pll", 18, 9), ("  lock_status (wave 2)", 8, 26),
             ("  tracking_vars -> lock seen", 11, 19), ("  lock seen -> epoch_post done", 19, 24), ("  epoch_finish", 24, 25),
-            ("  epoch_finish -> loop done (records)", 25, 7), ("seed (tracking_vars) -> next derive start", 11, 64), ("  tracking_vars -> seed published", 11, 33), ("  seed published -> next derive start", 33, 64), ("derive: sincos", 0, 35), ("derive: chains", 35, 36), ("derive: dz + publish", 36, 1), ("  run_dll_pll: PLL discriminator", 9, 37), ("  run_dll_pll: carrier filter", 37, 38), ("  run_dll_pll: DLL discriminator", 38, 39), ("  run_dll_pll: code loop filter", 39, 40), ("  run_dll_pll: code freq", 40, 10),
+            ("  epoch_finish -> loop done (records)", 25, 7), ("seed (tracking_vars) -> next derive start", 11, 80), ("  tracking_vars -> seed published", 11, 33), ("  seed published -> next derive start", 33, 80), ("derive: sincos", 0, 35), ("derive: chains", 35, 36), ("derive: dz + publish", 36, 1), ("  run_dll_pll: PLL discriminator", 9, 37), ("  run_dll_pll: carrier filter", 37, 38), ("  run_dll_pll: DLL discriminator", 38, 39), ("  run_dll_pll: code loop filter", 39, 40), ("  run_dll_pll: code freq", 40, 10),
             ("derive -> wave 0 starts accumulating", 1, 27), ("derive -> group 0 seen by wave 0", 1, 28), ("derive -> last group seen by wave 0", 1, 29),
             ("derive -> producer 2 has group 0's slots", 1, 30), ("derive -> producer 3 has its last group's slots", 1, 31),
             ("last group seen -> accumulation done", 29, 5)]
@@ -85,14 +86,14 @@ def main():
         wall = us(v[:, :, wb] - v[:, :, wa])[ok]
         print(f"  {nm:40s} median {np.median(cyc):8.0f} shader cycles, clock {np.median(cyc / wall) / 1e3:.2f} GHz")
     for g in range(8):
-        for nm, sl in (("ready (producer)", 48 + g), ("seen (accumulator)", 56 + g)):
+        for nm, sl in (("ready (producer)", 48 + g), ("seen (accumulator)", 56 + g), ("added (accumulator)", 64 + g)):
             ok = (v[:, :, 1] > 0) & (v[:, :, sl] > 0)
             if ok.any():
                 d = us(v[:, :, sl] - v[:, :, 1])[ok]
                 print(f"  derive -> group {g} {nm:22s} median {np.median(d):7.2f} us  p90 {np.percentile(d, 90):7.2f}  (n={ok.sum()})")
     roles = {0: "control", 1: "replay", 2: "producer"}
     for ch in range(min(n_ch, 4)):
-        ids = [int(t[ch, 2, 41 + w]) for w in range(6)]
+        ids = [int(t[ch, 0, 72 + w]) for w in range(6)]
         print(f"  channel {ch} waves: " + ", ".join(f"w{w} {roles.get(h >> 32, h >> 32)} simd {(h >> 4) & 3}" for w, h in enumerate(ids)))
     for ch in range(min(n_ch, 4)):
         ids = [int(t[ch, 0, 20 + w]) for w in range(4)]
