@@ -51,8 +51,13 @@ __shared__ int g_fprof_epoch;
 // stamps go to LDS and out to g_trkf_prof when the kernel ends: a global store per stamp would put
 // its write acknowledgement (≈ 0.8 µs) into the next vmcnt wait of the stamping wave
 __shared__ unsigned long long g_fprof_lds[kFProfEpochs * kFProfSlots];
+#ifndef GNSSHIP_PROF_MASK  // the stamps compiled in (bit k: slot k; bit 63: slots 63 and up)
+#define GNSSHIP_PROF_MASK 0xffffffffffffffffull
+#endif
+__device__ __forceinline__ constexpr bool prof_on(int k) { return ((GNSSHIP_PROF_MASK) >> (k < 63 ? k : 63)) & 1ull; }
 __device__ __forceinline__ void trkf_prof_stamp(int e, int k)
 {
+    if (!prof_on(k)) return;
     const int r = e - kFProfFirst;
     if (g_trkf_prof && r >= 0 && r < kFProfEpochs && (threadIdx.x & 63) == 0) g_fprof_lds[r * kFProfSlots + k] = wall_clock64();
 }
@@ -61,6 +66,7 @@ __device__ __forceinline__ void trkf_prof_stamp(int e, int k)
 namespace gnsship {
 __device__ __forceinline__ void trkf_prof_clock(int e, int k)
 {
+    if (!prof_on(k)) return;
     const int r = e - kFProfFirst;
     if (g_trkf_prof && r >= 0 && r < kFProfEpochs && (threadIdx.x & 63) == 0) g_fprof_lds[r * kFProfSlots + k] = clock64();
 }
@@ -99,14 +105,31 @@ namespace {
 #endif
 constexpr int kFWaves = GNSSHIP_FAST_WAVES;
 constexpr int kFThreads = kFWaves * kWave;
-constexpr int kFProducers = kFWaves - 2;  // every wave but the control and phasor waves forms products
+constexpr int kFProducers = kFWaves - 3;  // every wave but the phasor, accumulator and control waves forms products
 // Wave roles (fast_roles): the control wave and the phasor wave each get a SIMD of their own — the
 // phasor chain is the epoch's critical path and the control wave's loop update is the next — and the
 // producers share the other SIMDs (two producer waves on a SIMD interleave their issue).
-constexpr int kRoleControl = 0, kRoleReplay = 1, kRoleProducer = 2;
+constexpr int kRoleControl = 0, kRoleReplay = 1, kRoleProducer = 2, kRoleAccum = 3;
 // Polling waves back off this many s_sleep units (≈ 64 cycles each) between LDS polls.
+// Critical-path probes (A/B builds only): n × s_sleep 4 (≈ 256 cycles each; s_sleep takes 3 bits)
+#define GNSSHIP_PROBE(NAME)                                                  \
+    do {                                                                     \
+        _Pragma("unroll") for (int pr_ = 0; pr_ < (NAME); pr_++) __builtin_amdgcn_s_sleep(4); \
+    } while (0)
+#ifndef GNSSHIP_DELAY_ACC
+#define GNSSHIP_DELAY_ACC 0
+#endif
+#ifndef GNSSHIP_DELAY_PROD
+#define GNSSHIP_DELAY_PROD 0
+#endif
+#ifndef GNSSHIP_DELAY_REPLAY
+#define GNSSHIP_DELAY_REPLAY 0
+#endif
+#ifndef GNSSHIP_DELAY_LOOP
+#define GNSSHIP_DELAY_LOOP 0
+#endif
 #ifndef GNSSHIP_ACC_BATCH  // iterations per accumulator load batch
-#define GNSSHIP_ACC_BATCH 8
+#define GNSSHIP_ACC_BATCH 16
 #endif
 #ifndef GNSSHIP_POLL_SLEEP
 #define GNSSHIP_POLL_SLEEP 0
@@ -132,9 +155,18 @@ struct SpecArgs {
     int32_t n_pred;
 };
 
+#ifdef GNSSHIP_EXP_SERIAL  // experiment: the producers' phase B waits for the whole replay
+__shared__ int32_t g_replay_done;
+#endif
+
+struct SpecPred {
+    float rem, step, dz_re, dz_im;
+};
+
 struct FShared {
     FJob job;
-    float taps[2 * kMaxTaps + 2];  // the epoch's tap sums (+ the data prompt at 2·kMaxTaps), as epoch_pre reads them
+    float taps[2][2 * kMaxTaps + 2];  // epoch e's tap sums in [e & 1] (+ the data prompt at 2·kMaxTaps), as epoch_pre reads them
+    int32_t taps_seq;                  // e + 1 once the accumulator wave stored epoch e's taps
     gnsship_trk_dump_record drec;  // log_data's record of the epoch
     double coh;       // the coherent time lock_status is called with (0: no lock test this epoch)
     int32_t seed_seq; // e + 1 once wave 0 published epoch e's NCO arguments (sh.job without dz)
@@ -146,6 +178,9 @@ struct FShared {
     int32_t acc_groups; // product groups the accumulator has consumed (counted over the run)
     int32_t step_seq;   // e + 1 once wave 0 published epoch e's early loop values (state 4, SpecArgs)
     SpecArgs spec;      // those values
+    SpecPred pred;      // wave 1's phasor prediction for epoch e (published as pred_seq = e + 1)
+    int32_t pred_seq;
+    int32_t verdict;    // 4·(e + 1) + 1: wave 0 confirmed epoch e's prediction and published the job; + 2: refuted; + 3: not seen
     f2 tailp[kAvxLanes][kMaxTaps + 1];  // the tail's products (sample 16M + j, tap), wave 1 → wave 0
 };
 
@@ -220,9 +255,14 @@ __device__ __forceinline__ void lds_wait_ge(const int32_t* p, int v)
 // cycles per iteration on one wave, scripts/replay_bench.hip).  A DPP read needs two wait states
 // after the VALU write of its source: the step's plain multiply and one s_nop.  Each lane stores its
 // 32-bit half of the slot (the consumer polls until both halves are written).
+#ifdef GNSSHIP_PSTEP_VNOP  // experiment: the DPP wait state as a VALU nop
+#define GNSSHIP_PSTEP_NOP "v_nop\n\t"
+#else
+#define GNSSHIP_PSTEP_NOP "s_nop 0\n\t"
+#endif
 #define GNSSHIP_PSTEP(X, Y)                                                                   \
     "v_mul_f32 %[t], %[c], " X "\n\t"                                                      \
-    "s_nop 0\n\t"                                                                           \
+    GNSSHIP_PSTEP_NOP                                                                        \
     "v_mul_f32_dpp %[u], " X ", %[k2] quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t" \
     "v_add_f32 " Y ", %[t], %[u]\n\t"
 
@@ -301,6 +341,7 @@ __device__ __forceinline__ float fast_replay(float x, float c, float k2, int M, 
     static_assert(G % 4 == 0 && G >= 4 && G <= 64, "task length");
     constexpr int kTB = 64 / G;  // tasks per 64-iteration block
     if (S <= 0) return x;
+    c = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, c)));  // dz.re in an SGPR (uniform)
     // the flat address of an LDS location carries its LDS offset in the low 32 bits
     const uint32_t base = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(Zs)) + 4u * static_cast<uint32_t>(lane);
     uint32_t off = base;
@@ -356,46 +397,6 @@ __device__ __forceinline__ float fast_replay(float x, float c, float k2, int M, 
     // the last task: its producers continue it
     __hip_atomic_store(half0 + 2 * kAvxLanes * ts, __builtin_bit_cast(uint32_t, x), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     if (tail > 0) {  // z_l(M) for the tail (chain 0's is what the reference keeps)
-        for (int m = G * (S - 1); m < M; m++) {
-            x = pstep<1, false>(x, c, k2, 0);
-            if ((m & 63) == 0) x = pnormalise(x);
-        }
-    }
-    return x;
-}
-
-// fast_replay (whole-epoch slots) started before the epoch's seed, on the predicted phasors: at every
-// task the seed's arrival is polled (the load issued at the task's start, read at its end) and
-// `check` is run once it is there — it returns 1 (the prediction holds: the job is published and the
-// producers consume the slots as they come) or 2 (it does not: the replay stops here).  `status`
-// (0 / 1 / 2) is wave-uniform.
-template <int G, class Check>
-__device__ __forceinline__ float fast_replay_spec(float x, float c, float k2, int M, int S, int tail, uint64_t* __restrict__ Zs, int lane,
-    const int32_t* seed_seq, int need, int& status, Check&& check)
-{
-    static_assert(G % 4 == 0 && G >= 4 && G <= 64, "task length");
-    constexpr int kTB = 64 / G;
-    if (S <= 0) return x;
-    const uint32_t base = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(Zs)) + 4u * static_cast<uint32_t>(lane);
-    uint32_t off = base;
-    constexpr uint32_t kSlotRow = kAvxLanes * sizeof(uint64_t);
-    uint32_t* const half0 = reinterpret_cast<uint32_t*>(Zs) + lane;
-#pragma unroll 1
-    for (int t = 0; t < S - 1; t++) {
-        int v = 0;
-        if (status == 0) v = __hip_atomic_load(seed_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        if (t % kTB == 0)
-            x = ppow<G - 1>(pnormalise(pstep<1, true>(x, c, k2, off)), c, k2);
-        else
-            x = ppow<G - 4>(pstep<4, true>(x, c, k2, off), c, k2);
-        off += kSlotRow;
-        if (status == 0 && __builtin_amdgcn_readfirstlane(v) >= need) {
-            status = __builtin_amdgcn_readfirstlane(check());
-            if (status == 2) return x;
-        }
-    }
-    __hip_atomic_store(half0 + 2 * kAvxLanes * (S - 1), __builtin_bit_cast(uint32_t, x), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    if (tail > 0) {
         for (int m = G * (S - 1); m < M; m++) {
             x = pstep<1, false>(x, c, k2, 0);
             if ((m & 63) == 0) x = pnormalise(x);
@@ -518,6 +519,10 @@ __device__ __forceinline__ void fast_produce(const FJob& job, i4v span, const fl
             group_codes<NT, DATA, IN_MARGIN, G, true>(code0, code1, L, n0, G, step, rem, shifts, cv);
         else
             group_codes<NT, DATA, IN_MARGIN, G, false>(code0, code1, L, n0, cnt, step, rem, shifts, cv);
+        // the ring group is free once the accumulator consumed its previous occupant — and in the slot
+        // ring (rg ≤ 16 groups of its 64 tasks) that also means the slot this lane polls next was
+        // consumed on its previous lap (whichever producer took it)
+        if (g >= rg) lds_wait_ge(acc_groups, gbase + g - rg + 1);
         const int ts = active ? t % rs : 0;
         uint64_t* slot = Zs + ts * kAvxLanes + l;
         uint64_t v = kSlotEmpty;
@@ -528,8 +533,9 @@ __device__ __forceinline__ void fast_produce(const FJob& job, i4v span, const fl
         }
         if (g == pw && pw == 0) GNSSHIP_FSTAMP(pe, 30);
         if (g + kFProducers >= n_groups && pw == 1) GNSSHIP_FSTAMP(pe, 31);
-        // the ring group is free once the accumulator consumed its previous occupant
-        if (g >= rg) lds_wait_ge(acc_groups, gbase + g - rg + 1);
+#ifdef GNSSHIP_EXP_SERIAL
+        while (__hip_atomic_load(&g_replay_done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < pe + 1) __builtin_amdgcn_s_sleep(1);
+#endif
         const f2 z = active ? __builtin_bit_cast(f2, v) : f2{0.0f, 0.0f};
         const bool renorm = ((G * t) & 63) == 0;
         float* pdst = Pp + static_cast<size_t>(rslot) * PL::kGroup + tl * PL::kTask + l;
@@ -537,6 +543,7 @@ __device__ __forceinline__ void fast_produce(const FJob& job, i4v span, const fl
             group_phasors<FMT, NTT, G, true>(span, z, dz, renorm, n0, G, pdst, cv, xa, xb);
         else
             group_phasors<FMT, NTT, G, false>(span, z, dz, renorm, n0, cnt, pdst, cv, xa, xb);
+        GNSSHIP_PROBE(GNSSHIP_DELAY_PROD);
         if (lane == 0) lds_release_store(ready + rslot, gbase + g + 1);
         if (g < 8) GNSSHIP_FSTAMP(pe, 48 + g);
         rslot += rstep;
@@ -566,38 +573,52 @@ __device__ __forceinline__ void fast_accumulate(const float* __restrict__ Pp, in
         acc[k] = 0.0f;
         off[k] = min(r + 4 * k, 2 * NTT - 1) * kAvxLanes + l;
     }
+    // One stream of batches of kU iterations over the groups, the next batch's loads (and, at a group's
+    // last batch, the next group's ready flag with its first batch) issued before the current batch's
+    // adds: a wave's LDS operations complete in order, so loads issued after a flag read that shows
+    // the group ready see its products; when the flag did not show it, the batch is read again after
+    // the wait.  Every group is added whole: a partial group's iterations past the epoch's end hold −0.
+    constexpr int kJ = 4 * G;
+    constexpr int kU = GNSSHIP_ACC_BATCH < kJ ? GNSSHIP_ACC_BATCH : kJ;
+    static_assert(kJ % kU == 0, "accumulator batch");
+    constexpr int kNB = kJ / kU;
+    auto load_batch = [&](int slot, int b, float (&dst)[kU][NS]) {
+        const float* src = Pp + static_cast<size_t>(slot) * PL::kGroup;
+#pragma unroll
+        for (int u = 0; u < kU; u++) {
+            const int j = b * kU + u;
+#pragma unroll
+            for (int k = 0; k < NS; k++) dst[u][k] = src[off[k] + (j / G) * PL::kTask + (j % G) * PL::kIter];
+        }
+    };
     int rslot = 0;
+    int flag = __hip_atomic_load(ready + rslot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    float cur[kU][NS];
+    load_batch(rslot, 0, cur);
     for (int g = 0; g < n_groups; g++) {
-        lds_wait_eq(ready + rslot, gbase + g + 1);
+        if (__builtin_amdgcn_readfirstlane(flag) != gbase + g + 1) {
+            lds_wait_eq(ready + rslot, gbase + g + 1);
+            load_batch(rslot, 0, cur);
+        }
+        GNSSHIP_PROBE(GNSSHIP_DELAY_ACC);
         if (g == 0) GNSSHIP_FSTAMP(pe, 28);
         if (g == n_groups - 1) GNSSHIP_FSTAMP(pe, 29);
         if (g < 8) GNSSHIP_FSTAMP(pe, 56 + g);
-        // every group is added whole: a partial group's iterations past the epoch's end hold −0.
-        // Batches of kU iterations, the next batch's loads issued before the current one's adds.
-        const float* src = Pp + static_cast<size_t>(rslot) * PL::kGroup;
-        constexpr int kJ = 4 * G;
-        constexpr int kU = GNSSHIP_ACC_BATCH < kJ ? GNSSHIP_ACC_BATCH : kJ;
-        static_assert(kJ % kU == 0, "accumulator batch");
-        auto at = [&](int j, int k) { return src[off[k] + (j / G) * PL::kTask + (j % G) * PL::kIter]; };
-        float cur[kU][NS];
+        const int nslot = rslot + 1 == rg ? 0 : rslot + 1;
 #pragma unroll
-        for (int u = 0; u < kU; u++)
-#pragma unroll
-            for (int k = 0; k < NS; k++) cur[u][k] = at(u, k);
-#pragma unroll
-        for (int j0 = 0; j0 < kJ; j0 += kU) {
+        for (int b = 0; b < kNB; b++) {
             float nxt[kU][NS];
-            if (j0 + kU < kJ) {
-#pragma unroll
-                for (int u = 0; u < kU; u++)
-#pragma unroll
-                    for (int k = 0; k < NS; k++) nxt[u][k] = at(j0 + kU + u, k);
+            if (b + 1 < kNB) {
+                load_batch(rslot, b + 1, nxt);
+            } else if (g + 1 < n_groups) {
+                flag = __hip_atomic_load(ready + nslot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                load_batch(nslot, 0, nxt);
             }
 #pragma unroll
             for (int u = 0; u < kU; u++)
 #pragma unroll
                 for (int k = 0; k < NS; k++) acc[k] = __fadd_rn(acc[k], cur[u][k]);
-            if (j0 + kU < kJ) {
+            if (b + 1 < kNB || g + 1 < n_groups) {
 #pragma unroll
                 for (int u = 0; u < kU; u++)
 #pragma unroll
@@ -607,7 +628,7 @@ __device__ __forceinline__ void fast_accumulate(const float* __restrict__ Pp, in
         asm volatile("" ::: "memory");  // the group's loads are issued (and used) before it is released
         if (lane == 0) lds_release_store(acc_groups, gbase + g + 1);
         if (g < 8) GNSSHIP_FSTAMP(pe, 64 + g);
-        rslot = rslot + 1 == rg ? 0 : rslot + 1;
+        rslot = nslot;
     }
 }
 
@@ -683,6 +704,26 @@ __device__ __forceinline__ void derive_step(float step, f2& inc, f2& dz)
     dz = normalise_avx(d);
 }
 
+// derive_step and derive_chains at once: both phasors, then the 15-step z chain with dz's four
+// squarings interleaved (independent chains, one instruction stream)
+__device__ __forceinline__ void derive_all(float step, float rem, int lane, f2& inc, f2& dz, f2& zinit)
+{
+    float ss, cs, sr, cr;
+    glibc_sincosf(-step, &ss, &cs);
+    glibc_sincosf(rem, &sr, &cr);
+    inc = f2{cs, ss};
+    const f2 p0 = f2{cr, -sr};
+    f2 w = p0, z = p0, d = inc;
+#pragma unroll
+    for (int i = 0; i < kAvxLanes - 1; i++) {
+        w = cmul_exact_sc(w, inc);
+        if (i < 4) d = cmul_exact_sc(d, d);
+        z = i + 1 == (lane >> 1) ? w : z;
+    }
+    dz = normalise_avx(d);
+    zinit = z;
+}
+
 // a wave-uniform 64-bit value as scalar registers
 __device__ __forceinline__ uint64_t uni64(uint64_t v)
 {
@@ -746,25 +787,29 @@ __global__ __launch_bounds__(kFThreads, fast_waves_per_simd<THRU>()) void trk_fa
     // roles (in that order), the others produce; without two such SIMDs, waves 1 and 0 do
     int role = kRoleProducer, pw = 0;
     {
+        // the phasor and accumulator waves (the epoch's chain) alone on a SIMD each; the control wave
+        // shares one with a producer (its loop work overlaps the production of the next epoch)
         int cnt[4] = {0, 0, 0, 0};
         for (int w = 0; w < kFWaves; w++) cnt[simd_of[w] & 3]++;
-        int rep = -1, ctl = -1;
+        int rep = -1, acw = -1, ctl = -1;
         for (int w = 0; w < kFWaves; w++)
             if (cnt[simd_of[w] & 3] == 1) {
                 if (rep < 0) rep = w;
-                else if (ctl < 0) ctl = w;
+                else if (acw < 0) acw = w;
             }
-        if (rep < 0 || ctl < 0) {
+        if (rep < 0 || acw < 0) {
             rep = 1;
-            ctl = 0;
+            acw = 2;
         }
+        for (int w = 0; w < kFWaves && ctl < 0; w++)
+            if (w != rep && w != acw) ctl = w;
         int np = 0;
         for (int w = 0; w < kFWaves; w++) {
             if (w == wave) {
-                role = w == rep ? kRoleReplay : w == ctl ? kRoleControl : kRoleProducer;
+                role = w == rep ? kRoleReplay : w == acw ? kRoleAccum : w == ctl ? kRoleControl : kRoleProducer;
                 pw = np;
             }
-            if (w != rep && w != ctl) np++;
+            if (w != rep && w != acw && w != ctl) np++;
         }
         role = __builtin_amdgcn_readfirstlane(role);
         pw = __builtin_amdgcn_readfirstlane(pw);
@@ -781,8 +826,14 @@ __global__ __launch_bounds__(kFThreads, fast_waves_per_simd<THRU>()) void trk_fa
         sh.pre_seq = 0;
         sh.lock_seq = 0;
         sh.tail_seq = 0;
+        sh.taps_seq = 0;
         sh.acc_groups = 0;
         sh.step_seq = 0;
+        sh.pred_seq = 0;
+        sh.verdict = 0;
+#ifdef GNSSHIP_EXP_SERIAL
+        g_replay_done = 0;
+#endif
     }
     __syncthreads();
     if (skip) return;  // idle channel: its state is untouched
@@ -878,7 +929,21 @@ __global__ __launch_bounds__(kFThreads, fast_waves_per_simd<THRU>()) void trk_fa
                 j.S = S;
                 j.tail = tail;
             }
+            // wave 1's speculative replay of this epoch (whole-epoch slots): confirmed here when its
+            // remainder phase and step are the seed's floats, and the job goes out with the seed
+            int code = 3;
+            if (!SRING && __hip_atomic_load(&sh.pred_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= e + 1) {
+                code = 2;
+                if (runnable && __builtin_bit_cast(uint32_t, sh.pred.rem) == __builtin_bit_cast(uint32_t, rem_carr) &&
+                    __builtin_bit_cast(uint32_t, sh.pred.step) == __builtin_bit_cast(uint32_t, stepf)) {
+                    j.dz_re = sh.pred.dz_re;
+                    j.dz_im = sh.pred.dz_im;
+                    code = 1;
+                }
+            }
+            sh.verdict = 4 * (e + 1) + code;
             publish_seq(&sh.seed_seq, e + 1);
+            if (code == 1) publish_seq(&sh.job_seq, e + 1);
         }
     };
     if (role == kRoleControl) make_seed(0);
@@ -888,6 +953,9 @@ __global__ __launch_bounds__(kFThreads, fast_waves_per_simd<THRU>()) void trk_fa
     // places for one role's memory operations are not charged to another (a merged loop made the
     // control wave wait for the producers' sample loads it never issued).
     if (role == kRoleReplay) {
+#ifdef GNSSHIP_PRIO_REPLAY
+        __builtin_amdgcn_s_setprio(GNSSHIP_PRIO_REPLAY);
+#endif
         for (int e = 0;; e++) {
             FJob job;
                 // ---- derive: the phasors of the seeded epoch ----
@@ -920,10 +988,8 @@ __global__ __launch_bounds__(kFThreads, fast_waves_per_simd<THRU>()) void trk_fa
                 float step_pre = 0.0f;
                 bool published = false;
                 float xl = 0.0f;
-                if (spec) {
-                    step_pre = static_cast<float>(sp.step_d + if_step);  // make_seed's j.step
-                    derive_step(step_pre, inc, dz);
-                }
+                if (spec) step_pre = static_cast<float>(sp.step_d + if_step);  // make_seed's j.step
+                if (SRING && spec) derive_step(step_pre, inc, dz);
                 if (!SRING && spec) {
                     // make_seed's j.rem_carr after update_tracking_vars and epoch_consume, for n = n_pred
                     float rem_pred = carr_rem_next(sp.rem_prev, carr_advance(sp.step_d, sp.rate, static_cast<double>(sp.n_pred)));
@@ -932,11 +998,27 @@ __global__ __launch_bounds__(kFThreads, fast_waves_per_simd<THRU>()) void trk_fa
                         const double ifc = static_cast<double>(ifn) / static_cast<double>(kp.fs_int);
                         rem_pred = static_cast<float>(fmod_2pi(static_cast<double>(rem_pred) + kTwoPi * ifc));
                     }
-                    zinit = derive_chains(rem_pred, inc, lane);
+                    derive_all(step_pre, rem_pred, lane, inc, dz, zinit);
                     GNSSHIP_FSTAMP(e, 35);
-                    auto check = [&]() -> int {
-                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                    GNSSHIP_PROBE(GNSSHIP_DELAY_REPLAY);
+                    // the prediction goes to wave 0, which confirms it when it makes the seed (and then
+                    // publishes the job itself); the replay runs without looking at the seed
+                    if (lane == 0) {
+                        sh.pred.rem = rem_pred;
+                        sh.pred.step = step_pre;
+                        sh.pred.dz_re = dz.x;
+                        sh.pred.dz_im = dz.y;
+                        publish_seq(&sh.pred_seq, e + 1);
+                    }
+                    xl = (lane & 1) ? zinit.y : zinit.x;
+                    if (lane < 2 * kAvxLanes) xl = fast_replay<G, false>(xl, dz.x, (lane & 1) ? dz.y : -dz.y, M, S, tail, Zs, rs, lane);
+                    GNSSHIP_FSTAMP(e, 34);
+                    wait_seq(&sh.seed_seq, e + 1);
+                    const int v = __builtin_amdgcn_readfirstlane(sh.verdict);
+                    int status = (v >> 2) == e + 1 ? (v & 3) : 3;
+                    if (status == 3) {  // the seed was made before the prediction was published: compare here
                         const FJob sd = uniform_job(sh.job);
+                        status = 2;
                         if (sd.runnable && __builtin_bit_cast(uint32_t, sd.step) == __builtin_bit_cast(uint32_t, step_pre) &&
                             __builtin_bit_cast(uint32_t, sd.rem_carr) == __builtin_bit_cast(uint32_t, rem_pred)) {
                             if (lane == 0) {
@@ -944,17 +1026,8 @@ __global__ __launch_bounds__(kFThreads, fast_waves_per_simd<THRU>()) void trk_fa
                                 sh.job.dz_im = dz.y;
                                 publish_seq(&sh.job_seq, e + 1);
                             }
-                            return 1;
+                            status = 1;
                         }
-                        return 2;
-                    };
-                    int status = 0;
-                    xl = (lane & 1) ? zinit.y : zinit.x;
-                    if (lane < 2 * kAvxLanes) xl = fast_replay_spec<G>(xl, dz.x, (lane & 1) ? dz.y : -dz.y, M, S, tail, Zs, lane, &sh.seed_seq, e + 1, status, check);
-                    status = __builtin_amdgcn_readfirstlane(status);
-                    if (status == 0) {
-                        wait_seq(&sh.seed_seq, e + 1);
-                        status = check();
                     }
                     if (status == 1) {
                         published = true;
@@ -979,12 +1052,18 @@ __global__ __launch_bounds__(kFThreads, fast_waves_per_simd<THRU>()) void trk_fa
                     if (lane == 0) publish_seq(&sh.job_seq, e + 1);
                     if (!sd.runnable) break;
                 }
+#ifdef GNSSHIP_EXP_SERIAL
+                if (published && lane == 0) __hip_atomic_store(&g_replay_done, e + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#endif
                 GNSSHIP_FSTAMP(e, 1);
                 GNSSHIP_FCLK(e, 12);
                 job = uniform_job(sh.job);
                 if (!published) {
                     xl = (lane & 1) ? zinit.y : zinit.x;
                     if (lane < 2 * kAvxLanes) xl = fast_replay<G, SRING>(xl, job.dz_re, (lane & 1) ? job.dz_im : -job.dz_im, M, S, tail, Zs, rs, lane);
+#ifdef GNSSHIP_EXP_SERIAL
+                    if (lane == 0) __hip_atomic_store(&g_replay_done, e + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#endif
                 }
                 if (tail > 0) {  // the serial tail from normalise(z_0) after the loop (:294-308)
                     const i4v span = sample_span<FMT>(samples, job.off, N);
@@ -1030,13 +1109,13 @@ __global__ __launch_bounds__(kFThreads, fast_waves_per_simd<THRU>()) void trk_fa
                     }
                 }
         }
-    } else {
+    } else if (role == kRoleAccum) {
         for (int e = 0;; e++) {
             const int gbase = e * n_groups;  // the epoch's first product-group tag - 1
             wait_seq(&sh.job_seq, e + 1);
             const FJob job = uniform_job(sh.job);
             if (!job.runnable) break;
-            // ---- wave 0: the epoch's taps in u_avx's order ----
+            // ---- the epoch's taps in u_avx's order ----
             {
                 constexpr int NS = acc_slots<NTT>();
                 float acc[NS];
@@ -1064,13 +1143,24 @@ __global__ __launch_bounds__(kFThreads, fast_waves_per_simd<THRU>()) void trk_fa
                         if (sl < 2 * NTT) {
                             const int tap = sl >> 1;
                             const int o = (DATA && tap == NT) ? 2 * kMaxTaps : 2 * tap;
-                            sh.taps[o + (sl & 1)] = acc[kk];
+                            sh.taps[e & 1][o + (sl & 1)] = acc[kk];
                         }
                     }
                 }
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                if (lane == 0) lds_release_store(&sh.taps_seq, e + 1);
             }
             GNSSHIP_FSTAMP(e, 6);
+        }
+    } else {
+#ifdef GNSSHIP_PRIO_CONTROL
+        __builtin_amdgcn_s_setprio(GNSSHIP_PRIO_CONTROL);
+#endif
+        for (int e = 0;; e++) {
+            const int gbase = e * n_groups;  // the epoch's first product-group tag - 1
+            wait_seq(&sh.job_seq, e + 1);
+            const FJob job = uniform_job(sh.job);
+            if (!job.runnable) break;
+            wait_seq(&sh.taps_seq, e + 1);  // the accumulator wave's taps of this epoch
             GNSSHIP_FCLK(e, 14);
             if (cancel) {
                 // the epoch seeded speculatively before the last lock test failed: the channel stopped
@@ -1085,8 +1175,9 @@ __global__ __launch_bounds__(kFThreads, fast_waves_per_simd<THRU>()) void trk_fa
                 continue;
             }
             {
-                const float* taps = sh.taps;
+                const float* taps = sh.taps[e & 1];
                 GNSSHIP_FSTAMP(e, 16);
+                GNSSHIP_PROBE(GNSSHIP_DELAY_LOOP);
                 const float* pdata = DATA ? taps + 2 * kMaxTaps : taps;
                 gnsship_trk_epoch r{};
                 r.flags = 8;
@@ -1094,7 +1185,7 @@ __global__ __launch_bounds__(kFThreads, fast_waves_per_simd<THRU>()) void trk_fa
                 const uint64_t es = rc.epoch_start;  // this epoch's first sample
                 const double coh = epoch_pre(kp, rc, taps, pdata, r, nullptr, dr);
                 GNSSHIP_FSTAMP(e, 17);
-                // hand the prompt to the lock detectors (wave 2; coh 0: no lock test this epoch)
+                // hand the prompt to the lock detectors (producer 0; coh 0: no lock test this epoch)
                 if (lane == 0) {
                     sc.p[0] = rc.p[0];
                     sc.p[1] = rc.p[1];
@@ -1122,6 +1213,7 @@ __global__ __launch_bounds__(kFThreads, fast_waves_per_simd<THRU>()) void trk_fa
                             sh.spec.n_pred = rc.current_prn_length_samples;
                             publish_seq(&sh.step_seq, e + 2);
                         }
+                        GNSSHIP_FSTAMP(e, 32);
                     };
                     epoch_loop(kp, rc, nullptr, early_step);
                     // State 4: epoch_post cannot change what the next epoch's correlation needs (the

@@ -55,8 +55,8 @@ def main():
     prof.download(t)
     t = t.reshape(n_ch, EP, SLOTS).astype(np.int64)
     us = lambda v: v / 100.0  # noqa: E731
-    nxt = np.concatenate([t[:, 1:, 0:1], np.zeros((n_ch, 1, 1), np.int64)], axis=1)
-    t = np.concatenate([t, nxt], axis=2)  # slot 80 = next epoch start
+    nxt = np.concatenate([t[:, 1:, :], np.zeros((n_ch, 1, SLOTS), np.int64)], axis=1)
+    t = np.concatenate([t, nxt], axis=2)  # slots 80 + k = the next epoch's slot k
     v = t[:, 1:-1, :]
     print(f"{n_ch} channels: epoch period {us(np.median(np.diff(t[:, :, 0], axis=1))):.2f} us (median)")
     rows = [("derive", 0, 1), ("derive -> replay done", 1, 2), ("derive -> producer 2 done", 1, 3), ("derive -> producer 3 done", 1, 4),
@@ -68,7 +68,9 @@ def main():
             ("  epoch_finish -> loop done (records)", 25, 7), ("seed (tracking_vars) -> next derive start", 11, 80), ("  tracking_vars -> seed published", 11, 33), ("  seed published -> next derive start", 33, 80), ("derive: sincos", 0, 35), ("derive: chains", 35, 36), ("derive: dz + publish", 36, 1), ("  run_dll_pll: PLL discriminator", 9, 37), ("  run_dll_pll: carrier filter", 37, 38), ("  run_dll_pll: DLL discriminator", 38, 39), ("  run_dll_pll: code loop filter", 39, 40), ("  run_dll_pll: code freq", 40, 10),
             ("derive -> wave 0 starts accumulating", 1, 27), ("derive -> group 0 seen by wave 0", 1, 28), ("derive -> last group seen by wave 0", 1, 29),
             ("derive -> producer 2 has group 0's slots", 1, 30), ("derive -> producer 3 has its last group's slots", 1, 31),
-            ("last group seen -> accumulation done", 29, 5)]
+            ("last group seen -> accumulation done", 29, 5),
+            ("cycle: spec seen -> replay end", 0, 34), ("cycle: replay end -> taps stored", 34, 6),
+            ("cycle: taps stored -> spec published", 6, 32), ("cycle: spec published -> spec seen (next)", 32, 80 + 0)]
     for nm, a, b in rows:
         ok = (v[:, :, a] > 0) & (v[:, :, b] > 0)
         if not ok.any():
