@@ -129,7 +129,7 @@ constexpr int kRoleControl = 0, kRoleReplay = 1, kRoleProducer = 2, kRoleAccum =
 #define GNSSHIP_DELAY_LOOP 0
 #endif
 #ifndef GNSSHIP_ACC_BATCH  // iterations per accumulator load batch
-#define GNSSHIP_ACC_BATCH 16
+#define GNSSHIP_ACC_BATCH 8
 #endif
 #ifndef GNSSHIP_POLL_SLEEP
 #define GNSSHIP_POLL_SLEEP 0
@@ -573,52 +573,38 @@ __device__ __forceinline__ void fast_accumulate(const float* __restrict__ Pp, in
         acc[k] = 0.0f;
         off[k] = min(r + 4 * k, 2 * NTT - 1) * kAvxLanes + l;
     }
-    // One stream of batches of kU iterations over the groups, the next batch's loads (and, at a group's
-    // last batch, the next group's ready flag with its first batch) issued before the current batch's
-    // adds: a wave's LDS operations complete in order, so loads issued after a flag read that shows
-    // the group ready see its products; when the flag did not show it, the batch is read again after
-    // the wait.  Every group is added whole: a partial group's iterations past the epoch's end hold −0.
-    constexpr int kJ = 4 * G;
-    constexpr int kU = GNSSHIP_ACC_BATCH < kJ ? GNSSHIP_ACC_BATCH : kJ;
-    static_assert(kJ % kU == 0, "accumulator batch");
-    constexpr int kNB = kJ / kU;
-    auto load_batch = [&](int slot, int b, float (&dst)[kU][NS]) {
-        const float* src = Pp + static_cast<size_t>(slot) * PL::kGroup;
-#pragma unroll
-        for (int u = 0; u < kU; u++) {
-            const int j = b * kU + u;
-#pragma unroll
-            for (int k = 0; k < NS; k++) dst[u][k] = src[off[k] + (j / G) * PL::kTask + (j % G) * PL::kIter];
-        }
-    };
     int rslot = 0;
-    int flag = __hip_atomic_load(ready + rslot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    float cur[kU][NS];
-    load_batch(rslot, 0, cur);
     for (int g = 0; g < n_groups; g++) {
-        if (__builtin_amdgcn_readfirstlane(flag) != gbase + g + 1) {
-            lds_wait_eq(ready + rslot, gbase + g + 1);
-            load_batch(rslot, 0, cur);
-        }
-        GNSSHIP_PROBE(GNSSHIP_DELAY_ACC);
+        lds_wait_eq(ready + rslot, gbase + g + 1);
         if (g == 0) GNSSHIP_FSTAMP(pe, 28);
         if (g == n_groups - 1) GNSSHIP_FSTAMP(pe, 29);
         if (g < 8) GNSSHIP_FSTAMP(pe, 56 + g);
-        const int nslot = rslot + 1 == rg ? 0 : rslot + 1;
+        // every group is added whole: a partial group's iterations past the epoch's end hold −0.
+        // Batches of kU iterations, the next batch's loads issued before the current one's adds.
+        const float* src = Pp + static_cast<size_t>(rslot) * PL::kGroup;
+        constexpr int kJ = 4 * G;
+        constexpr int kU = GNSSHIP_ACC_BATCH < kJ ? GNSSHIP_ACC_BATCH : kJ;
+        static_assert(kJ % kU == 0, "accumulator batch");
+        auto at = [&](int j, int k) { return src[off[k] + (j / G) * PL::kTask + (j % G) * PL::kIter]; };
+        float cur[kU][NS];
 #pragma unroll
-        for (int b = 0; b < kNB; b++) {
+        for (int u = 0; u < kU; u++)
+#pragma unroll
+            for (int k = 0; k < NS; k++) cur[u][k] = at(u, k);
+#pragma unroll
+        for (int j0 = 0; j0 < kJ; j0 += kU) {
             float nxt[kU][NS];
-            if (b + 1 < kNB) {
-                load_batch(rslot, b + 1, nxt);
-            } else if (g + 1 < n_groups) {
-                flag = __hip_atomic_load(ready + nslot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                load_batch(nslot, 0, nxt);
+            if (j0 + kU < kJ) {
+#pragma unroll
+                for (int u = 0; u < kU; u++)
+#pragma unroll
+                    for (int k = 0; k < NS; k++) nxt[u][k] = at(j0 + kU + u, k);
             }
 #pragma unroll
             for (int u = 0; u < kU; u++)
 #pragma unroll
                 for (int k = 0; k < NS; k++) acc[k] = __fadd_rn(acc[k], cur[u][k]);
-            if (b + 1 < kNB || g + 1 < n_groups) {
+            if (j0 + kU < kJ) {
 #pragma unroll
                 for (int u = 0; u < kU; u++)
 #pragma unroll
@@ -628,7 +614,7 @@ __device__ __forceinline__ void fast_accumulate(const float* __restrict__ Pp, in
         asm volatile("" ::: "memory");  // the group's loads are issued (and used) before it is released
         if (lane == 0) lds_release_store(acc_groups, gbase + g + 1);
         if (g < 8) GNSSHIP_FSTAMP(pe, 64 + g);
-        rslot = nslot;
+        rslot = rslot + 1 == rg ? 0 : rslot + 1;
     }
 }
 

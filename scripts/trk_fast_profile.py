@@ -70,7 +70,10 @@ def main():
             ("derive -> producer 2 has group 0's slots", 1, 30), ("derive -> producer 3 has its last group's slots", 1, 31),
             ("last group seen -> accumulation done", 29, 5),
             ("cycle: spec seen -> replay end", 0, 34), ("cycle: replay end -> taps stored", 34, 6),
-            ("cycle: taps stored -> spec published", 6, 32), ("cycle: spec published -> spec seen (next)", 32, 80 + 0)]
+            ("cycle: taps stored -> spec published", 6, 32), ("cycle: spec published -> spec seen (next)", 32, 80 + 0),
+            ("tail: replay end -> producer 1 has its last slots", 34, 31), ("tail: replay end -> group 6 ready", 34, 54),
+            ("tail: replay end -> group 7 ready", 34, 55), ("tail: replay end -> group 6 seen", 34, 62), ("tail: replay end -> group 7 seen", 34, 63),
+            ("tail: group 7 seen -> accumulation done", 63, 5), ("tail: accumulation done -> taps stored", 5, 6)]
     for nm, a, b in rows:
         ok = (v[:, :, a] > 0) & (v[:, :, b] > 0)
         if not ok.any():
