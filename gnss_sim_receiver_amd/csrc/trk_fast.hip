@@ -101,11 +101,21 @@ namespace gnsship {
 namespace {
 
 #ifndef GNSSHIP_FAST_WAVES
-#define GNSSHIP_FAST_WAVES 6
+#define GNSSHIP_FAST_WAVES 8
 #endif
 constexpr int kFWaves = GNSSHIP_FAST_WAVES;
 constexpr int kFThreads = kFWaves * kWave;
-constexpr int kFProducers = kFWaves - 3;  // every wave but the phasor, accumulator and control waves forms products
+// The accumulation's waves: one for up to 8 product slots (2·taps, the data prompt included), two
+// above (the E1 engine's 12) — each lane adds at most two slots per iteration.
+#ifndef GNSSHIP_ACC_WAVES  // A/B: force the accumulator wave count
+#define GNSSHIP_ACC_WAVES 0
+#endif
+template <int NTT>
+constexpr int acc_waves() { return GNSSHIP_ACC_WAVES > 0 ? GNSSHIP_ACC_WAVES : (2 * NTT > 8 ? 2 : 1); }
+// every wave but the phasor, control and accumulator waves forms products
+template <int NTT>
+constexpr int n_producers() { return kFWaves - 2 - acc_waves<NTT>(); }
+static_assert(kFWaves - 4 >= 1, "trk_fast needs at least one producer wave");
 // Wave roles (fast_roles): the control wave and the phasor wave each get a SIMD of their own — the
 // phasor chain is the epoch's critical path and the control wave's loop update is the next — and the
 // producers share the other SIMDs (two producer waves on a SIMD interleave their issue).
@@ -166,7 +176,7 @@ struct SpecPred {
 struct FShared {
     FJob job;
     float taps[2][2 * kMaxTaps + 2];  // epoch e's tap sums in [e & 1] (+ the data prompt at 2·kMaxTaps), as epoch_pre reads them
-    int32_t taps_seq;                  // e + 1 once the accumulator wave stored epoch e's taps
+    int32_t taps_seq[2];               // [a]: e + 1 once accumulator wave a stored its taps of epoch e
     gnsship_trk_dump_record drec;  // log_data's record of the epoch
     double coh;       // the coherent time lock_status is called with (0: no lock test this epoch)
     int32_t seed_seq; // e + 1 once wave 0 published epoch e's NCO arguments (sh.job without dz)
@@ -175,7 +185,7 @@ struct FShared {
     int32_t lock_seq; // e + 1 once wave 2 published the lock outcome
     int32_t locked;
     int32_t tail_seq;   // e + 1 once wave 1 stored epoch e's N mod 16 tail products
-    int32_t acc_groups; // product groups the accumulator has consumed (counted over the run)
+    int32_t acc_groups[2]; // [a]: product groups accumulator wave a has consumed (counted over the run)
     int32_t step_seq;   // e + 1 once wave 0 published epoch e's early loop values (state 4, SpecArgs)
     SpecArgs spec;      // those values
     SpecPred pred;      // wave 1's phasor prediction for epoch e (published as pred_seq = e + 1)
@@ -260,11 +270,16 @@ __device__ __forceinline__ void lds_wait_ge(const int32_t* p, int v)
 #else
 #define GNSSHIP_PSTEP_NOP "s_nop 0\n\t"
 #endif
+#ifdef GNSSHIP_PSTEP_ADD64  // experiment: the add as VOP3 (24-byte steps, the DPP op at a fixed 8-byte phase)
+#define GNSSHIP_PSTEP_ADD "v_add_f32_e64 "
+#else
+#define GNSSHIP_PSTEP_ADD "v_add_f32 "
+#endif
 #define GNSSHIP_PSTEP(X, Y)                                                                   \
     "v_mul_f32 %[t], %[c], " X "\n\t"                                                      \
     GNSSHIP_PSTEP_NOP                                                                        \
     "v_mul_f32_dpp %[u], " X ", %[k2] quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t" \
-    "v_add_f32 " Y ", %[t], %[u]\n\t"
+    GNSSHIP_PSTEP_ADD Y ", %[t], %[u]\n\t"
 
 // N iterations (1-4) in one asm block (the hazard recognizer pads each block boundary with one
 // s_nop); STORE: the block's input (the task start) goes to its slot half at `lds_off` (a byte offset
@@ -427,16 +442,18 @@ __device__ __forceinline__ void group_codes(const float* __restrict__ code0, con
 
 // Producer phase B, once the slot holds z_l at the task start: per iteration the sample product
 // a = x·z_l (_mm256_complexmul_ps rounding) and its products with the taps' code values,
-// c = _mm256_mul_ps(a, code) (:252-258), into the ring group — the accumulator only adds them — and
-// the chain's own update z·dz (renormalised after the task's first iteration when that is ≡ 0 mod 64,
-// :265-272).  FULL: every lane's task has all G iterations, so nothing is masked.
-template <int FMT, int NTT, int G, bool FULL>
+// c = _mm256_mul_ps(a, code) (:252-258) — the accumulator only adds them — and the chain's own update
+// z·dz (renormalised after the task's first iteration when that is ≡ 0 mod 64, :265-272).  The
+// products of four consecutive iterations of one slot go to the ring as one 16-byte store
+// (ProdLayout).  FULL: every lane's task has all G iterations, so nothing is masked.
+typedef float f4 __attribute__((ext_vector_type(4)));
+template <int FMT, int NTT, int G, bool FULL, class PL>
 __device__ __forceinline__ void group_phasors(i4v span, f2 z, f2 dz, bool renorm, int n0, int cnt, float* __restrict__ pdst, const float (&cv)[G][NTT],
     f2 (&xa)[G < 8 ? G : 8], f2 (&xb)[G < 8 ? G : 8])
 {
     constexpr int SB = sample_bytes<FMT>();
     constexpr int kB = G < 8 ? G : 8;
-    constexpr int IS = 2 * NTT * kAvxLanes;  // one iteration's products (floats)
+    static_assert(kB % 4 == 0, "16-byte product stores");
 #pragma unroll 1
     for (int i0 = 0; i0 < G; i0 += kB) {
         if (i0 + kB < G) {
@@ -444,21 +461,26 @@ __device__ __forceinline__ void group_phasors(i4v span, f2 z, f2 dz, bool renorm
             for (int u = 0; u < kB; u++) xb[u] = load_sample<FMT>(span, (n0 + kAvxLanes * (i0 + kB + u)) * SB, 0);
         }
 #pragma unroll
-        for (int u = 0; u < kB; u++) {
-            const int i = i0 + u;
-            const bool on = FULL || i < cnt;
-            const f2 a = cmul_exact_pk(xa[u], z);
-            float* d = pdst + static_cast<size_t>(i) * IS;
-            // an iteration past the epoch's last holds −0, which the accumulator adds unconditionally:
-            // x + (−0) = x for every x, so its sums are the reference's
+        for (int h = 0; h < kB; h += 4) {
+            f4 q[2 * NTT];
 #pragma unroll
-            for (int q = 0; q < NTT; q++) {
-                d[(2 * q) * kAvxLanes] = on ? __fmul_rn(a.x, cv[i][q]) : -0.0f;
-                d[(2 * q + 1) * kAvxLanes] = on ? __fmul_rn(a.y, cv[i][q]) : -0.0f;
+            for (int u = 0; u < 4; u++) {
+                const int i = i0 + h + u;
+                const bool on = FULL || i < cnt;
+                const f2 a = cmul_exact_pk(xa[h + u], z);
+                // an iteration past the epoch's last holds −0, which the accumulator adds unconditionally:
+                // x + (−0) = x for every x, so its sums are the reference's
+#pragma unroll
+                for (int t = 0; t < NTT; t++) {
+                    q[2 * t][u] = on ? __fmul_rn(a.x, cv[i][t]) : -0.0f;
+                    q[2 * t + 1][u] = on ? __fmul_rn(a.y, cv[i][t]) : -0.0f;
+                }
+                f2 zn = cmul_exact_s(z, dz);
+                if (i == 0 && renorm) zn = normalise_avx(zn);
+                z = zn;
             }
-            f2 zn = cmul_exact_s(z, dz);
-            if (i == 0 && renorm) zn = normalise_avx(zn);
-            z = zn;
+#pragma unroll
+            for (int sl = 0; sl < 2 * NTT; sl++) *reinterpret_cast<f4*>(pdst + sl * PL::kSlot + i0 + h) = q[sl];
         }
         if (i0 + kB < G) {
 #pragma unroll
@@ -467,26 +489,31 @@ __device__ __forceinline__ void group_phasors(i4v span, f2 z, f2 dz, bool renorm
     }
 }
 
-// The product ring's layout (floats): group r, task t (of 4), iteration i (of G), product slot s
-// (2·tap + component), chain l at  r·group_floats + t·task_floats + i·2·NTT·16 + s·16 + l.  Each task
-// is padded by 16 floats so the four tasks a producer wave writes at once fall in different banks.
+// The product ring's layout (floats): group r, product slot s (2·tap + component), chain l, iteration
+// j of the group's 4G at  r·kGroup + s·kSlot + l·kRow + j.  A producer lane (task t, chain l) stores
+// four iterations of one slot at once (16 bytes at j = G·t + 4h), an accumulator lane (slot row,
+// chain l) loads four at once; rows padded to kRow = 4G + 4 floats make both conflict-free (the
+// eight lanes of a ds_write_b128 group start 4 banks apart, the sixteen of a ds_read_b128 group too).
 template <int NTT, int G>
 struct ProdLayout {
-    static constexpr int kIter = 2 * NTT * kAvxLanes;
-    static constexpr int kTask = G * kIter + kAvxLanes;
-    static constexpr int kGroup = 4 * kTask;
+    static constexpr int kJ = 4 * G;
+    static constexpr int kRow = kJ + 4;
+    static constexpr int kSlot = kAvxLanes * kRow;
+    static constexpr int kGroup = 2 * NTT * kSlot;
 };
 
 // ---- producer waves -------------------------------------------------------------------------------
-// Ring group r (of rg) holds one group of 4 tasks = 4G iterations: the products of iteration j of the
-// group, chain l, every tap and component (ProdLayout).  Group tags count over the run
-// (gbase = epoch · n_groups): no flag is re-armed.
+// Ring group r (of rg) holds one group of 4 tasks = 4G iterations: the products of every iteration of
+// the group, chain, tap and component (ProdLayout).  Group tags count over the run (gbase = epoch ·
+// n_groups): no flag is re-armed.  A ring group is reused once every accumulator wave consumed it.
 template <int FMT, int NT, bool DATA, bool IN_MARGIN, int G>
 __device__ __forceinline__ void fast_produce(const FJob& job, i4v span, const float* __restrict__ code0, const float* __restrict__ code1, int L,
     uint64_t* __restrict__ Zs, int rs, float* __restrict__ Pp, int rg, int32_t* ready, const int32_t* acc_groups, int gbase, int lane, int pw, int pe)
 {
     constexpr int SB = sample_bytes<FMT>();
     constexpr int NTT = NT + (DATA ? 1 : 0);
+    constexpr int NP = n_producers<NTT>();
+    constexpr int NA = acc_waves<NTT>();
     using PL = ProdLayout<NTT, G>;
     constexpr int kB = G < 8 ? G : 8;  // iterations whose samples are in flight together
     const int M = job.M, S = job.S;
@@ -506,8 +533,8 @@ __device__ __forceinline__ void fast_produce(const FJob& job, i4v span, const fl
     f2 xa[kB], xb[kB];
     float cv[G][NTT];
     int rslot = pw % rg;
-    const int rstep = kFProducers % rg;
-    for (int g = pw; g < n_groups; g += kFProducers) {
+    const int rstep = NP % rg;
+    for (int g = pw; g < n_groups; g += NP) {
         const int t = 4 * g + tl;
         const bool active = t < S;
         const int m_lo = G * (active ? t : 0);
@@ -519,10 +546,13 @@ __device__ __forceinline__ void fast_produce(const FJob& job, i4v span, const fl
             group_codes<NT, DATA, IN_MARGIN, G, true>(code0, code1, L, n0, G, step, rem, shifts, cv);
         else
             group_codes<NT, DATA, IN_MARGIN, G, false>(code0, code1, L, n0, cnt, step, rem, shifts, cv);
-        // the ring group is free once the accumulator consumed its previous occupant — and in the slot
-        // ring (rg ≤ 16 groups of its 64 tasks) that also means the slot this lane polls next was
-        // consumed on its previous lap (whichever producer took it)
-        if (g >= rg) lds_wait_ge(acc_groups, gbase + g - rg + 1);
+        // the ring group is free once every accumulator wave consumed its previous occupant — and in
+        // the slot ring (rg ≤ 16 groups of its 64 tasks) that also means the slot this lane polls next
+        // was consumed on its previous lap (whichever producer took it)
+        if (g >= rg) {
+#pragma unroll
+            for (int a = 0; a < NA; a++) lds_wait_ge(acc_groups + a, gbase + g - rg + 1);
+        }
         const int ts = active ? t % rs : 0;
         uint64_t* slot = Zs + ts * kAvxLanes + l;
         uint64_t v = kSlotEmpty;
@@ -532,17 +562,17 @@ __device__ __forceinline__ void fast_produce(const FJob& job, i4v span, const fl
             store_slot(slot, __builtin_bit_cast(f2, kSlotEmpty));  // re-armed for the next lap / epoch
         }
         if (g == pw && pw == 0) GNSSHIP_FSTAMP(pe, 30);
-        if (g + kFProducers >= n_groups && pw == 1) GNSSHIP_FSTAMP(pe, 31);
+        if (g + NP >= n_groups && pw == 1) GNSSHIP_FSTAMP(pe, 31);
 #ifdef GNSSHIP_EXP_SERIAL
         while (__hip_atomic_load(&g_replay_done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < pe + 1) __builtin_amdgcn_s_sleep(1);
 #endif
         const f2 z = active ? __builtin_bit_cast(f2, v) : f2{0.0f, 0.0f};
         const bool renorm = ((G * t) & 63) == 0;
-        float* pdst = Pp + static_cast<size_t>(rslot) * PL::kGroup + tl * PL::kTask + l;
+        float* pdst = Pp + static_cast<size_t>(rslot) * PL::kGroup + l * PL::kRow + G * tl;
         if (full)
-            group_phasors<FMT, NTT, G, true>(span, z, dz, renorm, n0, G, pdst, cv, xa, xb);
+            group_phasors<FMT, NTT, G, true, PL>(span, z, dz, renorm, n0, G, pdst, cv, xa, xb);
         else
-            group_phasors<FMT, NTT, G, false>(span, z, dz, renorm, n0, cnt, pdst, cv, xa, xb);
+            group_phasors<FMT, NTT, G, false, PL>(span, z, dz, renorm, n0, cnt, pdst, cv, xa, xb);
         GNSSHIP_PROBE(GNSSHIP_DELAY_PROD);
         if (lane == 0) lds_release_store(ready + rslot, gbase + g + 1);
         if (g < 8) GNSSHIP_FSTAMP(pe, 48 + g);
@@ -551,70 +581,63 @@ __device__ __forceinline__ void fast_produce(const FJob& job, i4v span, const fl
     }
 }
 
-// ---- control wave: the accumulation in u_avx's order ----------------------------------------------
-// Lane (l, r): chain l's accumulators of product slots r, r + 4, r + 8, r + 12 (slot s = 2·tap +
-// component) — each c = _mm256_mul_ps(a, code) the producers formed is added in iteration order,
-// dotProdVal_{l/4}[tap] += c (:252-260), one v_add_f32 per slot and iteration, the slots' chains
-// interleaved.
+// ---- accumulator waves: the accumulation in u_avx's order ---------------------------------------
+// Accumulator wave a (of NA) lane (r, l): chain l's accumulators of the product slots
+// s_k = 4·(a + NA·k) + r (slot s = 2·tap + component) — each c = _mm256_mul_ps(a, code) the producers
+// formed is added in iteration order, dotProdVal_{l/4}[tap] += c (:252-260), one v_add_f32 per slot
+// and iteration, four iterations of a slot per 16-byte load.  A slot index past the last reads the
+// last slot (its sums are discarded).
 template <int NTT>
-constexpr int acc_slots() { return (2 * NTT + 3) / 4; }
+constexpr int acc_slots() { return (2 * NTT + 4 * acc_waves<NTT>() - 1) / (4 * acc_waves<NTT>()); }
+template <int NTT>
+__device__ __forceinline__ int acc_slot(int a, int r, int k) { return 4 * (a + acc_waves<NTT>() * k) + r; }
 
 template <int NTT, int G>
-__device__ __forceinline__ void fast_accumulate(const float* __restrict__ Pp, int rg, const int32_t* ready, int32_t* acc_groups, int gbase, int M, int S,
-    int lane, float (&acc)[acc_slots<NTT>()], int pe)
+__device__ __forceinline__ void fast_accumulate(const float* __restrict__ Pp, int rg, const int32_t* ready, int32_t* acc_done, int gbase, int S,
+    int lane, int a, float (&acc)[acc_slots<NTT>()], int pe)
 {
     using PL = ProdLayout<NTT, G>;
     constexpr int NS = acc_slots<NTT>();
+    constexpr int kQ = PL::kJ / 4;  // four-iteration loads per slot and group
     const int l = lane & (kAvxLanes - 1), r = lane >> 4;
     const int n_groups = (S + 3) / 4;
-    int off[NS];  // lane offsets of the slots (a slot past the last reads the last: discarded)
+    int off[NS];
 #pragma unroll
     for (int k = 0; k < NS; k++) {
         acc[k] = 0.0f;
-        off[k] = min(r + 4 * k, 2 * NTT - 1) * kAvxLanes + l;
+        off[k] = min(acc_slot<NTT>(a, r, k), 2 * NTT - 1) * PL::kSlot + l * PL::kRow;
     }
     int rslot = 0;
+    int seen = __hip_atomic_load(ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     for (int g = 0; g < n_groups; g++) {
-        lds_wait_eq(ready + rslot, gbase + g + 1);
+        if (seen != gbase + g + 1) lds_wait_eq(ready + rslot, gbase + g + 1);
+        asm volatile("" ::: "memory");  // the group's loads follow the flag
         if (g == 0) GNSSHIP_FSTAMP(pe, 28);
         if (g == n_groups - 1) GNSSHIP_FSTAMP(pe, 29);
         if (g < 8) GNSSHIP_FSTAMP(pe, 56 + g);
-        // every group is added whole: a partial group's iterations past the epoch's end hold −0.
-        // Batches of kU iterations, the next batch's loads issued before the current one's adds.
+        // every group is added whole: a partial group's iterations past the epoch's end hold −0
         const float* src = Pp + static_cast<size_t>(rslot) * PL::kGroup;
-        constexpr int kJ = 4 * G;
-        constexpr int kU = GNSSHIP_ACC_BATCH < kJ ? GNSSHIP_ACC_BATCH : kJ;
-        static_assert(kJ % kU == 0, "accumulator batch");
-        auto at = [&](int j, int k) { return src[off[k] + (j / G) * PL::kTask + (j % G) * PL::kIter]; };
-        float cur[kU][NS];
+        f4 v[kQ][NS];
 #pragma unroll
-        for (int u = 0; u < kU; u++)
+        for (int q = 0; q < kQ; q++)
 #pragma unroll
-            for (int k = 0; k < NS; k++) cur[u][k] = at(u, k);
+            for (int k = 0; k < NS; k++) v[q][k] = *reinterpret_cast<const f4*>(src + off[k] + 4 * q);
+        const int rnext = rslot + 1 == rg ? 0 : rslot + 1;
+        // the next group's flag, read behind this group's loads (usually already set when they are added)
+        if (g + 1 < n_groups) seen = __hip_atomic_load(ready + rnext, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 #pragma unroll
-        for (int j0 = 0; j0 < kJ; j0 += kU) {
-            float nxt[kU][NS];
-            if (j0 + kU < kJ) {
+        for (int q = 0; q < kQ; q++)
 #pragma unroll
-                for (int u = 0; u < kU; u++)
+            for (int k = 0; k < NS; k++)
 #pragma unroll
-                    for (int k = 0; k < NS; k++) nxt[u][k] = at(j0 + kU + u, k);
-            }
+                for (int u = 0; u < 4; u++) acc[k] = __fadd_rn(acc[k], v[q][k][u]);
+        // the group is released after its adds (they consumed every load, so the release's wait for
+        // them is free; released earlier, that wait would stall the adds behind the last load)
 #pragma unroll
-            for (int u = 0; u < kU; u++)
-#pragma unroll
-                for (int k = 0; k < NS; k++) acc[k] = __fadd_rn(acc[k], cur[u][k]);
-            if (j0 + kU < kJ) {
-#pragma unroll
-                for (int u = 0; u < kU; u++)
-#pragma unroll
-                    for (int k = 0; k < NS; k++) cur[u][k] = nxt[u][k];
-            }
-        }
-        asm volatile("" ::: "memory");  // the group's loads are issued (and used) before it is released
-        if (lane == 0) lds_release_store(acc_groups, gbase + g + 1);
+        for (int k = 0; k < NS; k++) asm volatile("" ::"v"(acc[k]) : "memory");
+        if (lane == 0) lds_release_store(acc_done, gbase + g + 1);
         if (g < 8) GNSSHIP_FSTAMP(pe, 64 + g);
-        rslot = rslot + 1 == rg ? 0 : rslot + 1;
+        rslot = rnext;
     }
 }
 
@@ -663,10 +686,10 @@ __device__ void stage_code_f(float* dst, const CodeDesc& cd)
     for (int q = threadIdx.x; q < nq; q += kFThreads) d4[q] = src[q];
 }
 
-// THRU (more channels than CUs): two workgroups per CU (≤ 256 VGPRs — the control wave keeps the
-// channel in registers); otherwise one.  Two waves on a SIMD each keep their own issue cadence.
+// THRU (more channels than CUs): two workgroups per CU; otherwise one.  Two waves on a SIMD each keep
+// their own issue cadence.
 template <bool THRU>
-constexpr int fast_waves_per_simd() { return THRU ? 2 : 1; }
+constexpr int fast_waves_per_simd() { return (THRU ? 2 : 1) * ((kFWaves + 3) / 4); }
 
 template <bool THRU>
 __device__ __forceinline__ const auto& loop_params(const TrkParams& k, const KFast& kf)
@@ -769,34 +792,48 @@ __global__ __launch_bounds__(kFThreads, fast_waves_per_simd<THRU>()) void trk_fa
     for (int i = tid; i < kFProfEpochs * kFProfSlots; i += kFThreads) g_fprof_lds[i] = 0;
 #endif
     __syncthreads();
-    // the role of each wave: the first two waves alone on their SIMD take the phasor and control
-    // roles (in that order), the others produce; without two such SIMDs, waves 1 and 0 do
+    // The role of each wave, by SIMD: the phasor wave (the epoch's critical chain) takes the SIMD with
+    // the fewest waves and shares it with accumulator wave 0 (whose adds trail the replay); the control
+    // wave and accumulator wave 1 go next, the producers fill the rest.  pw: the index within the role.
+    constexpr int NA = acc_waves<NTT>();
     int role = kRoleProducer, pw = 0;
     {
-        // the phasor and accumulator waves (the epoch's chain) alone on a SIMD each; the control wave
-        // shares one with a producer (its loop work overlaps the production of the next epoch)
-        int cnt[4] = {0, 0, 0, 0};
-        for (int w = 0; w < kFWaves; w++) cnt[simd_of[w] & 3]++;
-        int rep = -1, acw = -1, ctl = -1;
-        for (int w = 0; w < kFWaves; w++)
-            if (cnt[simd_of[w] & 3] == 1) {
-                if (rep < 0) rep = w;
-                else if (acw < 0) acw = w;
+        auto count = [&](int sd) {
+            int c = 0;
+            for (int w = 0; w < kFWaves; w++) c += (simd_of[w] & 3) == sd ? 1 : 0;
+            return c;
+        };
+        int nacc = 0, nprod = 0;
+        bool ctl = false, rep = false;
+        // SIMDs in order of their wave count (no arrays: a dynamically indexed one would live in scratch)
+        for (int cc = 1; cc <= kFWaves; cc++)
+            for (int sd = 0; sd < 4; sd++) {
+                if (count(sd) != cc) continue;
+                for (int w = 0; w < kFWaves; w++) {
+                    if ((simd_of[w] & 3) != sd) continue;
+                    int rl, idx = 0;
+                    if (!rep) {
+                        rl = kRoleReplay;
+                        rep = true;
+                    } else if (nacc == 0) {
+                        rl = kRoleAccum;
+                        idx = nacc++;
+                    } else if (!ctl) {
+                        rl = kRoleControl;
+                        ctl = true;
+                    } else if (nacc < NA) {
+                        rl = kRoleAccum;
+                        idx = nacc++;
+                    } else {
+                        rl = kRoleProducer;
+                        idx = nprod++;
+                    }
+                    if (w == wave) {
+                        role = rl;
+                        pw = idx;
+                    }
+                }
             }
-        if (rep < 0 || acw < 0) {
-            rep = 1;
-            acw = 2;
-        }
-        for (int w = 0; w < kFWaves && ctl < 0; w++)
-            if (w != rep && w != acw) ctl = w;
-        int np = 0;
-        for (int w = 0; w < kFWaves; w++) {
-            if (w == wave) {
-                role = w == rep ? kRoleReplay : w == acw ? kRoleAccum : w == ctl ? kRoleControl : kRoleProducer;
-                pw = np;
-            }
-            if (w != rep && w != acw && w != ctl) np++;
-        }
         role = __builtin_amdgcn_readfirstlane(role);
         pw = __builtin_amdgcn_readfirstlane(pw);
     }
@@ -812,8 +849,8 @@ __global__ __launch_bounds__(kFThreads, fast_waves_per_simd<THRU>()) void trk_fa
         sh.pre_seq = 0;
         sh.lock_seq = 0;
         sh.tail_seq = 0;
-        sh.taps_seq = 0;
-        sh.acc_groups = 0;
+        sh.taps_seq[0] = sh.taps_seq[1] = 0;
+        sh.acc_groups[0] = sh.acc_groups[1] = 0;
         sh.step_seq = 0;
         sh.pred_seq = 0;
         sh.verdict = 0;
@@ -1079,9 +1116,9 @@ __global__ __launch_bounds__(kFThreads, fast_waves_per_simd<THRU>()) void trk_fa
             if (!job.runnable) break;
                 const i4v span = sample_span<FMT>(samples, job.off, N);
                 if (job.in_margin)
-                    fast_produce<FMT, NT, DATA, true, G>(job, span, c0, c1, L, Zs, rs, Pp, rg, ready, &sh.acc_groups, gbase, lane, pw, e);
+                    fast_produce<FMT, NT, DATA, true, G>(job, span, c0, c1, L, Zs, rs, Pp, rg, ready, sh.acc_groups, gbase, lane, pw, e);
                 else
-                    fast_produce<FMT, NT, DATA, false, G>(job, span, c0, c1, L, Zs, rs, Pp, rg, ready, &sh.acc_groups, gbase, lane, pw, e);
+                    fast_produce<FMT, NT, DATA, false, G>(job, span, c0, c1, L, Zs, rs, Pp, rg, ready, sh.acc_groups, gbase, lane, pw, e);
                 if (pw < 2) GNSSHIP_FSTAMP(e, 3 + pw);  // 3, 4: producers 0 and 1 done
                 if (pw == 0) {
                     // cn0_and_tracking_lock_status (:972-1029) on the LDS copy of its members, beside the loop update
@@ -1106,7 +1143,7 @@ __global__ __launch_bounds__(kFThreads, fast_waves_per_simd<THRU>()) void trk_fa
                 constexpr int NS = acc_slots<NTT>();
                 float acc[NS];
                 GNSSHIP_FSTAMP(e, 27);
-                fast_accumulate<NTT, G>(Pp, rg, ready, &sh.acc_groups, gbase, M, S, lane, acc, e);
+                fast_accumulate<NTT, G>(Pp, rg, ready, &sh.acc_groups[pw], gbase, S, lane, pw, acc, e);
                 GNSSHIP_FSTAMP(e, 5);
                 const int r = lane >> 4;
     #pragma unroll
@@ -1116,7 +1153,7 @@ __global__ __launch_bounds__(kFThreads, fast_waves_per_simd<THRU>()) void trk_fa
                     for (int j = 0; j < job.tail; j++) {
     #pragma unroll
                         for (int kk = 0; kk < NS; kk++) {
-                            const int sl = min(r + 4 * kk, 2 * NTT - 1);
+                            const int sl = min(acc_slot<NTT>(pw, r, kk), 2 * NTT - 1);
                             const f2 tv = sh.tailp[j][sl >> 1];
                             acc[kk] = acc[kk] + ((sl & 1) ? tv.y : tv.x);
                         }
@@ -1125,7 +1162,7 @@ __global__ __launch_bounds__(kFThreads, fast_waves_per_simd<THRU>()) void trk_fa
                 if ((lane & 15) == 0) {
     #pragma unroll
                     for (int kk = 0; kk < NS; kk++) {
-                        const int sl = r + 4 * kk;  // slot 2·tap + component
+                        const int sl = acc_slot<NTT>(pw, r, kk);  // slot 2·tap + component
                         if (sl < 2 * NTT) {
                             const int tap = sl >> 1;
                             const int o = (DATA && tap == NT) ? 2 * kMaxTaps : 2 * tap;
@@ -1133,7 +1170,7 @@ __global__ __launch_bounds__(kFThreads, fast_waves_per_simd<THRU>()) void trk_fa
                         }
                     }
                 }
-                if (lane == 0) lds_release_store(&sh.taps_seq, e + 1);
+                if (lane == 0) lds_release_store(&sh.taps_seq[pw], e + 1);
             }
             GNSSHIP_FSTAMP(e, 6);
         }
@@ -1146,7 +1183,8 @@ __global__ __launch_bounds__(kFThreads, fast_waves_per_simd<THRU>()) void trk_fa
             wait_seq(&sh.job_seq, e + 1);
             const FJob job = uniform_job(sh.job);
             if (!job.runnable) break;
-            wait_seq(&sh.taps_seq, e + 1);  // the accumulator wave's taps of this epoch
+#pragma unroll
+            for (int a = 0; a < NA; a++) wait_seq(&sh.taps_seq[a], e + 1);  // the accumulator waves' taps of this epoch
             GNSSHIP_FCLK(e, 14);
             if (cancel) {
                 // the epoch seeded speculatively before the last lock test failed: the channel stopped
@@ -1318,7 +1356,10 @@ struct FastPlan {
     size_t bytes = 0;
     int G = 8, rs = 0, rg = 0;
 };
-constexpr int kFastG = 8;
+#ifndef GNSSHIP_FAST_G
+#define GNSSHIP_FAST_G 8
+#endif
+constexpr int kFastG = GNSSHIP_FAST_G;
 constexpr int kFastSlotRingGroups = 16;
 static FastPlan fast_plan(const TrkParams& p, int code_cap_floats, int n_chans)
 {
@@ -1333,7 +1374,7 @@ static FastPlan fast_plan(const TrkParams& p, int code_cap_floats, int n_chans)
     const size_t slot_b = kAvxLanes * sizeof(uint64_t);
     // a group's products (ProdLayout: 4 tasks of G iterations × 2·ntt slots × 16 chains, each task
     // padded by 16 floats) and its flag
-    const size_t group_b = static_cast<size_t>(4) * (G * 2 * ntt * kAvxLanes + kAvxLanes) * sizeof(float) + sizeof(int32_t);
+    const size_t group_b = static_cast<size_t>(2 * ntt) * kAvxLanes * (4 * G + 4) * sizeof(float) + sizeof(int32_t);  // ProdLayout + flag
     // more channels than CUs: two workgroups per CU share its LDS
     size_t budget = n_chans > device_cus() ? 72 * 1024 : kTrkPersistMaxLds;
     if (const char* env = std::getenv("GNSSHIP_TRK_FAST_LDS"))  // tests: a smaller budget forces the rings

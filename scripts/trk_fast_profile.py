@@ -73,7 +73,8 @@ def main():
             ("cycle: taps stored -> spec published", 6, 32), ("cycle: spec published -> spec seen (next)", 32, 80 + 0),
             ("tail: replay end -> producer 1 has its last slots", 34, 31), ("tail: replay end -> group 6 ready", 34, 54),
             ("tail: replay end -> group 7 ready", 34, 55), ("tail: replay end -> group 6 seen", 34, 62), ("tail: replay end -> group 7 seen", 34, 63),
-            ("tail: group 7 seen -> accumulation done", 63, 5), ("tail: accumulation done -> taps stored", 5, 6)]
+            ("tail: group 7 seen -> accumulation done", 63, 5), ("tail: replay end -> last group seen", 34, 29),
+            ("tail: last group seen -> accumulation done", 29, 5), ("tail: accumulation done -> taps stored", 5, 6)]
     for nm, a, b in rows:
         ok = (v[:, :, a] > 0) & (v[:, :, b] > 0)
         if not ok.any():
