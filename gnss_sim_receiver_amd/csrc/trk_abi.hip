@@ -78,6 +78,7 @@ struct gnsship_trk {
     bool pending_out = false, pending_dump = false;
     // gnsship_trk_set_trace: per channel-epoch correlation trace of the last run
     bool trace_on = false;
+    int last_engine = GNSSHIP_TRK_ENGINE_NONE;  // the engine the last run / launch used
     gnsship_trk_corr_trace* trace_dev = nullptr;
     size_t trace_cap = 0;
     size_t trace_n = 0;  // records of the last run (max_rounds × max_channels)
@@ -312,6 +313,13 @@ void release(gnsship_trk* t)
 }
 
 }  // namespace
+
+extern "C" int gnsship_trk_last_engine(gnsship_trk* t, int* engine)
+{
+    if (!t || !engine) return GNSSHIP_E_INVAL;
+    *engine = t->last_engine;
+    return GNSSHIP_OK;
+}
 
 extern "C" int gnsship_trk_destroy(gnsship_trk* t)
 {
@@ -634,6 +642,7 @@ static int trk_enqueue(gnsship_trk* t, const void* src, int fmt, uint64_t buffer
         const int n_codes = static_cast<int>(ctx->codes_host.size());
         hipError_t e;
         const bool fast = avx && trk_fast_supported(t->params, code_cap, nc);
+        t->last_engine = fast ? (trk_fast_thru(nc) ? GNSSHIP_TRK_ENGINE_FAST_THROUGHPUT : GNSSHIP_TRK_ENGINE_FAST_LATENCY) : GNSSHIP_TRK_ENGINE_PERSIST;
         if (fast)
             e = launch_trk_fast(t->params_dev, t->params, t->chans_dev, nc, ctx->codes_dev, n_codes, code_cap, src, fmt, buffer_first_sample,
                 n_buffer_samples, max_rounds, out ? t->rec_dev : nullptr, dump ? t->dump_dev : nullptr, trace, t->ran_dev, ctx->stream);
@@ -642,6 +651,7 @@ static int trk_enqueue(gnsship_trk* t, const void* src, int fmt, uint64_t buffer
                 n_buffer_samples, max_rounds, out ? t->rec_dev : nullptr, dump ? t->dump_dev : nullptr, trace, t->ran_dev, avx, ctx->stream);
         if (e != hipSuccess) return hip_fail(ctx, e, fast ? "launch_trk_fast" : "launch_trk_persist");
     }
+    if (!persist) t->last_engine = GNSSHIP_TRK_ENGINE_ROUNDS;
     for (int r = 0; r <= max_rounds && !persist; r++) {
         const int consume = r > 0 ? 1 : 0, emit = r < max_rounds ? 1 : 0;
         gnsship_trk_epoch* rec = (out && r > 0) ? t->rec_dev + static_cast<size_t>(r - 1) * nc : nullptr;
@@ -678,6 +688,12 @@ static int trk_finish(gnsship_trk* t, gnsship_trk_epoch* out, gnsship_trk_dump_r
     if ((out && !t->pending_out) || (dump && !t->pending_dump)) {  // the launch did not keep them: nothing to copy
         HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
         t->pending_rounds = -1;
+        if (rounds_done) {  // the launch ran and advanced the channels: report the epochs it consumed
+            int n = 0;
+            for (int r = 0; r < max_rounds; r++)
+                if (ran[r] > 0) n = r + 1;
+            *rounds_done = n;
+        }
         return fail(ctx, GNSSHIP_E_INVAL, "gnsship_trk_collect: records / dump requested that the launch did not keep (want_records / want_dump)");
     }
     if (out) HIP_TRY(ctx, hipMemcpyAsync(out, t->rec_dev, sizeof(gnsship_trk_epoch) * nrec, hipMemcpyDeviceToHost, ctx->stream));

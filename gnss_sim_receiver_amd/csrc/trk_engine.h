@@ -143,6 +143,7 @@ hipError_t launch_trk_persist(const TrkParams* params_dev, const TrkParams& para
 // The latency-optimised persistent loop for the AVX rotator (trk_fast.hip): register-resident loop
 // state, flagless phasor slots, lock detectors beside the loop update.
 bool trk_fast_supported(const TrkParams& p, int code_cap_floats, int n_chans);
+bool trk_fast_thru(int n_chans);  // the throughput form (more channels than CUs)
 hipError_t launch_trk_fast(const TrkParams* params_dev, const TrkParams& params, TrkChannel* chans, int n_chans, const CodeDesc* codes, int n_codes,
     int code_cap_floats, const void* samples, int fmt, uint64_t buf_first, int64_t buf_len, int max_rounds, gnsship_trk_epoch* rec,
     gnsship_trk_dump_record* dump, gnsship_trk_corr_trace* trace, int* ran_count, hipStream_t stream);

@@ -72,6 +72,12 @@ __device__ __forceinline__ void trkf_prof_clock(int e, int k)
 }
 }  // namespace gnsship
 namespace gnsship {
+// a duration (shader cycles) into slot k of epoch e (per-role wait accounting)
+__device__ __forceinline__ void trkf_prof_val(int e, int k, unsigned long long v)
+{
+    const int r = e - kFProfFirst;
+    if (g_trkf_prof && r >= 0 && r < kFProfEpochs && (threadIdx.x & 63) == 0) g_fprof_lds[r * kFProfSlots + k] = v;
+}
 __device__ __forceinline__ void trkf_prof_hwid(int k)  // HW_ID (wave slot, SIMD, CU, SE) of the stamping wave (row 0)
 {
     if (g_trkf_prof && (threadIdx.x & 63) == 0) g_fprof_lds[k] = static_cast<uint32_t>(__builtin_amdgcn_s_getreg(4 | (31 << 11)));
@@ -80,6 +86,8 @@ __device__ __forceinline__ void trkf_prof_hwid(int k)  // HW_ID (wave slot, SIMD
 #define GNSSHIP_FSTAMP(e, k) gnsship::trkf_prof_stamp((e), (k))
 #define GNSSHIP_FCLK(e, k) gnsship::trkf_prof_clock((e), (k))
 #define GNSSHIP_FHWID(k) gnsship::trkf_prof_hwid((k))
+#define GNSSHIP_FVAL(e, k, v) gnsship::trkf_prof_val((e), (k), (v))
+#define GNSSHIP_FCLOCK() clock64()
 #define GNSSHIP_TRK_LOOP_STAMP(k) gnsship::trkf_prof_stamp(gnsship::g_fprof_epoch, (k))
 #else
 #define GNSSHIP_FSTAMP(e, k) \
@@ -91,8 +99,13 @@ __device__ __forceinline__ void trkf_prof_hwid(int k)  // HW_ID (wave slot, SIMD
 #define GNSSHIP_FHWID(k) \
     do {                 \
     } while (0)
+#define GNSSHIP_FVAL(e, k, v) \
+    do {                      \
+    } while (0)
+#define GNSSHIP_FCLOCK() 0ull
 #endif
 
+#define GNSSHIP_LOOP_INLINE __attribute__((always_inline))
 #include "trk_loop.h"
 
 #pragma clang fp contract(off)
@@ -103,19 +116,34 @@ namespace {
 #ifndef GNSSHIP_FAST_WAVES
 #define GNSSHIP_FAST_WAVES 8
 #endif
+#ifndef GNSSHIP_THRU_WAVES  // more channels than CUs: two workgroups per CU, fewer waves each
+#define GNSSHIP_THRU_WAVES 6
+#endif
+#ifndef GNSSHIP_FAST_WAVES_LONG  // long epochs (N ≥ kLongEpoch): production throughput counts, more producers
+#define GNSSHIP_FAST_WAVES_LONG 8
+#endif
 constexpr int kFWaves = GNSSHIP_FAST_WAVES;
-constexpr int kFThreads = kFWaves * kWave;
-// The accumulation's waves: one for up to 8 product slots (2·taps, the data prompt included), two
-// above (the E1 engine's 12) — each lane adds at most two slots per iteration.
+constexpr int kFWavesLong = GNSSHIP_FAST_WAVES_LONG;
+constexpr int kLongEpoch = 10000;  // samples per epoch from which the long-epoch wave count applies
+// The accumulation's waves: one per four product slots (2·taps, the data prompt included: GPS and
+// B1I 6 slots → 2 waves, the E1 engine's 12 → 3), so that each lane adds ONE slot per iteration —
+// a single serial chain per lane, and room for two groups' loads in flight (fast_accumulate).
+#ifndef GNSSHIP_ACC_PIPE  // A/B: the accumulator loads the next group behind the current one's adds (measured slower)
+#define GNSSHIP_ACC_PIPE 0
+#endif
+#ifndef GNSSHIP_ROLE_PLAN  // wave roles by SIMD: 0 phasor + accumulator 0 share a SIMD; 1 one primary role per SIMD
+#define GNSSHIP_ROLE_PLAN 0
+#endif
 #ifndef GNSSHIP_ACC_WAVES  // A/B: force the accumulator wave count
 #define GNSSHIP_ACC_WAVES 0
 #endif
 template <int NTT>
-constexpr int acc_waves() { return GNSSHIP_ACC_WAVES > 0 ? GNSSHIP_ACC_WAVES : (2 * NTT > 8 ? 2 : 1); }
+constexpr int acc_waves() { return GNSSHIP_ACC_WAVES > 0 ? GNSSHIP_ACC_WAVES : (2 * NTT + 3) / 4; }
 // every wave but the phasor, control and accumulator waves forms products
-template <int NTT>
-constexpr int n_producers() { return kFWaves - 2 - acc_waves<NTT>(); }
-static_assert(kFWaves - 4 >= 1, "trk_fast needs at least one producer wave");
+template <int NTT, int W>
+constexpr int n_producers() { return W - 2 - acc_waves<NTT>(); }
+constexpr int kMaxAccWaves = 4;  // 2·(kMaxTaps + 1) slots / 4 rows
+static_assert(kFWaves - 4 >= 1 && GNSSHIP_THRU_WAVES - 4 >= 1, "trk_fast needs at least one producer wave");
 // Wave roles (fast_roles): the control wave and the phasor wave each get a SIMD of their own — the
 // phasor chain is the epoch's critical path and the control wave's loop update is the next — and the
 // producers share the other SIMDs (two producer waves on a SIMD interleave their issue).
@@ -176,7 +204,7 @@ struct SpecPred {
 struct FShared {
     FJob job;
     float taps[2][2 * kMaxTaps + 2];  // epoch e's tap sums in [e & 1] (+ the data prompt at 2·kMaxTaps), as epoch_pre reads them
-    int32_t taps_seq[2];               // [a]: e + 1 once accumulator wave a stored its taps of epoch e
+    int32_t taps_seq[kMaxAccWaves];    // [a]: e + 1 once accumulator wave a stored its taps of epoch e
     gnsship_trk_dump_record drec;  // log_data's record of the epoch
     double coh;       // the coherent time lock_status is called with (0: no lock test this epoch)
     int32_t seed_seq; // e + 1 once wave 0 published epoch e's NCO arguments (sh.job without dz)
@@ -185,7 +213,7 @@ struct FShared {
     int32_t lock_seq; // e + 1 once wave 2 published the lock outcome
     int32_t locked;
     int32_t tail_seq;   // e + 1 once wave 1 stored epoch e's N mod 16 tail products
-    int32_t acc_groups[2]; // [a]: product groups accumulator wave a has consumed (counted over the run)
+    int32_t acc_groups[kMaxAccWaves]; // [a]: product groups accumulator wave a has consumed (counted over the run)
     int32_t step_seq;   // e + 1 once wave 0 published epoch e's early loop values (state 4, SpecArgs)
     SpecArgs spec;      // those values
     SpecPred pred;      // wave 1's phasor prediction for epoch e (published as pred_seq = e + 1)
@@ -326,6 +354,29 @@ __device__ __forceinline__ float pstep(float x, float c, float k2, uint32_t lds_
 }
 #undef GNSSHIP_ST
 #undef GNSSHIP_PSTEP_ASM
+
+// One whole 64-iteration block of 8-iteration tasks after its normalisation (the block's first
+// iteration and its task-0 store are done): the 7 remaining iterations of task 0, then tasks 1-7 —
+// each stores its start value (ds_write_b32 at its slot row, an immediate offset) and runs 8 steps —
+// as ONE asm block.  The hazard recognizer pads every inline-asm boundary with an s_nop and the
+// slot address would be re-derived per task otherwise; here one address serves the block.
+#define GNSSHIP_PS(A, B) GNSSHIP_PSTEP("%[" #A "]", "%[" #B "]")
+#define GNSSHIP_TASK8(A, B, OFF)                                                                                           \
+    GNSSHIP_PS(A, B) "ds_write_b32 %[p], %[" #A "] offset:" #OFF "\n\t" GNSSHIP_PS(B, A) GNSSHIP_PS(A, B) GNSSHIP_PS(B, A) \
+        GNSSHIP_PS(A, B) GNSSHIP_PS(B, A) GNSSHIP_PS(A, B) GNSSHIP_PS(B, A)
+__device__ __forceinline__ float pblock64_g8(float x, float c, float k2, uint32_t lds_off)
+{
+    float t, u, w;
+    asm volatile(GNSSHIP_PS(x, w) GNSSHIP_PS(w, x) GNSSHIP_PS(x, w) GNSSHIP_PS(w, x) GNSSHIP_PS(x, w) GNSSHIP_PS(w, x) GNSSHIP_PS(x, w)
+                     GNSSHIP_TASK8(w, x, 128) GNSSHIP_TASK8(w, x, 256) GNSSHIP_TASK8(w, x, 384) GNSSHIP_TASK8(w, x, 512)
+                         GNSSHIP_TASK8(w, x, 640) GNSSHIP_TASK8(w, x, 768) GNSSHIP_TASK8(w, x, 896) "v_mov_b32 %[x], %[w]\n\t"
+                 : [x] "+v"(x), [t] "=&v"(t), [u] "=&v"(u), [w] "=&v"(w)
+                 : [c] "s"(c), [k2] "v"(k2), [p] "v"(lds_off)
+                 : "memory");
+    return x;
+}
+#undef GNSSHIP_TASK8
+#undef GNSSHIP_PS
 // x·dz^N: N ≥ 0 iterations
 template <int N>
 __device__ __forceinline__ float ppow(float x, float c, float k2)
@@ -367,13 +418,19 @@ __device__ __forceinline__ float fast_replay(float x, float c, float k2, int M, 
         const int full = (S - 1) / kTB;  // whole blocks before the last task
 #pragma unroll 1
         for (int b = 0; b < full; b++) {
+            if constexpr (G == 8 && kSlotRow == 128) {
+                // the block's first iteration normalises; the other 63 run in one asm block
+                x = pblock64_g8(pnormalise(pstep<1, true>(x, c, k2, off)), c, k2, off);
+                off += kTB * kSlotRow;
+            } else {
 #pragma unroll
-            for (int q = 0; q < kTB; q++) {
-                if (q == 0)  // the block's first iteration normalises
-                    x = ppow<G - 1>(pnormalise(pstep<1, true>(x, c, k2, off)), c, k2);
-                else
-                    x = ppow<G - 4>(pstep<4, true>(x, c, k2, off), c, k2);
-                off += kSlotRow;
+                for (int q = 0; q < kTB; q++) {
+                    if (q == 0)  // the block's first iteration normalises
+                        x = ppow<G - 1>(pnormalise(pstep<1, true>(x, c, k2, off)), c, k2);
+                    else
+                        x = ppow<G - 4>(pstep<4, true>(x, c, k2, off), c, k2);
+                    off += kSlotRow;
+                }
             }
         }
         if (full * kTB < S - 1) {  // a partial block: its first task normalises, the rest do not
@@ -387,23 +444,45 @@ __device__ __forceinline__ float fast_replay(float x, float c, float k2, int M, 
         }
         ts = S - 1;
     } else {
-        uint32_t next_state = ~0u;  // the slot's state read one task ahead
+        // The slot ring (rs tasks, a multiple of kTB): a task's slot is rewritten once its producer
+        // re-armed it (its previous lap consumed).  Whole 64-iteration blocks check their kTB slots
+        // once, before the block, and run as one asm block; the rest go task by task.  (A slot read
+        // per task in front of the asm blocks cost a full LDS round trip per task.)
+        int t = 0;
+        if constexpr (G == 8 && kSlotRow == 128) {
+            if (rs % kTB == 0) {
+                const int full = (S - 1) / kTB;
 #pragma unroll 1
-        for (int t = 0; t < S - 1; t++) {
-            if (t >= rs) {
-                uint32_t v = next_state;
-                while (v != ~0u) {
-                    __builtin_amdgcn_s_sleep(GNSSHIP_POLL_SLEEP);
-                    v = __hip_atomic_load(half0 + 2 * kAvxLanes * ts, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                for (int b = 0; b < full; b++, t += kTB) {
+                    const int ts0 = t % rs;
+                    if (t >= rs) {
+                        bool busy = true;
+                        while (busy) {
+                            uint32_t v[kTB];
+#pragma unroll
+                            for (int q = 0; q < kTB; q++) v[q] = __hip_atomic_load(half0 + 2 * kAvxLanes * (ts0 + q), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                            busy = false;
+#pragma unroll
+                            for (int q = 0; q < kTB; q++) busy = busy || v[q] != ~0u;
+                            if (busy) __builtin_amdgcn_s_sleep(GNSSHIP_POLL_SLEEP);
+                        }
+                    }
+                    off = base + static_cast<uint32_t>(ts0) * kSlotRow;
+                    x = pblock64_g8(pnormalise(pstep<1, true>(x, c, k2, off)), c, k2, off);
                 }
             }
-            const int tn = ts + 1 == rs ? 0 : ts + 1;
-            if (t + 1 >= rs) next_state = __hip_atomic_load(half0 + 2 * kAvxLanes * tn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        ts = t % rs;
+        off = base + static_cast<uint32_t>(ts) * kSlotRow;
+#pragma unroll 1
+        for (; t < S - 1; t++) {
+            if (t >= rs)
+                while (__hip_atomic_load(half0 + 2 * kAvxLanes * ts, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != ~0u) __builtin_amdgcn_s_sleep(GNSSHIP_POLL_SLEEP);
             if (t % kTB == 0)
                 x = ppow<G - 1>(pnormalise(pstep<1, true>(x, c, k2, off)), c, k2);
             else
                 x = ppow<G - 4>(pstep<4, true>(x, c, k2, off), c, k2);
-            ts = tn;
+            ts = ts + 1 == rs ? 0 : ts + 1;
             off = base + static_cast<uint32_t>(ts) * kSlotRow;
         }
         if (S - 1 >= rs)
@@ -506,13 +585,13 @@ struct ProdLayout {
 // Ring group r (of rg) holds one group of 4 tasks = 4G iterations: the products of every iteration of
 // the group, chain, tap and component (ProdLayout).  Group tags count over the run (gbase = epoch ·
 // n_groups): no flag is re-armed.  A ring group is reused once every accumulator wave consumed it.
-template <int FMT, int NT, bool DATA, bool IN_MARGIN, int G>
+template <int FMT, int NT, bool DATA, bool IN_MARGIN, int G, int W>
 __device__ __forceinline__ void fast_produce(const FJob& job, i4v span, const float* __restrict__ code0, const float* __restrict__ code1, int L,
     uint64_t* __restrict__ Zs, int rs, float* __restrict__ Pp, int rg, int32_t* ready, const int32_t* acc_groups, int gbase, int lane, int pw, int pe)
 {
     constexpr int SB = sample_bytes<FMT>();
     constexpr int NTT = NT + (DATA ? 1 : 0);
-    constexpr int NP = n_producers<NTT>();
+    constexpr int NP = n_producers<NTT, W>();
     constexpr int NA = acc_waves<NTT>();
     using PL = ProdLayout<NTT, G>;
     constexpr int kB = G < 8 ? G : 8;  // iterations whose samples are in flight together
@@ -534,6 +613,8 @@ __device__ __forceinline__ void fast_produce(const FJob& job, i4v span, const fl
     float cv[G][NTT];
     int rslot = pw % rg;
     const int rstep = NP % rg;
+    unsigned long long w_ring = 0, w_slot = 0;  // profiling: cycles waiting for ring space / phasor slots
+    const unsigned long long t_run = GNSSHIP_FCLOCK();
     for (int g = pw; g < n_groups; g += NP) {
         const int t = 4 * g + tl;
         const bool active = t < S;
@@ -549,10 +630,13 @@ __device__ __forceinline__ void fast_produce(const FJob& job, i4v span, const fl
         // the ring group is free once every accumulator wave consumed its previous occupant — and in
         // the slot ring (rg ≤ 16 groups of its 64 tasks) that also means the slot this lane polls next
         // was consumed on its previous lap (whichever producer took it)
+        const unsigned long long t0 = GNSSHIP_FCLOCK();
         if (g >= rg) {
 #pragma unroll
             for (int a = 0; a < NA; a++) lds_wait_ge(acc_groups + a, gbase + g - rg + 1);
         }
+        const unsigned long long t1 = GNSSHIP_FCLOCK();
+        w_ring += t1 - t0;
         const int ts = active ? t % rs : 0;
         uint64_t* slot = Zs + ts * kAvxLanes + l;
         uint64_t v = kSlotEmpty;
@@ -561,6 +645,7 @@ __device__ __forceinline__ void fast_produce(const FJob& job, i4v span, const fl
             while (static_cast<uint32_t>(v = load_slot(slot)) == ~0u || static_cast<uint32_t>(v >> 32) == ~0u) __builtin_amdgcn_s_sleep(GNSSHIP_POLL_SLEEP);
             store_slot(slot, __builtin_bit_cast(f2, kSlotEmpty));  // re-armed for the next lap / epoch
         }
+        w_slot += GNSSHIP_FCLOCK() - t1;
         if (g == pw && pw == 0) GNSSHIP_FSTAMP(pe, 30);
         if (g + NP >= n_groups && pw == 1) GNSSHIP_FSTAMP(pe, 31);
 #ifdef GNSSHIP_EXP_SERIAL
@@ -569,15 +654,24 @@ __device__ __forceinline__ void fast_produce(const FJob& job, i4v span, const fl
         const f2 z = active ? __builtin_bit_cast(f2, v) : f2{0.0f, 0.0f};
         const bool renorm = ((G * t) & 63) == 0;
         float* pdst = Pp + static_cast<size_t>(rslot) * PL::kGroup + l * PL::kRow + G * tl;
+#ifndef GNSSHIP_EXP_NOPROD  // timing experiment: the producers only follow the slots and set the flags
         if (full)
             group_phasors<FMT, NTT, G, true, PL>(span, z, dz, renorm, n0, G, pdst, cv, xa, xb);
         else
             group_phasors<FMT, NTT, G, false, PL>(span, z, dz, renorm, n0, cnt, pdst, cv, xa, xb);
+#else
+        if (z.x == 12345.0f) pdst[0] = cv[0][0];
+#endif
         GNSSHIP_PROBE(GNSSHIP_DELAY_PROD);
         if (lane == 0) lds_release_store(ready + rslot, gbase + g + 1);
         if (g < 8) GNSSHIP_FSTAMP(pe, 48 + g);
         rslot += rstep;
         if (rslot >= rg) rslot -= rg;
+    }
+    if (pw == 0) {  // slots 41-43: producer 0's ring waits, slot waits, whole production
+        GNSSHIP_FVAL(pe, 41, w_ring);
+        GNSSHIP_FVAL(pe, 42, w_slot);
+        GNSSHIP_FVAL(pe, 43, GNSSHIP_FCLOCK() - t_run);
     }
 }
 
@@ -607,38 +701,96 @@ __device__ __forceinline__ void fast_accumulate(const float* __restrict__ Pp, in
         acc[k] = 0.0f;
         off[k] = min(acc_slot<NTT>(a, r, k), 2 * NTT - 1) * PL::kSlot + l * PL::kRow;
     }
-    int rslot = 0;
-    int seen = __hip_atomic_load(ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    for (int g = 0; g < n_groups; g++) {
-        if (seen != gbase + g + 1) lds_wait_eq(ready + rslot, gbase + g + 1);
-        asm volatile("" ::: "memory");  // the group's loads follow the flag
-        if (g == 0) GNSSHIP_FSTAMP(pe, 28);
-        if (g == n_groups - 1) GNSSHIP_FSTAMP(pe, 29);
-        if (g < 8) GNSSHIP_FSTAMP(pe, 56 + g);
-        // every group is added whole: a partial group's iterations past the epoch's end hold −0
-        const float* src = Pp + static_cast<size_t>(rslot) * PL::kGroup;
-        f4 v[kQ][NS];
+    // Software-pipelined: group g + 1's loads are issued before group g's adds whenever its flag is
+    // already set (the flag is read behind group g's loads, so seeing it costs no extra wait), and
+    // the two register sets alternate (the loop is unrolled by two: no register copies).
+    auto load_group = [&](int rs, f4 (&v)[kQ][NS]) __attribute__((always_inline)) {
+#ifdef GNSSHIP_EXP_NOACC  // timing experiment: the accumulator only follows the flags
+        return;
+#endif
+        const float* src = Pp + static_cast<size_t>(rs) * PL::kGroup;
 #pragma unroll
         for (int q = 0; q < kQ; q++)
 #pragma unroll
             for (int k = 0; k < NS; k++) v[q][k] = *reinterpret_cast<const f4*>(src + off[k] + 4 * q);
-        const int rnext = rslot + 1 == rg ? 0 : rslot + 1;
-        // the next group's flag, read behind this group's loads (usually already set when they are added)
-        if (g + 1 < n_groups) seen = __hip_atomic_load(ready + rnext, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    };
+    auto wait_group = [&](int g, int rs) __attribute__((always_inline)) {
+        lds_wait_eq(ready + rs, gbase + g + 1);
+        asm volatile("" ::: "memory");  // the group's loads follow the flag
+    };
+    // group g from registers `cur` (its loads issued); group g + 1 into `nxt`.  Returns whether
+    // group g + 1's loads were issued.
+    auto step = [&](int g, int rs, bool cur_issued, f4 (&cur)[kQ][NS], f4 (&nxt)[kQ][NS]) __attribute__((always_inline)) {
+        if (!cur_issued) {
+            wait_group(g, rs);
+            load_group(rs, cur);
+        }
+        if (g == 0) GNSSHIP_FSTAMP(pe, 28);
+        if (g == n_groups - 1) GNSSHIP_FSTAMP(pe, 29);
+        if (g < 8) GNSSHIP_FSTAMP(pe, 56 + g);
+        const int rn = rs + 1 == rg ? 0 : rs + 1;
+        bool next = false;
+        if (g + 1 < n_groups && __hip_atomic_load(ready + rn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == gbase + g + 2) {
+            asm volatile("" ::: "memory");
+            load_group(rn, nxt);
+            next = true;
+        }
+        // every group is added whole: a partial group's iterations past the epoch's end hold −0
+#pragma unroll
+        for (int q = 0; q < kQ; q++)
+#pragma unroll
+            for (int k = 0; k < NS; k++)
+#pragma unroll
+                for (int u = 0; u < 4; u++) acc[k] = __fadd_rn(acc[k], cur[q][k][u]);
+        // released after its adds: they consumed every load of the group, so the ring slot may be
+        // rewritten (no wait: group g + 1's loads may still be in flight)
+#pragma unroll
+        for (int k = 0; k < NS; k++) asm volatile("" ::"v"(acc[k]) : "memory");
+        if (lane == 0) __hip_atomic_store(acc_done, gbase + g + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (g < 8) GNSSHIP_FSTAMP(pe, 64 + g);
+        return next;
+    };
+    int rslot = 0;
+#if GNSSHIP_ACC_PIPE
+    f4 va[kQ][NS], vb[kQ][NS];
+    bool issued = false;
+    for (int g = 0; g < n_groups; g += 2) {
+        issued = step(g, rslot, issued, va, vb);
+        rslot = rslot + 1 == rg ? 0 : rslot + 1;
+        if (g + 1 < n_groups) {
+            issued = step(g + 1, rslot, issued, vb, va);
+            rslot = rslot + 1 == rg ? 0 : rslot + 1;
+        }
+    }
+#else
+    (void)step;
+    unsigned long long w_flag = 0;  // profiling: cycles spent waiting for the groups' flags
+    const unsigned long long t_run = GNSSHIP_FCLOCK();
+    for (int g = 0; g < n_groups; g++) {
+        const unsigned long long t0 = GNSSHIP_FCLOCK();
+        wait_group(g, rslot);
+        w_flag += GNSSHIP_FCLOCK() - t0;
+        if (g == 0) GNSSHIP_FSTAMP(pe, 28);
+        if (g == n_groups - 1) GNSSHIP_FSTAMP(pe, 29);
+        f4 v[kQ][NS];
+        load_group(rslot, v);
 #pragma unroll
         for (int q = 0; q < kQ; q++)
 #pragma unroll
             for (int k = 0; k < NS; k++)
 #pragma unroll
                 for (int u = 0; u < 4; u++) acc[k] = __fadd_rn(acc[k], v[q][k][u]);
-        // the group is released after its adds (they consumed every load, so the release's wait for
-        // them is free; released earlier, that wait would stall the adds behind the last load)
 #pragma unroll
         for (int k = 0; k < NS; k++) asm volatile("" ::"v"(acc[k]) : "memory");
-        if (lane == 0) lds_release_store(acc_done, gbase + g + 1);
-        if (g < 8) GNSSHIP_FSTAMP(pe, 64 + g);
-        rslot = rnext;
+        GNSSHIP_PROBE(GNSSHIP_DELAY_ACC);
+        if (lane == 0) __hip_atomic_store(acc_done, gbase + g + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        rslot = rslot + 1 == rg ? 0 : rslot + 1;
     }
+    if (a < 2) {  // slots 44/45 (accumulator 0), 46/47 (accumulator 1): flag waits, whole accumulation
+        GNSSHIP_FVAL(pe, 44 + 2 * a, w_flag);
+        GNSSHIP_FVAL(pe, 45 + 2 * a, GNSSHIP_FCLOCK() - t_run);
+    }
+#endif
 }
 
 // u_avx's final combination of the 16 chains (:279-291), valid at lane 0 of each 16-lane row:
@@ -678,18 +830,18 @@ __device__ __forceinline__ void fast_tail_products(const FJob& job, i4v span, co
     }
 }
 
-__device__ void stage_code_f(float* dst, const CodeDesc& cd)
+__device__ __forceinline__ void stage_code_f(float* dst, const CodeDesc& cd, int nthreads)
 {
     const int nq = padded_code_quads(cd.len);
     const float4* src = reinterpret_cast<const float4*>(cd.ptr - kCodeMargin);
     float4* d4 = reinterpret_cast<float4*>(dst);
-    for (int q = threadIdx.x; q < nq; q += kFThreads) d4[q] = src[q];
+    for (int q = threadIdx.x; q < nq; q += nthreads) d4[q] = src[q];
 }
 
 // THRU (more channels than CUs): two workgroups per CU; otherwise one.  Two waves on a SIMD each keep
 // their own issue cadence.
-template <bool THRU>
-constexpr int fast_waves_per_simd() { return (THRU ? 2 : 1) * ((kFWaves + 3) / 4); }
+template <bool THRU, int W>
+constexpr int fast_waves_per_simd() { return ((THRU ? 2 : 1) * W + 3) / 4; }
 
 template <bool THRU>
 __device__ __forceinline__ const auto& loop_params(const TrkParams& k, const KFast& kf)
@@ -756,13 +908,16 @@ __device__ __forceinline__ f2 derive_chains(float rem, f2 inc, int lane)
     return z;
 }
 
-template <int FMT, int NT, bool DATA, int G, bool THRU, bool SRING>
-__global__ __launch_bounds__(kFThreads, fast_waves_per_simd<THRU>()) void trk_fast_kernel(const TrkParams* __restrict__ pk, TrkChannel* __restrict__ chans,
+template <int FMT, int NT, bool DATA, int G, bool THRU, bool SRING, int W>
+__global__ __launch_bounds__(W * kWave, (fast_waves_per_simd<THRU, W>())) void trk_fast_kernel(const TrkParams* __restrict__ pk, TrkChannel* __restrict__ chans,
     const CodeDesc* __restrict__ codes, int n_codes, const void* __restrict__ samples, uint64_t buf_first, int64_t buf_len, int max_rounds,
     int n_chans, int code_cap_floats, int rs, int rg, gnsship_trk_epoch* __restrict__ rec, gnsship_trk_dump_record* __restrict__ dump,
     gnsship_trk_corr_trace* __restrict__ trace, int* __restrict__ ran_count)
 {
     constexpr int NTT = NT + (DATA ? 1 : 0);
+    constexpr int kFWaves = W;  // this instance's waves
+    constexpr int kFThreads = kFWaves * kWave;
+    static_assert(acc_waves<NTT>() <= kMaxAccWaves && n_producers<NTT, kFWaves>() >= 1, "trk_fast wave roles");
     extern __shared__ __attribute__((aligned(16))) float lds[];
     __shared__ TrkChannel sc;
     __shared__ FShared sh;
@@ -803,37 +958,88 @@ __global__ __launch_bounds__(kFThreads, fast_waves_per_simd<THRU>()) void trk_fa
             for (int w = 0; w < kFWaves; w++) c += (simd_of[w] & 3) == sd ? 1 : 0;
             return c;
         };
-        int nacc = 0, nprod = 0;
-        bool ctl = false, rep = false;
-        // SIMDs in order of their wave count (no arrays: a dynamically indexed one would live in scratch)
-        for (int cc = 1; cc <= kFWaves; cc++)
-            for (int sd = 0; sd < 4; sd++) {
-                if (count(sd) != cc) continue;
-                for (int w = 0; w < kFWaves; w++) {
-                    if ((simd_of[w] & 3) != sd) continue;
-                    int rl, idx = 0;
-                    if (!rep) {
-                        rl = kRoleReplay;
-                        rep = true;
-                    } else if (nacc == 0) {
-                        rl = kRoleAccum;
-                        idx = nacc++;
-                    } else if (!ctl) {
-                        rl = kRoleControl;
-                        ctl = true;
-                    } else if (nacc < NA) {
-                        rl = kRoleAccum;
-                        idx = nacc++;
-                    } else {
-                        rl = kRoleProducer;
-                        idx = nprod++;
+        // plan 1: one primary role per SIMD — the phasor wave, the accumulators, the control wave —
+        // each beside producers only; plan 0: the phasor wave shares its SIMD with accumulator 0.
+        // A plan that leaves a role unassigned (an unusual wave placement) falls back to plan 0.
+        auto assign = [&](int plan) __attribute__((always_inline)) {
+            int nacc = 0, nprod = 0, nsimd = 0;
+            bool ctl = false, rep = false;
+            // SIMDs in order of their wave count (no arrays: a dynamically indexed one would live in scratch)
+            for (int cc = 1; cc <= kFWaves; cc++)
+                for (int sd = 0; sd < 4; sd++) {
+                    if (count(sd) != cc) continue;
+                    bool first = true;
+                    for (int w = 0; w < kFWaves; w++) {
+                        if ((simd_of[w] & 3) != sd) continue;
+                        int rl, idx = 0;
+                        if (plan == 3) {
+                            // the phasor wave beside a producer, the accumulators together, the
+                            // control wave beside a producer
+                            if (nsimd == 0 && !rep) {
+                                rl = kRoleReplay;
+                                rep = true;
+                            } else if (nsimd == 1 && nacc < NA) {
+                                rl = kRoleAccum;
+                                idx = nacc++;
+                            } else if (nsimd == 2 && !ctl) {
+                                rl = kRoleControl;
+                                ctl = true;
+                            } else if (nsimd >= 2 && nacc < NA) {
+                                rl = kRoleAccum;
+                                idx = nacc++;
+                            } else if (nsimd >= 3 && !ctl) {
+                                rl = kRoleControl;
+                                ctl = true;
+                            } else {
+                                rl = kRoleProducer;
+                                idx = nprod++;
+                            }
+                        } else if (plan == 2) {
+                            // the phasor wave beside the control wave (whose loop work mostly falls
+                            // between replays), the accumulators together, the producers together
+                            if (nsimd == 0 && !rep) {
+                                rl = kRoleReplay;
+                                rep = true;
+                            } else if (nsimd == 0 && !ctl) {
+                                rl = kRoleControl;
+                                ctl = true;
+                            } else if (nsimd >= 1 && nacc < NA) {
+                                rl = kRoleAccum;
+                                idx = nacc++;
+                            } else if (!ctl) {
+                                rl = kRoleControl;
+                                ctl = true;
+                            } else {
+                                rl = kRoleProducer;
+                                idx = nprod++;
+                            }
+                        } else if (!rep) {
+                            rl = kRoleReplay;
+                            rep = true;
+                        } else if (plan == 1 ? (first && nacc < NA) : nacc == 0) {
+                            rl = kRoleAccum;
+                            idx = nacc++;
+                        } else if (plan == 1 ? (first && !ctl) : !ctl) {
+                            rl = kRoleControl;
+                            ctl = true;
+                        } else if (plan == 0 && nacc < NA) {
+                            rl = kRoleAccum;
+                            idx = nacc++;
+                        } else {
+                            rl = kRoleProducer;
+                            idx = nprod++;
+                        }
+                        first = false;
+                        if (w == wave) {
+                            role = rl;
+                            pw = idx;
+                        }
                     }
-                    if (w == wave) {
-                        role = rl;
-                        pw = idx;
-                    }
+                    nsimd++;
                 }
-            }
+            return rep && ctl && nacc == NA && nprod >= 1;
+        };
+        if (!assign(GNSSHIP_ROLE_PLAN)) assign(0);
         role = __builtin_amdgcn_readfirstlane(role);
         pw = __builtin_amdgcn_readfirstlane(pw);
     }
@@ -849,8 +1055,7 @@ __global__ __launch_bounds__(kFThreads, fast_waves_per_simd<THRU>()) void trk_fa
         sh.pre_seq = 0;
         sh.lock_seq = 0;
         sh.tail_seq = 0;
-        sh.taps_seq[0] = sh.taps_seq[1] = 0;
-        sh.acc_groups[0] = sh.acc_groups[1] = 0;
+        for (int a = 0; a < kMaxAccWaves; a++) sh.taps_seq[a] = sh.acc_groups[a] = 0;
         sh.step_seq = 0;
         sh.pred_seq = 0;
         sh.verdict = 0;
@@ -865,8 +1070,8 @@ __global__ __launch_bounds__(kFThreads, fast_waves_per_simd<THRU>()) void trk_fa
     if (g_trkf_prof && lane == 0)  // row 0's slots 72-77: HW_ID | role << 32 of every wave
         g_fprof_lds[72 + wave] = static_cast<uint32_t>(__builtin_amdgcn_s_getreg(4 | (31 << 11))) | (static_cast<unsigned long long>(role) << 32);
 #endif
-    stage_code_f(code0, codes[sc.code_id]);
-    if constexpr (DATA) stage_code_f(code1, codes[sc.data_code_id]);
+    stage_code_f(code0, codes[sc.code_id], kFThreads);
+    if constexpr (DATA) stage_code_f(code1, codes[sc.data_code_id], kFThreads);
     __syncthreads();  // the code replicas are staged before any wave correlates
     const int L = codes[sc.code_id].len;
     const float* c0 = code0 + kCodeMargin;
@@ -956,6 +1161,7 @@ __global__ __launch_bounds__(kFThreads, fast_waves_per_simd<THRU>()) void trk_fa
             // remainder phase and step are the seed's floats, and the job goes out with the seed
             int code = 3;
             if (!SRING && __hip_atomic_load(&sh.pred_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= e + 1) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");  // sh.pred is read after its sequence number
                 code = 2;
                 if (runnable && __builtin_bit_cast(uint32_t, sh.pred.rem) == __builtin_bit_cast(uint32_t, rem_carr) &&
                     __builtin_bit_cast(uint32_t, sh.pred.step) == __builtin_bit_cast(uint32_t, stepf)) {
@@ -975,6 +1181,14 @@ __global__ __launch_bounds__(kFThreads, fast_waves_per_simd<THRU>()) void trk_fa
     // One epoch loop per role: the roles never share a control-flow path, so the waits the compiler
     // places for one role's memory operations are not charged to another (a merged loop made the
     // control wave wait for the producers' sample loads it never issued).
+#ifdef GNSSHIP_PRIO_ACC  // A/B: the accumulators issue ahead of their SIMD partner
+    if (role == kRoleAccum) __builtin_amdgcn_s_setprio(GNSSHIP_PRIO_ACC);
+#endif
+#ifdef GNSSHIP_PRIO_ROLES  // A/B: issue priority by role — phasor 3, accumulators 2, control 1, producers 0
+    if (role == kRoleReplay) __builtin_amdgcn_s_setprio(3);
+    else if (role == kRoleAccum) __builtin_amdgcn_s_setprio(2);
+    else if (role == kRoleControl) __builtin_amdgcn_s_setprio(1);
+#endif
     if (role == kRoleReplay) {
 #ifdef GNSSHIP_PRIO_REPLAY
         __builtin_amdgcn_s_setprio(GNSSHIP_PRIO_REPLAY);
@@ -1052,6 +1266,7 @@ __global__ __launch_bounds__(kFThreads, fast_waves_per_simd<THRU>()) void trk_fa
                             status = 1;
                         }
                     }
+                    GNSSHIP_FVAL(e, 78, static_cast<unsigned long long>(status));  // profiling: 1 confirmed, 2 refuted
                     if (status == 1) {
                         published = true;
                     } else {  // mispredicted (or the end of the run): the slots are cleared before the job goes out
@@ -1116,9 +1331,9 @@ __global__ __launch_bounds__(kFThreads, fast_waves_per_simd<THRU>()) void trk_fa
             if (!job.runnable) break;
                 const i4v span = sample_span<FMT>(samples, job.off, N);
                 if (job.in_margin)
-                    fast_produce<FMT, NT, DATA, true, G>(job, span, c0, c1, L, Zs, rs, Pp, rg, ready, sh.acc_groups, gbase, lane, pw, e);
+                    fast_produce<FMT, NT, DATA, true, G, kFWaves>(job, span, c0, c1, L, Zs, rs, Pp, rg, ready, sh.acc_groups, gbase, lane, pw, e);
                 else
-                    fast_produce<FMT, NT, DATA, false, G>(job, span, c0, c1, L, Zs, rs, Pp, rg, ready, sh.acc_groups, gbase, lane, pw, e);
+                    fast_produce<FMT, NT, DATA, false, G, kFWaves>(job, span, c0, c1, L, Zs, rs, Pp, rg, ready, sh.acc_groups, gbase, lane, pw, e);
                 if (pw < 2) GNSSHIP_FSTAMP(e, 3 + pw);  // 3, 4: producers 0 and 1 done
                 if (pw == 0) {
                     // cn0_and_tracking_lock_status (:972-1029) on the LDS copy of its members, beside the loop update
@@ -1352,6 +1567,14 @@ static int device_cus()
     return cache[dev];
 }
 
+// More channels than CUs: the throughput form (fast_waves<true>, two workgroups per CU, each with
+// half the LDS budget).  GNSSHIP_TRK_THRU=0/1 forces either form (A/B, tests).
+static bool fast_thru(int n_chans)
+{
+    if (const char* env = std::getenv("GNSSHIP_TRK_THRU")) return env[0] == '1';
+    return n_chans > device_cus();
+}
+
 struct FastPlan {
     size_t bytes = 0;
     int G = 8, rs = 0, rg = 0;
@@ -1361,6 +1584,7 @@ struct FastPlan {
 #endif
 constexpr int kFastG = GNSSHIP_FAST_G;
 constexpr int kFastSlotRingGroups = 16;
+constexpr int kFastMinRingGroups = 4;
 static FastPlan fast_plan(const TrkParams& p, int code_cap_floats, int n_chans)
 {
     FastPlan f;
@@ -1376,7 +1600,7 @@ static FastPlan fast_plan(const TrkParams& p, int code_cap_floats, int n_chans)
     // padded by 16 floats) and its flag
     const size_t group_b = static_cast<size_t>(2 * ntt) * kAvxLanes * (4 * G + 4) * sizeof(float) + sizeof(int32_t);  // ProdLayout + flag
     // more channels than CUs: two workgroups per CU share its LDS
-    size_t budget = n_chans > device_cus() ? 72 * 1024 : kTrkPersistMaxLds;
+    size_t budget = fast_thru(n_chans) ? 72 * 1024 : kTrkPersistMaxLds;
     if (const char* env = std::getenv("GNSSHIP_TRK_FAST_LDS"))  // tests: a smaller budget forces the rings
         budget = std::min(budget, static_cast<size_t>(std::atol(env)) * 1024);
     auto fit = [&](int rs) -> int {  // product groups that fit beside `rs` slots (0: fewer than 2)
@@ -1387,8 +1611,10 @@ static FastPlan fast_plan(const TrkParams& p, int code_cap_floats, int n_chans)
     };
     int rs = S, rg = fit(S);
     // the slot ring must hold at least 4 tasks per product group (a producer passed the ring's
-    // back-pressure before it polls a slot, so the slot's previous lap is consumed)
-    if (rg < n_groups && S > 4 * kFastSlotRingGroups) {
+    // back-pressure before it polls a slot, so the slot's previous lap is consumed).  It is used only
+    // when the whole epoch's slots leave fewer than kFastMinRingGroups product groups: with every
+    // slot in LDS the replay never waits and may run speculatively (ahead of the seed).
+    if (rg < std::min(n_groups, kFastMinRingGroups) && S > 4 * kFastSlotRingGroups) {
         const int rg2 = std::min(fit(4 * kFastSlotRingGroups), kFastSlotRingGroups);
         if (rg2 > rg) {
             rs = 4 * kFastSlotRingGroups;
@@ -1403,6 +1629,8 @@ static FastPlan fast_plan(const TrkParams& p, int code_cap_floats, int n_chans)
     return f;
 }
 
+bool trk_fast_thru(int n_chans) { return fast_thru(n_chans); }
+
 bool trk_fast_supported(const TrkParams& p, int code_cap_floats, int n_chans)
 {
     if (!trk_persist_supports(p) || p.conf.rotator != GNSSHIP_ROTATOR_AVX || p.conf.high_dyn) return false;
@@ -1411,10 +1639,8 @@ bool trk_fast_supported(const TrkParams& p, int code_cap_floats, int n_chans)
         if (env[0] == '0') return false;
         if (env[0] == '1') return fast_plan(p, code_cap_floats, n_chans).bytes > 0;
     }
-    // More channels than CUs: channel-epochs per second, not epoch latency, is what counts, and
-    // trk_persist.hip's four equal correlating waves sustain more of them (measured at 65536
-    // channels: 76.6 M vs 64.8 M channel-epochs/s)
-    if (n_chans > device_cus()) return false;
+    // every channel count: with more channels than CUs the throughput form (fast_thru), which keeps
+    // u_avx's accumulation order as the latency form does (trk_persist.hip's tree sums do not)
     return fast_plan(p, code_cap_floats, n_chans).bytes > 0;
 }
 
@@ -1428,13 +1654,16 @@ hipError_t launch_trk_fast(const TrkParams* params_dev, const TrkParams& params,
     const int S = std::max(1, (N / kAvxLanes + f.G - 1) / f.G);
     const bool sring = f.rs < S;
     const bool data = params.jobs_per_channel > 1;
-    bool thru = n_chans > device_cus();
-    if (const char* env = std::getenv("GNSSHIP_TRK_THRU")) thru = env[0] == '1';
+    const bool thru = fast_thru(n_chans);
     const int nt = params.n_taps;
-    dim3 grid(n_chans), block(kFThreads);
+    // the form: throughput (more channels than CUs), long epochs (more producer waves), latency
+    const int form = thru ? 1 : (N >= kLongEpoch ? 2 : 0);
+    const int waves = form == 1 ? GNSSHIP_THRU_WAVES : form == 2 ? kFWavesLong : kFWaves;
+    dim3 grid(n_chans), block(waves * kWave);
 #define GNSSHIP_FAST(F, NTV, DV, SR)                                                                                                               \
     do {                                                                                                                                         \
-        auto kfn = thru ? trk_fast_kernel<F, NTV, DV, kFastG, true, SR> : trk_fast_kernel<F, NTV, DV, kFastG, false, SR>;                        \
+        auto kfn = form == 1 ? trk_fast_kernel<F, NTV, DV, kFastG, true, SR, GNSSHIP_THRU_WAVES>                                                  \
+                             : form == 2 ? trk_fast_kernel<F, NTV, DV, kFastG, false, SR, kFWavesLong> : trk_fast_kernel<F, NTV, DV, kFastG, false, SR, kFWaves>; \
         hipError_t e0 = hipFuncSetAttribute(reinterpret_cast<const void*>(kfn), hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(f.bytes)); \
         if (e0 != hipSuccess) return e0;                                                                                                         \
         hipLaunchKernelGGL(kfn, grid, block, f.bytes, stream, params_dev, chans, codes, n_codes, samples, buf_first, buf_len, max_rounds, n_chans, \

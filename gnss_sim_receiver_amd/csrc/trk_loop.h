@@ -13,6 +13,12 @@
 //   :1189-1260, save_correlation_results :1262-1350, acquire_secondary :925-970,
 //   general_work states 2 (:1789-1932), 3 (:1933-1970) and 4 (:1971-2028).
 #pragma once
+// GNSSHIP_LOOP_INLINE: the loop functions' inlining attribute — trk_fast.hip forces them inline (its
+// epoch loops are large enough for the inliner to give up, and an out-of-line call there caps the
+// whole kernel's registers); the other engines leave the choice to the compiler.
+#ifndef GNSSHIP_LOOP_INLINE
+#define GNSSHIP_LOOP_INLINE
+#endif
 #include <cmath>
 #include <type_traits>
 
@@ -42,7 +48,7 @@ __device__ __forceinline__ double div_carrier(const K& k, double x) { return div
 constexpr double kHalfPi = kGnssPi / 2.0;
 
 // fll_diff_atan + phase_unwrap (tracking_discriminators.cc:27-41, 68-76)
-__device__ double fll_diff_atan(const float* s1, const float* s2, double t1, double t2)
+__device__ GNSSHIP_LOOP_INLINE double fll_diff_atan(const float* s1, const float* s2, double t1, double t2)
 {
     double d = static_cast<double>(__fsub_rn(glibc_atanf(__fdiv_rn(s2[1], s2[0])), glibc_atanf(__fdiv_rn(s1[1], s1[0]))));
     if (isnan(d)) d = 0.0;
@@ -53,7 +59,7 @@ __device__ double fll_diff_atan(const float* s1, const float* s2, double t1, dou
     return d / (t2 - t1);
 }
 
-__device__ float smooth(Smoother& s, float raw, float alpha, float one_minus_alpha, float min_value, float offset, int init_samples)
+__device__ GNSSHIP_LOOP_INLINE float smooth(Smoother& s, float raw, float alpha, float one_minus_alpha, float min_value, float offset, int init_samples)
 {
     float v;
     if (s.initializing) {
@@ -92,7 +98,7 @@ __device__ __forceinline__ void m2m4_sums(const float* prompt, int length, float
     }
 }
 
-__device__ float cn0_m2m4(const float* prompt, int length, float coh_integration_time_s)
+__device__ GNSSHIP_LOOP_INLINE float cn0_m2m4(const float* prompt, int length, float coh_integration_time_s)
 {
     float psig = 0.0f, m_2 = 0.0f, m_4 = 0.0f, aux;
     const float n = static_cast<float>(length);
@@ -110,7 +116,7 @@ __device__ float cn0_m2m4(const float* prompt, int length, float coh_integration
     return __fsub_rn(__fmul_rn(10.0f, glibc_log10f(snr)), __fmul_rn(10.0f, glibc_log10f(coh_integration_time_s)));
 }
 
-__device__ float carrier_lock_detector(const float* prompt)  // called with length 1 (:989)
+__device__ GNSSHIP_LOOP_INLINE float carrier_lock_detector(const float* prompt)  // called with length 1 (:989)
 {
     const float si = prompt[0], sq = prompt[1];
     const float nbp = __fadd_rn(__fmul_rn(si, si), __fmul_rn(sq, sq));
@@ -118,7 +124,7 @@ __device__ float carrier_lock_detector(const float* prompt)  // called with leng
     return __fdiv_rn(nbd, nbp);
 }
 
-__device__ bool lock_status(const TrkParams& k, TrkChannel& c, double coh_integration_time_s)
+__device__ GNSSHIP_LOOP_INLINE bool lock_status(const TrkParams& k, TrkChannel& c, double coh_integration_time_s)
 {
     const int ns = k.conf.cn0_samples;
     if (c.cn0_counter < ns) {
@@ -467,7 +473,7 @@ __device__ __forceinline__ void store_regs(const LoopRegs& r, TrkChannel& c)
     c.rem_code_phase_chips = r.rem_code_phase_chips;
 }
 
-__device__ float loop_filter_apply(const TrkParams& k, TrkChannel& c, float x)
+__device__ GNSSHIP_LOOP_INLINE float loop_filter_apply(const TrkParams& k, TrkChannel& c, float x)
 {
     const LoopSet& q = loopset(k, c);
     float result = 0.0f;
@@ -484,7 +490,7 @@ __device__ float loop_filter_apply(const TrkParams& k, TrkChannel& c, float x)
 // products in the same order (outputs[(idx+ii)%4] ≡ lfo[ii] before the insert, inputs[(idx'+ii)%4] ≡
 // lfi[ii] after it).
 template <class K, class C>
-__device__ float loop_filter_apply(const K& k, C& c, float x)
+__device__ GNSSHIP_LOOP_INLINE float loop_filter_apply(const K& k, C& c, float x)
 {
     const LoopSet& q = loopset(k, c);
     float result = 0.0f;
@@ -505,7 +511,7 @@ __device__ float loop_filter_apply(const K& k, C& c, float x)
 }
 
 template <class K, class C>
-__device__ float carrier_filter(const K& k, C& c, float fll, float pll, float T)
+__device__ GNSSHIP_LOOP_INLINE float carrier_filter(const K& k, C& c, float fll, float pll, float T)
 {
     const LoopSet& q = loopset(k, c);
     if (k.fp_order == 3) {
@@ -528,7 +534,7 @@ struct NoDopplerHook {
 };
 
 template <class K, class C, class H = NoDopplerHook>
-__device__ void run_dll_pll(const K& k, C& c, const H& on_doppler = H{})
+__device__ GNSSHIP_LOOP_INLINE void run_dll_pll(const K& k, C& c, const H& on_doppler = H{})
 {
     double disc;
     if (c.cloop)
@@ -579,7 +585,7 @@ __device__ void run_dll_pll(const K& k, C& c, const H& on_doppler = H{})
 
 // high_dyn rate estimate (:1208-1221, :1241-1254): mean step of the newest smoother_length entries
 // minus the mean of the oldest, over the newest entries' samples; sums in the reference's order.
-__device__ double smoothed_rate(const TrkChannel& c, const TrkHist& h, const double* first, int L)
+__device__ GNSSHIP_LOOP_INLINE double smoothed_rate(const TrkChannel& c, const TrkHist& h, const double* first, int L)
 {
     const int cap = 2 * L;
     double cp1 = 0.0, cp2 = 0.0, samples = 0.0;
@@ -606,7 +612,7 @@ __device__ __forceinline__ float carr_rem_next(float rem, double adv)
 }
 
 template <class K, class C>
-__device__ void update_tracking_vars(const K& k, C& c, TrkHist* h)
+__device__ GNSSHIP_LOOP_INLINE void update_tracking_vars(const K& k, C& c, TrkHist* h)
 {
     const double fs = k.conf.fs_in;
     const double T_chip = 1.0 / c.code_freq_chips;
@@ -646,7 +652,7 @@ __device__ void update_tracking_vars(const K& k, C& c, TrkHist* h)
 __device__ __forceinline__ int bit_at(const uint32_t* bits, int i) { return (bits[i >> 5] >> (i & 31)) & 1; }
 
 template <class K, class C>
-__device__ void push_sign(const K& k, C& c, float prompt_re)
+__device__ GNSSHIP_LOOP_INLINE void push_sign(const K& k, C& c, float prompt_re)
 {
     const int cap = syncset(k, c).secondary_len;
     const uint32_t neg = prompt_re < 0.0f ? 1u : 0u;
@@ -665,7 +671,7 @@ __device__ void push_sign(const K& k, C& c, float prompt_re)
 }
 
 template <class K, class C>
-__device__ bool acquire_secondary(const K& k, C& c)
+__device__ GNSSHIP_LOOP_INLINE bool acquire_secondary(const K& k, C& c)
 {
     int corr = 0;
     const uint32_t* bits = mem(c).sign_bits;
@@ -682,7 +688,7 @@ __device__ bool acquire_secondary(const K& k, C& c)
 }
 
 template <class C>
-__device__ void clear_tracking_vars(C& c)
+__device__ GNSSHIP_LOOP_INLINE void clear_tracking_vars(C& c)
 {
     c.p_data[0] = c.p_data[1] = 0.0f;
     c.p_old[0] = c.p_old[1] = 0.0f;
@@ -706,7 +712,7 @@ __device__ __forceinline__ void cadd(float* acc, const float* v, float sgn)
 }
 
 template <class C>
-__device__ void zero_accu(C& c)
+__device__ GNSSHIP_LOOP_INLINE void zero_accu(C& c)
 {
     c.ve[0] = c.ve[1] = c.e[0] = c.e[1] = c.p[0] = c.p[1] = 0.0f;
     c.l[0] = c.l[1] = c.vl[0] = c.vl[1] = 0.0f;
@@ -714,7 +720,7 @@ __device__ void zero_accu(C& c)
 
 // log_data (:1376-1466) at epoch start nir, after update_tracking_vars.
 template <class K, class C>
-__device__ void log_data(const K& k, const C& c, const float* taps, const float* pdata, uint64_t nir, gnsship_trk_dump_record* d)
+__device__ GNSSHIP_LOOP_INLINE void log_data(const K& k, const C& c, const float* taps, const float* pdata, uint64_t nir, gnsship_trk_dump_record* d)
 {
     if (!d) return;
     const int eo = k.veml ? 2 : 0;
@@ -771,7 +777,7 @@ __device__ __forceinline__ int next_mod(int i, int n)
 }
 
 template <class K, class C>
-__device__ double epoch_pre(const K& k, C& c, const float* taps, const float* pdata, gnsship_trk_epoch& rec, TrkHist* h,
+__device__ GNSSHIP_LOOP_INLINE double epoch_pre(const K& k, C& c, const float* taps, const float* pdata, gnsship_trk_epoch& rec, TrkHist* h,
     gnsship_trk_dump_record* dump)
 {
     const uint64_t nir = c.epoch_start;
@@ -864,7 +870,7 @@ __device__ __forceinline__ void epoch_loop(const K& k, C& c, TrkHist* h, const H
 // After epoch_pre returned a coherent time: the rest of state 2 / 4 given the lock outcome (epoch_loop
 // has run iff locked).
 template <class K, class C>
-__device__ void epoch_post(const K& k, C& c, const float* taps, const float* pdata, gnsship_trk_epoch& rec, bool locked,
+__device__ GNSSHIP_LOOP_INLINE void epoch_post(const K& k, C& c, const float* taps, const float* pdata, gnsship_trk_epoch& rec, bool locked,
     gnsship_trk_dump_record* dump)
 {
     const uint64_t nir = c.epoch_start;
@@ -936,7 +942,7 @@ __device__ __forceinline__ void epoch_consume(const K& k, C& c)
 // The record's loop outputs and consume_each (:2061); false when the channel stopped (loss of lock).
 // consume = false: the caller has already run epoch_consume (the fast kernel's early seed).
 template <class K, class C>
-__device__ bool epoch_finish(const K& k, C& c, gnsship_trk_epoch& rec, bool consume = true)
+__device__ GNSSHIP_LOOP_INLINE bool epoch_finish(const K& k, C& c, gnsship_trk_epoch& rec, bool consume = true)
 {
     if (c.pll_180) rec.flags |= 4;
     rec.code_phase_samples = c.rem_code_phase_samples;
@@ -977,7 +983,7 @@ __device__ __forceinline__ float corr_phase_step(const K& k, const C& c)
 }
 
 // The phases in the reference's order on one lane (the round-based step kernel).
-__device__ bool epoch_update(const TrkParams& k, TrkChannel& c, const float* taps, const float* pdata, gnsship_trk_epoch& rec, TrkHist* h,
+__device__ GNSSHIP_LOOP_INLINE bool epoch_update(const TrkParams& k, TrkChannel& c, const float* taps, const float* pdata, gnsship_trk_epoch& rec, TrkHist* h,
     gnsship_trk_dump_record* dump)
 {
     const double coh = epoch_pre(k, c, taps, pdata, rec, h, dump);

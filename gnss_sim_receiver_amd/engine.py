@@ -560,6 +560,12 @@ class DllPllVemlTracking:
         check(self.ctx.lib.gnsship_trk_trace_records(self.h, out.ctypes.data, out.size), "gnsship_trk_trace_records", self.ctx.h)
         return out
 
+    def last_engine(self) -> int:
+        """gnsship_trk_last_engine: the kernel the last run / launch ran (abi.TRK_ENGINE_*)."""
+        v = ctypes.c_int(0)
+        check(self.ctx.lib.gnsship_trk_last_engine(self.h, ctypes.byref(v)), "gnsship_trk_last_engine", self.ctx.h)
+        return v.value
+
     def states(self) -> np.ndarray:
         """Tracking state (0 idle/lost, 2, 3, 4) of every channel."""
         return np.array([self.channel_state(ch)[0] for ch in range(self.max_channels)], np.int32)

@@ -24,7 +24,8 @@ SLOTS = 80
 
 def main():
     n_ch = int(sys.argv[1]) if len(sys.argv) > 1 else 12
-    fs, vl = 4e6, 4000
+    fs = float(sys.argv[2]) if len(sys.argv) > 2 else 4e6
+    vl = int(round(fs / 1000))
     lib = abi.load()
     lib.gnsship_debug_trk_fast_profile.argtypes = [ctypes.c_void_p]
     ctx = engine.Context(0)
@@ -97,6 +98,16 @@ def main():
             if ok.any():
                 d = us(v[:, :, sl] - v[:, :, 1])[ok]
                 print(f"  derive -> group {g} {nm:22s} median {np.median(d):7.2f} us  p90 {np.percentile(d, 90):7.2f}  (n={ok.sum()})")
+    for nm, k in (("producer 0: ring waits", 41), ("producer 0: slot waits", 42), ("producer 0: whole production", 43),
+                  ("accumulator 0: flag waits", 44), ("accumulator 0: whole accumulation", 45), ("accumulator 1: flag waits", 46),
+                  ("accumulator 1: whole accumulation", 47)):
+        d = v[:, :, k]
+        d = d[d > 0]
+        if len(d):
+            print(f"  {nm:40s} median {np.median(d):8.0f} shader cycles ({np.median(d) / 2.4e3:6.2f} us at 2.4 GHz)")
+    vv = v[:, :, 78]
+    if np.any(vv > 0):
+        print(f"  speculative replay: {int(np.sum(vv == 1))} confirmed, {int(np.sum(vv == 2))} refuted of {int(np.sum(vv > 0))} epochs")
     roles = {0: "control", 1: "replay", 2: "producer"}
     for ch in range(min(n_ch, 4)):
         ids = [int(t[ch, 0, 72 + w]) for w in range(6)]

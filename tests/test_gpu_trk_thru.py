@@ -1,0 +1,66 @@
+"""The AVX tracking engine's throughput form — trk_fast_kernel with more channels than compute units
+(two workgroups per CU, trk_fast.hip fast_thru) — the kernel behind bench.py's
+tracked_channels_sustained.  It keeps u_avx's accumulation order (volk_gnsssdr_32fc_32f_rotator_dot_
+prod_32fc_xn.h:257-291) as the latency form does, so a sample of channels out of a 1024-channel run
+through the DEFAULT dispatch is held bit for bit to the oracle: every traced epoch's taps on the
+device's own arguments (trace_exact) and every record field against the oracle loop (compare_exact).
+
+Channels c take satellite c mod 32 of one sky (as the bench's sweep does); each channel starts at its
+own code-delay and Doppler offset, so channels sharing a satellite run different loops."""
+import concurrent.futures as cf
+
+import numpy as np
+import pytest
+
+from gnss_sim_receiver_amd import abi, engine, signals
+from oracle import trk as T
+
+from test_gpu_c5_closed_loop import trace_exact
+from test_gpu_trk import compare_exact, dev_conf
+
+pytestmark = pytest.mark.gpu
+
+
+def test_1024_avx_channels_default_dispatch_exact(ctx):
+    fs, vl, n_ch, epochs = 4e6, 4000, 1024, 700
+    sats = signals.random_sky(32, seed=0x6E550012)
+    for s in sats:
+        s.bits = "1000101100110"  # navigation bits with the preamble: the channels bit-synchronise (state 4)
+    k = T.conf("GPS", fs, vl, rotator_avx=1)
+    first = int(11 * fs)  # acquisition stamped at sample 0: the 10 s pull-in is over (bench.py's sweep)
+    x = signals.generate_if(fs, vl * (epochs + 4), sats, seed=0x6E550013, start=first)
+    trk = engine.DllPllVemlTracking(ctx, dev_conf(k, "GPS"), n_ch)
+    for i, s in enumerate(sats):
+        ctx.set_code(400 + i, s.code)
+    starts = []
+    for ch in range(n_ch):
+        s = sats[ch % 32]
+        lap = ch // 32  # 0..31: the start offsets of the channels that share satellite ch mod 32
+        delay = signals.acq_delay_samples(s, fs, 0, first) + 0.37 * ((lap * 7) % 5 - 2) / 2.0
+        dop = s.doppler_hz + 2.5 * ((lap * 11) % 9 - 4)
+        trk.start(ch, 400 + ch % 32, delay, dop, 0, first)
+        starts.append((delay, dop))
+    trk.set_trace(True)
+    rec, rounds = trk.run(x, first, epochs)
+    assert rounds == epochs
+    assert trk.last_engine() == abi.TRK_ENGINE_FAST_THROUGHPUT, abi.TRK_ENGINE_NAMES[trk.last_engine()]
+    tr = trk.trace(epochs)
+    states = trk.states()
+    trk.close()
+    xf = x.astype(np.complex64)
+    sample = [0, 33, 100, 257, 511, 700, 901, 1023]
+
+    def oracle(ch):
+        s = sats[ch % 32]
+        return T.track(k, xf, s.code, starts[ch][0], starts[ch][1], 0, first, epochs, buffer_first=first)
+
+    with cf.ThreadPoolExecutor(8) as ex:
+        refs = dict(zip(sample, ex.map(oracle, sample)))
+    n_traced = 0
+    for ch, ref in refs.items():
+        label = f"throughput form ch{ch}"
+        n_traced += trace_exact(tr[:, ch], xf, first, sats[ch % 32].code, None, label)
+        compare_exact(rec[:, ch], ref, label)
+        assert np.count_nonzero(ref["state"] == 4) > 0, (label, "the sampled channel never reached state 4")
+    assert n_traced >= 8 * 500
+    assert np.mean(states >= 2) >= 0.95, np.bincount(states)
