@@ -9,31 +9,37 @@
 // update_tracking_vars :1189-1260), which sets epoch k+1's NCO.  The rate at which one channel
 // advances is 1 / (epoch latency), so this kernel shortens the chain itself:
 //
-//  * wave 1 is the phasor wave: from the seed it derives glibc's cos/sin of the NCO phase and step
-//    (glibc_sincosf.h, two lanes), dz = normalise(inc^16) and the 16 AVX lane starts, then replays
-//    the 16 phasor chains (z ← z·dz, the reference's float products, two lanes per chain with a DPP
-//    partner product) and stores each chain's phasor at every task start (G iterations, 8 for GPS
-//    at 4 Msps) with a plain LDS store — no fence, no flag: the phasor slot itself is the signal
-//    (all-ones NaN = not yet written; a phasor is never NaN); then the N mod 16 tail's products;
-//  * waves 2 and 3 are the producers: groups of four tasks, lane (task, l) polls its slot, re-arms
-//    it, and continues chain l over the task's iterations with the same float products — every
-//    phasor bit-identical to u_avx's — forming at iteration m the sample product
-//    a = x[16m + l]·z_l(m) (_mm256_complexmul_ps rounding) and per tap the product a·code[tap]
-//    (_mm256_mul_ps), which it stores to an LDS product ring; a group's flag is set once its
-//    products have landed.  Wave 2 also runs the lock detectors (lock_status) beside wave 0's
-//    speculative loop update, kept only when the lock test passes, as the reference runs it;
-//  * wave 0 is the control wave and the accumulator.  Lane (l, r) keeps u_avx's accumulator of
-//    chain l for taps r and r + 4 and adds the products in iteration order (dotProdVal += c,
-//    :257-260) as the groups land, then combines the 16 chains exactly as u_avx does —
-//    ((d_k + d_{k+4}) + d_{k+8}) + d_{k+12}, then the four lanes serially from 0 (:279-291) — and
-//    the serial N mod 16 tail (:298-308): every tap bit-identical to the reference's.  The channel's
-//    loop state lives in its registers for the whole run (RChan, trk_loop.h); in state 4 it
-//    publishes the next epoch's correlator arguments (the seed) as soon as update_tracking_vars has
-//    set them — before the lock test's outcome, which a failed test cancels (the channel stops) —
-//    and only then finishes this epoch and writes its records (other states: after epoch_post).
+//  * the phasor wave: from the seed (or, in state 4, speculatively from the loop's early values,
+//    confirmed by the seed) it derives glibc's cos/sin of the NCO phase and step (glibc_sincosf.h),
+//    dz = normalise(inc^16) and the 16 AVX lane starts, then replays the 16 phasor chains (z ← z·dz,
+//    the reference's float products, two lanes per chain with a DPP partner product; one asm block
+//    per 64-iteration block) and stores each chain's phasor at every task start (G = 8 iterations)
+//    with a plain LDS store — no fence, no flag: the slot itself is the signal (all-ones NaN = not
+//    yet written); then the N mod 16 tail's products;
+//  * the producer waves: groups of four tasks, lane (task, chain) polls its slot and continues chain l
+//    over the task's iterations with the same float products — every phasor bit-identical to
+//    u_avx's — forming at iteration m the sample product a = x[16m + l]·z_l(m) (_mm256_complexmul_ps
+//    rounding) and per tap a·code[tap] (_mm256_mul_ps); four iterations of one product slot (2·tap +
+//    component) go to the product ring as one 16-byte store, slot-major (ProdLayout); a group's flag
+//    is set once its products have landed.  Producer 0 also runs the lock detectors (lock_status)
+//    beside the control wave's speculative loop update, kept only when the lock test passes;
+//  * the accumulator waves (one per four product slots): lane (slot row, chain l) keeps u_avx's
+//    accumulator of chain l for ONE slot and adds its products in iteration order (dotProdVal +=
+//    c, :257-260), four per 16-byte load, as the groups land (the group's flag and loads in one
+//    batch); then combines the 16 chains exactly as u_avx does — ((d_k + d_{k+4}) + d_{k+8}) +
+//    d_{k+12}, then the four lanes serially from 0 (:279-291) — and adds the serial N mod 16 tail
+//    (:298-308): every tap bit-identical to the reference's;
+//  * the control wave: the channel's loop state in its registers for the whole run (RChan,
+//    trk_loop.h); epoch_pre → run_dll_pll (publishing the next carrier step for the phasor wave
+//    right after the carrier filter) → update_tracking_vars; in state 4 it publishes the next epoch's
+//    correlator arguments (the seed) before the lock test's outcome — which a failed test cancels (the
+//    channel stops) — and only then finishes this epoch and writes its records.
+// Roles go by SIMD (the phasor wave with accumulator 0, the control wave with accumulator 1, the
+// producers in pairs, numbered round-robin over their SIMDs); the throughput form (more channels than
+// CUs) runs the same roles with fewer producers, two workgroups per CU.
 //
-// Epochs too long for the LDS rings, the generic rotator, high_dyn and runs of more channels than
-// CUs stay on trk_persist.hip / the round-based loop.
+// Epochs too long for the LDS rings, the generic rotator and high_dyn stay on trk_persist.hip / the
+// round-based loop.
 #include <algorithm>
 #include <cstdlib>
 
@@ -128,6 +134,9 @@ constexpr int kLongEpoch = 10000;  // samples per epoch from which the long-epoc
 // The accumulation's waves: one per four product slots (2·taps, the data prompt included: GPS and
 // B1I 6 slots → 2 waves, the E1 engine's 12 → 3), so that each lane adds ONE slot per iteration —
 // a single serial chain per lane, and room for two groups' loads in flight (fast_accumulate).
+#ifndef GNSSHIP_PROD_SPLIT  // A/B: two producers per product group (fast_produce; measured slower)
+#define GNSSHIP_PROD_SPLIT 0
+#endif
 #ifndef GNSSHIP_ACC_PIPE  // A/B: the accumulator loads the next group behind the current one's adds (measured slower)
 #define GNSSHIP_ACC_PIPE 0
 #endif
@@ -361,20 +370,39 @@ __device__ __forceinline__ float pstep(float x, float c, float k2, uint32_t lds_
 // as ONE asm block.  The hazard recognizer pads every inline-asm boundary with an s_nop and the
 // slot address would be re-derived per task otherwise; here one address serves the block.
 #define GNSSHIP_PS(A, B) GNSSHIP_PSTEP("%[" #A "]", "%[" #B "]")
-#define GNSSHIP_TASK8(A, B, OFF)                                                                                           \
-    GNSSHIP_PS(A, B) "ds_write_b32 %[p], %[" #A "] offset:" #OFF "\n\t" GNSSHIP_PS(B, A) GNSSHIP_PS(A, B) GNSSHIP_PS(B, A) \
-        GNSSHIP_PS(A, B) GNSSHIP_PS(B, A) GNSSHIP_PS(A, B) GNSSHIP_PS(B, A)
-__device__ __forceinline__ float pblock64_g8(float x, float c, float k2, uint32_t lds_off)
+// A/B (GNSSHIP_SLOT_ADDTID=1; measured equal, 638.3 vs 637.6 Msps): the task stores as
+// ds_write_addtid_b32 (address M0 + offset + 4·lane: no address VGPR, half the store path of
+// ds_write_b32) with M0 = the block's slot row in LDS (`m0v`, < 64 KiB: the slots sit at the front of
+// the dynamic LDS).  Default: ds_write_b32.
+#ifndef GNSSHIP_SLOT_ADDTID
+#define GNSSHIP_SLOT_ADDTID 0
+#endif
+#if GNSSHIP_SLOT_ADDTID
+#define GNSSHIP_TST(A, OFF) "ds_write_addtid_b32 %[" #A "] offset:" #OFF "\n\t"
+#define GNSSHIP_M0SET "s_mov_b32 m0, %[m0v]\n\t"
+#else
+#define GNSSHIP_TST(A, OFF) "ds_write_b32 %[p], %[" #A "] offset:" #OFF "\n\t"
+#define GNSSHIP_M0SET ""
+#endif
+#define GNSSHIP_TASK8(A, B, OFF)                                                                                            \
+    GNSSHIP_PS(A, B) GNSSHIP_TST(A, OFF) GNSSHIP_PS(B, A) GNSSHIP_PS(A, B) GNSSHIP_PS(B, A) GNSSHIP_PS(A, B) GNSSHIP_PS(B, A) \
+        GNSSHIP_PS(A, B) GNSSHIP_PS(B, A)
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"  // m0: reserved to the compiler, which uses it nowhere in this kernel (checked in the ISA)
+__device__ __forceinline__ float pblock64_g8(float x, float c, float k2, uint32_t lds_off, uint32_t m0v)
 {
     float t, u, w;
-    asm volatile(GNSSHIP_PS(x, w) GNSSHIP_PS(w, x) GNSSHIP_PS(x, w) GNSSHIP_PS(w, x) GNSSHIP_PS(x, w) GNSSHIP_PS(w, x) GNSSHIP_PS(x, w)
-                     GNSSHIP_TASK8(w, x, 128) GNSSHIP_TASK8(w, x, 256) GNSSHIP_TASK8(w, x, 384) GNSSHIP_TASK8(w, x, 512)
+    asm volatile(GNSSHIP_M0SET GNSSHIP_PS(x, w) GNSSHIP_PS(w, x) GNSSHIP_PS(x, w) GNSSHIP_PS(w, x) GNSSHIP_PS(x, w) GNSSHIP_PS(w, x)
+                     GNSSHIP_PS(x, w) GNSSHIP_TASK8(w, x, 128) GNSSHIP_TASK8(w, x, 256) GNSSHIP_TASK8(w, x, 384) GNSSHIP_TASK8(w, x, 512)
                          GNSSHIP_TASK8(w, x, 640) GNSSHIP_TASK8(w, x, 768) GNSSHIP_TASK8(w, x, 896) "v_mov_b32 %[x], %[w]\n\t"
                  : [x] "+v"(x), [t] "=&v"(t), [u] "=&v"(u), [w] "=&v"(w)
-                 : [c] "s"(c), [k2] "v"(k2), [p] "v"(lds_off)
-                 : "memory");
+                 : [c] "s"(c), [k2] "v"(k2), [p] "v"(lds_off), [m0v] "s"(m0v)
+                 : "memory", "m0");
     return x;
 }
+#pragma clang diagnostic pop
+#undef GNSSHIP_TST
+#undef GNSSHIP_M0SET
 #undef GNSSHIP_TASK8
 #undef GNSSHIP_PS
 // x·dz^N: N ≥ 0 iterations
@@ -420,7 +448,7 @@ __device__ __forceinline__ float fast_replay(float x, float c, float k2, int M, 
         for (int b = 0; b < full; b++) {
             if constexpr (G == 8 && kSlotRow == 128) {
                 // the block's first iteration normalises; the other 63 run in one asm block
-                x = pblock64_g8(pnormalise(pstep<1, true>(x, c, k2, off)), c, k2, off);
+                x = pblock64_g8(pnormalise(pstep<1, true>(x, c, k2, off)), c, k2, off, __builtin_amdgcn_readfirstlane(off - 4u * lane));
                 off += kTB * kSlotRow;
             } else {
 #pragma unroll
@@ -468,7 +496,7 @@ __device__ __forceinline__ float fast_replay(float x, float c, float k2, int M, 
                         }
                     }
                     off = base + static_cast<uint32_t>(ts0) * kSlotRow;
-                    x = pblock64_g8(pnormalise(pstep<1, true>(x, c, k2, off)), c, k2, off);
+                    x = pblock64_g8(pnormalise(pstep<1, true>(x, c, k2, off)), c, k2, off, __builtin_amdgcn_readfirstlane(off - 4u * lane));
                 }
             }
         }
@@ -585,6 +613,12 @@ struct ProdLayout {
 // Ring group r (of rg) holds one group of 4 tasks = 4G iterations: the products of every iteration of
 // the group, chain, tap and component (ProdLayout).  Group tags count over the run (gbase = epoch ·
 // n_groups): no flag is re-armed.  A ring group is reused once every accumulator wave consumed it.
+// Producers per group: two when there is an even number of producers (each takes half of every task's
+// iterations — the second half's lanes first advance their chain G/2 steps from the slot), so the
+// latency from a group's last slot to its products halves; otherwise one.
+template <int NTT, int W, int G>
+constexpr int producers_per_group() { return (GNSSHIP_PROD_SPLIT && n_producers<NTT, W>() % 2 == 0 && G == 8) ? 2 : 1; }
+
 template <int FMT, int NT, bool DATA, bool IN_MARGIN, int G, int W>
 __device__ __forceinline__ void fast_produce(const FJob& job, i4v span, const float* __restrict__ code0, const float* __restrict__ code1, int L,
     uint64_t* __restrict__ Zs, int rs, float* __restrict__ Pp, int rg, int32_t* ready, const int32_t* acc_groups, int gbase, int lane, int pw, int pe)
@@ -593,8 +627,11 @@ __device__ __forceinline__ void fast_produce(const FJob& job, i4v span, const fl
     constexpr int NTT = NT + (DATA ? 1 : 0);
     constexpr int NP = n_producers<NTT, W>();
     constexpr int NA = acc_waves<NTT>();
+    constexpr int NH = producers_per_group<NTT, W, G>();
+    constexpr int GH = G / NH;  // iterations of each task this wave produces
+    constexpr int NG = NP / NH; // groups in production at once
     using PL = ProdLayout<NTT, G>;
-    constexpr int kB = G < 8 ? G : 8;  // iterations whose samples are in flight together
+    constexpr int kB = GH < 8 ? GH : 8;  // iterations whose samples are in flight together
     const int M = job.M, S = job.S;
     const int n_groups = (S + 3) / 4;
     const f2 dz = f2{job.dz_re, job.dz_im};
@@ -603,30 +640,32 @@ __device__ __forceinline__ void fast_produce(const FJob& job, i4v span, const fl
 #pragma unroll
     for (int q = 0; q < NT; q++) shifts[q] = job.shifts[q];
     const int tl = lane >> 4, l = lane & (kAvxLanes - 1);
+    const int h = NH == 2 ? (pw & 1) : 0, pp = NH == 2 ? (pw >> 1) : pw;
     auto first_samples = [&](int g, f2 (&x)[kB]) {
         const int t = 4 * g + tl;
-        const int n0 = kAvxLanes * G * (t < S ? t : 0) + l;
+        const int n0 = kAvxLanes * (G * (t < S ? t : 0) + GH * h) + l;
 #pragma unroll
         for (int u = 0; u < kB; u++) x[u] = load_sample<FMT>(span, (n0 + kAvxLanes * u) * SB, 0);
     };
     f2 xa[kB], xb[kB];
-    float cv[G][NTT];
-    int rslot = pw % rg;
-    const int rstep = NP % rg;
+    float cv[GH][NTT];
+    int rslot = pp % rg;
+    const int rstep = NG % rg;
     unsigned long long w_ring = 0, w_slot = 0;  // profiling: cycles waiting for ring space / phasor slots
     const unsigned long long t_run = GNSSHIP_FCLOCK();
-    for (int g = pw; g < n_groups; g += NP) {
+    for (int g = pp; g < n_groups; g += NG) {
         const int t = 4 * g + tl;
         const bool active = t < S;
         const int m_lo = G * (active ? t : 0);
         const int cnt = active ? min(G, M - m_lo) : 0;
-        const int n0 = kAvxLanes * m_lo + l;
+        const int cnth = max(0, min(GH, cnt - GH * h));  // this wave's iterations of the task within the epoch
+        const int n0 = kAvxLanes * (m_lo + GH * h) + l;
         const bool full = 4 * g + 4 <= S && G * (4 * g + 4) <= M;  // every task of the group whole
         first_samples(g, xa);  // in flight during phase A and the slot poll
         if (full)
-            group_codes<NT, DATA, IN_MARGIN, G, true>(code0, code1, L, n0, G, step, rem, shifts, cv);
+            group_codes<NT, DATA, IN_MARGIN, GH, true>(code0, code1, L, n0, GH, step, rem, shifts, cv);
         else
-            group_codes<NT, DATA, IN_MARGIN, G, false>(code0, code1, L, n0, cnt, step, rem, shifts, cv);
+            group_codes<NT, DATA, IN_MARGIN, GH, false>(code0, code1, L, n0, cnth, step, rem, shifts, cv);
         // the ring group is free once every accumulator wave consumed its previous occupant — and in
         // the slot ring (rg ≤ 16 groups of its 64 tasks) that also means the slot this lane polls next
         // was consumed on its previous lap (whichever producer took it)
@@ -641,29 +680,38 @@ __device__ __forceinline__ void fast_produce(const FJob& job, i4v span, const fl
         uint64_t* slot = Zs + ts * kAvxLanes + l;
         uint64_t v = kSlotEmpty;
         if (active) {
-            // written when neither 32-bit half is the sentinel any more (two replay lanes write it)
+            // written when neither 32-bit half is the sentinel any more (two replay lanes write it);
+            // with two producers per group the accumulator re-arms it once both have read it
             while (static_cast<uint32_t>(v = load_slot(slot)) == ~0u || static_cast<uint32_t>(v >> 32) == ~0u) __builtin_amdgcn_s_sleep(GNSSHIP_POLL_SLEEP);
-            store_slot(slot, __builtin_bit_cast(f2, kSlotEmpty));  // re-armed for the next lap / epoch
+            if (NH == 1) store_slot(slot, __builtin_bit_cast(f2, kSlotEmpty));  // re-armed for the next lap / epoch
         }
         w_slot += GNSSHIP_FCLOCK() - t1;
-        if (g == pw && pw == 0) GNSSHIP_FSTAMP(pe, 30);
-        if (g + NP >= n_groups && pw == 1) GNSSHIP_FSTAMP(pe, 31);
+        if (g == pp && pw == 0) GNSSHIP_FSTAMP(pe, 30);
+        if (g + NG >= n_groups && pw == 1) GNSSHIP_FSTAMP(pe, 31);
 #ifdef GNSSHIP_EXP_SERIAL
         while (__hip_atomic_load(&g_replay_done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < pe + 1) __builtin_amdgcn_s_sleep(1);
 #endif
-        const f2 z = active ? __builtin_bit_cast(f2, v) : f2{0.0f, 0.0f};
+        f2 z = active ? __builtin_bit_cast(f2, v) : f2{0.0f, 0.0f};
         const bool renorm = ((G * t) & 63) == 0;
-        float* pdst = Pp + static_cast<size_t>(rslot) * PL::kGroup + l * PL::kRow + G * tl;
+        if (NH == 2 && h == 1) {  // the task's first half: the chain's own steps (renormalised after the first)
+#pragma unroll
+            for (int i = 0; i < GH; i++) {
+                f2 zn = cmul_exact_s(z, dz);
+                if (i == 0 && renorm) zn = normalise_avx(zn);
+                z = zn;
+            }
+        }
+        float* pdst = Pp + static_cast<size_t>(rslot) * PL::kGroup + l * PL::kRow + G * tl + GH * h;
 #ifndef GNSSHIP_EXP_NOPROD  // timing experiment: the producers only follow the slots and set the flags
         if (full)
-            group_phasors<FMT, NTT, G, true, PL>(span, z, dz, renorm, n0, G, pdst, cv, xa, xb);
+            group_phasors<FMT, NTT, GH, true, PL>(span, z, dz, renorm && h == 0, n0, GH, pdst, cv, xa, xb);
         else
-            group_phasors<FMT, NTT, G, false, PL>(span, z, dz, renorm, n0, cnt, pdst, cv, xa, xb);
+            group_phasors<FMT, NTT, GH, false, PL>(span, z, dz, renorm && h == 0, n0, cnth, pdst, cv, xa, xb);
 #else
         if (z.x == 12345.0f) pdst[0] = cv[0][0];
 #endif
         GNSSHIP_PROBE(GNSSHIP_DELAY_PROD);
-        if (lane == 0) lds_release_store(ready + rslot, gbase + g + 1);
+        if (lane == 0) lds_release_store(ready + 2 * rslot + h, gbase + g + 1);
         if (g < 8) GNSSHIP_FSTAMP(pe, 48 + g);
         rslot += rstep;
         if (rslot >= rg) rslot -= rg;
@@ -686,10 +734,11 @@ constexpr int acc_slots() { return (2 * NTT + 4 * acc_waves<NTT>() - 1) / (4 * a
 template <int NTT>
 __device__ __forceinline__ int acc_slot(int a, int r, int k) { return 4 * (a + acc_waves<NTT>() * k) + r; }
 
-template <int NTT, int G>
+template <int NTT, int G, int W>
 __device__ __forceinline__ void fast_accumulate(const float* __restrict__ Pp, int rg, const int32_t* ready, int32_t* acc_done, int gbase, int S,
-    int lane, int a, float (&acc)[acc_slots<NTT>()], int pe)
+    int lane, int a, float (&acc)[acc_slots<NTT>()], int pe, uint64_t* __restrict__ Zs, int rs)
 {
+    constexpr int NH = producers_per_group<NTT, W, G>();
     using PL = ProdLayout<NTT, G>;
     constexpr int NS = acc_slots<NTT>();
     constexpr int kQ = PL::kJ / 4;  // four-iteration loads per slot and group
@@ -714,8 +763,14 @@ __device__ __forceinline__ void fast_accumulate(const float* __restrict__ Pp, in
 #pragma unroll
             for (int k = 0; k < NS; k++) v[q][k] = *reinterpret_cast<const f4*>(src + off[k] + 4 * q);
     };
-    auto wait_group = [&](int g, int rs) __attribute__((always_inline)) {
-        lds_wait_eq(ready + rs, gbase + g + 1);
+    auto wait_group = [&](int g, int rsl) __attribute__((always_inline)) {
+        lds_wait_eq(ready + 2 * rsl, gbase + g + 1);
+        if (NH == 2) {
+            lds_wait_eq(ready + 2 * rsl + 1, gbase + g + 1);
+            // both producers of the group have read its phasor slots: accumulator 0 re-arms them
+            const int t = 4 * g + (lane >> 4);
+            if (a == 0 && t < S) store_slot(Zs + (t % rs) * kAvxLanes + (lane & (kAvxLanes - 1)), __builtin_bit_cast(f2, kSlotEmpty));
+        }
         asm volatile("" ::: "memory");  // the group's loads follow the flag
     };
     // group g from registers `cur` (its loads issued); group g + 1 into `nxt`.  Returns whether
@@ -730,7 +785,7 @@ __device__ __forceinline__ void fast_accumulate(const float* __restrict__ Pp, in
         if (g < 8) GNSSHIP_FSTAMP(pe, 56 + g);
         const int rn = rs + 1 == rg ? 0 : rs + 1;
         bool next = false;
-        if (g + 1 < n_groups && __hip_atomic_load(ready + rn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == gbase + g + 2) {
+        if (NH == 1 && g + 1 < n_groups && __hip_atomic_load(ready + 2 * rn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == gbase + g + 2) {
             asm volatile("" ::: "memory");
             load_group(rn, nxt);
             next = true;
@@ -768,12 +823,13 @@ __device__ __forceinline__ void fast_accumulate(const float* __restrict__ Pp, in
     const unsigned long long t_run = GNSSHIP_FCLOCK();
     for (int g = 0; g < n_groups; g++) {
         const unsigned long long t0 = GNSSHIP_FCLOCK();
+        f4 v[kQ][NS];
         wait_group(g, rslot);
+        load_group(rslot, v);
+
         w_flag += GNSSHIP_FCLOCK() - t0;
         if (g == 0) GNSSHIP_FSTAMP(pe, 28);
         if (g == n_groups - 1) GNSSHIP_FSTAMP(pe, 29);
-        f4 v[kQ][NS];
-        load_group(rslot, v);
 #pragma unroll
         for (int q = 0; q < kQ; q++)
 #pragma unroll
@@ -932,15 +988,15 @@ __global__ __launch_bounds__(W * kWave, (fast_waves_per_simd<THRU, W>())) void t
         int* dst = reinterpret_cast<int*>(&sc);
         for (int i = tid; i < static_cast<int>(sizeof(TrkChannel) / 4); i += kFThreads) dst[i] = src[i];
     }
-    // dynamic LDS: code replica(s) | phasor slots (rs tasks) | ring: sample products (rg groups) |
+    // dynamic LDS: phasor slots (rs tasks) | code replica(s) | ring: sample products (rg groups) |
     // ring: code values | ring flags
-    float* code0 = lds;
-    float* code1 = lds + code_cap_floats;
-    uint64_t* Zs = reinterpret_cast<uint64_t*>(lds + (DATA ? 2 : 1) * code_cap_floats);
-    float* Pp = reinterpret_cast<float*>(Zs + static_cast<size_t>(rs) * kAvxLanes);
+    uint64_t* Zs = reinterpret_cast<uint64_t*>(lds);  // first: the replay's slot stores address it through M0[15:0]
+    float* code0 = reinterpret_cast<float*>(Zs + static_cast<size_t>(rs) * kAvxLanes);
+    float* code1 = code0 + code_cap_floats;
+    float* Pp = code0 + (DATA ? 2 : 1) * code_cap_floats;
     int32_t* ready = reinterpret_cast<int32_t*>(Pp + static_cast<size_t>(rg) * ProdLayout<NTT, G>::kGroup);
     for (int i = tid; i < rs * kAvxLanes; i += kFThreads) Zs[i] = kSlotEmpty;
-    for (int i = tid; i < rg; i += kFThreads) ready[i] = 0;
+    for (int i = tid; i < 2 * rg; i += kFThreads) ready[i] = 0;
     __shared__ int32_t simd_of[kFWaves];
     if (lane == 0) simd_of[wave] = static_cast<int32_t>((__builtin_amdgcn_s_getreg(4 | (31 << 11)) >> 4) & 3);  // HW_ID.SIMD_ID
 #ifdef GNSSHIP_CORR_PROFILE
@@ -1043,6 +1099,8 @@ __global__ __launch_bounds__(W * kWave, (fast_waves_per_simd<THRU, W>())) void t
         role = __builtin_amdgcn_readfirstlane(role);
         pw = __builtin_amdgcn_readfirstlane(pw);
     }
+    __shared__ int32_t role_of[kFWaves];
+    if (lane == 0) role_of[wave] = role;
     if (tid == 0) {
         const bool tracking = sc.state == 2 || sc.state == 3 || sc.state == 4;
         const bool codes_ok = sc.code_id >= 0 && sc.code_id < n_codes && codes[sc.code_id].ptr && codes[sc.code_id].len > 0 &&
@@ -1065,6 +1123,23 @@ __global__ __launch_bounds__(W * kWave, (fast_waves_per_simd<THRU, W>())) void t
     }
     __syncthreads();
     if (skip) return;  // idle channel: its state is untouched
+    if (role == kRoleProducer) {
+        // producers numbered round-robin over their SIMDs (rank within the SIMD first), so that the
+        // producers of consecutive groups — the epoch's last two above all — sit on different SIMDs
+        auto rank_in_simd = [&](int w) {
+            int r = 0;
+            for (int v = 0; v < w; v++) r += (role_of[v] == kRoleProducer && (simd_of[v] & 3) == (simd_of[w] & 3)) ? 1 : 0;
+            return r;
+        };
+        const int rk = rank_in_simd(wave), sd = simd_of[wave] & 3;
+        int idx = 0;
+        for (int v = 0; v < kFWaves; v++) {
+            if (v == wave || role_of[v] != kRoleProducer) continue;
+            const int rv = rank_in_simd(v), sv = simd_of[v] & 3;
+            idx += (rv < rk || (rv == rk && sv < sd)) ? 1 : 0;
+        }
+        pw = __builtin_amdgcn_readfirstlane(idx);
+    }
     if (wave < 4) GNSSHIP_FHWID(20 + wave);  // epoch 0's slots 20-23 (the epoch loop stamps 0-15)
 #ifdef GNSSHIP_CORR_PROFILE
     if (g_trkf_prof && lane == 0)  // row 0's slots 72-77: HW_ID | role << 32 of every wave
@@ -1099,15 +1174,9 @@ __global__ __launch_bounds__(W * kWave, (fast_waves_per_simd<THRU, W>())) void t
         __syncthreads();
     }
     const auto& kp = loop_params<THRU>(k, kf);
-    // Wave roles (one channel per workgroup, its epochs a serial chain):
-    //   control  — the accumulation in u_avx order, the loop update on its register-resident
-    //              channel (RChan) and the epoch records;
-    //   phasor   — derives the epoch's phasors (cos/sin of the NCO phase and step, dz, the 16 lane
-    //              starts) and replays them into the task slots, plus the N mod 16 tail;
-    //   producers — the products of the groups pw, pw + kFProducers, ...; producer 0 also runs the
-    //              lock detectors.
-    // Wave 0 hands the next epoch's NCO arguments (the seed) to wave 1 as soon as epoch_post has
-    // settled them, so the derive and the first tasks of epoch e + 1 overlap epoch e's record writes.
+    // Wave roles (one channel per workgroup, its epochs a serial chain): see the file header.  The
+    // control wave hands the next epoch's NCO arguments (the seed) to the phasor wave as soon as they
+    // are settled, so the derive and the first tasks of epoch e + 1 overlap epoch e's record writes.
     uint64_t seed_start = 0;              // wave 0: the epoch start the seed was made for
     // wave 0: the seed's per-run constants, read once (inside the epoch loop each TrkParams member is a
     // dependent scalar load on the chain)
@@ -1358,7 +1427,7 @@ __global__ __launch_bounds__(W * kWave, (fast_waves_per_simd<THRU, W>())) void t
                 constexpr int NS = acc_slots<NTT>();
                 float acc[NS];
                 GNSSHIP_FSTAMP(e, 27);
-                fast_accumulate<NTT, G>(Pp, rg, ready, &sh.acc_groups[pw], gbase, S, lane, pw, acc, e);
+                fast_accumulate<NTT, G, kFWaves>(Pp, rg, ready, &sh.acc_groups[pw], gbase, S, lane, pw, acc, e, Zs, rs);
                 GNSSHIP_FSTAMP(e, 5);
                 const int r = lane >> 4;
     #pragma unroll
@@ -1585,6 +1654,7 @@ struct FastPlan {
 constexpr int kFastG = GNSSHIP_FAST_G;
 constexpr int kFastSlotRingGroups = 16;
 constexpr int kFastMinRingGroups = 4;
+constexpr size_t kFastMaxSlotBytes = 48 * 1024;
 static FastPlan fast_plan(const TrkParams& p, int code_cap_floats, int n_chans)
 {
     FastPlan f;
@@ -1598,7 +1668,7 @@ static FastPlan fast_plan(const TrkParams& p, int code_cap_floats, int n_chans)
     const size_t slot_b = kAvxLanes * sizeof(uint64_t);
     // a group's products (ProdLayout: 4 tasks of G iterations × 2·ntt slots × 16 chains, each task
     // padded by 16 floats) and its flag
-    const size_t group_b = static_cast<size_t>(2 * ntt) * kAvxLanes * (4 * G + 4) * sizeof(float) + sizeof(int32_t);  // ProdLayout + flag
+    const size_t group_b = static_cast<size_t>(2 * ntt) * kAvxLanes * (4 * G + 4) * sizeof(float) + 2 * sizeof(int32_t);  // ProdLayout + flags
     // more channels than CUs: two workgroups per CU share its LDS
     size_t budget = fast_thru(n_chans) ? 72 * 1024 : kTrkPersistMaxLds;
     if (const char* env = std::getenv("GNSSHIP_TRK_FAST_LDS"))  // tests: a smaller budget forces the rings
@@ -1609,7 +1679,9 @@ static FastPlan fast_plan(const TrkParams& p, int code_cap_floats, int n_chans)
         const int rg = static_cast<int>(std::min<size_t>((budget - used) / group_b, static_cast<size_t>(n_groups)));
         return rg >= std::min(2, n_groups) ? rg : 0;
     };
-    int rs = S, rg = fit(S);
+    // whole-epoch slots only while they stay within the first 48 KiB of LDS (the replay's slot stores
+    // address them through M0[15:0], beside the static LDS)
+    int rs = S, rg = static_cast<size_t>(S) * slot_b <= kFastMaxSlotBytes ? fit(S) : 0;
     // the slot ring must hold at least 4 tasks per product group (a producer passed the ring's
     // back-pressure before it polls a slot, so the slot's previous lap is consumed).  It is used only
     // when the whole epoch's slots leave fewer than kFastMinRingGroups product groups: with every

@@ -79,14 +79,18 @@ def check_trace(tr, xf, first, codes, data_code=None):
     return jobs
 
 
-def trace_errors(tr, xf, first, code, data_code, rotator_avx):
+def trace_errors(tr, xf, first, code, data_code, rotator_avx, long_n=None):
+    """Worst per-tap relative error of the traced taps against the oracle correlator on the device's
+    own arguments.  long_n (default: N ≥ 1e5) compares with the oracle's float products summed in
+    double, scaled by max(|ref|, ‖x‖₂); otherwise with the reference's serial float sum, scaled by |ref|."""
     from gnss_sim_receiver_amd import abi as A
     from oracle import oracle as O
     tr = tr[tr["n_samples"] > 0]
     jobs = check_trace(tr, xf, first, [code])
     jobs["code_id"] = 0
     jobs["flags"] = A.JOB_ROTATOR_AVX if rotator_avx else 0
-    long_n = int(jobs["n_samples"][0]) >= 50000
+    if long_n is None:
+        long_n = int(jobs["n_samples"][0]) >= 100000
     ref = O.corr_batch(xf, jobs, [code], n_threads=8, accum_f64=long_n)
     worst = 0.0
     for j in range(len(jobs)):
@@ -136,6 +140,11 @@ def trace_exact(tr, xf, first, code, data_code, label=""):
 
 FS = 50e6
 F_IF = 7.161e6
+# The generic rotator's tree-summed taps against the reference's serial float sum at C5's N (one float
+# accumulator per tap, N = 50000 for GPS / B1I, 200000 for E1): the serial sum's own rounding walk
+# (√N half-ulps of the accumulator) is ~1e-5 of the taps there, so the tree, which is closer to the
+# exact sum, lands up to the measured figures below from it (DESIGN §4 lists them).  1e-5 where met.
+GENERIC_SERIAL = {"GPS": 1e-5, "GAL": 2.2e-5, "BDS": 1.2e-5}  # measured 9.17e-6, 2.058e-5, 1.092e-5 (round 5)
 IF_OF = {"GPS": F_IF, "GAL": F_IF, "BDS": -F_IF}
 
 
@@ -163,8 +172,15 @@ def test_c5_channel_closed_loop_ibyte_if(ctx, system, epochs, avx):
     if avx:  # bit-exact: the taps on the device's own arguments, then the loop
         trace_exact(tr, xf, first, sat.code, sat.code_data, f"C5 {system}")
         compare_exact(rec[:, 0], ref, f"C5 {system} avx")
-    else:  # the correlations on the device's own arguments at the 1e-5 contract, the loop at compare_if
-        assert trace_errors(tr, xf, first, sat.code, sat.code_data, avx) <= TOL
+    else:
+        # the generic engine's tree sums against the reference's serial float sum (the plain oracle) —
+        # held to 1e-5 where they meet it and to the measured excess where they do not (GENERIC_SERIAL,
+        # DESIGN §4) — and to 1e-5 against the exact sum of the same float products (double accumulation)
+        e_serial = trace_errors(tr, xf, first, sat.code, sat.code_data, avx, long_n=False)
+        e_exact = trace_errors(tr, xf, first, sat.code, sat.code_data, avx, long_n=True)
+        print(f"C5 {system} generic: max per-tap error {e_serial:.3e} vs the serial float sum, {e_exact:.3e} vs the exact sum")
+        assert e_serial <= GENERIC_SERIAL[system], (system, e_serial)
+        assert e_exact <= TOL, (system, e_exact)
         compare_if(rec[:, 0], ref, f"C5 {system} generic")
     # the IF is wiped off: the loop holds the signal's Doppler (± the narrow-loop walk), not Doppler + IF
     assert np.all(np.abs(ref[-20:]["carrier_doppler_hz"] - sat.doppler_hz) < 200.0)
