@@ -51,7 +51,7 @@ namespace gnsship {
 namespace {
 constexpr int kFProfEpochs = 16;  // profiled epochs kFProfFirst .. kFProfFirst + 15, stamped into LDS
 constexpr int kFProfFirst = 8;
-constexpr int kFProfSlots = 80;
+constexpr int kFProfSlots = 88;
 __device__ unsigned long long* g_trkf_prof = nullptr;
 __shared__ int g_fprof_epoch;
 // stamps go to LDS and out to g_trkf_prof when the kernel ends: a global store per stamp would put
@@ -136,6 +136,12 @@ constexpr int kLongEpoch = 10000;  // samples per epoch from which the long-epoc
 // a single serial chain per lane, and room for two groups' loads in flight (fast_accumulate).
 #ifndef GNSSHIP_PROD_SPLIT  // A/B: two producers per product group (fast_produce; measured slower)
 #define GNSSHIP_PROD_SPLIT 0
+#endif
+#ifndef GNSSHIP_ACC_PAIRS  // A/B: the accumulator takes two ready groups per round trip (measured slower)
+#define GNSSHIP_ACC_PAIRS 0
+#endif
+#ifndef GNSSHIP_SAMPLE_CMUL_SCALAR  // A/B: the sample product a = x·z as six scalar ops instead of three packed
+#define GNSSHIP_SAMPLE_CMUL_SCALAR 0
 #endif
 #ifndef GNSSHIP_ACC_PIPE  // A/B: the accumulator loads the next group behind the current one's adds (measured slower)
 #define GNSSHIP_ACC_PIPE 0
@@ -540,9 +546,15 @@ __device__ __forceinline__ void group_codes(const float* __restrict__ code0, con
     for (int i = 0; i < G; i++) {
         const bool on = FULL || i < cnt;
         const float sn = __fmul_rn(step, on ? fn : fn0);
+#ifdef GNSSHIP_EXP_NOCODES  // timing experiment only (wrong taps): no code lookups
+#pragma unroll
+        for (int q = 0; q < NT; q++) cv[i][q] = (q & 1) ? sn : 1.0f;
+        if constexpr (DATA) cv[i][NT] = 1.0f;
+#else
 #pragma unroll
         for (int q = 0; q < NT; q++) cv[i][q] = code_at<IN_MARGIN>(code0, L, sn, shifts[q], rem);
         if constexpr (DATA) cv[i][NT] = code_at<IN_MARGIN>(code1, L, sn, 0.0f, rem);
+#endif
         fn += static_cast<float>(kAvxLanes);
     }
 }
@@ -574,7 +586,11 @@ __device__ __forceinline__ void group_phasors(i4v span, f2 z, f2 dz, bool renorm
             for (int u = 0; u < 4; u++) {
                 const int i = i0 + h + u;
                 const bool on = FULL || i < cnt;
+#if GNSSHIP_SAMPLE_CMUL_SCALAR
+                const f2 a = cmul_exact_sc(xa[h + u], z);
+#else
                 const f2 a = cmul_exact_pk(xa[h + u], z);
+#endif
                 // an iteration past the epoch's last holds −0, which the accumulator adds unconditionally:
                 // x + (−0) = x for every x, so its sums are the reference's
 #pragma unroll
@@ -651,7 +667,7 @@ __device__ __forceinline__ void fast_produce(const FJob& job, i4v span, const fl
     float cv[GH][NTT];
     int rslot = pp % rg;
     const int rstep = NG % rg;
-    unsigned long long w_ring = 0, w_slot = 0;  // profiling: cycles waiting for ring space / phasor slots
+    unsigned long long w_ring = 0, w_slot = 0, w_codes = 0, w_prod = 0;  // profiling: ring / slot waits, phase A / B
     const unsigned long long t_run = GNSSHIP_FCLOCK();
     for (int g = pp; g < n_groups; g += NG) {
         const int t = 4 * g + tl;
@@ -661,11 +677,17 @@ __device__ __forceinline__ void fast_produce(const FJob& job, i4v span, const fl
         const int cnth = max(0, min(GH, cnt - GH * h));  // this wave's iterations of the task within the epoch
         const int n0 = kAvxLanes * (m_lo + GH * h) + l;
         const bool full = 4 * g + 4 <= S && G * (4 * g + 4) <= M;  // every task of the group whole
+        const unsigned long long tA = GNSSHIP_FCLOCK();
         first_samples(g, xa);  // in flight during phase A and the slot poll
         if (full)
             group_codes<NT, DATA, IN_MARGIN, GH, true>(code0, code1, L, n0, GH, step, rem, shifts, cv);
         else
             group_codes<NT, DATA, IN_MARGIN, GH, false>(code0, code1, L, n0, cnth, step, rem, shifts, cv);
+#ifdef GNSSHIP_CORR_PROFILE
+        for (int i = 0; i < GH; i++)  // phase A's code loads landed (profiling only)
+            for (int q = 0; q < NTT; q++) asm volatile("" ::"v"(cv[i][q]));
+#endif
+        w_codes += GNSSHIP_FCLOCK() - tA;
         // the ring group is free once every accumulator wave consumed its previous occupant — and in
         // the slot ring (rg ≤ 16 groups of its 64 tasks) that also means the slot this lane polls next
         // was consumed on its previous lap (whichever producer took it)
@@ -702,6 +724,7 @@ __device__ __forceinline__ void fast_produce(const FJob& job, i4v span, const fl
             }
         }
         float* pdst = Pp + static_cast<size_t>(rslot) * PL::kGroup + l * PL::kRow + G * tl + GH * h;
+        const unsigned long long tB = GNSSHIP_FCLOCK();
 #ifndef GNSSHIP_EXP_NOPROD  // timing experiment: the producers only follow the slots and set the flags
         if (full)
             group_phasors<FMT, NTT, GH, true, PL>(span, z, dz, renorm && h == 0, n0, GH, pdst, cv, xa, xb);
@@ -712,14 +735,17 @@ __device__ __forceinline__ void fast_produce(const FJob& job, i4v span, const fl
 #endif
         GNSSHIP_PROBE(GNSSHIP_DELAY_PROD);
         if (lane == 0) lds_release_store(ready + 2 * rslot + h, gbase + g + 1);
+        w_prod += GNSSHIP_FCLOCK() - tB;
         if (g < 8) GNSSHIP_FSTAMP(pe, 48 + g);
         rslot += rstep;
         if (rslot >= rg) rslot -= rg;
     }
-    if (pw == 0) {  // slots 41-43: producer 0's ring waits, slot waits, whole production
+    if (pw == 0) {  // slots 41-43, 79, 80: producer 0's ring waits, slot waits, whole production, phase A, phase B
         GNSSHIP_FVAL(pe, 41, w_ring);
         GNSSHIP_FVAL(pe, 42, w_slot);
         GNSSHIP_FVAL(pe, 43, GNSSHIP_FCLOCK() - t_run);
+        GNSSHIP_FVAL(pe, 79, w_codes);
+        GNSSHIP_FVAL(pe, 80, w_prod);
     }
 }
 
@@ -821,26 +847,51 @@ __device__ __forceinline__ void fast_accumulate(const float* __restrict__ Pp, in
     (void)step;
     unsigned long long w_flag = 0;  // profiling: cycles spent waiting for the groups' flags
     const unsigned long long t_run = GNSSHIP_FCLOCK();
-    for (int g = 0; g < n_groups; g++) {
-        const unsigned long long t0 = GNSSHIP_FCLOCK();
-        f4 v[kQ][NS];
-        wait_group(g, rslot);
-        load_group(rslot, v);
-
-        w_flag += GNSSHIP_FCLOCK() - t0;
-        if (g == 0) GNSSHIP_FSTAMP(pe, 28);
-        if (g == n_groups - 1) GNSSHIP_FSTAMP(pe, 29);
+    auto add_group = [&](const f4 (&v)[kQ][NS]) __attribute__((always_inline)) {
 #pragma unroll
         for (int q = 0; q < kQ; q++)
 #pragma unroll
             for (int k = 0; k < NS; k++)
 #pragma unroll
                 for (int u = 0; u < 4; u++) acc[k] = __fadd_rn(acc[k], v[q][k][u]);
+    };
+    // Groups in pairs when both are ready (the accumulator is usually behind, and each LDS round
+    // trip — flag, then data — is what a group costs it): the two flags in one read batch, then the
+    // two groups' loads in one batch, then their adds in order.
+    for (int g = 0; g < n_groups;) {
+        const unsigned long long t0 = GNSSHIP_FCLOCK();
+        const int rn = rslot + 1 == rg ? 0 : rslot + 1;
+        bool pair = false;
+#if GNSSHIP_ACC_PAIRS
+        if (NH == 1 && g + 1 < n_groups) {
+            const int f0 = __hip_atomic_load(ready + 2 * rslot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            const int f1 = __hip_atomic_load(ready + 2 * rn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            pair = __builtin_amdgcn_readfirstlane(f0 == gbase + g + 1 && f1 == gbase + g + 2);
+        }
+#endif
+        f4 v[kQ][NS];
+        if (pair) {
+            asm volatile("" ::: "memory");  // the groups' loads follow both flags
+            f4 v2[kQ][NS];
+            load_group(rslot, v);
+            load_group(rn, v2);
+            w_flag += GNSSHIP_FCLOCK() - t0;
+            add_group(v);
+            add_group(v2);
+        } else {
+            wait_group(g, rslot);
+            load_group(rslot, v);
+            w_flag += GNSSHIP_FCLOCK() - t0;
+            add_group(v);
+        }
+        if (g == 0) GNSSHIP_FSTAMP(pe, 28);
+        if (g + (pair ? 1 : 0) == n_groups - 1) GNSSHIP_FSTAMP(pe, 29);
 #pragma unroll
         for (int k = 0; k < NS; k++) asm volatile("" ::"v"(acc[k]) : "memory");
         GNSSHIP_PROBE(GNSSHIP_DELAY_ACC);
-        if (lane == 0) __hip_atomic_store(acc_done, gbase + g + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        rslot = rslot + 1 == rg ? 0 : rslot + 1;
+        g += pair ? 2 : 1;
+        if (lane == 0) __hip_atomic_store(acc_done, gbase + g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        rslot = pair ? (rn + 1 == rg ? 0 : rn + 1) : rn;
     }
     if (a < 2) {  // slots 44/45 (accumulator 0), 46/47 (accumulator 1): flag waits, whole accumulation
         GNSSHIP_FVAL(pe, 44 + 2 * a, w_flag);

@@ -19,7 +19,7 @@ from gnss_sim_receiver_amd import abi, engine, signals  # noqa: E402
 
 EP = 16  # epochs 8-23 of the profiled launch (trk_fast.hip kFProfFirst)
 RUN = 64  # epochs in the profiled launch
-SLOTS = 80
+SLOTS = 88
 
 
 def main():
@@ -57,21 +57,25 @@ def main():
     t = t.reshape(n_ch, EP, SLOTS).astype(np.int64)
     us = lambda v: v / 100.0  # noqa: E731
     nxt = np.concatenate([t[:, 1:, :], np.zeros((n_ch, 1, SLOTS), np.int64)], axis=1)
-    t = np.concatenate([t, nxt], axis=2)  # slots 80 + k = the next epoch's slot k
+    t = np.concatenate([t, nxt], axis=2)  # slots SLOTS + k = the next epoch's slot k
     v = t[:, 1:-1, :]
     print(f"{n_ch} channels: epoch period {us(np.median(np.diff(t[:, :, 0], axis=1))):.2f} us (median)")
     rows = [("derive", 0, 1), ("derive -> replay done", 1, 2), ("derive -> producer 2 done", 1, 3), ("derive -> producer 3 done", 1, 4),
             ("derive -> accumulation done", 1, 5), ("replay done -> accumulation done", 2, 5), ("accumulation -> taps stored", 5, 6),
             ("taps stored -> loop done", 6, 7), ("  taps -> run_dll_pll", 6, 9), ("  run_dll_pll", 9, 10), ("  update_tracking_vars", 10, 11),
-            ("  tracking_vars -> loop done", 11, 7), ("loop done -> next derive", 7, 80), ("  taps -> epoch_pre done", 16, 17),
+            ("  tracking_vars -> loop done", 11, 7), ("loop done -> next derive", 7, SLOTS), ("  taps -> epoch_pre done", 16, 17),
             ("  epoch_pre -> published", 17, 18), ("  published -> run_dll_pll", 18, 9), ("  lock_status (wave 2)", 8, 26),
             ("  tracking_vars -> lock seen", 11, 19), ("  lock seen -> epoch_post done", 19, 24), ("  epoch_finish", 24, 25),
-            ("  epoch_finish -> loop done (records)", 25, 7), ("seed (tracking_vars) -> next derive start", 11, 80), ("  tracking_vars -> seed published", 11, 33), ("  seed published -> next derive start", 33, 80), ("derive: sincos", 0, 35), ("derive: chains", 35, 36), ("derive: dz + publish", 36, 1), ("  run_dll_pll: PLL discriminator", 9, 37), ("  run_dll_pll: carrier filter", 37, 38), ("  run_dll_pll: DLL discriminator", 38, 39), ("  run_dll_pll: code loop filter", 39, 40), ("  run_dll_pll: code freq", 40, 10),
+            ("  epoch_finish -> loop done (records)", 25, 7), ("seed (tracking_vars) -> next derive start", 11, SLOTS), ("  tracking_vars -> seed published", 11, 33), ("  seed published -> next derive start", 33, SLOTS), ("derive: sincos", 0, 35), ("derive: chains", 35, 36), ("derive: dz + publish", 36, 1), ("  run_dll_pll: PLL discriminator", 9, 37), ("  run_dll_pll: carrier filter", 37, 38), ("  run_dll_pll: DLL discriminator", 38, 39), ("  run_dll_pll: code loop filter", 39, 40), ("  run_dll_pll: code freq", 40, 10),
             ("derive -> wave 0 starts accumulating", 1, 27), ("derive -> group 0 seen by wave 0", 1, 28), ("derive -> last group seen by wave 0", 1, 29),
             ("derive -> producer 2 has group 0's slots", 1, 30), ("derive -> producer 3 has its last group's slots", 1, 31),
             ("last group seen -> accumulation done", 29, 5),
+            ("ctl: taps stored -> control reads taps", 6, 16), ("ctl: reads taps -> run_dll_pll", 16, 9),
+            ("ctl: PLL discriminator", 9, 37), ("ctl: carrier filter + spec hook", 37, 32), ("ctl: spec -> DLL start", 32, 38),
+            ("ctl: DLL discriminator", 38, 39), ("ctl: code filter + code freq", 39, 10), ("ctl: update_tracking_vars", 10, 11),
+            ("ctl: consume + seed", 11, 33), ("ctl: taps stored -> seed published", 6, 33), ("ctl: spec published -> spec seen", 32, SLOTS + 0),
             ("cycle: spec seen -> replay end", 0, 34), ("cycle: replay end -> taps stored", 34, 6),
-            ("cycle: taps stored -> spec published", 6, 32), ("cycle: spec published -> spec seen (next)", 32, 80 + 0),
+            ("cycle: taps stored -> spec published", 6, 32), ("cycle: spec published -> spec seen (next)", 32, SLOTS + 0),
             ("tail: replay end -> producer 1 has its last slots", 34, 31), ("tail: replay end -> group 6 ready", 34, 54),
             ("tail: replay end -> group 7 ready", 34, 55), ("tail: replay end -> group 6 seen", 34, 62), ("tail: replay end -> group 7 seen", 34, 63),
             ("tail: group 7 seen -> accumulation done", 63, 5), ("tail: replay end -> last group seen", 34, 29),
@@ -99,6 +103,7 @@ def main():
                 d = us(v[:, :, sl] - v[:, :, 1])[ok]
                 print(f"  derive -> group {g} {nm:22s} median {np.median(d):7.2f} us  p90 {np.percentile(d, 90):7.2f}  (n={ok.sum()})")
     for nm, k in (("producer 0: ring waits", 41), ("producer 0: slot waits", 42), ("producer 0: whole production", 43),
+                  ("producer 0: phase A (codes, sample loads issued)", 79), ("producer 0: phase B (products, stores, flag)", 80),
                   ("accumulator 0: flag waits", 44), ("accumulator 0: whole accumulation", 45), ("accumulator 1: flag waits", 46),
                   ("accumulator 1: whole accumulation", 47)):
         d = v[:, :, k]
