@@ -205,13 +205,14 @@ def sweep(ctx, h, rot, counts, rounds=1000):
         dt = time.perf_counter() - t0
         ctx.event_record(3)
         k_ms = ctx.event_elapsed_ms(2, 3)
+        eng = rx.trk.last_engine()  # the kernel the timed launch ran (gnsship_trk_last_engine)
         n_rec = int(np.count_nonzero(rec[:done]["flags"] & 8))
         idx = np.linspace(0, n - 1, min(n, 64)).astype(int)
         tracking = float(np.mean([rx.trk.channel_state(int(c))[0] in (2, 3, 4) for c in idx]))
         rx.close()
         del rec, host
         cps = n_rec / dt
-        out.append({"channels": n, "epochs": done, "epoch_records": n_rec, "record_bytes": n_rec * 96, "us_per_epoch_round": round(dt / done * 1e6, 2),
+        out.append({"channels": n, "kernel": abi.TRK_ENGINE_NAMES.get(eng, str(eng)), "epochs": done, "epoch_records": n_rec, "record_bytes": n_rec * 96, "us_per_epoch_round": round(dt / done * 1e6, 2),
                     "kernel_us_per_round": round(k_ms * 1e3 / done, 2), "channel_epochs_per_s": round(cps, 0),
                     "realtime_factor": round(done * 1e-3 / dt, 2), "tracking_fraction_sampled": round(tracking, 3)})
     return out
@@ -1010,14 +1011,16 @@ def main():
             if "sweeps_per_s" in c3 and "sweeps_per_s" in c3["cpu_baseline"]:
                 c3["gpu_vs_cpu"] = round(c3["sweeps_per_s"] / c3["cpu_baseline"]["sweeps_per_s"], 1)
     if rank == 0 and not args.no_aux and not args.sharded_aux_only:
-        counts = [12, 256, 1024, 4096, 16384, 32768, 65536, 81920]
+        counts = [12, 256, 1024, 4096, 16384, 65536, 98304, 131072, 163840]
         sw = sweep(ctx, h, h["rotator"], counts)
         rt = [r["channels"] for r in sw if r["realtime_factor"] >= 1.0]
         result["tracked_channels_sustained"] = max(rt) if rt else 0
         result["channel_sweep"] = sw
         result["tracked_channels_note"] = ("the largest channel count of the sweep measured at >= real time: 1 s of signal (1000 epochs) per "
-                                           "point, every channel-epoch record copied to the host inside the timed run; channels beyond the "
-                                           "resident workgroups run in successive generations of the persistent kernel")
+                                           "point, every channel-epoch record copied to the host inside the timed run; each point names the "
+                                           "kernel its timed launch ran (gnsship_trk_last_engine): with the AVX rotator, trk_fast_kernel's "
+                                           "latency form up to one workgroup per CU, its throughput form (the same u_avx accumulation order, "
+                                           "several workgroups per CU, channels beyond the resident ones in successive workgroup generations) above")
         if h["rotator"] != 0:
             g = Receiver(ctx, "GPS", FS, VL, [h["sats"][i] for i in range(N_CH)], N_CH, h["first"], 0, code_base=800)
             pre = int(round(PRE_ROLL_S * FS))

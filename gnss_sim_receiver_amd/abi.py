@@ -78,9 +78,9 @@ class AcqResult(ctypes.Structure):
 
 SYS_GPS_L1CA, SYS_GAL_E1, SYS_BDS_B1I = 0, 1, 2
 # gnsship_trk_last_engine (include/gnsship.h GNSSHIP_TRK_ENGINE_*)
-TRK_ENGINE_NONE, TRK_ENGINE_FAST_LATENCY, TRK_ENGINE_FAST_THROUGHPUT, TRK_ENGINE_PERSIST, TRK_ENGINE_ROUNDS = 0, 1, 2, 3, 4
+TRK_ENGINE_NONE, TRK_ENGINE_FAST_LATENCY, TRK_ENGINE_FAST_THROUGHPUT, TRK_ENGINE_PERSIST, TRK_ENGINE_ROUNDS, TRK_ENGINE_LANES = 0, 1, 2, 3, 4, 5
 TRK_ENGINE_NAMES = {0: "none", 1: "trk_fast_kernel (latency form)", 2: "trk_fast_kernel (throughput form)", 3: "trk_persist_kernel",
-                    4: "round-based loop (trk_step_kernel + correlator)"}
+                    4: "round-based loop (trk_step_kernel + correlator)", 5: "trk_lane_kernel (throughput form, one 16-lane row per channel)"}
 # rotator dot-product variant (include/gnsship.h GNSSHIP_ROTATOR_*, job flag bits GNSSHIP_JOB_*)
 ROTATOR_GENERIC, ROTATOR_AVX, ROTATOR_AUTO = 0, 1, -1
 JOB_HIGH_DYN, JOB_ROTATOR_AVX = 1, 2

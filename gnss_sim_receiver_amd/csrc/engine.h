@@ -20,7 +20,7 @@ constexpr int kMaxCodeLen = 16384;       // LDS budget for the local code replic
 struct CodeDesc {
     const float* ptr;
     int32_t len;
-    int32_t pad;
+    int32_t binary;  // every chip is exactly +1 or -1 (gnsship_code_set)
 };
 
 constexpr int kRenorm = 256;             // the generic rotator renormalises |phase| every 256 samples

@@ -370,6 +370,9 @@ extern "C" int gnsship_code_set(gnsship_ctx* ctx, int code_id, const float* code
     HIP_TRY(ctx, upload_padded_code(code, len, &p));
     d.ptr = p;
     d.len = len;
+    d.binary = 1;
+    for (int i = 0; i < len; i++)
+        if (code[i] != 1.0f && code[i] != -1.0f) d.binary = 0;
     ctx->codes_dirty = true;
     ctx->codes_version++;
     return GNSSHIP_OK;

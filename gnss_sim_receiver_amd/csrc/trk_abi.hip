@@ -641,15 +641,24 @@ static int trk_enqueue(gnsship_trk* t, const void* src, int fmt, uint64_t buffer
         if (dump) HIP_TRY(ctx, hipMemsetAsync(t->dump_dev, 0, sizeof(gnsship_trk_dump_record) * nrec, ctx->stream));
         const int n_codes = static_cast<int>(ctx->codes_host.size());
         hipError_t e;
-        const bool fast = avx && trk_fast_supported(t->params, code_cap, nc);
-        t->last_engine = fast ? (trk_fast_thru(nc) ? GNSSHIP_TRK_ENGINE_FAST_THROUGHPUT : GNSSHIP_TRK_ENGINE_FAST_LATENCY) : GNSSHIP_TRK_ENGINE_PERSIST;
-        if (fast)
+        bool binary = true;
+        for (const CodeDesc& cd : ctx->codes_host)
+            if (cd.ptr && !cd.binary) binary = false;
+        const bool lanes = avx && trk_lane_supported(t->params, code_cap, nc, fmt, n_buffer_samples, binary);
+        const bool fast = avx && !lanes && trk_fast_supported(t->params, code_cap, nc);
+        t->last_engine = lanes  ? GNSSHIP_TRK_ENGINE_LANES
+                         : fast ? (trk_fast_thru(nc) ? GNSSHIP_TRK_ENGINE_FAST_THROUGHPUT : GNSSHIP_TRK_ENGINE_FAST_LATENCY)
+                                : GNSSHIP_TRK_ENGINE_PERSIST;
+        if (lanes)
+            e = launch_trk_lane(t->params_dev, t->params, t->chans_dev, nc, ctx->codes_dev, n_codes, code_cap, src, fmt, buffer_first_sample,
+                n_buffer_samples, max_rounds, out ? t->rec_dev : nullptr, dump ? t->dump_dev : nullptr, trace, t->ran_dev, ctx->stream);
+        else if (fast)
             e = launch_trk_fast(t->params_dev, t->params, t->chans_dev, nc, ctx->codes_dev, n_codes, code_cap, src, fmt, buffer_first_sample,
                 n_buffer_samples, max_rounds, out ? t->rec_dev : nullptr, dump ? t->dump_dev : nullptr, trace, t->ran_dev, ctx->stream);
         else
             e = launch_trk_persist(t->params_dev, t->params, t->chans_dev, nc, ctx->codes_dev, n_codes, code_cap, src, fmt, buffer_first_sample,
                 n_buffer_samples, max_rounds, out ? t->rec_dev : nullptr, dump ? t->dump_dev : nullptr, trace, t->ran_dev, avx, ctx->stream);
-        if (e != hipSuccess) return hip_fail(ctx, e, fast ? "launch_trk_fast" : "launch_trk_persist");
+        if (e != hipSuccess) return hip_fail(ctx, e, lanes ? "launch_trk_lane" : fast ? "launch_trk_fast" : "launch_trk_persist");
     }
     if (!persist) t->last_engine = GNSSHIP_TRK_ENGINE_ROUNDS;
     for (int r = 0; r <= max_rounds && !persist; r++) {

@@ -144,6 +144,14 @@ hipError_t launch_trk_persist(const TrkParams* params_dev, const TrkParams& para
 // state, flagless phasor slots, lock detectors beside the loop update.
 bool trk_fast_supported(const TrkParams& p, int code_cap_floats, int n_chans);
 bool trk_fast_thru(int n_chans);  // the throughput form (more channels than CUs)
+int trk_device_cus();             // compute units of the current device
+// The throughput form with one 16-lane row per channel (trk_lane.hip): every code ±1 (codes_binary),
+// the buffer addressable with 32-bit byte offsets; used above one channel per CU (GNSSHIP_TRK_LANE=0/1
+// forces it off / on).
+bool trk_lane_supported(const TrkParams& p, int code_cap_floats, int n_chans, int fmt, int64_t buf_len, bool codes_binary);
+hipError_t launch_trk_lane(const TrkParams* params_dev, const TrkParams& params, TrkChannel* chans, int n_chans, const CodeDesc* codes, int n_codes,
+    int code_cap_floats, const void* samples, int fmt, uint64_t buf_first, int64_t buf_len, int max_rounds, gnsship_trk_epoch* rec,
+    gnsship_trk_dump_record* dump, gnsship_trk_corr_trace* trace, int* ran_count, hipStream_t stream);
 hipError_t launch_trk_fast(const TrkParams* params_dev, const TrkParams& params, TrkChannel* chans, int n_chans, const CodeDesc* codes, int n_codes,
     int code_cap_floats, const void* samples, int fmt, uint64_t buf_first, int64_t buf_len, int max_rounds, gnsship_trk_epoch* rec,
     gnsship_trk_dump_record* dump, gnsship_trk_corr_trace* trace, int* ran_count, hipStream_t stream);

@@ -1753,6 +1753,7 @@ static FastPlan fast_plan(const TrkParams& p, int code_cap_floats, int n_chans)
 }
 
 bool trk_fast_thru(int n_chans) { return fast_thru(n_chans); }
+int trk_device_cus() { return device_cus(); }
 
 bool trk_fast_supported(const TrkParams& p, int code_cap_floats, int n_chans)
 {

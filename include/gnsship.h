@@ -456,14 +456,15 @@ int gnsship_trk_set_trace(gnsship_trk* t, int enable);
 /* The last run's trace: max_rounds × max_channels records (the run's max_rounds), zero where no epoch ran. */
 int gnsship_trk_trace_records(gnsship_trk* t, gnsship_trk_corr_trace* out, int max_records);
 /* Which kernel the last gnsship_trk_run / _launch ran (GNSSHIP_TRK_ENGINE_*; NONE before any run):
- * the AVX rotator runs trk_fast (the latency form while the channels fit one per compute unit, the
- * throughput form — two workgroups per CU — beyond), the generic rotator trk_persist, high_dyn and
- * epochs too long for LDS the round-based loop. */
+ * the AVX rotator runs trk_fast's latency form while the channels fit one per compute unit and
+ * trk_lane beyond (one 16-lane row per channel; trk_fast's throughput form when a code is not ±1),
+ * the generic rotator trk_persist, high_dyn and epochs too long for LDS the round-based loop. */
 #define GNSSHIP_TRK_ENGINE_NONE 0
 #define GNSSHIP_TRK_ENGINE_FAST_LATENCY 1
 #define GNSSHIP_TRK_ENGINE_FAST_THROUGHPUT 2
 #define GNSSHIP_TRK_ENGINE_PERSIST 3
 #define GNSSHIP_TRK_ENGINE_ROUNDS 4
+#define GNSSHIP_TRK_ENGINE_LANES 5
 int gnsship_trk_last_engine(gnsship_trk* t, int* engine);
 int gnsship_trk_destroy(gnsship_trk* t);
 

@@ -2,7 +2,10 @@
 N channels of GPS L1 C/A at 4 Msps on the bench's file (seed 0x6E550002), the AVX rotator, pre-rolled
 to state 4, then one timed launch of R epochs.
 
-    python scripts/trk_sweep_point.py [channels=65536] [epochs=20]"""
+    python scripts/trk_sweep_point.py [channels=65536] [epochs=20] [records]
+
+With `records` the timed launch writes every channel-epoch record (as bench.py's sweep does) and they
+are collected to the host after the timing.  The line names the kernel the timed launch ran."""
 import os
 import sys
 import time
@@ -38,13 +41,23 @@ def main():
     lo = first + pre * vl
     ctx.sync()
     t0 = time.perf_counter()
-    done = trk.run_ptr(base + (lo - first + 2 * vl) * 8, abi.FMT_CF32, lo, (rounds + 2) * vl, rounds)
-    dt = time.perf_counter() - t0
+    recs = "records" in sys.argv[3:]
+    if recs:
+        trk.launch_ptr(base + (lo - first + 2 * vl) * 8, abi.FMT_CF32, lo, (rounds + 2) * vl, rounds, records=True)
+        ctx.sync()
+        dt = time.perf_counter() - t0
+        rec, done = trk.collect()
+        n_rec = int(np.count_nonzero(rec[:done]["flags"] & 8))
+    else:
+        done = trk.run_ptr(base + (lo - first + 2 * vl) * 8, abi.FMT_CF32, lo, (rounds + 2) * vl, rounds)
+        dt = time.perf_counter() - t0
+        n_rec = 0
+    eng = abi.TRK_ENGINE_NAMES.get(trk.last_engine())
     st = np.bincount(trk.states(), minlength=5).tolist()
     trk.close()
     ctx.close()
     print(f"channels {n}: {done} epochs in {dt * 1e3:.2f} ms -> {n * done / dt / 1e6:.2f} M channel-epochs/s, realtime x{done * 1e-3 / dt:.2f}, "
-          f"states {st}", flush=True)
+          f"states {st}, kernel {eng}, records {n_rec}", flush=True)
 
 
 if __name__ == "__main__":

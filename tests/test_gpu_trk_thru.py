@@ -1,9 +1,10 @@
-"""The AVX tracking engine's throughput form — trk_fast_kernel with more channels than compute units
-(two workgroups per CU, trk_fast.hip fast_thru) — the kernel behind bench.py's
-tracked_channels_sustained.  It keeps u_avx's accumulation order (volk_gnsssdr_32fc_32f_rotator_dot_
-prod_32fc_xn.h:257-291) as the latency form does, so a sample of channels out of a 1024-channel run
-through the DEFAULT dispatch is held bit for bit to the oracle: every traced epoch's taps on the
-device's own arguments (trace_exact) and every record field against the oracle loop (compare_exact).
+"""The AVX tracking engine's throughput forms — with more channels than compute units the default
+dispatch runs trk_lane_kernel (one 16-lane row per channel, trk_lane.hip), the kernel behind bench.py's
+tracked_channels_sustained; trk_fast_kernel's throughput form (two workgroups per CU) is the fallback
+for codes that are not ±1.  Both keep u_avx's accumulation order (volk_gnsssdr_32fc_32f_rotator_dot_
+prod_32fc_xn.h:220-308), so a sample of channels out of a 1024-channel run is held bit for bit to the
+oracle: every traced epoch's taps on the device's own arguments (trace_exact) and every record field
+against the oracle loop (compare_exact).
 
 Channels c take satellite c mod 32 of one sky (as the bench's sweep does); each channel starts at its
 own code-delay and Doppler offset, so channels sharing a satellite run different loops."""
@@ -21,7 +22,10 @@ from test_gpu_trk import compare_exact, dev_conf
 pytestmark = pytest.mark.gpu
 
 
-def test_1024_avx_channels_default_dispatch_exact(ctx):
+@pytest.mark.parametrize("form", ["default", "trk_fast"])
+def test_1024_avx_channels_default_dispatch_exact(ctx, form, monkeypatch):
+    if form == "trk_fast":
+        monkeypatch.setenv("GNSSHIP_TRK_LANE", "0")
     fs, vl, n_ch, epochs = 4e6, 4000, 1024, 700
     sats = signals.random_sky(32, seed=0x6E550012)
     for s in sats:
@@ -43,7 +47,8 @@ def test_1024_avx_channels_default_dispatch_exact(ctx):
     trk.set_trace(True)
     rec, rounds = trk.run(x, first, epochs)
     assert rounds == epochs
-    assert trk.last_engine() == abi.TRK_ENGINE_FAST_THROUGHPUT, abi.TRK_ENGINE_NAMES[trk.last_engine()]
+    want = abi.TRK_ENGINE_LANES if form == "default" else abi.TRK_ENGINE_FAST_THROUGHPUT
+    assert trk.last_engine() == want, abi.TRK_ENGINE_NAMES[trk.last_engine()]
     tr = trk.trace(epochs)
     states = trk.states()
     trk.close()
