@@ -446,6 +446,9 @@ def allgather_rows(ctx, torch, rows, world):
     return torch.cat(outs).cpu().numpy()
 
 
+C3_CN0 = 50.0  # dB-Hz of the C3 bench signal's ten present PRNs
+
+
 def acq_c3_sharded(ctx, torch, rank, world, device, barrier, reps=20):
     """C3 (32 PRN x 40 bins x 25000 at 25 Msps, BASELINE's signal: 10 present, seed 0x6E550003) with
     the (PRN x bin) cells sharded by PRN over the ranks: the 25000-sample block fanned out from rank 0,
@@ -453,7 +456,7 @@ def acq_c3_sharded(ctx, torch, rank, world, device, barrier, reps=20):
     sweeps/s = reps / max-over-ranks wall."""
     from gnss_sim_receiver_amd import codes as C, engine, sharding, signals as S
     fs, n = 25000000, 25000
-    c3 = S.c3_sky()
+    c3 = S.c3_sky(cn0=C3_CN0)
     x = torch.empty(n, dtype=torch.complex64, device=f"cuda:{device}")
     if rank == 0:
         x.copy_(torch.from_numpy(S.generate_if(fs, n, c3, seed=0x6E550003)))
@@ -478,13 +481,17 @@ def acq_c3_sharded(ctx, torch, rank, world, device, barrier, reps=20):
     stat = {k + 1: float(merged[k][6]) for k in merged}
     dt = wall / reps
     cells = 32 * 40
-    return {"config": "C3: 32 PRN (10 present, seed 0x6E550003) x 40 bins, fft 25000 (four-step), 25 Msps; "
+    absent_max = max(v for p, v in stat.items() if p not in present)
+    return {"config": f"C3: 32 PRN (10 present at {C3_CN0:g} dB-Hz, seed 0x6E550003) x 40 bins, fft 25000 (four-step), 25 Msps; "
                       f"cells sharded by PRN over {world} rank(s), per-PRN results all-gathered",
+            "signal_note": "at 45 dB-Hz a 1 ms coherent search is marginal over 1280 cells (post-correlation SNR 31.6 against a "
+                           "noise-only maximum near 14x the mean); the present PRNs are set 5 dB stronger so the line shows detection",
+            "present_detected": sum(stat[p] > absent_max for p in present),
             "n_ranks": world, "prns_per_rank": len(mine), "sweep_ms": round(dt * 1e3, 3), "sweeps_per_s": round(1 / dt, 1),
             "cells_per_s": round(cells / dt, 0), "algorithmic_GBps": round(cells * 20 * n / dt / 1e9, 1),
             "prns_present": present, "prns_reported": len(merged),
             "present_min_test_statistic": round(min(stat[p] for p in present), 2),
-            "absent_max_test_statistic": round(max(v for p, v in stat.items() if p not in present), 2),
+            "absent_max_test_statistic": round(absent_max, 2),
             "fanout": COMM["transport"]}
 
 
@@ -646,7 +653,7 @@ def cpu_acq_c3(budget_s=8.0):
     from oracle import oracle as O
     fs, n = 25000000, 25000
     workers = len(os.sched_getaffinity(0))
-    x = S.generate_if(fs, n, S.c3_sky(), seed=0x6E550003).astype(np.complex64)
+    x = S.generate_if(fs, n, S.c3_sky(cn0=C3_CN0), seed=0x6E550003).astype(np.complex64)
     nb = O.num_doppler_bins(5000, 250)
     w = O.doppler_wipeoff_grid(nb, n, 5000, 250, 0, fs)
     cf = [np.conj(sf.fft(C.gps_l1_ca_code_gen_complex_sampled(k + 1, fs)[:n].astype(np.complex64), workers=workers)) for k in range(32)]
