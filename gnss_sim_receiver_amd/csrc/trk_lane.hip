@@ -37,13 +37,16 @@ namespace {
 #ifndef GNSSHIP_LANE_OCC
 #define GNSSHIP_LANE_OCC 4  // waves per SIMD the register budget is sized for (512 / OCC VGPRs each)
 #endif
+#ifndef GNSSHIP_LANE_BLOCK
+#define GNSSHIP_LANE_BLOCK 8  // iterations per block with three taps
+#endif
 constexpr int kLRows = kWave / kAvxLanes;  // channels per wave
 constexpr int kLWaves = GNSSHIP_LANE_WAVES;
 constexpr int kLChans = kLWaves * kLRows;  // channels per workgroup
 constexpr int kLThreads = kLWaves * kWave;
 // iterations per block: their samples are in flight and their chips looked up together (kB divides 64)
 template <int NTT>
-constexpr int lane_block() { return NTT > 3 ? 4 : 8; }
+constexpr int lane_block() { return NTT > 3 ? 4 : GNSSHIP_LANE_BLOCK; }
 
 // Sign-bit replica of a padded code (engine.h padded_code_quads): bit p of the table is chip
 // p − kCodeMargin < 0 (p over the replica and its wrapped margins).
