@@ -38,7 +38,7 @@ namespace {
 #define GNSSHIP_LANE_OCC 4  // waves per SIMD the register budget is sized for (512 / OCC VGPRs each)
 #endif
 #ifndef GNSSHIP_LANE_BLOCK
-#define GNSSHIP_LANE_BLOCK 8  // iterations per block with three taps
+#define GNSSHIP_LANE_BLOCK 4  // iterations per block with three taps (4: no spills in the loop update at 128 VGPRs)
 #endif
 constexpr int kLRows = kWave / kAvxLanes;  // channels per wave
 constexpr int kLWaves = GNSSHIP_LANE_WAVES;
