@@ -146,6 +146,9 @@ constexpr int kLongEpoch = 10000;  // samples per epoch from which the long-epoc
 #ifndef GNSSHIP_ACC_PIPE  // A/B: the accumulator loads the next group behind the current one's adds (measured slower)
 #define GNSSHIP_ACC_PIPE 0
 #endif
+#ifndef GNSSHIP_PRE_DISC  // the accumulator waves evaluate the discriminators ahead of the loop (0: the control wave does)
+#define GNSSHIP_PRE_DISC 1
+#endif
 #ifndef GNSSHIP_ROLE_PLAN  // wave roles by SIMD: 0 phasor + accumulator 0 share a SIMD; 1 one primary role per SIMD
 #define GNSSHIP_ROLE_PLAN 0
 #endif
@@ -235,6 +238,8 @@ struct FShared {
     int32_t pred_seq;
     int32_t verdict;    // 4·(e + 1) + 1: wave 0 confirmed epoch e's prediction and published the job; + 2: refuted; + 3: not seen
     f2 tailp[kAvxLanes][kMaxTaps + 1];  // the tail's products (sample 16M + j, tap), wave 1 → wave 0
+    double pre_pll[2], pre_dll[2];  // epoch e's discriminators in [e & 1], from accumulator waves 0 / 1 (PreDisc)
+    int32_t pll_seq, dll_seq;       // e + 1 once they are stored
 };
 
 // The job as wave-uniform values (scalar registers): read from LDS it would otherwise be per-lane,
@@ -1168,6 +1173,7 @@ __global__ __launch_bounds__(W * kWave, (fast_waves_per_simd<THRU, W>())) void t
         sh.step_seq = 0;
         sh.pred_seq = 0;
         sh.verdict = 0;
+        sh.pll_seq = sh.dll_seq = 0;
 #ifdef GNSSHIP_EXP_SERIAL
         g_replay_done = 0;
 #endif
@@ -1225,6 +1231,11 @@ __global__ __launch_bounds__(W * kWave, (fast_waves_per_simd<THRU, W>())) void t
         __syncthreads();
     }
     const auto& kp = loop_params<THRU>(k, kf);
+    // Discriminators ahead of the loop: where every state-4 epoch's E / P / L are its own taps (no
+    // secondary code to strip, no extended integration), the accumulator waves evaluate the PLL and
+    // DLL discriminators right after storing the taps — the same operations on the same floats as
+    // epoch_pre + run_dll_pll — while the control wave runs epoch_pre; it then takes both values.
+    const bool pre_disc = __builtin_amdgcn_readfirstlane(GNSSHIP_PRE_DISC && !k.sync[sc.geo].secondary && k.sync[sc.geo].extend == 1 ? 1 : 0) != 0;
     // Wave roles (one channel per workgroup, its epochs a serial chain): see the file header.  The
     // control wave hands the next epoch's NCO arguments (the seed) to the phasor wave as soon as they
     // are settled, so the derive and the first tasks of epoch e + 1 overlap epoch e's record writes.
@@ -1506,6 +1517,33 @@ __global__ __launch_bounds__(W * kWave, (fast_waves_per_simd<THRU, W>())) void t
                     }
                 }
                 if (lane == 0) lds_release_store(&sh.taps_seq[pw], e + 1);
+                if (pre_disc && pw < 2) {
+                    // the discriminators of this epoch from its taps, as epoch_pre's save_correlation_results
+                    // (0 + 1·tap) and run_dll_pll form them (used by the control wave in state 4 only)
+#pragma unroll
+                    for (int a = 0; a < NA; a++) wait_seq(&sh.taps_seq[a], e + 1);
+                    const float* tp = sh.taps[e & 1];
+                    const int eo = k.veml ? 2 : 0;
+                    auto own = [&](int i) { return __fadd_rn(0.0f, __fmul_rn(1.0f, tp[i])); };
+                    if (pw == 0 || NA == 1) {
+                        const double v = pll_error_hz(k.track_pilot ? 0 : 1, own(eo + 2), own(eo + 3));
+                        if (lane == 0) {
+                            sh.pre_pll[e & 1] = v;
+                            publish_seq(&sh.pll_seq, e + 1);
+                        }
+                    }
+                    if (pw == 1 || NA == 1) {
+                        const float ve[2] = {k.veml ? own(0) : 0.0f, k.veml ? own(1) : 0.0f};
+                        const float ee[2] = {own(eo), own(eo + 1)};
+                        const float ll[2] = {own(eo + 4), own(eo + 5)};
+                        const float vl[2] = {k.veml ? own(8) : 0.0f, k.veml ? own(9) : 0.0f};
+                        const double v = dll_error_chips(k, ve, ee, ll, vl, k.conf.early_late_space_chips);
+                        if (lane == 0) {
+                            sh.pre_dll[e & 1] = v;
+                            publish_seq(&sh.dll_seq, e + 1);
+                        }
+                    }
+                }
             }
             GNSSHIP_FSTAMP(e, 6);
         }
@@ -1574,7 +1612,17 @@ __global__ __launch_bounds__(W * kWave, (fast_waves_per_simd<THRU, W>())) void t
                         }
                         GNSSHIP_FSTAMP(e, 32);
                     };
-                    epoch_loop(kp, rc, nullptr, early_step);
+                    // the accumulator waves' discriminators (state 4 with the run's spacing; epoch_pre
+                    // left E / P / L equal to 0 + the taps, as they formed them)
+                    PreDisc pd{0.0, 0.0, 0};
+                    if (pre_disc && r.state == 4 && __builtin_bit_cast(uint32_t, unif(rc.spc)) == __builtin_bit_cast(uint32_t, k.conf.early_late_space_chips)) {
+                        wait_seq(&sh.pll_seq, e + 1);
+                        wait_seq(&sh.dll_seq, e + 1);
+                        pd.pll = sh.pre_pll[e & 1];
+                        pd.dll = sh.pre_dll[e & 1];
+                        pd.ok = 3;
+                    }
+                    epoch_loop(kp, rc, nullptr, early_step, &pd);
                     // State 4: epoch_post cannot change what the next epoch's correlation needs (the
                     // channel stays runnable — 4, or 3 for extended integration — on the same taps), so
                     // the next epoch is seeded now, before the lock test's outcome, and wave 1 derives

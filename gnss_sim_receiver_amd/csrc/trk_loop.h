@@ -533,15 +533,51 @@ struct NoDopplerHook {
     __device__ void operator()(double) const {}
 };
 
-template <class K, class C, class H = NoDopplerHook>
-__device__ GNSSHIP_LOOP_INLINE void run_dll_pll(const K& k, C& c, const H& on_doppler = H{})
+// The PLL discriminator in Hz (:1065-1078): pll_cloop_two_quadrant_atan, or pll_four_quadrant_atan
+// once the pilot is tracked (gr::fast_atan2f restated as atan2f, glibc_atanf.h), over 2π.
+__device__ __forceinline__ double pll_error_hz(int cloop, float p0, float p1)
 {
     double disc;
-    if (c.cloop)
-        disc = (c.p[0] != 0.0f) ? static_cast<double>(glibc_atanf(__fdiv_rn(c.p[1], c.p[0]))) : 0.0;
+    if (cloop)
+        disc = (p0 != 0.0f) ? static_cast<double>(glibc_atanf(__fdiv_rn(p1, p0))) : 0.0;
     else
-        disc = static_cast<double>(glibc_atan2f(c.p[1], c.p[0]));  // gr::fast_atan2f restated as atan2f (glibc_atanf.h)
-    c.carr_phase_error_hz = div_2pi(disc);
+        disc = static_cast<double>(glibc_atan2f(p1, p0));
+    return div_2pi(disc);
+}
+
+// The DLL discriminator in chips (:1100-1110): dll_nc_vemlp_normalized or dll_nc_e_minus_l_normalized.
+template <class K>
+__device__ __forceinline__ double dll_error_chips(const K& k, const float* ve, const float* e, const float* l, const float* vl, float spc)
+{
+    if (k.veml) {
+        const double early = static_cast<double>(sqrt_rn_f32(__fadd_rn(__fadd_rn(__fadd_rn(__fmul_rn(ve[0], ve[0]), __fmul_rn(ve[1], ve[1])),
+                                                                          __fmul_rn(e[0], e[0])),
+            __fmul_rn(e[1], e[1]))));
+        const double late = static_cast<double>(sqrt_rn_f32(__fadd_rn(__fadd_rn(__fadd_rn(__fmul_rn(l[0], l[0]), __fmul_rn(l[1], l[1])),
+                                                                         __fmul_rn(vl[0], vl[0])),
+            __fmul_rn(vl[1], vl[1]))));
+        const double s = early + late;
+        return (s == 0.0) ? 0.0 : (early - late) / s;
+    }
+    const double pe = static_cast<double>(hypotf_glibc(e[0], e[1]));
+    const double pl = static_cast<double>(hypotf_glibc(l[0], l[1]));
+    const double s = pe + pl;
+    const float slope = k.conf.slope;
+    const float norm = __fdiv_rn(__fsub_rn(k.conf.y_intercept, __fmul_rn(slope, spc)), slope);
+    return (s == 0.0) ? 0.0 : static_cast<double>(norm) * (pe - pl) / s;
+}
+
+// Both discriminators of an epoch evaluated ahead by other waves (the fast kernel's accumulator waves,
+// from the same taps with the same operations); ok bit 0: pll, bit 1: dll.
+struct PreDisc {
+    double pll, dll;
+    int ok;
+};
+
+template <class K, class C, class H = NoDopplerHook>
+__device__ GNSSHIP_LOOP_INLINE void run_dll_pll(const K& k, C& c, const H& on_doppler = H{}, const PreDisc* pre = nullptr)
+{
+    c.carr_phase_error_hz = (pre && (pre->ok & 1)) ? pre->pll : pll_error_hz(c.cloop, c.p[0], c.p[1]);
     GNSSHIP_TRK_LOOP_STAMP(37);
     // d_current_correlation_time_s: the code period, or extend × code period once extended
     const float T = c.narrow ? syncset(k, c).T_ext : static_cast<float>(k.code_period);
@@ -559,23 +595,7 @@ __device__ GNSSHIP_LOOP_INLINE void run_dll_pll(const K& k, C& c, const H& on_do
     c.carrier_doppler_hz = c.carr_error_filt_hz;
     on_doppler(c.carrier_doppler_hz);
     GNSSHIP_TRK_LOOP_STAMP(38);
-    if (k.veml) {
-        const double early = static_cast<double>(sqrt_rn_f32(__fadd_rn(__fadd_rn(__fadd_rn(__fmul_rn(c.ve[0], c.ve[0]), __fmul_rn(c.ve[1], c.ve[1])),
-                                                                          __fmul_rn(c.e[0], c.e[0])),
-            __fmul_rn(c.e[1], c.e[1]))));
-        const double late = static_cast<double>(sqrt_rn_f32(__fadd_rn(__fadd_rn(__fadd_rn(__fmul_rn(c.l[0], c.l[0]), __fmul_rn(c.l[1], c.l[1])),
-                                                                         __fmul_rn(c.vl[0], c.vl[0])),
-            __fmul_rn(c.vl[1], c.vl[1]))));
-        const double s = early + late;
-        c.code_error_chips = (s == 0.0) ? 0.0 : (early - late) / s;
-    } else {
-        const double pe = static_cast<double>(hypotf_glibc(c.e[0], c.e[1]));
-        const double pl = static_cast<double>(hypotf_glibc(c.l[0], c.l[1]));
-        const double s = pe + pl;
-        const float slope = k.conf.slope;
-        const float norm = __fdiv_rn(__fsub_rn(k.conf.y_intercept, __fmul_rn(slope, c.spc)), slope);
-        c.code_error_chips = (s == 0.0) ? 0.0 : static_cast<double>(norm) * (pe - pl) / s;
-    }
+    c.code_error_chips = (pre && (pre->ok & 2)) ? pre->dll : dll_error_chips(k, c.ve, c.e, c.l, c.vl, c.spc);
     GNSSHIP_TRK_LOOP_STAMP(39);
     c.code_error_filt_chips = loop_filter_apply(k, c, static_cast<float>(c.code_error_chips));
     GNSSHIP_TRK_LOOP_STAMP(40);
@@ -858,10 +878,10 @@ __device__ GNSSHIP_LOOP_INLINE double epoch_pre(const K& k, C& c, const float* t
 }
 
 template <class K, class C, class H = NoDopplerHook>
-__device__ __forceinline__ void epoch_loop(const K& k, C& c, TrkHist* h, const H& on_doppler = H{})
+__device__ __forceinline__ void epoch_loop(const K& k, C& c, TrkHist* h, const H& on_doppler = H{}, const PreDisc* pre = nullptr)
 {
     GNSSHIP_TRK_LOOP_STAMP(9);
-    run_dll_pll(k, c, on_doppler);
+    run_dll_pll(k, c, on_doppler, pre);
     GNSSHIP_TRK_LOOP_STAMP(10);
     update_tracking_vars(k, c, h);
     GNSSHIP_TRK_LOOP_STAMP(11);
