@@ -146,6 +146,9 @@ constexpr int kLongEpoch = 10000;  // samples per epoch from which the long-epoc
 #ifndef GNSSHIP_ACC_PIPE  // A/B: the accumulator loads the next group behind the current one's adds (measured slower)
 #define GNSSHIP_ACC_PIPE 0
 #endif
+#ifndef GNSSHIP_EARLY_JOB  // the control wave publishes the next epoch's code / sample arguments before the seed (state 4)
+#define GNSSHIP_EARLY_JOB 0  // measured: 622 vs 663 Msps with it on (the control wave pays the early publish on its chain)
+#endif
 #ifndef GNSSHIP_PRE_DISC  // the accumulator waves evaluate the discriminators ahead of the loop (0: the control wave does)
 #define GNSSHIP_PRE_DISC 1
 #endif
@@ -240,6 +243,8 @@ struct FShared {
     f2 tailp[kAvxLanes][kMaxTaps + 1];  // the tail's products (sample 16M + j, tap), wave 1 → wave 0
     double pre_pll[2], pre_dll[2];  // epoch e's discriminators in [e & 1], from accumulator waves 0 / 1 (PreDisc)
     int32_t pll_seq, dll_seq;       // e + 1 once they are stored
+    FJob early;         // epoch e's code / sample arguments (no phasors), published as early_seq = e + 1 (state 4)
+    int32_t early_seq;
 };
 
 // The job as wave-uniform values (scalar registers): read from LDS it would otherwise be per-lane,
@@ -642,7 +647,9 @@ constexpr int producers_per_group() { return (GNSSHIP_PROD_SPLIT && n_producers<
 
 template <int FMT, int NT, bool DATA, bool IN_MARGIN, int G, int W>
 __device__ __forceinline__ void fast_produce(const FJob& job, i4v span, const float* __restrict__ code0, const float* __restrict__ code1, int L,
-    uint64_t* __restrict__ Zs, int rs, float* __restrict__ Pp, int rg, int32_t* ready, const int32_t* acc_groups, int gbase, int lane, int pw, int pe)
+    uint64_t* __restrict__ Zs, int rs, float* __restrict__ Pp, int rg, int32_t* ready, const int32_t* acc_groups, int gbase, int lane, int pw, int pe,
+    bool pre, f2 (&xa)[(G / producers_per_group<NT + (DATA ? 1 : 0), W, G>()) < 8 ? (G / producers_per_group<NT + (DATA ? 1 : 0), W, G>()) : 8],
+    float (&cv)[G / producers_per_group<NT + (DATA ? 1 : 0), W, G>()][NT + (DATA ? 1 : 0)])
 {
     constexpr int SB = sample_bytes<FMT>();
     constexpr int NTT = NT + (DATA ? 1 : 0);
@@ -668,8 +675,7 @@ __device__ __forceinline__ void fast_produce(const FJob& job, i4v span, const fl
 #pragma unroll
         for (int u = 0; u < kB; u++) x[u] = load_sample<FMT>(span, (n0 + kAvxLanes * u) * SB, 0);
     };
-    f2 xa[kB], xb[kB];
-    float cv[GH][NTT];
+    f2 xb[kB];
     int rslot = pp % rg;
     const int rstep = NG % rg;
     unsigned long long w_ring = 0, w_slot = 0, w_codes = 0, w_prod = 0;  // profiling: ring / slot waits, phase A / B
@@ -683,11 +689,13 @@ __device__ __forceinline__ void fast_produce(const FJob& job, i4v span, const fl
         const int n0 = kAvxLanes * (m_lo + GH * h) + l;
         const bool full = 4 * g + 4 <= S && G * (4 * g + 4) <= M;  // every task of the group whole
         const unsigned long long tA = GNSSHIP_FCLOCK();
-        first_samples(g, xa);  // in flight during phase A and the slot poll
-        if (full)
-            group_codes<NT, DATA, IN_MARGIN, GH, true>(code0, code1, L, n0, GH, step, rem, shifts, cv);
-        else
-            group_codes<NT, DATA, IN_MARGIN, GH, false>(code0, code1, L, n0, cnth, step, rem, shifts, cv);
+        if (!(pre && g == pp)) {  // (pre: the first group's phase A ran on the early arguments, fast_produce_early)
+            first_samples(g, xa);  // in flight during phase A and the slot poll
+            if (full)
+                group_codes<NT, DATA, IN_MARGIN, GH, true>(code0, code1, L, n0, GH, step, rem, shifts, cv);
+            else
+                group_codes<NT, DATA, IN_MARGIN, GH, false>(code0, code1, L, n0, cnth, step, rem, shifts, cv);
+        }
 #ifdef GNSSHIP_CORR_PROFILE
         for (int i = 0; i < GH; i++)  // phase A's code loads landed (profiling only)
             for (int q = 0; q < NTT; q++) asm volatile("" ::"v"(cv[i][q]));
@@ -752,6 +760,43 @@ __device__ __forceinline__ void fast_produce(const FJob& job, i4v span, const fl
         GNSSHIP_FVAL(pe, 79, w_codes);
         GNSSHIP_FVAL(pe, 80, w_prod);
     }
+}
+
+// Phase A of a producer's first group on the early arguments (FShared::early): the same samples and
+// code values fast_produce's first iteration forms from the job, issued while the control wave still
+// makes the seed.  Returns false when the group needs nothing early.
+template <int FMT, int NT, bool DATA, bool IN_MARGIN, int G, int W>
+__device__ __forceinline__ void fast_produce_early(const FJob& job, i4v span, const float* __restrict__ code0, const float* __restrict__ code1, int L,
+    int lane, int pw, f2 (&xa)[(G / producers_per_group<NT + (DATA ? 1 : 0), W, G>()) < 8 ? (G / producers_per_group<NT + (DATA ? 1 : 0), W, G>()) : 8],
+    float (&cv)[G / producers_per_group<NT + (DATA ? 1 : 0), W, G>()][NT + (DATA ? 1 : 0)])
+{
+    constexpr int SB = sample_bytes<FMT>();
+    constexpr int NTT = NT + (DATA ? 1 : 0);
+    constexpr int NH = producers_per_group<NTT, W, G>();
+    constexpr int GH = G / NH;
+    constexpr int kB = GH < 8 ? GH : 8;
+    const int M = job.M, S = job.S;
+    float shifts[NT];
+#pragma unroll
+    for (int q = 0; q < NT; q++) shifts[q] = job.shifts[q];
+    const int tl = lane >> 4, l = lane & (kAvxLanes - 1);
+    const int h = NH == 2 ? (pw & 1) : 0, g = NH == 2 ? (pw >> 1) : pw;
+    const int t = 4 * g + tl;
+    const bool active = t < S;
+    const int m_lo = G * (active ? t : 0);
+    const int cnt = active ? min(G, M - m_lo) : 0;
+    const int cnth = max(0, min(GH, cnt - GH * h));
+    const int n0 = kAvxLanes * (m_lo + GH * h) + l;
+    const bool full = 4 * g + 4 <= S && G * (4 * g + 4) <= M;
+    {
+        const int n0s = kAvxLanes * (G * (t < S ? t : 0) + GH * h) + l;
+#pragma unroll
+        for (int u = 0; u < kB; u++) xa[u] = load_sample<FMT>(span, (n0s + kAvxLanes * u) * SB, 0);
+    }
+    if (full)
+        group_codes<NT, DATA, IN_MARGIN, GH, true>(code0, code1, L, n0, GH, job.code_step, job.rem_code, shifts, cv);
+    else
+        group_codes<NT, DATA, IN_MARGIN, GH, false>(code0, code1, L, n0, cnth, job.code_step, job.rem_code, shifts, cv);
 }
 
 // ---- accumulator waves: the accumulation in u_avx's order ---------------------------------------
@@ -1173,7 +1218,7 @@ __global__ __launch_bounds__(W * kWave, (fast_waves_per_simd<THRU, W>())) void t
         sh.step_seq = 0;
         sh.pred_seq = 0;
         sh.verdict = 0;
-        sh.pll_seq = sh.dll_seq = 0;
+        sh.pll_seq = sh.dll_seq = sh.early_seq = 0;
 #ifdef GNSSHIP_EXP_SERIAL
         g_replay_done = 0;
 #endif
@@ -1257,6 +1302,23 @@ __global__ __launch_bounds__(W * kWave, (fast_waves_per_simd<THRU, W>())) void t
         smin_n = fminf(smin_n, shv_n[t]);
         smax_n = fmaxf(smax_n, shv_n[t]);
     }
+    // wave 0: the job's code and sample arguments for an epoch starting at absolute sample nir
+    auto code_fields = [&](FJob& j, uint64_t nir) __attribute__((always_inline)) {
+        const bool nw = uni(rc.narrow) != 0;
+        j.off = static_cast<int64_t>(nir - buf_first);
+        j.rem_code = __fmul_rn(static_cast<float>(rc.rem_code_phase_chips), spcf);
+        j.code_step = __fmul_rn(static_cast<float>(rc.code_phase_step_chips), spcf);
+#pragma unroll
+        for (int t = 0; t < 5; t++) j.shifts[t] = nw ? shv_n[t] : shv_w[t];
+        const float smin = nw ? smin_n : smin_w, smax = nw ? smax_n : smax_w;
+        const double span = static_cast<double>(j.code_step) * static_cast<double>(N > 0 ? N - 1 : 0);
+        const double lo = fmin(0.0, span) + smin - j.rem_code - 2.0;
+        const double hi = fmax(0.0, span) + smax - j.rem_code + 2.0;
+        j.in_margin = (isfinite(lo) && isfinite(hi) && lo >= -kCodeMargin && hi < static_cast<double>(L + kCodeMargin)) ? 1 : 0;
+        j.M = M;
+        j.S = S;
+        j.tail = tail;
+    };
     // wave 0: do_correlation_step's arguments for the epoch at nitems_read (all but the phasors)
     auto make_seed = [&](int e) {
         const bool runnable = e < max_rounds && (rc.state == 2 || rc.state == 3 || rc.state == 4) && rc.nitems_read >= buf_first &&
@@ -1271,22 +1333,9 @@ __global__ __launch_bounds__(W * kWave, (fast_waves_per_simd<THRU, W>())) void t
             FJob& j = sh.job;
             j.runnable = runnable ? 1 : 0;
             if (runnable) {
-                const bool nw = uni(rc.narrow) != 0;
-                j.off = static_cast<int64_t>(rc.nitems_read - buf_first);
-                j.rem_code = __fmul_rn(static_cast<float>(rc.rem_code_phase_chips), spcf);
-                j.code_step = __fmul_rn(static_cast<float>(rc.code_phase_step_chips), spcf);
-#pragma unroll
-                for (int t = 0; t < 5; t++) j.shifts[t] = nw ? shv_n[t] : shv_w[t];
-                const float smin = nw ? smin_n : smin_w, smax = nw ? smax_n : smax_w;
-                const double span = static_cast<double>(j.code_step) * static_cast<double>(N > 0 ? N - 1 : 0);
-                const double lo = fmin(0.0, span) + smin - j.rem_code - 2.0;
-                const double hi = fmax(0.0, span) + smax - j.rem_code + 2.0;
-                j.in_margin = (isfinite(lo) && isfinite(hi) && lo >= -kCodeMargin && hi < static_cast<double>(L + kCodeMargin)) ? 1 : 0;
+                code_fields(j, rc.nitems_read);
                 j.rem_carr = rem_carr;
                 j.step = stepf;
-                j.M = M;
-                j.S = S;
-                j.tail = tail;
             }
             // wave 1's speculative replay of this epoch (whole-epoch slots): confirmed here when its
             // remainder phase and step are the seed's floats, and the job goes out with the seed
@@ -1455,16 +1504,45 @@ __global__ __launch_bounds__(W * kWave, (fast_waves_per_simd<THRU, W>())) void t
                 GNSSHIP_FCLK(e, 13);
         }
     } else if (role == kRoleProducer) {
+        constexpr int NHp = producers_per_group<NTT, kFWaves, G>();
+        constexpr int GHp = G / NHp;
+        f2 xa[GHp < 8 ? GHp : 8];
+        float cv[GHp][NTT];
         for (int e = 0;; e++) {
             const int gbase = e * n_groups;  // the epoch's first product-group tag - 1
+            // the early arguments (state 4: published by the control wave before it makes the seed)
+            // let the first group's sample loads and code values start ahead of the job
+            int early_in = -1;  // the in_margin the early phase A ran with (-1: none)
+            FJob ej;
+            if (GNSSHIP_EARLY_JOB) {
+                while (__hip_atomic_load(&sh.early_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < e + 1 &&
+                       __hip_atomic_load(&sh.job_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < e + 1)
+                    __builtin_amdgcn_s_sleep(GNSSHIP_POLL_SLEEP);
+                if (__hip_atomic_load(&sh.early_seq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) >= e + 1) {
+                    ej = uniform_job(sh.early);
+                    const i4v espan = sample_span<FMT>(samples, ej.off, N);
+                    if (ej.in_margin)
+                        fast_produce_early<FMT, NT, DATA, true, G, kFWaves>(ej, espan, c0, c1, L, lane, pw, xa, cv);
+                    else
+                        fast_produce_early<FMT, NT, DATA, false, G, kFWaves>(ej, espan, c0, c1, L, lane, pw, xa, cv);
+                    early_in = ej.in_margin;
+                }
+            }
             wait_seq(&sh.job_seq, e + 1);
             const FJob job = uniform_job(sh.job);
             if (!job.runnable) break;
+                // the early phase A stands if it ran on the job's own arguments (it always does: the
+                // control wave publishes both from the same values; checked bit for bit)
+                const bool pre = early_in >= 0 && ej.off == job.off && early_in == job.in_margin && ej.M == job.M && ej.S == job.S &&
+                                 __builtin_bit_cast(uint32_t, ej.rem_code) == __builtin_bit_cast(uint32_t, job.rem_code) &&
+                                 __builtin_bit_cast(uint32_t, ej.code_step) == __builtin_bit_cast(uint32_t, job.code_step) &&
+                                 __builtin_bit_cast(uint32_t, ej.shifts[0]) == __builtin_bit_cast(uint32_t, job.shifts[0]) &&
+                                 __builtin_bit_cast(uint32_t, ej.shifts[NT - 1]) == __builtin_bit_cast(uint32_t, job.shifts[NT - 1]);
                 const i4v span = sample_span<FMT>(samples, job.off, N);
                 if (job.in_margin)
-                    fast_produce<FMT, NT, DATA, true, G, kFWaves>(job, span, c0, c1, L, Zs, rs, Pp, rg, ready, sh.acc_groups, gbase, lane, pw, e);
+                    fast_produce<FMT, NT, DATA, true, G, kFWaves>(job, span, c0, c1, L, Zs, rs, Pp, rg, ready, sh.acc_groups, gbase, lane, pw, e, pre, xa, cv);
                 else
-                    fast_produce<FMT, NT, DATA, false, G, kFWaves>(job, span, c0, c1, L, Zs, rs, Pp, rg, ready, sh.acc_groups, gbase, lane, pw, e);
+                    fast_produce<FMT, NT, DATA, false, G, kFWaves>(job, span, c0, c1, L, Zs, rs, Pp, rg, ready, sh.acc_groups, gbase, lane, pw, e, pre, xa, cv);
                 if (pw < 2) GNSSHIP_FSTAMP(e, 3 + pw);  // 3, 4: producers 0 and 1 done
                 if (pw == 0) {
                     // cn0_and_tracking_lock_status (:972-1029) on the LDS copy of its members, beside the loop update
@@ -1631,6 +1709,15 @@ __global__ __launch_bounds__(W * kWave, (fast_waves_per_simd<THRU, W>())) void t
                     const int64_t k_ifn = rc.if_num;
                     const double k_ifc = rc.if_cyc;
                     if (rc.state == 4) {
+                        // the next epoch's code and sample arguments to the producers first (their first
+                        // group's loads and code values start while the seed is made)
+                        if (GNSSHIP_EARLY_JOB && lane == 0) {
+                            const uint64_t nir = rc.epoch_start + static_cast<uint64_t>(rc.current_prn_length_samples);  // epoch_consume's
+                            if (e + 1 < max_rounds && nir >= buf_first && nir + vl <= buf_first + static_cast<uint64_t>(buf_len)) {
+                                code_fields(sh.early, nir);
+                                publish_seq(&sh.early_seq, e + 2);
+                            }
+                        }
                         epoch_consume(kp, rc);
                         make_seed(e + 1);
                         GNSSHIP_FSTAMP(e, 33);
