@@ -83,7 +83,7 @@ TRK_ENGINE_NAMES = {0: "none", 1: "trk_fast_kernel (latency form)", 2: "trk_fast
                     4: "round-based loop (trk_step_kernel + correlator)", 5: "trk_lane_kernel (throughput form, one 16-lane row per channel)"}
 # rotator dot-product variant (include/gnsship.h GNSSHIP_ROTATOR_*, job flag bits GNSSHIP_JOB_*)
 ROTATOR_GENERIC, ROTATOR_AVX, ROTATOR_AUTO = 0, 1, -1
-JOB_HIGH_DYN, JOB_ROTATOR_AVX = 1, 2
+JOB_HIGH_DYN, JOB_ROTATOR_AVX, JOB_ROTATOR_TREE = 1, 2, 4
 
 
 class TrkConf(ctypes.Structure):
@@ -200,6 +200,7 @@ _SIGNATURES = {
     "gnsship_corr_create": ([_vp, _i, _i, _vpp], _i),
     "gnsship_corr_set_local_code_and_taps": ([_vp, _i, _f32p, _f32p], _i),
     "gnsship_corr_set_high_dynamics_resampler": ([_vp, _i], _i),
+    "gnsship_corr_set_rotator": ([_vp, _i], _i),
     "gnsship_corr_run": ([_vp, _vp, _i, _i, _f, _f, _f, _f, _f, _f, _i, _f32p], _i),
     "gnsship_corr_destroy": ([_vp], _i),
     "gnsship_batch_create": ([_vp, _i, _vpp], _i),

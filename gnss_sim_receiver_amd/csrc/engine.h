@@ -156,6 +156,17 @@ hipError_t launch_corr_batch(const void* samples, int fmt, const DevJob* jobs, i
 int plan_chunks(std::vector<DevJob>& jobs, std::vector<ChunkDesc>& chunks, std::vector<WorkItem>& items, bool& any_multi, int64_t* n_anchors,
     ChunkClass* classes, int chunks_per_item, bool pair_by_code);
 
+// ---- Generic-rotator jobs in the reference's serial order (corr_serial.hip) ---------------------
+// One workgroup per job: the job's own DevJob (its slot in the chunk plan is an empty job), its
+// padded code replica (chip 0) and the output row.
+struct SerialJob {
+    DevJob job;
+    const float* code;
+    int32_t code_len;
+    int32_t out_index;
+};
+hipError_t launch_corr_serial(const void* samples, int fmt, const SerialJob* jobs, int n_jobs, float* out, hipStream_t stream);
+
 // ---- High-dynamics correlator (Dll_Pll_Conf::high_dyn; corr_hd_kernel.hip) -------------------
 // Replaces volk_gnsssdr_32f_xn_high_dynamics_resampler_32f_xn_generic + volk_gnsssdr_32fc_32f_
 // high_dynamic_rotator_dot_prod_32fc_xn_generic, the pair Cpu_Multicorrelator_Real_Codes runs when

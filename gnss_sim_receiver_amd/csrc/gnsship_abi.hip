@@ -421,12 +421,17 @@ struct gnsship_batch {
     // high-dynamics jobs (flags bit 0): correlated by corr_hd_kernel.hip after the main classes; their
     // slots in the main plan are empty jobs
     HdPlan hd;
+    // generic-rotator jobs in the reference's serial order (no AVX / TREE / HIGH_DYN flag):
+    // corr_serial.hip after the main classes, likewise empty slots in the main plan
+    std::vector<SerialJob> serial;
+    SerialJob* serial_dev = nullptr;
+    int serial_cap = 0;
 };
 
 static void batch_release(gnsship_batch* b)
 {
     hd_plan_free(b->hd);
-    void* ptrs[] = {b->jobs_dev, b->chunks_dev, b->items_dev, b->partials_dev, b->out_dev, b->anchors_dev};
+    void* ptrs[] = {b->jobs_dev, b->chunks_dev, b->items_dev, b->partials_dev, b->out_dev, b->anchors_dev, b->serial_dev};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     if (b->anchors_ready) (void)hipEventDestroy(b->anchors_ready);
@@ -468,12 +473,16 @@ extern "C" int gnsship_batch_set_jobs(gnsship_batch* b, const gnsship_corr_job* 
     if (int rc = sync_code_table(ctx)) return rc;
     b->jobs_host.resize(n_jobs);
     b->hd.jobs.clear();
+    b->serial.clear();
     int max_len = 1;
     for (int j = 0; j < n_jobs; j++) {
         const gnsship_corr_job& in = jobs[j];
         if (in.code_id < 0 || in.code_id >= static_cast<int>(ctx->codes_host.size()) || !ctx->codes_host[in.code_id].ptr)
             return fail(ctx, GNSSHIP_E_INVAL, "gnsship_batch_set_jobs: job refers to an unset code id");
-        if (in.flags & ~(GNSSHIP_JOB_HIGH_DYN | GNSSHIP_JOB_ROTATOR_AVX)) return fail(ctx, GNSSHIP_E_INVAL, "gnsship_batch_set_jobs: unknown job flags");
+        if (in.flags & ~(GNSSHIP_JOB_HIGH_DYN | GNSSHIP_JOB_ROTATOR_AVX | GNSSHIP_JOB_ROTATOR_TREE))
+            return fail(ctx, GNSSHIP_E_INVAL, "gnsship_batch_set_jobs: unknown job flags");
+        if ((in.flags & GNSSHIP_JOB_ROTATOR_AVX) && (in.flags & GNSSHIP_JOB_ROTATOR_TREE))
+            return fail(ctx, GNSSHIP_E_INVAL, "gnsship_batch_set_jobs: GNSSHIP_JOB_ROTATOR_AVX and _TREE are exclusive");
         if (in.flags & 1) {  // high-dynamics resampler/rotator: its own plan, an empty slot here
             HdJob h;
             if (!derive_hd_job(in, ctx->codes_host[in.code_id].ptr, ctx->codes_host[in.code_id].len, j, h))
@@ -489,6 +498,14 @@ extern "C" int gnsship_batch_set_jobs(gnsship_batch* b, const gnsship_corr_job* 
         if (!derive_job(in, ctx->codes_host[in.code_id].len, b->jobs_host[j]))
             return fail(ctx, GNSSHIP_E_INVAL, "gnsship_batch_set_jobs: invalid job (taps, length, offset or flags)");
         if (in.sample_offset + in.n_samples > n_buffer_samples) return fail(ctx, GNSSHIP_E_INVAL, "gnsship_batch_set_jobs: job reads past the sample buffer");
+        if (!(in.flags & (GNSSHIP_JOB_ROTATOR_AVX | GNSSHIP_JOB_ROTATOR_TREE))) {  // generic, serial order: its own kernel
+            const CodeDesc& cd = ctx->codes_host[in.code_id];
+            b->serial.push_back(SerialJob{b->jobs_host[j], cd.ptr, cd.len, j});
+            gnsship_corr_job empty = in;
+            empty.n_samples = 0;
+            derive_job(empty, cd.len, b->jobs_host[j]);
+            continue;
+        }
         if (ctx->codes_host[in.code_id].len > max_len) max_len = ctx->codes_host[in.code_id].len;
     }
     b->max_code_len = max_len;
@@ -524,6 +541,15 @@ extern "C" int gnsship_batch_set_jobs(gnsship_batch* b, const gnsship_corr_job* 
     }
     b->n_jobs = n_jobs;
     HIP_TRY(ctx, hd_plan_upload(b->hd, ctx->stream));
+    if (static_cast<int>(b->serial.size()) > b->serial_cap) {
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+        if (b->serial_dev) HIP_TRY(ctx, hipFree(b->serial_dev));
+        b->serial_dev = nullptr;
+        HIP_TRY(ctx, hipMalloc(&b->serial_dev, sizeof(SerialJob) * b->serial.size()));
+        b->serial_cap = static_cast<int>(b->serial.size());
+    }
+    if (!b->serial.empty())
+        HIP_TRY(ctx, hipMemcpyAsync(b->serial_dev, b->serial.data(), sizeof(SerialJob) * b->serial.size(), hipMemcpyHostToDevice, ctx->stream));
     if (n_jobs) {
         HIP_TRY(ctx, hipMemcpyAsync(b->jobs_dev, b->jobs_host.data(), sizeof(DevJob) * n_jobs, hipMemcpyHostToDevice, ctx->stream));
         HIP_TRY(ctx, hipMemcpyAsync(b->chunks_dev, b->chunks_host.data(), sizeof(ChunkDesc) * b->n_chunks, hipMemcpyHostToDevice, ctx->stream));
@@ -560,6 +586,8 @@ extern "C" int gnsship_batch_launch_stages(gnsship_batch* b, const void* dev_sam
         if (e != hipSuccess) return hip_fail(ctx, e, "launch_corr_batch(correlate)");
         e = launch_corr_hd(dev_samples, fmt, b->hd, b->out_dev, ctx->stream);
         if (e != hipSuccess) return hip_fail(ctx, e, "launch_corr_hd");
+        e = launch_corr_serial(dev_samples, fmt, b->serial_dev, static_cast<int>(b->serial.size()), b->out_dev, ctx->stream);
+        if (e != hipSuccess) return hip_fail(ctx, e, "launch_corr_serial");
         HIP_TRY(ctx, hipEventRecord(b->corr_done, ctx->stream));
     }
     return GNSSHIP_OK;
@@ -604,6 +632,8 @@ extern "C" int gnsship_batch_launch_pipelined2(gnsship_batch* b, const void* dev
     if (b->n_jobs > 0) {
         hipError_t e = launch_corr_hd(dev_samples, fmt, b->hd, b->out_dev, ctx->stream);
         if (e != hipSuccess) return hip_fail(ctx, e, "launch_corr_hd");
+        e = launch_corr_serial(dev_samples, fmt, b->serial_dev, static_cast<int>(b->serial.size()), b->out_dev, ctx->stream);
+        if (e != hipSuccess) return hip_fail(ctx, e, "launch_corr_serial");
     }
     b->anchor_segs = b->n_jobs > 0 ? kAnchorSegments : 0;
     if (p1) next->anchor_segs = kAnchorSegments;
@@ -665,6 +695,8 @@ struct gnsship_corr {
     Anchor* anchors_dev = nullptr;
     int chunk_cap = 0;
     HdPlan hd;  // set_high_dynamics_resampler(true): the high-dynamics kernels
+    int rotator = GNSSHIP_ROTATOR_GENERIC;  // gnsship_corr_set_rotator (resolved: GENERIC or AVX)
+    SerialJob* serial_dev = nullptr;        // the generic rotator's job (corr_serial.hip)
 };
 
 extern "C" int gnsship_corr_create(gnsship_ctx* ctx, int max_signal_length_samples, int n_correlators, gnsship_corr** out)
@@ -686,7 +718,7 @@ extern "C" int gnsship_corr_create(gnsship_ctx* ctx, int max_signal_length_sampl
     if (e == hipSuccess) e = hipMalloc(&c->items_dev, sizeof(WorkItem) * c->chunk_cap);
     if (e == hipSuccess) e = hipMalloc(&c->partials_dev, sizeof(float) * 2 * kMaxTaps * c->chunk_cap);
     if (e == hipSuccess) e = hipMalloc(&c->out_dev, sizeof(float) * 2 * kMaxTaps);
-    const size_t n_anc = (max_signal_length_samples + kRenorm - 1) / kRenorm + 1 + kAnchorPad;
+    const size_t n_anc = static_cast<size_t>(anchor_entries(max_signal_length_samples, true)) + 1 + kAnchorPad;  // either variant
     if (e == hipSuccess) e = hipMalloc(&c->anchors_dev, sizeof(Anchor) * n_anc);
     if (e == hipSuccess) e = hipMemset(c->anchors_dev, 0, sizeof(Anchor) * n_anc);
     if (e != hipSuccess) {
@@ -726,6 +758,18 @@ extern "C" int gnsship_corr_set_high_dynamics_resampler(gnsship_corr* c, int ena
     return GNSSHIP_OK;
 }
 
+extern "C" int gnsship_corr_set_rotator(gnsship_corr* c, int variant)
+{
+    if (!c) return GNSSHIP_E_INVAL;
+    if (variant == GNSSHIP_ROTATOR_AUTO) {
+        if (gnsship_rotator_dispatch(&variant) != GNSSHIP_OK)
+            return fail(c->ctx, GNSSHIP_E_INVAL, "gnsship_corr_set_rotator: the host's volk_gnsssdr preference names a rotator variant the engine does not reproduce");
+    }
+    if (variant != GNSSHIP_ROTATOR_GENERIC && variant != GNSSHIP_ROTATOR_AVX) return fail(c->ctx, GNSSHIP_E_INVAL, "gnsship_corr_set_rotator: unknown variant");
+    c->rotator = variant;
+    return GNSSHIP_OK;
+}
+
 extern "C" int gnsship_corr_run(gnsship_corr* c, const void* sig, int fmt, int sig_on_device, float rem_carr, float phase_step,
     float phase_rate_step, float rem_code, float code_step, float code_rate_step, int n, float* corr_out)
 {
@@ -740,7 +784,7 @@ extern "C" int gnsship_corr_run(gnsship_corr* c, const void* sig, int fmt, int s
     in.n_samples = n;
     in.code_id = 0;
     in.n_taps = c->n_taps;
-    in.flags = 0;
+    in.flags = c->rotator == GNSSHIP_ROTATOR_AVX ? GNSSHIP_JOB_ROTATOR_AVX : 0;
     in.rem_carrier_phase_rad = rem_carr;
     in.phase_step_rad = phase_step;
     in.phase_rate_step_rad = phase_rate_step;
@@ -768,6 +812,18 @@ extern "C" int gnsship_corr_run(gnsship_corr* c, const void* sig, int fmt, int s
     }
     std::vector<DevJob> jobs(1);
     if (!derive_job(in, c->code_len, jobs[0])) return fail(ctx, GNSSHIP_E_INVAL, "gnsship_corr_run: invalid job");
+    if (c->rotator == GNSSHIP_ROTATOR_GENERIC) {  // the generic rotator in the reference's order (corr_serial.hip)
+        if (!c->serial_dev) HIP_TRY(ctx, hipMalloc(&c->serial_dev, sizeof(SerialJob)));
+        const SerialJob sj{jobs[0], c->code_dev, c->code_len, 0};
+        HIP_TRY(ctx, hipMemcpyAsync(c->serial_dev, &sj, sizeof(sj), hipMemcpyHostToDevice, ctx->stream));
+        hipError_t e = launch_corr_serial(src, fmt, c->serial_dev, 1, c->out_dev, ctx->stream);
+        if (e != hipSuccess) return hip_fail(ctx, e, "launch_corr_serial");
+        float tmp[2 * kMaxTaps];
+        HIP_TRY(ctx, hipMemcpyAsync(tmp, c->out_dev, sizeof(tmp), hipMemcpyDeviceToHost, ctx->stream));
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+        std::memcpy(corr_out, tmp, sizeof(float) * 2 * c->n_taps);
+        return GNSSHIP_OK;
+    }
     std::vector<ChunkDesc> chunks;
     std::vector<WorkItem> items;
     bool multi = false;
@@ -779,7 +835,7 @@ extern "C" int gnsship_corr_run(gnsship_corr* c, const void* sig, int fmt, int s
     HIP_TRY(ctx, hipMemcpyAsync(c->chunks_dev, chunks.data(), sizeof(ChunkDesc) * nch, hipMemcpyHostToDevice, ctx->stream));
     HIP_TRY(ctx, hipMemcpyAsync(c->items_dev, items.data(), sizeof(WorkItem) * items.size(), hipMemcpyHostToDevice, ctx->stream));
     hipError_t e = launch_corr_batch(src, fmt, c->job_dev, 1, c->chunks_dev, c->items_dev, static_cast<int>(items.size()), classes, c->code_len, multi,
-        c->anchors_dev, c->partials_dev, c->out_dev, ctx->stream);
+        c->anchors_dev, c->partials_dev, c->out_dev, ctx->stream, GNSSHIP_STAGE_ANCHORS | GNSSHIP_STAGE_CORRELATE, nullptr, kAvxLanes);  // the AVX variant
     if (e != hipSuccess) return hip_fail(ctx, e, "launch_corr_batch");
     float tmp[2 * kMaxTaps];
     HIP_TRY(ctx, hipMemcpyAsync(tmp, c->out_dev, sizeof(tmp), hipMemcpyDeviceToHost, ctx->stream));
@@ -795,7 +851,7 @@ extern "C" int gnsship_corr_destroy(gnsship_corr* c)
     (void)hipStreamSynchronize(c->ctx->stream);
     (void)free_padded_code(c->code_dev);
     hd_plan_free(c->hd);
-    void* ptrs[] = {c->code_table_dev, c->sig_dev, c->job_dev, c->chunks_dev, c->items_dev, c->partials_dev, c->out_dev, c->anchors_dev};
+    void* ptrs[] = {c->code_table_dev, c->sig_dev, c->job_dev, c->chunks_dev, c->items_dev, c->partials_dev, c->out_dev, c->anchors_dev, c->serial_dev};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     delete c;

@@ -18,19 +18,24 @@
 //
 // Rotator variants (include/gnsship.h GNSSHIP_ROTATOR_*):
 //  * generic (volk_gnsssdr_32fc_32f_rotator_dot_prod_32fc_xn.h:66-98): one phasor, N dependent
-//    products per epoch, renormalised every 256 samples.  The replay is one lane; each 256-sample
-//    block is correlated with the block's exact anchors and the lane factor |inc|^j e^{ijΔ} (the
-//    batched correlator's scheme, corr_device.h correlate_block).
+//    products per epoch, renormalised every 256 samples, and ONE serial float sum per tap component
+//    (result[t] += (x·phase)·a_t[n], n = 0..N−1).  Reproduced bit for bit as a three-stage pipeline
+//    through LDS rings of 64-sample chunks: wave 0's lane 0 replays the phasor chain and stores the
+//    phase of every sample; waves 1-2 (alternate chunks, one lane per sample) form x·phase and its
+//    products with every tap's chip; wave 3's lane j < 2·taps (+2 for the data prompt) adds tap
+//    component j's products serially in sample order — the reference's own float sum.
 //  * AVX (…:155-316, what volk_gnsssdr dispatches on AVX hosts): 16 phasors z_l advanced by
 //    dz = normalise(inc^16), renormalised every 64 iterations.  The replay is 16 lanes × N/16 steps
 //    (16× shorter than the generic chain); it publishes z_l at every renormalisation, and the
 //    correlating lane of (segment, l) continues that lane's chain itself — the same float products
-//    in the same order, so every phasor is bit-identical to the reference's.
+//    in the same order, so every phasor is bit-identical to the reference's (the sums are trees;
+//    the exact AVX engines are trk_fast.hip and trk_lane.hip).
 //
 // High-dynamics tracking and epochs too long for LDS stay on the round-based path (trk_kernel.hip).
 #include <cstdlib>
 
 #include "corr_device.h"
+#include "serial_rotator.h"
 #include "trk_engine.h"
 
 // Epoch phase timestamps for the profiling build only (make prof → scripts/libgnsship_prof.so,
@@ -73,7 +78,8 @@ struct PEpoch {
     float dz_re, dz_im;  // normalise(inc^16) (AVX)
     int32_t runnable;
     int32_t in_margin;   // every chip index of the epoch lies in the padded LDS replica
-    int32_t published;   // anchors ready: generic blocks, or AVX segments (S + 1 = all, tail included)
+    int32_t published;   // AVX: segments whose anchors are ready (S + 1 = all, tail included)
+    SerialSync sync;     // generic: the serial pipeline's ring counters
     int32_t locked;      // lock_status outcome (wave 1) for the loop update (wave 0)
     double coh;          // epoch_pre's coherent integration time (0: no lock test this epoch)
     float trace_rem_carr, trace_step;  // the carrier arguments as passed (IF folded in)
@@ -104,34 +110,34 @@ __device__ __forceinline__ void wait_published(int32_t* p, int need)
 // then only ever fall after a task's last iteration.  The N mod 16 tail runs serially after them.
 __host__ __device__ __forceinline__ int avx_tasks(int M, int G) { return M <= 1 ? 1 : 1 + (M - 1 + G - 1) / G; }
 
-// ---- replays ---------------------------------------------------------------------------------
-// Generic (one lane): the anchors of every 256-sample block, as replay_anchors (anchor_replay.h).
-__device__ void replay_generic(const DevJob& job, Anchor* A, int nblk, int32_t* published)
+// ---- the generic rotator: serial pipeline (serial_rotator.h) ---------------------------------------
+// Ring of RC chunks in the dynamic LDS after the codes: phases, then 2·(taps + data prompt) product
+// rows per chunk.  The accumulator's lane j stores component j where the loop update reads it.
+template <int FMT, int NT, bool DATA>
+__device__ void serial_epoch(PEpoch& ep, float* anc, int RC, i4v span, int N, const float* c0, const float* c1, int L, int lane, int wave)
 {
-    const f2 inc = f2{job.inc_re, job.inc_im};
-    f2 p = f2{job.p0_re, job.p0_im};
-    for (int k = 0; k < nblk; k++) {
-        const float m = hypotf_glibc(p.x, p.y);  // sample 256k uses p; then p /= |p| (:86-92)
-        p = f2{__fdiv_rn(p.x, m), __fdiv_rn(p.y, m)};
-        Anchor a;
-        a.p[0] = p.x;
-        a.p[1] = p.y;
+    constexpr int TM = NT + (DATA ? 1 : 0);
+    SerialSync& sy = ep.sync;
+    f2* Zr = reinterpret_cast<f2*>(anc);
+    float* P = anc + 2 * kSChunk * RC;
+    if (wave == 0) {
+        if (lane == 0) serial_replay(sy, Zr, RC, N, f2{ep.job.p0_re, ep.job.p0_im}, f2{ep.job.inc_re, ep.job.inc_im});
+    } else if (wave < kPWaves - 1) {
+        const float* code[TM];
+        float shift[TM];
 #pragma unroll
-        for (int s = 1; s <= 16; s++) {
-            p = cmul_exact(p, inc);
-            if (s < 4) {
-                a.p[2 * s] = p.x;
-                a.p[2 * s + 1] = p.y;
-            }
+        for (int t = 0; t < TM; t++) {
+            code[t] = t < NT ? c0 : c1;
+            shift[t] = t < NT ? ep.job.shifts[t] : 0.0f;
         }
-        A[k] = a;
-        publish(published, k + 1);
-        if (k + 1 < nblk) {
-            for (int s0 = 16; s0 < kRenorm; s0 += 16) {
-#pragma unroll
-                for (int s = 0; s < 16; s++) p = cmul_exact(p, inc);
-            }
-        }
+        if (ep.in_margin)
+            serial_produce<FMT, TM, true>(sy, Zr, P, RC, span, N, TM, code, shift, L, ep.job.code_step, ep.job.rem_code, lane, wave - 1);
+        else
+            serial_produce<FMT, TM, false>(sy, Zr, P, RC, span, N, TM, code, shift, L, ep.job.code_step, ep.job.rem_code, lane, wave - 1);
+    } else {
+        const float acc = serial_accumulate(sy, P, RC, N, TM, lane);
+        // the taps' components, then the data prompt at 2·kMaxTaps (the other entries were zeroed)
+        if (lane < 2 * TM) ep.taps[lane < 2 * NT ? lane : 2 * kMaxTaps + lane - 2 * NT] = acc;
     }
 }
 
@@ -208,47 +214,7 @@ __device__ void replay_avx(const PEpoch& ep, f2* Z, f2* T, int N, int lane, int3
     }
 }
 
-// ---- correlation -------------------------------------------------------------------------------
-// Generic: blocks in publication order, one per wave step (64 lanes × 4 samples), with the block's
-// exact anchor and, once per epoch, the lane factor (corr_device.h correlate_block).
-template <int FMT, int NT, bool DATA, bool IN_MARGIN>
-__device__ void consume_generic(PEpoch& ep, const Anchor* A, i4v span, int N, const float* code0, const float* code1, int L, int lane,
-    int wave, f2 (&acc)[NT + 1])
-{
-    const DevJob& job = ep.job;
-    const int nblk = (N + kRenorm - 1) / kRenorm;
-    ChunkDesc ch;
-    ch.job = 0;
-    ch.start = 0;
-    ch.len = N;
-    ch.code_len = L;
-    ch.code = nullptr;
-    float shifts[NT];
-#pragma unroll
-    for (int t = 0; t < NT; t++) shifts[t] = job.shifts[t];
-    const float zero_shift[1] = {0.0f};
-    if (wave == 0) return;  // the replay wave
-    for (int kb = wave - 1; kb < nblk; kb += kPWaves - 1) {  // static: wave w ≥ 1 takes blocks w − 1 (mod 3)
-        f2 x[kLaneSamples];
-        load_any<FMT>(span, lane, kb, N, x);  // in flight while the anchor is awaited
-        wait_published(&ep.published, kb + 1);
-        const Anchor a = A[kb];
-        f2 ap[NT], ad[1];
-#pragma unroll
-        for (int t = 0; t < NT; t++) ap[t] = f2{0.0f, 0.0f};
-        ad[0] = f2{0.0f, 0.0f};
-        if ((kb + 1) * kRenorm <= N) {
-            correlate_block<NT, IN_MARGIN, true>(job, ch, a, shifts, code0, L, lane, kb, x, ap);
-            if constexpr (DATA) correlate_block<1, IN_MARGIN, true>(job, ch, a, zero_shift, code1, L, lane, kb, x, ad);
-        } else {
-            correlate_block<NT, IN_MARGIN, false>(job, ch, a, shifts, code0, L, lane, kb, x, ap);
-            if constexpr (DATA) correlate_block<1, IN_MARGIN, false>(job, ch, a, zero_shift, code1, L, lane, kb, x, ad);
-        }
-        for (int t = 0; t < NT; t++) acc[t] += ap[t];
-        if constexpr (DATA) acc[NT] += ad[0];
-    }
-}
-
+// ---- correlation (AVX) ---------------------------------------------------------------------------
 // AVX: wave step g = tasks 4g..4g+3 × the 16 phasors (64 lanes: lane = 16·(t − 4g) + l), each lane
 // continuing its phasor's chain over the task's ≤ G iterations (sample 16m + l at iteration m), 16
 // iterations per step with the next 16 samples in flight (the first 16 are loaded before the
@@ -349,7 +315,7 @@ __device__ void derive_epoch(PEpoch& ep, const TrkParams& k, const TrkChannel& c
     j.n_samples = static_cast<int32_t>(k.conf.vector_length);
     j.code_id = c.code_id;
     j.n_taps = NT;
-    j.rot_avx = 0;  // the batch lane-factor rule (this kernel's AVX path has its own replay)
+    j.rot_avx = 0;  // (the batch path's flag: this kernel has its own replays)
     j.p0_re = p0.x;
     j.p0_im = p0.y;
     j.inc_re = inc.x;
@@ -363,9 +329,6 @@ __device__ void derive_epoch(PEpoch& ep, const TrkParams& k, const TrkChannel& c
         d = normalise_avx(d);
         ep.dz_re = d.x;
         ep.dz_im = d.y;
-    } else {
-        j.dtheta = atan2(static_cast<double>(j.inc_im), static_cast<double>(j.inc_re));
-        j.log_mag_inc = static_cast<float>(log(hypot(static_cast<double>(j.inc_re), static_cast<double>(j.inc_im))));
     }
     // chip-index range (monotone in n): inside the padded replica the modulo is skipped (the data
     // prompt's shift 0 lies inside the taps' range)
@@ -432,7 +395,6 @@ __global__ __launch_bounds__(kPThreads, persist_waves_per_simd<THRU>()) void trk
     const float* c0 = code0 + kCodeMargin;
     const float* c1 = code1 + kCodeMargin;
     const int N = static_cast<int>(k.conf.vector_length);
-    Anchor* A = reinterpret_cast<Anchor*>(anc);
     f2* Z = reinterpret_cast<f2*>(anc);
     f2* T = AVX ? Z + (avx_tasks(N / kAvxLanes, avx_g) + 1) * kAvxLanes : nullptr;
     for (int e = 0; e < max_rounds; e++) {
@@ -462,6 +424,9 @@ __global__ __launch_bounds__(kPThreads, persist_waves_per_simd<THRU>()) void trk
                     sc.epoch_start = sc.nitems_read;
                 }
                 ep.published = 0;
+                ep.sync = SerialSync{};
+                if constexpr (!AVX)
+                    for (int i = 0; i < 2 * kMaxTaps + 2; i++) ep.taps[i] = 0.0f;
                 GNSSHIP_TRK_STAMP(e, 1);
             }
         }
@@ -488,37 +453,30 @@ __global__ __launch_bounds__(kPThreads, persist_waves_per_simd<THRU>()) void trk
             else
                 consume_avx<FMT, NT, DATA, false, THRU ? 4 : 16>(ep, Z, T, span, N, avx_g, c0, c1, L, lane, wave, acc);
         } else {
-            if (wave == 0 && lane == 0) replay_generic(ep.job, A, (N + kRenorm - 1) / kRenorm, &ep.published);
+            serial_epoch<FMT, NT, DATA>(ep, anc, avx_g, span, N, c0, c1, L, lane, wave);  // avx_g = the ring's chunks
             if (tid == 0) GNSSHIP_TRK_STAMP(e, 2);
-            if (ep.in_margin)
-                consume_generic<FMT, NT, DATA, true>(ep, A, span, N, c0, c1, L, lane, wave, acc);
-            else
-                consume_generic<FMT, NT, DATA, false>(ep, A, span, N, c0, c1, L, lane, wave, acc);
-            // anchor frame → sample frame: × E_{4·lane} (corr_kernel.hip)
-            const f2 er = lane_rotation(ep.job, kLaneSamples * lane);
-            const f2 esw = f2{-er.y, er.x};
-#pragma unroll
-            for (int t = 0; t <= NT; t++) acc[t] = cmul_pk(acc[t], er, esw);
         }
         if (lane == 0) GNSSHIP_TRK_STAMP(e, wave <= 1 ? 3 + wave : 14 + wave);  // waves 2, 3: slots 16, 17
-        constexpr int kOut = NT + (DATA ? 1 : 0);
+        if constexpr (AVX) {
+            constexpr int kOut = NT + (DATA ? 1 : 0);
 #pragma unroll
-        for (int t = 0; t < kOut; t++) {
-            const float sr = wave_sum(acc[t].x), si = wave_sum(acc[t].y);
-            if (lane == 0) {
-                ep.red[wave][2 * t] = sr;
-                ep.red[wave][2 * t + 1] = si;
+            for (int t = 0; t < kOut; t++) {
+                const float sr = wave_sum(acc[t].x), si = wave_sum(acc[t].y);
+                if (lane == 0) {
+                    ep.red[wave][2 * t] = sr;
+                    ep.red[wave][2 * t + 1] = si;
+                }
             }
-        }
-        if (lane == 0) GNSSHIP_TRK_STAMP(e, 18 + wave);  // wave sums stored: slots 18-21
-        __syncthreads();
-        // tap sums over the waves (each in the serial order w = 0..3), the data prompt at 2·kMaxTaps
-        if (tid < 2 * kMaxTaps + 2) {
-            const int v = tid < 2 * kMaxTaps ? tid : 2 * NT + (tid - 2 * kMaxTaps);
-            float s = 0.0f;
-            if (tid < 2 * NT || (DATA && tid >= 2 * kMaxTaps))
-                for (int w = 0; w < kPWaves; w++) s += ep.red[w][v];
-            ep.taps[tid] = s;
+            if (lane == 0) GNSSHIP_TRK_STAMP(e, 18 + wave);  // wave sums stored: slots 18-21
+            __syncthreads();
+            // tap sums over the waves (each in the serial order w = 0..3), the data prompt at 2·kMaxTaps
+            if (tid < 2 * kMaxTaps + 2) {
+                const int v = tid < 2 * kMaxTaps ? tid : 2 * NT + (tid - 2 * kMaxTaps);
+                float s = 0.0f;
+                if (tid < 2 * NT || (DATA && tid >= 2 * kMaxTaps))
+                    for (int w = 0; w < kPWaves; w++) s += ep.red[w][v];
+                ep.taps[tid] = s;
+            }
         }
         __syncthreads();
         const float* taps = ep.taps;
@@ -596,15 +554,22 @@ extern "C" int gnsship_debug_trk_profile(void* dev_buf)
 namespace gnsship {
 #endif
 
-// LDS bytes of the persistent kernel's dynamic region (codes + anchors) and, for the AVX rotator, the
-// task granularity G: 16 iterations where the anchors fit, else 32 or 64.
+// LDS bytes of the persistent kernel's dynamic region (codes + rings) and, for the AVX rotator, the
+// task granularity G (16 iterations where the anchors fit, else 32 or 64), for the generic rotator the
+// serial pipeline's ring chunks.
 static size_t persist_lds(const TrkParams& p, int code_cap_floats, bool avx, int* g_out)
 {
     const int N = static_cast<int>(p.conf.vector_length);
     const size_t codes = static_cast<size_t>(p.jobs_per_channel > 1 ? 2 : 1) * code_cap_floats * sizeof(float);
-    if (!avx) {
-        if (g_out) *g_out = 0;
-        return codes + static_cast<size_t>((N + kRenorm - 1) / kRenorm) * sizeof(Anchor);
+    if (!avx) {  // the serial pipeline's rings: 16 chunks where they fit, else 8 or 4 (g_out = RC)
+        const int na = 2 * (p.n_taps + (p.jobs_per_channel > 1 ? 1 : 0));
+        size_t bytes = 0;
+        for (int rc = 16; rc >= 4; rc /= 2) {
+            bytes = codes + serial_ring_bytes(rc, na);
+            if (g_out) *g_out = rc;
+            if (bytes <= kTrkPersistMaxLds) break;
+        }
+        return bytes;
     }
     size_t bytes = 0;
     for (int G = 16; G <= kAvxSeg; G *= 2) {

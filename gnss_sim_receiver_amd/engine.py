@@ -188,10 +188,13 @@ class Comm:
 
 
 class MultiCorrelatorRealCodes:
-    """Mirror of Cpu_Multicorrelator_Real_Codes (cpu_multicorrelator_real_codes.h:37-61)."""
+    """Mirror of Cpu_Multicorrelator_Real_Codes (cpu_multicorrelator_real_codes.h:37-61).  rotator: the
+    volk_gnsssdr rotator variant its Carrier_wipeoff_multicorrelator_resampler runs (abi.ROTATOR_*;
+    default AUTO = what the reference's dispatcher picks on this host)."""
 
-    def __init__(self, ctx: Context):
+    def __init__(self, ctx: Context, rotator: int = abi.ROTATOR_AUTO):
         self.ctx = ctx
+        self.rotator = rotator
         self.h = None
         self.n_correlators = 0
         self._out = None
@@ -203,6 +206,7 @@ class MultiCorrelatorRealCodes:
               "gnsship_corr_create", self.ctx.h)
         self.h = h
         self.n_correlators = n_correlators
+        check(self.ctx.lib.gnsship_corr_set_rotator(self.h, self.rotator), "gnsship_corr_set_rotator", self.ctx.h)
         return True
 
     def set_high_dynamics_resampler(self, use: bool):

@@ -63,10 +63,10 @@ extern "C" {
  * u_avx/a_avx kernel (:155-316; any AVX host without a volk_gnsssdr_config override): 16 phasors
  * advanced by normalise(inc^16), renormalised every 64 iterations.  The two differ by up to 1e-2
  * relative at 50 Msps with a 7 MHz IF, so the engine reproduces either one, selected per job / per
- * tracking engine.  Generic: the phasor at every renormalisation point is bit-identical, inside a
- * 256-sample block the engine applies the exact lane rotation (the reference's own ≤255-step rounding
- * walk, ~1e-6, is the only difference).  AVX: all 16 phasor lanes are replayed and continued with the
- * reference's float products, so every phasor is bit-identical (batch jobs and tracking engines).
+ * tracking engine.  Generic: the phasor chain and the serial float sum per tap component are
+ * replayed in the reference's order (bit-identical taps; GNSSHIP_JOB_ROTATOR_TREE selects the faster
+ * anchored tree sums for batch jobs).  AVX: all 16 phasor lanes are replayed and continued with the
+ * reference's float products, in u_avx's accumulation order in the tracking engines (bit-identical taps).
  * Default in every binding (Python TrkConf.defaults, the C++ mirror's Dll_Pll_Conf, tools/gnsship_rx):
  * GNSSHIP_ROTATOR_AUTO, i.e. what the reference itself would run on this host. */
 #define GNSSHIP_ROTATOR_GENERIC 0
@@ -75,6 +75,12 @@ extern "C" {
 /* gnsship_corr_job::flags bits */
 #define GNSSHIP_JOB_HIGH_DYN 1     /* high-dynamics resampler + rotator (set_high_dynamics_resampler) */
 #define GNSSHIP_JOB_ROTATOR_AVX 2  /* the AVX rotator variant (ignored with GNSSHIP_JOB_HIGH_DYN) */
+/* Generic rotator with the anchored parallel sums (the phasor bit-identical at every renormalisation
+ * point, the taps summed as a tree: within 1e-5 of the exact sum of the reference's float products,
+ * not in its serial order).  Without this flag (and without _AVX / _HIGH_DYN) a job runs the
+ * generic rotator in the reference's own order — one phasor chain and one serial float sum per tap
+ * component, bit-identical taps (one workgroup per job, latency ≈ the N-step chain). */
+#define GNSSHIP_JOB_ROTATOR_TREE 4
 /* The variant volk_gnsssdr's dispatcher would select for the rotator dot-product on this host:
  * VOLK_GENERIC set in the environment -> generic; an entry for the kernel in the volk_gnsssdr
  * preferences file ($VOLK_CONFIGPATH or $HOME/.volk_gnsssdr/volk_gnsssdr_config) -> that entry
@@ -141,6 +147,12 @@ int gnsship_corr_create(gnsship_ctx* ctx, int max_signal_length_samples, int n_c
 int gnsship_corr_set_local_code_and_taps(gnsship_corr* c, int code_length_chips, const float* local_code_in, const float* shifts_chips);
 /* set_high_dynamics_resampler (:163-167).  Default false, as Dll_Pll_Conf::high_dyn (dll_pll_conf.h:80). */
 int gnsship_corr_set_high_dynamics_resampler(gnsship_corr* c, int enable);
+/* Which volk_gnsssdr rotator variant the volk_gnsssdr_32fc_32f_rotator_dot_prod_32fc_xn call inside
+ * Carrier_wipeoff_multicorrelator_resampler (:123-124) runs as: GNSSHIP_ROTATOR_GENERIC (the handle's
+ * default; serial order, bit-identical taps), _AVX (u_avx: 16 phasor lanes) or _AUTO (what the
+ * dispatcher would pick on this host, gnsship_rotator_dispatch; E_INVAL if it names a variant the
+ * engine does not reproduce).  The C++ / Python mirrors default to _AUTO. */
+int gnsship_corr_set_rotator(gnsship_corr* c, int variant);
 /* Carrier_wipeoff_multicorrelator_resampler(...)  (:103-126).  `sig` is `fmt` samples; if
  * sig_on_device != 0 it is a device pointer (e.g. into a gnsship_dev_alloc ring), else host.
  * corr_out receives n_correlators complex<float> (2 floats each).  Synchronous. */
@@ -162,7 +174,7 @@ typedef struct gnsship_corr_job {
     int32_t n_samples;       /* correlation length (vector_length)                            */
     int32_t code_id;         /* code bank id                                                   */
     int32_t n_taps;          /* 1..GNSSHIP_MAX_TAPS                                            */
-    int32_t flags;           /* GNSSHIP_JOB_HIGH_DYN | GNSSHIP_JOB_ROTATOR_AVX                   */
+    int32_t flags;           /* GNSSHIP_JOB_HIGH_DYN | GNSSHIP_JOB_ROTATOR_AVX | _TREE           */
     float rem_carrier_phase_rad;
     float phase_step_rad;
     float phase_rate_step_rad;

@@ -73,6 +73,13 @@ public:
         high_dyn_ = use_high_dynamics_resampler;
         if (h_) gnsship_corr_set_high_dynamics_resampler(h_, high_dyn_ ? 1 : 0);
     }
+    // The volk_gnsssdr rotator variant (GNSSHIP_ROTATOR_*); default AUTO: what the reference's
+    // dispatcher runs on this host.  Not part of the reference class (volk chooses there).
+    bool set_rotator(int variant)
+    {
+        rotator_ = variant;
+        return !h_ || gnsship_corr_set_rotator(h_, rotator_) == GNSSHIP_OK;
+    }
     bool init(int max_signal_length_samples, int n_correlators)
     {
         std::lock_guard<std::mutex> lk(dev_->mutex());
@@ -80,6 +87,10 @@ public:
         n_ = n_correlators;
         if (gnsship_corr_create(dev_->ctx(), max_signal_length_samples, n_correlators, &h_) != GNSSHIP_OK) return false;
         gnsship_corr_set_high_dynamics_resampler(h_, high_dyn_ ? 1 : 0);
+        if (gnsship_corr_set_rotator(h_, rotator_) != GNSSHIP_OK) {
+            free_locked();
+            return false;
+        }
         return true;
     }
     // The reference borrows the pointers (:53-63); the device engine copies the code at this call.
@@ -132,6 +143,7 @@ private:
     }
     std::shared_ptr<Device> dev_;
     gnsship_corr* h_ = nullptr;
+    int rotator_ = GNSSHIP_ROTATOR_AUTO;
     int n_ = 0;
     bool high_dyn_ = false;  // Dll_Pll_Conf::high_dyn default (dll_pll_conf.h:80)
     std::complex<float>* out_ = nullptr;

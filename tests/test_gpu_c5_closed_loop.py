@@ -10,15 +10,12 @@ ibyte_to_complex.cc:39) and to the oracle converted to float.
 
 With the IF in the NCO the phase step is ≈ 0.9 rad per sample, and one ulp of phase_inc turns the
 carrier by ≈ 3e-3 rad over 50000 samples: the phasors must be glibc's cosf / sinf exactly, which the
-engine reproduces (glibc_sincosf.h).  The AVX engine (trk_fast.hip) then equals the oracle: every
-traced epoch's taps equal the oracle correlator's on the same arguments, and every record field
-equals the oracle loop's (test_gpu_trk.compare_exact).  The generic-rotator engine (trk_persist.hip)
-sums in a tree; it is held to the correlator contract (1e-5 on its own arguments, against the
-oracle's double-accumulated sums at N ≥ 5e4, where the reference's serial float sum is itself ~1e-5
-from the exact sum of its products: measured 1.09e-5 between the tree and the serial sum on B1I) and, for the loop, to compare_if's bounds: two loops
-whose correlation sums differ by ~1e-7 now and then round the float step one ulp apart, a ≈ 3e-3 rad
-prompt phase step, so Doppler and carrier phase are compared at 0.25 Hz / 0.05 rad, the code
-frequency at 5e-2 Hz and the code phase at 2e-4 chips (epoch boundaries, states and flags exact).
+engine reproduces (glibc_sincosf.h).  Both engines then equal the oracle: the AVX engine
+(trk_fast.hip) sums in u_avx's order, the generic engine (trk_persist.hip) keeps the generic rotator's
+one serial float sum per tap component (volk_gnsssdr_32fc_32f_rotator_dot_prod_32fc_xn.h:66-98);
+every traced epoch's taps equal the oracle correlator's on the same arguments, and every record
+field equals the oracle loop's (test_gpu_trk.compare_exact).  compare_if (the IF loop's bounds for
+two loops whose sums differ in order) is kept for callers that compare across variants.
 """
 import concurrent.futures as cf
 
@@ -113,15 +110,16 @@ def trace_errors(tr, xf, first, code, data_code, rotator_avx, long_n=None):
     return worst
 
 
-def trace_exact(tr, xf, first, code, data_code, label=""):
-    """Each traced channel-epoch of the AVX engine re-run on the oracle's u_avx correlator with the
-    device's own arguments: every tap (and the data prompt) equal, bit for bit."""
+def trace_exact(tr, xf, first, code, data_code, label="", avx=True):
+    """Each traced channel-epoch re-run on the oracle correlator of the engine's rotator variant (u_avx,
+    or the generic serial one) with the device's own arguments: every tap (and the data prompt)
+    equal, bit for bit."""
     from gnss_sim_receiver_amd import abi as A
     from oracle import oracle as O
     tr = tr[tr["n_samples"] > 0]
     jobs = check_trace(tr, xf, first, [code])
     jobs["code_id"] = 0
-    jobs["flags"] = A.JOB_ROTATOR_AVX
+    jobs["flags"] = A.JOB_ROTATOR_AVX if avx else 0
     ref = O.corr_batch(xf, jobs, [code], n_threads=8).astype(np.complex64)
     t = int(jobs["n_taps"][0])
     got = (tr["taps"][:, 0:2 * t:2] + 1j * tr["taps"][:, 1:2 * t:2]).astype(np.complex64)
@@ -140,11 +138,6 @@ def trace_exact(tr, xf, first, code, data_code, label=""):
 
 FS = 50e6
 F_IF = 7.161e6
-# The generic rotator's tree-summed taps against the reference's serial float sum at C5's N (one float
-# accumulator per tap, N = 50000 for GPS / B1I, 200000 for E1): the serial sum's own rounding walk
-# (√N half-ulps of the accumulator) is ~1e-5 of the taps there, so the tree, which is closer to the
-# exact sum, lands up to the measured figures below from it (DESIGN §4 lists them).  1e-5 where met.
-GENERIC_SERIAL = {"GPS": 1e-5, "GAL": 2.2e-5, "BDS": 1.2e-5}  # measured 9.17e-6, 2.058e-5, 1.092e-5 (round 5)
 IF_OF = {"GPS": F_IF, "GAL": F_IF, "BDS": -F_IF}
 
 
@@ -152,8 +145,7 @@ IF_OF = {"GPS": F_IF, "GAL": F_IF, "BDS": -F_IF}
 @pytest.mark.parametrize("system,epochs", [("GPS", 300), ("GAL", 60), ("BDS", 300)])
 def test_c5_channel_closed_loop_ibyte_if(ctx, system, epochs, avx):
     """One channel per system at 50 Msps, ibyte, IF fused into the NCO, both rotator variants."""
-    sat, k, x, stamp, first, delay, dop = S.sync(system, FS, epochs, f_if_hz=IF_OF[system], rotator_avx=1 if avx else 0,
-                                                 accum_f64=0 if avx else 1, cn0=48.0)
+    sat, k, x, stamp, first, delay, dop = S.sync(system, FS, epochs, f_if_hz=IF_OF[system], rotator_avx=1 if avx else 0, cn0=48.0)
     raw = signals.to_ibyte(x)
     xf = raw.astype(np.float32).view(np.complex64)
     c = dev_conf(k, system)
@@ -169,19 +161,10 @@ def test_c5_channel_closed_loop_ibyte_if(ctx, system, epochs, avx):
     trk.close()
     ref = T.track(k, xf, sat.code, delay, dop, stamp, first, epochs, data_code=sat.code_data, buffer_first=first, prn=sat.prn)
     assert len(ref) == epochs and ref["state"][-1] in (3, 4), np.bincount(ref["state"])
-    if avx:  # bit-exact: the taps on the device's own arguments, then the loop
-        trace_exact(tr, xf, first, sat.code, sat.code_data, f"C5 {system}")
-        compare_exact(rec[:, 0], ref, f"C5 {system} avx")
-    else:
-        # the generic engine's tree sums against the reference's serial float sum (the plain oracle) —
-        # held to 1e-5 where they meet it and to the measured excess where they do not (GENERIC_SERIAL,
-        # DESIGN §4) — and to 1e-5 against the exact sum of the same float products (double accumulation)
-        e_serial = trace_errors(tr, xf, first, sat.code, sat.code_data, avx, long_n=False)
-        e_exact = trace_errors(tr, xf, first, sat.code, sat.code_data, avx, long_n=True)
-        print(f"C5 {system} generic: max per-tap error {e_serial:.3e} vs the serial float sum, {e_exact:.3e} vs the exact sum")
-        assert e_serial <= GENERIC_SERIAL[system], (system, e_serial)
-        assert e_exact <= TOL, (system, e_exact)
-        compare_if(rec[:, 0], ref, f"C5 {system} generic")
+    # bit-exact, both variants: the taps on the device's own arguments (u_avx order, or the generic
+    # rotator's one serial float sum per tap component), then every record field of the loop
+    trace_exact(tr, xf, first, sat.code, sat.code_data, f"C5 {system} avx={avx}", avx=avx)
+    compare_exact(rec[:, 0], ref, f"C5 {system} avx={avx}")
     # the IF is wiped off: the loop holds the signal's Doppler (± the narrow-loop walk), not Doppler + IF
     assert np.all(np.abs(ref[-20:]["carrier_doppler_hz"] - sat.doppler_hz) < 200.0)
 

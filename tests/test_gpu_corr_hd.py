@@ -133,7 +133,7 @@ def test_hd_invalid_tap_shifts_rejected(ctx):
     with pytest.raises(abi.GnssHipError):
         b.set_jobs(j, 8000)
     j["shifts_chips"][0, :3] = [-0.25, 0.0, 0.25]
-    j["flags"] = 4  # no such job flag (1 = high_dyn, 2 = AVX rotator)
+    j["flags"] = 8  # no such job flag (1 = high_dyn, 2 = AVX rotator, 4 = anchored tree sums)
     with pytest.raises(abi.GnssHipError):
         b.set_jobs(j, 8000)
     b.close()

@@ -4,9 +4,9 @@ loop (oracle/trk_oracle.c), for both volk_gnsssdr rotator variants the reference
 north_star's 25 Msps rates (GPS L1 C/A N = 25000, Galileo E1 N = 100000 — C3/C4's sampling rate).
 
 The AVX variant runs trk_fast.hip, which reproduces u_avx's products and accumulation order, glibc's
-phasor trig and the loop's libm calls: its records equal the oracle loop's (test_gpu_trk.compare_exact).  The generic variant (trk_persist.hip, tree sums) is held to test_gpu_trk.compare's
-tolerances: exact epoch boundaries / states / flags, Doppler and code frequency ≤ 2e-3, remnant code
-phase ≤ 1e-5 chip, CN0 ≤ 5e-3 dB, prompt ≤ 1e-4 relative.
+phasor trig and the loop's libm calls; the generic variant runs trk_persist.hip's serial pipeline,
+which reproduces the generic rotator's phasor chain and its one serial float sum per tap component.
+Both variants' records equal the oracle loop's (test_gpu_trk.compare_exact).
 """
 import os
 
@@ -17,21 +17,15 @@ from gnss_sim_receiver_amd import abi, engine
 from oracle import trk as T
 
 import trk_scenarios as S
-from test_gpu_trk import compare, compare_exact, dev_conf
+from test_gpu_trk import compare_exact, dev_conf
 
 pytestmark = pytest.mark.gpu
 
 
 def run_pair(ctx, system, fs, epochs, avx, n_ch=2, **kw):
-    """One channel (index 1) synchronising to state 4 on the device and in the oracle.  Generic
-    rotator at N ≥ 1e5: the oracle sums its float products in double (accum_f64): the reference's
-    serial float sum is itself ~1e-5 off the exact sum there (DESIGN.md §4 'Long integrations'), and
-    the loop turns that into ~0.07 Hz of Doppler walk, so the device's tree sums are held to the loop
-    on the exact sums of the same products.  The AVX engine sums in the reference's own order and is
-    compared with the plain oracle."""
-    vl = int(round(fs * T.SYSTEMS[system][2]))
-    long_n = 1 if (vl >= 100000 and not avx) else 0
-    sat, k, x, stamp, first, delay, dop = S.sync(system, fs, epochs, rotator_avx=1 if avx else 0, accum_f64=long_n, **kw)
+    """One channel (index 1) synchronising to state 4 on the device and in the oracle (both rotator
+    variants sum in the reference's own order and are compared with the plain oracle)."""
+    sat, k, x, stamp, first, delay, dop = S.sync(system, fs, epochs, rotator_avx=1 if avx else 0, **kw)
     c = dev_conf(k, system)
     c.rotator = abi.ROTATOR_AVX if avx else abi.ROTATOR_GENERIC
     trk = engine.DllPllVemlTracking(ctx, c, n_ch)
@@ -60,7 +54,7 @@ def test_closed_loop_25msps_matches_oracle(ctx, system, epochs, avx):
     N = 100000 with the data prompt (configs[3]'s per-channel epoch, dll_pll_veml_tracking.cc:1728-2094)."""
     rec, rounds, ref = run_pair(ctx, system, 25e6, epochs, avx=avx)
     assert ref["state"][-1] == 4
-    (compare_exact if avx else compare)(rec[:, 1], ref, f"{system} 25 Msps avx={avx}")
+    compare_exact(rec[:, 1], ref, f"{system} 25 Msps avx={avx}")
 
 
 def test_galileo_e1_50msps_avx_matches_oracle(ctx):
@@ -145,7 +139,7 @@ def test_many_channels_and_ragged_buffers(ctx):
     for ch in (0, 5, 7, 40):
         ref = T.track(k, x, sats[ch].code, starts[ch][0], starts[ch][1], 0, 0, 200)
         d = np.concatenate([r1[:, ch][(r1[:, ch]["flags"] & 8) == 8], r2[:, ch][(r2[:, ch]["flags"] & 8) == 8]])
-        compare(d[:len(ref)], ref[:len(d)], f"ch{ch}")
+        compare_exact(d[:len(ref)], ref[:len(d)], f"ch{ch}")
 
 
 @pytest.mark.parametrize("avx", [False, True])
@@ -162,7 +156,7 @@ def test_telemetry_fault_forces_loss_of_lock(ctx, avx):
     ref_ch = T.Channel(k, sat.code, delay, dop, stamp, first)
     r1, _ = trk.run(x, first, 120)
     o1 = ref_ch.run(x, first, 120)
-    cmp = compare_exact if avx else compare
+    cmp = compare_exact
     cmp(r1[:, 0], o1, "before")
     trk.telemetry_event(0, 2)  # not a fault: ignored
     trk.telemetry_event(0, 1)
