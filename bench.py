@@ -100,11 +100,13 @@ class Receiver:
             ctx.set_code(code_base + 2 * i, s.code)
             if s.code_data is not None:
                 ctx.set_code(code_base + 2 * i + 1, s.code_data)
+        starts = []
         for ch in range(n_ch):
             i = ch % len(sats)
             s = sats[i]
-            self.trk.start(ch, code_base + 2 * i, signals.acq_delay_samples(s, fs, 0, first), s.doppler_hz, 0, first,
-                           data_code_id=code_base + 2 * i + 1, prn=s.prn)
+            starts.append((ch, code_base + 2 * i, signals.acq_delay_samples(s, fs, 0, first), s.doppler_hz, 0, first,
+                           code_base + 2 * i + 1, s.prn))
+        self.trk.start_many(starts)  # one transaction (gnsship_trk_start_many)
 
     def run(self, dev_ptr, fmt, first, n):
         return self.trk.run_ptr(dev_ptr, fmt, first, n, 1 << 20)
@@ -179,25 +181,42 @@ def headline(ctx, torch, args, rank, world, device, barrier):
                 first=first, records=n_rec)
 
 
-def sweep(ctx, h, rot, counts, rounds=1000):
+SWEEP_PRE = 450  # epochs: every channel bit-synchronised (state 4) before a sweep point's timed epochs
+
+
+def sweep_file_25msps(torch, device, rounds=1000):
+    """The 25 Msps sweep's file: the same 32-satellite GPS sky model (navigation bits with the
+    preamble), long enough for the pre-roll and `rounds` timed epochs of N = 25000, resident in HBM."""
+    from gnss_sim_receiver_amd import signals
+    fs, vl = 25_000_000, 25000
+    sats = gps_sky(seed=SEED + 25)
+    first = int(T_START_S * fs)
+    n = (SWEEP_PRE + rounds + 8) * vl
+    x = signals.generate_if_device(fs, n, sats, seed=SEED + 25, start=first - 2 * vl, device=f"cuda:{device}")
+    torch.cuda.synchronize()
+    return dict(x=x, base=(x.data_ptr(), first - 2 * vl), first=first, sats=sats, fs=fs, vl=vl)
+
+
+def sweep(ctx, h, rot, counts, rounds=1000, fs=FS, vl=VL):
     """Tracked channels sustained: channels c -> satellite c mod 32 on the same file, each point run
-    for `rounds` epochs (1 s of signal) from the steady-state point of the headline run, every
-    channel-epoch's record (the Gnss_Synchro the reference emits, dll_pll_veml_tracking.cc:2063-2091)
-    copied to the host inside the timed region."""
+    for `rounds` epochs (1 s of signal) from the steady-state point of the file, every channel-epoch's
+    record (the Gnss_Synchro the reference emits, dll_pll_veml_tracking.cc:2063-2091) copied to the
+    host inside the timed region.  fs / vl: the file's rate and the GPS vector_length (4 Msps: 4000,
+    the headline's file; 25 Msps: 25000, gps_l1_ca_dll_pll_tracking.cc:47)."""
     from gnss_sim_receiver_amd import abi
     out = []
     t_abs = h["first"]
-    pre = 450  # epochs: every channel bit-synchronised (state 4) before the timed epochs
+    pre = SWEEP_PRE
     for n in counts:
-        rx = Receiver(ctx, "GPS", FS, VL, h["sats"], n, t_abs, rot, code_base=2000)
-        n_samp = rounds * VL + 4 * VL
+        rx = Receiver(ctx, "GPS", fs, vl, h["sats"], n, t_abs, rot, code_base=2000)
+        n_samp = rounds * vl + 4 * vl
         # untimed: the pre-roll, with records on and the timed run's round count, so the device record
         # buffer is sized here; the host record array is allocated and touched here too
-        rx.trk.launch_ptr(h["base"][0] + (t_abs - h["base"][1]) * 8, 0, t_abs, (pre + 2) * VL, rounds + 4, records=True)
+        rx.trk.launch_ptr(h["base"][0] + (t_abs - h["base"][1]) * 8, 0, t_abs, (pre + 2) * vl, rounds + 4, records=True)
         rx.trk.collect()
         host = np.empty((rounds + 4, n), abi.TRK_EPOCH_DTYPE)
         host.view(np.uint8).fill(0)
-        lo = t_abs + pre * VL
+        lo = t_abs + pre * vl
         ctx.event_record(2)
         t0 = time.perf_counter()
         rx.trk.launch_ptr(h["base"][0] + (lo - h["base"][1]) * 8, 0, lo, n_samp, rounds + 4, records=True)
@@ -495,8 +514,8 @@ def acq_c3_sharded(ctx, torch, rank, world, device, barrier, reps=20):
             "fanout": COMM["transport"]}
 
 
-def c1_receiver(torch, device, seconds=10.0, cpu_seconds=1.0):
-    """BASELINE configs[0] (C1): a 10-s 4 Msps gr_complex file with GPS PRN 7 (fD 1730 Hz, delay 1234
+def c1_receiver(torch, device, seconds=15.0, cpu_seconds=1.0):
+    """BASELINE configs[0] (C1): a 15-s 4 Msps gr_complex file with GPS PRN 7 (fD 1730 Hz, delay 1234
     samples) through the Channel role end to end — tools/gnsship_rx (include/gnsship_receiver.hpp:
     5 channels, 1 in acquisition, pfa 0.01, ±10 kHz / 250 Hz, pll 40 / dll 4 — conf/gnss-sdr_GPS_L1_
     gr_complex.conf) — timed as a process over the file; beside it the oracle restatement of the same
@@ -523,7 +542,8 @@ def c1_receiver(torch, device, seconds=10.0, cpu_seconds=1.0):
     summ = json.loads(out.stdout.strip().splitlines()[-1])
     ev = np.loadtxt(os.path.join(d, "ev.csv"), delimiter=",", skiprows=1, ndmin=2)
     pos = ev[ev[:, 2] == 1]
-    res = {"config": "C1 (configs[0]): GPS L1 C/A PRN 7, 4 Msps gr_complex file, 10 s; 5 channels, 1 in acquisition, pfa 0.01, "
+    res = {"config": f"C1 (configs[0]): GPS L1 C/A PRN 7, 4 Msps gr_complex file, {seconds:g} s (past the 10 s pull-in: bit sync, "
+                     "state 4); 5 channels, 1 in acquisition, pfa 0.01, "
                      "dmax 10000 / step 250, pll 40 / dll 4 (conf/gnss-sdr_GPS_L1_gr_complex.conf) — tools/gnsship_rx end to end",
            "signal_s": summ["signal_s"], "process_wall_s": round(wall, 3), "receiver_wall_s": round(summ["wall_s"], 3),
            "init_s": round(summ["init_s"], 3), "file_read_s": round(summ["io_s"], 3),
@@ -1026,8 +1046,22 @@ def main():
         result["tracked_channels_note"] = ("the largest channel count of the sweep measured at >= real time: 1 s of signal (1000 epochs) per "
                                            "point, every channel-epoch record copied to the host inside the timed run; each point names the "
                                            "kernel its timed launch ran (gnsship_trk_last_engine): with the AVX rotator, trk_fast_kernel's "
-                                           "latency form up to one workgroup per CU, its throughput form (the same u_avx accumulation order, "
-                                           "several workgroups per CU, channels beyond the resident ones in successive workgroup generations) above")
+                                           "latency form up to one workgroup per CU, trk_lane_kernel above (one 16-lane row per channel, "
+                                           "u_avx's own accumulation order, channels beyond the resident ones in successive workgroup generations)")
+        # north_star's second rate: the same sweep on a 25 Msps file (N = 25000)
+        f25 = guarded(sweep_file_25msps, torch, device)
+        if "x" in f25:
+            sw25 = guarded(sweep, ctx, f25, h["rotator"], [12, 1024, 4096, 8192, 16384, 24576, 28672, 32768], fs=f25["fs"], vl=f25["vl"])
+            del f25
+            torch.cuda.empty_cache()
+            if isinstance(sw25, list):
+                rt25 = [r["channels"] for r in sw25 if r["realtime_factor"] >= 1.0]
+                result["tracked_channels_sustained_25msps"] = max(rt25) if rt25 else 0
+                result["channel_sweep_25msps"] = sw25
+            else:
+                result["channel_sweep_25msps"] = sw25
+        else:
+            result["channel_sweep_25msps"] = f25
         if h["rotator"] != 0:
             g = Receiver(ctx, "GPS", FS, VL, [h["sats"][i] for i in range(N_CH)], N_CH, h["first"], 0, code_base=800)
             pre = int(round(PRE_ROLL_S * FS))
@@ -1058,6 +1092,19 @@ def main():
     if world > 1 and not args.no_aux:
         result["streaming_broadcast"] = guarded(streaming_broadcast, ctx, torch, rank, world, device, barrier, h)
     del h
+    # the line's key figures once more at its end (a reader of the line's tail sees them)
+    def pick(key, field):
+        v = result.get(key)
+        return v.get(field) if isinstance(v, dict) else None
+    result["summary"] = {"value_msps": result["value"], "us_per_epoch": result["us_per_epoch"], "roofline_frac": roof["frac"],
+                         "cpu_baseline_msps": pick("cpu_baseline", "value"),
+                         "tracked_channels_sustained": result.get("tracked_channels_sustained"),
+                         "tracked_channels_sustained_25msps": result.get("tracked_channels_sustained_25msps"),
+                         "gps_25msps_realtime": pick("closed_loop_gps_25msps", "realtime_factor"),
+                         "e1_c4_share_realtime": pick("closed_loop_e1_25msps_c4_share", "realtime_factor"),
+                         "c5_share_realtime": pick("closed_loop_c5_share", "realtime_factor"),
+                         "generic_rotator_realtime": pick("closed_loop_generic_rotator", "realtime_factor"),
+                         "c3_sweep_ms": pick("acquisition_c3", "sweep_ms"), "e1_sweep_ms": pick("acquisition_e1", "sweep_ms")}
     if rank == 0:
         print(json.dumps(result), flush=True)
     if COMM["comm"] is not None:

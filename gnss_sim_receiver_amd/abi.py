@@ -228,6 +228,7 @@ _SIGNATURES = {
     "gnsship_acq_resampler_destroy": ([_vp], _i),
     "gnsship_trk_create": ([_vp, ctypes.POINTER(TrkConf), _i, _vpp], _i),
     "gnsship_trk_start": ([_vp, _i, ctypes.POINTER(TrkStartArgs)], _i),
+    "gnsship_trk_start_many": ([_vp, _i, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(TrkStartArgs)], _i),
     "gnsship_trk_stop": ([_vp, _i], _i),
     "gnsship_trk_telemetry_event": ([_vp, _i, _i], _i),
     "gnsship_trk_run": ([_vp, _vp, _i, _i, ctypes.c_uint64, ctypes.c_int64, _i, _vp, ctypes.POINTER(_i)], _i),

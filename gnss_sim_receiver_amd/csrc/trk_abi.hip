@@ -67,6 +67,8 @@ struct gnsship_trk {
     size_t ran_cap = 0;
     void* stage_dev = nullptr;
     size_t stage_cap = 0;
+    void* start_stage_dev = nullptr;  // gnsship_trk_start_many's staged channel states + indices
+    size_t start_stage_cap = 0;
     // high_dyn: the high-dynamics correlator's fixed plan (one HdJob per job, out_index = job) and
     // the channels' rate-smoother rings
     bool high_dyn = false;
@@ -306,7 +308,7 @@ hipError_t upload_hd_code(gnsship_trk* t, int job, const CodeDesc& cd)
 void release(gnsship_trk* t)
 {
     void* ptrs[] = {t->params_dev, t->chans_dev, t->jobs_dev, t->chunks_dev, t->items_dev, t->anchors_dev, t->partials_dev, t->out_dev, t->rec_dev,
-        t->ran_dev, t->stage_dev, t->hist_dev, t->dump_dev, t->trace_dev};
+        t->ran_dev, t->stage_dev, t->hist_dev, t->dump_dev, t->trace_dev, t->start_stage_dev};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     hd_plan_free(t->hd);
@@ -441,10 +443,10 @@ extern "C" int gnsship_trk_create(gnsship_ctx* ctx, const gnsship_trk_conf* conf
     return GNSSHIP_OK;
 }
 
-// start_tracking (:643-883) and the state-1 pull-in (:1757-1788) at nitems_read = first_sample.
-extern "C" int gnsship_trk_start(gnsship_trk* t, int channel, const gnsship_trk_start_args* a)
+// start_tracking (:643-883) and the state-1 pull-in (:1757-1788) at nitems_read = first_sample: the
+// channel's state on the host (validated), and the channel's jobs' code ids in the host tables.
+static int trk_start_state(gnsship_trk* t, int channel, const gnsship_trk_start_args* a, TrkChannel& c)
 {
-    if (!t) return GNSSHIP_E_INVAL;
     gnsship_ctx* ctx = t->ctx;
     if (!a || channel < 0 || channel >= t->max_channels) return fail(ctx, GNSSHIP_E_INVAL, "gnsship_trk_start: bad channel / arguments");
     if (a->code_id < 0 || a->code_id >= static_cast<int>(ctx->codes_host.size()) || !ctx->codes_host[a->code_id].ptr)
@@ -453,7 +455,6 @@ extern "C" int gnsship_trk_start(gnsship_trk* t, int channel, const gnsship_trk_
     if (p.track_pilot && (a->data_code_id < 0 || a->data_code_id >= static_cast<int>(ctx->codes_host.size()) || !ctx->codes_host[a->data_code_id].ptr))
         return fail(ctx, GNSSHIP_E_STATE, "gnsship_trk_start: data code not in the code bank");
     if (a->first_sample < a->acq_samplestamp_samples) return fail(ctx, GNSSHIP_E_INVAL, "gnsship_trk_start: first_sample before the acquisition stamp");
-    TrkChannel c;
     std::memset(&c, 0, sizeof(c));
     const gnsship_trk_conf& k = p.conf;
     c.code_id = a->code_id;
@@ -500,24 +501,105 @@ extern "C" int gnsship_trk_start(gnsship_trk* t, int channel, const gnsship_trk_
         c.if_num = static_cast<int64_t>(prod % fsu);
         c.if_cyc = static_cast<double>(c.if_num) / static_cast<double>(p.fs_int);
     }
-    if (int rc = set_device(ctx)) return rc;
-    // the channel's chunks carry its code replica(s): only the code fields are rewritten (the
-    // device owns the lengths)
+    // the channel's chunks carry its code replica(s) (host tables; the caller uploads them)
     for (int q = 0; q < p.jobs_per_channel; q++) {
         const int job = channel * p.jobs_per_channel + q;
         t->job_code[job] = q == 0 ? c.code_id : c.data_code_id;
         const CodeDesc& cd = ctx->codes_host[t->job_code[job]];
         for (int m = 0; m < p.chunks_per_job; m++) {
-            const int ci = t->jobs_first_chunk[job] + m;
-            ChunkDesc& d = t->chunks_host[ci];
+            ChunkDesc& d = t->chunks_host[t->jobs_first_chunk[job] + m];
             d.code = cd.ptr;
             d.code_len = cd.len;
+        }
+    }
+    return GNSSHIP_OK;
+}
+
+extern "C" int gnsship_trk_start(gnsship_trk* t, int channel, const gnsship_trk_start_args* a)
+{
+    if (!t) return GNSSHIP_E_INVAL;
+    gnsship_ctx* ctx = t->ctx;
+    TrkChannel c;
+    if (int rc = trk_start_state(t, channel, a, c)) return rc;
+    if (int rc = set_device(ctx)) return rc;
+    const TrkParams& p = t->params;
+    // only the chunks' code fields are rewritten (the device owns the lengths)
+    for (int q = 0; q < p.jobs_per_channel; q++) {
+        const int job = channel * p.jobs_per_channel + q;
+        for (int m = 0; m < p.chunks_per_job; m++) {
+            const int ci = t->jobs_first_chunk[job] + m;
+            const ChunkDesc& d = t->chunks_host[ci];
             HIP_TRY(ctx, hipMemcpyAsync(reinterpret_cast<char*>(t->chunks_dev + ci) + offsetof(ChunkDesc, code_len), &d.code_len,
                              sizeof(ChunkDesc) - offsetof(ChunkDesc, code_len), hipMemcpyHostToDevice, ctx->stream));
         }
-        if (t->high_dyn) HIP_TRY(ctx, upload_hd_code(t, job, cd));
+        if (t->high_dyn) HIP_TRY(ctx, upload_hd_code(t, job, ctx->codes_host[t->job_code[job]]));
     }
     HIP_TRY(ctx, hipMemcpyAsync(t->chans_dev + channel, &c, sizeof(TrkChannel), hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    return GNSSHIP_OK;
+}
+
+// Scatter of staged channel states: block b copies channel record b to its slot idx[b].
+__global__ void trk_scatter_kernel(TrkChannel* __restrict__ chans, const TrkChannel* __restrict__ staged, const int32_t* __restrict__ idx, int n)
+{
+    const int b = blockIdx.x;
+    if (b >= n) return;
+    constexpr int kWords = sizeof(TrkChannel) / 4;
+    const int* src = reinterpret_cast<const int*>(staged + b);
+    int* dst = reinterpret_cast<int*>(chans + idx[b]);
+    for (int i = threadIdx.x; i < kWords; i += blockDim.x) dst[i] = src[i];
+}
+
+// n start_tracking calls at once: the channel states built on the host, one upload of states +
+// channel indices, one scatter launch, one upload of the chunk table's code fields, one sync.
+extern "C" int gnsship_trk_start_many(gnsship_trk* t, int n, const int32_t* channels, const gnsship_trk_start_args* args)
+{
+    if (!t) return GNSSHIP_E_INVAL;
+    gnsship_ctx* ctx = t->ctx;
+    if (n < 0 || (n > 0 && (!channels || !args))) return fail(ctx, GNSSHIP_E_INVAL, "gnsship_trk_start_many: bad arguments");
+    if (n == 0) return GNSSHIP_OK;
+    std::vector<int32_t> seen(t->max_channels, 0);
+    for (int i = 0; i < n; i++) {
+        if (channels[i] < 0 || channels[i] >= t->max_channels) return fail(ctx, GNSSHIP_E_INVAL, "gnsship_trk_start_many: bad channel");
+        if (seen[channels[i]]++) return fail(ctx, GNSSHIP_E_INVAL, "gnsship_trk_start_many: a channel appears twice");
+    }
+    // staging: n TrkChannel records, then the n channel indices
+    const size_t st_bytes = sizeof(TrkChannel) * static_cast<size_t>(n), idx_off = (st_bytes + 15) & ~size_t{15};
+    std::vector<char> host(idx_off + sizeof(int32_t) * static_cast<size_t>(n));
+    // validate and build every channel before anything reaches the device (a failure leaves the
+    // device state untouched; the host code tables of the channels built so far are restored)
+    const std::vector<int32_t> job_code_before = t->job_code;
+    const std::vector<ChunkDesc> chunks_before = t->chunks_host;
+    for (int i = 0; i < n; i++) {
+        if (int rc = trk_start_state(t, channels[i], args + i, reinterpret_cast<TrkChannel*>(host.data())[i])) {
+            t->job_code = job_code_before;
+            t->chunks_host = chunks_before;
+            return rc;
+        }
+    }
+    std::memcpy(host.data() + idx_off, channels, sizeof(int32_t) * static_cast<size_t>(n));
+    if (int rc = set_device(ctx)) return rc;
+    if (t->start_stage_cap < host.size()) {
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+        if (t->start_stage_dev) HIP_TRY(ctx, hipFree(t->start_stage_dev));
+        t->start_stage_dev = nullptr;
+        HIP_TRY(ctx, hipMalloc(&t->start_stage_dev, host.size()));
+        t->start_stage_cap = host.size();
+    }
+    char* stage = static_cast<char*>(t->start_stage_dev);
+    HIP_TRY(ctx, hipMemcpyAsync(stage, host.data(), host.size(), hipMemcpyHostToDevice, ctx->stream));
+    hipLaunchKernelGGL(trk_scatter_kernel, dim3(n), dim3(256), 0, ctx->stream, t->chans_dev, reinterpret_cast<const TrkChannel*>(stage),
+        reinterpret_cast<const int32_t*>(stage + idx_off), n);
+    HIP_TRY(ctx, hipGetLastError());
+    // the chunk table (the round-based loop's code pointers; its lengths are rewritten by the step
+    // kernel before any correlation of a run)
+    HIP_TRY(ctx, hipMemcpyAsync(t->chunks_dev, t->chunks_host.data(), sizeof(ChunkDesc) * t->n_chunks, hipMemcpyHostToDevice, ctx->stream));
+    if (t->high_dyn)
+        for (int i = 0; i < n; i++)
+            for (int q = 0; q < t->params.jobs_per_channel; q++) {
+                const int job = channels[i] * t->params.jobs_per_channel + q;
+                HIP_TRY(ctx, upload_hd_code(t, job, ctx->codes_host[t->job_code[job]]));
+            }
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     return GNSSHIP_OK;
 }
@@ -641,14 +723,16 @@ static int trk_enqueue(gnsship_trk* t, const void* src, int fmt, uint64_t buffer
         if (dump) HIP_TRY(ctx, hipMemsetAsync(t->dump_dev, 0, sizeof(gnsship_trk_dump_record) * nrec, ctx->stream));
         const int n_codes = static_cast<int>(ctx->codes_host.size());
         hipError_t e;
+        // the sign-bit replicas need every chip ±1 — of the codes this tracker's channels use
         bool binary = true;
-        for (const CodeDesc& cd : ctx->codes_host)
-            if (cd.ptr && !cd.binary) binary = false;
-        const bool lanes = avx && trk_lane_supported(t->params, code_cap, nc, fmt, n_buffer_samples, binary);
+        for (int id : t->job_code)
+            if (id >= 0 && id < n_codes && ctx->codes_host[id].ptr && !ctx->codes_host[id].binary) binary = false;
+        // GNSSHIP_TRK_FAST=0 (A/B runs against trk_persist.hip) turns both exact AVX forms off
+        const char* fast_env = std::getenv("GNSSHIP_TRK_FAST");
+        const bool no_fast = fast_env && fast_env[0] == '0';
+        const bool lanes = avx && !no_fast && trk_lane_supported(t->params, code_cap, nc, fmt, n_buffer_samples, binary);
         const bool fast = avx && !lanes && trk_fast_supported(t->params, code_cap, nc);
-        t->last_engine = lanes  ? GNSSHIP_TRK_ENGINE_LANES
-                         : fast ? (trk_fast_thru(nc) ? GNSSHIP_TRK_ENGINE_FAST_THROUGHPUT : GNSSHIP_TRK_ENGINE_FAST_LATENCY)
-                                : GNSSHIP_TRK_ENGINE_PERSIST;
+        t->last_engine = GNSSHIP_TRK_ENGINE_NONE;
         if (lanes)
             e = launch_trk_lane(t->params_dev, t->params, t->chans_dev, nc, ctx->codes_dev, n_codes, code_cap, src, fmt, buffer_first_sample,
                 n_buffer_samples, max_rounds, out ? t->rec_dev : nullptr, dump ? t->dump_dev : nullptr, trace, t->ran_dev, ctx->stream);
@@ -659,6 +743,9 @@ static int trk_enqueue(gnsship_trk* t, const void* src, int fmt, uint64_t buffer
             e = launch_trk_persist(t->params_dev, t->params, t->chans_dev, nc, ctx->codes_dev, n_codes, code_cap, src, fmt, buffer_first_sample,
                 n_buffer_samples, max_rounds, out ? t->rec_dev : nullptr, dump ? t->dump_dev : nullptr, trace, t->ran_dev, avx, ctx->stream);
         if (e != hipSuccess) return hip_fail(ctx, e, lanes ? "launch_trk_lane" : fast ? "launch_trk_fast" : "launch_trk_persist");
+        t->last_engine = lanes  ? GNSSHIP_TRK_ENGINE_LANES
+                         : fast ? (trk_fast_thru(nc) ? GNSSHIP_TRK_ENGINE_FAST_THROUGHPUT : GNSSHIP_TRK_ENGINE_FAST_LATENCY)
+                                : GNSSHIP_TRK_ENGINE_PERSIST;
     }
     if (!persist) t->last_engine = GNSSHIP_TRK_ENGINE_ROUNDS;
     for (int r = 0; r <= max_rounds && !persist; r++) {

@@ -133,22 +133,7 @@ constexpr int kFWavesLong = GNSSHIP_FAST_WAVES_LONG;
 constexpr int kLongEpoch = 10000;  // samples per epoch from which the long-epoch wave count applies
 // The accumulation's waves: one per four product slots (2·taps, the data prompt included: GPS and
 // B1I 6 slots → 2 waves, the E1 engine's 12 → 3), so that each lane adds ONE slot per iteration —
-// a single serial chain per lane, and room for two groups' loads in flight (fast_accumulate).
-#ifndef GNSSHIP_PROD_SPLIT  // A/B: two producers per product group (fast_produce; measured slower)
-#define GNSSHIP_PROD_SPLIT 0
-#endif
-#ifndef GNSSHIP_ACC_PAIRS  // A/B: the accumulator takes two ready groups per round trip (measured slower)
-#define GNSSHIP_ACC_PAIRS 0
-#endif
-#ifndef GNSSHIP_SAMPLE_CMUL_SCALAR  // A/B: the sample product a = x·z as six scalar ops instead of three packed
-#define GNSSHIP_SAMPLE_CMUL_SCALAR 0
-#endif
-#ifndef GNSSHIP_ACC_PIPE  // A/B: the accumulator loads the next group behind the current one's adds (measured slower)
-#define GNSSHIP_ACC_PIPE 0
-#endif
-#ifndef GNSSHIP_EARLY_JOB  // the control wave publishes the next epoch's code / sample arguments before the seed (state 4)
-#define GNSSHIP_EARLY_JOB 0  // measured: 622 vs 663 Msps with it on (the control wave pays the early publish on its chain)
-#endif
+// a single serial chain per lane (fast_accumulate).
 #ifndef GNSSHIP_PRE_DISC  // the accumulator waves evaluate the discriminators ahead of the loop (0: the control wave does)
 #define GNSSHIP_PRE_DISC 1
 #endif
@@ -158,11 +143,8 @@ constexpr int kLongEpoch = 10000;  // samples per epoch from which the long-epoc
 #ifndef GNSSHIP_ROLE_PLAN  // wave roles by SIMD: 0 phasor + accumulator 0 share a SIMD; 1 one primary role per SIMD
 #define GNSSHIP_ROLE_PLAN 0
 #endif
-#ifndef GNSSHIP_ACC_WAVES  // A/B: force the accumulator wave count
-#define GNSSHIP_ACC_WAVES 0
-#endif
 template <int NTT>
-constexpr int acc_waves() { return GNSSHIP_ACC_WAVES > 0 ? GNSSHIP_ACC_WAVES : (2 * NTT + 3) / 4; }
+constexpr int acc_waves() { return (2 * NTT + 3) / 4; }
 // every wave but the phasor, control and accumulator waves forms products
 template <int NTT, int W>
 constexpr int n_producers() { return W - 2 - acc_waves<NTT>(); }
@@ -190,9 +172,6 @@ constexpr int kRoleControl = 0, kRoleReplay = 1, kRoleProducer = 2, kRoleAccum =
 #ifndef GNSSHIP_DELAY_LOOP
 #define GNSSHIP_DELAY_LOOP 0
 #endif
-#ifndef GNSSHIP_ACC_BATCH  // iterations per accumulator load batch
-#define GNSSHIP_ACC_BATCH 8
-#endif
 #ifndef GNSSHIP_POLL_SLEEP
 #define GNSSHIP_POLL_SLEEP 0
 #endif
@@ -216,10 +195,6 @@ struct SpecArgs {
     float rem_prev;
     int32_t n_pred;
 };
-
-#ifdef GNSSHIP_EXP_SERIAL  // experiment: the producers' phase B waits for the whole replay
-__shared__ int32_t g_replay_done;
-#endif
 
 struct SpecPred {
     float rem, step, dz_re, dz_im;
@@ -246,8 +221,6 @@ struct FShared {
     f2 tailp[kAvxLanes][kMaxTaps + 1];  // the tail's products (sample 16M + j, tap), wave 1 → wave 0
     double pre_pll[2], pre_dll[2];  // epoch e's discriminators in [e & 1], from accumulator waves 0 / 1 (PreDisc)
     int32_t pll_seq, dll_seq;       // e + 1 once they are stored
-    FJob early;         // epoch e's code / sample arguments (no phasors), published as early_seq = e + 1 (state 4)
-    int32_t early_seq;
 };
 
 // The job as wave-uniform values (scalar registers): read from LDS it would otherwise be per-lane,
@@ -321,21 +294,11 @@ __device__ __forceinline__ void lds_wait_ge(const int32_t* p, int v)
 // cycles per iteration on one wave, scripts/replay_bench.hip).  A DPP read needs two wait states
 // after the VALU write of its source: the step's plain multiply and one s_nop.  Each lane stores its
 // 32-bit half of the slot (the consumer polls until both halves are written).
-#ifdef GNSSHIP_PSTEP_VNOP  // experiment: the DPP wait state as a VALU nop
-#define GNSSHIP_PSTEP_NOP "v_nop\n\t"
-#else
-#define GNSSHIP_PSTEP_NOP "s_nop 0\n\t"
-#endif
-#ifdef GNSSHIP_PSTEP_ADD64  // experiment: the add as VOP3 (24-byte steps, the DPP op at a fixed 8-byte phase)
-#define GNSSHIP_PSTEP_ADD "v_add_f32_e64 "
-#else
-#define GNSSHIP_PSTEP_ADD "v_add_f32 "
-#endif
 #define GNSSHIP_PSTEP(X, Y)                                                                   \
     "v_mul_f32 %[t], %[c], " X "\n\t"                                                      \
-    GNSSHIP_PSTEP_NOP                                                                        \
+    "s_nop 0\n\t"                                                                           \
     "v_mul_f32_dpp %[u], " X ", %[k2] quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t" \
-    GNSSHIP_PSTEP_ADD Y ", %[t], %[u]\n\t"
+    "v_add_f32 " Y ", %[t], %[u]\n\t"
 
 // N iterations (1-4) in one asm block (the hazard recognizer pads each block boundary with one
 // s_nop); STORE: the block's input (the task start) goes to its slot half at `lds_off` (a byte offset
@@ -389,39 +352,22 @@ __device__ __forceinline__ float pstep(float x, float c, float k2, uint32_t lds_
 // as ONE asm block.  The hazard recognizer pads every inline-asm boundary with an s_nop and the
 // slot address would be re-derived per task otherwise; here one address serves the block.
 #define GNSSHIP_PS(A, B) GNSSHIP_PSTEP("%[" #A "]", "%[" #B "]")
-// A/B (GNSSHIP_SLOT_ADDTID=1; measured equal, 638.3 vs 637.6 Msps): the task stores as
-// ds_write_addtid_b32 (address M0 + offset + 4·lane: no address VGPR, half the store path of
-// ds_write_b32) with M0 = the block's slot row in LDS (`m0v`, < 64 KiB: the slots sit at the front of
-// the dynamic LDS).  Default: ds_write_b32.
-#ifndef GNSSHIP_SLOT_ADDTID
-#define GNSSHIP_SLOT_ADDTID 0
-#endif
-#if GNSSHIP_SLOT_ADDTID
-#define GNSSHIP_TST(A, OFF) "ds_write_addtid_b32 %[" #A "] offset:" #OFF "\n\t"
-#define GNSSHIP_M0SET "s_mov_b32 m0, %[m0v]\n\t"
-#else
 #define GNSSHIP_TST(A, OFF) "ds_write_b32 %[p], %[" #A "] offset:" #OFF "\n\t"
-#define GNSSHIP_M0SET ""
-#endif
 #define GNSSHIP_TASK8(A, B, OFF)                                                                                            \
     GNSSHIP_PS(A, B) GNSSHIP_TST(A, OFF) GNSSHIP_PS(B, A) GNSSHIP_PS(A, B) GNSSHIP_PS(B, A) GNSSHIP_PS(A, B) GNSSHIP_PS(B, A) \
         GNSSHIP_PS(A, B) GNSSHIP_PS(B, A)
-#pragma clang diagnostic push
-#pragma clang diagnostic ignored "-Winline-asm"  // m0: reserved to the compiler, which uses it nowhere in this kernel (checked in the ISA)
-__device__ __forceinline__ float pblock64_g8(float x, float c, float k2, uint32_t lds_off, uint32_t m0v)
+__device__ __forceinline__ float pblock64_g8(float x, float c, float k2, uint32_t lds_off)
 {
     float t, u, w;
-    asm volatile(GNSSHIP_M0SET GNSSHIP_PS(x, w) GNSSHIP_PS(w, x) GNSSHIP_PS(x, w) GNSSHIP_PS(w, x) GNSSHIP_PS(x, w) GNSSHIP_PS(w, x)
+    asm volatile(GNSSHIP_PS(x, w) GNSSHIP_PS(w, x) GNSSHIP_PS(x, w) GNSSHIP_PS(w, x) GNSSHIP_PS(x, w) GNSSHIP_PS(w, x)
                      GNSSHIP_PS(x, w) GNSSHIP_TASK8(w, x, 128) GNSSHIP_TASK8(w, x, 256) GNSSHIP_TASK8(w, x, 384) GNSSHIP_TASK8(w, x, 512)
                          GNSSHIP_TASK8(w, x, 640) GNSSHIP_TASK8(w, x, 768) GNSSHIP_TASK8(w, x, 896) "v_mov_b32 %[x], %[w]\n\t"
                  : [x] "+v"(x), [t] "=&v"(t), [u] "=&v"(u), [w] "=&v"(w)
-                 : [c] "s"(c), [k2] "v"(k2), [p] "v"(lds_off), [m0v] "s"(m0v)
-                 : "memory", "m0");
+                 : [c] "s"(c), [k2] "v"(k2), [p] "v"(lds_off)
+                 : "memory");
     return x;
 }
-#pragma clang diagnostic pop
 #undef GNSSHIP_TST
-#undef GNSSHIP_M0SET
 #undef GNSSHIP_TASK8
 #undef GNSSHIP_PS
 // x·dz^N: N ≥ 0 iterations
@@ -467,7 +413,7 @@ __device__ __forceinline__ float fast_replay(float x, float c, float k2, int M, 
         for (int b = 0; b < full; b++) {
             if constexpr (G == 8 && kSlotRow == 128) {
                 // the block's first iteration normalises; the other 63 run in one asm block
-                x = pblock64_g8(pnormalise(pstep<1, true>(x, c, k2, off)), c, k2, off, __builtin_amdgcn_readfirstlane(off - 4u * lane));
+                x = pblock64_g8(pnormalise(pstep<1, true>(x, c, k2, off)), c, k2, off);
                 off += kTB * kSlotRow;
             } else {
 #pragma unroll
@@ -515,7 +461,7 @@ __device__ __forceinline__ float fast_replay(float x, float c, float k2, int M, 
                         }
                     }
                     off = base + static_cast<uint32_t>(ts0) * kSlotRow;
-                    x = pblock64_g8(pnormalise(pstep<1, true>(x, c, k2, off)), c, k2, off, __builtin_amdgcn_readfirstlane(off - 4u * lane));
+                    x = pblock64_g8(pnormalise(pstep<1, true>(x, c, k2, off)), c, k2, off);
                 }
             }
         }
@@ -559,26 +505,53 @@ __device__ __forceinline__ void group_codes(const float* __restrict__ code0, con
     for (int i = 0; i < G; i++) {
         const bool on = FULL || i < cnt;
         const float sn = __fmul_rn(step, on ? fn : fn0);
-#ifdef GNSSHIP_EXP_NOCODES  // timing experiment only (wrong taps): no code lookups
-#pragma unroll
-        for (int q = 0; q < NT; q++) cv[i][q] = (q & 1) ? sn : 1.0f;
-        if constexpr (DATA) cv[i][NT] = 1.0f;
-#else
 #pragma unroll
         for (int q = 0; q < NT; q++) cv[i][q] = code_at<IN_MARGIN>(code0, L, sn, shifts[q], rem);
         if constexpr (DATA) cv[i][NT] = code_at<IN_MARGIN>(code1, L, sn, 0.0f, rem);
-#endif
         fn += static_cast<float>(kAvxLanes);
     }
 }
 
-// Producer phase B, once the slot holds z_l at the task start: per iteration the sample product
-// a = x·z_l (_mm256_complexmul_ps rounding) and its products with the taps' code values,
-// c = _mm256_mul_ps(a, code) (:252-258) — the accumulator only adds them — and the chain's own update
-// z·dz (renormalised after the task's first iteration when that is ≡ 0 mod 64, :265-272).  The
-// products of four consecutive iterations of one slot go to the ring as one 16-byte store
-// (ProdLayout).  FULL: every lane's task has all G iterations, so nothing is masked.
 typedef float f4 __attribute__((ext_vector_type(4)));
+
+// The product ring's layout (floats): group r, product slot s (2·tap + component), chain l, iteration
+// j of the group's 4G at  r·kGroup + s·kSlot + l·kRow + j.  A producer lane (task t, chain l) stores
+// four iterations of one slot at once (16 bytes at j = G·t + 4h), an accumulator lane (slot row,
+// chain l) loads four at once; rows padded to kRow = 4G + 4 floats make both conflict-free (the
+// eight lanes of a ds_write_b128 group start 4 banks apart, the sixteen of a ds_read_b128 group too).
+template <int NTT, int G>
+struct ProdLayout {
+    static constexpr int kJ = 4 * G;
+    static constexpr int kRow = kJ + 4;
+    static constexpr int kSlot = kAvxLanes * kRow;
+    static constexpr int kGroup = 2 * NTT * kSlot;
+};
+
+// The products of four consecutive iterations of every product slot (2·tap + component) from the
+// iterations' sample products a = x·z_l and code values: c = _mm256_mul_ps(a, code) (:252-258), one
+// 16-byte store per slot.  An iteration past the epoch's last holds −0, which the accumulator adds
+// unconditionally: x + (−0) = x for every x, so its sums are the reference's.
+template <int NTT, int G, bool FULL, class PL>
+__device__ __forceinline__ void store_products4(float* __restrict__ pdst, int i0, int cnt, const f2 (&a)[4], const float (&cv)[G][NTT])
+{
+    f4 q[2 * NTT];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+        const bool on = FULL || i0 + u < cnt;
+#pragma unroll
+        for (int t = 0; t < NTT; t++) {
+            q[2 * t][u] = on ? __fmul_rn(a[u].x, cv[i0 + u][t]) : -0.0f;
+            q[2 * t + 1][u] = on ? __fmul_rn(a[u].y, cv[i0 + u][t]) : -0.0f;
+        }
+    }
+#pragma unroll
+    for (int sl = 0; sl < 2 * NTT; sl++) *reinterpret_cast<f4*>(pdst + sl * PL::kSlot + i0) = q[sl];
+}
+
+// Producer phase B, once the slot holds z_l at the task start: per iteration the sample product
+// a = x·z_l (_mm256_complexmul_ps rounding) and its products with the taps' code values, and the
+// chain's own update z·dz (renormalised after the task's first iteration when that is ≡ 0 mod 64,
+// :265-272).  FULL: every lane's task has all G iterations, so nothing is masked.
 template <int FMT, int NTT, int G, bool FULL, class PL>
 __device__ __forceinline__ void group_phasors(i4v span, f2 z, f2 dz, bool renorm, int n0, int cnt, float* __restrict__ pdst, const float (&cv)[G][NTT],
     f2 (&xa)[G < 8 ? G : 8], f2 (&xb)[G < 8 ? G : 8])
@@ -594,29 +567,16 @@ __device__ __forceinline__ void group_phasors(i4v span, f2 z, f2 dz, bool renorm
         }
 #pragma unroll
         for (int h = 0; h < kB; h += 4) {
-            f4 q[2 * NTT];
+            f2 a[4];
 #pragma unroll
             for (int u = 0; u < 4; u++) {
                 const int i = i0 + h + u;
-                const bool on = FULL || i < cnt;
-#if GNSSHIP_SAMPLE_CMUL_SCALAR
-                const f2 a = cmul_exact_sc(xa[h + u], z);
-#else
-                const f2 a = cmul_exact_pk(xa[h + u], z);
-#endif
-                // an iteration past the epoch's last holds −0, which the accumulator adds unconditionally:
-                // x + (−0) = x for every x, so its sums are the reference's
-#pragma unroll
-                for (int t = 0; t < NTT; t++) {
-                    q[2 * t][u] = on ? __fmul_rn(a.x, cv[i][t]) : -0.0f;
-                    q[2 * t + 1][u] = on ? __fmul_rn(a.y, cv[i][t]) : -0.0f;
-                }
+                a[u] = cmul_exact_pk(xa[h + u], z);
                 f2 zn = cmul_exact_s(z, dz);
                 if (i == 0 && renorm) zn = normalise_avx(zn);
                 z = zn;
             }
-#pragma unroll
-            for (int sl = 0; sl < 2 * NTT; sl++) *reinterpret_cast<f4*>(pdst + sl * PL::kSlot + i0 + h) = q[sl];
+            store_products4<NTT, G, FULL, PL>(pdst, i0 + h, cnt, a, cv);
         }
         if (i0 + kB < G) {
 #pragma unroll
@@ -625,44 +585,22 @@ __device__ __forceinline__ void group_phasors(i4v span, f2 z, f2 dz, bool renorm
     }
 }
 
-// The product ring's layout (floats): group r, product slot s (2·tap + component), chain l, iteration
-// j of the group's 4G at  r·kGroup + s·kSlot + l·kRow + j.  A producer lane (task t, chain l) stores
-// four iterations of one slot at once (16 bytes at j = G·t + 4h), an accumulator lane (slot row,
-// chain l) loads four at once; rows padded to kRow = 4G + 4 floats make both conflict-free (the
-// eight lanes of a ds_write_b128 group start 4 banks apart, the sixteen of a ds_read_b128 group too).
-template <int NTT, int G>
-struct ProdLayout {
-    static constexpr int kJ = 4 * G;
-    static constexpr int kRow = kJ + 4;
-    static constexpr int kSlot = kAvxLanes * kRow;
-    static constexpr int kGroup = 2 * NTT * kSlot;
-};
-
 // ---- producer waves -------------------------------------------------------------------------------
 // Ring group r (of rg) holds one group of 4 tasks = 4G iterations: the products of every iteration of
 // the group, chain, tap and component (ProdLayout).  Group tags count over the run (gbase = epoch ·
 // n_groups): no flag is re-armed.  A ring group is reused once every accumulator wave consumed it.
-// Producers per group: two when there is an even number of producers (each takes half of every task's
-// iterations — the second half's lanes first advance their chain G/2 steps from the slot), so the
-// latency from a group's last slot to its products halves; otherwise one.
-template <int NTT, int W, int G>
-constexpr int producers_per_group() { return (GNSSHIP_PROD_SPLIT && n_producers<NTT, W>() % 2 == 0 && G == 8) ? 2 : 1; }
-
+// One producer per group; producer pw takes groups pw, pw + NP, ...
 template <int FMT, int NT, bool DATA, bool IN_MARGIN, int G, int W>
 __device__ __forceinline__ void fast_produce(const FJob& job, i4v span, const float* __restrict__ code0, const float* __restrict__ code1, int L,
     uint64_t* __restrict__ Zs, int rs, float* __restrict__ Pp, int rg, int32_t* ready, const int32_t* acc_groups, int gbase, int lane, int pw, int pe,
-    bool pre, f2 (&xa)[(G / producers_per_group<NT + (DATA ? 1 : 0), W, G>()) < 8 ? (G / producers_per_group<NT + (DATA ? 1 : 0), W, G>()) : 8],
-    float (&cv)[G / producers_per_group<NT + (DATA ? 1 : 0), W, G>()][NT + (DATA ? 1 : 0)])
+    f2 (&xa)[G < 8 ? G : 8], float (&cv)[G][NT + (DATA ? 1 : 0)])
 {
     constexpr int SB = sample_bytes<FMT>();
     constexpr int NTT = NT + (DATA ? 1 : 0);
     constexpr int NP = n_producers<NTT, W>();
     constexpr int NA = acc_waves<NTT>();
-    constexpr int NH = producers_per_group<NTT, W, G>();
-    constexpr int GH = G / NH;  // iterations of each task this wave produces
-    constexpr int NG = NP / NH; // groups in production at once
     using PL = ProdLayout<NTT, G>;
-    constexpr int kB = GH < 8 ? GH : 8;  // iterations whose samples are in flight together
+    constexpr int kB = G < 8 ? G : 8;  // iterations whose samples are in flight together
     const int M = job.M, S = job.S;
     const int n_groups = (S + 3) / 4;
     const f2 dz = f2{job.dz_re, job.dz_im};
@@ -671,36 +609,27 @@ __device__ __forceinline__ void fast_produce(const FJob& job, i4v span, const fl
 #pragma unroll
     for (int q = 0; q < NT; q++) shifts[q] = job.shifts[q];
     const int tl = lane >> 4, l = lane & (kAvxLanes - 1);
-    const int h = NH == 2 ? (pw & 1) : 0, pp = NH == 2 ? (pw >> 1) : pw;
-    auto first_samples = [&](int g, f2 (&x)[kB]) {
-        const int t = 4 * g + tl;
-        const int n0 = kAvxLanes * (G * (t < S ? t : 0) + GH * h) + l;
-#pragma unroll
-        for (int u = 0; u < kB; u++) x[u] = load_sample<FMT>(span, (n0 + kAvxLanes * u) * SB, 0);
-    };
     f2 xb[kB];
-    int rslot = pp % rg;
-    const int rstep = NG % rg;
+    int rslot = pw % rg;
+    const int rstep = NP % rg;
     unsigned long long w_ring = 0, w_slot = 0, w_codes = 0, w_prod = 0;  // profiling: ring / slot waits, phase A / B
-    const unsigned long long t_run = GNSSHIP_FCLOCK();
-    for (int g = pp; g < n_groups; g += NG) {
+    [[maybe_unused]] const unsigned long long t_run = GNSSHIP_FCLOCK();
+    for (int g = pw; g < n_groups; g += NP) {
         const int t = 4 * g + tl;
         const bool active = t < S;
         const int m_lo = G * (active ? t : 0);
         const int cnt = active ? min(G, M - m_lo) : 0;
-        const int cnth = max(0, min(GH, cnt - GH * h));  // this wave's iterations of the task within the epoch
-        const int n0 = kAvxLanes * (m_lo + GH * h) + l;
+        const int n0 = kAvxLanes * m_lo + l;
         const bool full = 4 * g + 4 <= S && G * (4 * g + 4) <= M;  // every task of the group whole
         const unsigned long long tA = GNSSHIP_FCLOCK();
-        if (!(pre && g == pp)) {  // (pre: the first group's phase A ran on the early arguments, fast_produce_early)
-            first_samples(g, xa);  // in flight during phase A and the slot poll
-            if (full)
-                group_codes<NT, DATA, IN_MARGIN, GH, true>(code0, code1, L, n0, GH, step, rem, shifts, cv);
-            else
-                group_codes<NT, DATA, IN_MARGIN, GH, false>(code0, code1, L, n0, cnth, step, rem, shifts, cv);
-        }
+#pragma unroll
+        for (int u = 0; u < kB; u++) xa[u] = load_sample<FMT>(span, (n0 + kAvxLanes * u) * SB, 0);  // in flight during phase A and the slot poll
+        if (full)
+            group_codes<NT, DATA, IN_MARGIN, G, true>(code0, code1, L, n0, G, step, rem, shifts, cv);
+        else
+            group_codes<NT, DATA, IN_MARGIN, G, false>(code0, code1, L, n0, cnt, step, rem, shifts, cv);
 #ifdef GNSSHIP_CORR_PROFILE
-        for (int i = 0; i < GH; i++)  // phase A's code loads landed (profiling only)
+        for (int i = 0; i < G; i++)  // phase A's code loads landed (profiling only)
             for (int q = 0; q < NTT; q++) asm volatile("" ::"v"(cv[i][q]));
 #endif
         w_codes += GNSSHIP_FCLOCK() - tA;
@@ -714,43 +643,26 @@ __device__ __forceinline__ void fast_produce(const FJob& job, i4v span, const fl
         }
         const unsigned long long t1 = GNSSHIP_FCLOCK();
         w_ring += t1 - t0;
-        const int ts = active ? t % rs : 0;
-        uint64_t* slot = Zs + ts * kAvxLanes + l;
+        uint64_t* slot = Zs + (active ? t % rs : 0) * kAvxLanes + l;
         uint64_t v = kSlotEmpty;
         if (active) {
-            // written when neither 32-bit half is the sentinel any more (two replay lanes write it);
-            // with two producers per group the accumulator re-arms it once both have read it
+            // written when neither 32-bit half is the sentinel any more (two replay lanes write it)
             while (static_cast<uint32_t>(v = load_slot(slot)) == ~0u || static_cast<uint32_t>(v >> 32) == ~0u) __builtin_amdgcn_s_sleep(GNSSHIP_POLL_SLEEP);
-            if (NH == 1) store_slot(slot, __builtin_bit_cast(f2, kSlotEmpty));  // re-armed for the next lap / epoch
+            store_slot(slot, __builtin_bit_cast(f2, kSlotEmpty));  // re-armed for the next lap / epoch
         }
         w_slot += GNSSHIP_FCLOCK() - t1;
-        if (g == pp && pw == 0) GNSSHIP_FSTAMP(pe, 30);
-        if (g + NG >= n_groups && pw == 1) GNSSHIP_FSTAMP(pe, 31);
-#ifdef GNSSHIP_EXP_SERIAL
-        while (__hip_atomic_load(&g_replay_done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < pe + 1) __builtin_amdgcn_s_sleep(1);
-#endif
-        f2 z = active ? __builtin_bit_cast(f2, v) : f2{0.0f, 0.0f};
+        if (g == pw && pw == 0) GNSSHIP_FSTAMP(pe, 30);
+        if (g + NP >= n_groups && pw == 1) GNSSHIP_FSTAMP(pe, 31);
+        const f2 z = active ? __builtin_bit_cast(f2, v) : f2{0.0f, 0.0f};
         const bool renorm = ((G * t) & 63) == 0;
-        if (NH == 2 && h == 1) {  // the task's first half: the chain's own steps (renormalised after the first)
-#pragma unroll
-            for (int i = 0; i < GH; i++) {
-                f2 zn = cmul_exact_s(z, dz);
-                if (i == 0 && renorm) zn = normalise_avx(zn);
-                z = zn;
-            }
-        }
-        float* pdst = Pp + static_cast<size_t>(rslot) * PL::kGroup + l * PL::kRow + G * tl + GH * h;
+        float* pdst = Pp + static_cast<size_t>(rslot) * PL::kGroup + l * PL::kRow + G * tl;
         const unsigned long long tB = GNSSHIP_FCLOCK();
-#ifndef GNSSHIP_EXP_NOPROD  // timing experiment: the producers only follow the slots and set the flags
         if (full)
-            group_phasors<FMT, NTT, GH, true, PL>(span, z, dz, renorm && h == 0, n0, GH, pdst, cv, xa, xb);
+            group_phasors<FMT, NTT, G, true, PL>(span, z, dz, renorm, n0, G, pdst, cv, xa, xb);
         else
-            group_phasors<FMT, NTT, GH, false, PL>(span, z, dz, renorm && h == 0, n0, cnth, pdst, cv, xa, xb);
-#else
-        if (z.x == 12345.0f) pdst[0] = cv[0][0];
-#endif
+            group_phasors<FMT, NTT, G, false, PL>(span, z, dz, renorm, n0, cnt, pdst, cv, xa, xb);
         GNSSHIP_PROBE(GNSSHIP_DELAY_PROD);
-        if (lane == 0) lds_release_store(ready + 2 * rslot + h, gbase + g + 1);
+        if (lane == 0) lds_release_store(ready + 2 * rslot, gbase + g + 1);
         w_prod += GNSSHIP_FCLOCK() - tB;
         if (g < 8) GNSSHIP_FSTAMP(pe, 48 + g);
         rslot += rstep;
@@ -765,43 +677,6 @@ __device__ __forceinline__ void fast_produce(const FJob& job, i4v span, const fl
     }
 }
 
-// Phase A of a producer's first group on the early arguments (FShared::early): the same samples and
-// code values fast_produce's first iteration forms from the job, issued while the control wave still
-// makes the seed.  Returns false when the group needs nothing early.
-template <int FMT, int NT, bool DATA, bool IN_MARGIN, int G, int W>
-__device__ __forceinline__ void fast_produce_early(const FJob& job, i4v span, const float* __restrict__ code0, const float* __restrict__ code1, int L,
-    int lane, int pw, f2 (&xa)[(G / producers_per_group<NT + (DATA ? 1 : 0), W, G>()) < 8 ? (G / producers_per_group<NT + (DATA ? 1 : 0), W, G>()) : 8],
-    float (&cv)[G / producers_per_group<NT + (DATA ? 1 : 0), W, G>()][NT + (DATA ? 1 : 0)])
-{
-    constexpr int SB = sample_bytes<FMT>();
-    constexpr int NTT = NT + (DATA ? 1 : 0);
-    constexpr int NH = producers_per_group<NTT, W, G>();
-    constexpr int GH = G / NH;
-    constexpr int kB = GH < 8 ? GH : 8;
-    const int M = job.M, S = job.S;
-    float shifts[NT];
-#pragma unroll
-    for (int q = 0; q < NT; q++) shifts[q] = job.shifts[q];
-    const int tl = lane >> 4, l = lane & (kAvxLanes - 1);
-    const int h = NH == 2 ? (pw & 1) : 0, g = NH == 2 ? (pw >> 1) : pw;
-    const int t = 4 * g + tl;
-    const bool active = t < S;
-    const int m_lo = G * (active ? t : 0);
-    const int cnt = active ? min(G, M - m_lo) : 0;
-    const int cnth = max(0, min(GH, cnt - GH * h));
-    const int n0 = kAvxLanes * (m_lo + GH * h) + l;
-    const bool full = 4 * g + 4 <= S && G * (4 * g + 4) <= M;
-    {
-        const int n0s = kAvxLanes * (G * (t < S ? t : 0) + GH * h) + l;
-#pragma unroll
-        for (int u = 0; u < kB; u++) xa[u] = load_sample<FMT>(span, (n0s + kAvxLanes * u) * SB, 0);
-    }
-    if (full)
-        group_codes<NT, DATA, IN_MARGIN, GH, true>(code0, code1, L, n0, GH, job.code_step, job.rem_code, shifts, cv);
-    else
-        group_codes<NT, DATA, IN_MARGIN, GH, false>(code0, code1, L, n0, cnth, job.code_step, job.rem_code, shifts, cv);
-}
-
 // ---- accumulator waves: the accumulation in u_avx's order ---------------------------------------
 // Accumulator wave a (of NA) lane (r, l): chain l's accumulators of the product slots
 // s_k = 4·(a + NA·k) + r (slot s = 2·tap + component) — each c = _mm256_mul_ps(a, code) the producers
@@ -813,11 +688,10 @@ constexpr int acc_slots() { return (2 * NTT + 4 * acc_waves<NTT>() - 1) / (4 * a
 template <int NTT>
 __device__ __forceinline__ int acc_slot(int a, int r, int k) { return 4 * (a + acc_waves<NTT>() * k) + r; }
 
-template <int NTT, int G, int W>
+template <int NTT, int G>
 __device__ __forceinline__ void fast_accumulate(const float* __restrict__ Pp, int rg, const int32_t* ready, int32_t* acc_done, int gbase, int S,
-    int lane, int a, float (&acc)[acc_slots<NTT>()], int pe, uint64_t* __restrict__ Zs, int rs)
+    int lane, int a, float (&acc)[acc_slots<NTT>()], int pe)
 {
-    constexpr int NH = producers_per_group<NTT, W, G>();
     using PL = ProdLayout<NTT, G>;
     constexpr int NS = acc_slots<NTT>();
     constexpr int kQ = PL::kJ / 4;  // four-iteration loads per slot and group
@@ -829,128 +703,40 @@ __device__ __forceinline__ void fast_accumulate(const float* __restrict__ Pp, in
         acc[k] = 0.0f;
         off[k] = min(acc_slot<NTT>(a, r, k), 2 * NTT - 1) * PL::kSlot + l * PL::kRow;
     }
-    // Software-pipelined: group g + 1's loads are issued before group g's adds whenever its flag is
-    // already set (the flag is read behind group g's loads, so seeing it costs no extra wait), and
-    // the two register sets alternate (the loop is unrolled by two: no register copies).
-    auto load_group = [&](int rs, f4 (&v)[kQ][NS]) __attribute__((always_inline)) {
-#ifdef GNSSHIP_EXP_NOACC  // timing experiment: the accumulator only follows the flags
-        return;
-#endif
-        const float* src = Pp + static_cast<size_t>(rs) * PL::kGroup;
+    unsigned long long w_flag = 0;  // profiling: cycles spent waiting for the groups' flags
+    [[maybe_unused]] const unsigned long long t_run = GNSSHIP_FCLOCK();
+    int rslot = 0;
+    // per group: its flag, then all its loads in one batch, then the adds in iteration order (every
+    // group is added whole: a partial group's iterations past the epoch's end hold −0)
+    for (int g = 0; g < n_groups; g++) {
+        const unsigned long long t0 = GNSSHIP_FCLOCK();
+        lds_wait_eq(ready + 2 * rslot, gbase + g + 1);  // the group's loads follow the flag
+        const float* src = Pp + static_cast<size_t>(rslot) * PL::kGroup;
+        f4 v[kQ][NS];
 #pragma unroll
         for (int q = 0; q < kQ; q++)
 #pragma unroll
             for (int k = 0; k < NS; k++) v[q][k] = *reinterpret_cast<const f4*>(src + off[k] + 4 * q);
-    };
-    auto wait_group = [&](int g, int rsl) __attribute__((always_inline)) {
-        lds_wait_eq(ready + 2 * rsl, gbase + g + 1);
-        if (NH == 2) {
-            lds_wait_eq(ready + 2 * rsl + 1, gbase + g + 1);
-            // both producers of the group have read its phasor slots: accumulator 0 re-arms them
-            const int t = 4 * g + (lane >> 4);
-            if (a == 0 && t < S) store_slot(Zs + (t % rs) * kAvxLanes + (lane & (kAvxLanes - 1)), __builtin_bit_cast(f2, kSlotEmpty));
-        }
-        asm volatile("" ::: "memory");  // the group's loads follow the flag
-    };
-    // group g from registers `cur` (its loads issued); group g + 1 into `nxt`.  Returns whether
-    // group g + 1's loads were issued.
-    auto step = [&](int g, int rs, bool cur_issued, f4 (&cur)[kQ][NS], f4 (&nxt)[kQ][NS]) __attribute__((always_inline)) {
-        if (!cur_issued) {
-            wait_group(g, rs);
-            load_group(rs, cur);
-        }
-        if (g == 0) GNSSHIP_FSTAMP(pe, 28);
-        if (g == n_groups - 1) GNSSHIP_FSTAMP(pe, 29);
-        if (g < 8) GNSSHIP_FSTAMP(pe, 56 + g);
-        const int rn = rs + 1 == rg ? 0 : rs + 1;
-        bool next = false;
-        if (NH == 1 && g + 1 < n_groups && __hip_atomic_load(ready + 2 * rn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == gbase + g + 2) {
-            asm volatile("" ::: "memory");
-            load_group(rn, nxt);
-            next = true;
-        }
-        // every group is added whole: a partial group's iterations past the epoch's end hold −0
-#pragma unroll
-        for (int q = 0; q < kQ; q++)
-#pragma unroll
-            for (int k = 0; k < NS; k++)
-#pragma unroll
-                for (int u = 0; u < 4; u++) acc[k] = __fadd_rn(acc[k], cur[q][k][u]);
-        // released after its adds: they consumed every load of the group, so the ring slot may be
-        // rewritten (no wait: group g + 1's loads may still be in flight)
-#pragma unroll
-        for (int k = 0; k < NS; k++) asm volatile("" ::"v"(acc[k]) : "memory");
-        if (lane == 0) __hip_atomic_store(acc_done, gbase + g + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        if (g < 8) GNSSHIP_FSTAMP(pe, 64 + g);
-        return next;
-    };
-    int rslot = 0;
-#if GNSSHIP_ACC_PIPE
-    f4 va[kQ][NS], vb[kQ][NS];
-    bool issued = false;
-    for (int g = 0; g < n_groups; g += 2) {
-        issued = step(g, rslot, issued, va, vb);
-        rslot = rslot + 1 == rg ? 0 : rslot + 1;
-        if (g + 1 < n_groups) {
-            issued = step(g + 1, rslot, issued, vb, va);
-            rslot = rslot + 1 == rg ? 0 : rslot + 1;
-        }
-    }
-#else
-    (void)step;
-    unsigned long long w_flag = 0;  // profiling: cycles spent waiting for the groups' flags
-    const unsigned long long t_run = GNSSHIP_FCLOCK();
-    auto add_group = [&](const f4 (&v)[kQ][NS]) __attribute__((always_inline)) {
+        w_flag += GNSSHIP_FCLOCK() - t0;
 #pragma unroll
         for (int q = 0; q < kQ; q++)
 #pragma unroll
             for (int k = 0; k < NS; k++)
 #pragma unroll
                 for (int u = 0; u < 4; u++) acc[k] = __fadd_rn(acc[k], v[q][k][u]);
-    };
-    // Groups in pairs when both are ready (the accumulator is usually behind, and each LDS round
-    // trip — flag, then data — is what a group costs it): the two flags in one read batch, then the
-    // two groups' loads in one batch, then their adds in order.
-    for (int g = 0; g < n_groups;) {
-        const unsigned long long t0 = GNSSHIP_FCLOCK();
-        const int rn = rslot + 1 == rg ? 0 : rslot + 1;
-        bool pair = false;
-#if GNSSHIP_ACC_PAIRS
-        if (NH == 1 && g + 1 < n_groups) {
-            const int f0 = __hip_atomic_load(ready + 2 * rslot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            const int f1 = __hip_atomic_load(ready + 2 * rn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            pair = __builtin_amdgcn_readfirstlane(f0 == gbase + g + 1 && f1 == gbase + g + 2);
-        }
-#endif
-        f4 v[kQ][NS];
-        if (pair) {
-            asm volatile("" ::: "memory");  // the groups' loads follow both flags
-            f4 v2[kQ][NS];
-            load_group(rslot, v);
-            load_group(rn, v2);
-            w_flag += GNSSHIP_FCLOCK() - t0;
-            add_group(v);
-            add_group(v2);
-        } else {
-            wait_group(g, rslot);
-            load_group(rslot, v);
-            w_flag += GNSSHIP_FCLOCK() - t0;
-            add_group(v);
-        }
         if (g == 0) GNSSHIP_FSTAMP(pe, 28);
-        if (g + (pair ? 1 : 0) == n_groups - 1) GNSSHIP_FSTAMP(pe, 29);
+        if (g == n_groups - 1) GNSSHIP_FSTAMP(pe, 29);
+        // released after its adds: they consumed every load of the group, so the ring slot may be rewritten
 #pragma unroll
         for (int k = 0; k < NS; k++) asm volatile("" ::"v"(acc[k]) : "memory");
         GNSSHIP_PROBE(GNSSHIP_DELAY_ACC);
-        g += pair ? 2 : 1;
-        if (lane == 0) __hip_atomic_store(acc_done, gbase + g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        rslot = pair ? (rn + 1 == rg ? 0 : rn + 1) : rn;
+        if (lane == 0) __hip_atomic_store(acc_done, gbase + g + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        rslot = rslot + 1 == rg ? 0 : rslot + 1;
     }
     if (a < 2) {  // slots 44/45 (accumulator 0), 46/47 (accumulator 1): flag waits, whole accumulation
         GNSSHIP_FVAL(pe, 44 + 2 * a, w_flag);
         GNSSHIP_FVAL(pe, 45 + 2 * a, GNSSHIP_FCLOCK() - t_run);
     }
-#endif
 }
 
 // u_avx's final combination of the 16 chains (:279-291), valid at lane 0 of each 16-lane row:
@@ -1225,10 +1011,7 @@ __global__ __launch_bounds__(W * kWave, (fast_waves_per_simd<THRU, W>())) void t
         sh.step_seq = 0;
         sh.pred_seq = 0;
         sh.verdict = 0;
-        sh.pll_seq = sh.dll_seq = sh.early_seq = 0;
-#ifdef GNSSHIP_EXP_SERIAL
-        g_replay_done = 0;
-#endif
+        sh.pll_seq = sh.dll_seq = 0;
     }
     __syncthreads();
     if (skip) return;  // idle channel: its state is untouched
@@ -1368,18 +1151,7 @@ __global__ __launch_bounds__(W * kWave, (fast_waves_per_simd<THRU, W>())) void t
     // One epoch loop per role: the roles never share a control-flow path, so the waits the compiler
     // places for one role's memory operations are not charged to another (a merged loop made the
     // control wave wait for the producers' sample loads it never issued).
-#ifdef GNSSHIP_PRIO_ACC  // A/B: the accumulators issue ahead of their SIMD partner
-    if (role == kRoleAccum) __builtin_amdgcn_s_setprio(GNSSHIP_PRIO_ACC);
-#endif
-#ifdef GNSSHIP_PRIO_ROLES  // A/B: issue priority by role — phasor 3, accumulators 2, control 1, producers 0
-    if (role == kRoleReplay) __builtin_amdgcn_s_setprio(3);
-    else if (role == kRoleAccum) __builtin_amdgcn_s_setprio(2);
-    else if (role == kRoleControl) __builtin_amdgcn_s_setprio(1);
-#endif
     if (role == kRoleReplay) {
-#ifdef GNSSHIP_PRIO_REPLAY
-        __builtin_amdgcn_s_setprio(GNSSHIP_PRIO_REPLAY);
-#endif
         for (int e = 0;; e++) {
             FJob job;
                 // ---- derive: the phasors of the seeded epoch ----
@@ -1477,18 +1249,12 @@ __global__ __launch_bounds__(W * kWave, (fast_waves_per_simd<THRU, W>())) void t
                     if (lane == 0) publish_seq(&sh.job_seq, e + 1);
                     if (!sd.runnable) break;
                 }
-#ifdef GNSSHIP_EXP_SERIAL
-                if (published && lane == 0) __hip_atomic_store(&g_replay_done, e + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-#endif
                 GNSSHIP_FSTAMP(e, 1);
                 GNSSHIP_FCLK(e, 12);
                 job = uniform_job(sh.job);
                 if (!published) {
                     xl = (lane & 1) ? zinit.y : zinit.x;
                     if (lane < 2 * kAvxLanes) xl = fast_replay<G, SRING>(xl, job.dz_re, (lane & 1) ? job.dz_im : -job.dz_im, M, S, tail, Zs, rs, lane);
-#ifdef GNSSHIP_EXP_SERIAL
-                    if (lane == 0) __hip_atomic_store(&g_replay_done, e + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-#endif
                 }
                 if (tail > 0) {  // the serial tail from normalise(z_0) after the loop (:294-308)
                     const i4v span = sample_span<FMT>(samples, job.off, N);
@@ -1511,57 +1277,30 @@ __global__ __launch_bounds__(W * kWave, (fast_waves_per_simd<THRU, W>())) void t
                 GNSSHIP_FCLK(e, 13);
         }
     } else if (role == kRoleProducer) {
-        constexpr int NHp = producers_per_group<NTT, kFWaves, G>();
-        constexpr int GHp = G / NHp;
-        f2 xa[GHp < 8 ? GHp : 8];
-        float cv[GHp][NTT];
+        f2 xa[G < 8 ? G : 8];
+        float cv[G][NTT];
         for (int e = 0;; e++) {
             const int gbase = e * n_groups;  // the epoch's first product-group tag - 1
-            // the early arguments (state 4: published by the control wave before it makes the seed)
-            // let the first group's sample loads and code values start ahead of the job
-            int early_in = -1;  // the in_margin the early phase A ran with (-1: none)
-            FJob ej;
-            if (GNSSHIP_EARLY_JOB) {
-                while (__hip_atomic_load(&sh.early_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < e + 1 &&
-                       __hip_atomic_load(&sh.job_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < e + 1)
-                    __builtin_amdgcn_s_sleep(GNSSHIP_POLL_SLEEP);
-                if (__hip_atomic_load(&sh.early_seq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) >= e + 1) {
-                    ej = uniform_job(sh.early);
-                    const i4v espan = sample_span<FMT>(samples, ej.off, N);
-                    if (ej.in_margin)
-                        fast_produce_early<FMT, NT, DATA, true, G, kFWaves>(ej, espan, c0, c1, L, lane, pw, xa, cv);
-                    else
-                        fast_produce_early<FMT, NT, DATA, false, G, kFWaves>(ej, espan, c0, c1, L, lane, pw, xa, cv);
-                    early_in = ej.in_margin;
-                }
-            }
             wait_seq(&sh.job_seq, e + 1);
             const FJob job = uniform_job(sh.job);
             if (!job.runnable) break;
-                // the early phase A stands if it ran on the job's own arguments (it always does: the
-                // control wave publishes both from the same values; checked bit for bit)
-                const bool pre = early_in >= 0 && ej.off == job.off && early_in == job.in_margin && ej.M == job.M && ej.S == job.S &&
-                                 __builtin_bit_cast(uint32_t, ej.rem_code) == __builtin_bit_cast(uint32_t, job.rem_code) &&
-                                 __builtin_bit_cast(uint32_t, ej.code_step) == __builtin_bit_cast(uint32_t, job.code_step) &&
-                                 __builtin_bit_cast(uint32_t, ej.shifts[0]) == __builtin_bit_cast(uint32_t, job.shifts[0]) &&
-                                 __builtin_bit_cast(uint32_t, ej.shifts[NT - 1]) == __builtin_bit_cast(uint32_t, job.shifts[NT - 1]);
-                const i4v span = sample_span<FMT>(samples, job.off, N);
-                if (job.in_margin)
-                    fast_produce<FMT, NT, DATA, true, G, kFWaves>(job, span, c0, c1, L, Zs, rs, Pp, rg, ready, sh.acc_groups, gbase, lane, pw, e, pre, xa, cv);
-                else
-                    fast_produce<FMT, NT, DATA, false, G, kFWaves>(job, span, c0, c1, L, Zs, rs, Pp, rg, ready, sh.acc_groups, gbase, lane, pw, e, pre, xa, cv);
-                if (pw < 2) GNSSHIP_FSTAMP(e, 3 + pw);  // 3, 4: producers 0 and 1 done
-                if (pw == 0) {
-                    // cn0_and_tracking_lock_status (:972-1029) on the LDS copy of its members, beside the loop update
-                    wait_seq(&sh.pre_seq, e + 1);
-                    const double coh = sh.coh;
-                    if (lane == 0) {
-                        GNSSHIP_TRK_LOOP_STAMP(8);
-                        sh.locked = (coh > 0.0 && !lock_status(k, sc, coh)) ? 0 : 1;
-                        GNSSHIP_TRK_LOOP_STAMP(26);
-                        publish_seq(&sh.lock_seq, e + 1);
-                    }
+            const i4v span = sample_span<FMT>(samples, job.off, N);
+            if (job.in_margin)
+                fast_produce<FMT, NT, DATA, true, G, kFWaves>(job, span, c0, c1, L, Zs, rs, Pp, rg, ready, sh.acc_groups, gbase, lane, pw, e, xa, cv);
+            else
+                fast_produce<FMT, NT, DATA, false, G, kFWaves>(job, span, c0, c1, L, Zs, rs, Pp, rg, ready, sh.acc_groups, gbase, lane, pw, e, xa, cv);
+            if (pw < 2) GNSSHIP_FSTAMP(e, 3 + pw);  // 3, 4: producers 0 and 1 done
+            if (pw == 0) {
+                // cn0_and_tracking_lock_status (:972-1029) on the LDS copy of its members, beside the loop update
+                wait_seq(&sh.pre_seq, e + 1);
+                const double coh = sh.coh;
+                if (lane == 0) {
+                    GNSSHIP_TRK_LOOP_STAMP(8);
+                    sh.locked = (coh > 0.0 && !lock_status(k, sc, coh)) ? 0 : 1;
+                    GNSSHIP_TRK_LOOP_STAMP(26);
+                    publish_seq(&sh.lock_seq, e + 1);
                 }
+            }
         }
     } else if (role == kRoleAccum) {
         for (int e = 0;; e++) {
@@ -1574,7 +1313,7 @@ __global__ __launch_bounds__(W * kWave, (fast_waves_per_simd<THRU, W>())) void t
                 constexpr int NS = acc_slots<NTT>();
                 float acc[NS];
                 GNSSHIP_FSTAMP(e, 27);
-                fast_accumulate<NTT, G, kFWaves>(Pp, rg, ready, &sh.acc_groups[pw], gbase, S, lane, pw, acc, e, Zs, rs);
+                fast_accumulate<NTT, G>(Pp, rg, ready, &sh.acc_groups[pw], gbase, S, lane, pw, acc, e);
                 GNSSHIP_FSTAMP(e, 5);
                 const int r = lane >> 4;
     #pragma unroll
@@ -1633,9 +1372,6 @@ __global__ __launch_bounds__(W * kWave, (fast_waves_per_simd<THRU, W>())) void t
             GNSSHIP_FSTAMP(e, 6);
         }
     } else {
-#ifdef GNSSHIP_PRIO_CONTROL
-        __builtin_amdgcn_s_setprio(GNSSHIP_PRIO_CONTROL);
-#endif
         for (int e = 0;; e++) {
             const int gbase = e * n_groups;  // the epoch's first product-group tag - 1
             wait_seq(&sh.job_seq, e + 1);
@@ -1716,15 +1452,6 @@ __global__ __launch_bounds__(W * kWave, (fast_waves_per_simd<THRU, W>())) void t
                     const int64_t k_ifn = rc.if_num;
                     const double k_ifc = rc.if_cyc;
                     if (rc.state == 4) {
-                        // the next epoch's code and sample arguments to the producers first (their first
-                        // group's loads and code values start while the seed is made)
-                        if (GNSSHIP_EARLY_JOB && lane == 0) {
-                            const uint64_t nir = rc.epoch_start + static_cast<uint64_t>(rc.current_prn_length_samples);  // epoch_consume's
-                            if (e + 1 < max_rounds && nir >= buf_first && nir + vl <= buf_first + static_cast<uint64_t>(buf_len)) {
-                                code_fields(sh.early, nir);
-                                publish_seq(&sh.early_seq, e + 2);
-                            }
-                        }
                         epoch_consume(kp, rc);
                         make_seed(e + 1);
                         GNSSHIP_FSTAMP(e, 33);

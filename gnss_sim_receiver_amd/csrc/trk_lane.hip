@@ -19,6 +19,7 @@
 // gnsship_code_set): the product a·c of the sample product with a ±1 chip is a sign flip, exact, so the
 // taps are bit-identical to the float replica's.  The latency form for few channels is trk_fast.hip.
 #include <algorithm>
+#include <cstddef>
 #include <cstdlib>
 #include <type_traits>
 
@@ -263,6 +264,9 @@ __global__ __launch_bounds__(kLThreads, GNSSHIP_LANE_OCC) void trk_lane_kernel(c
         stage_code_bits(d0, codes[cr.code_id], CW, lane);
         if constexpr (DATA) stage_code_bits(d0 + CW, codes[cr.data_code_id], CW, lane);
     }
+    // lane 0 wrote the replicas (and, below, each row's lane 0 updates its channel in LDS) that the
+    // row's other lanes read next: order those LDS accesses within the wave
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     const int L = valid ? codes[c.code_id].len : 1;
     const int N = static_cast<int>(k.conf.vector_length);
     const int M = N / kAvxLanes, tail = N - kAvxLanes * M;
@@ -351,13 +355,20 @@ __global__ __launch_bounds__(kLThreads, GNSSHIP_LANE_OCC) void trk_lane_kernel(c
             }
         }
         if (lane == 0) atomicAdd(ran_count + e, __popcll(run_rows));
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");  // the loop update's state, before the next epoch's reads
     }
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");  // before the write-back reads the updated state
     if (valid) {
         if (l == 0) c.ran = 0;
+        // the channel's state back to HBM, all but the prompt buffer's unused capacity (entries past
+        // cn0_samples are never written: 352 of the 928 bytes at the default 20 samples)
         constexpr int kWords = sizeof(TrkChannel) / 4;
+        constexpr int kPb = static_cast<int>(offsetof(TrkChannel, prompt_buf) / 4), kPbEnd = kPb + 2 * kTrkMaxCn0Samples;
+        const int pb_used = kPb + 2 * static_cast<int>(k.conf.cn0_samples);
         const int* src = reinterpret_cast<const int*>(&c);
         int* dst = reinterpret_cast<int*>(chans + ch);
-        for (int i = l; i < kWords; i += kAvxLanes) dst[i] = src[i];
+        for (int i = l; i < kWords; i += kAvxLanes)
+            if (i < pb_used || i >= kPbEnd) dst[i] = src[i];
     }
 }
 

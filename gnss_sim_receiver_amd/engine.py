@@ -488,6 +488,23 @@ class DllPllVemlTracking:
                              prn=prn)
         check(self.ctx.lib.gnsship_trk_start(self.h, channel, ctypes.byref(a)), "gnsship_trk_start", self.ctx.h)
 
+    def start_many(self, starts):
+        """gnsship_trk_start_many: `starts` = [(channel, code_id, acq_delay_samples, acq_doppler_hz,
+        acq_samplestamp, first_sample[, data_code_id[, prn]]), ...] in one transaction."""
+        n = len(starts)
+        if n == 0:
+            return
+        chans = (ctypes.c_int32 * n)()
+        args = (abi.TrkStartArgs * n)()
+        for i, st in enumerate(starts):
+            ch, code_id, delay, dop, stamp, first = st[:6]
+            data_code_id = st[6] if len(st) > 6 else -1
+            prn = st[7] if len(st) > 7 else 0
+            chans[i] = ch
+            args[i] = abi.TrkStartArgs(code_id=code_id, data_code_id=data_code_id, acq_delay_samples=delay, acq_doppler_hz=dop,
+                                       acq_samplestamp_samples=stamp, first_sample=first, prn=prn)
+        check(self.ctx.lib.gnsship_trk_start_many(self.h, n, chans, args), "gnsship_trk_start_many", self.ctx.h)
+
     def stop(self, channel: int):
         check(self.ctx.lib.gnsship_trk_stop(self.h, channel), "gnsship_trk_stop", self.ctx.h)
 

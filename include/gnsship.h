@@ -397,6 +397,10 @@ typedef struct gnsship_trk_epoch { /* one general_work call of one channel (Gnss
 typedef struct gnsship_trk gnsship_trk;
 int gnsship_trk_create(gnsship_ctx* ctx, const gnsship_trk_conf* conf, int max_channels, gnsship_trk** out);
 int gnsship_trk_start(gnsship_trk* t, int channel, const gnsship_trk_start_args* args);
+/* n gnsship_trk_start calls in one transaction (a mass hand-off from acquisition): channels[i]
+ * starts from args[i]; every channel is validated before any device state changes (on an error
+ * nothing is started); one upload, one scatter launch, one synchronisation.  Distinct channels. */
+int gnsship_trk_start_many(gnsship_trk* t, int n, const int32_t* channels, const gnsship_trk_start_args* args);
 int gnsship_trk_stop(gnsship_trk* t, int channel);
 /* msg_handler_telemetry_to_trk (dll_pll_veml_tracking.cc:617-640): a telemetry fault (tlm_event 1)
  * from the channel's telemetry decoder sets the carrier lock-fail counter to 200000, so the next

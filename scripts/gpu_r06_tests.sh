@@ -3,7 +3,7 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT
 O=gpurun_out/${OUT:-r06iter}
 mkdir -p $O
-timeout -k 10 ${TLIM:-900} python3 -u -m pytest -x -v -rA --timeout 300 --timeout-method thread -m gpu $TESTS > $O/tests.log 2>&1
+timeout -k 10 ${TLIM:-900} python3 -u -m pytest -x -v -rA --timeout 170 --timeout-method thread -m gpu $TESTS > $O/tests.log 2>&1
 rc=$?
 tail -n 8 $O/tests.log
 [ $rc -ne 0 ] && { grep -E "FAILED|Error|error|assert" $O/tests.log | head -30; exit 1; }

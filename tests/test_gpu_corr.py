@@ -144,7 +144,7 @@ def test_bounds_and_state_errors(ctx):
     j = np.array([mk_job(100, 1000, 0, [0.0], 0, 0, 0, 0.25)], abi.JOB_DTYPE)
     with pytest.raises(abi.GnssHipError):
         b.set_jobs(j, 500)  # reads past the buffer
-    j2 = np.array([mk_job(0, 10, 7, [0.0], 0, 0, 0, 0.25)], abi.JOB_DTYPE)
+    j2 = np.array([mk_job(0, 10, 9999, [0.0], 0, 0, 0, 0.25)], abi.JOB_DTYPE)
     with pytest.raises(abi.GnssHipError):
         b.set_jobs(j2, 500)  # unset code id
     j3 = np.array([mk_job(0, 10, 0, [0.0] * 1, 0, 0, 0, 0.25)], abi.JOB_DTYPE)

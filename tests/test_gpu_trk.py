@@ -335,3 +335,34 @@ def test_auto_rotator_with_unreproduced_preference_fails_create(tmp_path):
     assert out.returncode == 0, out.stderr
     last = out.stdout.strip().splitlines()[-1]
     assert last.startswith("ERR") and "E_INVAL" in last and "generic_reload" in last, last
+
+
+def test_start_many_matches_start(ctx):
+    """gnsship_trk_start_many (one upload, one scatter, one sync) starts channels exactly as
+    gnsship_trk_start does: the runs' records are identical; a bad entry starts nothing."""
+    sats = [S.sync("GPS", 4e6, 150, prn=p, dop=d, delay_chips=c, seed=p) for p, d, c in ((3, 900.0, 10.5), (9, -1500.0, 700.2), (17, 40.0, 333.3))]
+    x = np.sum([s[2] for s in sats], axis=0).astype(np.complex64)
+    k, first = sats[0][1], sats[0][4]
+    starts = []
+    for i, (sat, _, _, stamp, _, delay, dop) in enumerate(sats):
+        ctx.set_code(90 + i, sat.code)
+        starts.append((2 * i + 1, 90 + i, delay, dop, stamp, first))
+    recs = []
+    for many in (False, True):
+        trk = engine.DllPllVemlTracking(ctx, dev_conf(k, "GPS"), 7)
+        if many:
+            trk.start_many(starts)
+        else:
+            for st in starts:
+                trk.start(*st)
+        rec, rounds = trk.run(x, first, 150)
+        recs.append(rec)
+        if many:
+            with pytest.raises(abi.GnssHipError):  # a channel twice
+                trk.start_many([(0, 90, 10.0, 0.0, 0, first), (0, 91, 10.0, 0.0, 0, first)])
+            with pytest.raises(abi.GnssHipError):  # the second entry's code is not in the bank: nothing starts
+                trk.start_many([(0, 90, 10.0, 0.0, 0, first), (2, 999, 10.0, 0.0, 0, first)])
+            assert trk.channel_state(0)[0] == 0
+        trk.close()
+    assert np.array_equal(recs[0].view(np.uint8), recs[1].view(np.uint8))
+    assert np.count_nonzero(recs[1][:, 1]["flags"] & 8) == 150

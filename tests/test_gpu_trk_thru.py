@@ -69,3 +69,49 @@ def test_1024_avx_channels_default_dispatch_exact(ctx, form, monkeypatch):
         assert np.count_nonzero(ref["state"] == 4) > 0, (label, "the sampled channel never reached state 4")
     assert n_traced >= 8 * 500
     assert np.mean(states >= 2) >= 0.95, np.bincount(states)
+
+
+def test_512_avx_channels_25msps_default_dispatch_exact(ctx):
+    """north_star's second rate: 512 GPS L1 C/A channels at 25 Msps (N = 25000 = 1562 u_avx iterations
+    + an 8-sample serial tail, gps_l1_ca_dll_pll_tracking.cc:47) through the default dispatch — the
+    lane form behind bench.py's tracked_channels_sustained_25msps.  Eight sampled channels bit for bit:
+    traced taps on the device's own arguments and every record field against the oracle loop."""
+    fs, vl, n_ch, epochs = 25e6, 25000, 512, 300
+    sats = signals.random_sky(32, seed=0x6E550022)
+    for s in sats:
+        s.bits = "1000101100110"
+    k = T.conf("GPS", fs, vl, rotator_avx=1)
+    first = int(11 * fs)
+    x = signals.generate_if_device(fs, vl * (epochs + 4), sats, seed=0x6E550023, start=first, device="cpu").numpy()
+    trk = engine.DllPllVemlTracking(ctx, dev_conf(k, "GPS"), n_ch)
+    for i, s in enumerate(sats):
+        ctx.set_code(700 + i, s.code)
+    starts = []
+    for ch in range(n_ch):
+        s = sats[ch % 32]
+        lap = ch // 32
+        delay = signals.acq_delay_samples(s, fs, 0, first) + 2.3 * ((lap * 7) % 5 - 2) / 2.0
+        dop = s.doppler_hz + 2.5 * ((lap * 11) % 9 - 4)
+        trk.start(ch, 700 + ch % 32, delay, dop, 0, first)
+        starts.append((delay, dop))
+    trk.set_trace(True)
+    rec, rounds = trk.run(x, first, epochs)
+    assert rounds == epochs
+    assert trk.last_engine() == abi.TRK_ENGINE_LANES, abi.TRK_ENGINE_NAMES[trk.last_engine()]
+    tr = trk.trace(epochs)
+    states = trk.states()
+    trk.close()
+    xf = x.astype(np.complex64)
+    sample = [0, 45, 130, 255, 256, 377, 480, 511]
+
+    def oracle(ch):
+        s = sats[ch % 32]
+        return T.track(k, xf, s.code, starts[ch][0], starts[ch][1], 0, first, epochs, buffer_first=first)
+
+    with cf.ThreadPoolExecutor(8) as ex:
+        refs = dict(zip(sample, ex.map(oracle, sample)))
+    for ch, ref in refs.items():
+        label = f"25 Msps lane form ch{ch}"
+        trace_exact(tr[:, ch], xf, first, sats[ch % 32].code, None, label)
+        compare_exact(rec[:, ch], ref, label)
+    assert np.mean(states >= 2) >= 0.95, np.bincount(states)
