@@ -824,7 +824,7 @@ def acq_e1_bench(ctx, reps=5):
     present = {s.prn for s in sats}
     stat = np.array([r.test_statistic for r in res])
     cells = 32 * acq.n_bins
-    out = {"config": "Galileo E1: 32 PRN x 40 bins, fft 100000 (huge layout, 8 x 12500), 25 Msps, first-vs-second statistic",
+    out = {"config": "Galileo E1: 32 PRN x 40 bins, fft 100000 (huge layout, 10 x 10000), 25 Msps, first-vs-second statistic",
            "sweep_ms": round(dt * 1e3, 3), "sweeps_per_s": round(1 / dt, 1), "cells_per_s": round(cells / dt, 0),
            "prns_present": sorted(present),
            "present_min_test_statistic": round(float(min(stat[p - 1] for p in present)), 2),

@@ -61,7 +61,20 @@ bool choose_acq_layout(int n, int force, FftPlan& plan, int& P, bool& huge)
         }
     }
     if (n < 8 || n > kMaxAcqHugeN) return false;
+    // Prefer rows with a compile-time plan: 10000 = 10⁴ (four radix-10 passes, one butterfly per
+    // thread) before 12500 (five passes, two or three butterflies per thread); GNSSHIP_ACQ_HUGE_P
+    // picks P for measurement.
+    int p_env = 0;
+    if (const char* env = std::getenv("GNSSHIP_ACQ_HUGE_P")) p_env = std::atoi(env);
+    for (const int mc : {10000, 12500}) {
+        const int p = n / mc;
+        if (n % mc != 0 || !huge_p_supported(p) || (p_env && p != p_env) || !make_fft_plan(mc, plan)) continue;
+        P = p;
+        huge = true;
+        return true;
+    }
     for (int p = 4; p <= 32; p++) {
+        if (p_env && p != p_env) continue;
         if (!huge_p_supported(p) || n % p != 0) continue;
         if (make_fft_plan(n / p, plan)) {
             P = p;

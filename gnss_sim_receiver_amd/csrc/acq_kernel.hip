@@ -1511,6 +1511,8 @@ __global__ __launch_bounds__(kAcqThreads) void acq_huge_finalize_kernel(const fl
 }
 
 
+bool huge_ct_rows(int M) { return M == 10000 || M == 12500; }
+
 bool huge_p_supported(int P)
 {
 #define GNSSHIP_P_CASE(p) \
@@ -1548,10 +1550,15 @@ hipError_t launch_acq_fft_huge(const void* sig, int fmt, const float2* mult, int
     if (e != hipSuccess) return e;
     const size_t lds = sizeof(float2) * static_cast<size_t>(M);
     const size_t lds_q = sizeof(float2) * static_cast<size_t>(M + M / 4);  // + the quarter twiddle table
-    if (M == 12500)  // Galileo E1 at 25 Msps (N = 100000 = 8 × 12500), GPS/B1I at 50 Msps: compile-time plan
-        hipLaunchKernelGGL((acq_huge_rows_kernel<-1, 12500>), dim3(P, n_rows, 1), dim3(kAcqThreads), lds_q, stream, scratch, N, int64_t(0),
-            static_cast<const float2*>(nullptr), int64_t(0), int64_t(0), rowsT, N, int64_t(0), row_plan, twM, conj_out);
+    // the compile-time rows (huge_ct_rows): Galileo E1 at 25 Msps (N = 100000 = 10 × 10000), GPS/B1I at
+    // 50 Msps (5 × 10000), E1 at 50 Msps (20 × 10000); 12500-point rows where 10000 does not divide N
+#define GNSSHIP_CT_ROWS(mc)                                                                                                               \
+    if (M == mc)                                                                                                                          \
+        hipLaunchKernelGGL((acq_huge_rows_kernel<-1, mc>), dim3(P, n_rows, 1), dim3(kAcqThreads), lds_q, stream, scratch, N, int64_t(0), \
+            static_cast<const float2*>(nullptr), int64_t(0), int64_t(0), rowsT, N, int64_t(0), row_plan, twM, conj_out);                  \
     else
+    GNSSHIP_CT_ROWS(10000) GNSSHIP_CT_ROWS(12500)
+#undef GNSSHIP_CT_ROWS
         hipLaunchKernelGGL((acq_huge_rows_kernel<-1>), dim3(P, n_rows, 1), dim3(kAcqThreads), lds, stream, scratch, N, int64_t(0),
             static_cast<const float2*>(nullptr), int64_t(0), int64_t(0), rowsT, N, int64_t(0), row_plan, twM, conj_out);
     return hipGetLastError();
@@ -1566,15 +1573,19 @@ hipError_t launch_acq_search_huge(const float2* XT, const float2* codesT, int pr
     const size_t lds = sizeof(float2) * static_cast<size_t>(M);
     const size_t lds_q = sizeof(float2) * static_cast<size_t>(M + M / 4);
     // rows: blockIdx.y = bin (XT row set), blockIdx.z = prn (code spectrum), U cell = z·n_bins + y
-    if (M == 12500) {
-        // persistent: one workgroup per CU (125 KB of LDS each), rows pipelined through it
+    if (huge_ct_rows(M)) {
+        // persistent: one workgroup per CU (100 or 125 KB of LDS each), rows pipelined through it
         int n_cu = 256;
         int dev = 0;
         if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) n_cu = 256;
         const int total = P * n_bins * n_prns;
         const int blocks = total < n_cu ? total : n_cu;
-        hipLaunchKernelGGL((acq_huge_rows_pipe_kernel<+1, 12500>), dim3(blocks), dim3(kAcqThreads), lds_q, stream, XT, N, int64_t(0),
-            codesT + static_cast<int64_t>(prn_offset) * N, int64_t(0), N, U, N, N * n_bins, twM, P, n_bins, n_prns);
+        if (M == 10000)
+            hipLaunchKernelGGL((acq_huge_rows_pipe_kernel<+1, 10000>), dim3(blocks), dim3(kAcqThreads), lds_q, stream, XT, N, int64_t(0),
+                codesT + static_cast<int64_t>(prn_offset) * N, int64_t(0), N, U, N, N * n_bins, twM, P, n_bins, n_prns);
+        else
+            hipLaunchKernelGGL((acq_huge_rows_pipe_kernel<+1, 12500>), dim3(blocks), dim3(kAcqThreads), lds_q, stream, XT, N, int64_t(0),
+                codesT + static_cast<int64_t>(prn_offset) * N, int64_t(0), N, U, N, N * n_bins, twM, P, n_bins, n_prns);
     }
     else
         hipLaunchKernelGGL((acq_huge_rows_kernel<+1>), dim3(P, n_bins, n_prns), dim3(kAcqThreads), lds, stream, XT, N, int64_t(0),
