@@ -107,6 +107,7 @@ struct gnsship_acq {
     float* grid_scratch = nullptr; // unused: the huge search keeps no |y|² rows without a kept grid
     TileStat* tiles = nullptr;   // huge: lanes × prn_batch × n_bins × huge_tiles(M)
     int prn_batch = 0;
+    int first_share = 50;        // huge, two lanes: percent of the PRNs in the first batch
     int lanes = 1;               // huge: PRN batches in flight together (U and tiles per lane)
     hipStream_t lane_stream = nullptr;  // huge, lanes = 2: the second batch lane
     hipEvent_t ev_fwd = nullptr, ev_lane = nullptr;
@@ -117,6 +118,9 @@ struct gnsship_acq {
     float2* codes_fft = nullptr; // max_prns × N  conj(FFT(code))
     float2* X = nullptr;         // n_bins × N  FFT(in ⊙ w_b)
     RowStat* rowstat = nullptr;  // max_prns × n_bins
+    // The decision kernel writes the results straight into mapped pinned host memory (res_dev is its
+    // device address): no device-to-host copy after the sweep, only the host memcpy to the caller.
+    gnsship_acq_result* res_host = nullptr;
     gnsship_acq_result* res_dev = nullptr;
     void* sig_dev = nullptr;     // staging for host input (N CF32)
     float* grid_dev = nullptr;   // optional |Y|² grid (max_prns × n_bins × N)
@@ -178,9 +182,10 @@ extern "C" int gnsship_acq_destroy(gnsship_acq* a)
     (void)hipStreamSynchronize(a->ctx->stream);
     acq_free_grid_buffers(a);
     acq_graph_reset(a);
-    void* ptrs[] = {a->tw, a->twM, a->twC, a->codes_fft, a->res_dev, a->sig_dev};
+    void* ptrs[] = {a->tw, a->twM, a->twC, a->codes_fft, a->sig_dev};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
+    if (a->res_host) (void)hipHostFree(a->res_host);
     if (a->lane_stream) (void)hipStreamDestroy(a->lane_stream);
     if (a->ev_fwd) (void)hipEventDestroy(a->ev_fwd);
     if (a->ev_lane) (void)hipEventDestroy(a->ev_lane);
@@ -204,19 +209,21 @@ static int acq_upload_wipeoffs(gnsship_acq* a, int nb, const std::vector<float>&
         HIP_TRY(ctx, hipMalloc(&a->rowstat, sizeof(RowStat) * static_cast<size_t>(nb) * a->conf.max_prns));
         a->n_bins = nb;
         if (a->huge) {
-            // PRNs searched per round: the inverse row-stage scratch U held to ~128 MiB, so that the
-            // row stage's writes are still in the 256 MB MALL when the column stage reads them
-            // (GNSSHIP_ACQ_U_MIB overrides, for measurement)
+            // PRNs searched per round: the PRNs split over the two batch lanes, one round each (E1 at 25
+            // Msps: 2 × 16 PRNs, 1.05 GB of inverse row-stage scratch U), so that batch 0's column stage
+            // and finalize overlap batch 1's row stage with the fewest persistent-row launches and
+            // drains (GNSSHIP_ACQ_U_MIB caps U instead, for measurement: 0.84 ms at 2 × 16 against 0.89
+            // at 11 + 11 + 10 and 0.94 at 16 rounds of 2; GNSSHIP_ACQ_SPLIT sets the first batch's
+            // percentage: 18 + 14, 20 + 12 and 23 + 9 measured the same as 16 + 16).  Two batch lanes
+            // (GNSSHIP_ACQ_LANES=1: one): batch i runs on lane i mod 2 with its own U and tiles.
             const size_t cell = static_cast<size_t>(nb) * N * sizeof(float2);
-            size_t u_mib = 128;
-            if (const char* env = std::getenv("GNSSHIP_ACQ_U_MIB")) u_mib = static_cast<size_t>(std::max(1, std::atoi(env)));
-            // Two batch lanes (GNSSHIP_ACQ_LANES=1: one): batch i runs on lane i mod 2 with its own U and
-            // tiles, so one batch's column stage and finalize overlap the next batch's row stage (the
-            // persistent row kernel's drain and the finalize's small grid no longer idle the chip);
-            // the two lanes share the U budget.
             a->lanes = 2;
             if (const char* env = std::getenv("GNSSHIP_ACQ_LANES")) a->lanes = std::atoi(env) == 1 ? 1 : 2;
-            int pb = static_cast<int>((u_mib << 20) / (cell * a->lanes));
+            if (const char* env = std::getenv("GNSSHIP_ACQ_SPLIT")) a->first_share = std::min(95, std::max(5, std::atoi(env)));
+            int pb = a->lanes == 2 ? (a->conf.max_prns * a->first_share + 99) / 100 : a->conf.max_prns;
+            size_t u_cap = size_t(4) << 30;  // U above 4 GiB: more, smaller rounds
+            if (const char* env = std::getenv("GNSSHIP_ACQ_U_MIB")) u_cap = static_cast<size_t>(std::max(1, std::atoi(env))) << 20;
+            if (cell * pb * a->lanes > u_cap) pb = static_cast<int>(u_cap / (cell * a->lanes));
             a->prn_batch = pb < 1 ? 1 : (pb > a->conf.max_prns ? a->conf.max_prns : pb);
             const size_t tiles = static_cast<size_t>(a->prn_batch) * nb * huge_tiles(a->plan.n);
             HIP_TRY(ctx, hipMalloc(&a->T, sizeof(float2) * static_cast<size_t>(nb) * N));
@@ -339,7 +346,8 @@ extern "C" int gnsship_acq_create(gnsship_ctx* ctx, const gnsship_acq_conf* conf
         if (e == hipSuccess) e = hipMalloc(&a->twC, sizeof(float2) * N);
         if (e == hipSuccess) e = hipMemcpy(a->twC, twc.data(), sizeof(float2) * N, hipMemcpyHostToDevice);
     }
-    if (e == hipSuccess) e = hipMalloc(&a->res_dev, sizeof(gnsship_acq_result) * conf->max_prns);
+    if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void**>(&a->res_host), sizeof(gnsship_acq_result) * conf->max_prns, hipHostMallocMapped);
+    if (e == hipSuccess) e = hipHostGetDevicePointer(reinterpret_cast<void**>(&a->res_dev), a->res_host, 0);
     if (e == hipSuccess) e = hipMalloc(&a->sig_dev, sizeof(float2) * static_cast<size_t>(N));
     if (e != hipSuccess) {
         gnsship_acq_destroy(a);
@@ -435,8 +443,9 @@ extern "C" int gnsship_acq_run(gnsship_acq* a, const void* sig, int fmt, int sig
             }
             const size_t u_lane = static_cast<size_t>(a->prn_batch) * a->n_bins * a->conf.fft_size;
             const size_t t_lane = static_cast<size_t>(a->prn_batch) * a->n_bins * huge_tiles(a->plan.n);
-            for (int p0 = 0, i = 0; p0 < n_prns; p0 += a->prn_batch, i++) {
-                const int np = std::min(a->prn_batch, n_prns - p0);
+            for (int p0 = 0, i = 0, np = 0; p0 < n_prns; p0 += np, i++) {
+                np = std::min(a->prn_batch, n_prns - p0);
+                if (two && i == 0) np = std::min(np, std::max(1, (n_prns * a->first_share + 99) / 100));
                 const int lane = two ? (i & 1) : 0;  // batches i and i + 2 share a lane's U and tiles, in stream order
                 // without a kept grid the |y|² rows never reach HBM (tile statistics + finalize's recomputation)
                 float* g = keep_grid ? a->grid_dev + static_cast<size_t>(p0) * a->n_bins * rs.row_len : nullptr;
@@ -491,11 +500,11 @@ extern "C" int gnsship_acq_run(gnsship_acq* a, const void* sig, int fmt, int sig
     } else if (int rc = enqueue()) {
         return rc;
     }
-    HIP_TRY(ctx, hipMemcpyAsync(results, a->res_dev, sizeof(gnsship_acq_result) * n_prns, hipMemcpyDeviceToHost, ctx->stream));
     if (grid)
         HIP_TRY(ctx, hipMemcpyAsync(grid, a->grid_dev, sizeof(float) * static_cast<size_t>(n_prns) * a->n_bins * rs.row_len, hipMemcpyDeviceToHost,
                          ctx->stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    std::memcpy(results, a->res_host, sizeof(gnsship_acq_result) * n_prns);
     return GNSSHIP_OK;
 }
 static_assert(sizeof(gnsship_acq_conf) == 64, "gnsship_acq_conf layout (abi.AcqConf)");

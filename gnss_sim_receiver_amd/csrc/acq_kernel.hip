@@ -247,54 +247,64 @@ __device__ __forceinline__ void fft_lds_ct(float2* __restrict__ buf, const float
 // memory its loads sat in every pass's vmcnt queue.  tw[t] for t = q·M/4 + u
 // is tq[u]·(−j)^q — exact, the same float values as the full table (whose entries are rounded from
 // the same double cos/sin up to the quarter-turn symmetry).
+// One butterfly of fft_lds_ct_q's pass at NsC: thread index j's R inputs buf[j + r·nb], twiddled,
+// through the R-point DFT (the only arithmetic of the pass; its output goes to (j / NsC)·NsC·R +
+// j % NsC + r·NsC).
 template <int MC, int NsC, int SIGN>
+__device__ __forceinline__ void ctq_bfly(const float2* __restrict__ buf, const float2* __restrict__ tq, int j, float2 (&v)[ct_radix(MC / NsC)])
+{
+    constexpr int R = ct_radix(MC / NsC);
+    constexpr int nb = MC / R;
+    constexpr int tstep = MC / (NsC * R);
+    constexpr int Q = MC / 4;
+    const int k = j % NsC;
+    if constexpr (NsC > 1 && (NsC - 1) * tstep < Q) {
+        // W^{k·r·tstep} = (W^{k·tstep})^r: one table read (k·tstep < M/4, no quarter turn),
+        // the other powers as a balanced product tree (≤ 4 products deep)
+        float2 w[R];
+        w[1] = tq[k * tstep];
+        if (SIGN > 0) w[1].y = -w[1].y;
+#pragma unroll
+        for (int r = 2; r < R; r++) w[r] = cmulf(w[r / 2], w[r - r / 2]);
+        v[0] = buf[j];
+#pragma unroll
+        for (int r = 1; r < R; r++) v[r] = cmulf(buf[j + r * nb], w[r]);
+    } else {
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+            float2 x = buf[j + r * nb];
+            if (r > 0 && NsC > 1) {
+                const int t = k * r * tstep;  // < MC
+                const int q = t / Q, u = t - q * Q;
+                const float2 w0 = tq[u];
+                float wx = (q & 1) ? w0.y : w0.x, wy = (q & 1) ? -w0.x : w0.y;
+                if (q & 2) {
+                    wx = -wx;
+                    wy = -wy;
+                }
+                if (SIGN > 0) wy = -wy;
+                x = cmulf(x, make_float2(wx, wy));
+            }
+            v[r] = x;
+        }
+    }
+    dft_small<R, SIGN>(v);
+}
+
+// The passes from NsC up to (not including) the one at NSTOP (NSTOP = MC: every remaining pass).
+template <int MC, int NsC, int SIGN, int NSTOP = MC>
 __device__ __forceinline__ void fft_lds_ct_q(float2* __restrict__ buf, const float2* __restrict__ tq, int tid)
 {
     static_assert(MC % 4 == 0, "quarter twiddle table");
-    if constexpr (NsC < MC) {
+    if constexpr (NsC < NSTOP) {
         constexpr int R = ct_radix(MC / NsC);
         constexpr int nb = MC / R;
-        constexpr int tstep = MC / (NsC * R);
-        constexpr int Q = MC / 4;
         constexpr int MAXB = (nb + kAcqThreads - 1) / kAcqThreads;
         float2 v[MAXB][R];
 #pragma unroll
         for (int c = 0; c < MAXB; c++) {
             const int j = tid + c * kAcqThreads;
-            if (j < nb) {
-                const int k = j % NsC;
-                if constexpr (NsC > 1 && (NsC - 1) * tstep < Q) {
-                    // W^{k·r·tstep} = (W^{k·tstep})^r: one table read (k·tstep < M/4, no quarter turn),
-                    // the other powers as a balanced product tree (≤ 4 products deep)
-                    float2 w[R];
-                    w[1] = tq[k * tstep];
-                    if (SIGN > 0) w[1].y = -w[1].y;
-#pragma unroll
-                    for (int r = 2; r < R; r++) w[r] = cmulf(w[r / 2], w[r - r / 2]);
-                    v[c][0] = buf[j];
-#pragma unroll
-                    for (int r = 1; r < R; r++) v[c][r] = cmulf(buf[j + r * nb], w[r]);
-                } else {
-#pragma unroll
-                for (int r = 0; r < R; r++) {
-                    float2 x = buf[j + r * nb];
-                    if (r > 0 && NsC > 1) {
-                        const int t = k * r * tstep;  // < MC
-                        const int q = t / Q, u = t - q * Q;
-                        const float2 w0 = tq[u];
-                        float wx = (q & 1) ? w0.y : w0.x, wy = (q & 1) ? -w0.x : w0.y;
-                        if (q & 2) {
-                            wx = -wx;
-                            wy = -wy;
-                        }
-                        if (SIGN > 0) wy = -wy;
-                        x = cmulf(x, make_float2(wx, wy));
-                    }
-                    v[c][r] = x;
-                }
-                }
-                dft_small<R, SIGN>(v[c]);
-            }
+            if (j < nb) ctq_bfly<MC, NsC, SIGN>(buf, tq, j, v[c]);
         }
         __syncthreads();
 #pragma unroll
@@ -308,9 +318,12 @@ __device__ __forceinline__ void fft_lds_ct_q(float2* __restrict__ buf, const flo
             }
         }
         __syncthreads();
-        fft_lds_ct_q<MC, NsC * R, SIGN>(buf, tq, tid);
+        fft_lds_ct_q<MC, NsC * R, SIGN, NSTOP>(buf, tq, tid);
     }
 }
+
+// The stride before the last pass of the compile-time plan (its NsC): MC / (the last radix).
+constexpr int ct_last_ns(int m, int ns = 1) { return ns * ct_radix(m / ns) >= m ? ns : ct_last_ns(m, ns * ct_radix(m / ns)); }
 
 // Transforms of up to kTwLdsMax points read their twiddles from LDS: the N-entry table is staged
 // next to the data once per workgroup (every Stockham pass otherwise waits on L2 for its R − 1
@@ -1319,33 +1332,38 @@ __global__ __launch_bounds__(kAcqThreads) void acq_huge_rows_pipe_kernel(const f
 {
     extern __shared__ __attribute__((aligned(16))) float2 lds[];
     constexpr int PER = (MC + kAcqThreads - 1) / kAcqThreads;
+    // the 10000-point rows (10 samples per thread) prefetch the code-spectrum row as well; the
+    // 12500-point rows (13) keep it out of the registers the transform needs
+    constexpr bool kPrefB = PER <= 10;
     const int total = P * ny * nz;
     const int tid = threadIdx.x;
     for (int i = tid; i < MC / 4; i += kAcqThreads) lds[MC + i] = twM[i];
-    constexpr int PF = PER;  // prefetched: all of each thread's PER XT samples
-    float2 av[PF];  // the next row's XT samples (the code spectrum rows, 8 per PRN, stay cache-resident)
+    float2 av[PER];                   // the next row's XT samples
+    float2 bp[kPrefB ? PER : 1];      // and its code-spectrum samples (kPrefB)
     auto issue = [&](int r) {
         const int x = r % P, yz = r / P, y = yz % ny, z = yz / ny;
         const float2* a = A + y * a_sy + z * a_sz + static_cast<int64_t>(x) * MC;
 #pragma unroll
-        for (int u = 0; u < PF; u++) av[u] = a[min(tid + u * kAcqThreads, MC - 1)];
+        for (int u = 0; u < PER; u++) av[u] = a[min(tid + u * kAcqThreads, MC - 1)];
+        if constexpr (kPrefB) {
+            const float2* b = B + y * b_sy + z * b_sz + static_cast<int64_t>(x) * MC;
+#pragma unroll
+            for (int u = 0; u < PER; u++) bp[u] = b[min(tid + u * kAcqThreads, MC - 1)];
+        }
     };
     int r = blockIdx.x;
     if (r < total) issue(r);
     for (; r < total; r += gridDim.x) {
         {
             const int x = r % P, yz = r / P, y = yz % ny, z = yz / ny;
-            const float2* a = A + y * a_sy + z * a_sz + static_cast<int64_t>(x) * MC;
             const float2* b = B + y * b_sy + z * b_sz + static_cast<int64_t>(x) * MC;
-            float2 bv[PER], ar[PER - PF + 1];
+            float2 bv[PER];
 #pragma unroll
-            for (int u = PF; u < PER; u++) ar[u - PF] = a[min(tid + u * kAcqThreads, MC - 1)];
-#pragma unroll
-            for (int u = 0; u < PER; u++) bv[u] = b[min(tid + u * kAcqThreads, MC - 1)];
+            for (int u = 0; u < PER; u++) bv[u] = kPrefB ? bp[kPrefB ? u : 0] : b[min(tid + u * kAcqThreads, MC - 1)];
 #pragma unroll
             for (int u = 0; u < PER; u++) {
                 const int i = tid + u * kAcqThreads;
-                if (i < MC) lds[i] = cmulf(u < PF ? av[u] : ar[u - PF], bv[u]);  // XT ⊙ conj(code FFT)
+                if (i < MC) lds[i] = cmulf(av[u], bv[u]);  // XT ⊙ conj(code FFT)
             }
         }
         __syncthreads();
@@ -1359,6 +1377,64 @@ __global__ __launch_bounds__(kAcqThreads) void acq_huge_rows_pipe_kernel(const f
         float2* d = D + y * d_sy + z * d_sz + static_cast<int64_t>(x) * MC;
         for (int i = tid; i < MC; i += kAcqThreads) d[i] = lds[i];
         __syncthreads();  // the row is read out before the next one is written
+    }
+}
+
+// The pipelined search rows when the plan's first and last passes take one butterfly per thread
+// (10000 = 10⁴: 1000 butterflies of radix 10 in every pass): thread j < MC / R1 loads its first-pass
+// inputs XT[j + r·nb] and code[j + r·nb] straight from memory (the next row's prefetched during the
+// transform), forms their products and the first pass's butterfly in registers, and the last pass
+// stores its outputs d[j + r·NsC_last] straight to memory — two LDS passes and two barriers per row
+// fewer than staging the row in LDS, with the same operations in the same order (bit-identical).
+template <int SIGN, int MC>
+__global__ __launch_bounds__(kAcqThreads) void acq_huge_rows_reg_kernel(const float2* __restrict__ A, int64_t a_sy, int64_t a_sz,
+    const float2* __restrict__ B, int64_t b_sy, int64_t b_sz, float2* __restrict__ D, int64_t d_sy, int64_t d_sz, const float2* __restrict__ twM,
+    int P, int ny, int nz)
+{
+    extern __shared__ __attribute__((aligned(16))) float2 lds[];
+    constexpr int R1 = ct_radix(MC), NB1 = MC / R1;
+    constexpr int NL = ct_last_ns(MC), RL = MC / NL;
+    static_assert(NB1 <= kAcqThreads && NL <= kAcqThreads && MC / RL == NL, "one butterfly per thread in the first and last passes");
+    const int total = P * ny * nz;
+    const int tid = threadIdx.x;
+    for (int i = tid; i < MC / 4; i += kAcqThreads) lds[MC + i] = twM[i];
+    const bool first = tid < NB1, last = tid < NL;
+    float2 av[R1], bv[R1];  // the next row's first-pass inputs
+    auto issue = [&](int r) {
+        const int x = r % P, yz = r / P, y = yz % ny, z = yz / ny;
+        const float2* a = A + y * a_sy + z * a_sz + static_cast<int64_t>(x) * MC;
+        const float2* b = B + y * b_sy + z * b_sz + static_cast<int64_t>(x) * MC;
+        const int j = first ? tid : 0;
+#pragma unroll
+        for (int u = 0; u < R1; u++) av[u] = a[j + u * NB1];
+#pragma unroll
+        for (int u = 0; u < R1; u++) bv[u] = b[j + u * NB1];
+    };
+    int r = blockIdx.x;
+    if (r < total) issue(r);
+    for (; r < total; r += gridDim.x) {
+        float2 v[R1];
+#pragma unroll
+        for (int u = 0; u < R1; u++) v[u] = cmulf(av[u], bv[u]);  // XT ⊙ conj(code FFT)
+        if (r + static_cast<int>(gridDim.x) < total) issue(r + gridDim.x);  // in flight during this transform
+        dft_small<R1, SIGN>(v);  // the first pass (NsC = 1: no twiddles)
+        __syncthreads();         // the previous row's last pass has read the LDS
+        if (first) {
+#pragma unroll
+            for (int u = 0; u < R1; u++) lds[tid * R1 + u] = v[u];
+        }
+        __syncthreads();
+        int tid_r = tid;  // an opaque thread id: the passes' index arithmetic is not hoisted into registers
+        asm volatile("" : "+v"(tid_r));
+        fft_lds_ct_q<MC, R1, SIGN, NL>(lds, lds + MC, tid_r);
+        const int x = r % P, yz = r / P, y = yz % ny, z = yz / ny;
+        float2* d = D + y * d_sy + z * d_sz + static_cast<int64_t>(x) * MC;
+        if (last) {
+            float2 w[RL];
+            ctq_bfly<MC, NL, SIGN>(lds, lds + MC, tid_r, w);  // the last pass
+#pragma unroll
+            for (int u = 0; u < RL; u++) d[tid + u * NL] = w[u];
+        }
     }
 }
 
@@ -1581,7 +1657,7 @@ hipError_t launch_acq_search_huge(const float2* XT, const float2* codesT, int pr
         const int total = P * n_bins * n_prns;
         const int blocks = total < n_cu ? total : n_cu;
         if (M == 10000)
-            hipLaunchKernelGGL((acq_huge_rows_pipe_kernel<+1, 10000>), dim3(blocks), dim3(kAcqThreads), lds_q, stream, XT, N, int64_t(0),
+            hipLaunchKernelGGL((acq_huge_rows_reg_kernel<+1, 10000>), dim3(blocks), dim3(kAcqThreads), lds_q, stream, XT, N, int64_t(0),
                 codesT + static_cast<int64_t>(prn_offset) * N, int64_t(0), N, U, N, N * n_bins, twM, P, n_bins, n_prns);
         else
             hipLaunchKernelGGL((acq_huge_rows_pipe_kernel<+1, 12500>), dim3(blocks), dim3(kAcqThreads), lds_q, stream, XT, N, int64_t(0),

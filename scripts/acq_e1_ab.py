@@ -28,7 +28,7 @@ def run_one():
     for _ in range(2):
         acq.run(dev, n_prns=32)
     t0 = time.perf_counter()
-    reps = 10
+    reps = 30
     for _ in range(reps):
         res, _ = acq.run(dev, n_prns=32)
     dt = (time.perf_counter() - t0) / reps
@@ -41,7 +41,8 @@ def main():
         run_one()
         return
     outs = []
-    for spec in sys.argv[1:3]:
+    runs = []
+    for spec in sys.argv[1:3] * 2:  # A, B, A, B: each side's best of two processes
         lib, _, extra = spec.partition(":")
         env = dict(os.environ, GNSSHIP_LIB_PATH=os.path.abspath(lib))
         env.update(kv.split("=", 1) for kv in extra.split(",") if kv)
@@ -50,7 +51,10 @@ def main():
         if not line:
             print(p.stdout[-2000:], p.stderr[-2000:])
             raise SystemExit(f"{lib}: no result")
-        outs.append(json.loads(line[0][7:]))
+        runs.append(json.loads(line[0][7:]))
+    for k in range(2):
+        best = min((runs[k], runs[k + 2]), key=lambda o: o["sweep_ms"])
+        outs.append(best)
     a, b = outs
     same_idx = sum(1 for x, y in zip(a["rows"], b["rows"]) if x[0] == y[0] and x[1] == y[1])
     dstat = max(abs(x[2] - y[2]) / max(abs(x[2]), 1e-30) for x, y in zip(a["rows"], b["rows"]))
