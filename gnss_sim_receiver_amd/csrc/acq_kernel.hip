@@ -41,9 +41,15 @@ __device__ unsigned long long* g_acq_prof = nullptr;
     } while (0)
 #endif
 
+// The FFT arithmetic (complex products, butterflies) contracts to FMAs: the reference's transform
+// (FFTW through gr::fft) is matched to float accuracy, not bit for bit, and a contracted complex
+// product is 2 multiplies + 2 FMAs instead of 4 + 2 (the C3 search is VALU-bound).  The
+// bit-specified steps keep explicit roundings: |y|² as volk_32fc_magnitude_squared_32f, the grid
+// accumulation, the decision's arithmetic.
 __device__ __forceinline__ float2 cmulf(float2 a, float2 b)
 {
-    return make_float2(__fsub_rn(__fmul_rn(a.x, b.x), __fmul_rn(a.y, b.y)), __fadd_rn(__fmul_rn(a.x, b.y), __fmul_rn(a.y, b.x)));
+#pragma clang fp contract(fast)
+    return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
 }
 
 template <int FMT>
@@ -64,6 +70,7 @@ __device__ __forceinline__ float2 load_if(const void* __restrict__ base, int64_t
 template <int R, int SIGN>
 __device__ __forceinline__ void dft_small(float2* v)
 {
+#pragma clang fp contract(fast)
     if constexpr (R == 2) {
         const float2 a = v[0], b = v[1];
         v[0] = make_float2(a.x + b.x, a.y + b.y);
@@ -247,6 +254,22 @@ __device__ __forceinline__ void fft_lds_ct(float2* __restrict__ buf, const float
 // memory its loads sat in every pass's vmcnt queue.  tw[t] for t = q·M/4 + u
 // is tq[u]·(−j)^q — exact, the same float values as the full table (whose entries are rounded from
 // the same double cos/sin up to the quarter-turn symmetry).
+// R consecutive points from a 16-byte-aligned slot (R even): R/2 16-byte stores.  The first pass's
+// outputs (slot j·R, stride R points between lanes) as 8-byte stores put 4 lanes on a bank; as
+// 16-byte stores the 8 lanes of each store cycle fall on distinct banks.
+template <int R>
+__device__ __forceinline__ void store_run(float2* __restrict__ dst, const float2 (&v)[R])
+{
+    if constexpr (R % 2 == 0) {
+        float4* d4 = reinterpret_cast<float4*>(dst);
+#pragma unroll
+        for (int r = 0; r < R; r += 2) d4[r / 2] = make_float4(v[r].x, v[r].y, v[r + 1].x, v[r + 1].y);
+    } else {
+#pragma unroll
+        for (int r = 0; r < R; r++) dst[r] = v[r];
+    }
+}
+
 // One butterfly of fft_lds_ct_q's pass at NsC: thread index j's R inputs buf[j + r·nb], twiddled,
 // through the R-point DFT (the only arithmetic of the pass; its output goes to (j / NsC)·NsC·R +
 // j % NsC + r·NsC).
@@ -313,8 +336,12 @@ __device__ __forceinline__ void fft_lds_ct_q(float2* __restrict__ buf, const flo
             if (j < nb) {
                 const int k = j % NsC;
                 const int base = (j / NsC) * NsC * R + k;
+                if constexpr (NsC == 1) {
+                    store_run<R>(buf + base, v[c]);
+                } else {
 #pragma unroll
-                for (int r = 0; r < R; r++) buf[base + r * NsC] = v[c][r];
+                    for (int r = 0; r < R; r++) buf[base + r * NsC] = v[c][r];
+                }
             }
         }
         __syncthreads();
@@ -564,8 +591,12 @@ __device__ __forceinline__ void wave_fft_row_ct(float2* __restrict__ buf, const 
             if (j < nb) {
                 const int k = j % NsC;
                 const int base = (j / NsC) * NsC * R + k;
+                if constexpr (NsC == 1) {
+                    store_run<R>(buf + base, v[c]);
+                } else {
 #pragma unroll
-                for (int r = 0; r < R; r++) buf[base + r * NsC] = v[c][r];
+                    for (int r = 0; r < R; r++) buf[base + r * NsC] = v[c][r];
+                }
             }
         }
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
@@ -1091,7 +1122,7 @@ __global__ __launch_bounds__(NT) void acq_search_big_kernel(const float2* __rest
         GNSSHIP_ACQ_STAMP(r0 == 0 ? 3 : 6);
     }
     // |y|² stays in registers (g[], the thread's own P points) for the rare second-peak rescan below.
-    MaxIdx m{-1.0f, 0x7fffffff}, m2t{-1.0f, 0x7fffffff};
+    MaxIdx m{-1.0f, 0x7fffffff};
     float s = 0.0f;
     float g[P];
     if (t < M) {
@@ -1116,16 +1147,13 @@ __global__ __launch_bounds__(NT) void acq_search_big_kernel(const float2* __rest
                 }
             }
         }
-        // The thread's top two and its row sum, branch-free (selects, no divergent exec masks).  A
+        // The thread's best and its row sum, branch-free (selects, no divergent exec masks).  A
         // thread's row indices rise with q, so "x beats m" in better() order (strict >, ties to the
         // smaller index) is plain x > m for every earlier m; a point outside the row adds +0 to s.
         auto stat = [&](int q, bool valid) {
             const float x = g[q];
             const int i = t + M * q - rs.row_off;
             const bool gt = valid && x > m.v;
-            const bool gt2 = valid && !gt && x > m2t.v;
-            m2t.v = gt ? m.v : (gt2 ? x : m2t.v);
-            m2t.i = gt ? m.i : (gt2 ? i : m2t.i);
             m.v = gt ? x : m.v;
             m.i = gt ? i : m.i;
             s += valid ? x : 0.0f;
@@ -1152,14 +1180,13 @@ __global__ __launch_bounds__(NT) void acq_search_big_kernel(const float2* __rest
     if (e1 < 0) e1 += rs.win_mod; else if (e2 >= rs.win_mod) e2 -= rs.win_mod;
     // Second peak outside the window (first_vs_second_peak_statistic :566-593): only its value is
     // kept, i.e. max(0, the largest |y|² outside the window).  The window spans 2·spc < M
-    // consecutive indices, so it holds at most one of a thread's indices unless it wraps: the
-    // thread's best outside it is its first or second value, and a thread with both inside rescans.
+    // consecutive indices, so it holds at most one or two of a thread's indices: a thread whose best
+    // lies outside it contributes that best, and only the few threads whose best lies inside rescan
+    // their P values.
     auto in_win = [&](int i) { return (e1 < e2) ? (i >= e1 && i < e2) : (i >= e1 || i < e2); };
     MaxIdx m2{0.0f, 0x7fffffff};
     if (m1t.i != 0x7fffffff && !in_win(m1t.i)) {
         m2 = better(m2, m1t);
-    } else if (m2t.i != 0x7fffffff && !in_win(m2t.i)) {
-        m2 = better(m2, m2t);
     } else if (m1t.i != 0x7fffffff) {
 #pragma unroll
         for (int q = 0; q < P; q++) {  // this thread's indices (natural t + M·q, row-shifted)
@@ -1419,10 +1446,7 @@ __global__ __launch_bounds__(kAcqThreads) void acq_huge_rows_reg_kernel(const fl
         if (r + static_cast<int>(gridDim.x) < total) issue(r + gridDim.x);  // in flight during this transform
         dft_small<R1, SIGN>(v);  // the first pass (NsC = 1: no twiddles)
         __syncthreads();         // the previous row's last pass has read the LDS
-        if (first) {
-#pragma unroll
-            for (int u = 0; u < R1; u++) lds[tid * R1 + u] = v[u];
-        }
+        if (first) store_run<R1>(lds + tid * R1, v);
         __syncthreads();
         int tid_r = tid;  // an opaque thread id: the passes' index arithmetic is not hoisted into registers
         asm volatile("" : "+v"(tid_r));
