@@ -570,15 +570,21 @@ __device__ __forceinline__ void wave_fft_row_ct(float2* __restrict__ buf, const 
             const int j = lane + 64 * c;
             if (j < nb) {
                 const int k = j % NsC;
+                if constexpr (NsC > 1) {
+                    // W^{k·r·tstep} = (W^{k·tstep})^r: one table read (the pass table's r = 1 row), the
+                    // other powers as a balanced product tree (≤ 4 products deep) — the LDS pipe, which
+                    // the CU's waves share, carried a third of the row traffic as twiddle reads
+                    float2 w[R];
+                    w[1] = tw[off + k];
+                    if (SIGN > 0) w[1].y = -w[1].y;
 #pragma unroll
-                for (int r = 0; r < R; r++) {
-                    float2 x = buf[j + r * nb];
-                    if (r > 0 && NsC > 1) {
-                        float2 w = tw[off + (r - 1) * NsC + k];
-                        if (SIGN > 0) w.y = -w.y;
-                        x = cmulf(x, w);
-                    }
-                    v[c][r] = x;
+                    for (int r = 2; r < R; r++) w[r] = cmulf(w[r / 2], w[r - r / 2]);
+                    v[c][0] = buf[j];
+#pragma unroll
+                    for (int r = 1; r < R; r++) v[c][r] = cmulf(buf[j + r * nb], w[r]);
+                } else {
+#pragma unroll
+                    for (int r = 0; r < R; r++) v[c][r] = buf[j + r * nb];
                 }
                 dft_small<R, SIGN>(v[c]);
             }
@@ -1184,17 +1190,30 @@ __global__ __launch_bounds__(NT) void acq_search_big_kernel(const float2* __rest
     // lies outside it contributes that best, and only the few threads whose best lies inside rescan
     // their P values.
     auto in_win = [&](int i) { return (e1 < e2) ? (i >= e1 && i < e2) : (i >= e1 || i < e2); };
-    MaxIdx m2{0.0f, 0x7fffffff};
+    float v2 = 0.0f;  // only the value is kept: max(0, …)
     if (m1t.i != 0x7fffffff && !in_win(m1t.i)) {
-        m2 = better(m2, m1t);
+        v2 = m1t.v;
     } else if (m1t.i != 0x7fffffff) {
+        // this thread's indices (natural t + M·q, row-shifted) outside the window; the window's
+        // form (one interval, or two at the wrap) is uniform over the block
+        if (e1 < e2) {
+            const unsigned w = static_cast<unsigned>(e2 - e1);
 #pragma unroll
-        for (int q = 0; q < P; q++) {  // this thread's indices (natural t + M·q, row-shifted)
-            const int i = t + M * q - rs.row_off;
-            if (i >= 0 && i < rs.row_len && !in_win(i)) m2 = better(m2, MaxIdx{g[q], i});
+            for (int q = 0; q < P; q++) {
+                const int i = t + M * q - rs.row_off;
+                const bool out = i >= 0 && i < rs.row_len && static_cast<unsigned>(i - e1) >= w;
+                v2 = out ? fmaxf(v2, g[q]) : v2;
+            }
+        } else {
+#pragma unroll
+            for (int q = 0; q < P; q++) {
+                const int i = t + M * q - rs.row_off;
+                const bool out = i >= 0 && i < rs.row_len && i < e1 && i >= e2;
+                v2 = out ? fmaxf(v2, g[q]) : v2;
+            }
         }
     }
-    const float second = block_max<NT / 64>(m2.v, red_s);  // values ≥ 0: max(0, the largest outside the window)
+    const float second = block_max<NT / 64>(v2, red_s);  // values ≥ 0: max(0, the largest outside the window)
     GNSSHIP_ACQ_STAMP(9);
     if (t == 0) {
         RowStat r;
