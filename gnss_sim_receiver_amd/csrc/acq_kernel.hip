@@ -780,10 +780,17 @@ __global__ __launch_bounds__(kBigColThreads) void acq_fft_big_cols_kernel(const 
     }
     dft_reg_inplace<P, -1>(v, tw, N);  // X[kq] in v[reg_slot<P>(kq)]
     float2* out = rowsT + static_cast<int64_t>(b) * N;
+    // W_N^{t·kq} = (W_N^t)^kq: one coalesced table read and a balanced product tree (≤ 5 products
+    // deep) instead of P − 1 reads gathered at stride kq from the N-entry table
+    float2 w[P];
+    w[0] = make_float2(1.0f, 0.0f);
+    if constexpr (P > 1) w[1] = tw[t];
+#pragma unroll
+    for (int kq = 2; kq < P; kq++) w[kq] = cmulf(w[kq / 2], w[kq - kq / 2]);
 #pragma unroll
     for (int kq = 0; kq < P; kq++) {
         const float2 xk = v[reg_slot<P>(kq)];
-        out[kq * M + t] = kq ? cmulf(xk, tw[t * kq]) : xk;  // W_N^{t·kq}, t·kq < N
+        out[kq * M + t] = kq ? cmulf(xk, w[kq]) : xk;
     }
 }
 

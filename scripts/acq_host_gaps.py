@@ -1,7 +1,8 @@
 """Host-side gaps of repeated acquisition sweeps from a rocprofv3 --hip-trace --kernel-trace run:
 per gnsship_acq_run call, hipGraphLaunch entry -> first kernel start, last kernel end ->
 hipStreamSynchronize return, and the call's whole span.
-    python scripts/acq_host_gaps.py <dir with run_hip_api_trace.csv and run_kernel_trace.csv>"""
+    python scripts/acq_host_gaps.py <dir with run_hip_api_trace.csv and run_kernel_trace.csv> [kernel name part]
+(with a name part, only the calls whose kernels include one so named)"""
 import csv
 import glob
 import os
@@ -19,7 +20,7 @@ rows = []
 for i, t in enumerate(launches):
     nxt = launches[i + 1] if i + 1 < len(launches) else 1 << 62
     ks = [k for k in ker if t <= k[0] < nxt]
-    if not ks:
+    if not ks or (len(sys.argv) > 2 and not any(sys.argv[2] in k[2] for k in ks)):
         continue
     kend = max(k[1] for k in ks)
     s = [x for x in syncs if x >= kend and x < nxt]

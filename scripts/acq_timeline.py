@@ -1,13 +1,15 @@
-"""Timeline of the last E1 all-sky sweep in a rocprofv3 kernel trace (run_kernel_trace.csv): each
-dispatch's start and end relative to the sweep's first kernel, and the sweep's span.
-    python scripts/acq_timeline.py gpurun_out/.../run_kernel_trace.csv"""
+"""Timeline of the last acquisition sweep in a rocprofv3 kernel trace (run_kernel_trace.csv): each
+dispatch's start and end relative to the sweep's first kernel, and the sweep's span.  The sweep starts
+at the last launch whose name contains FIRST (default: the E1 huge layout's forward column kernel).
+    python scripts/acq_timeline.py gpurun_out/.../run_kernel_trace.csv [FIRST]"""
 import csv
 import sys
 
 rows = [r for r in csv.DictReader(open(sys.argv[1])) if "rocclr" not in r["Kernel_Name"]]
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 # the last sweep: from the last forward column launch of the huge layout to the decision after it
-idx = [i for i, r in enumerate(rows) if "acq_huge_cols_fwd" in r["Kernel_Name"]]
+first_pat = sys.argv[2] if len(sys.argv) > 2 else "acq_huge_cols_fwd"
+idx = [i for i, r in enumerate(rows) if first_pat in r["Kernel_Name"]]
 if not idx:
     raise SystemExit("no huge sweep in the trace")
 first = idx[-1]
