@@ -1439,10 +1439,10 @@ __global__ __launch_bounds__(kAcqThreads) void acq_huge_rows_pipe_kernel(const f
 // transform), forms their products and the first pass's butterfly in registers, and the last pass
 // stores its outputs d[j + r·NsC_last] straight to memory — two LDS passes and two barriers per row
 // fewer than staging the row in LDS, with the same operations in the same order (bit-identical).
-template <int SIGN, int MC>
+template <int SIGN, int MC, bool HAS_B = true>
 __global__ __launch_bounds__(kAcqThreads) void acq_huge_rows_reg_kernel(const float2* __restrict__ A, int64_t a_sy, int64_t a_sz,
     const float2* __restrict__ B, int64_t b_sy, int64_t b_sz, float2* __restrict__ D, int64_t d_sy, int64_t d_sz, const float2* __restrict__ twM,
-    int P, int ny, int nz)
+    int P, int ny, int nz, int conj_out = 0)
 {
     extern __shared__ __attribute__((aligned(16))) float2 lds[];
     constexpr int R1 = ct_radix(MC), NB1 = MC / R1;
@@ -1456,19 +1456,21 @@ __global__ __launch_bounds__(kAcqThreads) void acq_huge_rows_reg_kernel(const fl
     auto issue = [&](int r) {
         const int x = r % P, yz = r / P, y = yz % ny, z = yz / ny;
         const float2* a = A + y * a_sy + z * a_sz + static_cast<int64_t>(x) * MC;
-        const float2* b = B + y * b_sy + z * b_sz + static_cast<int64_t>(x) * MC;
         const int j = first ? tid : 0;
 #pragma unroll
         for (int u = 0; u < R1; u++) av[u] = a[j + u * NB1];
+        if constexpr (HAS_B) {
+            const float2* b = B + y * b_sy + z * b_sz + static_cast<int64_t>(x) * MC;
 #pragma unroll
-        for (int u = 0; u < R1; u++) bv[u] = b[j + u * NB1];
+            for (int u = 0; u < R1; u++) bv[u] = b[j + u * NB1];
+        }
     };
     int r = blockIdx.x;
     if (r < total) issue(r);
     for (; r < total; r += gridDim.x) {
         float2 v[R1];
 #pragma unroll
-        for (int u = 0; u < R1; u++) v[u] = cmulf(av[u], bv[u]);  // XT ⊙ conj(code FFT)
+        for (int u = 0; u < R1; u++) v[u] = HAS_B ? cmulf(av[u], bv[u]) : av[u];  // XT ⊙ conj(code FFT) (search rows)
         if (r + static_cast<int>(gridDim.x) < total) issue(r + gridDim.x);  // in flight during this transform
         dft_small<R1, SIGN>(v);  // the first pass (NsC = 1: no twiddles)
         __syncthreads();         // the previous row's last pass has read the LDS
@@ -1483,7 +1485,10 @@ __global__ __launch_bounds__(kAcqThreads) void acq_huge_rows_reg_kernel(const fl
             float2 w[RL];
             ctq_bfly<MC, NL, SIGN>(lds, lds + MC, tid_r, w);  // the last pass
 #pragma unroll
-            for (int u = 0; u < RL; u++) d[tid + u * NL] = w[u];
+            for (int u = 0; u < RL; u++) {
+                if (conj_out) w[u].y = -w[u].y;
+                d[tid + u * NL] = w[u];
+            }
         }
     }
 }
@@ -1683,7 +1688,15 @@ hipError_t launch_acq_fft_huge(const void* sig, int fmt, const float2* mult, int
         hipLaunchKernelGGL((acq_huge_rows_kernel<-1, mc>), dim3(P, n_rows, 1), dim3(kAcqThreads), lds_q, stream, scratch, N, int64_t(0), \
             static_cast<const float2*>(nullptr), int64_t(0), int64_t(0), rowsT, N, int64_t(0), row_plan, twM, conj_out);                  \
     else
-    GNSSHIP_CT_ROWS(10000) GNSSHIP_CT_ROWS(12500)
+    if (M == 10000) {  // persistent, first and last passes in registers (as the search rows)
+        int n_cu = 256;
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) n_cu = 256;
+        const int total = P * n_rows;
+        hipLaunchKernelGGL((acq_huge_rows_reg_kernel<-1, 10000, false>), dim3(total < n_cu ? total : n_cu), dim3(kAcqThreads), lds_q, stream, scratch, N,
+            int64_t(0), static_cast<const float2*>(nullptr), int64_t(0), int64_t(0), rowsT, N, int64_t(0), twM, P, n_rows, 1, conj_out);
+    } else
+    GNSSHIP_CT_ROWS(12500)
 #undef GNSSHIP_CT_ROWS
         hipLaunchKernelGGL((acq_huge_rows_kernel<-1>), dim3(P, n_rows, 1), dim3(kAcqThreads), lds, stream, scratch, N, int64_t(0),
             static_cast<const float2*>(nullptr), int64_t(0), int64_t(0), rowsT, N, int64_t(0), row_plan, twM, conj_out);
