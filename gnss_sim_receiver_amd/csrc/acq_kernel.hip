@@ -1535,7 +1535,11 @@ __global__ __launch_bounds__(kHugeColThreads) void acq_huge_cols_inv_kernel(cons
 // first_vs_second_peak_statistic :566-593) takes the maximum of every tile that misses the window
 // from its tile statistic and rescans from the grid only the few tiles the window meets (the window
 // is 2·spc consecutive indices: one or two column runs), instead of the whole row.
-constexpr int kHugeFlagMax = 64;  // tiles met by the window that are rescanned together (more: full-row fallback)
+constexpr int kHugeFlagMax = 64;
+// The finalize's work is the tile statistics of one cell (40-49 tiles) and the recomputation of the one
+// or two tiles the window meets (one column per thread): 256 threads, four workgroups per CU (1024
+// threads left 768 idle and held a CU per cell).
+constexpr int kHugeFinThreads = 256;  // tiles met by the window that are rescanned together (more: full-row fallback)
 
 __device__ __forceinline__ bool interval_meets(int a0, int a1, int b0, int b1) { return a0 < b1 && b0 < a1; }
 
@@ -1547,7 +1551,7 @@ __device__ __forceinline__ float huge_tile_max_outside(const float2* __restrict_
     int e1, int e2)
 {
     float v2 = 0.0f;
-    for (int c = threadIdx.x; c < kHugeColThreads; c += kAcqThreads) {
+    for (int c = threadIdx.x; c < kHugeColThreads; c += kHugeFinThreads) {
         const int mm = lo + c;
         if (mm >= M) continue;
         float2 v[P];
@@ -1564,12 +1568,12 @@ __device__ __forceinline__ float huge_tile_max_outside(const float2* __restrict_
     return v2;
 }
 
-__global__ __launch_bounds__(kAcqThreads) void acq_huge_finalize_kernel(const float* __restrict__ grid, const TileStat* __restrict__ tiles,
+__global__ __launch_bounds__(kHugeFinThreads) void acq_huge_finalize_kernel(const float* __restrict__ grid, const TileStat* __restrict__ tiles,
     int n_tiles, int n_bins, int prn_offset, RowSpec rs, int M, int P, RowStat* __restrict__ rowstat, const float2* __restrict__ U,
     const float2* __restrict__ twN)
 {
-    __shared__ MaxIdx red_m[kAcqThreads / 64];
-    __shared__ float red_s[kAcqThreads / 64];
+    __shared__ MaxIdx red_m[kHugeFinThreads / 64];
+    __shared__ float red_s[kHugeFinThreads / 64];
     __shared__ int flag_list[kHugeFlagMax];
     __shared__ int n_flag;
     const int64_t cell = static_cast<int64_t>(blockIdx.y) * n_bins + blockIdx.x;
@@ -1577,11 +1581,11 @@ __global__ __launch_bounds__(kAcqThreads) void acq_huge_finalize_kernel(const fl
     if (threadIdx.x == 0) n_flag = 0;
     MaxIdx m{-1.0f, 0x7fffffff};
     float s = 0.0f;
-    for (int i = threadIdx.x; i < n_tiles; i += kAcqThreads) {
+    for (int i = threadIdx.x; i < n_tiles; i += kHugeFinThreads) {
         m = better(m, MaxIdx{ts[i].max, ts[i].argmax});
         s += ts[i].sum;
     }
-    block_argmax_sum<kAcqThreads / 64>(m, s, red_m, red_s);  // its barriers also publish n_flag = 0
+    block_argmax_sum<kHugeFinThreads / 64>(m, s, red_m, red_s);  // its barriers also publish n_flag = 0
     const MaxIdx best = m;
     const float sum = s;
     int e1 = best.i - rs.spc, e2 = best.i + rs.spc;
@@ -1590,7 +1594,7 @@ __global__ __launch_bounds__(kAcqThreads) void acq_huge_finalize_kernel(const fl
     const int w0a = e1 < e2 ? e1 : e1, w0b = e1 < e2 ? e2 : rs.win_mod;
     const int w1a = 0, w1b = e1 < e2 ? 0 : e2;
     float v2 = 0.0f;  // max(0, …): the reference's second peak starts from 0
-    for (int i = threadIdx.x; i < n_tiles; i += kAcqThreads) {
+    for (int i = threadIdx.x; i < n_tiles; i += kHugeFinThreads) {
         const int lo = i * kHugeColThreads, hi = min(M, lo + kHugeColThreads);
         bool meets = false;
         for (int q = 0; q < P; q++) {
@@ -1619,7 +1623,7 @@ __global__ __launch_bounds__(kAcqThreads) void acq_huge_finalize_kernel(const fl
 #undef GNSSHIP_P_CASE
             v2 = fmaxf(v2, t);
         }
-        const float second = block_max<kAcqThreads / 64>(v2, red_s);
+        const float second = block_max<kHugeFinThreads / 64>(v2, red_s);
         if (threadIdx.x == 0) rowstat[(static_cast<int64_t>(prn_offset) + blockIdx.y) * n_bins + blockIdx.x] = RowStat{best.v, best.i, sum, second};
         return;
     }
@@ -1627,17 +1631,17 @@ __global__ __launch_bounds__(kAcqThreads) void acq_huge_finalize_kernel(const fl
     if (nf <= kHugeFlagMax) {
         for (int f = 0; f < nf; f++) {
             const int lo = flag_list[f] * kHugeColThreads;
-            for (int j = threadIdx.x; j < kHugeColThreads * P; j += kAcqThreads) {
+            for (int j = threadIdx.x; j < kHugeColThreads * P; j += kHugeFinThreads) {
                 const int mm = lo + j % kHugeColThreads, q = j / kHugeColThreads;
                 const int n = mm + M * q - rs.row_off;
                 if (mm < M && n >= 0 && n < rs.row_len && !in_win(n)) v2 = fmaxf(v2, g[n]);
             }
         }
     } else {  // more tiles met than listed: scan the whole row
-        for (int i = threadIdx.x; i < rs.row_len; i += kAcqThreads)
+        for (int i = threadIdx.x; i < rs.row_len; i += kHugeFinThreads)
             if (!in_win(i)) v2 = fmaxf(v2, g[i]);
     }
-    const float second = block_max<kAcqThreads / 64>(v2, red_s);
+    const float second = block_max<kHugeFinThreads / 64>(v2, red_s);
     if (threadIdx.x == 0) rowstat[(static_cast<int64_t>(prn_offset) + blockIdx.y) * n_bins + blockIdx.x] = RowStat{best.v, best.i, sum, second};
 }
 
@@ -1745,7 +1749,7 @@ hipError_t launch_acq_search_huge(const float2* XT, const float2* codesT, int pr
 #undef GNSSHIP_P_CASE
     e = hipGetLastError();
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(acq_huge_finalize_kernel, dim3(n_bins, n_prns), dim3(kAcqThreads), 0, stream, grid, tiles, n_tiles, n_bins, prn_offset, rs,
+    hipLaunchKernelGGL(acq_huge_finalize_kernel, dim3(n_bins, n_prns), dim3(kHugeFinThreads), 0, stream, grid, tiles, n_tiles, n_bins, prn_offset, rs,
         M, P, rowstat, U, twN);
     return hipGetLastError();
 }
