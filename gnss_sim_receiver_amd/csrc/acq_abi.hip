@@ -329,6 +329,7 @@ extern "C" int gnsship_acq_create(gnsship_ctx* ctx, const gnsship_acq_conf* conf
     hipError_t e = hipMalloc(&a->tw, sizeof(float2) * N);
     if (e == hipSuccess) e = hipMemcpy(a->tw, tw.data(), sizeof(float2) * N, hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMalloc(&a->codes_fft, sizeof(float2) * static_cast<size_t>(N) * conf->max_prns);
+    if (e == hipSuccess && huge && plan.n == 10000) e = ensure_lane_perm10();
     if (e == hipSuccess && huge) {
         const int M = plan.n;
         std::vector<float2> twm(M);

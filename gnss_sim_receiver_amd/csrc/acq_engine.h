@@ -61,7 +61,8 @@ struct TileStat {  // one column tile of one |IFFT|² row
     int32_t pad;
 };
 bool huge_p_supported(int P);
-bool huge_ct_rows(int M);  // M-point rows with a compile-time plan and the pipelined search rows
+bool huge_ct_rows(int M);
+hipError_t ensure_lane_perm10();  // the 10000-point rows' butterfly table on the current device (outside any capture)  // M-point rows with a compile-time plan and the pipelined search rows
 constexpr int huge_tiles(int M) { return (M + 255) / 256; }
 // rowsT[b] = transposed FFT(sig ⊙ mult[b]) for b < n_rows; scratch: n_rows × N complex.
 hipError_t launch_acq_fft_huge(const void* sig, int fmt, const float2* mult, int n_rows, int P, const FftPlan& row_plan, const float2* twN,

@@ -16,6 +16,8 @@
 //                         maxima + opposite-row input power → gnsship_acq_result.
 // FFT: Stockham autosort, mixed radix {2,3,4,5,8}, natural order in and out, twiddles from an
 // N-entry table rounded from double.  Unnormalised like FFTW (forward e^{-j}, backward e^{+j}).
+#include <vector>
+
 #include "acq_engine.h"
 
 namespace gnsship {
@@ -315,8 +317,10 @@ __device__ __forceinline__ void ctq_bfly(const float2* __restrict__ buf, const f
 }
 
 // The passes from NsC up to (not including) the one at NSTOP (NSTOP = MC: every remaining pass).
+// jp10: this thread's butterfly in the NsC = 10 pass when that pass has one butterfly per thread
+// (kLanePerm10 below; −1: none), else the thread index.
 template <int MC, int NsC, int SIGN, int NSTOP = MC>
-__device__ __forceinline__ void fft_lds_ct_q(float2* __restrict__ buf, const float2* __restrict__ tq, int tid)
+__device__ __forceinline__ void fft_lds_ct_q(float2* __restrict__ buf, const float2* __restrict__ tq, int tid, int jp10 = -2)
 {
     static_assert(MC % 4 == 0, "quarter twiddle table");
     if constexpr (NsC < NSTOP) {
@@ -326,14 +330,14 @@ __device__ __forceinline__ void fft_lds_ct_q(float2* __restrict__ buf, const flo
         float2 v[MAXB][R];
 #pragma unroll
         for (int c = 0; c < MAXB; c++) {
-            const int j = tid + c * kAcqThreads;
-            if (j < nb) ctq_bfly<MC, NsC, SIGN>(buf, tq, j, v[c]);
+            const int j = (NsC == 10 && MAXB == 1 && jp10 != -2) ? jp10 : tid + c * kAcqThreads;
+            if (j >= 0 && j < nb) ctq_bfly<MC, NsC, SIGN>(buf, tq, j, v[c]);
         }
         __syncthreads();
 #pragma unroll
         for (int c = 0; c < MAXB; c++) {
-            const int j = tid + c * kAcqThreads;
-            if (j < nb) {
+            const int j = (NsC == 10 && MAXB == 1 && jp10 != -2) ? jp10 : tid + c * kAcqThreads;
+            if (j >= 0 && j < nb) {
                 const int k = j % NsC;
                 const int base = (j / NsC) * NsC * R + k;
                 if constexpr (NsC == 1) {
@@ -345,7 +349,7 @@ __device__ __forceinline__ void fft_lds_ct_q(float2* __restrict__ buf, const flo
             }
         }
         __syncthreads();
-        fft_lds_ct_q<MC, NsC * R, SIGN, NSTOP>(buf, tq, tid);
+        fft_lds_ct_q<MC, NsC * R, SIGN, NSTOP>(buf, tq, tid, jp10);
     }
 }
 
@@ -1433,6 +1437,52 @@ __global__ __launch_bounds__(kAcqThreads) void acq_huge_rows_pipe_kernel(const f
     }
 }
 
+// kLanePerm10: the butterflies of the 10000-point rows' NsC = 10 pass (radix 10, 1000 butterflies
+// j = 10a + b) dealt to the 1024 threads so that each 16-lane group reads buf[j + 1000r] and writes
+// buf[100a + b + 10r] on 16 distinct bank pairs — j mod 32 and (4a + b) mod 32 distinct in the group
+// (thread order made two lanes of a group write one bank pair: 58 % LDS conflict cycles in the rows).
+// Greedy in increasing j: 62 full groups and one of 8; −1 marks an idle thread.  Set once per device.
+__device__ int16_t g_lane_perm10[kAcqThreads];
+
+static std::vector<int16_t> lane_perm10_table()
+{
+    std::vector<int16_t> perm(kAcqThreads, -1);
+    std::vector<int> rest(1000);
+    for (int j = 0; j < 1000; j++) rest[j] = j;
+    int slot = 0;
+    while (!rest.empty()) {
+        std::vector<int> left;
+        unsigned long long used_r = 0, used_w = 0;
+        int n = 0;
+        for (int j : rest) {
+            const int kr = j % 32, kw = (4 * (j / 10) + j % 10) % 32;
+            if (n < 16 && !((used_r >> kr) & 1) && !((used_w >> kw) & 1)) {
+                used_r |= 1ull << kr;
+                used_w |= 1ull << kw;
+                perm[slot + n++] = static_cast<int16_t>(j);
+            } else {
+                left.push_back(j);
+            }
+        }
+        slot += 16;
+        rest.swap(left);
+    }
+    return perm;
+}
+
+hipError_t ensure_lane_perm10()
+{
+    static bool done[64] = {};
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    if (dev < 64 && done[dev]) return hipSuccess;
+    static const std::vector<int16_t> perm = lane_perm10_table();
+    e = hipMemcpyToSymbol(HIP_SYMBOL(g_lane_perm10), perm.data(), sizeof(int16_t) * kAcqThreads);
+    if (e == hipSuccess && dev < 64) done[dev] = true;
+    return e;
+}
+
 // The pipelined search rows when the plan's first and last passes take one butterfly per thread
 // (10000 = 10⁴: 1000 butterflies of radix 10 in every pass): thread j < MC / R1 loads its first-pass
 // inputs XT[j + r·nb] and code[j + r·nb] straight from memory (the next row's prefetched during the
@@ -1452,6 +1502,9 @@ __global__ __launch_bounds__(kAcqThreads) void acq_huge_rows_reg_kernel(const fl
     const int tid = threadIdx.x;
     for (int i = tid; i < MC / 4; i += kAcqThreads) lds[MC + i] = twM[i];
     const bool first = tid < NB1, last = tid < NL;
+    // the stride-10 pass's butterfly for this thread (kLanePerm10): every 16-lane group's reads and
+    // writes on distinct bank pairs
+    const int jp10 = (MC == 10000) ? static_cast<int>(g_lane_perm10[tid]) : -2;
     float2 av[R1], bv[R1];  // the next row's first-pass inputs
     auto issue = [&](int r) {
         const int x = r % P, yz = r / P, y = yz % ny, z = yz / ny;
@@ -1478,7 +1531,7 @@ __global__ __launch_bounds__(kAcqThreads) void acq_huge_rows_reg_kernel(const fl
         __syncthreads();
         int tid_r = tid;  // an opaque thread id: the passes' index arithmetic is not hoisted into registers
         asm volatile("" : "+v"(tid_r));
-        fft_lds_ct_q<MC, R1, SIGN, NL>(lds, lds + MC, tid_r);
+        fft_lds_ct_q<MC, R1, SIGN, NL>(lds, lds + MC, tid_r, jp10);
         const int x = r % P, yz = r / P, y = yz % ny, z = yz / ny;
         float2* d = D + y * d_sy + z * d_sz + static_cast<int64_t>(x) * MC;
         if (last) {
@@ -1693,6 +1746,7 @@ hipError_t launch_acq_fft_huge(const void* sig, int fmt, const float2* mult, int
             static_cast<const float2*>(nullptr), int64_t(0), int64_t(0), rowsT, N, int64_t(0), row_plan, twM, conj_out);                  \
     else
     if (M == 10000) {  // persistent, first and last passes in registers (as the search rows)
+        if (hipError_t pe = ensure_lane_perm10(); pe != hipSuccess) return pe;
         int n_cu = 256;
         int dev = 0;
         if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) n_cu = 256;
@@ -1723,6 +1777,7 @@ hipError_t launch_acq_search_huge(const float2* XT, const float2* codesT, int pr
         if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) n_cu = 256;
         const int total = P * n_bins * n_prns;
         const int blocks = total < n_cu ? total : n_cu;
+        if (M == 10000 && ensure_lane_perm10() != hipSuccess) return hipErrorInvalidValue;
         if (M == 10000)
             hipLaunchKernelGGL((acq_huge_rows_reg_kernel<+1, 10000>), dim3(blocks), dim3(kAcqThreads), lds_q, stream, XT, N, int64_t(0),
                 codesT + static_cast<int64_t>(prn_offset) * N, int64_t(0), N, U, N, N * n_bins, twM, P, n_bins, n_prns);
