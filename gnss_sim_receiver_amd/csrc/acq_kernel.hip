@@ -1300,6 +1300,18 @@ __global__ __launch_bounds__(64) void acq_decide_kernel(const RowStat* __restric
 constexpr int kHugeColThreads = 256;
 #define GNSSHIP_HUGE_P_LIST(X) X(4) X(5) X(8) X(10) X(16) X(20) X(25) X(32)
 
+// W_N^{m·kq} for kq < P from the column-layout table twC[kq·M + m]: the kq = 1 entry read (coalesced)
+// and the other powers as a balanced product tree (≤ 5 products deep) — the other P − 2 reads were
+// as many bytes of L2 traffic per column as the column's own data.
+template <int P>
+__device__ __forceinline__ void col_twiddles(const float2* __restrict__ twC, int M, int m, float2 (&w)[P])
+{
+    w[0] = make_float2(1.0f, 0.0f);
+    if constexpr (P > 1) w[1] = twC[M + m];
+#pragma unroll
+    for (int kq = 2; kq < P; kq++) w[kq] = cmulf(w[kq / 2], w[kq - kq / 2]);
+}
+
 template <int FMT, int P>
 __global__ __launch_bounds__(kHugeColThreads) void acq_huge_cols_fwd_kernel(const void* __restrict__ sig, const float2* __restrict__ mult,
     int M, const float2* __restrict__ twN, float2* __restrict__ T, int n_valid)
@@ -1326,8 +1338,10 @@ __global__ __launch_bounds__(kHugeColThreads) void acq_huge_cols_fwd_kernel(cons
     }
     dft_reg<P, 1, -1>(v, twN, N);
     float2* out = T + static_cast<int64_t>(b) * N + m;
+    float2 wt[P];
+    col_twiddles<P>(twN, M, m, wt);
 #pragma unroll
-    for (int kq = 0; kq < P; kq++) out[kq * M] = kq ? cmulf(v[kq], twN[kq * M + m]) : v[kq];  // W_N^{m·kq} (column layout, coalesced)
+    for (int kq = 0; kq < P; kq++) out[kq * M] = kq ? cmulf(v[kq], wt[kq]) : v[kq];  // W_N^{m·kq}
 }
 
 // One LDS-resident M-point transform per block: row blockIdx.x of cell (blockIdx.y, blockIdx.z).
@@ -1364,11 +1378,13 @@ template <int P>
 __device__ __forceinline__ void huge_col_inv(const float2* __restrict__ u, int m, int M, const float2* __restrict__ twN, float2 (&v)[P])
 {
     const int N = P * M;
+    float2 wt[P];
+    col_twiddles<P>(twN, M, m, wt);
 #pragma unroll
     for (int kq = 0; kq < P; kq++) {
         float2 x = u[kq * M];
         if (kq) {
-            float2 w = twN[kq * M + m];  // W_N^{−m·kq}: the column-layout table twC[kq·M + m] = W_N^{m·kq} (coalesced)
+            float2 w = wt[kq];  // W_N^{−m·kq}
             w.y = -w.y;
             x = cmulf(x, w);
         }
