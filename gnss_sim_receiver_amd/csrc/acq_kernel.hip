@@ -462,16 +462,6 @@ constexpr int first_radix(int m)
     return (m % 8 == 0) ? 8 : (m % 5 == 0) ? 5 : (m % 4 == 0) ? 4 : (m % 3 == 0) ? 3 : 2;
 }
 
-// Column twiddles W_N^{t·kq} of the four-step with the row length known at compile time, from two
-// small LDS tables instead of the N-entry table in HBM: t = B·a + b (B | M) gives
-// W_N^{t·kq} = W_N^{B·a·kq} · W_N^{b·kq}, tables tw[B·e] (e = a·kq < (M/B)·P) and tw[e] (e = b·kq < B·P).
-constexpr int col_split(int m)
-{
-    int b = 1;
-    while (b * b < m || m % b) b++;
-    return b;
-}
-
 // Wave-level row transforms: each wave owns whole rows of the four-step and runs every Stockham
 // pass of its row in place, with no workgroup barrier — a pass loads all of the lane's butterflies
 // into registers before any store, and a wave's LDS operations complete in program order (the fence
@@ -1076,16 +1066,6 @@ __global__ __launch_bounds__(NT) void acq_search_big_kernel(const float2* __rest
     float2* rtw = lds + kRoundRows * M;  // row twiddles exp(−2πi m/M) = tw[m·P], m < M
     if constexpr (MC > 0) fill_row_pass_tw<MC, 1>(rtw, tw, P, t, NT);  // per-pass tables (conflict-free reads)
     else for (int i = t; i < M; i += NT) rtw[i] = tw[i * P];
-    // column twiddles W_N^{t·kq} = tw[B·a·kq]·tw[b·kq] (t = B·a + b), tables laid out [kq][a] and
-    // [kq][b] so that the lanes of a wave (consecutive t) read consecutive or equal entries
-    constexpr int kB = MC > 0 ? col_split(MC) : 1;
-    constexpr int kA = MC > 0 ? MC / kB : 1;
-    float2* ct_lo = rtw + M;       // ct_lo[kq·B + b] = tw[b·kq]     (MC > 0)
-    float2* ct_hi = ct_lo + kB * P;  // ct_hi[kq·A + a] = tw[B·a·kq]  (MC > 0)
-    if constexpr (MC > 0) {
-        for (int i = t; i < kB * P; i += NT) ct_lo[i] = tw[(i % kB) * (i / kB)];
-        for (int i = t; i < kA * P; i += NT) ct_hi[i] = tw[kB * (i % kA) * (i / kA)];
-    }
     const int lane = t & 63, wave = t >> 6;
     // the short round first: the v[kq] of finished rounds stay live in registers through the later
     // rounds' row passes, so the fewer of them the better (P = 25: 9 rows, then 16)
@@ -1120,13 +1100,22 @@ __global__ __launch_bounds__(NT) void acq_search_big_kernel(const float2* __rest
         __syncthreads();
         GNSSHIP_ACQ_STAMP(r0 == 0 ? 2 : 5);
         if (t < M) {
+            // MC > 0: W_N^{t·kq} as powers of W_N^t (one table read, a product tree ≤ 5 deep) — the
+            // two-table form read 2 LDS entries per point
+            float2 wp[P];
+            if constexpr (MC > 0) {
+                wp[0] = make_float2(1.0f, 0.0f);
+                wp[1] = tw[t];
+#pragma unroll
+                for (int q = 2; q < P; q++) wp[q] = cmulf(wp[q / 2], wp[q - q / 2]);
+            }
 #pragma unroll
             for (int kk = 0; kk < kRoundRows; kk++) {
                 const int kq = (kPrefetch && rr == 1) ? (kk < kFirst ? kk + kRoundRows : kk) : r0 + kk;
                 if (kk < nrows) {
                     float2 w;
                     if constexpr (MC > 0) {
-                        w = cmulf(ct_hi[kq * kA + t / kB], ct_lo[kq * kB + t % kB]);
+                        w = wp[kq];
                     } else {
                         w = tw[t * kq];
                     }
@@ -1906,15 +1895,13 @@ hipError_t launch_acq_search_big(const float2* XT, const float2* codesT, int n_p
     const size_t lds = (static_cast<size_t>(kWaveRows) + 1) * sizeof(float2) * row_plan.n;
     if (row_plan.n > kAcqThreads) return hipErrorInvalidValue;
     if (P == 25 && row_plan.n == 1000) {  // C3: N = 25000
-        constexpr int kB = col_split(1000);
-        const size_t lds_c3 = lds + sizeof(float2) * static_cast<size_t>(kB * 25 + (1000 / kB) * 25);
-        hipLaunchKernelGGL((acq_search_big_kernel<25, 1000>), dim3(n_bins, n_prns), dim3(kAcqThreads), lds_c3, stream, XT, codesT, row_plan, tw, n_bins,
+        hipLaunchKernelGGL((acq_search_big_kernel<25, 1000>), dim3(n_bins, n_prns), dim3(kAcqThreads), lds, stream, XT, codesT, row_plan, tw, n_bins,
             rs, accumulate, rowstat, grid);
         return hipGetLastError();
     }
     if (P == 16 && row_plan.n == 250) {  // C1: N = 4000 in 256-thread workgroups (several per CU)
-        constexpr int kNT = 256, kB = col_split(250);
-        const size_t lds_c1 = (static_cast<size_t>(kNT / 64) + 1) * sizeof(float2) * 250 + sizeof(float2) * static_cast<size_t>(kB * 16 + (250 / kB) * 16);
+        constexpr int kNT = 256;
+        const size_t lds_c1 = (static_cast<size_t>(kNT / 64) + 1) * sizeof(float2) * 250;
         hipLaunchKernelGGL((acq_search_big_kernel<16, 250, kNT>), dim3(n_bins, n_prns), dim3(kNT), lds_c1, stream, XT, codesT, row_plan, tw, n_bins,
             rs, accumulate, rowstat, grid);
         return hipGetLastError();
