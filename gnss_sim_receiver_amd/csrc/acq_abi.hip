@@ -128,9 +128,12 @@ struct gnsship_acq {
     std::vector<char> code_set;
     int consumed = 0;            // d_consumed_samples: input samples used, the rest zero-padded
     Step2Spec step2{};           // make_2_steps: step-two grid active
-    // The sweep's launches (forward transform, search, decision) as one hipGraph, re-captured when
-    // any launch argument changes: a C3 sweep is four short kernels, and the launch gaps between
-    // them cost ~15 % of its time when launched one by one.  GNSSHIP_ACQ_GRAPH=0: plain launches.
+    // The huge layout's sweep (forward transform, two batch lanes of row / column / finalize launches
+    // with their events, decision) as one hipGraph, re-captured when any launch argument changes:
+    // launched one by one it is 5 % slower (E1 0.760 → 0.797 ms).  The four launches of the other
+    // layouts go straight to the stream: the graph's launch latency (≈ 12 µs to the first kernel)
+    // outweighed the gaps it saved (C3 0.164 → 0.153 ms, C1 shape 0.069 → 0.058 ms without it).
+    // GNSSHIP_ACQ_GRAPH=0 / 1: plain launches / a graph for every layout.
     hipGraphExec_t graph = nullptr;
     struct GraphKey {
         const void* src;
@@ -471,10 +474,11 @@ extern "C" int gnsship_acq_run(gnsship_acq* a, const void* sig, int fmt, int sig
                          a->conf.resampler_latency_samples, a->step2, a->res_dev, ctx->stream));
         return GNSSHIP_OK;
     };
-    static const bool graphs_on = [] {
+    static const int graph_env = [] {
         const char* env = std::getenv("GNSSHIP_ACQ_GRAPH");
-        return !(env && env[0] == '0');
+        return env ? (env[0] == '0' ? 0 : 1) : -1;
     }();
+    const bool graphs_on = graph_env < 0 ? a->huge : graph_env == 1;
     if (graphs_on && !a->graph_broken) {
         const gnsship_acq::GraphKey key{src, fmt, n_prns, accumulate, keep_grid ? 1 : 0, a->dwell_count, keep_grid ? a->grid_dev : nullptr, a->step2};
         const bool same = a->graph && std::memcmp(&key, &a->graph_key, sizeof(key)) == 0;

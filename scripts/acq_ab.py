@@ -2,6 +2,7 @@
 25000) and the C1-shape sweep (32 x 81 x 4000) with the grid returned, each build in its own
 process (the library is chosen by GNSSHIP_LIB_PATH), results and timings compared.
     python scripts/acq_ab.py scripts/libgnsship_base.so gnss_sim_receiver_amd/libgnsship.so [--tolerant]
+Either side may carry environment settings after a colon: lib.so:GNSSHIP_ACQ_GRAPH=0.
 --tolerant: a different FFT factorisation (other rounding) passes when every PRN's Doppler and code
 delay agree exactly; the test-statistic difference is reported."""
 import hashlib
@@ -74,10 +75,12 @@ def main():
     TOLERANT = "--tolerant" in sys.argv
     libs = [x for x in sys.argv[1:] if not x.startswith("--")]
     outs = []
-    for i, lib in enumerate(libs[:2]):
+    for i, spec in enumerate(libs[:2]):
+        lib, _, extra = spec.partition(":")  # lib.so[:ENV=value,ENV2=value]
         out = os.path.join(ROOT, "gpurun_out", f"acq_ab_{i}.npz")
         os.makedirs(os.path.dirname(out), exist_ok=True)
         env = dict(os.environ, GNSSHIP_LIB_PATH=os.path.abspath(lib))
+        env.update(kv.split("=", 1) for kv in extra.split(",") if kv)
         subprocess.run([sys.executable, os.path.abspath(__file__), "--one", out], env=env, check=True, timeout=300)
         outs.append(np.load(out))
     a, b = outs

@@ -12,6 +12,18 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs through libgnsship.so on cuda:0)")
 
 
+@pytest.fixture(scope="session", autouse=True)
+def _torch_hip_first(request):
+    """torch's HIP runtime is initialised before libgnsship's in every GPU run, whichever test comes
+    first (a module that loads libgnsship before the `ctx` fixture did otherwise leave the context
+    creation that follows with no device)."""
+    if any(item.get_closest_marker("gpu") for item in request.session.items):
+        import torch
+        if torch.cuda.is_available():
+            torch.cuda.init()
+    yield
+
+
 @pytest.fixture(scope="session")
 def built():
     """Make sure libgnsship.so and the oracle exist (gcc/hipcc cross-compile, no GPU needed)."""
